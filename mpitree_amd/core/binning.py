@@ -1,0 +1,110 @@
+"""Feature binning: raw feature values -> small integer codes.
+
+The reference considers every unique value of a feature as a threshold
+(``np.unique(X[:, f])``, reference ``mpitree/tree/decision_tree.py:73``) and
+routes ``x <= t`` left. We keep that contract exactly whenever a feature has at
+most ``max_bins`` unique values ("exact" features): the bin edges *are* the
+unique values and bin ``b`` holds the values equal to ``edges[b]``, so a split
+"code <= b" is the reference split "x <= edges[b]". Features with more unique
+values use quantile edges drawn from the data (every edge is a data value and
+``x <= edges[b]`` <=> ``code <= b`` still holds), bounding the histogram size
+that the gfx950 kernels work on.
+
+Codes are ``uint8`` when every feature fits in 256 bins, else ``uint16``.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+__all__ = ["BinMapper", "quantile_edges", "fit_bin_mapper"]
+
+MAX_BINS_LIMIT = 65536
+
+
+def quantile_edges(sorted_values: np.ndarray, max_bins: int) -> np.ndarray:
+    """Upper-quantile edges taken from sorted sample values (all data values)."""
+    s = sorted_values.shape[0]
+    k = np.arange(1, max_bins + 1, dtype=np.int64)
+    idx = np.minimum((k * s + max_bins - 1) // max_bins - 1, s - 1)
+    return np.unique(sorted_values[idx])
+
+
+@dataclass
+class BinMapper:
+    edges: list  # per-feature float64 sorted edge values
+    exact: np.ndarray  # bool [F]
+    max_bins: int
+
+    @property
+    def n_features(self) -> int:
+        return len(self.edges)
+
+    @property
+    def n_bins(self) -> np.ndarray:
+        return np.asarray([len(e) for e in self.edges], dtype=np.int32)
+
+    @property
+    def max_n_bins(self) -> int:
+        return int(self.n_bins.max()) if self.edges else 1
+
+    @property
+    def code_dtype(self):
+        return np.uint8 if self.max_n_bins <= 256 else np.uint16
+
+    def padded_edges(self, dtype=np.float64) -> np.ndarray:
+        """[F, Bmax] edge table padded with +inf (what the kernels search)."""
+        bmax = self.max_n_bins
+        out = np.full((self.n_features, bmax), np.inf, dtype=dtype)
+        for f, e in enumerate(self.edges):
+            out[f, : len(e)] = e
+        return out
+
+    def transform(self, X: np.ndarray) -> np.ndarray:
+        """Row-major codes ``[n, F]``: first edge >= x, clamped to the last bin."""
+        X = np.asarray(X)
+        n, F = X.shape
+        codes = np.empty((n, F), dtype=self.code_dtype)
+        for f, e in enumerate(self.edges):
+            c = np.searchsorted(e, X[:, f], side="left")
+            np.minimum(c, len(e) - 1, out=c)
+            codes[:, f] = c
+        return codes
+
+
+def fit_bin_mapper(X: np.ndarray, max_bins=256, sample: int | None = None, seed: int = 0):
+    """Compute per-feature edges on the host.
+
+    ``max_bins=None`` requests exact mode for every feature (up to 65536
+    unique values). ``sample`` limits the rows used for quantile features;
+    exact features are always detected on the full column.
+    """
+    X = np.asarray(X)
+    if X.ndim != 2:
+        raise ValueError("X must be 2-D")
+    limit = MAX_BINS_LIMIT if max_bins is None else int(max_bins)
+    if not 2 <= limit <= MAX_BINS_LIMIT:
+        raise ValueError(f"max_bins must be in [2, {MAX_BINS_LIMIT}]")
+    n, F = X.shape
+    edges, exact = [], np.zeros(F, dtype=bool)
+    rows = None
+    if sample is not None and n > sample:
+        rng = np.random.default_rng(seed)
+        rows = np.sort(rng.choice(n, size=sample, replace=False))
+    for f in range(F):
+        col = np.asarray(X[:, f], dtype=np.float64)
+        u = np.unique(col)
+        if u.shape[0] <= limit:
+            edges.append(u)
+            exact[f] = True
+            continue
+        if max_bins is None:
+            raise ValueError(
+                f"feature {f} has {u.shape[0]} unique values; exact mode supports "
+                f"at most {MAX_BINS_LIMIT}"
+            )
+        src = np.sort(col[rows]) if rows is not None else np.sort(col)
+        edges.append(quantile_edges(src, limit))
+    return BinMapper(edges=edges, exact=exact, max_bins=limit)

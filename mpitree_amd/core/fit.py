@@ -1,0 +1,260 @@
+"""Fit dispatch: input validation, label encoding, binning and engine choice.
+
+One entry point, :func:`fit_tree`, used by every estimator. It owns the
+parts of the reference's ``fit`` (``mpitree/tree/decision_tree.py:168-190``)
+that are not tree growth: ``check_X_y``-style validation (finite 2-D
+features), class discovery (``classes_ = np.unique(y)``) -- labels are encoded
+to ``0..K-1`` internally so non-contiguous labels work -- and it picks the
+engine:
+
+* ``device="cuda"`` (or ``"auto"`` with a GPU and a device tensor or a large
+  input): binning and growth on the current MI355X through the HIP kernels;
+* ``device="cpu"``: the native C++ builder when built, else the numpy
+  level-wise engine.
+
+Distributed fits pass a communication strategy (``comm``) and use the same
+level-wise engine on either device.
+"""
+
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .binning import BinMapper, fit_bin_mapper
+from .criterion import Criterion
+from .levelwise import GrowParams, LevelwiseBuilder, LocalComm
+from ..models.tree_arrays import TreeArrays
+from ..ops import native
+
+__all__ = ["FitResult", "fit_tree", "resolve_device", "AUTO_GPU_MIN_CELLS"]
+
+AUTO_GPU_MIN_CELLS = 1 << 18  # n*F below this stays on the host in device="auto"
+
+
+@dataclass
+class FitResult:
+    arrays: TreeArrays
+    classes: np.ndarray | None
+    n_features: int
+    mapper: BinMapper
+    y_scale_exp: int = 0
+    engine: str = ""
+    timings: dict = field(default_factory=dict)
+    stats: dict = field(default_factory=dict)
+
+
+def _is_tensor(x) -> bool:
+    return isinstance(x, torch.Tensor)
+
+
+def resolve_device(device, X) -> str:
+    """Map ``device`` ('auto'|'cpu'|'cuda'|'gpu'|torch.device) to 'cpu' or 'cuda'."""
+    if isinstance(device, torch.device):
+        device = device.type
+    device = (device or "auto").lower()
+    if device in ("cuda", "gpu", "hip", "rocm"):
+        if not torch.cuda.is_available():
+            raise RuntimeError("device='cuda' requested but no GPU is visible")
+        return "cuda"
+    if device == "cpu":
+        return "cpu"
+    if device != "auto":
+        raise ValueError(f"unknown device {device!r}")
+    if _is_tensor(X) and X.is_cuda:
+        return "cuda"
+    if torch.cuda.is_available() and native.has_hip():
+        n, F = X.shape
+        if n * F >= AUTO_GPU_MIN_CELLS:
+            return "cuda"
+    return "cpu"
+
+
+def _validate_X(X, allow_tensor=True):
+    if _is_tensor(X):
+        if X.dim() != 2:
+            raise ValueError(f"Expected 2D array, got {X.dim()}D tensor")
+        if X.shape[0] < 1:
+            raise ValueError("Found array with 0 sample(s)")
+        if not torch.is_floating_point(X):
+            X = X.double()
+        if not bool(torch.isfinite(X).all()):
+            raise ValueError("Input X contains NaN or infinity.")
+        return X
+    X = np.asarray(X)
+    if X.dtype == object:
+        X = X.astype(np.float64)
+    if X.ndim != 2:
+        raise ValueError(f"Expected 2D array, got {X.ndim}D array instead")
+    if X.shape[0] < 1:
+        raise ValueError("Found array with 0 sample(s) (shape=%s)" % (X.shape,))
+    if X.shape[1] < 1:
+        raise ValueError("Found array with 0 feature(s)")
+    if not np.issubdtype(X.dtype, np.number) and X.dtype != bool:
+        raise ValueError(f"Unsupported feature dtype {X.dtype}")
+    if X.dtype not in (np.float32, np.float64):
+        X = X.astype(np.float64)
+    if not np.isfinite(X).all():
+        raise ValueError("Input X contains NaN or infinity.")
+    return X
+
+
+def _encode_labels(y, n):
+    if _is_tensor(y):
+        if y.dim() != 1 or y.shape[0] != n:
+            raise ValueError("y must be 1-D with one label per row")
+        classes, enc = torch.unique(y, return_inverse=True)
+        return classes.cpu().numpy(), enc.to(torch.int32)
+    y = np.asarray(y)
+    if y.ndim == 2 and y.shape[1] == 1:
+        y = y.ravel()
+    if y.ndim != 1 or y.shape[0] != n:
+        raise ValueError(f"y must be 1-D with {n} labels, got shape {y.shape}")
+    classes, enc = np.unique(y, return_inverse=True)
+    return classes, enc.astype(np.int32)
+
+
+def fixed_point_exponent(absmax: float, n: int) -> int:
+    """Exponent e with sum(|round(y * 2**e)|) < 2**62 for n rows."""
+    if absmax <= 0 or not math.isfinite(absmax):
+        return 0
+    e = 62 - math.ceil(math.log2(max(n, 1) + 1)) - math.ceil(math.log2(absmax * (1 + 2**-40)))
+    return int(max(min(e, 1000), -1000))
+
+
+def _encode_targets(y, n):
+    if _is_tensor(y):
+        if y.dim() != 1 or y.shape[0] != n:
+            raise ValueError("y must be 1-D")
+        yd = y.double()
+        if not bool(torch.isfinite(yd).all()):
+            raise ValueError("Input y contains NaN or infinity.")
+        e = fixed_point_exponent(float(yd.abs().max().item()), n)
+        return torch.round(torch.ldexp(yd, torch.tensor(float(e), device=y.device))).long(), e
+    y = np.asarray(y, dtype=np.float64)
+    if y.ndim == 2 and y.shape[1] == 1:
+        y = y.ravel()
+    if y.ndim != 1 or y.shape[0] != n:
+        raise ValueError("y must be 1-D")
+    if not np.isfinite(y).all():
+        raise ValueError("Input y contains NaN or infinity.")
+    e = fixed_point_exponent(float(np.abs(y).max()), n)
+    return np.round(np.ldexp(y, e)).astype(np.int64), e
+
+
+def _finalize(ta: TreeArrays, mapper: BinMapper, regression: bool, y_exp: int) -> TreeArrays:
+    ta.with_thresholds(mapper.edges)
+    m = ta.n_samples.astype(np.float64)
+    term = ta.impurity
+    with np.errstate(invalid="ignore", divide="ignore"):
+        if regression:
+            s = ta.meta["sum_fixed"].astype(np.float64)
+            ta.value = np.ldexp(s / np.maximum(m, 1), -y_exp)
+            ta.meta["term"] = term
+            ta.impurity = np.full(ta.node_count, np.nan)
+        else:
+            ta.meta["term"] = term
+            ta.impurity = np.where(m > 0, term / np.maximum(m, 1), 0.0)
+    return ta
+
+
+def fit_tree(
+    X,
+    y,
+    *,
+    regression: bool,
+    criterion,
+    max_depth,
+    min_samples_split,
+    min_samples_leaf=1,
+    max_bins=256,
+    device="auto",
+    comm=None,
+    finisher_rows=None,
+    engine: str | None = None,
+) -> FitResult:
+    t_start = time.perf_counter()
+    X = _validate_X(X)
+    n, F = X.shape
+    crit = Criterion(criterion)
+    if max_depth is not None and (int(max_depth) != max_depth or max_depth < 0):
+        raise ValueError("max_depth must be None or a non-negative int")
+    if int(min_samples_split) < 2:
+        raise ValueError("min_samples_split must be >= 2")
+    if int(min_samples_leaf) < 1:
+        raise ValueError("min_samples_leaf must be >= 1")
+    dev = resolve_device(device, X)
+    if regression:
+        yv, y_exp = _encode_targets(y, n)
+        classes = None
+        C = 0
+    else:
+        classes, yv = _encode_labels(y, n)
+        y_exp = 0
+        C = len(classes)
+    comm = comm or LocalComm()
+    params = GrowParams(
+        criterion=crit,
+        max_depth=None if max_depth is None else int(max_depth),
+        min_samples_split=int(min_samples_split),
+        min_samples_leaf=int(min_samples_leaf),
+    )
+    timings = {}
+    if dev == "cuda":
+        from ..ops.hip_backend import HipBackend, gpu_bin_features
+
+        Xd = X if _is_tensor(X) else torch.from_numpy(np.ascontiguousarray(X))
+        Xd = Xd.to("cuda")
+        if Xd.dtype not in (torch.float32, torch.float64):
+            Xd = Xd.double()
+        Xd = Xd.contiguous()
+        t0 = time.perf_counter()
+        mapper, codes_rm, codes_fm, nb = gpu_bin_features(Xd, max_bins)
+        yd = (yv if _is_tensor(yv) else torch.from_numpy(np.ascontiguousarray(yv))).to("cuda")
+        yd = yd.contiguous()
+        timings["bin"] = time.perf_counter() - t0
+        be = HipBackend()
+        be.setup(codes_rm, codes_fm, yd, nb, n_bins=mapper.max_n_bins, n_classes=C,
+                 criterion=crit)
+        if finisher_rows is None:
+            finisher_rows = 0
+        params.finisher_rows = int(finisher_rows)
+        builder = LevelwiseBuilder(be, params, comm)
+        ta = builder.fit(n, C, F)
+        eng = "hip-levelwise"
+        timings.update(builder.timings)
+        stats = dict(builder.stats)
+    else:
+        Xh = X.cpu().numpy() if _is_tensor(X) else X
+        yh = yv.cpu().numpy() if _is_tensor(yv) else yv
+        t0 = time.perf_counter()
+        mapper = fit_bin_mapper(Xh, max_bins)
+        codes = mapper.transform(Xh)
+        timings["bin"] = time.perf_counter() - t0
+        use_native = (
+            engine in (None, "native") and comm.world_size == 1 and native.has_cpu()
+        )
+        if use_native:
+            from ..ops.cpu_builder import fit_native
+
+            ta = fit_native(codes, yh, mapper, C, params)
+            eng = "cpu-native"
+            stats = {}
+        else:
+            from .backend_numpy import NumpyBackend
+
+            be = NumpyBackend()
+            be.setup(codes, yh, n_bins=mapper.max_n_bins, n_classes=C, criterion=crit)
+            builder = LevelwiseBuilder(be, params, comm)
+            ta = builder.fit(n, C, F)
+            eng = "numpy-levelwise"
+            timings.update(builder.timings)
+            stats = dict(builder.stats)
+    ta = _finalize(ta, mapper, regression, y_exp)
+    timings["total"] = time.perf_counter() - t_start
+    return FitResult(arrays=ta, classes=classes, n_features=F, mapper=mapper, y_scale_exp=y_exp,
+                     engine=eng, timings=timings, stats=stats)

@@ -1,0 +1,375 @@
+// Split search over node histograms on gfx950.
+//
+// Replaces the reference's per-threshold cost loop and its argmin/argmax
+// (mpitree/tree/decision_tree.py:76-91 and :130-140): one wavefront scans one
+// (node, feature) histogram. Each lane owns 4 consecutive bins; per class the
+// wave does a 64-lane prefix sum (with a carry across 256-bin chunks), and the
+// per-bin split cost is accumulated in fp64 from the integer left/right class
+// counts with the shared integer-form criterion (criterion.h), so the result
+// is bit-identical to the host builders. A wave argmin over (cost, bin) picks
+// the first minimum; ``select_kernel`` then reduces (gain, feature) per node
+// with ties to the lowest feature and gathers the winning split's left counts.
+#include "common.h"
+#include "criterion.h"
+
+namespace mt {
+
+constexpr int kBinsPerLane = 4;
+constexpr int kChunk = kWave * kBinsPerLane;  // 256 bins per wave pass
+
+// hist: uint32 [slots][F_h][B][C]; nodes: int64 [k] slot ids
+// out_cost: f64 [k][F_h]; out_bin: i32 [k][F_h]
+__global__ __launch_bounds__(256) void scan_cls_kernel(
+    const uint32_t* __restrict__ hist, const int64_t* __restrict__ nodes,
+    const int32_t* __restrict__ nbins, int F_h, int f_lo, int B, int C, int crit, int msl,
+    double* __restrict__ out_cost, int32_t* __restrict__ out_bin) {
+  extern __shared__ uint32_t sm[];  // per wave: C class totals + C carries
+  const int wave = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const int f = blockIdx.y * 4 + wave;
+  if (f >= F_h) return;
+  const int64_t node = blockIdx.x;
+  const int64_t slot = nodes[node];
+  const uint32_t* h = hist + (slot * F_h + f) * (int64_t)B * C;
+  uint32_t* tot = sm + wave * 2 * C;
+  uint32_t* carry = tot + C;
+  const int nb = min(B, nbins[f_lo + f]);
+
+  // pass 1: per-class totals
+  uint32_t m = 0;
+  for (int c = 0; c < C; ++c) {
+    uint32_t s = 0;
+    for (int b = lane; b < nb; b += kWave) s += h[(int64_t)b * C + c];
+    s = wave_sum_u32(s);
+    if (lane == 0) {
+      tot[c] = s;
+      carry[c] = 0;
+    }
+    m += s;
+  }
+  // tot/carry are private to this wave: order lane 0's LDS writes before the
+  // other lanes' reads without a workgroup barrier (waves may have exited).
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+
+  double best_cost = __builtin_inf();
+  int best_bin = 0x7fffffff;
+  for (int base = 0; base < nb; base += kChunk) {
+    const int b0 = base + lane * kBinsPerLane;
+    uint32_t mL[kBinsPerLane];
+    uint32_t nonempty[kBinsPerLane];
+    double sL[kBinsPerLane], sR[kBinsPerLane];
+    int64_t qL[kBinsPerLane], qR[kBinsPerLane];
+#pragma unroll
+    for (int k = 0; k < kBinsPerLane; ++k) {
+      mL[k] = 0;
+      nonempty[k] = 0;
+      sL[k] = 0.0;
+      sR[k] = 0.0;
+      qL[k] = 0;
+      qR[k] = 0;
+    }
+    for (int c = 0; c < C; ++c) {
+      uint32_t v[kBinsPerLane];
+#pragma unroll
+      for (int k = 0; k < kBinsPerLane; ++k) {
+        const int b = b0 + k;
+        v[k] = (b < nb) ? h[(int64_t)b * C + c] : 0u;
+      }
+      uint32_t p[kBinsPerLane];
+      p[0] = v[0];
+#pragma unroll
+      for (int k = 1; k < kBinsPerLane; ++k) p[k] = p[k - 1] + v[k];
+      const uint32_t incl = wave_incl_scan_u32(p[kBinsPerLane - 1]);
+      const uint32_t excl = incl - p[kBinsPerLane - 1] + carry[c];
+      const uint32_t tc = tot[c];
+#pragma unroll
+      for (int k = 0; k < kBinsPerLane; ++k) {
+        const uint32_t L = excl + p[k];
+        const uint32_t R = tc - L;
+        mL[k] += L;
+        nonempty[k] |= v[k];
+        if (crit == kEntropy) {
+          sL[k] = sL[k] + xlog2x(L);
+          sR[k] = sR[k] + xlog2x(R);
+        } else {
+          qL[k] += (int64_t)L * L;
+          qR[k] += (int64_t)R * R;
+        }
+      }
+      const uint32_t chunk_total = __shfl(incl, kWave - 1, kWave);
+      if (lane == 0) carry[c] += chunk_total;
+    }
+#pragma unroll
+    for (int k = 0; k < kBinsPerLane; ++k) {
+      const int b = b0 + k;
+      const int64_t ml = mL[k];
+      const int64_t mr = (int64_t)m - ml;
+      if (b < nb && nonempty[k] && ml >= msl && mr >= msl) {
+        double cost;
+        if (crit == kEntropy)
+          cost = (xlog2x((uint64_t)ml) - sL[k]) + (xlog2x((uint64_t)mr) - sR[k]);
+        else
+          cost = gini_term(ml, qL[k]) + gini_term(mr, qR[k]);
+        if (cost < best_cost) {
+          best_cost = cost;
+          best_bin = b;
+        }
+      }
+    }
+  }
+  wave_argmin(best_cost, best_bin);
+  if (lane == 0) {
+    out_cost[node * F_h + f] = best_cost;
+    out_bin[node * F_h + f] = best_cost < __builtin_inf() ? best_bin : -1;
+  }
+}
+
+// hist: int64 [slots][F_h][B][2] = {count, fixed sum}
+__global__ __launch_bounds__(256) void scan_reg_kernel(
+    const int64_t* __restrict__ hist, const int64_t* __restrict__ nodes,
+    const int32_t* __restrict__ nbins, int F_h, int f_lo, int B, int msl,
+    double* __restrict__ out_cost, int32_t* __restrict__ out_bin) {
+  const int wave = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const int f = blockIdx.y * 4 + wave;
+  if (f >= F_h) return;
+  const int64_t node = blockIdx.x;
+  const int64_t slot = nodes[node];
+  const int64_t* h = hist + (slot * F_h + f) * (int64_t)B * 2;
+  const int nb = min(B, nbins[f_lo + f]);
+  int64_t m = 0, S = 0;
+  for (int b = lane; b < nb; b += kWave) {
+    m += h[2 * b];
+    S += h[2 * b + 1];
+  }
+  m = wave_sum_i64(m);
+  S = wave_sum_i64(S);
+  double best_cost = __builtin_inf();
+  int best_bin = 0x7fffffff;
+  int64_t carry_n = 0, carry_s = 0;
+  for (int base = 0; base < nb; base += kChunk) {
+    const int b0 = base + lane * kBinsPerLane;
+    int64_t cn[kBinsPerLane], cs[kBinsPerLane];
+#pragma unroll
+    for (int k = 0; k < kBinsPerLane; ++k) {
+      const int b = b0 + k;
+      cn[k] = b < nb ? h[2 * b] : 0;
+      cs[k] = b < nb ? h[2 * b + 1] : 0;
+    }
+    int64_t pn[kBinsPerLane], ps[kBinsPerLane];
+    pn[0] = cn[0];
+    ps[0] = cs[0];
+#pragma unroll
+    for (int k = 1; k < kBinsPerLane; ++k) {
+      pn[k] = pn[k - 1] + cn[k];
+      ps[k] = ps[k - 1] + cs[k];
+    }
+    const int64_t in_n = wave_incl_scan_i64(pn[kBinsPerLane - 1]);
+    const int64_t in_s = wave_incl_scan_i64(ps[kBinsPerLane - 1]);
+    const int64_t ex_n = in_n - pn[kBinsPerLane - 1] + carry_n;
+    const int64_t ex_s = in_s - ps[kBinsPerLane - 1] + carry_s;
+#pragma unroll
+    for (int k = 0; k < kBinsPerLane; ++k) {
+      const int b = b0 + k;
+      const int64_t ml = ex_n + pn[k];
+      const int64_t sl = ex_s + ps[k];
+      const int64_t mr = m - ml;
+      if (b < nb && cn[k] > 0 && ml >= msl && mr >= msl) {
+        const double cost = mse_term(ml, sl) + mse_term(mr, S - sl);
+        if (cost < best_cost) {
+          best_cost = cost;
+          best_bin = b;
+        }
+      }
+    }
+    carry_n += __shfl(in_n, kWave - 1, kWave);
+    carry_s += __shfl(in_s, kWave - 1, kWave);
+  }
+  wave_argmin(best_cost, best_bin);
+  if (lane == 0) {
+    out_cost[node * F_h + f] = best_cost;
+    out_bin[node * F_h + f] = best_cost < __builtin_inf() ? best_bin : -1;
+  }
+}
+
+// One workgroup per node: best feature and the winning split's statistics.
+// rec: int64 [k][R]: {gain bits, feature(global), bin, n_left, m,
+//                     left[C], total[C]}             (classification, R = 5 + 2C)
+//                    {gain bits, feature, bin, n_left, m, left_sum, total_sum}
+//                                                     (regression, R = 7)
+__global__ __launch_bounds__(256) void select_kernel(
+    const void* __restrict__ hist_v, const int64_t* __restrict__ nodes,
+    const double* __restrict__ cost, const int32_t* __restrict__ bins, int F_h, int f_lo, int B,
+    int C, int crit, int64_t* __restrict__ rec) {
+  extern __shared__ int64_t cls[];  // [C] totals, then [C] left counts
+  __shared__ double s_gain[4];
+  __shared__ int s_feat[4], s_bin[4];
+  __shared__ int64_t s_a[4], s_b[4];
+  __shared__ double s_pterm;
+  const int wave = threadIdx.x >> 6;
+  const int lane = lane_id();
+  const int64_t node = blockIdx.x;
+  const int64_t slot = nodes[node];
+  const bool reg = crit == kSquaredError;
+  const int R = reg ? 7 : 5 + 2 * C;
+  int64_t* out = rec + node * R;
+
+  // node statistics from feature 0 of the histogram (every feature sums the same)
+  if (reg) {
+    const int64_t* h = (const int64_t*)hist_v + (slot * F_h) * (int64_t)B * 2;
+    int64_t a = 0, s = 0;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) {
+      a += h[2 * b];
+      s += h[2 * b + 1];
+    }
+    a = wave_sum_i64(a);
+    s = wave_sum_i64(s);
+    if (lane == 0) {
+      s_a[wave] = a;
+      s_b[wave] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int64_t m = s_a[0] + s_a[1] + s_a[2] + s_a[3];
+      const int64_t S = s_b[0] + s_b[1] + s_b[2] + s_b[3];
+      s_pterm = mse_term(m, S);
+      out[4] = m;
+      out[6] = S;
+    }
+  } else {
+    const uint32_t* h = (const uint32_t*)hist_v + (slot * F_h) * (int64_t)B * C;
+    for (int c = wave; c < C; c += 4) {
+      uint32_t s = 0;
+      for (int b = lane; b < B; b += kWave) s += h[(int64_t)b * C + c];
+      s = wave_sum_u32(s);
+      if (lane == 0) cls[c] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // sequential over classes, matching the host order
+      double acc = 0.0;
+      int64_t mm = 0, sq = 0;
+      for (int c = 0; c < C; ++c) {
+        const int64_t t = cls[c];
+        mm += t;
+        acc = acc + xlog2x((uint64_t)t);
+        sq += t * t;
+      }
+      s_pterm = crit == kEntropy ? xlog2x((uint64_t)mm) - acc : gini_term(mm, sq);
+      out[4] = mm;
+    }
+    for (int c = threadIdx.x; c < C; c += blockDim.x) out[5 + C + c] = cls[c];
+  }
+  __syncthreads();
+  const double pterm = s_pterm;
+
+  // best feature: argmax gain, ties -> lowest feature
+  double g = -__builtin_inf();
+  int bf = 0x7fffffff, bb = -1;
+  for (int f = threadIdx.x; f < F_h; f += blockDim.x) {
+    const double c = cost[node * F_h + f];
+    if (c < __builtin_inf()) {
+      const double gf = pterm - c;
+      if (gf > g) {
+        g = gf;
+        bf = f;
+        bb = bins[node * F_h + f];
+      }
+    }
+  }
+  wave_argmax(g, bf, bb);
+  if (lane == 0) {
+    s_gain[wave] = g;
+    s_feat[wave] = bf;
+    s_bin[wave] = bb;
+  }
+  __syncthreads();
+  g = s_gain[0];
+  bf = s_feat[0];
+  bb = s_bin[0];
+  for (int w = 1; w < 4; ++w) {
+    if (s_gain[w] > g || (s_gain[w] == g && s_feat[w] < bf)) {
+      g = s_gain[w];
+      bf = s_feat[w];
+      bb = s_bin[w];
+    }
+  }
+  const bool ok = g > -__builtin_inf();
+  if (threadIdx.x == 0) {
+    out[0] = (int64_t)double_to_bits(g);
+    out[1] = ok ? f_lo + bf : -1;
+    out[2] = ok ? bb : -1;
+  }
+  if (!ok) {
+    if (threadIdx.x == 0) {
+      out[3] = 0;
+      if (reg) out[5] = 0;
+    }
+    if (!reg)
+      for (int c = threadIdx.x; c < C; c += blockDim.x) out[5 + c] = 0;
+    return;
+  }
+  // winning split's left statistics
+  if (reg) {
+    const int64_t* h = (const int64_t*)hist_v + (slot * F_h + bf) * (int64_t)B * 2;
+    int64_t a = 0, s = 0;
+    for (int b = threadIdx.x; b <= bb; b += blockDim.x) {
+      a += h[2 * b];
+      s += h[2 * b + 1];
+    }
+    a = wave_sum_i64(a);
+    s = wave_sum_i64(s);
+    __syncthreads();
+    if (lane == 0) {
+      s_a[wave] = a;
+      s_b[wave] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      out[3] = s_a[0] + s_a[1] + s_a[2] + s_a[3];
+      out[5] = s_b[0] + s_b[1] + s_b[2] + s_b[3];
+    }
+  } else {
+    const uint32_t* h = (const uint32_t*)hist_v + (slot * F_h + bf) * (int64_t)B * C;
+    int64_t* left = cls + C;
+    for (int c = wave; c < C; c += 4) {
+      uint32_t s = 0;
+      for (int b = lane; b <= bb; b += kWave) s += h[(int64_t)b * C + c];
+      s = wave_sum_u32(s);
+      if (lane == 0) left[c] = s;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) out[5 + c] = left[c];
+    if (threadIdx.x == 0) {
+      int64_t nl = 0;
+      for (int c = 0; c < C; ++c) nl += left[c];
+      out[3] = nl;
+    }
+  }
+}
+
+void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int k,
+                 const int32_t* nbins, int F_h, int f_lo, int B, int C, int crit, int msl,
+                 double* cost, int32_t* bins, int64_t* rec) {
+  if (k <= 0) return;
+  dim3 grid(k, (F_h + 3) / 4);
+  if (crit == kSquaredError) {
+    hipLaunchKernelGGL(scan_reg_kernel, grid, dim3(256), 0, stream, (const int64_t*)hist, nodes,
+                       nbins, F_h, f_lo, B, msl, cost, bins);
+  } else {
+    size_t lds = (size_t)4 * 2 * C * sizeof(uint32_t);
+    MT_HIP_CHECK(hipFuncSetAttribute((const void*)scan_cls_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(scan_cls_kernel, grid, dim3(256), lds, stream, (const uint32_t*)hist,
+                       nodes, nbins, F_h, f_lo, B, C, crit, msl, cost, bins);
+  }
+  MT_HIP_CHECK(hipGetLastError());
+  const size_t sel_lds = crit == kSquaredError ? 16 : (size_t)2 * C * sizeof(int64_t);
+  MT_HIP_CHECK(hipFuncSetAttribute((const void*)select_kernel,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sel_lds));
+  hipLaunchKernelGGL(select_kernel, dim3(k), dim3(256), sel_lds, stream, hist, nodes, cost, bins,
+                     F_h, f_lo, B, C, crit, rec);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace mt

@@ -1,0 +1,340 @@
+"""gfx950 backend of the level-wise engine: device buffers + kernel launches.
+
+Implements the same operations as :class:`mpitree_amd.core.backend_numpy.NumpyBackend`
+with the HIP kernels in ``ops/csrc``. Device data (row-major and
+feature-major codes, labels, the row permutation) stays resident in HBM for
+the whole fit; per level the host only uploads a small work plan and reads
+back one record per frontier node.
+"""
+
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from ..core.binning import BinMapper, MAX_BINS_LIMIT
+from ..core.criterion import Criterion
+from . import native
+
+__all__ = ["HipBackend", "gpu_bin_features"]
+
+LDS_BUDGET = int(os.environ.get("MPITREE_HIST_LDS", 80 * 1024))
+MAX_ITEM_ROWS = 65535  # 16-bit packed LDS counters
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+class _Uploader:
+    """Pack several small int64 host arrays into one asynchronous pinned H2D copy.
+
+    A ring of pinned staging buffers, each guarded by the event recorded after
+    its copy, lets the host prepare the next plan while earlier copies are in
+    flight without ever overwriting a buffer the DMA engine still reads.
+    """
+
+    RING = 8
+
+    def __init__(self, device):
+        self.device = device
+        self._bufs = [torch.empty(256, dtype=torch.int64).pin_memory() for _ in range(self.RING)]
+        self._events = [None] * self.RING
+        self._i = 0
+
+    def __call__(self, *arrays):
+        arrays = [np.asarray(a, dtype=np.int64).ravel() for a in arrays]
+        sizes = [a.size for a in arrays]
+        total = max(1, sum(sizes))
+        i = self._i
+        self._i = (i + 1) % self.RING
+        if self._events[i] is not None:
+            self._events[i].synchronize()
+        if self._bufs[i].numel() < total:
+            self._bufs[i] = torch.empty(max(total, 2 * self._bufs[i].numel()),
+                                        dtype=torch.int64).pin_memory()
+        buf = self._bufs[i].numpy()
+        o = 0
+        for a, s in zip(arrays, sizes):
+            buf[o : o + s] = a
+            o += s
+        dev = self._bufs[i][:total].to(self.device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._events[i] = ev
+        outs, o = [], 0
+        for s in sizes:
+            outs.append(dev[o : o + s])
+            o += s
+        return outs
+
+
+def gpu_bin_features(X: torch.Tensor, max_bins=256, sample_rows: int = 1 << 17):
+    """Bin a device feature matrix; returns (BinMapper, codes_rm, codes_fm, nbins_dev).
+
+    Edges come from a deterministic strided row sample sorted on the device;
+    features whose sample has at most ``max_bins`` distinct values are binned
+    in exact mode and verified by the bin kernel, falling back to the full
+    column when the sample missed a value.
+    """
+    hip = native.hip()
+    n, F = X.shape
+    dev = X.device
+    limit = MAX_BINS_LIMIT if max_bins is None else int(max_bins)
+    if n > sample_rows:
+        ridx = (torch.arange(sample_rows, device=dev, dtype=torch.int64) * n) // sample_rows
+        S = X.index_select(0, ridx)
+    else:
+        S = X
+    s = S.shape[0]
+    srt = torch.sort(S, dim=0).values.t().contiguous()  # [F, s]
+    distinct = torch.ones((F, s), dtype=torch.bool, device=dev)
+    if s > 1:
+        distinct[:, 1:] = srt[:, 1:] != srt[:, :-1]
+    nuniq = distinct.sum(1)
+    exact = nuniq <= limit
+    # exact edges: distinct values compacted per row
+    pos = torch.cumsum(distinct, 1) - 1
+    width = limit + 1
+    pos = torch.where(distinct & exact[:, None], pos, torch.full_like(pos, limit))
+    edges = torch.full((F, width), float("inf"), dtype=X.dtype, device=dev)
+    edges.scatter_(1, pos, srt)
+    # quantile edges for the others
+    if (~exact).any():
+        k = torch.arange(1, limit + 1, device=dev, dtype=torch.int64)
+        qi = torch.clamp((k * s + limit - 1) // limit - 1, max=s - 1)
+        qv = srt[:, qi]  # [F, limit] sorted
+        qd = torch.ones_like(qv, dtype=torch.bool)
+        qd[:, 1:] = qv[:, 1:] != qv[:, :-1]
+        qpos = torch.cumsum(qd, 1) - 1
+        qpos = torch.where(qd & ~exact[:, None], qpos, torch.full_like(qpos, limit))
+        qedges = torch.full((F, width), float("inf"), dtype=X.dtype, device=dev)
+        qedges.scatter_(1, qpos, qv)
+        edges = torch.where(exact[:, None], edges, qedges)
+    edges = edges[:, :limit]
+    nb = torch.isfinite(edges).sum(1).to(torch.int32)
+    host_edges = edges.double().cpu().numpy()
+    host_nb = nb.cpu().numpy()
+    host_exact = exact.cpu().numpy()
+
+    def run_bin(edges_t, nb_t, exact_t):
+        bmax = int(nb_t.max().item()) if F else 1
+        cb = 1 if bmax <= 256 else 2
+        ctype = torch.uint8 if cb == 1 else torch.int16
+        row_elems = ((F * cb + 3) // 4) * 4 // cb
+        codes_rm = torch.empty((n, row_elems), dtype=ctype, device=dev)
+        codes_fm = torch.empty((F, n), dtype=ctype, device=dev)
+        bad = torch.zeros(F, dtype=torch.int32, device=dev)
+        et = edges_t[:, :bmax].contiguous()
+        hip.bin(_stream(), X.data_ptr(), X.dtype == torch.float64, n, F, et.data_ptr(), bmax,
+                nb_t.data_ptr(), exact_t.to(torch.uint8).contiguous().data_ptr(),
+                codes_rm.data_ptr(), row_elems, codes_fm.data_ptr(), cb, bad.data_ptr())
+        return codes_rm, codes_fm, bad, bmax
+
+    codes_rm, codes_fm, bad, _ = run_bin(edges, nb, exact)
+    bad_h = bad.cpu().numpy()
+    if bad_h.any():
+        # the sample missed values of an "exact" feature: use the full column
+        for f in np.nonzero(bad_h)[0]:
+            col = X[:, f]
+            u = torch.unique(col)
+            if u.numel() <= limit:
+                e = u
+                host_exact[f] = True
+            else:
+                srtc = torch.sort(col).values
+                k = torch.arange(1, limit + 1, device=dev, dtype=torch.int64)
+                qi = torch.clamp((k * n + limit - 1) // limit - 1, max=n - 1)
+                e = torch.unique(srtc[qi])
+                host_exact[f] = False
+            edges[f].fill_(float("inf"))
+            edges[f, : e.numel()] = e
+            host_edges[f] = np.inf
+            host_edges[f, : e.numel()] = e.double().cpu().numpy()
+            host_nb[f] = e.numel()
+        nb = torch.from_numpy(host_nb.astype(np.int32)).to(dev)
+        exact = torch.from_numpy(host_exact).to(dev)
+        codes_rm, codes_fm, bad, _ = run_bin(edges, nb, exact)
+    mapper = BinMapper(
+        edges=[host_edges[f, : host_nb[f]].copy() for f in range(F)],
+        exact=host_exact.astype(bool),
+        max_bins=limit,
+    )
+    return mapper, codes_rm, codes_fm, nb
+
+
+class HipBackend:
+    """Device state and kernel launches for one fit on the current GPU."""
+
+    name = "hip"
+
+    def __init__(self, device=None):
+        self.hip = native.hip()
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        self.up = _Uploader(self.device)
+        self.timing = False
+
+    # ---------------------------------------------------------------- setup
+    def setup(self, codes_rm, codes_fm, y, nbins_dev, *, n_bins: int, n_classes: int,
+              criterion: Criterion):
+        self.codes_rm = codes_rm
+        self.codes_fm = codes_fm
+        self.n, self.row_elems = codes_rm.shape
+        self.F = codes_fm.shape[0]
+        self.cb = codes_rm.element_size()
+        self.y = y
+        self.nbins = nbins_dev
+        self.B = int(n_bins)
+        self.crit = criterion
+        self.reg = criterion == Criterion.SQUARED_ERROR
+        self.C = 2 if self.reg else int(n_classes)
+        self.idx = torch.arange(self.n, dtype=torch.int32, device=self.device)
+        self.tmp = torch.empty_like(self.idx)
+
+    def hist_elems(self, F_h: int) -> int:
+        return F_h * self.B * (2 if self.reg else self.C)
+
+    def alloc_hist(self, slots: int, F_h: int | None = None):
+        F_h = self.F if F_h is None else F_h
+        self._F_h = F_h
+        dt = torch.int64 if self.reg else torch.int32
+        shape = (max(slots, 1), F_h, self.B, 2 if self.reg else self.C)
+        ft = self.hip.hist_feature_tile(F_h, self.B, self.C, self.reg, LDS_BUDGET)
+        if ft == 0:
+            return torch.zeros(shape, dtype=dt, device=self.device)
+        return torch.empty(shape, dtype=dt, device=self.device)
+
+    # ------------------------------------------------------------ histograms
+    def build_hist(self, hist, slots, starts, counts, f_lo=0, f_hi=None):
+        f_hi = self.F if f_hi is None else f_hi
+        F_h = f_hi - f_lo
+        if len(slots) == 0:
+            return
+        counts = np.asarray(counts, dtype=np.int64)
+        total = int(counts.sum())
+        chunk = int(min(MAX_ITEM_ROWS, max(2048, -(-total // 1024))))
+        ft = self.hip.hist_feature_tile(F_h, self.B, self.C, self.reg, LDS_BUDGET)
+        items, red = [], []
+        nslab = 0
+        for s, st, ct in zip(slots, starts, counts):
+            k = max(1, -(-int(ct) // chunk))
+            if k == 1 or ft == 0:
+                # one item (or global-atomic fallback): write the node's hist directly
+                if ft == 0:
+                    for c0 in range(0, max(int(ct), 1), MAX_ITEM_ROWS):
+                        items.append((s, st + c0, min(MAX_ITEM_ROWS, ct - c0), -1))
+                else:
+                    items.append((s, st, ct, -1))
+                continue
+            red.append((s, nslab, k))
+            for i in range(k):
+                c0 = i * chunk
+                items.append((s, st + c0, min(chunk, ct - c0), nslab + i))
+            nslab += k
+        items = np.asarray(items, dtype=np.int64).reshape(-1, 4)
+        red = np.asarray(red, dtype=np.int64).reshape(-1, 3)
+        d_items, d_red = self.up(items, red)
+        E = self.hist_elems(F_h)
+        slab = None
+        if nslab:
+            slab = torch.empty((nslab, E), dtype=hist.dtype, device=self.device)
+        self.hip.hist(_stream(), self.codes_rm.data_ptr(), self.cb, self.row_elems * self.cb,
+                      self.idx.data_ptr(), self.y.data_ptr(), d_items.data_ptr(), items.shape[0],
+                      hist.data_ptr(), 0 if slab is None else slab.data_ptr(), F_h, f_lo, self.B,
+                      self.C, self.reg, LDS_BUDGET)
+        if nslab:
+            self.hip.hist_reduce(_stream(), d_red.data_ptr(), red.shape[0], slab.data_ptr(),
+                                 hist.data_ptr(), E, self.reg)
+        self._keep = (slab, d_items, d_red)
+
+    def derive_hist(self, hist, prev_hist, slots, parent_slots, sibling_slots):
+        if len(slots) == 0:
+            return
+        der = np.stack([slots, parent_slots, sibling_slots], 1).astype(np.int64)
+        (d_der,) = self.up(der)
+        E = hist[0].numel()
+        self.hip.hist_derive(_stream(), d_der.data_ptr(), der.shape[0], prev_hist.data_ptr(),
+                             hist.data_ptr(), E, self.reg)
+        self._keep_d = d_der
+
+    # ------------------------------------------------------------------ scan
+    def scan(self, hist, slots, min_samples_leaf=1, f_lo=0, f_hi=None):
+        f_hi = self.F if f_hi is None else f_hi
+        F_h = f_hi - f_lo
+        k = len(slots)
+        C = self.C
+        R = 7 if self.reg else 5 + 2 * C
+        (d_nodes,) = self.up(np.asarray(slots, dtype=np.int64))
+        cost = torch.empty((k, F_h), dtype=torch.float64, device=self.device)
+        bins = torch.empty((k, F_h), dtype=torch.int32, device=self.device)
+        rec = torch.empty((k, R), dtype=torch.int64, device=self.device)
+        self.hip.scan(_stream(), hist.data_ptr(), d_nodes.data_ptr(), k, self.nbins.data_ptr(),
+                      F_h, f_lo, self.B, C, int(self.crit), int(max(1, min_samples_leaf)),
+                      cost.data_ptr(), bins.data_ptr(), rec.data_ptr())
+        r = rec.cpu().numpy()
+        gain = r[:, 0].copy().view(np.float64)
+        out = {
+            "gain": gain,
+            "feature": r[:, 1].astype(np.int32),
+            "bin": r[:, 2].astype(np.int32),
+            "n_left": r[:, 3].copy(),
+            "m": r[:, 4].copy(),
+        }
+        if self.reg:
+            out["left"] = np.stack([r[:, 3], r[:, 5]], 1)
+        else:
+            out["left"] = r[:, 5 : 5 + C].copy()
+        return out
+
+    # ------------------------------------------------------------- partition
+    def partition(self, starts, counts, features, bins, need_counts=True):
+        k = len(starts)
+        if k == 0:
+            return np.zeros(0, dtype=np.int64)
+        starts = np.asarray(starts, dtype=np.int64)
+        counts = np.asarray(counts, dtype=np.int64)
+        split = np.stack([starts, counts, np.asarray(features, np.int64),
+                          np.asarray(bins, np.int64)], 1)
+        items = []
+        for j in range(k):
+            for c0 in range(0, int(counts[j]), 1024):
+                items.append((j, starts[j] + c0, min(1024, counts[j] - c0)))
+        items = np.asarray(items, dtype=np.int64).reshape(-1, 3)
+        cursors = np.stack([starts, starts + counts], 1)
+        d_split, d_items, d_cur64 = self.up(split, items, cursors)
+        cur = d_cur64.view(k, 2).to(torch.int32)
+        self.hip.partition(_stream(), self.codes_fm.data_ptr(), self.cb, self.n,
+                           self.idx.data_ptr(), self.tmp.data_ptr(), d_items.data_ptr(),
+                           items.shape[0], d_split.data_ptr(), cur.data_ptr())
+        if not need_counts:
+            self._keep_p = (d_split, d_items, cur)
+            return None
+        return cur[:, 0].cpu().numpy().astype(np.int64) - starts
+
+    def segment_stats(self, starts, counts):
+        k = len(starts)
+        items = np.stack([np.arange(k), np.asarray(starts, np.int64),
+                          np.asarray(counts, np.int64)], 1).astype(np.int64)
+        # split long segments into 64K-row items for parallelism
+        rows = []
+        for s, st, ct in items:
+            for c0 in range(0, max(int(ct), 1), 65536):
+                rows.append((s, st + c0, min(65536, ct - c0)))
+        items = np.asarray(rows, dtype=np.int64).reshape(-1, 3)
+        (d_items,) = self.up(items)
+        if self.reg:
+            out = torch.zeros((k, 4), dtype=torch.int64, device=self.device)
+            out[:, 2] = np.iinfo(np.int64).max
+            out[:, 3] = np.iinfo(np.int64).min
+        else:
+            out = torch.zeros((k, self.C), dtype=torch.int32, device=self.device)
+        self.hip.seg_stats(_stream(), self.idx.data_ptr(), self.y.data_ptr(), self.reg,
+                           d_items.data_ptr(), items.shape[0], out.data_ptr(), self.C)
+        return out.cpu().numpy().astype(np.int64)
+
+    def sync(self):
+        if self.timing:
+            torch.cuda.synchronize(self.device)

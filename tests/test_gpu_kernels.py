@@ -1,0 +1,97 @@
+"""gfx950 kernels vs the host oracle (exact equality: every quantity is integer
+or produced by the shared criterion with identical IEEE operations)."""
+
+import numpy as np
+import pytest
+import torch
+
+from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
+from mpitree_amd.core.criterion import Criterion, xlog2x
+
+from .helpers import oracle, random_problem
+
+pytestmark = pytest.mark.gpu
+
+
+def test_native_extension_loaded():
+    from mpitree_amd.ops import native
+
+    hip = native.hip()
+    assert hip.__file__.startswith(str(__import__("pathlib").Path(__file__).parents[1]))
+
+
+def test_xlog2x_device_matches_host_bitwise():
+    from mpitree_amd.ops import native
+
+    n = 1 << 20
+    out = torch.empty(n, dtype=torch.float64, device="cuda")
+    native.hip().xlog2x_device(torch.cuda.current_stream().cuda_stream, out.data_ptr(), n)
+    dev = out.cpu().numpy()
+    host = xlog2x(np.arange(n, dtype=np.int64))
+    assert np.array_equal(dev.view(np.int64), host.view(np.int64))
+
+
+@pytest.mark.parametrize("crit", ["entropy", "gini"])
+@pytest.mark.parametrize("seed", range(4))
+def test_gpu_classifier_matches_oracle(crit, seed):
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(50, 3000))
+    F = int(rng.integers(1, 12))
+    C = int(rng.integers(2, 6))
+    X, y = random_problem(rng, n, F, C, levels=int(rng.integers(2, 40)))
+    md = [None, 4, 8, None][seed]
+    ref = oracle(X, y, Criterion.ENTROPY if crit == "entropy" else Criterion.GINI, md)
+    clf = DecisionTreeClassifier(max_depth=md, criterion=crit, device="cuda").fit(X, y)
+    assert clf.fit_stats_["engine"].startswith("hip")
+    assert clf.tree_arrays_.equal(ref), (clf.tree_arrays_.node_count, ref.node_count)
+    Xd = torch.from_numpy(X).cuda()
+    np.testing.assert_array_equal(clf.predict(Xd).cpu().numpy(), clf.predict(X))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_gpu_regressor_matches_oracle(seed):
+    rng = np.random.default_rng(100 + seed)
+    n = int(rng.integers(50, 2000))
+    F = int(rng.integers(1, 8))
+    X, y = random_problem(rng, n, F, 0, levels=int(rng.integers(2, 30)), regression=True)
+    md = [None, 5, 3][seed]
+    ref = oracle(X, y, Criterion.SQUARED_ERROR, md, regression=True)
+    reg = DecisionTreeRegressor(max_depth=md, device="cuda").fit(X, y)
+    assert reg.tree_arrays_.equal(ref, check_impurity=False)
+    np.testing.assert_array_equal(reg.tree_arrays_.value, ref.value)
+
+
+def test_gpu_iris_goldens(iris2):
+    from .conftest import GOLDEN_DEPTH3, GOLDEN_DEPTH5
+
+    X, y, iris = iris2
+    clf = DecisionTreeClassifier(max_depth=3, device="cuda").fit(X, y)
+    assert clf.export_text(feature_names=iris.feature_names,
+                           class_names=iris.target_names) == GOLDEN_DEPTH3
+    clf = DecisionTreeClassifier(max_depth=5, device="cuda").fit(X, y)
+    assert clf.export_text(feature_names=iris.feature_names, class_names=iris.target_names,
+                           precision=1) == GOLDEN_DEPTH5
+
+
+def test_gpu_large_multiitem_and_u16_bins():
+    # > 2048 rows per node -> multi-item slabs + reduce; 300 unique values -> u16 codes
+    rng = np.random.default_rng(7)
+    n, F = 20000, 5
+    X = rng.integers(0, 300, size=(n, F)).astype(np.float32)
+    y = (X[:, 0] + rng.normal(scale=40, size=n) > 150).astype(np.int64)
+    ref = oracle(X.astype(np.float64), y, Criterion.ENTROPY, 6, max_bins=512)
+    clf = DecisionTreeClassifier(max_depth=6, max_bins=512, device="cuda").fit(
+        torch.from_numpy(X).cuda(), torch.from_numpy(y).cuda())
+    assert clf.tree_arrays_.equal(ref)
+
+
+def test_gpu_quantile_bins_consistent_predict():
+    rng = np.random.default_rng(3)
+    n, F = 50000, 8
+    X = rng.normal(size=(n, F)).astype(np.float32)
+    y = (X[:, 0] * X[:, 1] > 0).astype(np.int64)
+    Xd = torch.from_numpy(X).cuda()
+    clf = DecisionTreeClassifier(max_depth=8, device="cuda").fit(Xd, torch.from_numpy(y).cuda())
+    # device and host traversal agree exactly on the raw values
+    np.testing.assert_array_equal(clf.apply(Xd).cpu().numpy(), clf.tree_arrays_.apply(X))
+    assert clf.score(X, y) > 0.9
