@@ -156,5 +156,40 @@ class NumpyBackend:
             out[j] = np.bincount(self.y[self.idx[st : st + ct]], minlength=self.C)
         return out
 
+    # ------------------------------------------------------------- finisher
+    def finisher_supported(self) -> bool:
+        return True
+
+    def finish_subtrees(self, starts, counts, depths, params):
+        """Reference (depth-first) growth of each deferred subtree.
+
+        Same contract as the gfx950 finisher: concatenated node tables with
+        job-local child indices, job j at ``offsets[j]:offsets[j+1]``.
+        """
+        from .reference import fit_reference
+
+        parts = []
+        for st, ct, d in zip(starts, counts, depths):
+            rows = self.idx[st : st + ct]
+            md = None if params.max_depth is None else int(params.max_depth) - int(d)
+            ta = fit_reference(
+                self.codes[rows], self.y[rows], n_classes=self.C, n_bins=self.B,
+                criterion=self.crit, max_depth=md, min_samples_split=params.min_samples_split,
+                min_samples_leaf=params.min_samples_leaf,
+            )
+            stats = (np.stack([ta.n_samples, ta.meta["sum_fixed"]], 1) if self.reg
+                     else ta.count)
+            parts.append(dict(feature=ta.feature, bin=ta.threshold_bin,
+                              left=ta.left.astype(np.int64), right=ta.right.astype(np.int64),
+                              depth=ta.depth + int(d), nsamp=ta.n_samples, stats=stats))
+        lens = np.array([len(p["feature"]) for p in parts], dtype=np.int64)
+        out = {k: (np.concatenate([p[k] for p in parts]) if parts else np.zeros(0, np.int64))
+               for k in ("feature", "bin", "left", "right", "depth", "nsamp")}
+        C = 2 if self.reg else self.C
+        out["stats"] = (np.concatenate([p["stats"] for p in parts]) if parts
+                        else np.zeros((0, C), np.int64))
+        out["offsets"] = np.concatenate([[0], np.cumsum(lens)])
+        return out
+
     def sync(self):
         pass

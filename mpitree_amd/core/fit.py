@@ -19,6 +19,7 @@ level-wise engine on either device.
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -221,6 +222,10 @@ def fit_tree(
         be.setup(codes_rm, codes_fm, yd, nb, n_bins=mapper.max_n_bins, n_classes=C,
                  criterion=crit)
         if finisher_rows is None:
+            env = os.environ.get("MPITREE_FINISHER_ROWS")
+            # ~2 subtree jobs per workgroup slot of the finisher grid
+            finisher_rows = int(env) if env else max(2048, n // 512)
+        if not be.finisher_supported():
             finisher_rows = 0
         params.finisher_rows = int(finisher_rows)
         builder = LevelwiseBuilder(be, params, comm)

@@ -21,13 +21,14 @@ Children whose fate is already known from the parent's split record (pure,
 ``max_depth`` reached, fewer than ``min_samples_split`` rows) become leaves
 without any device work. Subtrees that become small enough are handed to the
 backend's subtree finisher (one workgroup per subtree on gfx950), which removes
-the long tail of tiny levels.
+the long tail of tiny levels. All host bookkeeping is vectorised over the
+level's nodes.
 """
 
 from __future__ import annotations
 
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 
 import numpy as np
 
@@ -68,42 +69,63 @@ class LocalComm:
     def reduce_stats(self, stats: np.ndarray, reg: bool) -> np.ndarray:
         return stats
 
-    def owns_subtree(self, j: int) -> bool:
-        return True
+    def finish_assignment(self, m: np.ndarray) -> np.ndarray:
+        """Which deferred subtrees this rank finishes (all of them locally)."""
+        return np.ones(len(m), dtype=bool)
+
+    def merge_subtrees(self, local: list, owned: np.ndarray, n_jobs: int) -> list:
+        return local
+
+    def fit_kwargs(self) -> dict:
+        return {}
 
 
-@dataclass
 class _Table:
-    C: int
-    reg: bool
-    feature: list = field(default_factory=list)
-    tbin: list = field(default_factory=list)
-    left: list = field(default_factory=list)
-    right: list = field(default_factory=list)
-    depth: list = field(default_factory=list)
-    nsamp: list = field(default_factory=list)
-    term: list = field(default_factory=list)
-    stats: list = field(default_factory=list)  # class counts or (count, sum)
+    """Growing node table (unordered ids; pre-ordered at the end)."""
 
-    def add(self, depth, nsamp, stats, term) -> int:
-        i = len(self.feature)
-        self.feature.append(-1)
-        self.tbin.append(-1)
-        self.left.append(-1)
-        self.right.append(-1)
-        self.depth.append(depth)
-        self.nsamp.append(nsamp)
-        self.stats.append(np.asarray(stats, dtype=np.int64))
-        self.term.append(term)
-        return i
+    def __init__(self, C: int):
+        self.C = C
+        self.n = 0
+        self.cap = 1024
+        self.feature = np.full(self.cap, -1, np.int32)
+        self.tbin = np.full(self.cap, -1, np.int32)
+        self.left = np.full(self.cap, -1, np.int64)
+        self.right = np.full(self.cap, -1, np.int64)
+        self.depth = np.zeros(self.cap, np.int32)
+        self.nsamp = np.zeros(self.cap, np.int64)
+        self.stats = np.zeros((self.cap, C), np.int64)
+
+    def _grow(self, need):
+        if need <= self.cap:
+            return
+        cap = max(need, 2 * self.cap)
+        for name in ("feature", "tbin", "left", "right", "depth", "nsamp", "stats"):
+            a = getattr(self, name)
+            fill = -1 if name in ("feature", "tbin", "left", "right") else 0
+            b = np.full((cap,) + a.shape[1:], fill, a.dtype)
+            b[: self.n] = a[: self.n]
+            setattr(self, name, b)
+        self.cap = cap
+
+    def add(self, depth, nsamp, stats) -> np.ndarray:
+        depth = np.atleast_1d(np.asarray(depth))
+        k = depth.shape[0]
+        self._grow(self.n + k)
+        ids = np.arange(self.n, self.n + k)
+        self.depth[ids] = depth
+        self.nsamp[ids] = nsamp
+        self.stats[ids] = np.asarray(stats, dtype=np.int64).reshape(k, self.C)
+        self.n += k
+        return ids
 
 
-def _node_term(crit, stats):
+def _node_terms(crit, stats: np.ndarray) -> np.ndarray:
+    """Vectorised node terms for every node (stats: [N, C] counts or [N, 2])."""
     if crit == Criterion.ENTROPY:
-        return float(entropy_term(stats))
+        return entropy_term(stats)
     if crit == Criterion.GINI:
-        return float(gini_term(stats))
-    return float(mse_term(int(stats[0]), int(stats[1])))
+        return gini_term(stats)
+    return mse_term(stats[:, 0], stats[:, 1])
 
 
 class LevelwiseBuilder:
@@ -117,15 +139,19 @@ class LevelwiseBuilder:
         self.stats: dict = {}
 
     # ------------------------------------------------------------ helpers
-    def _terminal(self, depth, m, stats, minmax=None) -> bool:
+    def _terminal(self, depth, m, stats, minmax=None) -> np.ndarray:
         p = self.p
-        if p.max_depth is not None and depth >= p.max_depth:
-            return True
-        if m < p.min_samples_split or m < 2 * max(1, p.min_samples_leaf):
-            return True
+        depth = np.asarray(depth)
+        m = np.asarray(m)
+        t = (m < p.min_samples_split) | (m < 2 * max(1, p.min_samples_leaf))
+        if p.max_depth is not None:
+            t |= depth >= p.max_depth
         if p.criterion == Criterion.SQUARED_ERROR:
-            return minmax is not None and minmax[0] == minmax[1]
-        return int((np.asarray(stats) > 0).sum()) <= 1
+            if minmax is not None:
+                t |= minmax[:, 0] == minmax[:, 1]
+        else:
+            t |= (np.asarray(stats) > 0).sum(-1) <= 1
+        return t
 
     def _tick(self, key, t0):
         self.be.sync()
@@ -137,206 +163,194 @@ class LevelwiseBuilder:
         reg = p.criterion == Criterion.SQUARED_ERROR
         C = 2 if reg else n_classes
         f_lo, f_hi = comm.feature_range(n_features)
-        tab = _Table(C=C, reg=reg)
+        F_h = f_hi - f_lo
+        tab = _Table(C)
 
-        # root statistics (global)
-        st = comm.reduce_stats(be.segment_stats(np.array([0]), np.array([n_local])), reg)[0]
+        t0 = time.perf_counter()
+        st = comm.reduce_stats(be.segment_stats(np.array([0]), np.array([n_local])), reg)
+        self._tick("stats", t0)
         if reg:
-            m_root, rstats, minmax = int(st[0]), st[:2], st[2:4]
+            m_root, rstats, minmax = int(st[0, 0]), st[:, :2], st[:, 2:4]
         else:
-            m_root, rstats, minmax = int(st.sum()), st, None
-        root = tab.add(0, m_root, rstats, _node_term(p.criterion, rstats))
-        # frontier arrays: node id, local start, local count, global count,
-        # hist source (-1 = build from rows, else parent slot in prev level),
-        # sibling frontier index for derived nodes
-        frontier = []
-        deferred = []  # (node id, start, count, depth) for the subtree finisher
-        if not self._terminal(0, m_root, rstats, minmax):
-            frontier.append(dict(id=root, start=0, count=n_local, m=m_root, depth=0,
-                                 src=-1, sib=-1, slot_prev=-1))
+            m_root, rstats, minmax = int(st[0].sum()), st, None
+        root = tab.add(0, m_root, rstats)
+        # frontier columns
+        fr = dict(
+            id=root,
+            start=np.zeros(1, np.int64),
+            count=np.array([n_local], np.int64),
+            m=np.array([m_root], np.int64),
+            depth=np.zeros(1, np.int64),
+            src=np.full(1, -1, np.int64),  # parent slot in prev level if derived
+            sib=np.full(1, -1, np.int64),  # frontier index of the built sibling
+        )
+        if self._terminal(np.zeros(1), np.array([m_root]), rstats, minmax)[0]:
+            fr = {k: v[:0] for k, v in fr.items()}
+        deferred = {k: [] for k in ("id", "start", "count", "m", "depth")}
         prev_hist = None
         levels = 0
-        while frontier:
+        while fr["id"].size:
             levels += 1
+            K = fr["id"].size
             # small subtrees go to the finisher (global row count decides)
             if p.finisher_rows > 0 and hasattr(be, "finish_subtrees"):
-                keep = []
-                for nd in frontier:
-                    if nd["m"] <= p.finisher_rows:
-                        deferred.append(nd)
-                    else:
-                        keep.append(nd)
-                if len(keep) != len(frontier):
-                    # a derived node whose sibling left the frontier must be built
-                    ids = {id(nd) for nd in keep}
-                    for nd in keep:
-                        if nd["src"] >= 0 and id(nd["sib_ref"]) not in ids:
-                            nd["src"] = -1
-                frontier = keep
-                if not frontier:
-                    break
-            # slots: nodes built from rows first (contiguous for all-reduce)
-            built = [nd for nd in frontier if nd["src"] < 0]
-            derived = [nd for nd in frontier if nd["src"] >= 0]
-            order = built + derived
-            for s, nd in enumerate(order):
-                nd["slot"] = s
-            hist = be.alloc_hist(len(order), f_hi - f_lo)
+                small = fr["m"] <= p.finisher_rows
+                if small.any():
+                    for key in deferred:
+                        deferred[key].append(fr[key][small])
+                    keep = ~small
+                    # derived nodes whose built sibling was deferred: build from rows
+                    sib = fr["sib"]
+                    lost = (fr["src"] >= 0) & small[np.maximum(sib, 0)]
+                    fr["src"] = np.where(lost, -1, fr["src"])
+                    new_index = np.cumsum(keep) - 1
+                    fr["sib"] = np.where(fr["src"] >= 0, new_index[np.maximum(sib, 0)], -1)
+                    fr = {k: v[keep] for k, v in fr.items()}
+                    K = fr["id"].size
+                    if K == 0:
+                        break
+            built = np.nonzero(fr["src"] < 0)[0]
+            derived = np.nonzero(fr["src"] >= 0)[0]
+            order = np.concatenate([built, derived])
+            slot_of = np.empty(K, np.int64)
+            slot_of[order] = np.arange(K)
+            o = {k: v[order] for k, v in fr.items()}  # frontier in slot order
+            nb = built.size
+            hist = be.alloc_hist(K, F_h)
             t0 = time.perf_counter()
-            if built:
-                be.build_hist(
-                    hist,
-                    np.array([nd["slot"] for nd in built]),
-                    np.array([nd["start"] for nd in built]),
-                    np.array([nd["count"] for nd in built]),
-                    f_lo,
-                    f_hi,
-                )
+            if nb:
+                be.build_hist(hist, np.arange(nb), o["start"][:nb], o["count"][:nb], f_lo, f_hi)
             self._tick("hist", t0)
             t0 = time.perf_counter()
-            comm.reduce_hist(hist, len(built))
+            comm.reduce_hist(hist, nb)
             self._tick("reduce", t0)
             t0 = time.perf_counter()
-            if derived:
-                be.derive_hist(
-                    hist,
-                    prev_hist,
-                    np.array([nd["slot"] for nd in derived]),
-                    np.array([nd["src"] for nd in derived]),
-                    np.array([nd["sib_ref"]["slot"] for nd in derived]),
-                )
+            if derived.size:
+                be.derive_hist(hist, prev_hist, np.arange(nb, K), o["src"][nb:],
+                               slot_of[o["sib"][nb:]])
             self._tick("derive", t0)
             t0 = time.perf_counter()
-            res = be.scan(hist, np.arange(len(order)), p.min_samples_leaf, f_lo, f_hi)
+            res = be.scan(hist, np.arange(K), p.min_samples_leaf, f_lo, f_hi)
             self._tick("scan", t0)
             t0 = time.perf_counter()
             res = comm.combine_scan(res)
             self._tick("combine", t0)
-            split = np.nonzero(res["gain"] > -np.inf)[0]
+            split = np.nonzero(res["gain"] > -np.inf)[0]  # positions in slot order
+            S = split.size
+            ids = o["id"][split]
+            tab.feature[ids] = res["feature"][split]
+            tab.tbin[ids] = res["bin"][split]
             # partition rows of split nodes
             t0 = time.perf_counter()
             replicated = getattr(comm, "rows_replicated", True)
-            nl_local = be.partition(
-                np.array([order[j]["start"] for j in split], dtype=np.int64),
-                np.array([order[j]["count"] for j in split], dtype=np.int64),
-                res["feature"][split],
-                res["bin"][split],
-                need_counts=not replicated,
-            )
+            nl_local = be.partition(o["start"][split], o["count"][split], res["feature"][split],
+                                    res["bin"][split], need_counts=not replicated)
             if replicated:
                 nl_local = np.asarray(res["n_left"])[split].astype(np.int64)
             self._tick("partition", t0)
-            # children
-            child_stats = None
-            if reg and len(split):
-                starts, counts = [], []
-                for k, j in enumerate(split):
-                    nd = order[j]
-                    starts += [nd["start"], nd["start"] + nl_local[k]]
-                    counts += [nl_local[k], nd["count"] - nl_local[k]]
+            if S == 0:
+                break
+            # children (left, right interleaved: 2j, 2j+1)
+            ml = np.asarray(res["n_left"])[split].astype(np.int64)
+            m_par = o["m"][split]
+            lstats = np.asarray(res["left"])[split].astype(np.int64)
+            pstats = tab.stats[ids]
+            cstats = np.stack([lstats, pstats - lstats], 1).reshape(2 * S, C)
+            cm = np.stack([ml, m_par - ml], 1).reshape(-1)
+            cstart = np.stack([o["start"][split], o["start"][split] + nl_local], 1).reshape(-1)
+            ccount = np.stack([nl_local, o["count"][split] - nl_local], 1).reshape(-1)
+            cdepth = np.repeat(o["depth"][split] + 1, 2)
+            cids = tab.add(cdepth, cm, cstats)
+            tab.left[ids] = cids[0::2]
+            tab.right[ids] = cids[1::2]
+            mm = None
+            if reg:
                 t0 = time.perf_counter()
-                child_stats = comm.reduce_stats(
-                    be.segment_stats(np.array(starts), np.array(counts)), reg
-                )
+                cs = comm.reduce_stats(be.segment_stats(cstart, ccount), reg)
+                mm = cs[:, 2:4]
                 self._tick("stats", t0)
-            nxt = []
-            for k, j in enumerate(split):
-                nd = order[j]
-                nid = nd["id"]
-                tab.feature[nid] = int(res["feature"][j])
-                tab.tbin[nid] = int(res["bin"][j])
-                ml = int(res["n_left"][j])
-                pstats = tab.stats[nid]
-                lstats = np.asarray(res["left"][j], dtype=np.int64)
-                rstats = pstats - lstats
-                d = nd["depth"] + 1
-                kids = []
-                for side, (cs, cm, lst, lct) in enumerate(
-                    (
-                        (lstats, ml, nd["start"], int(nl_local[k])),
-                        (rstats, nd["m"] - ml, nd["start"] + int(nl_local[k]),
-                         nd["count"] - int(nl_local[k])),
-                    )
-                ):
-                    cid = tab.add(d, cm, cs, _node_term(p.criterion, cs))
-                    if side == 0:
-                        tab.left[nid] = cid
-                    else:
-                        tab.right[nid] = cid
-                    mm = None
-                    if reg:
-                        mm = child_stats[2 * k + side][2:4]
-                    if not self._terminal(d, cm, cs, mm):
-                        kids.append(dict(id=cid, start=lst, count=lct, m=cm, depth=d,
-                                         src=-1, sib=-1, slot_prev=nd["slot"]))
-                if len(kids) == 2:
-                    a, b = kids
-                    # build the smaller child (ties: left), derive the larger
-                    small, large = (a, b) if a["m"] <= b["m"] else (b, a)
-                    large["src"] = nd["slot"]
-                    large["sib_ref"] = small
-                nxt.extend(kids)
+            alive = ~self._terminal(cdepth, cm, cstats, mm)
+            # the smaller child (ties: left) is built from rows, the larger is
+            # derived as parent - sibling; the parent's slot is its position
+            both = np.nonzero(alive[0::2] & alive[1::2])[0]
+            big = np.where(ml <= (m_par - ml), 1, 0)  # offset of the larger child
+            keep_idx = np.nonzero(alive)[0]
+            new_pos = np.full(2 * S, -1, np.int64)
+            new_pos[keep_idx] = np.arange(keep_idx.size)
+            src = np.full(2 * S, -1, np.int64)
+            sib = np.full(2 * S, -1, np.int64)
+            src[2 * both + big[both]] = split[both]
+            sib[2 * both + big[both]] = new_pos[2 * both + 1 - big[both]]
+            fr = dict(
+                id=cids[keep_idx],
+                start=cstart[keep_idx],
+                count=ccount[keep_idx],
+                m=cm[keep_idx],
+                depth=cdepth[keep_idx].astype(np.int64),
+                src=src[keep_idx],
+                sib=sib[keep_idx],
+            )
             prev_hist = hist
-            frontier = nxt
         self.stats["levels"] = levels
-        if deferred:
+        if deferred["id"]:
+            d = {k: np.concatenate(v) for k, v in deferred.items()}
             t0 = time.perf_counter()
-            self._finish(tab, deferred)
+            self._finish(tab, d)
             self._tick("finisher", t0)
+            self.stats["finisher_subtrees"] = int(d["id"].size)
         return self._to_arrays(tab)
 
     # ------------------------------------------------------------ finisher
-    def _finish(self, tab: _Table, deferred: list):
+    def _finish(self, tab: _Table, d: dict):
         """Grow each deferred subtree with the backend's subtree finisher."""
-        p = self.p
-        sub = self.be.finish_subtrees(
-            np.array([nd["start"] for nd in deferred], dtype=np.int64),
-            np.array([nd["count"] for nd in deferred], dtype=np.int64),
-            np.array([nd["depth"] for nd in deferred], dtype=np.int64),
-            p,
-            self.comm,
-        )
-        # ``sub`` holds one node table per deferred subtree, root first, with
-        # local child indices; splice them into the global table.
-        for nd, t in zip(deferred, sub):
-            base = len(tab.feature) - 1  # local index 0 maps onto nd['id']
-            nloc = len(t["feature"])
-            gid = [nd["id"]] + list(range(base + 1, base + nloc))
-            for li in range(nloc):
-                if li > 0:
-                    tab.add(int(t["depth"][li]), int(t["nsamp"][li]), t["stats"][li],
-                            float(t["term"][li]))
-                g = gid[li]
-                if t["feature"][li] >= 0:
-                    tab.feature[g] = int(t["feature"][li])
-                    tab.tbin[g] = int(t["bin"][li])
-                    tab.left[g] = gid[int(t["left"][li])]
-                    tab.right[g] = gid[int(t["right"][li])]
+        comm = self.comm
+        owned = comm.finish_assignment(d["m"])
+        local = self.be.finish_subtrees(d["start"][owned], d["count"][owned], d["depth"][owned],
+                                        self.p)
+        t = comm.merge_subtrees(local, owned, d["id"].size)
+        # ``t`` concatenates one node table per deferred subtree (job j at
+        # offsets[j]:offsets[j+1], root first, job-local child indices);
+        # splice them into the global table in one vectorised pass.
+        off = t["offsets"]
+        lens = np.diff(off)
+        T = int(off[-1])
+        if T == 0:
+            return
+        job_of = np.repeat(np.arange(lens.size), lens)
+        is_root = np.zeros(T, bool)
+        is_root[off[:-1][lens > 0]] = True
+        gids = np.empty(T, np.int64)
+        gids[is_root] = d["id"][lens > 0]
+        nr = np.nonzero(~is_root)[0]
+        gids[nr] = tab.add(t["depth"][nr], t["nsamp"][nr], t["stats"][nr])
+        inner = np.nonzero(t["feature"] >= 0)[0]
+        g = gids[inner]
+        jb = off[job_of[inner]]
+        tab.feature[g] = t["feature"][inner]
+        tab.tbin[g] = t["bin"][inner]
+        tab.left[g] = gids[jb + t["left"][inner]]
+        tab.right[g] = gids[jb + t["right"][inner]]
 
     # -------------------------------------------------------------- output
     def _to_arrays(self, tab: _Table) -> TreeArrays:
-        reg = tab.reg
-        st = np.stack(tab.stats) if tab.stats else np.zeros((0, tab.C), np.int64)
-        nsamp = np.asarray(tab.nsamp, dtype=np.int64)
+        reg = self.p.criterion == Criterion.SQUARED_ERROR
+        n = tab.n
+        st = tab.stats[:n]
+        term = _node_terms(self.p.criterion, st)
         ta = TreeArrays.from_unordered(
-            feature=np.asarray(tab.feature, dtype=np.int32),
-            threshold_bin=np.asarray(tab.tbin, dtype=np.int32),
-            left=np.asarray(tab.left, dtype=np.int64),
-            right=np.asarray(tab.right, dtype=np.int64),
-            n_samples=nsamp,
-            impurity=np.asarray(tab.term, dtype=np.float64),
+            feature=tab.feature[:n],
+            threshold_bin=tab.tbin[:n],
+            left=tab.left[:n],
+            right=tab.right[:n],
+            n_samples=tab.nsamp[:n],
+            impurity=term,
             count=None if reg else st,
             value=st[:, 1].astype(np.float64) if reg else None,
         )
         if reg:
-            # keep exact fixed-point sums alongside (value is filled by the estimator)
-            order_sum = TreeArrays.from_unordered(
-                feature=np.asarray(tab.feature, dtype=np.int32),
-                threshold_bin=np.asarray(tab.tbin, dtype=np.int32),
-                left=np.asarray(tab.left, dtype=np.int64),
-                right=np.asarray(tab.right, dtype=np.int64),
-                n_samples=st[:, 1],
-                impurity=np.asarray(tab.term, dtype=np.float64),
-            )
-            ta.meta["sum_fixed"] = order_sum.n_samples.astype(np.int64)
+            ta.meta["sum_fixed"] = ta.value.astype(np.int64)
+            ta.meta["sum_fixed"] = TreeArrays.from_unordered(
+                feature=tab.feature[:n], threshold_bin=tab.tbin[:n], left=tab.left[:n],
+                right=tab.right[:n], n_samples=st[:, 1], impurity=term,
+            ).n_samples.astype(np.int64)
         return ta

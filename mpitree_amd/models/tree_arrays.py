@@ -92,25 +92,36 @@ class TreeArrays:
     ) -> "TreeArrays":
         """Re-number an arbitrary node table into depth-first pre-order."""
         feature = np.asarray(feature)
-        left = np.asarray(left)
-        right = np.asarray(right)
+        left = np.asarray(left, dtype=np.int64)
+        right = np.asarray(right, dtype=np.int64)
         n = feature.shape[0]
-        order = np.empty(n, dtype=np.int64)
+        # level-synchronous passes (vectorised over each depth):
+        # 1) nodes per depth from the root, 2) subtree sizes bottom-up,
+        # 3) pre-order index top-down: left = parent + 1, right = left + |left subtree|
         depth_old = np.zeros(n, dtype=np.int32)
-        k = 0
-        stack = [root]
-        while stack:
-            i = stack.pop()
-            order[k] = i
-            k += 1
-            if feature[i] >= 0:
-                depth_old[right[i]] = depth_old[i] + 1
-                depth_old[left[i]] = depth_old[i] + 1
-                stack.append(right[i])
-                stack.append(left[i])
-        order = order[:k]
+        levels = [np.array([root], dtype=np.int64)]
+        while True:
+            cur = levels[-1]
+            inner = cur[feature[cur] >= 0]
+            if inner.size == 0:
+                break
+            nxt = np.concatenate([left[inner], right[inner]])
+            depth_old[nxt] = len(levels)
+            levels.append(nxt)
+        size = np.ones(n, dtype=np.int64)
+        for cur in reversed(levels):
+            inner = cur[feature[cur] >= 0]
+            size[inner] = 1 + size[left[inner]] + size[right[inner]]
         new_id = np.full(n, -1, dtype=np.int64)
-        new_id[order] = np.arange(k)
+        new_id[root] = 0
+        for cur in levels:
+            inner = cur[feature[cur] >= 0]
+            new_id[left[inner]] = new_id[inner] + 1
+            new_id[right[inner]] = new_id[inner] + 1 + size[left[inner]]
+        k = int(size[root])
+        order = np.empty(k, dtype=np.int64)
+        reach = new_id >= 0
+        order[new_id[reach]] = np.nonzero(reach)[0]
         f = feature[order].astype(np.int32)
         lm = left[order]
         rm = right[order]
@@ -140,8 +151,12 @@ class TreeArrays:
         """Fill ``threshold`` from per-feature bin edges (edge value of the bin)."""
         thr = np.full(self.node_count, np.nan)
         inner = np.nonzero(self.feature >= 0)[0]
-        for i in inner:
-            thr[i] = float(edges[self.feature[i]][self.threshold_bin[i]])
+        if inner.size:
+            bmax = max(len(e) for e in edges)
+            table = np.full((len(edges), bmax), np.nan)
+            for f, e in enumerate(edges):
+                table[f, : len(e)] = e
+            thr[inner] = table[self.feature[inner], self.threshold_bin[inner]]
         self.threshold = thr
         return self
 

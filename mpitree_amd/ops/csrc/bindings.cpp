@@ -4,8 +4,8 @@
 // current HIP stream handle, so no PyTorch headers are compiled here: the
 // extension builds in seconds with hipcc and calls cost one pybind hop.
 #include <hip/hip_runtime.h>
-#include <pybind11/pybind11.h>
 #include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
 
 #include "common.h"
 #include "criterion.h"
@@ -14,21 +14,29 @@ namespace py = pybind11;
 
 namespace mt {
 int hist_feature_tile(int F_h, int B, int C, bool reg, int lds_budget);
-void launch_hist(hipStream_t, const void*, int, int64_t, const int32_t*, const void*,
+int64_t hist_slab_words(int F_h, int B, int C, bool reg);
+void launch_hist(hipStream_t, const void*, int, int64_t, const uint32_t*, const void*, int,
                  const int64_t*, int, void*, void*, int, int, int, int, bool, int);
-void launch_hist_reduce(hipStream_t, const int64_t*, int, const void*, void*, int64_t, bool);
+void launch_hist_reduce(hipStream_t, const int64_t*, int, int, const void*, void*, int, int, int,
+                        bool);
 void launch_hist_derive(hipStream_t, const int64_t*, int, const void*, void*, int64_t, bool);
 void launch_scan(hipStream_t, const void*, const int64_t*, int, const int32_t*, int, int, int,
-                 int, int, int, double*, int32_t*, int64_t*);
-void launch_partition(hipStream_t, const void*, int, int64_t, int32_t*, int32_t*, const int64_t*,
-                      int, const int64_t*, int32_t*);
-void launch_seg_stats(hipStream_t, const int32_t*, const void*, bool, const int64_t*, int, void*,
-                      int);
+                 int, int, int, double*, int32_t*, int64_t*, const double*, int);
+void launch_partition(hipStream_t, const void*, int, int64_t, uint32_t*, uint32_t*, uint32_t,
+                      const int64_t*, int, const int64_t*, int32_t*);
+void launch_seg_stats(hipStream_t, const uint32_t*, const void*, int, bool, const int64_t*, int,
+                      void*, int);
+void launch_init_idx(hipStream_t, uint32_t*, const int32_t*, int, int64_t);
 void launch_predict(hipStream_t, const void*, bool, int64_t, int, const void*, const double*,
                     int32_t*);
 void launch_bin(hipStream_t, const void*, bool, int64_t, int, const void*, int, const int32_t*,
                 const uint8_t*, void*, int, void*, int, int32_t*);
 void launch_xlog2x(hipStream_t, double*, int64_t);
+void launch_finish(hipStream_t, const void*, int64_t, const void*, int, int64_t, uint32_t*,
+                   uint32_t*, const int32_t*, int, const int64_t*, int, int32_t*, const int32_t*,
+                   int, int, int, int, int, int64_t, int64_t, const double*, int, int32_t*,
+                   int32_t*, int32_t*, int);
+int finish_lds_bytes(int F, int B, int C);
 }  // namespace mt
 
 template <typename T>
@@ -40,15 +48,18 @@ static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "mpitree_amd gfx950 HIP kernels";
   m.def("hist_feature_tile", &mt::hist_feature_tile);
+  m.def("hist_slab_words", &mt::hist_slab_words);
   m.def("hist", [](uintptr_t s, uintptr_t codes, int cb, int64_t rs, uintptr_t idx, uintptr_t y,
-                   uintptr_t items, int n_items, uintptr_t hist, uintptr_t slab, int F_h,
-                   int f_lo, int B, int C, bool reg, int lds) {
-    mt::launch_hist(S(s), P<void>(codes), cb, rs, P<int32_t>(idx), P<void>(y), P<int64_t>(items),
-                    n_items, P<void>(hist), P<void>(slab), F_h, f_lo, B, C, reg, lds);
+                   int lab_shift, uintptr_t items, int n_items, uintptr_t hist, uintptr_t slab,
+                   int F_h, int f_lo, int B, int C, bool reg, int lds) {
+    mt::launch_hist(S(s), P<void>(codes), cb, rs, P<uint32_t>(idx), P<void>(y), lab_shift,
+                    P<int64_t>(items), n_items, P<void>(hist), P<void>(slab), F_h, f_lo, B, C,
+                    reg, lds);
   });
-  m.def("hist_reduce", [](uintptr_t s, uintptr_t red, int n, uintptr_t slab, uintptr_t hist,
-                          int64_t E, bool is64) {
-    mt::launch_hist_reduce(S(s), P<int64_t>(red), n, P<void>(slab), P<void>(hist), E, is64);
+  m.def("hist_reduce", [](uintptr_t s, uintptr_t red, int n, int max_k, uintptr_t slab,
+                          uintptr_t hist, int F_h, int B, int C, bool reg) {
+    mt::launch_hist_reduce(S(s), P<int64_t>(red), n, max_k, P<void>(slab), P<void>(hist), F_h, B,
+                           C, reg);
   });
   m.def("hist_derive", [](uintptr_t s, uintptr_t der, int n, uintptr_t prev, uintptr_t hist,
                           int64_t E, bool is64) {
@@ -56,20 +67,25 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("scan", [](uintptr_t s, uintptr_t hist, uintptr_t nodes, int k, uintptr_t nbins, int F_h,
                    int f_lo, int B, int C, int crit, int msl, uintptr_t cost, uintptr_t bins,
-                   uintptr_t rec) {
+                   uintptr_t rec, uintptr_t xtab, int xtab_n) {
     mt::launch_scan(S(s), P<void>(hist), P<int64_t>(nodes), k, P<int32_t>(nbins), F_h, f_lo, B, C,
-                    crit, msl, P<double>(cost), P<int32_t>(bins), P<int64_t>(rec));
+                    crit, msl, P<double>(cost), P<int32_t>(bins), P<int64_t>(rec),
+                    P<double>(xtab), xtab_n);
   });
   m.def("partition", [](uintptr_t s, uintptr_t codes_fm, int cb, int64_t n_rows, uintptr_t idx,
-                        uintptr_t tmp, uintptr_t items, int n_items, uintptr_t split,
-                        uintptr_t cursors) {
-    mt::launch_partition(S(s), P<void>(codes_fm), cb, n_rows, P<int32_t>(idx), P<int32_t>(tmp),
-                         P<int64_t>(items), n_items, P<int64_t>(split), P<int32_t>(cursors));
+                        uintptr_t tmp, uint32_t mask, uintptr_t items, int n_items,
+                        uintptr_t split, uintptr_t cursors) {
+    mt::launch_partition(S(s), P<void>(codes_fm), cb, n_rows, P<uint32_t>(idx),
+                         P<uint32_t>(tmp), mask, P<int64_t>(items), n_items, P<int64_t>(split),
+                         P<int32_t>(cursors));
   });
-  m.def("seg_stats", [](uintptr_t s, uintptr_t idx, uintptr_t y, bool reg, uintptr_t items,
-                        int n_items, uintptr_t out, int C) {
-    mt::launch_seg_stats(S(s), P<int32_t>(idx), P<void>(y), reg, P<int64_t>(items), n_items,
-                         P<void>(out), C);
+  m.def("seg_stats", [](uintptr_t s, uintptr_t idx, uintptr_t y, int lab_shift, bool reg,
+                        uintptr_t items, int n_items, uintptr_t out, int C) {
+    mt::launch_seg_stats(S(s), P<uint32_t>(idx), P<void>(y), lab_shift, reg, P<int64_t>(items),
+                         n_items, P<void>(out), C);
+  });
+  m.def("init_idx", [](uintptr_t s, uintptr_t idx, uintptr_t y, int lab_shift, int64_t n) {
+    mt::launch_init_idx(S(s), P<uint32_t>(idx), P<int32_t>(y), lab_shift, n);
   });
   m.def("predict", [](uintptr_t s, uintptr_t X, bool x64, int64_t n, int F, uintptr_t nodes,
                       uintptr_t thr, uintptr_t leaf) {
@@ -82,6 +98,19 @@ PYBIND11_MODULE(_hip, m) {
     mt::launch_bin(S(s), P<void>(X), x64, n, F, P<void>(edges), Bmax, P<int32_t>(nbins),
                    P<uint8_t>(exact), P<void>(codes_rm), row_elems, P<void>(codes_fm), cb,
                    P<int32_t>(bad));
+  });
+  m.def("finish_lds_bytes", &mt::finish_lds_bytes);
+  m.def("finish", [](uintptr_t s, uintptr_t codes_rm, int64_t row_words, uintptr_t codes_fm,
+                     int cb, int64_t n_rows, uintptr_t idx, uintptr_t tmp, uintptr_t y,
+                     int lab_shift, uintptr_t jobs, int J, uintptr_t counter, uintptr_t nbins,
+                     int F, int B, int C, int crit, int max_depth, int64_t mss, int64_t msl,
+                     uintptr_t xtab, int xtab_n, uintptr_t node_i32, uintptr_t node_cnt,
+                     uintptr_t job_nodes, int grid) {
+    mt::launch_finish(S(s), P<void>(codes_rm), row_words, P<void>(codes_fm), cb, n_rows,
+                      P<uint32_t>(idx), P<uint32_t>(tmp), P<int32_t>(y), lab_shift,
+                      P<int64_t>(jobs), J, P<int32_t>(counter), P<int32_t>(nbins), F, B, C, crit,
+                      max_depth, mss, msl, P<double>(xtab), xtab_n, P<int32_t>(node_i32),
+                      P<int32_t>(node_cnt), P<int32_t>(job_nodes), grid);
   });
   m.def("xlog2x_device", [](uintptr_t s, uintptr_t out, int64_t n) {
     mt::launch_xlog2x(S(s), P<double>(out), n);

@@ -6,78 +6,126 @@
 // and right class distributions are prefix sums (split_scan.hip).
 //
 // Design (CDNA4):
-//  * rows of a node are addressed through the row permutation ``idx`` and
-//    read as 32-bit words of the row-major code matrix, several lanes per row
-//    (one lane per 4 u8 codes), so a wave touches whole 64-B rows;
+//  * rows of a node are addressed through the row permutation ``idx``. For
+//    classification with n < 2^24 rows and <= 256 classes the label rides in
+//    the top byte of the permutation entry (row | label << 24), so one
+//    coalesced 4-B load yields both and no label gather is needed;
+//  * the row-major code matrix is read with 16-B loads (4 lanes per 64-B row
+//    for 64 u8 features), each lane keeping 4 rows in flight, so a 512-thread
+//    workgroup has 512 row gathers outstanding to hide HBM/L2 latency;
 //  * each workgroup privatises the histogram of its feature tile in LDS.
-//    Classification packs two classes per 32-bit LDS word (16-bit halves;
-//    a work item is at most 65535 rows so a half never overflows), halving
-//    LDS footprint and atomics; the feature stride is padded by one word so
-//    lanes of one row with equal codes hit different banks;
-//  * no global atomics: a work item that covers a whole node writes the
-//    final histogram with plain stores, items of a multi-item node write a
-//    private slab that ``hist_reduce`` sums (integer, so order-free and
-//    bitwise deterministic);
+//    Classification packs two classes per 32-bit LDS word (16-bit halves; a
+//    work item is at most 65535 rows so a half never overflows), halving LDS
+//    footprint and atomics; the feature stride is padded by one word so lanes
+//    of one row with equal codes land in different banks;
+//  * no global atomics on the hot path: a work item that covers a whole node
+//    writes the final histogram with plain stores; items of a multi-item node
+//    write their packed LDS image to a private slab, and ``hist_reduce``
+//    sums groups of slabs in parallel (integer sums: order-free, bitwise
+//    deterministic);
 //  * histograms that cannot fit one feature in LDS (very large B*C) fall back
 //    to direct global atomics.
 #include "common.h"
 
 namespace mt {
 
-// items: int64 [n_items][4] = {slot, start, count, dest}; dest < 0 -> write
-// hist[slot], dest >= 0 -> write slab[dest].
-template <typename CodeT>
-__global__ __launch_bounds__(256) void hist_cls_lds_kernel(
-    const CodeT* __restrict__ codes, int64_t row_words, const int32_t* __restrict__ idx,
-    const int32_t* __restrict__ y, const int64_t* __restrict__ items,
-    uint32_t* __restrict__ hist, uint32_t* __restrict__ slab, int F_h, int f_lo, int B,
-    int C, int ft, int wpr_shift) {
+constexpr int kHistThreads = 512;
+constexpr int kUnroll = 4;  // rows in flight per lane
+
+struct RowLab {
+  uint32_t mask;
+  int shift;  // > 0: label packed in the permutation entry
+};
+
+// items: int64 [n_items][4] = {slot, start, count, dest}; dest < 0 -> unpack
+// into hist[slot], dest >= 0 -> raw packed LDS image into slab[dest].
+template <typename CodeT, int VEC>
+__global__ __launch_bounds__(kHistThreads) void hist_cls_lds_kernel(
+    const uint32_t* __restrict__ codes, int64_t row_words, const uint32_t* __restrict__ idx,
+    const int32_t* __restrict__ y, RowLab rl, const int64_t* __restrict__ items,
+    uint32_t* __restrict__ hist, uint32_t* __restrict__ slab, int F_h, int f_lo, int B, int C,
+    int ft, int lane_shift) {
   extern __shared__ uint32_t lds[];
   constexpr int cpw = 4 / sizeof(CodeT);  // codes per 32-bit word
   const int W = (C + 1) >> 1;
   const int fstride = B * W + 1;
-  const int tile = blockIdx.y;
-  const int t0 = tile * ft;                       // first hist feature of tile
-  const int t1 = min(F_h, t0 + ft);               // end (exclusive)
-  const int g0 = f_lo + t0;                       // global feature index
-  const int gw0 = g0 / cpw;                       // first code word
-  const int nwords = (f_lo + t1 + cpw - 1) / cpw - gw0;
+  const int t0 = blockIdx.y * ft;
+  const int t1 = min(F_h, t0 + ft);
+  const int nf = t1 - t0;
+  const int g0 = f_lo + t0, g1 = f_lo + t1;
+  const int gw0 = (g0 / cpw) & ~(VEC - 1);  // first (VEC-aligned) code word
+  const int nwords = (g1 + cpw - 1) / cpw - gw0;
   const int64_t slot = items[blockIdx.x * 4 + 0];
   const int64_t start = items[blockIdx.x * 4 + 1];
   const int64_t count = items[blockIdx.x * 4 + 2];
   const int64_t dest = items[blockIdx.x * 4 + 3];
 
-  const int lds_words = (t1 - t0) * fstride;
+  const int lds_words = nf * fstride;
   for (int e = threadIdx.x; e < lds_words; e += blockDim.x) lds[e] = 0u;
   __syncthreads();
 
-  const uint32_t* __restrict__ cw = reinterpret_cast<const uint32_t*>(codes);
-  const int wpr = 1 << wpr_shift;
-  const int sub = threadIdx.x & (wpr - 1);
-  const int rows_per_pass = blockDim.x >> wpr_shift;
-  if (sub < nwords) {
-    for (int64_t r = threadIdx.x >> wpr_shift; r < count; r += rows_per_pass) {
-      const int32_t row = idx[start + r];
-      const int32_t lab = y[row];
-      const uint32_t word = cw[(int64_t)row * row_words + gw0 + sub];
-      const uint32_t inc = 1u << ((lab & 1) * 16);
-      const int cw_off = lab >> 1;
+  const int L = 1 << lane_shift;  // lanes per row
+  const int sub = threadIdx.x & (L - 1);
+  const int rpp = blockDim.x >> lane_shift;  // rows per block pass
+  const int my_w = gw0 + sub * VEC;
+  const bool active = sub * VEC < nwords;
+  for (int64_t base = threadIdx.x >> lane_shift; base < count; base += (int64_t)rpp * kUnroll) {
+    uint32_t ent[kUnroll];
 #pragma unroll
-      for (int j = 0; j < cpw; ++j) {
-        const int gf = (gw0 + sub) * cpw + j;
-        if (gf >= g0 && gf < f_lo + t1) {
-          const uint32_t code = (word >> (j * 8 * sizeof(CodeT))) &
-                                ((sizeof(CodeT) == 1) ? 0xffu : 0xffffu);
-          atomicAdd(&lds[(gf - g0) * fstride + (int)code * W + cw_off], inc);
+    for (int u = 0; u < kUnroll; ++u) {
+      const int64_t r = base + (int64_t)u * rpp;
+      ent[u] = (active && r < count) ? idx[start + r] : 0xffffffffu;
+    }
+    uint32_t w[kUnroll][VEC];
+    int lab[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const bool ok = ent[u] != 0xffffffffu;
+      const uint32_t row = rl.shift ? (ent[u] & rl.mask) : ent[u];
+      lab[u] = ok ? (rl.shift ? (int)(ent[u] >> rl.shift) : y[row]) : 0;
+      if constexpr (VEC == 4) {
+        uint4 v = ok ? *reinterpret_cast<const uint4*>(codes + (int64_t)row * row_words + my_w)
+                     : make_uint4(0, 0, 0, 0);
+        w[u][0] = v.x;
+        w[u][1] = v.y;
+        w[u][2] = v.z;
+        w[u][3] = v.w;
+      } else {
+        w[u][0] = ok ? codes[(int64_t)row * row_words + my_w] : 0u;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      if (ent[u] == 0xffffffffu) continue;
+      const uint32_t inc = 1u << ((lab[u] & 1) * 16);
+      const int off = lab[u] >> 1;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+#pragma unroll
+        for (int j = 0; j < cpw; ++j) {
+          const int gf = (my_w + v) * cpw + j;
+          if (gf >= g0 && gf < g1) {
+            const uint32_t code = (w[u][v] >> (j * 8 * sizeof(CodeT))) &
+                                  ((sizeof(CodeT) == 1) ? 0xffu : 0xffffu);
+            atomicAdd(&lds[(gf - g0) * fstride + (int)code * W + off], inc);
+          }
         }
       }
     }
   }
   __syncthreads();
 
-  uint32_t* out = dest < 0 ? hist + slot * (int64_t)F_h * B * C : slab + dest * (int64_t)F_h * B * C;
   const int per_f = B * W;
-  for (int e = threadIdx.x; e < lds_words - (t1 - t0); e += blockDim.x) {
+  if (dest >= 0) {  // packed image -> slab (tile's features are contiguous)
+    uint32_t* out = slab + dest * (int64_t)F_h * per_f + (int64_t)t0 * per_f;
+    for (int e = threadIdx.x; e < nf * per_f; e += blockDim.x) {
+      const int f = e / per_f;
+      out[e] = lds[f * fstride + (e - f * per_f)];
+    }
+    return;
+  }
+  uint32_t* out = hist + slot * (int64_t)F_h * B * C;
+  for (int e = threadIdx.x; e < nf * per_f; e += blockDim.x) {
     const int f = e / per_f;
     const int rem = e - f * per_f;
     const int b = rem / W;
@@ -91,20 +139,19 @@ __global__ __launch_bounds__(256) void hist_cls_lds_kernel(
 
 // Regression payload: per bin {count, fixed-point target sum} as two int64.
 template <typename CodeT>
-__global__ __launch_bounds__(256) void hist_reg_lds_kernel(
-    const CodeT* __restrict__ codes, int64_t row_words, const int32_t* __restrict__ idx,
+__global__ __launch_bounds__(kHistThreads) void hist_reg_lds_kernel(
+    const CodeT* __restrict__ codes, int64_t row_words, const uint32_t* __restrict__ idx,
     const int64_t* __restrict__ y, const int64_t* __restrict__ items,
     int64_t* __restrict__ hist, int64_t* __restrict__ slab, int F_h, int f_lo, int B, int ft,
-    int wpr_shift) {
+    int lane_shift) {
   extern __shared__ uint32_t lds[];
   constexpr int cpw = 4 / sizeof(CodeT);
-  const int tile = blockIdx.y;
-  const int t0 = tile * ft;
+  const int t0 = blockIdx.y * ft;
   const int t1 = min(F_h, t0 + ft);
   const int nf = t1 - t0;
-  const int g0 = f_lo + t0;
+  const int g0 = f_lo + t0, g1 = f_lo + t1;
   const int gw0 = g0 / cpw;
-  const int nwords = (f_lo + t1 + cpw - 1) / cpw - gw0;
+  const int nwords = (g1 + cpw - 1) / cpw - gw0;
   const int64_t slot = items[blockIdx.x * 4 + 0];
   const int64_t start = items[blockIdx.x * 4 + 1];
   const int64_t count = items[blockIdx.x * 4 + 2];
@@ -117,18 +164,18 @@ __global__ __launch_bounds__(256) void hist_reg_lds_kernel(
   for (int e = threadIdx.x; e < nf * cstride; e += blockDim.x) cnts[e] = 0u;
   __syncthreads();
   const uint32_t* __restrict__ cw = reinterpret_cast<const uint32_t*>(codes);
-  const int wpr = 1 << wpr_shift;
-  const int sub = threadIdx.x & (wpr - 1);
-  const int rows_per_pass = blockDim.x >> wpr_shift;
+  const int L = 1 << lane_shift;
+  const int sub = threadIdx.x & (L - 1);
+  const int rpp = blockDim.x >> lane_shift;
   if (sub < nwords) {
-    for (int64_t r = threadIdx.x >> wpr_shift; r < count; r += rows_per_pass) {
-      const int32_t row = idx[start + r];
+    for (int64_t r = threadIdx.x >> lane_shift; r < count; r += rpp) {
+      const uint32_t row = idx[start + r];
       const unsigned long long yv = (unsigned long long)y[row];
       const uint32_t word = cw[(int64_t)row * row_words + gw0 + sub];
 #pragma unroll
       for (int j = 0; j < cpw; ++j) {
         const int gf = (gw0 + sub) * cpw + j;
-        if (gf >= g0 && gf < f_lo + t1) {
+        if (gf >= g0 && gf < g1) {
           const uint32_t code = (word >> (j * 8 * sizeof(CodeT))) &
                                 ((sizeof(CodeT) == 1) ? 0xffu : 0xffffu);
           atomicAdd(&cnts[(gf - g0) * cstride + (int)code], 1u);
@@ -151,8 +198,8 @@ __global__ __launch_bounds__(256) void hist_reg_lds_kernel(
 // Fallback: direct global atomics (B*C too large for an LDS feature tile).
 template <typename CodeT>
 __global__ __launch_bounds__(256) void hist_cls_global_kernel(
-    const CodeT* __restrict__ codes, int64_t row_elems, const int32_t* __restrict__ idx,
-    const int32_t* __restrict__ y, const int64_t* __restrict__ items,
+    const CodeT* __restrict__ codes, int64_t row_elems, const uint32_t* __restrict__ idx,
+    const int32_t* __restrict__ y, RowLab rl, const int64_t* __restrict__ items,
     uint32_t* __restrict__ hist, int F_h, int f_lo, int B, int C) {
   const int64_t slot = items[blockIdx.x * 4 + 0];
   const int64_t start = items[blockIdx.x * 4 + 1];
@@ -162,15 +209,17 @@ __global__ __launch_bounds__(256) void hist_cls_global_kernel(
   for (int64_t e = threadIdx.x; e < total; e += blockDim.x) {
     const int64_t r = e / F_h;
     const int f = (int)(e - r * F_h);
-    const int32_t row = idx[start + r];
+    const uint32_t ent = idx[start + r];
+    const uint32_t row = rl.shift ? (ent & rl.mask) : ent;
+    const int lab = rl.shift ? (int)(ent >> rl.shift) : y[row];
     const int code = (int)codes[(int64_t)row * row_elems + f_lo + f];
-    atomicAdd(&out[((int64_t)f * B + code) * C + y[row]], 1u);
+    atomicAdd(&out[((int64_t)f * B + code) * C + lab], 1u);
   }
 }
 
 template <typename CodeT>
 __global__ __launch_bounds__(256) void hist_reg_global_kernel(
-    const CodeT* __restrict__ codes, int64_t row_elems, const int32_t* __restrict__ idx,
+    const CodeT* __restrict__ codes, int64_t row_elems, const uint32_t* __restrict__ idx,
     const int64_t* __restrict__ y, const int64_t* __restrict__ items,
     int64_t* __restrict__ hist, int F_h, int f_lo, int B) {
   const int64_t slot = items[blockIdx.x * 4 + 0];
@@ -182,24 +231,71 @@ __global__ __launch_bounds__(256) void hist_reg_global_kernel(
   for (int64_t e = threadIdx.x; e < total; e += blockDim.x) {
     const int64_t r = e / F_h;
     const int f = (int)(e - r * F_h);
-    const int32_t row = idx[start + r];
+    const uint32_t row = idx[start + r];
     const int code = (int)codes[(int64_t)row * row_elems + f_lo + f];
     atomicAdd(&out[((int64_t)f * B + code) * 2], 1ull);
     atomicAdd(&out[((int64_t)f * B + code) * 2 + 1], (unsigned long long)y[row]);
   }
 }
 
-// hist[slot] = sum of slab[first .. first+k) ; red: int64 [n][3] = {slot, first, k}
-template <typename T>
-__global__ __launch_bounds__(256) void hist_reduce_kernel(const int64_t* __restrict__ red,
-                                                          const T* __restrict__ slab,
-                                                          T* __restrict__ hist, int64_t E) {
+// ---------------------------------------------------------------- reduction
+// red: int64 [n][3] = {slot, first slab, k slabs}.
+// Classification slabs hold the packed [F_h][B][W] LDS image (two 16-bit
+// classes per word); grid = (word chunks, red entries, slab groups). Each
+// thread unpacks and sums up to G slabs of one word and adds the result to
+// the (zeroed) histogram.
+__global__ __launch_bounds__(256) void zero_slots_kernel(const int64_t* __restrict__ red,
+                                                         uint32_t* __restrict__ hist,
+                                                         int64_t E) {
+  const int64_t slot = red[blockIdx.y * 3 + 0];
+  if ((E & 3) == 0) {  // every slot base is 16-B aligned
+    uint4* h = reinterpret_cast<uint4*>(hist + slot * E);
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E / 4;
+         e += (int64_t)gridDim.x * blockDim.x)
+      h[e] = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E;
+       e += (int64_t)gridDim.x * blockDim.x)
+    hist[slot * E + e] = 0;
+}
+
+__global__ __launch_bounds__(256) void hist_reduce_cls_kernel(
+    const int64_t* __restrict__ red, const uint32_t* __restrict__ slab,
+    uint32_t* __restrict__ hist, int64_t Ep, int C, int W, int G) {
+  const int64_t slot = red[blockIdx.y * 3 + 0];
+  const int64_t first = red[blockIdx.y * 3 + 1];
+  const int64_t k = red[blockIdx.y * 3 + 2];
+  const int64_t k0 = (int64_t)blockIdx.z * G;
+  if (k0 >= k) return;
+  const int64_t k1 = min(k, k0 + G);
+  const int64_t Eu = (Ep / W) * C;
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e >= Ep) return;
+  uint32_t a0 = 0, a1 = 0;
+  for (int64_t j = k0; j < k1; ++j) {
+    const uint32_t v = slab[(first + j) * Ep + e];
+    a0 += v & 0xffffu;
+    a1 += v >> 16;
+  }
+  const int64_t fb = e / W;
+  const int wc = (int)(e - fb * W);
+  uint32_t* out = hist + slot * Eu + fb * C + 2 * wc;
+  if (a0) atomicAdd(out, a0);
+  if (a1 && 2 * wc + 1 < C) atomicAdd(out + 1, a1);
+}
+
+// regression slabs are already [F][B][2] int64
+__global__ __launch_bounds__(256) void hist_reduce_reg_kernel(const int64_t* __restrict__ red,
+                                                              const int64_t* __restrict__ slab,
+                                                              int64_t* __restrict__ hist,
+                                                              int64_t E) {
   const int64_t slot = red[blockIdx.y * 3 + 0];
   const int64_t first = red[blockIdx.y * 3 + 1];
   const int64_t k = red[blockIdx.y * 3 + 2];
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E;
        e += (int64_t)gridDim.x * blockDim.x) {
-    T acc = 0;
+    int64_t acc = 0;
     for (int64_t j = 0; j < k; ++j) acc += slab[(first + j) * E + e];
     hist[slot * E + e] = acc;
   }
@@ -213,6 +309,38 @@ __global__ __launch_bounds__(256) void hist_derive_kernel(const int64_t* __restr
   const int64_t slot = der[blockIdx.y * 3 + 0];
   const int64_t ps = der[blockIdx.y * 3 + 1];
   const int64_t ss = der[blockIdx.y * 3 + 2];
+  // 16-B vectors (E is a multiple of 4 elements for every histogram shape we allocate
+  // whenever B*C % 4 == 0; the scalar tail handles the rest)
+  constexpr int V = 16 / sizeof(T);
+  const int64_t nv = E / V;
+  using VT = uint4;
+  const VT* pp = reinterpret_cast<const VT*>(prev + ps * E);
+  const VT* sp = reinterpret_cast<const VT*>(hist + ss * E);
+  VT* op = reinterpret_cast<VT*>(hist + slot * E);
+  const bool aligned = (E % V) == 0;
+  if (aligned) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < nv;
+         e += (int64_t)gridDim.x * blockDim.x) {
+      const VT a = pp[e], b = sp[e];
+      VT r;
+      if (sizeof(T) == 4) {
+        r.x = a.x - b.x;
+        r.y = a.y - b.y;
+        r.z = a.z - b.z;
+        r.w = a.w - b.w;
+      } else {
+        const uint64_t a0 = ((uint64_t)a.y << 32) | a.x, a1 = ((uint64_t)a.w << 32) | a.z;
+        const uint64_t b0 = ((uint64_t)b.y << 32) | b.x, b1 = ((uint64_t)b.w << 32) | b.z;
+        const uint64_t r0 = a0 - b0, r1 = a1 - b1;
+        r.x = (uint32_t)r0;
+        r.y = (uint32_t)(r0 >> 32);
+        r.z = (uint32_t)r1;
+        r.w = (uint32_t)(r1 >> 32);
+      }
+      op[e] = r;
+    }
+    return;
+  }
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E;
        e += (int64_t)gridDim.x * blockDim.x) {
     hist[slot * E + e] = prev[ps * E + e] - hist[ss * E + e];
@@ -224,44 +352,47 @@ __global__ __launch_bounds__(256) void hist_derive_kernel(const int64_t* __restr
 // ----------------------------------------------------------------- launchers
 namespace mt {
 
-static int floor_pow2_shift(int v) {
-  int s = 0;
-  while ((1 << (s + 1)) <= v) ++s;
-  return s;
-}
 static int ceil_pow2_shift(int v) {
   int s = 0;
   while ((1 << s) < v) ++s;
   return s;
 }
 
-// Returns the features-per-tile used by the LDS kernel (0 -> global fallback).
+// Features per LDS tile for the histogram kernel (0 -> global-atomic fallback).
 int hist_feature_tile(int F_h, int B, int C, bool reg, int lds_budget) {
   int per_f = reg ? (B * 8 + (B + 1) * 4) : (B * ((C + 1) / 2) + 1) * 4;
   int ft = lds_budget / per_f;
   if (ft <= 0) return 0;
   if (ft >= F_h) return F_h;
-  if (ft >= 4) ft &= ~3;
+  if (ft >= 16) ft &= ~15;
+  else if (ft >= 4) ft &= ~3;
   return ft;
 }
 
+// Words of the packed classification slab per work item ([F_h][B][W]).
+int64_t hist_slab_words(int F_h, int B, int C, bool reg) {
+  return reg ? (int64_t)F_h * B * 2 : (int64_t)F_h * B * ((C + 1) / 2);
+}
+
 void launch_hist(hipStream_t stream, const void* codes, int code_bytes, int64_t row_stride_bytes,
-                 const int32_t* idx, const void* y, const int64_t* items, int n_items, void* hist,
-                 void* slab, int F_h, int f_lo, int B, int C, bool reg, int lds_budget) {
+                 const uint32_t* idx, const void* y, int lab_shift, const int64_t* items,
+                 int n_items, void* hist, void* slab, int F_h, int f_lo, int B, int C, bool reg,
+                 int lds_budget) {
   if (n_items <= 0) return;
   const int ft = hist_feature_tile(F_h, B, C, reg, lds_budget);
-  dim3 block(256);
+  RowLab rl{lab_shift ? ((1u << lab_shift) - 1u) : 0xffffffffu, lab_shift};
   if (ft == 0) {
     dim3 grid(n_items);
     const int64_t row_elems = row_stride_bytes / code_bytes;
-#define MT_GLOBAL(CT)                                                                        \
-  if (reg)                                                                                   \
-    hipLaunchKernelGGL(hist_reg_global_kernel<CT>, grid, block, 0, stream, (const CT*)codes, \
-                       row_elems, idx, (const int64_t*)y, items, (int64_t*)hist, F_h, f_lo, B); \
-  else                                                                                       \
-    hipLaunchKernelGGL(hist_cls_global_kernel<CT>, grid, block, 0, stream, (const CT*)codes, \
-                       row_elems, idx, (const int32_t*)y, items, (uint32_t*)hist, F_h, f_lo, B, \
-                       C);
+#define MT_GLOBAL(CT)                                                                          \
+  if (reg)                                                                                     \
+    hipLaunchKernelGGL(hist_reg_global_kernel<CT>, grid, dim3(256), 0, stream,                 \
+                       (const CT*)codes, row_elems, idx, (const int64_t*)y, items,             \
+                       (int64_t*)hist, F_h, f_lo, B);                                          \
+  else                                                                                         \
+    hipLaunchKernelGGL(hist_cls_global_kernel<CT>, grid, dim3(256), 0, stream,                 \
+                       (const CT*)codes, row_elems, idx, (const int32_t*)y, rl, items,         \
+                       (uint32_t*)hist, F_h, f_lo, B, C);
     if (code_bytes == 1) {
       MT_GLOBAL(uint8_t)
     } else {
@@ -273,60 +404,97 @@ void launch_hist(hipStream_t stream, const void* codes, int code_bytes, int64_t 
   }
   const int n_tiles = (F_h + ft - 1) / ft;
   const int cpw = 4 / code_bytes;
-  // 32-bit code words spanned by the widest tile; lanes per row = pow2 >= that
+  const int64_t row_words = row_stride_bytes / 4;
+  dim3 grid(n_items, n_tiles);
+  if (reg) {
+    int words = 1;
+    for (int t = 0; t < n_tiles; ++t) {
+      const int a = f_lo + t * ft, b = f_lo + std::min(F_h, (t + 1) * ft);
+      words = std::max(words, (b + cpw - 1) / cpw - a / cpw);
+    }
+    int shift = std::min(ceil_pow2_shift(words), 9);
+    size_t lds = (size_t)ft * (B * 8 + (B + 1) * 4);
+#define MT_REG(CT)                                                                            \
+  MT_HIP_CHECK(hipFuncSetAttribute((const void*)hist_reg_lds_kernel<CT>,                      \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));    \
+  hipLaunchKernelGGL(hist_reg_lds_kernel<CT>, grid, dim3(kHistThreads), lds, stream,          \
+                     (const CT*)codes, row_words, idx, (const int64_t*)y, items,              \
+                     (int64_t*)hist, (int64_t*)slab, F_h, f_lo, B, ft, shift);
+    if (code_bytes == 1) {
+      MT_REG(uint8_t)
+    } else {
+      MT_REG(uint16_t)
+    }
+#undef MT_REG
+    MT_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  // 16-B row loads when every tile's word range is 4-word aligned
+  bool vec4 = (row_words % 4) == 0;
   int words = 1;
   for (int t = 0; t < n_tiles; ++t) {
     const int a = f_lo + t * ft, b = f_lo + std::min(F_h, (t + 1) * ft);
-    words = std::max(words, (b + cpw - 1) / cpw - a / cpw);
+    const int w0 = (a / cpw) & ~3;
+    words = std::max(words, (b + cpw - 1) / cpw - (vec4 ? w0 : a / cpw));
   }
-  int wpr_shift = ceil_pow2_shift(words);
-  if (wpr_shift > 8) wpr_shift = 8;
-  (void)floor_pow2_shift;
-  size_t lds = reg ? (size_t)ft * (B * 8 + (B + 1) * 4)
-                   : (size_t)ft * (B * ((C + 1) / 2) + 1) * 4;
-  dim3 grid(n_items, n_tiles);
-  const int64_t row_words = row_stride_bytes / 4;
-#define MT_LDS(CT)                                                                            \
-  if (reg) {                                                                                  \
-    MT_HIP_CHECK(hipFuncSetAttribute((const void*)hist_reg_lds_kernel<CT>,                    \
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));  \
-    hipLaunchKernelGGL(hist_reg_lds_kernel<CT>, grid, block, lds, stream, (const CT*)codes,   \
-                       row_words, idx, (const int64_t*)y, items, (int64_t*)hist,              \
-                       (int64_t*)slab, F_h, f_lo, B, ft, wpr_shift);                          \
-  } else {                                                                                    \
-    MT_HIP_CHECK(hipFuncSetAttribute((const void*)hist_cls_lds_kernel<CT>,                    \
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));  \
-    hipLaunchKernelGGL(hist_cls_lds_kernel<CT>, grid, block, lds, stream, (const CT*)codes,   \
-                       row_words, idx, (const int32_t*)y, items, (uint32_t*)hist,             \
-                       (uint32_t*)slab, F_h, f_lo, B, C, ft, wpr_shift);                      \
-  }
+  const int vec = vec4 ? 4 : 1;
+  const int lanes = (words + vec - 1) / vec;
+  const int shift = std::min(ceil_pow2_shift(lanes), 6);
+  size_t lds = (size_t)ft * (B * ((C + 1) / 2) + 1) * 4;
+#define MT_CLS(CT, V)                                                                         \
+  MT_HIP_CHECK(hipFuncSetAttribute((const void*)hist_cls_lds_kernel<CT, V>,                   \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));    \
+  hipLaunchKernelGGL((hist_cls_lds_kernel<CT, V>), grid, dim3(kHistThreads), lds, stream,     \
+                     (const uint32_t*)codes, row_words, idx, (const int32_t*)y, rl, items,    \
+                     (uint32_t*)hist, (uint32_t*)slab, F_h, f_lo, B, C, ft, shift);
   if (code_bytes == 1) {
-    MT_LDS(uint8_t)
+    if (vec4) {
+      MT_CLS(uint8_t, 4)
+    } else {
+      MT_CLS(uint8_t, 1)
+    }
   } else {
-    MT_LDS(uint16_t)
+    if (vec4) {
+      MT_CLS(uint16_t, 4)
+    } else {
+      MT_CLS(uint16_t, 1)
+    }
   }
-#undef MT_LDS
+#undef MT_CLS
   MT_HIP_CHECK(hipGetLastError());
 }
 
-void launch_hist_reduce(hipStream_t stream, const int64_t* red, int n_red, const void* slab,
-                        void* hist, int64_t E, bool is64) {
+void launch_hist_reduce(hipStream_t stream, const int64_t* red, int n_red, int max_k,
+                        const void* slab, void* hist, int F_h, int B, int C, bool reg) {
   if (n_red <= 0) return;
-  int gx = (int)std::min<int64_t>((E + 255) / 256, 512);
-  dim3 grid(gx, n_red);
-  if (is64)
-    hipLaunchKernelGGL(hist_reduce_kernel<int64_t>, grid, dim3(256), 0, stream, red,
+  if (reg) {
+    const int64_t E = (int64_t)F_h * B * 2;
+    int gx = (int)std::min<int64_t>((E + 255) / 256, 1024);
+    hipLaunchKernelGGL(hist_reduce_reg_kernel, dim3(gx, n_red), dim3(256), 0, stream, red,
                        (const int64_t*)slab, (int64_t*)hist, E);
-  else
-    hipLaunchKernelGGL(hist_reduce_kernel<uint32_t>, grid, dim3(256), 0, stream, red,
-                       (const uint32_t*)slab, (uint32_t*)hist, E);
+    MT_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  const int W = (C + 1) / 2;
+  const int64_t Ep = (int64_t)F_h * B * W;
+  const int64_t Eu = (int64_t)F_h * B * C;
+  hipLaunchKernelGGL(zero_slots_kernel, dim3((unsigned)std::min<int64_t>((Eu / 4 + 255) / 256, 256),
+                                             n_red),
+                     dim3(256), 0, stream, red, (uint32_t*)hist, Eu);
+  MT_HIP_CHECK(hipGetLastError());
+  const int G = 16;
+  const int groups = (max_k + G - 1) / G;
+  dim3 grid((unsigned)((Ep + 255) / 256), n_red, groups);
+  hipLaunchKernelGGL(hist_reduce_cls_kernel, grid, dim3(256), 0, stream, red,
+                     (const uint32_t*)slab, (uint32_t*)hist, Ep, C, W, G);
   MT_HIP_CHECK(hipGetLastError());
 }
 
 void launch_hist_derive(hipStream_t stream, const int64_t* der, int n_der, const void* prev,
                         void* hist, int64_t E, bool is64) {
   if (n_der <= 0) return;
-  int gx = (int)std::min<int64_t>((E + 255) / 256, 512);
+  int gx = (int)std::min<int64_t>((E / 4 + 255) / 256, 256);
+  if (gx < 1) gx = 1;
   dim3 grid(gx, n_der);
   if (is64)
     hipLaunchKernelGGL(hist_derive_kernel<int64_t>, grid, dim3(256), 0, stream, der,

@@ -2,17 +2,19 @@
 //
 // Replaces the reference's ``X[region], y[region]`` / ``X[~region]`` copies
 // that feed the recursion (mpitree/tree/decision_tree.py:150-164, :428-454):
-// instead of copying feature rows, only the int32 row permutation ``idx`` is
+// instead of copying feature rows, only the 4-B row permutation ``idx`` is
 // reordered so that each child's rows are contiguous inside the parent's
 // segment. The split feature is read from the feature-major code matrix, a
 // single 1-byte column per node that stays L2-resident.
 //
 // Each workgroup handles a 1024-row chunk of one split node's segment, counts
-// its left rows with wave ballots, reserves space with one atomic per cursor
-// (left cursor grows from the segment start, right cursor shrinks from the
-// segment end) and scatters into a temporary buffer; a copy kernel writes the
-// segments back. The order of rows inside a child is not stable, which is
+// its left rows with wave prefix sums, reserves space with one atomic per
+// cursor (left cursor grows from the segment start, right cursor shrinks from
+// the segment end) and scatters into a temporary buffer; a copy kernel writes
+// the segments back. The order of rows inside a child is not stable, which is
 // harmless: every statistic downstream is an integer (or fixed-point) sum.
+// Permutation entries may carry the class label in their top bits
+// (``row | label << shift``, see hist.hip); ``mask`` extracts the row.
 #include "common.h"
 
 namespace mt {
@@ -25,8 +27,8 @@ constexpr int kPartRows = 4;  // rows per thread -> 1024 rows per workgroup
 // cursors: int32 [k][2] = {left cursor, right cursor} (initialised by host)
 template <typename CodeT>
 __global__ __launch_bounds__(kPartThreads) void partition_kernel(
-    const CodeT* __restrict__ codes_fm, int64_t n_rows, const int32_t* __restrict__ idx,
-    int32_t* __restrict__ tmp, const int64_t* __restrict__ items,
+    const CodeT* __restrict__ codes_fm, int64_t n_rows, const uint32_t* __restrict__ idx,
+    uint32_t* __restrict__ tmp, uint32_t mask, const int64_t* __restrict__ items,
     const int64_t* __restrict__ split, int32_t* __restrict__ cursors) {
   __shared__ uint32_t s_left[kPartThreads / kWave];
   __shared__ uint32_t s_right[kPartThreads / kWave];
@@ -40,20 +42,21 @@ __global__ __launch_bounds__(kPartThreads) void partition_kernel(
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
 
-  int32_t rows[kPartRows];
+  uint32_t ent[kPartRows];
   bool go[kPartRows], valid[kPartRows];
   uint32_t my_l = 0, my_r = 0;
 #pragma unroll
   for (int k = 0; k < kPartRows; ++k) {
-    // wave-contiguous layout: element e = (k * 256 + threadIdx.x)
     const int64_t e = (int64_t)k * kPartThreads + threadIdx.x;
     valid[k] = e < cn;
-    rows[k] = valid[k] ? idx[c0 + e] : 0;
-    go[k] = valid[k] && (uint32_t)col[rows[k]] <= bin;
+    ent[k] = valid[k] ? idx[c0 + e] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < kPartRows; ++k) {
+    go[k] = valid[k] && (uint32_t)col[ent[k] & mask] <= bin;
     my_l += (valid[k] && go[k]) ? 1u : 0u;
     my_r += (valid[k] && !go[k]) ? 1u : 0u;
   }
-  // per-wave exclusive prefix of left/right counts
   uint32_t il = my_l, ir = my_r;
 #pragma unroll
   for (int d = 1; d < kWave; d <<= 1) {
@@ -87,16 +90,16 @@ __global__ __launch_bounds__(kPartThreads) void partition_kernel(
   for (int k = 0; k < kPartRows; ++k) {
     if (valid[k]) {
       if (go[k])
-        tmp[pl++] = rows[k];
+        tmp[pl++] = ent[k];
       else
-        tmp[pr++] = rows[k];
+        tmp[pr++] = ent[k];
     }
   }
 }
 
 // idx[seg] = tmp[seg] for every chunk item
-__global__ __launch_bounds__(256) void copy_back_kernel(const int32_t* __restrict__ tmp,
-                                                        int32_t* __restrict__ idx,
+__global__ __launch_bounds__(256) void copy_back_kernel(const uint32_t* __restrict__ tmp,
+                                                        uint32_t* __restrict__ idx,
                                                         const int64_t* __restrict__ items) {
   const int64_t c0 = items[blockIdx.x * 3 + 1];
   const int64_t cn = items[blockIdx.x * 3 + 2];
@@ -106,8 +109,9 @@ __global__ __launch_bounds__(256) void copy_back_kernel(const int32_t* __restric
 // segment statistics: items int64 [n][3] = {segment s, start, count}
 // classification: out uint32 [S][C] (class counts)
 // regression: out int64 [S][4] = {count, sum, min, max}
-__global__ __launch_bounds__(256) void seg_stats_cls_kernel(const int32_t* __restrict__ idx,
+__global__ __launch_bounds__(256) void seg_stats_cls_kernel(const uint32_t* __restrict__ idx,
                                                             const int32_t* __restrict__ y,
+                                                            int lab_shift,
                                                             const int64_t* __restrict__ items,
                                                             uint32_t* __restrict__ out, int C) {
   extern __shared__ uint32_t cnt[];
@@ -116,13 +120,17 @@ __global__ __launch_bounds__(256) void seg_stats_cls_kernel(const int32_t* __res
   const int64_t cn = items[blockIdx.x * 3 + 2];
   for (int c = threadIdx.x; c < C; c += blockDim.x) cnt[c] = 0;
   __syncthreads();
-  for (int64_t e = threadIdx.x; e < cn; e += blockDim.x) atomicAdd(&cnt[y[idx[c0 + e]]], 1u);
+  for (int64_t e = threadIdx.x; e < cn; e += blockDim.x) {
+    const uint32_t v = idx[c0 + e];
+    const int lab = lab_shift ? (int)(v >> lab_shift) : y[v];
+    atomicAdd(&cnt[lab], 1u);
+  }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x)
     if (cnt[c]) atomicAdd(&out[s * C + c], cnt[c]);
 }
 
-__global__ __launch_bounds__(256) void seg_stats_reg_kernel(const int32_t* __restrict__ idx,
+__global__ __launch_bounds__(256) void seg_stats_reg_kernel(const uint32_t* __restrict__ idx,
                                                             const int64_t* __restrict__ y,
                                                             const int64_t* __restrict__ items,
                                                             int64_t* __restrict__ out) {
@@ -170,23 +178,31 @@ __global__ __launch_bounds__(256) void seg_stats_reg_kernel(const int32_t* __res
   }
 }
 
+// idx[i] = i | y[i] << shift  (packed permutation with labels) or i
+__global__ __launch_bounds__(256) void init_idx_kernel(uint32_t* __restrict__ idx,
+                                                       const int32_t* __restrict__ y,
+                                                       int lab_shift, int64_t n) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) idx[i] = lab_shift ? ((uint32_t)i | ((uint32_t)y[i] << lab_shift)) : (uint32_t)i;
+}
+
 void launch_partition(hipStream_t stream, const void* codes_fm, int code_bytes, int64_t n_rows,
-                      int32_t* idx, int32_t* tmp, const int64_t* items, int n_items,
-                      const int64_t* split, int32_t* cursors) {
+                      uint32_t* idx, uint32_t* tmp, uint32_t mask, const int64_t* items,
+                      int n_items, const int64_t* split, int32_t* cursors) {
   if (n_items <= 0) return;
   if (code_bytes == 1)
     hipLaunchKernelGGL(partition_kernel<uint8_t>, dim3(n_items), dim3(kPartThreads), 0, stream,
-                       (const uint8_t*)codes_fm, n_rows, idx, tmp, items, split, cursors);
+                       (const uint8_t*)codes_fm, n_rows, idx, tmp, mask, items, split, cursors);
   else
     hipLaunchKernelGGL(partition_kernel<uint16_t>, dim3(n_items), dim3(kPartThreads), 0, stream,
-                       (const uint16_t*)codes_fm, n_rows, idx, tmp, items, split, cursors);
+                       (const uint16_t*)codes_fm, n_rows, idx, tmp, mask, items, split, cursors);
   MT_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(copy_back_kernel, dim3(n_items), dim3(256), 0, stream, tmp, idx, items);
   MT_HIP_CHECK(hipGetLastError());
 }
 
-void launch_seg_stats(hipStream_t stream, const int32_t* idx, const void* y, bool reg,
-                      const int64_t* items, int n_items, void* out, int C) {
+void launch_seg_stats(hipStream_t stream, const uint32_t* idx, const void* y, int lab_shift,
+                      bool reg, const int64_t* items, int n_items, void* out, int C) {
   if (n_items <= 0) return;
   if (reg) {
     hipLaunchKernelGGL(seg_stats_reg_kernel, dim3(n_items), dim3(256), 0, stream, idx,
@@ -196,8 +212,16 @@ void launch_seg_stats(hipStream_t stream, const int32_t* idx, const void* y, boo
     MT_HIP_CHECK(hipFuncSetAttribute((const void*)seg_stats_cls_kernel,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(seg_stats_cls_kernel, dim3(n_items), dim3(256), lds, stream, idx,
-                       (const int32_t*)y, items, (uint32_t*)out, C);
+                       (const int32_t*)y, lab_shift, items, (uint32_t*)out, C);
   }
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_init_idx(hipStream_t stream, uint32_t* idx, const int32_t* y, int lab_shift,
+                     int64_t n) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(init_idx_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                     idx, y, lab_shift, n);
   MT_HIP_CHECK(hipGetLastError());
 }
 

@@ -17,12 +17,20 @@ namespace mt {
 constexpr int kBinsPerLane = 4;
 constexpr int kChunk = kWave * kBinsPerLane;  // 256 bins per wave pass
 
+// T(x) = x*log2(x) from a device table built by the same function (so the
+// values are identical) for small counts, evaluated otherwise. The scan is
+// fp64-VALU bound without it at deep levels.
+__device__ __forceinline__ double tlog(uint64_t x, const double* __restrict__ tab, int tn) {
+  return x < (uint64_t)tn ? __ldg(tab + x) : xlog2x(x);
+}
+
 // hist: uint32 [slots][F_h][B][C]; nodes: int64 [k] slot ids
 // out_cost: f64 [k][F_h]; out_bin: i32 [k][F_h]
 __global__ __launch_bounds__(256) void scan_cls_kernel(
     const uint32_t* __restrict__ hist, const int64_t* __restrict__ nodes,
     const int32_t* __restrict__ nbins, int F_h, int f_lo, int B, int C, int crit, int msl,
-    double* __restrict__ out_cost, int32_t* __restrict__ out_bin) {
+    double* __restrict__ out_cost, int32_t* __restrict__ out_bin,
+    const double* __restrict__ xtab, int xtab_n) {
   extern __shared__ uint32_t sm[];  // per wave: C class totals + C carries
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
@@ -90,8 +98,8 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
         mL[k] += L;
         nonempty[k] |= v[k];
         if (crit == kEntropy) {
-          sL[k] = sL[k] + xlog2x(L);
-          sR[k] = sR[k] + xlog2x(R);
+          sL[k] = sL[k] + tlog(L, xtab, xtab_n);
+          sR[k] = sR[k] + tlog(R, xtab, xtab_n);
         } else {
           qL[k] += (int64_t)L * L;
           qR[k] += (int64_t)R * R;
@@ -108,7 +116,8 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
       if (b < nb && nonempty[k] && ml >= msl && mr >= msl) {
         double cost;
         if (crit == kEntropy)
-          cost = (xlog2x((uint64_t)ml) - sL[k]) + (xlog2x((uint64_t)mr) - sR[k]);
+          cost = (tlog((uint64_t)ml, xtab, xtab_n) - sL[k]) +
+                 (tlog((uint64_t)mr, xtab, xtab_n) - sR[k]);
         else
           cost = gini_term(ml, qL[k]) + gini_term(mr, qR[k]);
         if (cost < best_cost) {
@@ -350,7 +359,7 @@ __global__ __launch_bounds__(256) void select_kernel(
 
 void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int k,
                  const int32_t* nbins, int F_h, int f_lo, int B, int C, int crit, int msl,
-                 double* cost, int32_t* bins, int64_t* rec) {
+                 double* cost, int32_t* bins, int64_t* rec, const double* xtab, int xtab_n) {
   if (k <= 0) return;
   dim3 grid(k, (F_h + 3) / 4);
   if (crit == kSquaredError) {
@@ -361,7 +370,7 @@ void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int
     MT_HIP_CHECK(hipFuncSetAttribute((const void*)scan_cls_kernel,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(scan_cls_kernel, grid, dim3(256), lds, stream, (const uint32_t*)hist,
-                       nodes, nbins, F_h, f_lo, B, C, crit, msl, cost, bins);
+                       nodes, nbins, F_h, f_lo, B, C, crit, msl, cost, bins, xtab, xtab_n);
   }
   MT_HIP_CHECK(hipGetLastError());
   const size_t sel_lds = crit == kSquaredError ? 16 : (size_t)2 * C * sizeof(int64_t);

@@ -22,6 +22,7 @@ __all__ = ["HipBackend", "gpu_bin_features"]
 
 LDS_BUDGET = int(os.environ.get("MPITREE_HIST_LDS", 80 * 1024))
 MAX_ITEM_ROWS = 65535  # 16-bit packed LDS counters
+N_CU = 256  # MI355X compute units
 
 
 def _stream() -> int:
@@ -165,6 +166,22 @@ def gpu_bin_features(X: torch.Tensor, max_bins=256, sample_rows: int = 1 << 17):
     return mapper, codes_rm, codes_fm, nb
 
 
+XTAB_N = 1 << 16
+_xtab_cache: dict = {}
+
+
+def xlog2x_table(device) -> torch.Tensor:
+    """Device table of x*log2(x) for x < 2^16, built once per device by the same
+    device function the kernels would otherwise evaluate (identical bits)."""
+    key = str(device)
+    t = _xtab_cache.get(key)
+    if t is None:
+        t = torch.empty(XTAB_N, dtype=torch.float64, device=device)
+        native.hip().xlog2x_device(_stream(), t.data_ptr(), XTAB_N)
+        _xtab_cache[key] = t
+    return t
+
+
 class HipBackend:
     """Device state and kernel launches for one fit on the current GPU."""
 
@@ -191,8 +208,14 @@ class HipBackend:
         self.crit = criterion
         self.reg = criterion == Criterion.SQUARED_ERROR
         self.C = 2 if self.reg else int(n_classes)
-        self.idx = torch.arange(self.n, dtype=torch.int32, device=self.device)
+        # row permutation; classification packs the label into the top byte
+        self.lab_shift = 24 if (not self.reg and self.n < (1 << 24) and self.C <= 256) else 0
+        self.row_mask = (1 << self.lab_shift) - 1 if self.lab_shift else 0xFFFFFFFF
+        self.idx = torch.empty(self.n, dtype=torch.int32, device=self.device)
+        self.hip.init_idx(_stream(), self.idx.data_ptr(),
+                          self.y.data_ptr() if not self.reg else 0, self.lab_shift, self.n)
         self.tmp = torch.empty_like(self.idx)
+        self.xtab = xlog2x_table(self.device)
 
     def hist_elems(self, F_h: int) -> int:
         return F_h * self.B * (2 if self.reg else self.C)
@@ -213,41 +236,39 @@ class HipBackend:
         F_h = f_hi - f_lo
         if len(slots) == 0:
             return
+        slots = np.asarray(slots, dtype=np.int64)
+        starts = np.asarray(starts, dtype=np.int64)
         counts = np.asarray(counts, dtype=np.int64)
         total = int(counts.sum())
-        chunk = int(min(MAX_ITEM_ROWS, max(2048, -(-total // 1024))))
         ft = self.hip.hist_feature_tile(F_h, self.B, self.C, self.reg, LDS_BUDGET)
-        items, red = [], []
-        nslab = 0
-        for s, st, ct in zip(slots, starts, counts):
-            k = max(1, -(-int(ct) // chunk))
-            if k == 1 or ft == 0:
-                # one item (or global-atomic fallback): write the node's hist directly
-                if ft == 0:
-                    for c0 in range(0, max(int(ct), 1), MAX_ITEM_ROWS):
-                        items.append((s, st + c0, min(MAX_ITEM_ROWS, ct - c0), -1))
-                else:
-                    items.append((s, st, ct, -1))
-                continue
-            red.append((s, nslab, k))
-            for i in range(k):
-                c0 = i * chunk
-                items.append((s, st + c0, min(chunk, ct - c0), nslab + i))
-            nslab += k
-        items = np.asarray(items, dtype=np.int64).reshape(-1, 4)
-        red = np.asarray(red, dtype=np.int64).reshape(-1, 3)
+        # ~2 workgroups per CU over the whole level, at most 65535 rows per item
+        chunk = int(min(MAX_ITEM_ROWS, max(1024, -(-total // (2 * N_CU)))))
+        if ft == 0:
+            chunk = MAX_ITEM_ROWS  # global-atomic fallback: every item adds into hist
+        k = np.maximum(1, -(-counts // chunk))
+        node_of = np.repeat(np.arange(len(slots)), k)
+        first = np.cumsum(k) - k
+        i_in = np.arange(node_of.size) - first[node_of]
+        c0 = i_in * chunk
+        multi = (k > 1) & (ft > 0)
+        slab_base = np.cumsum(np.where(multi, k, 0)) - np.where(multi, k, 0)
+        dest = np.where(multi[node_of], slab_base[node_of] + i_in, -1)
+        items = np.stack([slots[node_of], starts[node_of] + c0,
+                          np.minimum(chunk, counts[node_of] - c0), dest], 1)
+        red = np.stack([slots[multi], slab_base[multi], k[multi]], 1)
+        nslab = int(k[multi].sum())
         d_items, d_red = self.up(items, red)
-        E = self.hist_elems(F_h)
         slab = None
         if nslab:
-            slab = torch.empty((nslab, E), dtype=hist.dtype, device=self.device)
+            sw = self.hip.hist_slab_words(F_h, self.B, self.C, self.reg)
+            slab = torch.empty((nslab, sw), dtype=hist.dtype, device=self.device)
         self.hip.hist(_stream(), self.codes_rm.data_ptr(), self.cb, self.row_elems * self.cb,
-                      self.idx.data_ptr(), self.y.data_ptr(), d_items.data_ptr(), items.shape[0],
-                      hist.data_ptr(), 0 if slab is None else slab.data_ptr(), F_h, f_lo, self.B,
-                      self.C, self.reg, LDS_BUDGET)
+                      self.idx.data_ptr(), self.y.data_ptr(), self.lab_shift, d_items.data_ptr(),
+                      items.shape[0], hist.data_ptr(), 0 if slab is None else slab.data_ptr(),
+                      F_h, f_lo, self.B, self.C, self.reg, LDS_BUDGET)
         if nslab:
-            self.hip.hist_reduce(_stream(), d_red.data_ptr(), red.shape[0], slab.data_ptr(),
-                                 hist.data_ptr(), E, self.reg)
+            self.hip.hist_reduce(_stream(), d_red.data_ptr(), red.shape[0], int(k[multi].max()),
+                                 slab.data_ptr(), hist.data_ptr(), F_h, self.B, self.C, self.reg)
         self._keep = (slab, d_items, d_red)
 
     def derive_hist(self, hist, prev_hist, slots, parent_slots, sibling_slots):
@@ -273,21 +294,11 @@ class HipBackend:
         rec = torch.empty((k, R), dtype=torch.int64, device=self.device)
         self.hip.scan(_stream(), hist.data_ptr(), d_nodes.data_ptr(), k, self.nbins.data_ptr(),
                       F_h, f_lo, self.B, C, int(self.crit), int(max(1, min_samples_leaf)),
-                      cost.data_ptr(), bins.data_ptr(), rec.data_ptr())
+                      cost.data_ptr(), bins.data_ptr(), rec.data_ptr(), self.xtab.data_ptr(),
+                      XTAB_N)
+        self.last_rec = rec
         r = rec.cpu().numpy()
-        gain = r[:, 0].copy().view(np.float64)
-        out = {
-            "gain": gain,
-            "feature": r[:, 1].astype(np.int32),
-            "bin": r[:, 2].astype(np.int32),
-            "n_left": r[:, 3].copy(),
-            "m": r[:, 4].copy(),
-        }
-        if self.reg:
-            out["left"] = np.stack([r[:, 3], r[:, 5]], 1)
-        else:
-            out["left"] = r[:, 5 : 5 + C].copy()
-        return out
+        return unpack_records(r, C, self.reg)
 
     # ------------------------------------------------------------- partition
     def partition(self, starts, counts, features, bins, need_counts=True):
@@ -298,17 +309,13 @@ class HipBackend:
         counts = np.asarray(counts, dtype=np.int64)
         split = np.stack([starts, counts, np.asarray(features, np.int64),
                           np.asarray(bins, np.int64)], 1)
-        items = []
-        for j in range(k):
-            for c0 in range(0, int(counts[j]), 1024):
-                items.append((j, starts[j] + c0, min(1024, counts[j] - c0)))
-        items = np.asarray(items, dtype=np.int64).reshape(-1, 3)
+        items = chunk_items(np.arange(k), starts, counts, 1024)
         cursors = np.stack([starts, starts + counts], 1)
         d_split, d_items, d_cur64 = self.up(split, items, cursors)
         cur = d_cur64.view(k, 2).to(torch.int32)
         self.hip.partition(_stream(), self.codes_fm.data_ptr(), self.cb, self.n,
-                           self.idx.data_ptr(), self.tmp.data_ptr(), d_items.data_ptr(),
-                           items.shape[0], d_split.data_ptr(), cur.data_ptr())
+                           self.idx.data_ptr(), self.tmp.data_ptr(), self.row_mask,
+                           d_items.data_ptr(), items.shape[0], d_split.data_ptr(), cur.data_ptr())
         if not need_counts:
             self._keep_p = (d_split, d_items, cur)
             return None
@@ -316,14 +323,8 @@ class HipBackend:
 
     def segment_stats(self, starts, counts):
         k = len(starts)
-        items = np.stack([np.arange(k), np.asarray(starts, np.int64),
-                          np.asarray(counts, np.int64)], 1).astype(np.int64)
-        # split long segments into 64K-row items for parallelism
-        rows = []
-        for s, st, ct in items:
-            for c0 in range(0, max(int(ct), 1), 65536):
-                rows.append((s, st + c0, min(65536, ct - c0)))
-        items = np.asarray(rows, dtype=np.int64).reshape(-1, 3)
+        items = chunk_items(np.arange(k), np.asarray(starts, np.int64),
+                            np.asarray(counts, np.int64), 4096)
         (d_items,) = self.up(items)
         if self.reg:
             out = torch.zeros((k, 4), dtype=torch.int64, device=self.device)
@@ -331,10 +332,98 @@ class HipBackend:
             out[:, 3] = np.iinfo(np.int64).min
         else:
             out = torch.zeros((k, self.C), dtype=torch.int32, device=self.device)
-        self.hip.seg_stats(_stream(), self.idx.data_ptr(), self.y.data_ptr(), self.reg,
-                           d_items.data_ptr(), items.shape[0], out.data_ptr(), self.C)
+        self.hip.seg_stats(_stream(), self.idx.data_ptr(), self.y.data_ptr(), self.lab_shift,
+                           self.reg, d_items.data_ptr(), items.shape[0], out.data_ptr(), self.C)
         return out.cpu().numpy().astype(np.int64)
+
+    # -------------------------------------------------------------- finisher
+    def finisher_supported(self) -> bool:
+        if self.reg or self.cb != 1 or self.C > 64 or self.B > 256:
+            return False
+        return self.F * (self.B * ((self.C + 1) // 2) + 1) * 4 <= 150 * 1024
+
+    def finish_subtrees(self, starts, counts, depths, params):
+        """Grow every job's subtree on the device; concatenated node tables out.
+
+        Returns a dict of arrays (feature, bin, left, right, depth, nsamp,
+        stats) holding all jobs' nodes, job j at ``offsets[j]:offsets[j+1]``
+        with root first and child indices local to the job.
+        """
+        J = len(starts)
+        starts = np.asarray(starts, np.int64)
+        counts = np.asarray(counts, np.int64)
+        depths = np.asarray(depths, np.int64)
+        order = np.argsort(-counts, kind="stable")  # largest first
+        slots = 2 * counts[order] - 1
+        base = np.cumsum(slots) - slots
+        jobs = np.stack([starts[order], counts[order], depths[order], base], 1)
+        total = int(slots.sum())
+        C = self.C
+        (d_jobs,) = self.up(jobs)
+        node_i32 = torch.empty((total, 6), dtype=torch.int32, device=self.device)
+        node_cnt = torch.empty((total, C), dtype=torch.int32, device=self.device)
+        job_nodes = torch.empty(J, dtype=torch.int32, device=self.device)
+        counter = torch.zeros(1, dtype=torch.int32, device=self.device)
+        md = -1 if params.max_depth is None else int(params.max_depth)
+        grid = int(min(J, 2 * N_CU))
+        self.hip.finish(_stream(), self.codes_rm.data_ptr(), self.row_elems * self.cb // 4,
+                        self.codes_fm.data_ptr(), self.cb, self.n, self.idx.data_ptr(),
+                        self.tmp.data_ptr(), self.y.data_ptr(), self.lab_shift, d_jobs.data_ptr(),
+                        J, counter.data_ptr(), self.nbins.data_ptr(), self.F, self.B, C,
+                        int(self.crit), md, int(params.min_samples_split),
+                        int(max(1, params.min_samples_leaf)), self.xtab.data_ptr(), XTAB_N,
+                        node_i32.data_ptr(), node_cnt.data_ptr(), job_nodes.data_ptr(), grid)
+        jn = job_nodes.cpu().numpy().astype(np.int64)
+        # compact the used slots on the device, one D2H copy
+        base_t = torch.from_numpy(base).to(self.device)
+        jn_t = torch.from_numpy(jn).to(self.device)
+        rep_base = torch.repeat_interleave(base_t, jn_t)
+        within = torch.arange(int(jn.sum()), device=self.device) - torch.repeat_interleave(
+            torch.cumsum(jn_t, 0) - jn_t, jn_t)
+        sel = rep_base + within
+        ni = node_i32.index_select(0, sel).cpu().numpy()
+        nc = node_cnt.index_select(0, sel).cpu().numpy()
+        # back to the caller's job order
+        inv = np.empty(J, np.int64)
+        inv[order] = np.arange(J)
+        off_sorted = np.concatenate([[0], np.cumsum(jn)])
+        lens = jn[inv]
+        offsets = np.concatenate([[0], np.cumsum(lens)])
+        take = np.repeat(off_sorted[inv], lens) + (
+            np.arange(int(offsets[-1])) - np.repeat(offsets[:-1], lens))
+        ni = ni[take]
+        nc = nc[take]
+        return dict(feature=ni[:, 0], bin=ni[:, 1], left=ni[:, 2].astype(np.int64),
+                    right=ni[:, 3].astype(np.int64), depth=ni[:, 4], nsamp=ni[:, 5].astype(np.int64),
+                    stats=nc.astype(np.int64), offsets=offsets)
 
     def sync(self):
         if self.timing:
             torch.cuda.synchronize(self.device)
+
+
+def chunk_items(ids, starts, counts, chunk):
+    """[n, 3] int64 items {id, start, count} cutting segments into <= chunk rows."""
+    ids = np.asarray(ids, dtype=np.int64)
+    k = np.maximum(1, -(-counts // chunk))
+    node_of = np.repeat(np.arange(len(ids)), k)
+    first = np.cumsum(k) - k
+    c0 = (np.arange(node_of.size) - first[node_of]) * chunk
+    return np.stack([ids[node_of], starts[node_of] + c0,
+                     np.maximum(0, np.minimum(chunk, counts[node_of] - c0))], 1)
+
+
+def unpack_records(r: np.ndarray, C: int, reg: bool) -> dict:
+    """Split-record rows (see split_scan.hip select_kernel) -> dict of arrays."""
+    out = {
+        "gain": r[:, 0].copy().view(np.float64),
+        "feature": r[:, 1].astype(np.int32),
+        "bin": r[:, 2].astype(np.int32),
+        "n_left": r[:, 3].copy(),
+        "m": r[:, 4].copy(),
+    }
+    if reg:
+        out["left"] = np.stack([r[:, 3], r[:, 5]], 1)
+    else:
+        out["left"] = r[:, 5 : 5 + C].copy()
+    return out

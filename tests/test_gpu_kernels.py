@@ -95,3 +95,29 @@ def test_gpu_quantile_bins_consistent_predict():
     # device and host traversal agree exactly on the raw values
     np.testing.assert_array_equal(clf.apply(Xd).cpu().numpy(), clf.tree_arrays_.apply(X))
     assert clf.score(X, y) > 0.9
+
+
+@pytest.mark.parametrize("rows", ["16", "200", "5000"])
+@pytest.mark.parametrize("crit", ["entropy", "gini"])
+def test_gpu_finisher_matches_oracle(monkeypatch, rows, crit):
+    monkeypatch.setenv("MPITREE_FINISHER_ROWS", rows)
+    rng = np.random.default_rng(int(rows) + len(crit))
+    n, F, C = 6000, 6, 3
+    X, y = random_problem(rng, n, F, C, levels=12)
+    for md in (None, 7):
+        ref = oracle(X, y, Criterion.ENTROPY if crit == "entropy" else Criterion.GINI, md)
+        clf = DecisionTreeClassifier(max_depth=md, criterion=crit, device="cuda").fit(X, y)
+        assert clf.tree_arrays_.equal(ref), (rows, md, clf.tree_arrays_.node_count, ref.node_count)
+        if rows != "5000":
+            assert clf.fit_stats_.get("finisher_subtrees", 0) > 0
+
+
+def test_gpu_finisher_deep_chain(monkeypatch):
+    # a fully grown tree whose splits peel one row at a time (deep, skinny)
+    monkeypatch.setenv("MPITREE_FINISHER_ROWS", "1000")
+    n = 600
+    X = np.arange(n, dtype=np.float64).reshape(-1, 1)
+    y = np.arange(n) % 7
+    ref = oracle(X, y, Criterion.ENTROPY, None, max_bins=1024)
+    clf = DecisionTreeClassifier(max_bins=1024, device="cuda").fit(X, y)
+    assert clf.tree_arrays_.equal(ref)
