@@ -216,6 +216,11 @@ def fit_tree(
         t0 = time.perf_counter()
         mapper, codes_rm, codes_fm, nb = gpu_bin_features(Xd, max_bins)
         yd = (yv if _is_tensor(yv) else torch.from_numpy(np.ascontiguousarray(yv))).to("cuda")
+        lo, hi = comm.local_rows(n)
+        if (lo, hi) != (0, n):  # data-parallel shard of a replicated input
+            codes_rm = codes_rm[lo:hi].contiguous()
+            codes_fm = codes_fm[:, lo:hi].contiguous()
+            yd = yd[lo:hi]
         yd = yd.contiguous()
         timings["bin"] = time.perf_counter() - t0
         be = HipBackend()
@@ -229,7 +234,7 @@ def fit_tree(
             finisher_rows = 0
         params.finisher_rows = int(finisher_rows)
         builder = LevelwiseBuilder(be, params, comm)
-        ta = builder.fit(n, C, F)
+        ta = builder.fit(hi - lo, C, F)
         eng = "hip-levelwise"
         timings.update(builder.timings)
         stats = dict(builder.stats)
@@ -239,6 +244,9 @@ def fit_tree(
         t0 = time.perf_counter()
         mapper = fit_bin_mapper(Xh, max_bins)
         codes = mapper.transform(Xh)
+        lo, hi = comm.local_rows(n)
+        if (lo, hi) != (0, n):
+            codes, yh = codes[lo:hi], yh[lo:hi]
         timings["bin"] = time.perf_counter() - t0
         use_native = (
             engine in (None, "native") and comm.world_size == 1 and native.has_cpu()
@@ -254,11 +262,15 @@ def fit_tree(
 
             be = NumpyBackend()
             be.setup(codes, yh, n_bins=mapper.max_n_bins, n_classes=C, criterion=crit)
+            params.finisher_rows = int(finisher_rows or 0)
             builder = LevelwiseBuilder(be, params, comm)
-            ta = builder.fit(n, C, F)
+            ta = builder.fit(hi - lo, C, F)
             eng = "numpy-levelwise"
             timings.update(builder.timings)
             stats = dict(builder.stats)
+    if comm.world_size > 1:
+        stats["strategy"] = comm.kind
+        stats["bytes_communicated"] = getattr(comm, "bytes_communicated", 0)
     ta = _finalize(ta, mapper, regression, y_exp)
     timings["total"] = time.perf_counter() - t_start
     return FitResult(arrays=ta, classes=classes, n_features=F, mapper=mapper, y_scale_exp=y_exp,

@@ -60,6 +60,10 @@ class LocalComm:
     def feature_range(self, F: int):
         return 0, F
 
+    def local_rows(self, n: int):
+        """Row range of the (replicated) input this rank trains on."""
+        return 0, n
+
     def reduce_hist(self, hist, n_slots: int):
         return None
 
@@ -121,6 +125,12 @@ class _Table:
 
 def _node_terms(crit, stats: np.ndarray) -> np.ndarray:
     """Vectorised node terms for every node (stats: [N, C] counts or [N, 2])."""
+    try:
+        from ..ops import native
+
+        return native.cpu().node_terms(np.ascontiguousarray(stats, dtype=np.int64), int(crit))
+    except ImportError:
+        pass
     if crit == Criterion.ENTROPY:
         return entropy_term(stats)
     if crit == Criterion.GINI:

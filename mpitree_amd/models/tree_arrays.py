@@ -95,6 +95,20 @@ class TreeArrays:
         left = np.asarray(left, dtype=np.int64)
         right = np.asarray(right, dtype=np.int64)
         n = feature.shape[0]
+        try:
+            from ..ops import native
+
+            cpu = native.cpu()
+        except ImportError:
+            cpu = None
+        if cpu is not None:
+            order, depth_old = cpu.preorder(feature.astype(np.int32), left, right, int(root))
+            k = order.shape[0]
+            new_id = np.full(n, -1, dtype=np.int64)
+            new_id[order] = np.arange(k)
+            return TreeArrays._reindex(order, new_id, depth_old, feature, left, right,
+                                       threshold_bin, n_samples, impurity, count, value,
+                                       threshold)
         # level-synchronous passes (vectorised over each depth):
         # 1) nodes per depth from the root, 2) subtree sizes bottom-up,
         # 3) pre-order index top-down: left = parent + 1, right = left + |left subtree|
@@ -122,6 +136,13 @@ class TreeArrays:
         order = np.empty(k, dtype=np.int64)
         reach = new_id >= 0
         order[new_id[reach]] = np.nonzero(reach)[0]
+        return TreeArrays._reindex(order, new_id, depth_old, feature, left, right, threshold_bin,
+                                   n_samples, impurity, count, value, threshold)
+
+    @staticmethod
+    def _reindex(order, new_id, depth_old, feature, left, right, threshold_bin, n_samples,
+                 impurity, count, value, threshold) -> "TreeArrays":
+        k = order.shape[0]
         f = feature[order].astype(np.int32)
         lm = left[order]
         rm = right[order]

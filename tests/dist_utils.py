@@ -1,0 +1,37 @@
+"""Multi-process harness: run a function on N gloo ranks (CPU, 127.0.0.1)."""
+
+import os
+import socket
+import tempfile
+
+import numpy as np
+import torch.multiprocessing as mp
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _entry(rank, world, port, fn, args, outdir):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = fn(rank, world, *args)
+        np.savez(os.path.join(outdir, f"r{rank}.npz"), **out)
+    finally:
+        dist.destroy_process_group()
+
+
+def run_ranks(fn, world, *args):
+    """Run ``fn(rank, world, *args) -> dict[str, array]`` on ``world`` ranks."""
+    port = free_port()
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_entry, args=(world, port, fn, args, d), nprocs=world, join=True,
+                           start_method="fork")
+        return [dict(np.load(os.path.join(d, f"r{r}.npz"), allow_pickle=False))
+                for r in range(world)]

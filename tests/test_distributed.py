@@ -1,0 +1,117 @@
+"""Distributed strategies on CPU ranks (gloo): every rank returns the same
+tree, and it is identical to the single-process tree."""
+
+import numpy as np
+import pytest
+
+from .dist_utils import run_ranks
+
+FIELDS = ("feature", "threshold_bin", "left", "right", "n_samples", "depth")
+
+
+def _data(seed=0, n=700, F=7, C=3, regression=False):
+    rng = np.random.default_rng(seed)
+    X = rng.integers(0, 16, size=(n, F)).astype(np.float64)
+    s = X @ rng.normal(size=F) + rng.normal(scale=2.0, size=n)
+    if regression:
+        return X, np.round(s, 2)
+    y = np.digitize(s, np.quantile(s, np.linspace(0, 1, C + 1)[1:-1]))
+    return X, y
+
+
+def _fit_rank(rank, world, strategy, seed, md, regression):
+    from mpitree_amd import ParallelDecisionTreeClassifier, ParallelDecisionTreeRegressor
+
+    X, y = _data(seed, regression=regression)
+    cls = ParallelDecisionTreeRegressor if regression else ParallelDecisionTreeClassifier
+    est = cls(max_depth=md, strategy=strategy, device="cpu").fit(X, y)
+    ta = est.tree_arrays_
+    out = {k: getattr(ta, k) for k in FIELDS}
+    out["value"] = ta.value if regression else ta.count
+    out["rank"] = np.array([est.WORLD_RANK, est.WORLD_SIZE])
+    out["strategy"] = np.array([est.fit_stats_.get("strategy", "local")])
+    return out
+
+
+def _serial(seed, md, regression):
+    from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
+
+    X, y = _data(seed, regression=regression)
+    cls = DecisionTreeRegressor if regression else DecisionTreeClassifier
+    return cls(max_depth=md, device="cpu").fit(X, y).tree_arrays_
+
+
+@pytest.mark.parametrize("strategy", ["feature", "data", "subtree", "auto"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_parallel_equals_serial_classifier(strategy, world):
+    md = None if world == 2 else 6
+    outs = run_ranks(_fit_rank, world, strategy, 1, md, False)
+    ref = _serial(1, md, False)
+    for r, o in enumerate(outs):
+        assert tuple(o["rank"]) == (r, world)
+        for k in FIELDS:
+            np.testing.assert_array_equal(o[k], getattr(ref, k), err_msg=f"{k} rank {r}")
+        np.testing.assert_array_equal(o["value"], ref.count)
+
+
+@pytest.mark.parametrize("strategy", ["feature", "data", "subtree"])
+def test_parallel_equals_serial_regressor(strategy):
+    outs = run_ranks(_fit_rank, 2, strategy, 2, 7, True)
+    ref = _serial(2, 7, True)
+    for o in outs:
+        for k in FIELDS:
+            np.testing.assert_array_equal(o[k], getattr(ref, k))
+        np.testing.assert_array_equal(o["value"], ref.value)
+
+
+def test_four_ranks_feature_parallel_deep():
+    outs = run_ranks(_fit_rank, 4, "feature", 3, None, False)
+    ref = _serial(3, None, False)
+    for o in outs:
+        for k in FIELDS:
+            np.testing.assert_array_equal(o[k], getattr(ref, k))
+
+
+def test_lpt_assignment_balances_rows():
+    from mpitree_amd.parallel.strategies import feature_blocks, lpt_assign
+
+    m = np.array([100, 90, 80, 10, 10, 10, 5])
+    owner = lpt_assign(m, 3)
+    loads = [m[owner == r].sum() for r in range(3)]
+    assert max(loads) - min(loads) <= 30
+    assert feature_blocks(64, 8) == [(8 * r, 8 * r + 8) for r in range(8)]
+    blocks = feature_blocks(7, 3)
+    assert blocks[0][0] == 0 and blocks[-1][1] == 7
+
+
+def _fit_rank_gpu(rank, world, strategy, seed, md):
+    import torch
+
+    from mpitree_amd import ParallelDecisionTreeClassifier
+
+    X, y = _data(seed, n=5000, F=9, C=3)
+    Xd = torch.from_numpy(X).cuda()
+    yd = torch.from_numpy(y).cuda()
+    est = ParallelDecisionTreeClassifier(max_depth=md, strategy=strategy, device="cuda").fit(Xd, yd)
+    ta = est.tree_arrays_
+    out = {k: getattr(ta, k) for k in FIELDS}
+    out["value"] = ta.count
+    out["engine"] = np.array([est.fit_stats_["engine"]])
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy", ["feature", "data", "subtree"])
+def test_gpu_ranks_equal_serial(strategy, monkeypatch):
+    # two ranks sharing one MI355X over gloo: exercises the HIP backend with
+    # every strategy's collectives (RCCL itself needs one GPU per rank)
+    monkeypatch.setenv("MPITREE_FINISHER_ROWS", "300")
+    from mpitree_amd import DecisionTreeClassifier
+
+    outs = run_ranks(_fit_rank_gpu, 2, strategy, 4, None)
+    X, y = _data(4, n=5000, F=9, C=3)
+    ref = DecisionTreeClassifier(device="cpu").fit(X, y).tree_arrays_
+    for o in outs:
+        assert str(o["engine"][0]).startswith("hip")
+        for k in FIELDS:
+            np.testing.assert_array_equal(o[k], getattr(ref, k))
