@@ -160,7 +160,7 @@ class NumpyBackend:
     def finisher_supported(self) -> bool:
         return True
 
-    def finish_subtrees(self, starts, counts, depths, params):
+    def finish_subtrees(self, starts, counts, depths, params, stats=None):
         """Reference (depth-first) growth of each deferred subtree.
 
         Same contract as the gfx950 finisher: concatenated node tables with

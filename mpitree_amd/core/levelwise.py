@@ -316,7 +316,7 @@ class LevelwiseBuilder:
         comm = self.comm
         owned = comm.finish_assignment(d["m"])
         local = self.be.finish_subtrees(d["start"][owned], d["count"][owned], d["depth"][owned],
-                                        self.p)
+                                        self.p, stats=tab.stats[d["id"][owned]])
         t = comm.merge_subtrees(local, owned, d["id"].size)
         # ``t`` concatenates one node table per deferred subtree (job j at
         # offsets[j]:offsets[j+1], root first, job-local child indices);

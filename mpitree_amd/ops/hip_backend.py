@@ -338,11 +338,11 @@ class HipBackend:
 
     # -------------------------------------------------------------- finisher
     def finisher_supported(self) -> bool:
-        if self.reg or self.cb != 1 or self.C > 64 or self.B > 256:
+        if self.reg or self.cb != 1 or self.C > 16 or self.B > 256:
             return False
         return self.F * (self.B * ((self.C + 1) // 2) + 1) * 4 <= 150 * 1024
 
-    def finish_subtrees(self, starts, counts, depths, params):
+    def finish_subtrees(self, starts, counts, depths, params, stats=None):
         """Grow every job's subtree on the device; concatenated node tables out.
 
         Returns a dict of arrays (feature, bin, left, right, depth, nsamp,
@@ -356,7 +356,10 @@ class HipBackend:
         order = np.argsort(-counts, kind="stable")  # largest first
         slots = 2 * counts[order] - 1
         base = np.cumsum(slots) - slots
-        jobs = np.stack([starts[order], counts[order], depths[order], base], 1)
+        st = np.asarray(stats, np.int64).reshape(J, self.C)
+        # {start, count, depth, base, row buffer, class counts[C]}
+        jobs = np.concatenate([np.stack([starts[order], counts[order], depths[order], base,
+                                         np.zeros(J, np.int64)], 1), st[order]], 1)
         total = int(slots.sum())
         C = self.C
         (d_jobs,) = self.up(jobs)
