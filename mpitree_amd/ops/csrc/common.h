@@ -52,6 +52,64 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
   return v;
 }
 
+// ---------------------------------------------------------------------------
+// DPP wave primitives (GFX9-family DPP: row_shr within 16-lane rows, then
+// row_bcast:15 / row_bcast:31 across rows). Each step is a VALU op with a
+// few cycles of latency instead of an LDS round trip through ds_bpermute.
+constexpr int kDppRowShr = 0x110;   // + n, n in 1..15
+constexpr int kDppRowBcast15 = 0x142;
+constexpr int kDppRowBcast31 = 0x143;
+
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t old, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+
+// Inclusive wave64 prefix sum in 6 DPP steps.
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+  v += dpp_u32<kDppRowShr + 1>(0u, v);
+  v += dpp_u32<kDppRowShr + 2>(0u, v);
+  v += dpp_u32<kDppRowShr + 4>(0u, v);
+  v += dpp_u32<kDppRowShr + 8>(0u, v);
+  v += dpp_u32<kDppRowBcast15, 0xa>(0u, v);
+  v += dpp_u32<kDppRowBcast31, 0xc>(0u, v);
+  return v;
+}
+
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_f64(double old, double v) {
+  const uint64_t o = (uint64_t)__double_as_longlong(old);
+  const uint64_t x = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = dpp_u32<CTRL, ROW_MASK>((uint32_t)o, (uint32_t)x);
+  const uint32_t hi = dpp_u32<CTRL, ROW_MASK>((uint32_t)(o >> 32), (uint32_t)(x >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// Wave-wide minimum of a double (every lane gets the result).
+__device__ __forceinline__ double wave_min_f64_dpp(double v) {
+  v = fmin(v, dpp_f64<kDppRowShr + 1>(v, v));
+  v = fmin(v, dpp_f64<kDppRowShr + 2>(v, v));
+  v = fmin(v, dpp_f64<kDppRowShr + 4>(v, v));
+  v = fmin(v, dpp_f64<kDppRowShr + 8>(v, v));
+  v = fmin(v, dpp_f64<kDppRowBcast15, 0xa>(v, v));
+  v = fmin(v, dpp_f64<kDppRowBcast31, 0xc>(v, v));
+  const uint64_t x = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// (cost, bin) argmin with ties to the lowest bin, for bins owned by lanes in
+// increasing order (lane l holds only bins below lane l+1's): the minimum
+// cost, then the lowest lane holding it. Result broadcast to every lane.
+__device__ __forceinline__ void wave_argmin_dpp(double& cost, int& bin) {
+  const double mn = wave_min_f64_dpp(cost);
+  const unsigned long long hit = __ballot(cost == mn);
+  const int src = hit ? __ffsll((long long)hit) - 1 : 0;
+  bin = __builtin_amdgcn_readlane(bin, src);
+  cost = mn;
+}
+
 // (cost, bin) lexicographic min across the wave; ties go to the lower bin.
 __device__ __forceinline__ void wave_argmin(double& cost, int& bin) {
 #pragma unroll

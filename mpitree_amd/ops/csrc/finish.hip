@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
             p[1] = p[0] + vv[1];
             p[2] = p[1] + vv[2];
             p[3] = p[2] + vv[3];
-            const uint32_t incl = wave_incl_scan_u32(p[3]);
+            const uint32_t incl = wave_incl_scan_dpp(p[3]);
             const uint32_t excl = incl - p[3];
             const uint32_t tc = (uint32_t)s_cnt[c];
 #pragma unroll
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
             }
           }
         }
-        wave_argmin(best_cost, best_bin);
+        wave_argmin_dpp(best_cost, best_bin);  // single 256-bin pass: lanes own ascending bins
         if (best_cost < __builtin_inf()) {
           const double g = pterm - best_cost;
           if (g > bg) {  // features visited in increasing order: strict > keeps the lowest

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
       p[0] = v[0];
 #pragma unroll
       for (int k = 1; k < kBinsPerLane; ++k) p[k] = p[k - 1] + v[k];
-      const uint32_t incl = wave_incl_scan_u32(p[kBinsPerLane - 1]);
+      const uint32_t incl = wave_incl_scan_dpp(p[kBinsPerLane - 1]);
       const uint32_t excl = incl - p[kBinsPerLane - 1] + carry[c];
       const uint32_t tc = tot[c];
 #pragma unroll
@@ -127,7 +127,10 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
       }
     }
   }
-  wave_argmin(best_cost, best_bin);
+  if (nb <= kChunk)
+    wave_argmin_dpp(best_cost, best_bin);  // one pass: lanes own ascending bins
+  else
+    wave_argmin(best_cost, best_bin);  // several passes: exact (cost, bin) order
   if (lane == 0) {
     out_cost[node * F_h + f] = best_cost;
     out_bin[node * F_h + f] = best_cost < __builtin_inf() ? best_bin : -1;

@@ -27,11 +27,11 @@ def _entry(rank, world, port, fn, args, outdir):
         dist.destroy_process_group()
 
 
-def run_ranks(fn, world, *args):
+def run_ranks(fn, world, *args, start_method="fork"):
     """Run ``fn(rank, world, *args) -> dict[str, array]`` on ``world`` ranks."""
     port = free_port()
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_entry, args=(world, port, fn, args, d), nprocs=world, join=True,
-                           start_method="fork")
+                           start_method=start_method)
         return [dict(np.load(os.path.join(d, f"r{r}.npz"), allow_pickle=False))
                 for r in range(world)]

@@ -108,7 +108,7 @@ def test_gpu_ranks_equal_serial(strategy, monkeypatch):
     monkeypatch.setenv("MPITREE_FINISHER_ROWS", "300")
     from mpitree_amd import DecisionTreeClassifier
 
-    outs = run_ranks(_fit_rank_gpu, 2, strategy, 4, None)
+    outs = run_ranks(_fit_rank_gpu, 2, strategy, 4, None, start_method="spawn")
     X, y = _data(4, n=5000, F=9, C=3)
     ref = DecisionTreeClassifier(device="cpu").fit(X, y).tree_arrays_
     for o in outs:
