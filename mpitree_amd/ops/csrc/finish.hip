@@ -48,7 +48,8 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
     int32_t* __restrict__ job_counter, const int32_t* __restrict__ nbins, int F, int B, int C,
     int crit, int max_depth, int64_t mss, int64_t msl, const double* __restrict__ xtab,
     int xtab_n, int32_t* __restrict__ node_i32, int32_t* __restrict__ node_cnt,
-    int32_t* __restrict__ job_nodes) {
+    int32_t* __restrict__ job_nodes, int tiny_rows, int64_t* __restrict__ tiny,
+    int32_t* __restrict__ tiny_count) {
   extern __shared__ __align__(16) uint32_t hist[];  // [F][B*W + 1] packed class pairs
   __shared__ double s_tab[kFinTab];
   __shared__ int s_job;
@@ -110,6 +111,20 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
     if (tid < C) {
       s_st_cnt[0][tid] = (int32_t)jb[5 + tid];
       nc[tid] = (int32_t)jb[5 + tid];
+    }
+    if (tid == 0 && jb[1] <= tiny_rows) {  // the whole job is tiny: one wave finishes it
+      const int t = atomicAdd(tiny_count, 1);
+      int64_t* tr = tiny + (int64_t)t * 8;
+      tr[0] = jb[0];
+      tr[1] = jb[1];
+      tr[2] = jb[2];
+      tr[3] = jb[4];
+      tr[4] = base;
+      tr[5] = base + 1;
+      tr[6] = base;
+      tr[7] = 0;
+      s_next = (int)(2 * jb[1] - 1);
+      s_sp = 0;
     }
     __syncthreads();
     while (s_sp > 0) {
@@ -332,6 +347,21 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
         for (int pass = 0; pass < 2; ++pass) {
           const bool is_left = (pass == 0) ? !left_small : left_small;
           if (is_left ? tlf : trf) continue;
+          const int cm_rows = is_left ? nl : nr;
+          if (cm_rows <= tiny_rows) {  // hand the tiny subtree to a wavefront
+            const int t = atomicAdd(tiny_count, 1);
+            int64_t* tr = tiny + (int64_t)t * 8;
+            tr[0] = is_left ? start : start + nl;
+            tr[1] = cm_rows;
+            tr[2] = cd;
+            tr[3] = s_buf ^ 1;
+            tr[4] = base + (is_left ? lid : rid);
+            tr[5] = base + s_next;
+            tr[6] = base;
+            tr[7] = 0;
+            s_next += 2 * cm_rows - 2;
+            continue;
+          }
           const int sp = s_sp++;
           s_st_start[sp] = is_left ? start : start + nl;
           s_st_count[sp] = is_left ? nl : nr;
@@ -349,6 +379,227 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Tiny subtrees (<= 64 rows): one wavefront per subtree, one row per lane.
+//
+// A node is a 64-bit mask of the wave's lanes, so partitioning is a mask AND
+// and never moves data. Per feature, each lane finds the set of lanes whose
+// code is <= its own with 8 ballots (an MSB-first radix rank over the code
+// bits); class counts of that left set are popcounts against per-class lane
+// masks; the split cost uses the same integer-form criterion (table lookups
+// for counts <= 64) and the wave picks (min cost, then min code) with DPP
+// reductions. No LDS histogram, no workgroup barriers: four independent
+// subtrees per 256-thread workgroup, dozens per CU.
+//
+// tiny: int64 [K][8] = {start, m, depth, buffer, root_slot, res_base_slot,
+//                       job_base_slot, 0}; descendants take slots from
+// [res_base, res_base + 2m - 2); unused reserved slots become unreachable
+// "dead" records that the host drops while re-numbering.
+constexpr int kTinyRows = 64;
+constexpr int kTinyWaves = 4;
+
+__device__ __forceinline__ uint32_t wave_min_u32_dpp(uint32_t v) {
+  v = min(v, dpp_u32<kDppRowShr + 1>(v, v));
+  v = min(v, dpp_u32<kDppRowShr + 2>(v, v));
+  v = min(v, dpp_u32<kDppRowShr + 4>(v, v));
+  v = min(v, dpp_u32<kDppRowShr + 8>(v, v));
+  v = min(v, dpp_u32<kDppRowBcast15, 0xa>(v, v));
+  v = min(v, dpp_u32<kDppRowBcast31, 0xc>(v, v));
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+constexpr int kTinyMaxF = 128;
+constexpr int kTinyStride = kTinyMaxF / 4 + 1;  // words per staged row (+1: bank spread)
+
+__global__ __launch_bounds__(256) void finish_tiny_kernel(
+    const uint32_t* __restrict__ codes_rm, int64_t row_words, const uint32_t* __restrict__ buf0,
+    const uint32_t* __restrict__ buf1, const int32_t* __restrict__ y, FinRowLab rl,
+    const int64_t* __restrict__ tiny, const int32_t* __restrict__ tiny_count,
+    int32_t* __restrict__ tiny_counter, int F, int C, int crit, int max_depth, int64_t mss,
+    int64_t msl, const double* __restrict__ xtab, int32_t* __restrict__ node_i32,
+    int32_t* __restrict__ node_cnt) {
+  __shared__ double s_tab[kTinyRows + 1];
+  __shared__ uint32_t s_codes[kTinyWaves][kTinyRows * kTinyStride];
+  __shared__ unsigned long long s_mask[kTinyWaves][16];
+  __shared__ int32_t s_dep[kTinyWaves][16], s_slot[kTinyWaves][16];
+  const int lane = lane_id();
+  const int wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i <= kTinyRows; i += blockDim.x) s_tab[i] = xtab[i];
+  __syncthreads();
+  const int K = *tiny_count;
+  const int nw = (int)min<int64_t>(row_words, kTinyMaxF / 4);
+  uint32_t* my_codes = &s_codes[wave][lane * kTinyStride];
+  const uint8_t* my_bytes = reinterpret_cast<const uint8_t*>(my_codes);
+  for (;;) {
+    int k = 0;
+    if (lane == 0) k = atomicAdd(tiny_counter, 1);
+    k = __builtin_amdgcn_readfirstlane(k);
+    if (k >= K) break;
+    const int64_t* rec = tiny + (int64_t)k * 8;
+    const int64_t start = rec[0];
+    const int m = (int)rec[1];
+    const int depth0 = (int)rec[2];
+    const uint32_t* src = rec[3] ? buf1 : buf0;
+    const int64_t root_slot = rec[4];
+    int64_t next = rec[5];
+    const int64_t res_end = rec[5] + 2 * (int64_t)m - 2;
+    const int64_t jbase = rec[6];
+    const bool act = lane < m;
+    int lab = 0;
+    if (act) {
+      const uint32_t ent = src[start + lane];
+      const uint32_t row = rl.shift ? (ent & rl.mask) : ent;
+      lab = rl.shift ? (int)(ent >> rl.shift) : y[row];
+      for (int i = 0; i < nw; ++i) my_codes[i] = codes_rm[(int64_t)row * row_words + i];
+    }
+    unsigned long long cm[kFinMaxC];
+#pragma unroll
+    for (int c = 0; c < kFinMaxC; ++c) cm[c] = c < C ? __ballot(act && lab == c) : 0ull;
+    if (lane == 0) {
+      s_mask[wave][0] = m == 64 ? ~0ull : ((1ull << m) - 1ull);
+      s_dep[wave][0] = depth0;
+      s_slot[wave][0] = (int32_t)root_slot;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    int sp = 1;
+    while (sp > 0) {
+      --sp;
+      const unsigned long long M = s_mask[wave][sp];
+      const int d = s_dep[wave][sp];
+      const int64_t slot = s_slot[wave][sp];
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const int mm = __popcll(M);
+      int mc[kFinMaxC];
+      double acc = 0.0;
+      int64_t sq = 0;
+#pragma unroll
+      for (int c = 0; c < kFinMaxC; ++c) {
+        mc[c] = c < C ? __popcll(M & cm[c]) : 0;
+        if (c < C) {
+          acc = acc + s_tab[mc[c]];
+          sq += (int64_t)mc[c] * mc[c];
+        }
+      }
+      const double pterm = crit == kEntropy ? s_tab[mm] - acc : gini_term(mm, sq);
+      const bool inm = (M >> lane) & 1ull;
+      double bg = -__builtin_inf();
+      int bf = -1;
+      uint32_t bb = 0;
+      for (int f = 0; f < F; ++f) {
+        const uint32_t code = my_bytes[f];
+        // lanes of M whose code is greater than / equal to mine (radix rank, MSB first)
+        unsigned long long eq = M, gt = 0ull;
+#pragma unroll
+        for (int b = 7; b >= 0; --b) {
+          const unsigned long long bm = __ballot((code >> b) & 1u) & M;
+          if ((code >> b) & 1u) {
+            eq &= bm;
+          } else {
+            gt |= eq & bm;
+            eq &= ~bm;
+          }
+        }
+        const unsigned long long le = M & ~gt;
+        const int ml = __popcll(le);
+        const int mr = mm - ml;
+        double cost = __builtin_inf();
+        if (inm && ml >= msl && mr >= msl) {
+          if (crit == kEntropy) {
+            double sl = 0.0, sr = 0.0;
+#pragma unroll
+            for (int c = 0; c < kFinMaxC; ++c) {
+              if (c < C) {
+                const int lc = __popcll(le & cm[c]);
+                sl = sl + s_tab[lc];
+                sr = sr + s_tab[mc[c] - lc];
+              }
+            }
+            cost = (s_tab[ml] - sl) + (s_tab[mr] - sr);
+          } else {
+            int64_t ql = 0, qr = 0;
+#pragma unroll
+            for (int c = 0; c < kFinMaxC; ++c) {
+              if (c < C) {
+                const int64_t lc = __popcll(le & cm[c]);
+                const int64_t rc = mc[c] - lc;
+                ql += lc * lc;
+                qr += rc * rc;
+              }
+            }
+            cost = gini_term(ml, ql) + gini_term(mr, qr);
+          }
+        }
+        const double cmin = wave_min_f64_dpp(cost);
+        if (cmin < __builtin_inf()) {
+          const uint32_t bcode = wave_min_u32_dpp(cost == cmin ? code : 0xffffffffu);
+          const double g = pterm - cmin;
+          if (g > bg) {  // features in increasing order: strict > keeps the lowest
+            bg = g;
+            bf = f;
+            bb = bcode;
+          }
+        }
+      }
+      if (bf < 0) continue;  // leaf: the record written at creation stands
+      const unsigned long long LM = M & __ballot((uint32_t)my_bytes[bf] <= bb);
+      const unsigned long long RM = M & ~LM;
+      const int64_t ls = next, rs = next + 1;
+      next += 2;
+      const int nl = __popcll(LM), nr = __popcll(RM);
+      int nzl = 0, nzr = 0;
+#pragma unroll
+      for (int c = 0; c < kFinMaxC; ++c) {
+        if (c < C) {
+          const int lc = __popcll(LM & cm[c]);
+          const int rc = mc[c] - lc;
+          nzl += lc > 0;
+          nzr += rc > 0;
+          if (lane == c) {
+            node_cnt[ls * C + c] = lc;
+            node_cnt[rs * C + c] = rc;
+          }
+        }
+      }
+      const int cd = d + 1;
+      if (lane == 0) {
+        int32_t* P = node_i32 + slot * 6;
+        P[0] = bf;
+        P[1] = (int32_t)bb;
+        P[2] = (int32_t)(ls - jbase);
+        P[3] = (int32_t)(rs - jbase);
+        int32_t* L = node_i32 + ls * 6;
+        int32_t* R = node_i32 + rs * 6;
+        L[0] = -1; L[1] = -1; L[2] = -1; L[3] = -1; L[4] = cd; L[5] = nl;
+        R[0] = -1; R[1] = -1; R[2] = -1; R[3] = -1; R[4] = cd; R[5] = nr;
+      }
+      const bool depth_stop = max_depth >= 0 && cd >= max_depth;
+      const bool tlf = depth_stop || nl < mss || nl < 2 * msl || nzl <= 1;
+      const bool trf = depth_stop || nr < mss || nr < 2 * msl || nzr <= 1;
+      const bool left_small = nl <= nr;
+      for (int pass = 0; pass < 2; ++pass) {
+        const bool is_left = (pass == 0) ? !left_small : left_small;
+        if (is_left ? tlf : trf) continue;
+        if (lane == 0) {
+          s_mask[wave][sp] = is_left ? LM : RM;
+          s_dep[wave][sp] = cd;
+          s_slot[wave][sp] = (int32_t)(is_left ? ls : rs);
+        }
+        ++sp;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    // unreachable filler for the unused part of the reservation
+    for (int64_t s = next + lane; s < res_end; s += kWave) {
+      int32_t* Q = node_i32 + s * 6;
+      Q[0] = -1; Q[1] = -1; Q[2] = -1; Q[3] = -1; Q[4] = 0; Q[5] = 0;
+      for (int c = 0; c < C; ++c) node_cnt[s * C + c] = 0;
+    }
+  }
+}
+
 int finish_lds_bytes(int F, int B, int C) { return F * (B * ((C + 1) / 2) + 1) * 4; }
 int finish_max_classes() { return kFinMaxC; }
 
@@ -357,9 +608,13 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                    uint32_t* buf1, const int32_t* y, int lab_shift, const int64_t* jobs, int J,
                    int32_t* counter, const int32_t* nbins, int F, int B, int C, int crit,
                    int max_depth, int64_t mss, int64_t msl, const double* xtab, int xtab_n,
-                   int32_t* node_i32, int32_t* node_cnt, int32_t* job_nodes, int grid) {
+                   int32_t* node_i32, int32_t* node_cnt, int32_t* job_nodes, int grid,
+                   int tiny_rows, int64_t* tiny, int tiny_grid) {
+  // counter: int32 [3] = {job cursor, tiny count, tiny cursor}, zeroed by the host
   if (J <= 0) return;
   if (C > kFinMaxC) throw std::runtime_error("finisher supports at most 16 classes");
+  if (code_bytes != 1 || F > kTinyMaxF || tiny == nullptr) tiny_rows = 0;
+  tiny_rows = std::min(tiny_rows, kTinyRows);
   FinRowLab rl{lab_shift ? ((1u << lab_shift) - 1u) : 0xffffffffu, lab_shift};
   const size_t lds = (size_t)finish_lds_bytes(F, B, C);
 #define MT_FIN(CT)                                                                            \
@@ -368,7 +623,8 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   hipLaunchKernelGGL(finish_cls_kernel<CT>, dim3(grid), dim3(kFinThreads), lds, stream,       \
                      (const uint32_t*)codes_rm, row_words, (const CT*)codes_fm, n_rows, buf0, \
                      buf1, y, rl, jobs, J, counter, nbins, F, B, C, crit, max_depth, mss,     \
-                     msl, xtab, xtab_n, node_i32, node_cnt, job_nodes);
+                     msl, xtab, xtab_n, node_i32, node_cnt, job_nodes, tiny_rows, tiny,       \
+                     counter + 1);
   if (code_bytes == 1) {
     MT_FIN(uint8_t)
   } else {
@@ -376,6 +632,13 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   }
 #undef MT_FIN
   MT_HIP_CHECK(hipGetLastError());
+  if (tiny_rows > 0) {
+    hipLaunchKernelGGL(finish_tiny_kernel, dim3(tiny_grid), dim3(kTinyWaves * kWave), 0, stream,
+                       (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,
+                       counter + 1, counter + 2, F, C, crit, max_depth, mss, msl, xtab,
+                       node_i32, node_cnt);
+    MT_HIP_CHECK(hipGetLastError());
+  }
 }
 
 }  // namespace mt

@@ -366,7 +366,11 @@ class HipBackend:
         node_i32 = torch.empty((total, 6), dtype=torch.int32, device=self.device)
         node_cnt = torch.empty((total, C), dtype=torch.int32, device=self.device)
         job_nodes = torch.empty(J, dtype=torch.int32, device=self.device)
-        counter = torch.zeros(1, dtype=torch.int32, device=self.device)
+        counter = torch.zeros(3, dtype=torch.int32, device=self.device)
+        tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
+        # every tiny subtree has >= 2 rows and they partition the job rows
+        tiny_cap = int(counts.sum() // 2 + J + 1)
+        tiny = torch.empty((tiny_cap, 8), dtype=torch.int64, device=self.device)
         md = -1 if params.max_depth is None else int(params.max_depth)
         grid = int(min(J, 2 * N_CU))
         self.hip.finish(_stream(), self.codes_rm.data_ptr(), self.row_elems * self.cb // 4,
@@ -375,7 +379,8 @@ class HipBackend:
                         J, counter.data_ptr(), self.nbins.data_ptr(), self.F, self.B, C,
                         int(self.crit), md, int(params.min_samples_split),
                         int(max(1, params.min_samples_leaf)), self.xtab.data_ptr(), XTAB_N,
-                        node_i32.data_ptr(), node_cnt.data_ptr(), job_nodes.data_ptr(), grid)
+                        node_i32.data_ptr(), node_cnt.data_ptr(), job_nodes.data_ptr(), grid,
+                        tiny_rows, tiny.data_ptr(), 4 * N_CU)
         jn = job_nodes.cpu().numpy().astype(np.int64)
         # compact the used slots on the device, one D2H copy
         base_t = torch.from_numpy(base).to(self.device)

@@ -121,3 +121,19 @@ def test_gpu_finisher_deep_chain(monkeypatch):
     ref = oracle(X, y, Criterion.ENTROPY, None, max_bins=1024)
     clf = DecisionTreeClassifier(max_bins=1024, device="cuda").fit(X, y)
     assert clf.tree_arrays_.equal(ref)
+
+
+@pytest.mark.parametrize("tiny", ["0", "8", "64"])
+def test_gpu_tiny_subtree_wave_path(monkeypatch, tiny):
+    # wave-per-subtree path for <= 64-row subtrees vs the oracle, many classes
+    monkeypatch.setenv("MPITREE_TINY_ROWS", tiny)
+    monkeypatch.setenv("MPITREE_FINISHER_ROWS", "400")
+    rng = np.random.default_rng(77)
+    n, F, C = 8000, 10, 5
+    X, y = random_problem(rng, n, F, C, levels=30)
+    for crit in ("entropy", "gini"):
+        ref = oracle(X, y, Criterion.ENTROPY if crit == "entropy" else Criterion.GINI, None,
+                     msl=2 if crit == "gini" else 1)
+        clf = DecisionTreeClassifier(criterion=crit, device="cuda",
+                                     min_samples_leaf=2 if crit == "gini" else 1).fit(X, y)
+        assert clf.tree_arrays_.equal(ref), (tiny, crit)
