@@ -381,16 +381,31 @@ class HipBackend:
                         int(max(1, params.min_samples_leaf)), self.xtab.data_ptr(), XTAB_N,
                         node_i32.data_ptr(), node_cnt.data_ptr(), job_nodes.data_ptr(), grid,
                         tiny_rows, tiny.data_ptr(), 4 * N_CU)
-        jn = job_nodes.cpu().numpy().astype(np.int64)
-        # compact the used slots on the device, one D2H copy
-        base_t = torch.from_numpy(base).to(self.device)
-        jn_t = torch.from_numpy(jn).to(self.device)
-        rep_base = torch.repeat_interleave(base_t, jn_t)
-        within = torch.arange(int(jn.sum()), device=self.device) - torch.repeat_interleave(
-            torch.cumsum(jn_t, 0) - jn_t, jn_t)
-        sel = rep_base + within
-        ni = node_i32.index_select(0, sel).cpu().numpy()
-        nc = node_cnt.index_select(0, sel).cpu().numpy()
+        # Compact on the device: keep the written, live slots of every job
+        # (unused tails and the unreachable fillers of tiny-subtree
+        # reservations are dropped), re-map job-local child ids to the
+        # compacted positions, and copy only live nodes to the host.
+        dev = self.device
+        slots_t = torch.from_numpy(slots).to(dev)
+        base_t = torch.from_numpy(base).to(dev)
+        job_of = torch.repeat_interleave(torch.arange(J, device=dev), slots_t)
+        within = torch.arange(total, device=dev) - base_t[job_of]
+        alive = (within < job_nodes.long()[job_of]) & (node_i32[:, 5] > 0)
+        cum = torch.cumsum(alive.long(), 0)
+        new_pos = cum - 1
+        cstart = (cum - alive.long())[base_t]  # compacted start of every job
+        sel = torch.nonzero(alive).squeeze(1)
+        ni_t = node_i32.index_select(0, sel).long()
+        nc_t = node_cnt.index_select(0, sel)
+        jsel = job_of[sel]
+        inner = ni_t[:, 0] >= 0
+        for col in (2, 3):
+            old_slot = base_t[jsel] + ni_t[:, col].clamp(min=0)
+            ni_t[:, col] = torch.where(inner, new_pos[old_slot] - cstart[jsel], ni_t[:, col])
+        jn_t = torch.bincount(jsel, minlength=J)
+        ni = ni_t.cpu().numpy()
+        nc = nc_t.cpu().numpy()
+        jn = jn_t.cpu().numpy().astype(np.int64)
         # back to the caller's job order
         inv = np.empty(J, np.int64)
         inv[order] = np.arange(J)
