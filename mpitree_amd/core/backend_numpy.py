@@ -163,8 +163,8 @@ class NumpyBackend:
     def finish_subtrees(self, starts, counts, depths, params, stats=None):
         """Reference (depth-first) growth of each deferred subtree.
 
-        Same contract as the gfx950 finisher: concatenated node tables with
-        job-local child indices, job j at ``offsets[j]:offsets[j+1]``.
+        Same contract as the gfx950 finisher: one node table for all jobs,
+        child links indexing it, ``roots[j]`` the row of job j's root.
         """
         from .reference import fit_reference
 
@@ -183,12 +183,17 @@ class NumpyBackend:
                               left=ta.left.astype(np.int64), right=ta.right.astype(np.int64),
                               depth=ta.depth + int(d), nsamp=ta.n_samples, stats=stats))
         lens = np.array([len(p["feature"]) for p in parts], dtype=np.int64)
+        offsets = np.concatenate([[0], np.cumsum(lens)])
+        for p, o in zip(parts, offsets[:-1]):
+            inner = p["feature"] >= 0
+            p["left"] = np.where(inner, p["left"] + o, -1)
+            p["right"] = np.where(inner, p["right"] + o, -1)
         out = {k: (np.concatenate([p[k] for p in parts]) if parts else np.zeros(0, np.int64))
                for k in ("feature", "bin", "left", "right", "depth", "nsamp")}
         C = 2 if self.reg else self.C
         out["stats"] = (np.concatenate([p["stats"] for p in parts]) if parts
                         else np.zeros((0, C), np.int64))
-        out["offsets"] = np.concatenate([[0], np.cumsum(lens)])
+        out["roots"] = offsets[:-1].copy()
         return out
 
     def sync(self):

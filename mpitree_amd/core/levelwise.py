@@ -318,33 +318,53 @@ class LevelwiseBuilder:
         local = self.be.finish_subtrees(d["start"][owned], d["count"][owned], d["depth"][owned],
                                         self.p, stats=tab.stats[d["id"][owned]])
         t = comm.merge_subtrees(local, owned, d["id"].size)
-        # ``t`` concatenates one node table per deferred subtree (job j at
-        # offsets[j]:offsets[j+1], root first, job-local child indices);
-        # splice them into the global table in one vectorised pass.
-        off = t["offsets"]
-        lens = np.diff(off)
-        T = int(off[-1])
+        # ``t`` is one node table for all deferred subtrees (child links index
+        # it, ``roots[j]`` is job j's root): append every row, link children,
+        # then copy each root's split onto the deferred node it continues (the
+        # appended copy of the root stays unreachable and is dropped when the
+        # tree is re-numbered).
+        T = len(t["feature"])
         if T == 0:
             return
-        job_of = np.repeat(np.arange(lens.size), lens)
-        is_root = np.zeros(T, bool)
-        is_root[off[:-1][lens > 0]] = True
-        gids = np.empty(T, np.int64)
-        gids[is_root] = d["id"][lens > 0]
-        nr = np.nonzero(~is_root)[0]
-        gids[nr] = tab.add(t["depth"][nr], t["nsamp"][nr], t["stats"][nr])
+        gids = tab.add(t["depth"], t["nsamp"], t["stats"])
         inner = np.nonzero(t["feature"] >= 0)[0]
         g = gids[inner]
-        jb = off[job_of[inner]]
         tab.feature[g] = t["feature"][inner]
         tab.tbin[g] = t["bin"][inner]
-        tab.left[g] = gids[jb + t["left"][inner]]
-        tab.right[g] = gids[jb + t["right"][inner]]
+        tab.left[g] = gids[t["left"][inner]]
+        tab.right[g] = gids[t["right"][inner]]
+        r = np.asarray(t["roots"], np.int64)
+        did = d["id"]
+        split = t["feature"][r] >= 0
+        tab.feature[did[split]] = t["feature"][r[split]]
+        tab.tbin[did[split]] = t["bin"][r[split]]
+        tab.left[did[split]] = gids[t["left"][r[split]]]
+        tab.right[did[split]] = gids[t["right"][r[split]]]
 
     # -------------------------------------------------------------- output
     def _to_arrays(self, tab: _Table) -> TreeArrays:
         reg = self.p.criterion == Criterion.SQUARED_ERROR
         n = tab.n
+        try:
+            from ..ops import native
+
+            cpu = native.cpu()
+        except ImportError:
+            cpu = None
+        if cpu is not None:  # one native pass: pre-order walk + column gather
+            a = cpu.assemble(tab.feature[:n], tab.tbin[:n], tab.left[:n], tab.right[:n],
+                             tab.nsamp[:n], tab.stats[:n], 0)
+            st = a["stats"]
+            ta = TreeArrays(
+                feature=a["feature"], threshold=np.full(len(st), np.nan),
+                threshold_bin=a["bin"], left=a["left"], right=a["right"], depth=a["depth"],
+                n_samples=a["nsamp"], impurity=_node_terms(self.p.criterion, st),
+                count=None if reg else st,
+                value=st[:, 1].astype(np.float64) if reg else None,
+            )
+            if reg:
+                ta.meta["sum_fixed"] = st[:, 1].copy()
+            return ta
         st = tab.stats[:n]
         term = _node_terms(self.p.criterion, st)
         ta = TreeArrays.from_unordered(

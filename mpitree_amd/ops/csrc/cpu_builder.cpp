@@ -401,6 +401,76 @@ py::tuple preorder(py::array_t<int32_t, py::array::c_style | py::array::forcecas
   return py::make_tuple(o, d);
 }
 
+// Re-number an arbitrary node table into pre-order and gather every column in
+// one pass (the tree-assembly step after a level-wise + finisher fit).
+py::dict assemble(py::array_t<int32_t, py::array::c_style | py::array::forcecast> feature,
+                  py::array_t<int32_t, py::array::c_style | py::array::forcecast> tbin,
+                  py::array_t<int64_t, py::array::c_style | py::array::forcecast> left,
+                  py::array_t<int64_t, py::array::c_style | py::array::forcecast> right,
+                  py::array_t<int64_t, py::array::c_style | py::array::forcecast> nsamp,
+                  py::array_t<int64_t, py::array::c_style | py::array::forcecast> stats,
+                  int64_t root) {
+  const int64_t n = feature.shape(0);
+  const int64_t C = stats.ndim() == 2 ? stats.shape(1) : 1;
+  const int32_t* f = feature.data();
+  const int64_t* l = left.data();
+  const int64_t* r = right.data();
+  std::vector<int64_t> order;
+  order.reserve(n);
+  std::vector<int64_t> new_id(n, -1);
+  std::vector<int32_t> dep;
+  dep.reserve(n);
+  std::vector<std::pair<int64_t, int32_t>> stack{{root, 0}};
+  while (!stack.empty()) {
+    auto [i, d] = stack.back();
+    stack.pop_back();
+    new_id[i] = (int64_t)order.size();
+    order.push_back(i);
+    dep.push_back(d);
+    if (f[i] >= 0) {
+      stack.push_back({r[i], d + 1});
+      stack.push_back({l[i], d + 1});
+    }
+  }
+  const int64_t k = (int64_t)order.size();
+  py::array_t<int32_t> of(k), ob(k), od(k), ol(k), orr(k);
+  py::array_t<int64_t> on(k), oo(k);
+  py::array_t<int64_t> os({k, C});
+  int32_t *pf = of.mutable_data(), *pb = ob.mutable_data(), *pd = od.mutable_data();
+  int32_t *pl = ol.mutable_data(), *pr = orr.mutable_data();
+  int64_t *pn = on.mutable_data(), *po = oo.mutable_data(), *ps = os.mutable_data();
+  const int32_t* b = tbin.data();
+  const int64_t* ns = nsamp.data();
+  const int64_t* st = stats.data();
+  for (int64_t j = 0; j < k; ++j) {
+    const int64_t i = order[j];
+    po[j] = i;
+    pf[j] = f[i];
+    pd[j] = dep[j];
+    pn[j] = ns[i];
+    for (int64_t c = 0; c < C; ++c) ps[j * C + c] = st[i * C + c];
+    if (f[i] >= 0) {
+      pb[j] = b[i];
+      pl[j] = (int32_t)new_id[l[i]];
+      pr[j] = (int32_t)new_id[r[i]];
+    } else {
+      pb[j] = -1;
+      pl[j] = -1;
+      pr[j] = -1;
+    }
+  }
+  py::dict out;
+  out["order"] = oo;
+  out["feature"] = of;
+  out["bin"] = ob;
+  out["left"] = ol;
+  out["right"] = orr;
+  out["depth"] = od;
+  out["nsamp"] = on;
+  out["stats"] = os;
+  return out;
+}
+
 // Node terms for every node: stats [N, C] class counts, or [N, 2] (count, sum).
 py::array_t<double> node_terms(py::array_t<int64_t, py::array::c_style | py::array::forcecast> st,
                                int crit) {
@@ -408,6 +478,12 @@ py::array_t<double> node_terms(py::array_t<int64_t, py::array::c_style | py::arr
   const int64_t* s = st.data();
   py::array_t<double> out(N);
   double* o = out.mutable_data();
+  static std::vector<double> tab;  // x*log2(x) for small counts (same function, same bits)
+  if (tab.empty()) {
+    tab.resize(1 << 16);
+    for (size_t x = 0; x < tab.size(); ++x) tab[x] = mt::xlog2x(x);
+  }
+  auto T = [&](int64_t x) { return x < (int64_t)tab.size() ? tab[x] : mt::xlog2x((uint64_t)x); };
   for (int64_t i = 0; i < N; ++i) {
     const int64_t* c = s + i * C;
     if (crit == mt::kSquaredError) {
@@ -416,10 +492,10 @@ py::array_t<double> node_terms(py::array_t<int64_t, py::array::c_style | py::arr
       double acc = 0.0;
       int64_t m = 0;
       for (int64_t k = 0; k < C; ++k) {
-        acc = acc + mt::xlog2x((uint64_t)c[k]);
+        acc = acc + T(c[k]);
         m += c[k];
       }
-      o[i] = mt::xlog2x((uint64_t)m) - acc;
+      o[i] = T(m) - acc;
     } else {
       int64_t m = 0, sq = 0;
       for (int64_t k = 0; k < C; ++k) {
@@ -444,6 +520,7 @@ PYBIND11_MODULE(_cpu, m) {
   m.doc() = "mpitree_amd native host builder and tree helpers";
   m.def("build_tree", &build_tree);
   m.def("preorder", &preorder);
+  m.def("assemble", &assemble);
   m.def("node_terms", &node_terms);
   m.def("xlog2x", &xlog2x_np);
 }

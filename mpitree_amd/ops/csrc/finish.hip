@@ -18,10 +18,10 @@
 //   checks, push the larger child first so the DFS stack stays O(log rows).
 //
 // Class counts travel on the DFS stack (known from the parent's split), so a
-// node needs five workgroup barriers. Node ids are local to the job and
-// allocated in processing order, which depends only on the data, so results
-// are deterministic; the host re-numbers the tree into pre-order. Every job
-// owns a disjoint output region of 2*rows-1 node slots.
+// node needs five workgroup barriers. Node slots are handed out by one global
+// atomic counter, so the output is compact; the allocation order varies from
+// run to run but every link is explicit and the host re-numbers the final
+// tree into pre-order, so the fitted tree is bitwise deterministic.
 #include "common.h"
 #include "criterion.h"
 
@@ -48,8 +48,8 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
     int32_t* __restrict__ job_counter, const int32_t* __restrict__ nbins, int F, int B, int C,
     int crit, int max_depth, int64_t mss, int64_t msl, const double* __restrict__ xtab,
     int xtab_n, int32_t* __restrict__ node_i32, int32_t* __restrict__ node_cnt,
-    int32_t* __restrict__ job_nodes, int tiny_rows, int64_t* __restrict__ tiny,
-    int32_t* __restrict__ tiny_count) {
+    int32_t* __restrict__ job_root, int32_t* __restrict__ node_counter, int tiny_rows,
+    int64_t* __restrict__ tiny, int32_t* __restrict__ tiny_count) {
   extern __shared__ __align__(16) uint32_t hist[];  // [F][B*W + 1] packed class pairs
   __shared__ double s_tab[kFinTab];
   __shared__ int s_job;
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
   __shared__ int32_t s_st_count[kFinStack], s_st_depth[kFinStack], s_st_id[kFinStack];
   __shared__ int32_t s_st_buf[kFinStack];
   __shared__ int32_t s_st_cnt[kFinStack][kFinMaxC];
-  __shared__ int s_sp, s_next;
+  __shared__ int s_sp, s_root;
   __shared__ int64_t s_start;
   __shared__ int32_t s_count, s_depth, s_id, s_buf;
   __shared__ int32_t s_cnt[kFinMaxC], s_left[kFinMaxC];
@@ -90,43 +90,39 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
     const int job = s_job;
     if (job >= J) break;
     const int64_t* jb = jobs + (int64_t)job * JW;
-    const int64_t base = jb[3];
-    int32_t* ni = node_i32 + base * 6;
-    int32_t* nc = node_cnt + base * C;
+    int32_t* ni = node_i32;  // node slots come from one global counter
+    int32_t* nc = node_cnt;
     if (tid == 0) {
+      const int r = atomicAdd(node_counter, 1);
+      s_root = r;
+      job_root[job] = r;
       s_sp = 1;
       s_st_start[0] = jb[0];
       s_st_count[0] = (int32_t)jb[1];
       s_st_depth[0] = (int32_t)jb[2];
-      s_st_id[0] = 0;
+      s_st_id[0] = r;
       s_st_buf[0] = (int32_t)jb[4];
-      s_next = 1;
-      ni[0] = -1;
-      ni[1] = -1;
-      ni[2] = -1;
-      ni[3] = -1;
-      ni[4] = (int32_t)jb[2];
-      ni[5] = (int32_t)jb[1];
+      int32_t* R = ni + (int64_t)r * 6;
+      R[0] = -1;
+      R[1] = -1;
+      R[2] = -1;
+      R[3] = -1;
+      R[4] = (int32_t)jb[2];
+      R[5] = (int32_t)jb[1];
+      if (jb[1] <= tiny_rows) {  // the whole job is tiny: one wave finishes it
+        const int t = atomicAdd(tiny_count, 1);
+        int64_t* tr = tiny + (int64_t)t * 8;
+        tr[0] = jb[0];
+        tr[1] = jb[1];
+        tr[2] = jb[2];
+        tr[3] = jb[4];
+        tr[4] = r;
+        s_sp = 0;
+      }
     }
-    if (tid < C) {
-      s_st_cnt[0][tid] = (int32_t)jb[5 + tid];
-      nc[tid] = (int32_t)jb[5 + tid];
-    }
-    if (tid == 0 && jb[1] <= tiny_rows) {  // the whole job is tiny: one wave finishes it
-      const int t = atomicAdd(tiny_count, 1);
-      int64_t* tr = tiny + (int64_t)t * 8;
-      tr[0] = jb[0];
-      tr[1] = jb[1];
-      tr[2] = jb[2];
-      tr[3] = jb[4];
-      tr[4] = base;
-      tr[5] = base + 1;
-      tr[6] = base;
-      tr[7] = 0;
-      s_next = (int)(2 * jb[1] - 1);
-      s_sp = 0;
-    }
+    if (tid < C) s_st_cnt[0][tid] = (int32_t)jb[5 + tid];
     __syncthreads();
+    if (tid < C) nc[(int64_t)s_root * C + tid] = (int32_t)jb[5 + tid];
     while (s_sp > 0) {
       __syncthreads();  // everyone has read s_sp before thread 0 pops
       // ---- pop + node term (thread 0); the histogram is already zero
@@ -320,17 +316,16 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
       if (tid == 0 && bf >= 0) {
         const int nl = s_lc;
         const int nr = m - nl;
-        const int lid = s_next, rid = s_next + 1;
-        s_next += 2;
-        ni[id * 6 + 0] = bf;
-        ni[id * 6 + 1] = bb;
-        ni[id * 6 + 2] = lid;
-        ni[id * 6 + 3] = rid;
+        const int lid = atomicAdd(node_counter, 2), rid = lid + 1;
+        ni[(int64_t)id * 6 + 0] = bf;
+        ni[(int64_t)id * 6 + 1] = bb;
+        ni[(int64_t)id * 6 + 2] = lid;
+        ni[(int64_t)id * 6 + 3] = rid;
         int nzl = 0, nzr = 0;
         for (int c = 0; c < C; ++c) {
           const int32_t lc = s_left[c], rc = s_cnt[c] - s_left[c];
-          nc[lid * C + c] = lc;
-          nc[rid * C + c] = rc;
+          nc[(int64_t)lid * C + c] = lc;
+          nc[(int64_t)rid * C + c] = rc;
           nzl += lc > 0;
           nzr += rc > 0;
         }
@@ -338,8 +333,8 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
         const bool depth_stop = max_depth >= 0 && cd >= max_depth;
         const bool tlf = depth_stop || nl < mss || nl < 2 * msl || nzl <= 1;
         const bool trf = depth_stop || nr < mss || nr < 2 * msl || nzr <= 1;
-        int32_t* L = ni + lid * 6;
-        int32_t* Rr = ni + rid * 6;
+        int32_t* L = ni + (int64_t)lid * 6;
+        int32_t* Rr = ni + (int64_t)rid * 6;
         L[0] = -1; L[1] = -1; L[2] = -1; L[3] = -1; L[4] = cd; L[5] = nl;
         Rr[0] = -1; Rr[1] = -1; Rr[2] = -1; Rr[3] = -1; Rr[4] = cd; Rr[5] = nr;
         // push the larger child first so the smaller one is processed next
@@ -355,11 +350,7 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
             tr[1] = cm_rows;
             tr[2] = cd;
             tr[3] = s_buf ^ 1;
-            tr[4] = base + (is_left ? lid : rid);
-            tr[5] = base + s_next;
-            tr[6] = base;
-            tr[7] = 0;
-            s_next += 2 * cm_rows - 2;
+            tr[4] = is_left ? lid : rid;
             continue;
           }
           const int sp = s_sp++;
@@ -374,8 +365,6 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
       }
       __syncthreads();
     }
-    if (tid == 0) job_nodes[job] = s_next;
-    __syncthreads();
   }
 }
 
@@ -391,10 +380,8 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
 // reductions. No LDS histogram, no workgroup barriers: four independent
 // subtrees per 256-thread workgroup, dozens per CU.
 //
-// tiny: int64 [K][8] = {start, m, depth, buffer, root_slot, res_base_slot,
-//                       job_base_slot, 0}; descendants take slots from
-// [res_base, res_base + 2m - 2); unused reserved slots become unreachable
-// "dead" records that the host drops while re-numbering.
+// tiny: int64 [K][8] = {start, m, depth, buffer, root_slot, -, -, -}; child
+// slots come from the global node counter, two per split.
 constexpr int kTinyRows = 64;
 constexpr int kTinyWaves = 4;
 
@@ -417,7 +404,7 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
     const int64_t* __restrict__ tiny, const int32_t* __restrict__ tiny_count,
     int32_t* __restrict__ tiny_counter, int F, int C, int crit, int max_depth, int64_t mss,
     int64_t msl, const double* __restrict__ xtab, int32_t* __restrict__ node_i32,
-    int32_t* __restrict__ node_cnt) {
+    int32_t* __restrict__ node_cnt, int32_t* __restrict__ node_counter) {
   __shared__ double s_tab[kTinyRows + 1];
   __shared__ uint32_t s_codes[kTinyWaves][kTinyRows * kTinyStride];
   __shared__ unsigned long long s_mask[kTinyWaves][16];
@@ -441,9 +428,6 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
     const int depth0 = (int)rec[2];
     const uint32_t* src = rec[3] ? buf1 : buf0;
     const int64_t root_slot = rec[4];
-    int64_t next = rec[5];
-    const int64_t res_end = rec[5] + 2 * (int64_t)m - 2;
-    const int64_t jbase = rec[6];
     const bool act = lane < m;
     int lab = 0;
     if (act) {
@@ -545,8 +529,9 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
       if (bf < 0) continue;  // leaf: the record written at creation stands
       const unsigned long long LM = M & __ballot((uint32_t)my_bytes[bf] <= bb);
       const unsigned long long RM = M & ~LM;
-      const int64_t ls = next, rs = next + 1;
-      next += 2;
+      int alloc = 0;
+      if (lane == 0) alloc = atomicAdd(node_counter, 2);
+      const int64_t ls = __builtin_amdgcn_readfirstlane(alloc), rs = ls + 1;
       const int nl = __popcll(LM), nr = __popcll(RM);
       int nzl = 0, nzr = 0;
 #pragma unroll
@@ -567,8 +552,8 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
         int32_t* P = node_i32 + slot * 6;
         P[0] = bf;
         P[1] = (int32_t)bb;
-        P[2] = (int32_t)(ls - jbase);
-        P[3] = (int32_t)(rs - jbase);
+        P[2] = (int32_t)ls;
+        P[3] = (int32_t)rs;
         int32_t* L = node_i32 + ls * 6;
         int32_t* R = node_i32 + rs * 6;
         L[0] = -1; L[1] = -1; L[2] = -1; L[3] = -1; L[4] = cd; L[5] = nl;
@@ -591,12 +576,6 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
     }
-    // unreachable filler for the unused part of the reservation
-    for (int64_t s = next + lane; s < res_end; s += kWave) {
-      int32_t* Q = node_i32 + s * 6;
-      Q[0] = -1; Q[1] = -1; Q[2] = -1; Q[3] = -1; Q[4] = 0; Q[5] = 0;
-      for (int c = 0; c < C; ++c) node_cnt[s * C + c] = 0;
-    }
   }
 }
 
@@ -608,9 +587,10 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                    uint32_t* buf1, const int32_t* y, int lab_shift, const int64_t* jobs, int J,
                    int32_t* counter, const int32_t* nbins, int F, int B, int C, int crit,
                    int max_depth, int64_t mss, int64_t msl, const double* xtab, int xtab_n,
-                   int32_t* node_i32, int32_t* node_cnt, int32_t* job_nodes, int grid,
+                   int32_t* node_i32, int32_t* node_cnt, int32_t* job_root, int grid,
                    int tiny_rows, int64_t* tiny, int tiny_grid) {
-  // counter: int32 [3] = {job cursor, tiny count, tiny cursor}, zeroed by the host
+  // counter: int32 [4] = {job cursor, tiny count, tiny cursor, node count}, zeroed by
+  // the host; node slots are handed out by the last one (compact output)
   if (J <= 0) return;
   if (C > kFinMaxC) throw std::runtime_error("finisher supports at most 16 classes");
   if (code_bytes != 1 || F > kTinyMaxF || tiny == nullptr) tiny_rows = 0;
@@ -623,8 +603,8 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   hipLaunchKernelGGL(finish_cls_kernel<CT>, dim3(grid), dim3(kFinThreads), lds, stream,       \
                      (const uint32_t*)codes_rm, row_words, (const CT*)codes_fm, n_rows, buf0, \
                      buf1, y, rl, jobs, J, counter, nbins, F, B, C, crit, max_depth, mss,     \
-                     msl, xtab, xtab_n, node_i32, node_cnt, job_nodes, tiny_rows, tiny,       \
-                     counter + 1);
+                     msl, xtab, xtab_n, node_i32, node_cnt, job_root, counter + 3, tiny_rows, \
+                     tiny, counter + 1);
   if (code_bytes == 1) {
     MT_FIN(uint8_t)
   } else {
@@ -636,7 +616,7 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
     hipLaunchKernelGGL(finish_tiny_kernel, dim3(tiny_grid), dim3(kTinyWaves * kWave), 0, stream,
                        (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,
                        counter + 1, counter + 2, F, C, crit, max_depth, mss, msl, xtab,
-                       node_i32, node_cnt);
+                       node_i32, node_cnt, counter + 3);
     MT_HIP_CHECK(hipGetLastError());
   }
 }

@@ -343,30 +343,29 @@ class HipBackend:
         return self.F * (self.B * ((self.C + 1) // 2) + 1) * 4 <= 150 * 1024
 
     def finish_subtrees(self, starts, counts, depths, params, stats=None):
-        """Grow every job's subtree on the device; concatenated node tables out.
+        """Grow every job's subtree on the device; one compact node table out.
 
         Returns a dict of arrays (feature, bin, left, right, depth, nsamp,
-        stats) holding all jobs' nodes, job j at ``offsets[j]:offsets[j+1]``
-        with root first and child indices local to the job.
+        stats) over all finisher nodes, child links indexing this table, and
+        ``roots[j]``: the row of job j's root.
         """
         J = len(starts)
         starts = np.asarray(starts, np.int64)
         counts = np.asarray(counts, np.int64)
         depths = np.asarray(depths, np.int64)
         order = np.argsort(-counts, kind="stable")  # largest first
-        slots = 2 * counts[order] - 1
-        base = np.cumsum(slots) - slots
         st = np.asarray(stats, np.int64).reshape(J, self.C)
-        # {start, count, depth, base, row buffer, class counts[C]}
-        jobs = np.concatenate([np.stack([starts[order], counts[order], depths[order], base,
-                                         np.zeros(J, np.int64)], 1), st[order]], 1)
-        total = int(slots.sum())
+        # {start, count, depth, -, row buffer, class counts[C]}
+        jobs = np.concatenate([np.stack([starts[order], counts[order], depths[order],
+                                         np.zeros(J, np.int64), np.zeros(J, np.int64)], 1),
+                               st[order]], 1)
+        total = int((2 * counts - 1).sum())  # a subtree of r rows has <= 2r-1 nodes
         C = self.C
         (d_jobs,) = self.up(jobs)
         node_i32 = torch.empty((total, 6), dtype=torch.int32, device=self.device)
         node_cnt = torch.empty((total, C), dtype=torch.int32, device=self.device)
-        job_nodes = torch.empty(J, dtype=torch.int32, device=self.device)
-        counter = torch.zeros(3, dtype=torch.int32, device=self.device)
+        job_root = torch.empty(J, dtype=torch.int32, device=self.device)
+        counter = torch.zeros(4, dtype=torch.int32, device=self.device)
         tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
         # every tiny subtree has >= 2 rows and they partition the job rows
         tiny_cap = int(counts.sum() // 2 + J + 1)
@@ -379,46 +378,16 @@ class HipBackend:
                         J, counter.data_ptr(), self.nbins.data_ptr(), self.F, self.B, C,
                         int(self.crit), md, int(params.min_samples_split),
                         int(max(1, params.min_samples_leaf)), self.xtab.data_ptr(), XTAB_N,
-                        node_i32.data_ptr(), node_cnt.data_ptr(), job_nodes.data_ptr(), grid,
+                        node_i32.data_ptr(), node_cnt.data_ptr(), job_root.data_ptr(), grid,
                         tiny_rows, tiny.data_ptr(), 4 * N_CU)
-        # Compact on the device: keep the written, live slots of every job
-        # (unused tails and the unreachable fillers of tiny-subtree
-        # reservations are dropped), re-map job-local child ids to the
-        # compacted positions, and copy only live nodes to the host.
-        dev = self.device
-        slots_t = torch.from_numpy(slots).to(dev)
-        base_t = torch.from_numpy(base).to(dev)
-        job_of = torch.repeat_interleave(torch.arange(J, device=dev), slots_t)
-        within = torch.arange(total, device=dev) - base_t[job_of]
-        alive = (within < job_nodes.long()[job_of]) & (node_i32[:, 5] > 0)
-        cum = torch.cumsum(alive.long(), 0)
-        new_pos = cum - 1
-        cstart = (cum - alive.long())[base_t]  # compacted start of every job
-        sel = torch.nonzero(alive).squeeze(1)
-        ni_t = node_i32.index_select(0, sel).long()
-        nc_t = node_cnt.index_select(0, sel)
-        jsel = job_of[sel]
-        inner = ni_t[:, 0] >= 0
-        for col in (2, 3):
-            old_slot = base_t[jsel] + ni_t[:, col].clamp(min=0)
-            ni_t[:, col] = torch.where(inner, new_pos[old_slot] - cstart[jsel], ni_t[:, col])
-        jn_t = torch.bincount(jsel, minlength=J)
-        ni = ni_t.cpu().numpy()
-        nc = nc_t.cpu().numpy()
-        jn = jn_t.cpu().numpy().astype(np.int64)
-        # back to the caller's job order
-        inv = np.empty(J, np.int64)
-        inv[order] = np.arange(J)
-        off_sorted = np.concatenate([[0], np.cumsum(jn)])
-        lens = jn[inv]
-        offsets = np.concatenate([[0], np.cumsum(lens)])
-        take = np.repeat(off_sorted[inv], lens) + (
-            np.arange(int(offsets[-1])) - np.repeat(offsets[:-1], lens))
-        ni = ni[take]
-        nc = nc[take]
+        N = int(counter[3].item())
+        ni = node_i32[:N].cpu().numpy()
+        nc = node_cnt[:N].cpu().numpy()
+        roots = np.empty(J, np.int64)
+        roots[order] = job_root.cpu().numpy()
         return dict(feature=ni[:, 0], bin=ni[:, 1], left=ni[:, 2].astype(np.int64),
                     right=ni[:, 3].astype(np.int64), depth=ni[:, 4], nsamp=ni[:, 5].astype(np.int64),
-                    stats=nc.astype(np.int64), offsets=offsets)
+                    stats=nc.astype(np.int64), roots=roots)
 
     def sync(self):
         if self.timing:

@@ -140,18 +140,22 @@ class DistComm(LocalComm):
         return self._owner == self.rank
 
     def merge_subtrees(self, local: dict, owned: np.ndarray, n_jobs: int) -> dict:
-        """All ranks receive every job's node table, in job order."""
+        """All ranks receive every job's nodes: one table, roots in job order.
+
+        Three collectives in total: the per-rank node counts, the job roots
+        (shifted to each rank's offset) and the padded node tables.
+        """
         P = self.world_size
-        owner = self._owner
         C = local["stats"].shape[1]
-        lens_local = np.zeros(n_jobs, dtype=np.int64)
-        lens_local[np.nonzero(owned)[0]] = np.diff(local["offsets"])
-        lens = self._all_reduce(lens_local)
-        rows_of = np.array([lens[owner == r].sum() for r in range(P)], dtype=np.int64)
-        Tmax = int(rows_of.max()) if P else 0
+        T = int(len(local["feature"]))
+        sizes = self._all_gather(np.array([T], dtype=np.int64)).reshape(P)
+        offs = np.concatenate([[0], np.cumsum(sizes)])
+        roots_local = np.zeros(n_jobs, dtype=np.int64)
+        roots_local[np.nonzero(owned)[0]] = np.asarray(local["roots"], np.int64) + offs[self.rank]
+        roots = self._all_reduce(roots_local)
         W = 6 + C
+        Tmax = int(sizes.max())
         pack = np.zeros((max(Tmax, 1), W), dtype=np.int64)
-        T = int(local["offsets"][-1])
         if T:
             pack[:T, 0] = local["feature"]
             pack[:T, 1] = local["bin"]
@@ -161,19 +165,15 @@ class DistComm(LocalComm):
             pack[:T, 5] = local["nsamp"]
             pack[:T, 6:] = local["stats"]
         allp = self._all_gather(pack)  # [P, Tmax, W]
-        offsets = np.concatenate([[0], np.cumsum(lens)])
-        out = np.empty((int(offsets[-1]), W), dtype=np.int64)
-        for r in range(P):
-            jobs = np.nonzero(owner == r)[0]  # increasing job order == rank's local order
-            if jobs.size == 0:
-                continue
-            L = lens[jobs]
-            dest = np.repeat(offsets[jobs], L) + (np.arange(L.sum()) - np.repeat(
-                np.cumsum(L) - L, L))
-            out[dest] = allp[r, : L.sum()]
+        out = np.concatenate([allp[r, : sizes[r]] for r in range(P)], 0)
+        for r in range(P):  # child links become global table rows
+            blk = out[offs[r] : offs[r + 1]]
+            inner = blk[:, 0] >= 0
+            blk[inner, 2] += offs[r]
+            blk[inner, 3] += offs[r]
         return dict(feature=out[:, 0].astype(np.int32), bin=out[:, 1].astype(np.int32),
                     left=out[:, 2], right=out[:, 3], depth=out[:, 4].astype(np.int32),
-                    nsamp=out[:, 5], stats=out[:, 6:], offsets=offsets)
+                    nsamp=out[:, 5], stats=out[:, 6:], roots=roots)
 
     def check_consistent(self, digest: int) -> bool:
         """Cross-rank check that every rank built the same tree."""
