@@ -271,7 +271,9 @@ def fit_tree(
     if comm.world_size > 1:
         stats["strategy"] = comm.kind
         stats["bytes_communicated"] = getattr(comm, "bytes_communicated", 0)
+    t0 = time.perf_counter()
     ta = _finalize(ta, mapper, regression, y_exp)
+    timings["finalize"] = time.perf_counter() - t0
     timings["total"] = time.perf_counter() - t_start
     return FitResult(arrays=ta, classes=classes, n_features=F, mapper=mapper, y_scale_exp=y_exp,
                      engine=eng, timings=timings, stats=stats)

@@ -308,16 +308,23 @@ class LevelwiseBuilder:
             self._finish(tab, d)
             self._tick("finisher", t0)
             self.stats["finisher_subtrees"] = int(d["id"].size)
-        return self._to_arrays(tab)
+        t0 = time.perf_counter()
+        ta = self._to_arrays(tab)
+        self.timings["assemble"] = time.perf_counter() - t0
+        return ta
 
     # ------------------------------------------------------------ finisher
     def _finish(self, tab: _Table, d: dict):
         """Grow each deferred subtree with the backend's subtree finisher."""
         comm = self.comm
         owned = comm.finish_assignment(d["m"])
+        t0 = time.perf_counter()
         local = self.be.finish_subtrees(d["start"][owned], d["count"][owned], d["depth"][owned],
                                         self.p, stats=tab.stats[d["id"][owned]])
+        self.timings["finisher_device"] = time.perf_counter() - t0
+        t0 = time.perf_counter()
         t = comm.merge_subtrees(local, owned, d["id"].size)
+        self.timings["finisher_merge"] = time.perf_counter() - t0
         # ``t`` is one node table for all deferred subtrees (child links index
         # it, ``roots[j]`` is job j's root): append every row, link children,
         # then copy each root's split onto the deferred node it continues (the
