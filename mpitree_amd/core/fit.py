@@ -148,7 +148,8 @@ def _encode_targets(y, n):
 
 
 def _finalize(ta: TreeArrays, mapper: BinMapper, regression: bool, y_exp: int) -> TreeArrays:
-    ta.with_thresholds(mapper.edges)
+    if not ta.meta.pop("thresholds_set", False):
+        ta.with_thresholds(mapper.edges)
     m = ta.n_samples.astype(np.float64)
     term = ta.impurity
     with np.errstate(invalid="ignore", divide="ignore"):
@@ -234,7 +235,7 @@ def fit_tree(
             finisher_rows = 0
         params.finisher_rows = int(finisher_rows)
         builder = LevelwiseBuilder(be, params, comm)
-        ta = builder.fit(hi - lo, C, F)
+        ta = builder.fit(hi - lo, C, F, edges=mapper.padded_edges())
         eng = "hip-levelwise"
         timings.update(builder.timings)
         stats = dict(builder.stats)
@@ -264,7 +265,7 @@ def fit_tree(
             be.setup(codes, yh, n_bins=mapper.max_n_bins, n_classes=C, criterion=crit)
             params.finisher_rows = int(finisher_rows or 0)
             builder = LevelwiseBuilder(be, params, comm)
-            ta = builder.fit(hi - lo, C, F)
+            ta = builder.fit(hi - lo, C, F, edges=mapper.padded_edges())
             eng = "numpy-levelwise"
             timings.update(builder.timings)
             stats = dict(builder.stats)

@@ -115,12 +115,12 @@ class _Table:
         depth = np.atleast_1d(np.asarray(depth))
         k = depth.shape[0]
         self._grow(self.n + k)
-        ids = np.arange(self.n, self.n + k)
-        self.depth[ids] = depth
-        self.nsamp[ids] = nsamp
-        self.stats[ids] = np.asarray(stats, dtype=np.int64).reshape(k, self.C)
+        lo = self.n
+        self.depth[lo : lo + k] = depth
+        self.nsamp[lo : lo + k] = nsamp
+        self.stats[lo : lo + k] = np.asarray(stats, dtype=np.int64).reshape(k, self.C)
         self.n += k
-        return ids
+        return np.arange(lo, lo + k)
 
 
 def _node_terms(crit, stats: np.ndarray) -> np.ndarray:
@@ -168,7 +168,9 @@ class LevelwiseBuilder:
         self.timings[key] = self.timings.get(key, 0.0) + time.perf_counter() - t0
 
     # ---------------------------------------------------------------- fit
-    def fit(self, n_local: int, n_classes: int, n_features: int) -> TreeArrays:
+    def fit(self, n_local: int, n_classes: int, n_features: int, edges=None) -> TreeArrays:
+        """Grow the tree; ``edges`` ([F, B] padded bin edges) fills thresholds."""
+        self._edges = edges
         p, be, comm = self.p, self.be, self.comm
         reg = p.criterion == Criterion.SQUARED_ERROR
         C = 2 if reg else n_classes
@@ -333,20 +335,23 @@ class LevelwiseBuilder:
         T = len(t["feature"])
         if T == 0:
             return
-        gids = tab.add(t["depth"], t["nsamp"], t["stats"])
-        inner = np.nonzero(t["feature"] >= 0)[0]
-        g = gids[inner]
-        tab.feature[g] = t["feature"][inner]
-        tab.tbin[g] = t["bin"][inner]
-        tab.left[g] = gids[t["left"][inner]]
-        tab.right[g] = gids[t["right"][inner]]
-        r = np.asarray(t["roots"], np.int64)
+        base = tab.n
+        tab.add(t["depth"], t["nsamp"], t["stats"])
+        f = np.asarray(t["feature"])
+        inner = f >= 0
+        sl = slice(base, base + T)
+        tab.feature[sl] = f
+        tab.tbin[sl] = t["bin"]
+        tab.left[sl] = np.where(inner, np.asarray(t["left"]) + base, -1)
+        tab.right[sl] = np.where(inner, np.asarray(t["right"]) + base, -1)
+        r = np.asarray(t["roots"], np.int64) + base
         did = d["id"]
-        split = t["feature"][r] >= 0
-        tab.feature[did[split]] = t["feature"][r[split]]
-        tab.tbin[did[split]] = t["bin"][r[split]]
-        tab.left[did[split]] = gids[t["left"][r[split]]]
-        tab.right[did[split]] = gids[t["right"][r[split]]]
+        split = tab.feature[r] >= 0
+        did, r = did[split], r[split]
+        tab.feature[did] = tab.feature[r]
+        tab.tbin[did] = tab.tbin[r]
+        tab.left[did] = tab.left[r]
+        tab.right[did] = tab.right[r]
 
     # -------------------------------------------------------------- output
     def _to_arrays(self, tab: _Table) -> TreeArrays:
@@ -358,17 +363,21 @@ class LevelwiseBuilder:
             cpu = native.cpu()
         except ImportError:
             cpu = None
-        if cpu is not None:  # one native pass: pre-order walk + column gather
+        if cpu is not None:  # one native pass: pre-order, gather, thresholds, terms
+            edges = self._edges
             a = cpu.assemble(tab.feature[:n], tab.tbin[:n], tab.left[:n], tab.right[:n],
-                             tab.nsamp[:n], tab.stats[:n], 0)
+                             tab.nsamp[:n], tab.stats[:n], 0,
+                             np.empty((0, 0)) if edges is None else edges,
+                             int(self.p.criterion))
             st = a["stats"]
             ta = TreeArrays(
-                feature=a["feature"], threshold=np.full(len(st), np.nan),
+                feature=a["feature"], threshold=a.get("threshold", np.full(len(st), np.nan)),
                 threshold_bin=a["bin"], left=a["left"], right=a["right"], depth=a["depth"],
-                n_samples=a["nsamp"], impurity=_node_terms(self.p.criterion, st),
+                n_samples=a["nsamp"], impurity=a["term"],
                 count=None if reg else st,
                 value=st[:, 1].astype(np.float64) if reg else None,
             )
+            ta.meta["thresholds_set"] = edges is not None
             if reg:
                 ta.meta["sum_fixed"] = st[:, 1].copy()
             return ta

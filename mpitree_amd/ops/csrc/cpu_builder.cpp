@@ -401,62 +401,130 @@ py::tuple preorder(py::array_t<int32_t, py::array::c_style | py::array::forcecas
   return py::make_tuple(o, d);
 }
 
-// Re-number an arbitrary node table into pre-order and gather every column in
-// one pass (the tree-assembly step after a level-wise + finisher fit).
+// x*log2(x) for small counts (same function, same bits as the kernels).
+const std::vector<double>& xlog_table() {
+  static const std::vector<double> tab = [] {
+    std::vector<double> t(1 << 16);
+    for (size_t x = 0; x < t.size(); ++x) t[x] = mt::xlog2x(x);
+    return t;
+  }();
+  return tab;
+}
+
+inline double tabled_xlog(const std::vector<double>& tab, int64_t x) {
+  return x < (int64_t)tab.size() ? tab[x] : mt::xlog2x((uint64_t)x);
+}
+
+// Node term of one node: c = C class counts, or (count, fixed-point sum).
+inline double node_term(const int64_t* c, int64_t C, int crit, const std::vector<double>& tab) {
+  if (crit == mt::kSquaredError) return mt::mse_term(c[0], c[1]);
+  if (crit == mt::kEntropy) {
+    double acc = 0.0;
+    int64_t m = 0;
+    for (int64_t k = 0; k < C; ++k) {
+      acc = acc + tabled_xlog(tab, c[k]);
+      m += c[k];
+    }
+    return tabled_xlog(tab, m) - acc;
+  }
+  int64_t m = 0, sq = 0;
+  for (int64_t k = 0; k < C; ++k) {
+    m += c[k];
+    sq += c[k] * c[k];
+  }
+  return mt::gini_term(m, sq);
+}
+
+// Re-number a node table into pre-order and emit every output column (the
+// tree-assembly step after a level-wise + finisher fit). Optional: split
+// thresholds from a padded [F, B] edge table, node terms for criterion ``crit``.
 py::dict assemble(py::array_t<int32_t, py::array::c_style | py::array::forcecast> feature,
                   py::array_t<int32_t, py::array::c_style | py::array::forcecast> tbin,
                   py::array_t<int64_t, py::array::c_style | py::array::forcecast> left,
                   py::array_t<int64_t, py::array::c_style | py::array::forcecast> right,
                   py::array_t<int64_t, py::array::c_style | py::array::forcecast> nsamp,
                   py::array_t<int64_t, py::array::c_style | py::array::forcecast> stats,
-                  int64_t root) {
+                  int64_t root,
+                  py::array_t<double, py::array::c_style | py::array::forcecast> edges,
+                  int crit) {
   const int64_t n = feature.shape(0);
   const int64_t C = stats.ndim() == 2 ? stats.shape(1) : 1;
   const int32_t* f = feature.data();
   const int64_t* l = left.data();
   const int64_t* r = right.data();
-  std::vector<int64_t> order;
-  order.reserve(n);
-  std::vector<int64_t> new_id(n, -1);
-  std::vector<int32_t> dep;
-  dep.reserve(n);
-  std::vector<std::pair<int64_t, int32_t>> stack{{root, 0}};
-  while (!stack.empty()) {
-    auto [i, d] = stack.back();
-    stack.pop_back();
-    new_id[i] = (int64_t)order.size();
-    order.push_back(i);
-    dep.push_back(d);
-    if (f[i] >= 0) {
-      stack.push_back({r[i], d + 1});
-      stack.push_back({l[i], d + 1});
-    }
-  }
-  const int64_t k = (int64_t)order.size();
-  py::array_t<int32_t> of(k), ob(k), od(k), ol(k), orr(k);
-  py::array_t<int64_t> on(k), oo(k);
-  py::array_t<int64_t> os({k, C});
-  int32_t *pf = of.mutable_data(), *pb = ob.mutable_data(), *pd = od.mutable_data();
-  int32_t *pl = ol.mutable_data(), *pr = orr.mutable_data();
-  int64_t *pn = on.mutable_data(), *po = oo.mutable_data(), *ps = os.mutable_data();
   const int32_t* b = tbin.data();
   const int64_t* ns = nsamp.data();
   const int64_t* st = stats.data();
-  for (int64_t j = 0; j < k; ++j) {
-    const int64_t i = order[j];
+  const bool want_thr = edges.ndim() == 2 && edges.size() > 0;
+  const int64_t EB = want_thr ? edges.shape(1) : 0;
+  const double* ed = want_thr ? edges.data() : nullptr;
+  const bool want_term = crit >= 0;
+  const std::vector<double>& tab = xlog_table();
+
+  std::vector<int64_t> new_id(n, -1);
+  std::vector<int32_t> depv(n, 0);
+  int64_t k = 0;
+  // Every builder creates children after their parent (child id > parent id),
+  // so subtree sizes come from one backward sweep and pre-order positions from
+  // one forward sweep: sequential reads, scattered writes, no DFS stack.
+  bool topo = root == 0;
+  for (int64_t i = 0; i < n && topo; ++i)
+    if (f[i] >= 0 && (l[i] <= i || r[i] <= i || l[i] >= n || r[i] >= n)) topo = false;
+  if (topo) {
+    std::vector<int64_t> size(n, 1);
+    for (int64_t i = n - 1; i >= 0; --i)
+      if (f[i] >= 0) size[i] = 1 + size[l[i]] + size[r[i]];
+    k = n ? size[0] : 0;
+    if (n) new_id[0] = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      if (new_id[i] < 0 || f[i] < 0) continue;
+      new_id[l[i]] = new_id[i] + 1;
+      new_id[r[i]] = new_id[i] + 1 + size[l[i]];
+      depv[l[i]] = depv[i] + 1;
+      depv[r[i]] = depv[i] + 1;
+    }
+  } else {  // general tables: explicit DFS
+    std::vector<int64_t> stack{root};
+    while (!stack.empty()) {
+      const int64_t i = stack.back();
+      stack.pop_back();
+      new_id[i] = k++;
+      if (f[i] >= 0) {
+        depv[l[i]] = depv[i] + 1;
+        depv[r[i]] = depv[i] + 1;
+        stack.push_back(r[i]);
+        stack.push_back(l[i]);
+      }
+    }
+  }
+  py::array_t<int32_t> of(k), ob(k), od(k), ol(k), orr(k);
+  py::array_t<int64_t> on(k), oo(k);
+  py::array_t<int64_t> os({k, C});
+  py::array_t<double> othr(want_thr ? k : 0), oterm(want_term ? k : 0);
+  int32_t *pf = of.mutable_data(), *pb = ob.mutable_data(), *pd = od.mutable_data();
+  int32_t *pl = ol.mutable_data(), *pr = orr.mutable_data();
+  int64_t *pn = on.mutable_data(), *po = oo.mutable_data(), *ps = os.mutable_data();
+  double* pt = want_thr ? othr.mutable_data() : nullptr;
+  double* pm = want_term ? oterm.mutable_data() : nullptr;
+  for (int64_t i = 0; i < n; ++i) {  // scatter node i to its pre-order slot
+    const int64_t j = new_id[i];
+    if (j < 0) continue;
     po[j] = i;
     pf[j] = f[i];
-    pd[j] = dep[j];
+    pd[j] = depv[i];
     pn[j] = ns[i];
     for (int64_t c = 0; c < C; ++c) ps[j * C + c] = st[i * C + c];
+    if (want_term) pm[j] = node_term(st + i * C, C, crit, tab);
     if (f[i] >= 0) {
       pb[j] = b[i];
       pl[j] = (int32_t)new_id[l[i]];
       pr[j] = (int32_t)new_id[r[i]];
+      if (want_thr) pt[j] = ed[(int64_t)f[i] * EB + b[i]];
     } else {
       pb[j] = -1;
       pl[j] = -1;
       pr[j] = -1;
+      if (want_thr) pt[j] = std::numeric_limits<double>::quiet_NaN();
     }
   }
   py::dict out;
@@ -468,6 +536,8 @@ py::dict assemble(py::array_t<int32_t, py::array::c_style | py::array::forcecast
   out["depth"] = od;
   out["nsamp"] = on;
   out["stats"] = os;
+  if (want_thr) out["threshold"] = othr;
+  if (want_term) out["term"] = oterm;
   return out;
 }
 
@@ -478,33 +548,8 @@ py::array_t<double> node_terms(py::array_t<int64_t, py::array::c_style | py::arr
   const int64_t* s = st.data();
   py::array_t<double> out(N);
   double* o = out.mutable_data();
-  static std::vector<double> tab;  // x*log2(x) for small counts (same function, same bits)
-  if (tab.empty()) {
-    tab.resize(1 << 16);
-    for (size_t x = 0; x < tab.size(); ++x) tab[x] = mt::xlog2x(x);
-  }
-  auto T = [&](int64_t x) { return x < (int64_t)tab.size() ? tab[x] : mt::xlog2x((uint64_t)x); };
-  for (int64_t i = 0; i < N; ++i) {
-    const int64_t* c = s + i * C;
-    if (crit == mt::kSquaredError) {
-      o[i] = mt::mse_term(c[0], c[1]);
-    } else if (crit == mt::kEntropy) {
-      double acc = 0.0;
-      int64_t m = 0;
-      for (int64_t k = 0; k < C; ++k) {
-        acc = acc + T(c[k]);
-        m += c[k];
-      }
-      o[i] = T(m) - acc;
-    } else {
-      int64_t m = 0, sq = 0;
-      for (int64_t k = 0; k < C; ++k) {
-        m += c[k];
-        sq += c[k] * c[k];
-      }
-      o[i] = mt::gini_term(m, sq);
-    }
-  }
+  const std::vector<double>& tab = xlog_table();
+  for (int64_t i = 0; i < N; ++i) o[i] = node_term(s + i * C, C, crit, tab);
   return out;
 }
 
@@ -520,7 +565,9 @@ PYBIND11_MODULE(_cpu, m) {
   m.doc() = "mpitree_amd native host builder and tree helpers";
   m.def("build_tree", &build_tree);
   m.def("preorder", &preorder);
-  m.def("assemble", &assemble);
+  m.def("assemble", &assemble, py::arg("feature"), py::arg("tbin"), py::arg("left"),
+        py::arg("right"), py::arg("nsamp"), py::arg("stats"), py::arg("root") = 0,
+        py::arg("edges") = py::array_t<double>(), py::arg("crit") = -1);
   m.def("node_terms", &node_terms);
   m.def("xlog2x", &xlog2x_np);
 }

@@ -32,6 +32,7 @@ constexpr int kFinWaves = kFinThreads / kWave;
 constexpr int kFinStack = 40;    // >= log2(max job rows) + 2
 constexpr int kFinMaxC = 16;     // classes supported by the finisher
 constexpr int kFinTab = 1024;    // LDS x*log2(x) entries
+constexpr int kFinUnroll = 4;    // row gathers in flight per lane
 
 struct FinRowLab {
   uint32_t mask;
@@ -76,6 +77,10 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
   const int words = (F + cpw - 1) / cpw;
   const int tn = min(kFinTab, xtab_n);
   const int JW = 5 + C;
+  // 16-B row loads when the row stride allows it; lanes per row = pow2 >= words/vec
+  const int vec = (row_words % 4) == 0 ? 4 : 1;
+  int lane_shift = 0;
+  while ((1 << lane_shift) * vec < words && lane_shift < 6) ++lane_shift;
 
   for (int i = tid; i < tn; i += kFinThreads) s_tab[i] = xtab[i];
   for (int e = tid; e < F * fstride; e += kFinThreads) hist[e] = 0u;
@@ -153,22 +158,58 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
       const int id = s_id;
       uint32_t* __restrict__ src = s_buf ? buf1 : buf0;
       uint32_t* __restrict__ dst = s_buf ? buf0 : buf1;
-      // ---- histogram of this node's rows (all features)
-      for (int e = tid; e < m * words; e += kFinThreads) {
-        const int r = e / words;
-        const int wi = e - r * words;
-        const uint32_t ent = src[start + r];
-        const uint32_t row = rl.shift ? (ent & rl.mask) : ent;
-        const int lab = rl.shift ? (int)(ent >> rl.shift) : y[row];
-        const uint32_t wv = codes_rm[(int64_t)row * row_words + wi];
-        const uint32_t inc = 1u << ((lab & 1) * 16);
+      // ---- histogram of this node's rows (all features): VEC words per lane,
+      // lanes_per_row lanes per row, kFinUnroll rows in flight per lane
+      {
+        const int L = 1 << lane_shift;
+        const int sub = tid & (L - 1);
+        const int rpp = kFinThreads >> lane_shift;
+        const int my_w = sub * vec;
+        const bool active = my_w < words;
+        for (int base_r = tid >> lane_shift; base_r < m; base_r += rpp * kFinUnroll) {
+          uint32_t ent[kFinUnroll];
 #pragma unroll
-        for (int j = 0; j < cpw; ++j) {
-          const int f = wi * cpw + j;
-          if (f < F) {
-            const uint32_t code =
-                (wv >> (j * 8 * sizeof(CodeT))) & ((sizeof(CodeT) == 1) ? 0xffu : 0xffffu);
-            atomicAdd(&hist[f * fstride + (int)code * W + (lab >> 1)], inc);
+          for (int u = 0; u < kFinUnroll; ++u) {
+            const int r = base_r + u * rpp;
+            ent[u] = (active && r < m) ? src[start + r] : 0xffffffffu;
+          }
+          uint32_t wv[kFinUnroll][4];
+          int lab[kFinUnroll];
+#pragma unroll
+          for (int u = 0; u < kFinUnroll; ++u) {
+            const bool ok = ent[u] != 0xffffffffu;
+            const uint32_t row = rl.shift ? (ent[u] & rl.mask) : ent[u];
+            lab[u] = ok ? (rl.shift ? (int)(ent[u] >> rl.shift) : y[row]) : 0;
+            if (vec == 4) {
+              const uint4 v = ok ? *reinterpret_cast<const uint4*>(codes_rm + (int64_t)row * row_words + my_w)
+                                 : make_uint4(0, 0, 0, 0);
+              wv[u][0] = v.x;
+              wv[u][1] = v.y;
+              wv[u][2] = v.z;
+              wv[u][3] = v.w;
+            } else {
+              wv[u][0] = ok ? codes_rm[(int64_t)row * row_words + my_w] : 0u;
+              wv[u][1] = wv[u][2] = wv[u][3] = 0u;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < kFinUnroll; ++u) {
+            if (ent[u] == 0xffffffffu) continue;
+            const uint32_t inc = 1u << ((lab[u] & 1) * 16);
+            const int off = lab[u] >> 1;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              if (v >= vec) break;
+#pragma unroll
+              for (int j = 0; j < cpw; ++j) {
+                const int f = (my_w + v) * cpw + j;
+                if (f < F) {
+                  const uint32_t code = (wv[u][v] >> (j * 8 * sizeof(CodeT))) &
+                                        ((sizeof(CodeT) == 1) ? 0xffu : 0xffffu);
+                  atomicAdd(&hist[f * fstride + (int)code * W + off], inc);
+                }
+              }
+            }
           }
         }
       }
@@ -285,27 +326,41 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
         }
         // ---- partition rows src -> dst (unstable; left from the front, right from the back)
         const CodeT* col = codes_fm + (int64_t)bf * n_rows;
-        for (int r0 = 0; r0 < m; r0 += kFinThreads) {
-          const int r = r0 + tid;
-          const bool valid = r < m;
-          const uint32_t ent = valid ? src[start + r] : 0u;
-          const bool go = valid && (uint32_t)col[ent & rl.mask] <= (uint32_t)bb;
-          const unsigned long long bl = __ballot(go);
-          const unsigned long long br = __ballot(valid && !go);
-          const unsigned long long lt = (1ull << lane) - 1ull;
-          int basel = 0, baser = 0;
-          if (lane == 0) {
-            const int nl = __popcll(bl), nr = __popcll(br);
-            basel = nl ? atomicAdd(&s_lc, nl) : 0;
-            baser = nr ? atomicAdd(&s_rc, nr) : 0;
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        for (int r0 = 0; r0 < m; r0 += kFinThreads * kFinUnroll) {
+          uint32_t ent[kFinUnroll];
+          uint32_t cv[kFinUnroll];
+#pragma unroll
+          for (int u = 0; u < kFinUnroll; ++u) {
+            const int r = r0 + u * kFinThreads + tid;
+            ent[u] = r < m ? src[start + r] : 0u;
           }
-          basel = __shfl(basel, 0, kWave);
-          baser = __shfl(baser, 0, kWave);
-          if (valid) {
-            if (go)
-              dst[start + basel + __popcll(bl & lt)] = ent;
-            else
-              dst[start + m - 1 - (baser + __popcll(br & lt))] = ent;
+#pragma unroll
+          for (int u = 0; u < kFinUnroll; ++u) {
+            const int r = r0 + u * kFinThreads + tid;
+            cv[u] = r < m ? (uint32_t)col[ent[u] & rl.mask] : 0u;
+          }
+#pragma unroll
+          for (int u = 0; u < kFinUnroll; ++u) {
+            const int r = r0 + u * kFinThreads + tid;
+            const bool valid = r < m;
+            const bool go = valid && cv[u] <= (uint32_t)bb;
+            const unsigned long long bl = __ballot(go);
+            const unsigned long long br = __ballot(valid && !go);
+            int basel = 0, baser = 0;
+            if (lane == 0) {
+              const int nl = __popcll(bl), nr = __popcll(br);
+              basel = nl ? atomicAdd(&s_lc, nl) : 0;
+              baser = nr ? atomicAdd(&s_rc, nr) : 0;
+            }
+            basel = __builtin_amdgcn_readfirstlane(basel);
+            baser = __builtin_amdgcn_readfirstlane(baser);
+            if (valid) {
+              if (go)
+                dst[start + basel + __popcll(bl & lt)] = ent[u];
+              else
+                dst[start + m - 1 - (baser + __popcll(br & lt))] = ent[u];
+            }
           }
         }
       }
