@@ -7,8 +7,8 @@ from mpitree_amd.core import fit as fitmod
 
 X, y = make_classification(1_000_000, 64, seed=0)
 for md in (None, 12):
-    for fr in (1024, 2048, 4096, 8192, 16384):
-        for tiny in (32, 64):
+    for fr in [int(v) for v in os.environ.get('SWEEP_FR', '1024,2048,4096,8192').split(',')]:
+        for tiny in [int(v) for v in os.environ.get('SWEEP_TINY', '64').split(',')]:
             os.environ["MPITREE_FINISHER_ROWS"] = str(fr)
             os.environ["MPITREE_TINY_ROWS"] = str(tiny)
             fitmod.fit_tree(X, y, regression=False, criterion=0, max_depth=md, min_samples_split=2, device="cuda")

@@ -233,6 +233,7 @@ def fit_tree(
             finisher_rows = int(env) if env else max(2048, n // 512)
         if not be.finisher_supported():
             finisher_rows = 0
+        finisher_rows = min(int(finisher_rows), be.max_finisher_rows)
         params.finisher_rows = int(finisher_rows)
         builder = LevelwiseBuilder(be, params, comm)
         ta = builder.fit(hi - lo, C, F, edges=mapper.padded_edges())

@@ -34,8 +34,9 @@ void launch_bin(hipStream_t, const void*, bool, int64_t, int, const void*, int, 
 void launch_xlog2x(hipStream_t, double*, int64_t);
 void launch_finish(hipStream_t, const void*, int64_t, const void*, int, int64_t, uint32_t*,
                    uint32_t*, const int32_t*, int, const int64_t*, int, int32_t*, const int32_t*,
-                   int, int, int, int, int, int64_t, int64_t, const double*, int, int32_t*,
-                   int32_t*, int32_t*, int, int, int64_t*, int);
+                   int, int, int, int, int, int64_t, int64_t, const double*, const float*, int,
+                   int32_t*,
+                   int32_t*, int32_t*, int, int, int64_t*, int, int64_t*);
 int finish_lds_bytes(int F, int B, int C);
 }  // namespace mt
 
@@ -104,15 +105,16 @@ PYBIND11_MODULE(_hip, m) {
                      int cb, int64_t n_rows, uintptr_t idx, uintptr_t tmp, uintptr_t y,
                      int lab_shift, uintptr_t jobs, int J, uintptr_t counter, uintptr_t nbins,
                      int F, int B, int C, int crit, int max_depth, int64_t mss, int64_t msl,
-                     uintptr_t xtab, int xtab_n, uintptr_t node_i32, uintptr_t node_cnt,
+                     uintptr_t xtab, uintptr_t xtabf, int xtab_n, uintptr_t node_i32,
+                     uintptr_t node_cnt,
                      uintptr_t job_nodes, int grid, int tiny_rows, uintptr_t tiny,
-                     int tiny_grid) {
+                     int tiny_grid, uintptr_t prof) {
     mt::launch_finish(S(s), P<void>(codes_rm), row_words, P<void>(codes_fm), cb, n_rows,
                       P<uint32_t>(idx), P<uint32_t>(tmp), P<int32_t>(y), lab_shift,
                       P<int64_t>(jobs), J, P<int32_t>(counter), P<int32_t>(nbins), F, B, C, crit,
-                      max_depth, mss, msl, P<double>(xtab), xtab_n, P<int32_t>(node_i32),
+                      max_depth, mss, msl, P<double>(xtab), P<float>(xtabf), xtab_n, P<int32_t>(node_i32),
                       P<int32_t>(node_cnt), P<int32_t>(job_nodes), grid, tiny_rows,
-                      P<int64_t>(tiny), tiny_grid);
+                      P<int64_t>(tiny), tiny_grid, P<int64_t>(prof));
   });
   m.def("xlog2x_device", [](uintptr_t s, uintptr_t out, int64_t n) {
     mt::launch_xlog2x(S(s), P<double>(out), n);

@@ -99,6 +99,18 @@ __device__ __forceinline__ double wave_min_f64_dpp(double v) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+// Wave-wide minimum of a float (every lane gets the result).
+__device__ __forceinline__ float wave_min_f32_dpp(float v) {
+  auto step = [](float x, uint32_t o) { return fminf(x, __uint_as_float(o)); };
+  v = step(v, dpp_u32<kDppRowShr + 1>(__float_as_uint(v), __float_as_uint(v)));
+  v = step(v, dpp_u32<kDppRowShr + 2>(__float_as_uint(v), __float_as_uint(v)));
+  v = step(v, dpp_u32<kDppRowShr + 4>(__float_as_uint(v), __float_as_uint(v)));
+  v = step(v, dpp_u32<kDppRowShr + 8>(__float_as_uint(v), __float_as_uint(v)));
+  v = step(v, dpp_u32<kDppRowBcast15, 0xa>(__float_as_uint(v), __float_as_uint(v)));
+  v = step(v, dpp_u32<kDppRowBcast31, 0xc>(__float_as_uint(v), __float_as_uint(v)));
+  return __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(v), 63));
+}
+
 // (cost, bin) argmin with ties to the lowest bin, for bins owned by lanes in
 // increasing order (lane l holds only bins below lane l+1's): the minimum
 // cost, then the lowest lane holding it. Result broadcast to every lane.

@@ -22,6 +22,8 @@
 // atomic counter, so the output is compact; the allocation order varies from
 // run to run but every link is explicit and the host re-numbers the final
 // tree into pre-order, so the fitted tree is bitwise deterministic.
+#include <type_traits>
+
 #include "common.h"
 #include "criterion.h"
 
@@ -33,6 +35,13 @@ constexpr int kFinStack = 40;    // >= log2(max job rows) + 2
 constexpr int kFinMaxC = 16;     // classes supported by the finisher
 constexpr int kFinTab = 1024;    // LDS x*log2(x) entries
 constexpr int kFinUnroll = 4;    // row gathers in flight per lane
+constexpr int kFinMaxF = 256;    // features (the LDS histogram bounds F far lower)
+constexpr int kFinPair = 2;      // features scanned together per wave (latency hiding)
+constexpr int kFinChunk = 16;    // features per wave whose per-lane minima stay in registers
+
+// Histogram row stride in words: >= B*W + 1 (the odd word staggers features over
+// LDS banks for the atomics), rounded to 4 so each feature row is 16-B aligned.
+__host__ __device__ inline int fin_fstride(int B, int W) { return ((B * W + 1) + 3) & ~3; }
 
 struct FinRowLab {
   uint32_t mask;
@@ -41,18 +50,27 @@ struct FinRowLab {
 
 // jobs: int64 [J][5 + C] = {start, count, depth, base, buffer, counts[C]}
 // node_i32: [slots][6] = {feature, bin, left, right, depth, n}; node_cnt: [slots][C]
-template <typename CodeT>
+
+template <typename CodeT, bool kC2>
 __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
     const uint32_t* __restrict__ codes_rm, int64_t row_words, const CodeT* __restrict__ codes_fm,
     int64_t n_rows, uint32_t* __restrict__ buf0, uint32_t* __restrict__ buf1,
     const int32_t* __restrict__ y, FinRowLab rl, const int64_t* __restrict__ jobs, int J,
     int32_t* __restrict__ job_counter, const int32_t* __restrict__ nbins, int F, int B, int C,
     int crit, int max_depth, int64_t mss, int64_t msl, const double* __restrict__ xtab,
-    int xtab_n, int32_t* __restrict__ node_i32, int32_t* __restrict__ node_cnt,
+    const float* __restrict__ xtabf, int xtab_n, int32_t* __restrict__ node_i32, int32_t* __restrict__ node_cnt,
     int32_t* __restrict__ job_root, int32_t* __restrict__ node_counter, int tiny_rows,
-    int64_t* __restrict__ tiny, int32_t* __restrict__ tiny_count) {
+    int64_t* __restrict__ tiny, int32_t* __restrict__ tiny_count, int64_t* __restrict__ prof) {
+  // prof (optional): per workgroup {wall start, wall end, nodes, rows, cycles in
+  // histogram, scan, partition, rest} -- the finisher's own phase profile
   extern __shared__ __align__(16) uint32_t hist[];  // [F][B*W + 1] packed class pairs
+  // x*log2(x) table: fp64 entries (generic path) or, for C <= 2, twice as many
+  // fp32 entries that drive the approximate first pass of the split scan
   __shared__ double s_tab[kFinTab];
+  float* const s_tabf = reinterpret_cast<float*>(s_tab);
+  __shared__ int32_t s_nb[kFinMaxF];
+  __shared__ float s_fmin[kFinMaxF];
+  __shared__ float w_fmin[kFinWaves];
   __shared__ int s_job;
   __shared__ int64_t s_st_start[kFinStack];
   __shared__ int32_t s_st_count[kFinStack], s_st_depth[kFinStack], s_st_id[kFinStack];
@@ -67,26 +85,155 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
   __shared__ int w_feat[kFinWaves], w_bin[kFinWaves];
   __shared__ int s_bf, s_bb;
   __shared__ int s_lc, s_rc;
+  __shared__ int s_cand_total;
+  if (threadIdx.x == 0) s_cand_total = 0;
 
   const int tid = threadIdx.x;
   const int wave = tid >> 6;
   const int lane = lane_id();
   const int W = (C + 1) >> 1;
-  const int fstride = B * W + 1;
+  const int fstride = fin_fstride(B, W);
   constexpr int cpw = 4 / sizeof(CodeT);
   const int words = (F + cpw - 1) / cpw;
-  const int tn = min(kFinTab, xtab_n);
+  const int tn = min(kC2 ? 2 * kFinTab : kFinTab, xtab_n);
   const int JW = 5 + C;
   // 16-B row loads when the row stride allows it; lanes per row = pow2 >= words/vec
   const int vec = (row_words % 4) == 0 ? 4 : 1;
   int lane_shift = 0;
   while ((1 << lane_shift) * vec < words && lane_shift < 6) ++lane_shift;
 
-  for (int i = tid; i < tn; i += kFinThreads) s_tab[i] = xtab[i];
-  for (int e = tid; e < F * fstride; e += kFinThreads) hist[e] = 0u;
+  int64_t pr_nodes = 0, pr_rows = 0, pr_c[5] = {0, 0, 0, 0, 0};
+  const int64_t pr_wall0 = prof ? (int64_t)wall_clock64() : 0;
+  int64_t pr_t = 0;
+  auto mark = [&](int k) {
+    if (prof && tid == 0) {
+      const int64_t t = (int64_t)clock64();
+      pr_c[k] += t - pr_t;
+      pr_t = t;
+    }
+  };
+  if constexpr (kC2) {
+    for (int i = tid; i < tn; i += kFinThreads) s_tabf[i] = xtabf[i];
+  } else {
+    for (int i = tid; i < tn; i += kFinThreads) s_tab[i] = xtab[i];
+  }
+  for (int f = tid; f < F; f += kFinThreads) s_nb[f] = min(B, nbins[f]);
+  const int hist_q = F * fstride / 4;  // uint4 words (fstride is a multiple of 4)
+  uint4* hist4 = reinterpret_cast<uint4*>(hist);
+  for (int e = tid; e < hist_q; e += kFinThreads) hist4[e] = make_uint4(0, 0, 0, 0);
 
   auto tl = [&](uint64_t x) -> double {
+    if constexpr (kC2) return x < (uint64_t)xtab_n ? __ldg(xtab + x) : xlog2x(x);
     return x < (uint64_t)tn ? s_tab[x] : (x < (uint64_t)xtab_n ? __ldg(xtab + x) : xlog2x(x));
+  };
+
+  // ---- C <= 2: both class counts of a bin packed in one 32-bit word (class 0
+  // low half, class 1 high half). Lane l owns bins 4l..4l+3: one 16-B LDS read
+  // and one packed DPP prefix sum give both classes' left counts.
+  auto load_c2 = [&](const uint32_t* h, int nb, uint32_t (&v)[4], uint32_t& excl) {
+    const int b0 = lane * 4;
+    const uint4 hv = b0 < nb ? *reinterpret_cast<const uint4*>(h + b0) : make_uint4(0, 0, 0, 0);
+    v[0] = hv.x;
+    v[1] = hv.y;
+    v[2] = hv.z;
+    v[3] = hv.w;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (b0 + k >= nb) v[k] = 0u;
+    excl = wave_incl_scan_dpp(v[0] + v[1] + v[2] + v[3]) - (v[0] + v[1] + v[2] + v[3]);
+  };
+  // Pass 1 (entropy): the minimum split cost of one feature in fp32 from the
+  // fp32 table, branch-free. |fp32 - exact| <= 12 * 2^-24 * T(m) (six rounded
+  // table values, six roundings of sums bounded by T(m), T superadditive), so
+  // only features whose fp32 minimum lies within 2^-19 * T(m) of the node's
+  // best can hold the exact optimum; pass 2 re-scores just those in fp64.
+  // Processes kFinPair features per call with every table read issued before
+  // the first wait: each feature is a dependent chain (LDS read -> DPP scan ->
+  // lookups -> DPP min), so independent features are what hides the latency.
+  auto scan_c2_f = [&](auto big_tag, int f0, uint32_t t0, uint32_t t1, int m,
+                       float (&out)[kFinPair]) {
+    constexpr bool kBig = decltype(big_tag)::value;
+    auto lk = [&](uint32_t x) -> float {
+      if constexpr (!kBig) {
+        return s_tabf[x];
+      } else {
+        return x < (uint32_t)tn ? s_tabf[x] : __ldg(xtabf + x);
+      }
+    };
+    uint32_t v[kFinPair][4], lp[kFinPair];
+#pragma unroll
+    for (int q = 0; q < kFinPair; ++q) {
+      const int f = f0 + q * kFinWaves;
+      if (f < F) {
+        load_c2(hist + f * fstride, s_nb[f], v[q], lp[q]);
+      } else {
+        v[q][0] = v[q][1] = v[q][2] = v[q][3] = 0u;
+        lp[q] = 0u;
+      }
+    }
+    float tv[kFinPair][4][6];
+    bool ok[kFinPair][4];
+#pragma unroll
+    for (int q = 0; q < kFinPair; ++q) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        lp[q] += v[q][k];
+        const uint32_t l0 = lp[q] & 0xffffu, l1 = lp[q] >> 16;
+        const uint32_t ml = l0 + l1, mr = (uint32_t)m - ml;
+        ok[q][k] = v[q][k] != 0u && (int64_t)ml >= msl && (int64_t)mr >= msl;
+        tv[q][k][0] = lk(ml);
+        tv[q][k][1] = lk(l0);
+        tv[q][k][2] = lk(l1);
+        tv[q][k][3] = lk(mr);
+        tv[q][k][4] = lk(t0 - l0);
+        tv[q][k][5] = lk(t1 - l1);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kFinPair; ++q) {
+      float best = __builtin_inff();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float* t = tv[q][k];
+        const float c = (t[0] - (t[1] + t[2])) + (t[3] - (t[4] + t[5]));
+        best = fminf(best, ok[q][k] ? c : __builtin_inff());
+      }
+      out[q] = best;
+    }
+  };
+  // Exact (fp64, global table) best split of one feature: (cost, lowest bin).
+  auto scan_c2 = [&](const uint32_t* h, int nb, uint32_t t0, uint32_t t1, int m,
+                     double& best_cost, int& best_bin) {
+    auto lk = [&](uint32_t x) -> double { return __ldg(xtab + x); };
+    uint32_t v[4], lp;
+    load_c2(h, nb, v, lp);
+    best_cost = __builtin_inf();
+    best_bin = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      lp += v[k];
+      const uint32_t l0 = lp & 0xffffu, l1 = lp >> 16;
+      const uint32_t r0 = t0 - l0, r1 = t1 - l1;
+      const int64_t ml = (int64_t)(l0 + l1);
+      const int64_t mr = (int64_t)m - ml;
+      if (v[k] != 0u && ml >= msl && mr >= msl) {
+        double cost;
+        if (crit == kEntropy) {
+          const double sl = lk(l0) + lk(l1);
+          const double sr = lk(r0) + lk(r1);
+          cost = (lk((uint32_t)ml) - sl) + (lk((uint32_t)mr) - sr);
+        } else {
+          const int64_t ql = (int64_t)l0 * l0 + (int64_t)l1 * l1;
+          const int64_t qr = (int64_t)r0 * r0 + (int64_t)r1 * r1;
+          cost = gini_term(ml, ql) + gini_term(mr, qr);
+        }
+        if (cost < best_cost) {
+          best_cost = cost;
+          best_bin = lane * 4 + k;
+        }
+      }
+    }
+    wave_argmin_dpp(best_cost, best_bin);
   };
 
   for (;;) {
@@ -94,6 +241,7 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
     __syncthreads();
     const int job = s_job;
     if (job >= J) break;
+    if (prof && tid == 0) pr_t = (int64_t)clock64();
     const int64_t* jb = jobs + (int64_t)job * JW;
     int32_t* ni = node_i32;  // node slots come from one global counter
     int32_t* nc = node_cnt;
@@ -156,6 +304,9 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
       const int m = s_count;
       const int depth = s_depth;
       const int id = s_id;
+      mark(3);
+      pr_nodes += 1;
+      pr_rows += m;
       uint32_t* __restrict__ src = s_buf ? buf1 : buf0;
       uint32_t* __restrict__ dst = s_buf ? buf0 : buf1;
       // ---- histogram of this node's rows (all features): VEC words per lane,
@@ -214,12 +365,86 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
         }
       }
       __syncthreads();
+      mark(0);
       const double pterm = s_pterm;
       // ---- wave-per-feature scan (B <= 256: one 256-bin pass)
       double bg = -__builtin_inf();
       int bfeat = 0x7fffffff, bbin = -1;
+      if constexpr (kC2) {
+        const uint32_t t0 = (uint32_t)s_cnt[0], t1 = C > 1 ? (uint32_t)s_cnt[1] : 0u;
+        bool cand_all = true, one_chunk = false;
+        float thr = 0.0f;
+        float lmin[kFinChunk];
+        uint32_t cand_mask = 0u;
+        if (crit == kEntropy) {
+          // pass 1: per-lane fp32 minima over each feature's bins (no per-feature
+          // wave reduction), one wave minimum, then the node-wide threshold.
+          // Features f = wave + 4 i; chunks of kFinChunk keep the per-lane minima
+          // in registers; past one chunk (F > 64) each feature is reduced to LDS.
+          const bool big = m >= tn;  // wave-uniform: small nodes never leave LDS
+          const int fpw = (F - wave + kFinWaves - 1) / kFinWaves;  // this wave's features
+          one_chunk = F <= kFinWaves * kFinChunk;
+          float wl = __builtin_inff();
+          for (int c0 = 0; c0 < fpw; c0 += kFinChunk) {
+#pragma unroll
+            for (int i = 0; i < kFinChunk; i += kFinPair) {
+              float fm[kFinPair];
+              if (c0 + i < fpw) {
+                const int f = wave + (c0 + i) * kFinWaves;
+                if (big)
+                  scan_c2_f(std::true_type{}, f, t0, t1, m, fm);
+                else
+                  scan_c2_f(std::false_type{}, f, t0, t1, m, fm);
+              }
+#pragma unroll
+              for (int q = 0; q < kFinPair; ++q)
+                lmin[i + q] = c0 + i + q < fpw ? fm[q] : __builtin_inff();
+            }
+#pragma unroll
+            for (int i = 0; i < kFinChunk; ++i) wl = fminf(wl, lmin[i]);
+            if (!one_chunk) {
+              for (int i = 0; i < kFinChunk && c0 + i < fpw; ++i) {
+                const float fm = wave_min_f32_dpp(lmin[i]);
+                if (lane == 0) s_fmin[wave + (c0 + i) * kFinWaves] = fm;
+              }
+            }
+          }
+          const float wmin = wave_min_f32_dpp(wl);
+          if (lane == 0) w_fmin[wave] = wmin;
+          __syncthreads();
+          mark(4);
+          float best = w_fmin[0];
+          for (int w = 1; w < kFinWaves; ++w) best = fminf(best, w_fmin[w]);
+          const float tm = m < tn ? s_tabf[m] : __ldg(xtabf + m);
+          thr = best + tm * 0x1p-19f + 0x1p-20f;
+          cand_all = false;
+          if (one_chunk) {
+#pragma unroll
+            for (int i = 0; i < kFinChunk; ++i)
+              if (__ballot(lmin[i] <= thr)) cand_mask |= 1u << i;
+          }
+        }
+        // pass 2: exact scores for candidate features only
+        for (int i = 0, f = wave; f < F; ++i, f += kFinWaves) {
+          if (!cand_all) {
+            if (one_chunk ? !((cand_mask >> i) & 1u) : !(s_fmin[f] <= thr)) continue;
+          }
+          if (prof && lane == 0) atomicAdd(&s_cand_total, 1);
+          double best_cost;
+          int best_bin;
+          scan_c2(hist + f * fstride, s_nb[f], t0, t1, m, best_cost, best_bin);
+          if (best_cost < __builtin_inf()) {
+            const double g = pterm - best_cost;
+            if (g > bg) {  // features visited in increasing order: strict > keeps the lowest
+              bg = g;
+              bfeat = f;
+              bbin = best_bin;
+            }
+          }
+        }
+      } else
       for (int f = wave; f < F; f += kFinWaves) {
-        const int nb = min(B, nbins[f]);
+        const int nb = s_nb[f];
         const uint32_t* h = hist + f * fstride;
         double best_cost = __builtin_inf();
         int best_bin = 0x7fffffff;
@@ -298,6 +523,7 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
         w_bin[wave] = bbin;
       }
       __syncthreads();
+      mark(1);
       int bf, bb;
       {
         double g = w_gain[0];
@@ -365,8 +591,9 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
         }
       }
       __syncthreads();
+      mark(2);
       // ---- clear the histogram for the next node (all scan reads are done)
-      for (int e = tid; e < F * fstride; e += kFinThreads) hist[e] = 0u;
+      for (int e = tid; e < hist_q; e += kFinThreads) hist4[e] = make_uint4(0, 0, 0, 0);
       // ---- children
       if (tid == 0 && bf >= 0) {
         const int nl = s_lc;
@@ -420,6 +647,16 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
       }
       __syncthreads();
     }
+    mark(3);
+  }
+  if (prof && tid == 0) {
+    int64_t* P = prof + (int64_t)blockIdx.x * 10;
+    P[0] = pr_wall0;
+    P[1] = (int64_t)wall_clock64();
+    P[2] = pr_nodes;
+    P[3] = pr_rows;
+    for (int k = 0; k < 5; ++k) P[4 + k] = pr_c[k];
+    P[9] = s_cand_total;
   }
 }
 
@@ -523,9 +760,9 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
       }
       const double pterm = crit == kEntropy ? s_tab[mm] - acc : gini_term(mm, sq);
       const bool inm = (M >> lane) & 1ull;
-      double bg = -__builtin_inf();
-      int bf = -1;
-      uint32_t bb = 0;
+      double bg = -__builtin_inf(), bc = __builtin_inf();
+      int bf = 0x7fffffff;
+      uint32_t bb = 0xffffffffu;
       for (int f = 0; f < F; ++f) {
         const uint32_t code = my_bytes[f];
         // lanes of M whose code is greater than / equal to mine (radix rank, MSB first)
@@ -570,18 +807,37 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
             cost = gini_term(ml, ql) + gini_term(mr, qr);
           }
         }
-        const double cmin = wave_min_f64_dpp(cost);
-        if (cmin < __builtin_inf()) {
-          const uint32_t bcode = wave_min_u32_dpp(cost == cmin ? code : 0xffffffffu);
-          const double g = pterm - cmin;
-          if (g > bg) {  // features in increasing order: strict > keeps the lowest
-            bg = g;
-            bf = f;
-            bb = bcode;
-          }
+        // per-lane running best; features ascend, so strict > keeps the lowest
+        const double g = pterm - cost;
+        if (g > bg) {
+          bg = g;
+          bf = f;
+          bc = cost;
+          bb = code;
         }
       }
-      if (bf < 0) continue;  // leaf: the record written at creation stands
+      // one wave reduction per node: max gain, then lowest feature, then lowest
+      // cost, then lowest code -- the same choice as reducing every feature
+      // separately (min cost, min code) and keeping the first strictly better gain
+#pragma unroll
+      for (int d = kWave / 2; d > 0; d >>= 1) {
+        const double og = __shfl_xor(bg, d, kWave);
+        const int of = __shfl_xor(bf, d, kWave);
+        const double oc = __shfl_xor(bc, d, kWave);
+        const uint32_t ob = (uint32_t)__shfl_xor((int)bb, d, kWave);
+        const bool take =
+            og > bg ||
+            (og == bg && (of < bf || (of == bf && (oc < bc || (oc == bc && ob < bb)))));
+        if (take) {
+          bg = og;
+          bf = of;
+          bc = oc;
+          bb = ob;
+        }
+      }
+      bf = __builtin_amdgcn_readfirstlane(bf);
+      bb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bb);
+      if (!(bg > -__builtin_inf()) || bf < 0) continue;  // leaf: the creation record stands
       const unsigned long long LM = M & __ballot((uint32_t)my_bytes[bf] <= bb);
       const unsigned long long RM = M & ~LM;
       int alloc = 0;
@@ -634,36 +890,46 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
   }
 }
 
-int finish_lds_bytes(int F, int B, int C) { return F * (B * ((C + 1) / 2) + 1) * 4; }
+int finish_lds_bytes(int F, int B, int C) { return F * fin_fstride(B, (C + 1) / 2) * 4; }
 int finish_max_classes() { return kFinMaxC; }
 
 void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                    const void* codes_fm, int code_bytes, int64_t n_rows, uint32_t* buf0,
                    uint32_t* buf1, const int32_t* y, int lab_shift, const int64_t* jobs, int J,
                    int32_t* counter, const int32_t* nbins, int F, int B, int C, int crit,
-                   int max_depth, int64_t mss, int64_t msl, const double* xtab, int xtab_n,
+                   int max_depth, int64_t mss, int64_t msl, const double* xtab,
+                   const float* xtabf, int xtab_n,
                    int32_t* node_i32, int32_t* node_cnt, int32_t* job_root, int grid,
-                   int tiny_rows, int64_t* tiny, int tiny_grid) {
+                   int tiny_rows, int64_t* tiny, int tiny_grid, int64_t* prof) {
   // counter: int32 [4] = {job cursor, tiny count, tiny cursor, node count}, zeroed by
   // the host; node slots are handed out by the last one (compact output)
   if (J <= 0) return;
   if (C > kFinMaxC) throw std::runtime_error("finisher supports at most 16 classes");
+  if (F > kFinMaxF) throw std::runtime_error("finisher supports at most 256 features");
   if (code_bytes != 1 || F > kTinyMaxF || tiny == nullptr) tiny_rows = 0;
   tiny_rows = std::min(tiny_rows, kTinyRows);
   FinRowLab rl{lab_shift ? ((1u << lab_shift) - 1u) : 0xffffffffu, lab_shift};
   const size_t lds = (size_t)finish_lds_bytes(F, B, C);
-#define MT_FIN(CT)                                                                            \
-  MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_cls_kernel<CT>,                        \
+#define MT_FIN(CT, C2)                                                                        \
+  MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_cls_kernel<CT, C2>,                    \
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));    \
-  hipLaunchKernelGGL(finish_cls_kernel<CT>, dim3(grid), dim3(kFinThreads), lds, stream,       \
+  hipLaunchKernelGGL((finish_cls_kernel<CT, C2>), dim3(grid), dim3(kFinThreads), lds, stream, \
                      (const uint32_t*)codes_rm, row_words, (const CT*)codes_fm, n_rows, buf0, \
                      buf1, y, rl, jobs, J, counter, nbins, F, B, C, crit, max_depth, mss,     \
-                     msl, xtab, xtab_n, node_i32, node_cnt, job_root, counter + 3, tiny_rows, \
-                     tiny, counter + 1);
+                     msl, xtab, xtabf, xtab_n, node_i32, node_cnt, job_root, counter + 3, tiny_rows, \
+                     tiny, counter + 1, prof);
   if (code_bytes == 1) {
-    MT_FIN(uint8_t)
+    if (C <= 2) {
+      MT_FIN(uint8_t, true)
+    } else {
+      MT_FIN(uint8_t, false)
+    }
   } else {
-    MT_FIN(uint16_t)
+    if (C <= 2) {
+      MT_FIN(uint16_t, true)
+    } else {
+      MT_FIN(uint16_t, false)
+    }
   }
 #undef MT_FIN
   MT_HIP_CHECK(hipGetLastError());

@@ -182,6 +182,16 @@ def xlog2x_table(device) -> torch.Tensor:
     return t
 
 
+def xlog2x_table_f32(device) -> torch.Tensor:
+    """fp32 rounding of :func:`xlog2x_table` (the finisher's approximate pass)."""
+    key = "f32:" + str(device)
+    t = _xtab_cache.get(key)
+    if t is None:
+        t = xlog2x_table(device).float()
+        _xtab_cache[key] = t
+    return t
+
+
 class HipBackend:
     """Device state and kernel launches for one fit on the current GPU."""
 
@@ -216,6 +226,7 @@ class HipBackend:
                           self.y.data_ptr() if not self.reg else 0, self.lab_shift, self.n)
         self.tmp = torch.empty_like(self.idx)
         self.xtab = xlog2x_table(self.device)
+        self.xtabf = xlog2x_table_f32(self.device)
 
     def hist_elems(self, F_h: int) -> int:
         return F_h * self.B * (2 if self.reg else self.C)
@@ -340,7 +351,10 @@ class HipBackend:
     def finisher_supported(self) -> bool:
         if self.reg or self.cb != 1 or self.C > 16 or self.B > 256:
             return False
-        return self.F * (self.B * ((self.C + 1) // 2) + 1) * 4 <= 150 * 1024
+        return self.hip.finish_lds_bytes(self.F, self.B, self.C) <= 150 * 1024 and self.F <= 256
+
+    # finisher jobs index the x*log2(x) table with row counts: keep them below it
+    max_finisher_rows = XTAB_N - 1
 
     def finish_subtrees(self, starts, counts, depths, params, stats=None):
         """Grow every job's subtree on the device; one compact node table out.
@@ -372,14 +386,21 @@ class HipBackend:
         tiny = torch.empty((tiny_cap, 8), dtype=torch.int64, device=self.device)
         md = -1 if params.max_depth is None else int(params.max_depth)
         grid = int(min(J, 2 * N_CU))
+        prof = None
+        if os.environ.get("MPITREE_FIN_PROF"):
+            prof = torch.zeros((grid, 10), dtype=torch.int64, device=self.device)
         self.hip.finish(_stream(), self.codes_rm.data_ptr(), self.row_elems * self.cb // 4,
                         self.codes_fm.data_ptr(), self.cb, self.n, self.idx.data_ptr(),
                         self.tmp.data_ptr(), self.y.data_ptr(), self.lab_shift, d_jobs.data_ptr(),
                         J, counter.data_ptr(), self.nbins.data_ptr(), self.F, self.B, C,
                         int(self.crit), md, int(params.min_samples_split),
-                        int(max(1, params.min_samples_leaf)), self.xtab.data_ptr(), XTAB_N,
+                        int(max(1, params.min_samples_leaf)), self.xtab.data_ptr(),
+                        self.xtabf.data_ptr(), XTAB_N,
                         node_i32.data_ptr(), node_cnt.data_ptr(), job_root.data_ptr(), grid,
-                        tiny_rows, tiny.data_ptr(), 4 * N_CU)
+                        tiny_rows, tiny.data_ptr(), 4 * N_CU,
+                        0 if prof is None else prof.data_ptr())
+        if prof is not None:
+            self.last_finisher_prof = prof.cpu().numpy()
         N = int(counter[3].item())
         ni = node_i32[:N].cpu().numpy()
         nc = node_cnt[:N].cpu().numpy()
