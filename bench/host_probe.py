@@ -15,6 +15,7 @@ orig = lw.LevelwiseBuilder._to_arrays
 def spy(self, tab):
     cap["tab"] = tab
     cap["edges"] = self._edges
+    cap["fin"] = self._fin
     return orig(self, tab)
 
 
@@ -27,18 +28,16 @@ torch.cuda.synchronize()
 tab = cap["tab"]
 n = tab.n
 cpu = native.cpu()
-args = (tab.feature[:n], tab.tbin[:n], tab.left[:n], tab.right[:n], tab.nsamp[:n], tab.stats[:n], 0)
-for label, kw in (("plain", ()), ("thr+term", (cap["edges"], 0))):
+fin, cnt, did, roots = cap["fin"]
+fin = np.array(fin); cnt = np.array(cnt)
+print("affinity cpus:", len(os.sched_getaffinity(0)), "host_threads:", native.host_threads())
+for nt in (1, 4, 8, 16):
     ts = []
     for _ in range(5):
         t = time.perf_counter()
-        cpu.assemble(*args, *kw)
+        a = cpu.assemble_tree(tab.feature[:n], tab.tbin[:n], tab.left[:n], tab.right[:n],
+                              tab.nsamp[:n], tab.stats[:n], fin, cnt, did, roots, cap["edges"], 0, nt)
         ts.append(time.perf_counter() - t)
-    print(f"assemble[{label}] n={n}: " + " ".join(f"{v*1e3:.2f}" for v in ts), flush=True)
-ts = []
-for _ in range(5):
-    t = time.perf_counter()
-    a = np.empty((n, 8), np.int64); a.fill(0)
-    ts.append(time.perf_counter() - t)
-print("first-touch 8 cols:", " ".join(f"{v*1e3:.2f}" for v in ts))
+    print(f"assemble_tree threads={nt} n1={n} T={len(fin)}: total " + " ".join(f"{v*1e3:.2f}" for v in ts)
+          + f" | order {a['ms_order']:.2f} scatter {a['ms_scatter']:.2f}", flush=True)
 print({k: round(v * 1e3, 3) for k, v in r.timings.items()})

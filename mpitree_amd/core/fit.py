@@ -148,6 +148,8 @@ def _encode_targets(y, n):
 
 
 def _finalize(ta: TreeArrays, mapper: BinMapper, regression: bool, y_exp: int) -> TreeArrays:
+    if ta.meta.pop("final", False):  # device assembly produced finished columns
+        return ta
     if not ta.meta.pop("thresholds_set", False):
         ta.with_thresholds(mapper.edges)
     m = ta.n_samples.astype(np.float64)
@@ -236,7 +238,7 @@ def fit_tree(
         finisher_rows = min(int(finisher_rows), be.max_finisher_rows)
         params.finisher_rows = int(finisher_rows)
         builder = LevelwiseBuilder(be, params, comm)
-        ta = builder.fit(hi - lo, C, F, edges=mapper.padded_edges())
+        ta = builder.fit(hi - lo, C, F, edges=mapper.padded_edges(), y_exp=y_exp)
         eng = "hip-levelwise"
         timings.update(builder.timings)
         stats = dict(builder.stats)

@@ -27,6 +27,7 @@ level's nodes.
 
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass
 
@@ -98,12 +99,13 @@ class _Table:
         self.depth = np.zeros(self.cap, np.int32)
         self.nsamp = np.zeros(self.cap, np.int64)
         self.stats = np.zeros((self.cap, C), np.int64)
+        self.pos = np.zeros(self.cap, np.int64)  # pre-order position (with holes)
 
     def _grow(self, need):
         if need <= self.cap:
             return
         cap = max(need, 2 * self.cap)
-        for name in ("feature", "tbin", "left", "right", "depth", "nsamp", "stats"):
+        for name in ("feature", "tbin", "left", "right", "depth", "nsamp", "stats", "pos"):
             a = getattr(self, name)
             fill = -1 if name in ("feature", "tbin", "left", "right") else 0
             b = np.full((cap,) + a.shape[1:], fill, a.dtype)
@@ -111,11 +113,13 @@ class _Table:
             setattr(self, name, b)
         self.cap = cap
 
-    def add(self, depth, nsamp, stats) -> np.ndarray:
+    def add(self, depth, nsamp, stats, pos=None) -> np.ndarray:
         depth = np.atleast_1d(np.asarray(depth))
         k = depth.shape[0]
         self._grow(self.n + k)
         lo = self.n
+        if pos is not None:
+            self.pos[lo : lo + k] = pos
         self.depth[lo : lo + k] = depth
         self.nsamp[lo : lo + k] = nsamp
         self.stats[lo : lo + k] = np.asarray(stats, dtype=np.int64).reshape(k, self.C)
@@ -136,6 +140,21 @@ def _node_terms(crit, stats: np.ndarray) -> np.ndarray:
     if crit == Criterion.GINI:
         return gini_term(stats)
     return mse_term(stats[:, 0], stats[:, 1])
+
+
+def _native_cpu():
+    try:
+        from ..ops import native
+
+        return native.cpu()
+    except ImportError:
+        return None
+
+
+def _host_threads() -> int:
+    from ..ops import native
+
+    return native.host_threads()
 
 
 class LevelwiseBuilder:
@@ -168,9 +187,13 @@ class LevelwiseBuilder:
         self.timings[key] = self.timings.get(key, 0.0) + time.perf_counter() - t0
 
     # ---------------------------------------------------------------- fit
-    def fit(self, n_local: int, n_classes: int, n_features: int, edges=None) -> TreeArrays:
-        """Grow the tree; ``edges`` ([F, B] padded bin edges) fills thresholds."""
+    def fit(self, n_local: int, n_classes: int, n_features: int, edges=None,
+            y_exp: int = 0) -> TreeArrays:
+        """Grow the tree; ``edges`` ([F, B] padded bin edges) fills thresholds,
+        ``y_exp`` is the regression targets' fixed-point exponent."""
         self._edges = edges
+        self._y_exp = int(y_exp)
+        self._fin = None
         p, be, comm = self.p, self.be, self.comm
         reg = p.criterion == Criterion.SQUARED_ERROR
         C = 2 if reg else n_classes
@@ -185,10 +208,20 @@ class LevelwiseBuilder:
             m_root, rstats, minmax = int(st[0, 0]), st[:, :2], st[:, 2:4]
         else:
             m_root, rstats, minmax = int(st[0].sum()), st, None
-        root = tab.add(0, m_root, rstats)
+        root = tab.add(0, m_root, rstats, pos=0)
+        # Device assembly: every node lives at its pre-order position with holes
+        # (a subtree of m rows owns 2m - 1 positions: root, left, right), so the
+        # backend lays the tree out on the device and compacts it in one pass.
+        self._device_asm = (
+            hasattr(be, "begin_positions") and comm.world_size == 1 and edges is not None
+            and os.environ.get("MPITREE_DEVICE_ASSEMBLY", "1") != "0"
+        )
+        if self._device_asm:
+            be.begin_positions(2 * m_root - 1)
         # frontier columns
         fr = dict(
             id=root,
+            pos=np.zeros(1, np.int64),
             start=np.zeros(1, np.int64),
             count=np.array([n_local], np.int64),
             m=np.array([m_root], np.int64),
@@ -198,7 +231,7 @@ class LevelwiseBuilder:
         )
         if self._terminal(np.zeros(1), np.array([m_root]), rstats, minmax)[0]:
             fr = {k: v[:0] for k, v in fr.items()}
-        deferred = {k: [] for k in ("id", "start", "count", "m", "depth")}
+        deferred = {k: [] for k in ("id", "start", "count", "m", "depth", "pos")}
         prev_hist = None
         levels = 0
         while fr["id"].size:
@@ -272,7 +305,9 @@ class LevelwiseBuilder:
             cstart = np.stack([o["start"][split], o["start"][split] + nl_local], 1).reshape(-1)
             ccount = np.stack([nl_local, o["count"][split] - nl_local], 1).reshape(-1)
             cdepth = np.repeat(o["depth"][split] + 1, 2)
-            cids = tab.add(cdepth, cm, cstats)
+            ppos = o["pos"][split]
+            cpos = np.stack([ppos + 1, ppos + 2 * ml], 1).reshape(-1)
+            cids = tab.add(cdepth, cm, cstats, pos=cpos)
             tab.left[ids] = cids[0::2]
             tab.right[ids] = cids[1::2]
             mm = None
@@ -295,6 +330,7 @@ class LevelwiseBuilder:
             sib[2 * both + big[both]] = new_pos[2 * both + 1 - big[both]]
             fr = dict(
                 id=cids[keep_idx],
+                pos=cpos[keep_idx],
                 start=cstart[keep_idx],
                 count=ccount[keep_idx],
                 m=cm[keep_idx],
@@ -319,6 +355,13 @@ class LevelwiseBuilder:
     def _finish(self, tab: _Table, d: dict):
         """Grow each deferred subtree with the backend's subtree finisher."""
         comm = self.comm
+        if self._device_asm:  # nodes stay in the device position space
+            t0 = time.perf_counter()
+            self.be.finish_subtrees(d["start"], d["count"], d["depth"], self.p,
+                                    stats=tab.stats[d["id"]], positions=d["pos"])
+            self.timings["finisher_device"] = time.perf_counter() - t0
+            self._deferred_ids = np.asarray(d["id"], np.int64)
+            return
         owned = comm.finish_assignment(d["m"])
         t0 = time.perf_counter()
         local = self.be.finish_subtrees(d["start"][owned], d["count"][owned], d["depth"][owned],
@@ -334,6 +377,17 @@ class LevelwiseBuilder:
         # tree is re-numbered).
         T = len(t["feature"])
         if T == 0:
+            return
+        if _native_cpu() is not None:  # joined and renumbered natively in _to_arrays
+            fin = t.get("i32")
+            if fin is None:
+                fin = np.stack([t["feature"], t["bin"], t["left"], t["right"], t["depth"],
+                                t["nsamp"]], 1).astype(np.int32)
+            cnt = t.get("cnt")
+            if cnt is None:
+                cnt = np.asarray(t["stats"], np.int64)
+            self._fin = (fin, cnt, np.asarray(d["id"], np.int64),
+                         np.asarray(t["roots"], np.int64))
             return
         base = tab.n
         tab.add(t["depth"], t["nsamp"], t["stats"])
@@ -354,21 +408,51 @@ class LevelwiseBuilder:
         tab.right[did] = tab.right[r]
 
     # -------------------------------------------------------------- output
+    def _to_arrays_device(self, tab: _Table, reg: bool) -> TreeArrays:
+        """Level-wise nodes join the finisher's in the device position space,
+        which the backend compacts into finished pre-ordered columns."""
+        n = tab.n
+        keep = np.ones(n, bool)
+        did = getattr(self, "_deferred_ids", None)
+        if did is not None and did.size:
+            keep[did] = False  # the finisher wrote these (with their splits)
+        ids = np.nonzero(keep)[0]
+        f = tab.feature[ids]
+        inner = f >= 0
+        lpos = np.where(inner, tab.pos[np.maximum(tab.left[ids], 0)], -1)
+        rpos = np.where(inner, tab.pos[np.maximum(tab.right[ids], 0)], -1)
+        self.be.put_positions(tab.pos[ids], f, tab.tbin[ids], lpos, rpos, tab.depth[ids],
+                              tab.nsamp[ids], tab.stats[ids])
+        a = self.be.assemble_positions(self._edges, int(self.p.criterion), self._y_exp)
+        st = a["stats"]
+        ta = TreeArrays(
+            feature=a["feature"], threshold=a["threshold"], threshold_bin=a["bin"],
+            left=a["left"], right=a["right"], depth=a["depth"], n_samples=a["nsamp"],
+            impurity=a["impurity"], count=None if reg else st,
+            value=a["value"] if reg else None,
+        )
+        ta.meta["term"] = a["term"]
+        if reg:
+            ta.meta["sum_fixed"] = st[:, 1]
+        ta.meta["final"] = True  # thresholds, impurity and values are filled in
+        return ta
+
     def _to_arrays(self, tab: _Table) -> TreeArrays:
         reg = self.p.criterion == Criterion.SQUARED_ERROR
         n = tab.n
-        try:
-            from ..ops import native
-
-            cpu = native.cpu()
-        except ImportError:
-            cpu = None
-        if cpu is not None:  # one native pass: pre-order, gather, thresholds, terms
+        if self._device_asm:
+            return self._to_arrays_device(tab, reg)
+        cpu = _native_cpu()
+        if cpu is not None:  # one native pass: join, pre-order, gather, thresholds, terms
             edges = self._edges
-            a = cpu.assemble(tab.feature[:n], tab.tbin[:n], tab.left[:n], tab.right[:n],
-                             tab.nsamp[:n], tab.stats[:n], 0,
-                             np.empty((0, 0)) if edges is None else edges,
-                             int(self.p.criterion))
+            C = tab.stats.shape[1]
+            fin, cnt, did, roots = self._fin or (np.zeros((0, 6), np.int32),
+                                                 np.zeros((0, C), np.int64),
+                                                 np.zeros(0, np.int64), np.zeros(0, np.int64))
+            a = cpu.assemble_tree(tab.feature[:n], tab.tbin[:n], tab.left[:n], tab.right[:n],
+                                  tab.nsamp[:n], tab.stats[:n], fin, cnt, did, roots,
+                                  np.empty((0, 0)) if edges is None else edges,
+                                  int(self.p.criterion), _host_threads())
             st = a["stats"]
             ta = TreeArrays(
                 feature=a["feature"], threshold=a.get("threshold", np.full(len(st), np.nan)),

@@ -65,9 +65,11 @@ class TreeArrays:
             return False
         if self.count is not None and not np.array_equal(self.count, other.count):
             return False
-        if self.value is not None and not np.array_equal(self.value, other.value):
+        if (self.value is None) != (other.value is None):
             return False
-        if check_impurity and not np.array_equal(self.impurity, other.impurity):
+        if self.value is not None and not np.array_equal(self.value, other.value, equal_nan=True):
+            return False
+        if check_impurity and not np.array_equal(self.impurity, other.impurity, equal_nan=True):
             return False
         return True
 

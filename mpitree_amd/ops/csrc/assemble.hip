@@ -1,0 +1,206 @@
+// Device tree assembly: pre-order position space -> compact tree arrays.
+//
+// The reference builds a linked Node graph while it recurses
+// (mpitree/tree/decision_tree.py:93-166) and its parallel fit pickles and
+// allgathers whole subtrees (:446-477). Here a fit writes every node at its
+// *pre-order position with holes*: a subtree of r rows owns 2r - 1 positions,
+// the root first, then the left subtree (2 n_left - 1 positions), then the right.
+// The level-wise host loop and both finisher kernels only ever need a node's
+// own position and its children's row counts, so the whole tree is laid out
+// without a global counter. This file removes the holes:
+//
+//   count_kernel   per 4096-position tile: number of written nodes (n > 0)
+//   offsets_kernel one workgroup: exclusive scan of the tile counts
+//   rank_kernel    per tile: each written position's final node id
+//   emit_kernel    per written position: the final row of every output column,
+//                  child links through the rank table, split thresholds from
+//                  the padded bin-edge table, node terms / impurity / leaf value
+//                  with the same integer-form criterion as every other builder
+//
+// so the host receives finished, pre-ordered columns in one pinned copy.
+#include "common.h"
+#include "criterion.h"
+
+namespace mt {
+
+constexpr int kAsmThreads = 256;
+constexpr int kAsmPer = 16;                        // positions per thread
+constexpr int kAsmTile = kAsmThreads * kAsmPer;    // positions per tile
+
+// rec: int32 [P][6] = {feature (-1 leaf), bin, left pos, right pos, depth, n}; n == 0
+// marks a position no node was written to.
+__global__ __launch_bounds__(kAsmThreads) void asm_count_kernel(const int32_t* __restrict__ rec,
+                                                                int64_t P,
+                                                                int32_t* __restrict__ tile_cnt) {
+  const int64_t base = (int64_t)blockIdx.x * kAsmTile;
+  int c = 0;
+  for (int k = 0; k < kAsmPer; ++k) {
+    const int64_t p = base + (int64_t)k * kAsmThreads + threadIdx.x;  // coalesced
+    c += (p < P && rec[p * 6 + 5] > 0) ? 1 : 0;
+  }
+  c = (int)wave_sum_u32((uint32_t)c);
+  __shared__ int w[kAsmThreads / kWave];
+  if (lane_id() == 0) w[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int i = 0; i < kAsmThreads / kWave; ++i) t += w[i];
+    tile_cnt[blockIdx.x] = t;
+  }
+}
+
+// Exclusive scan of tile counts in place (one workgroup; tiles = P / 4096, a few
+// thousand at most); total written to *total.
+__global__ __launch_bounds__(kAsmThreads) void asm_offsets_kernel(int32_t* __restrict__ tile,
+                                                                  int n_tiles,
+                                                                  int64_t* __restrict__ total) {
+  __shared__ int s_carry;
+  __shared__ int w[kAsmThreads / kWave];
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (int b = 0; b < n_tiles; b += kAsmThreads) {
+    const int i = b + threadIdx.x;
+    const int v = i < n_tiles ? tile[i] : 0;
+    const int incl = (int)wave_incl_scan_u32((uint32_t)v);
+    if (lane_id() == kWave - 1) w[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    int off = s_carry;
+    for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) off += w[k];
+    if (i < n_tiles) tile[i] = off + incl - v;
+    __syncthreads();
+    if (threadIdx.x == kAsmThreads - 1) s_carry = off + incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total = s_carry;
+}
+
+// Final node id of every written position (positions no node occupies get -1).
+__global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __restrict__ rec,
+                                                               int64_t P,
+                                                               const int32_t* __restrict__ tile_off,
+                                                               int32_t* __restrict__ rank) {
+  // thread t owns kAsmPer consecutive positions so the in-tile order is preserved
+  const int64_t base = (int64_t)blockIdx.x * kAsmTile + (int64_t)threadIdx.x * kAsmPer;
+  uint32_t flags = 0;
+  int c = 0;
+  for (int k = 0; k < kAsmPer; ++k) {
+    const int64_t p = base + k;
+    const bool v = p < P && rec[p * 6 + 5] > 0;
+    flags |= (uint32_t)v << k;
+    c += v;
+  }
+  const int incl = (int)wave_incl_scan_u32((uint32_t)c);
+  __shared__ int w[kAsmThreads / kWave];
+  if (lane_id() == kWave - 1) w[threadIdx.x >> 6] = incl;
+  __syncthreads();
+  int off = tile_off[blockIdx.x];
+  for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) off += w[k];
+  int r = off + incl - c;
+  for (int k = 0; k < kAsmPer; ++k) {
+    const int64_t p = base + k;
+    if (p >= P) break;
+    rank[p] = ((flags >> k) & 1u) ? r++ : -1;
+  }
+}
+
+struct AsmOut {
+  int32_t* feature;   // [N]
+  int32_t* bin;       // [N]
+  int32_t* left;      // [N]
+  int32_t* right;     // [N]
+  int32_t* depth;     // [N]
+  int64_t* nsamp;     // [N]
+  int64_t* stats;     // [N][C]
+  double* threshold;  // [N]
+  double* term;       // [N]
+  double* impurity;   // [N]
+  double* value;      // [N] (regression) or null
+};
+
+// StatT: int32 class counts (classification) or int64 {count, fixed-point sum}.
+template <typename StatT>
+__global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
+    const int32_t* __restrict__ rec, const StatT* __restrict__ st, int64_t P, int C,
+    const int32_t* __restrict__ rank, const double* __restrict__ edges, int EB,
+    const double* __restrict__ xtab, int xtab_n, int crit, int y_exp, AsmOut o) {
+  const int64_t p = (int64_t)blockIdx.x * kAsmThreads + threadIdx.x;
+  if (p >= P) return;
+  const int j = rank[p];
+  if (j < 0) return;
+  const int32_t* R = rec + p * 6;
+  const int f = R[0];
+  const int b = R[1];
+  const int64_t n = R[5];
+  o.feature[j] = f >= 0 ? f : -1;
+  o.depth[j] = R[4];
+  o.nsamp[j] = n;
+  if (f >= 0) {
+    o.bin[j] = b;
+    o.left[j] = rank[R[2]];
+    o.right[j] = rank[R[3]];
+    o.threshold[j] = edges[(int64_t)f * EB + b];
+  } else {
+    o.bin[j] = -1;
+    o.left[j] = -1;
+    o.right[j] = -1;
+    o.threshold[j] = __builtin_nan("");
+  }
+  auto T = [&](int64_t x) -> double {
+    return x < (int64_t)xtab_n ? xtab[x] : xlog2x((uint64_t)x);
+  };
+  const StatT* s = st + p * C;
+  double term;
+  if (crit == kSquaredError) {
+    const int64_t cnt = (int64_t)s[0], sum = (int64_t)s[1];
+    o.stats[(int64_t)j * C + 0] = cnt;
+    o.stats[(int64_t)j * C + 1] = sum;
+    term = mse_term(cnt, sum);
+    o.impurity[j] = __builtin_nan("");
+    if (o.value) o.value[j] = ldexp((double)sum / (double)(n > 1 ? n : 1), -y_exp);
+  } else {
+    double acc = 0.0;
+    int64_t m = 0, sq = 0;
+    for (int c = 0; c < C; ++c) {
+      const int64_t v = (int64_t)s[c];
+      o.stats[(int64_t)j * C + c] = v;
+      acc = acc + T(v);
+      m += v;
+      sq += v * v;
+    }
+    term = crit == kEntropy ? T(m) - acc : gini_term(m, sq);
+    o.impurity[j] = n > 0 ? term / (double)n : 0.0;
+  }
+  o.term[j] = term;
+}
+
+void launch_asm_rank(hipStream_t stream, const int32_t* rec, int64_t P, int32_t* tile,
+                     int64_t* total, int32_t* rank) {
+  const int n_tiles = (int)((P + kAsmTile - 1) / kAsmTile);
+  if (n_tiles == 0) return;
+  hipLaunchKernelGGL(asm_count_kernel, dim3(n_tiles), dim3(kAsmThreads), 0, stream, rec, P, tile);
+  hipLaunchKernelGGL(asm_offsets_kernel, dim3(1), dim3(kAsmThreads), 0, stream, tile, n_tiles,
+                     total);
+  hipLaunchKernelGGL(asm_rank_kernel, dim3(n_tiles), dim3(kAsmThreads), 0, stream, rec, P, tile,
+                     rank);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+int asm_tiles(int64_t P) { return (int)((P + kAsmTile - 1) / kAsmTile); }
+
+void launch_asm_emit(hipStream_t stream, const int32_t* rec, const void* st, bool st64,
+                     int64_t P, int C, const int32_t* rank, const double* edges, int EB,
+                     const double* xtab, int xtab_n, int crit, int y_exp, const AsmOut& o) {
+  const int64_t blocks = (P + kAsmThreads - 1) / kAsmThreads;
+  if (blocks == 0) return;
+  if (st64)
+    hipLaunchKernelGGL(asm_emit_kernel<int64_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
+                       stream, rec, (const int64_t*)st, P, C, rank, edges, EB, xtab, xtab_n, crit,
+                       y_exp, o);
+  else
+    hipLaunchKernelGGL(asm_emit_kernel<int32_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
+                       stream, rec, (const int32_t*)st, P, C, rank, edges, EB, xtab, xtab_n, crit,
+                       y_exp, o);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace mt

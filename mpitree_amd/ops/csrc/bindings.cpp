@@ -38,6 +38,24 @@ void launch_finish(hipStream_t, const void*, int64_t, const void*, int, int64_t,
                    int32_t*,
                    int32_t*, int32_t*, int, int, int64_t*, int, int64_t*);
 int finish_lds_bytes(int F, int B, int C);
+struct AsmOut {
+  int32_t* feature;
+  int32_t* bin;
+  int32_t* left;
+  int32_t* right;
+  int32_t* depth;
+  int64_t* nsamp;
+  int64_t* stats;
+  double* threshold;
+  double* term;
+  double* impurity;
+  double* value;
+};
+int asm_tiles(int64_t P);
+void launch_asm_rank(hipStream_t, const int32_t*, int64_t, int32_t*, int64_t*, int32_t*);
+void launch_asm_emit(hipStream_t, const int32_t*, const void*, bool, int64_t, int,
+                     const int32_t*, const double*, int, const double*, int, int, int,
+                     const AsmOut&);
 }  // namespace mt
 
 template <typename T>
@@ -115,6 +133,27 @@ PYBIND11_MODULE(_hip, m) {
                       max_depth, mss, msl, P<double>(xtab), P<float>(xtabf), xtab_n, P<int32_t>(node_i32),
                       P<int32_t>(node_cnt), P<int32_t>(job_nodes), grid, tiny_rows,
                       P<int64_t>(tiny), tiny_grid, P<int64_t>(prof));
+  });
+  m.def("asm_tiles", &mt::asm_tiles);
+  m.def("asm_rank", [](uintptr_t s, uintptr_t rec, int64_t npos, uintptr_t tile, uintptr_t total,
+                       uintptr_t rank) {
+    mt::launch_asm_rank(S(s), P<int32_t>(rec), npos, P<int32_t>(tile), P<int64_t>(total),
+                        P<int32_t>(rank));
+  });
+  m.def("asm_emit", [](uintptr_t s, uintptr_t rec, uintptr_t st, bool st64, int64_t npos, int C,
+                       uintptr_t rank, uintptr_t edges, int EB, uintptr_t xtab, int xtab_n,
+                       int crit, int y_exp, py::dict out) {
+    auto ptr = [&](const char* k) -> uintptr_t {
+      return out.contains(k) ? out[k].cast<uintptr_t>() : (uintptr_t)0;
+    };
+    mt::AsmOut o{P<int32_t>(ptr("feature")),  P<int32_t>(ptr("bin")),
+                 P<int32_t>(ptr("left")),     P<int32_t>(ptr("right")),
+                 P<int32_t>(ptr("depth")),    P<int64_t>(ptr("nsamp")),
+                 P<int64_t>(ptr("stats")),    P<double>(ptr("threshold")),
+                 P<double>(ptr("term")),      P<double>(ptr("impurity")),
+                 P<double>(ptr("value"))};
+    mt::launch_asm_emit(S(s), P<int32_t>(rec), P<void>(st), st64, npos, C, P<int32_t>(rank),
+                        P<double>(edges), EB, P<double>(xtab), xtab_n, crit, y_exp, o);
   });
   m.def("xlog2x_device", [](uintptr_t s, uintptr_t out, int64_t n) {
     mt::launch_xlog2x(S(s), P<double>(out), n);

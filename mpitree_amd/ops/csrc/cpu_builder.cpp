@@ -14,6 +14,7 @@
 #include <pybind11/pybind11.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <limits>
 #include <vector>
@@ -435,32 +436,22 @@ inline double node_term(const int64_t* c, int64_t C, int crit, const std::vector
   return mt::gini_term(m, sq);
 }
 
-// Re-number a node table into pre-order and emit every output column (the
-// tree-assembly step after a level-wise + finisher fit). Optional: split
-// thresholds from a padded [F, B] edge table, node terms for criterion ``crit``.
-py::dict assemble(py::array_t<int32_t, py::array::c_style | py::array::forcecast> feature,
-                  py::array_t<int32_t, py::array::c_style | py::array::forcecast> tbin,
-                  py::array_t<int64_t, py::array::c_style | py::array::forcecast> left,
-                  py::array_t<int64_t, py::array::c_style | py::array::forcecast> right,
-                  py::array_t<int64_t, py::array::c_style | py::array::forcecast> nsamp,
-                  py::array_t<int64_t, py::array::c_style | py::array::forcecast> stats,
-                  int64_t root,
-                  py::array_t<double, py::array::c_style | py::array::forcecast> edges,
-                  int crit) {
-  const int64_t n = feature.shape(0);
-  const int64_t C = stats.ndim() == 2 ? stats.shape(1) : 1;
-  const int32_t* f = feature.data();
-  const int64_t* l = left.data();
-  const int64_t* r = right.data();
-  const int32_t* b = tbin.data();
-  const int64_t* ns = nsamp.data();
-  const int64_t* st = stats.data();
-  const bool want_thr = edges.ndim() == 2 && edges.size() > 0;
-  const int64_t EB = want_thr ? edges.shape(1) : 0;
-  const double* ed = want_thr ? edges.data() : nullptr;
+// Pre-order re-numbering + column emission shared by both assembly entry
+// points. f/b/l/r: split feature, bin and child ids of N nodes; ns(i) and
+// st(i, c) read a node's row count and statistics. Optional outputs: split
+// thresholds from a padded [F, EB] edge table, node terms for ``crit``.
+template <typename NsFn, typename StFn>
+py::dict assemble_core(int64_t n, const int32_t* f, const int32_t* b, const int64_t* l,
+                       const int64_t* r, NsFn ns, StFn st, int64_t C, int64_t root,
+                       const double* ed, int64_t EB, int crit, int n_threads) {
+  using clk = std::chrono::steady_clock;
+  const auto t_begin = clk::now();
+  auto ms = [](clk::time_point a, clk::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  };
+  const bool want_thr = ed != nullptr;
   const bool want_term = crit >= 0;
   const std::vector<double>& tab = xlog_table();
-
   std::vector<int64_t> new_id(n, -1);
   std::vector<int32_t> depv(n, 0);
   int64_t k = 0;
@@ -497,6 +488,7 @@ py::dict assemble(py::array_t<int32_t, py::array::c_style | py::array::forcecast
       }
     }
   }
+  const auto t_order = clk::now();
   py::array_t<int32_t> of(k), ob(k), od(k), ol(k), orr(k);
   py::array_t<int64_t> on(k), oo(k);
   py::array_t<int64_t> os({k, C});
@@ -506,15 +498,32 @@ py::dict assemble(py::array_t<int32_t, py::array::c_style | py::array::forcecast
   int64_t *pn = on.mutable_data(), *po = oo.mutable_data(), *ps = os.mutable_data();
   double* pt = want_thr ? othr.mutable_data() : nullptr;
   double* pm = want_term ? oterm.mutable_data() : nullptr;
-  for (int64_t i = 0; i < n; ++i) {  // scatter node i to its pre-order slot
+  const double nan = std::numeric_limits<double>::quiet_NaN();
+  // scatter node i to its pre-order slot (independent per node)
+#pragma omp parallel for num_threads(n_threads) schedule(static) if (n > 32768)
+  for (int64_t i = 0; i < n; ++i) {
     const int64_t j = new_id[i];
     if (j < 0) continue;
     po[j] = i;
     pf[j] = f[i];
     pd[j] = depv[i];
-    pn[j] = ns[i];
-    for (int64_t c = 0; c < C; ++c) ps[j * C + c] = st[i * C + c];
-    if (want_term) pm[j] = node_term(st + i * C, C, crit, tab);
+    pn[j] = ns(i);
+    int64_t cs[64];
+    const int64_t cc = C < 64 ? C : 64;
+    for (int64_t c = 0; c < C; ++c) {
+      const int64_t v = st(i, c);
+      ps[j * C + c] = v;
+      if (c < cc) cs[c] = v;
+    }
+    if (want_term) {
+      if (C <= 64) {
+        pm[j] = node_term(cs, C, crit, tab);
+      } else {
+        std::vector<int64_t> tmp(C);
+        for (int64_t c = 0; c < C; ++c) tmp[c] = st(i, c);
+        pm[j] = node_term(tmp.data(), C, crit, tab);
+      }
+    }
     if (f[i] >= 0) {
       pb[j] = b[i];
       pl[j] = (int32_t)new_id[l[i]];
@@ -524,9 +533,10 @@ py::dict assemble(py::array_t<int32_t, py::array::c_style | py::array::forcecast
       pb[j] = -1;
       pl[j] = -1;
       pr[j] = -1;
-      if (want_thr) pt[j] = std::numeric_limits<double>::quiet_NaN();
+      if (want_thr) pt[j] = nan;
     }
   }
+  const auto t_end = clk::now();
   py::dict out;
   out["order"] = oo;
   out["feature"] = of;
@@ -538,7 +548,82 @@ py::dict assemble(py::array_t<int32_t, py::array::c_style | py::array::forcecast
   out["stats"] = os;
   if (want_thr) out["threshold"] = othr;
   if (want_term) out["term"] = oterm;
+  out["ms_order"] = ms(t_begin, t_order);
+  out["ms_scatter"] = ms(t_order, t_end);
   return out;
+}
+
+using I32 = py::array_t<int32_t, py::array::c_style | py::array::forcecast>;
+using I64 = py::array_t<int64_t, py::array::c_style | py::array::forcecast>;
+using F64 = py::array_t<double, py::array::c_style | py::array::forcecast>;
+
+// Re-number one node table into pre-order (see assemble_core).
+py::dict assemble(I32 feature, I32 tbin, I64 left, I64 right, I64 nsamp, I64 stats, int64_t root,
+                  F64 edges, int crit, int n_threads) {
+  const int64_t n = feature.shape(0);
+  const int64_t C = stats.ndim() == 2 ? stats.shape(1) : 1;
+  const int64_t* ns = nsamp.data();
+  const int64_t* st = stats.data();
+  const bool thr = edges.ndim() == 2 && edges.size() > 0;
+  return assemble_core(
+      n, feature.data(), tbin.data(), left.data(), right.data(),
+      [&](int64_t i) { return ns[i]; }, [&](int64_t i, int64_t c) { return st[i * C + c]; }, C,
+      root, thr ? edges.data() : nullptr, thr ? edges.shape(1) : 0, crit, n_threads);
+}
+
+// Tree assembly after a level-wise fit whose deferred nodes were grown by the
+// subtree finisher: the level table (n1 nodes) plus the finisher's compact node
+// table ``fin`` ([T, 6] = feature, bin, left, right, depth, n; links index
+// ``fin``) with class statistics ``fin_stats`` [T, C]. Deferred node did[j]
+// continues as finisher root roots[j] (the root's own row becomes unreachable).
+// One pass builds the joined table and renumbers it (no Python-side splice).
+py::dict assemble_tree(I32 feature, I32 tbin, I64 left, I64 right, I64 nsamp, I64 stats, I32 fin,
+                       I64 fin_stats, I64 did, I64 roots, F64 edges, int crit, int n_threads) {
+  const int64_t n1 = feature.shape(0);
+  const int64_t C = stats.ndim() == 2 ? stats.shape(1) : 1;
+  const int64_t T = fin.ndim() == 2 ? fin.shape(0) : 0;
+  if (T && fin.shape(1) != 6) throw std::invalid_argument("fin must be [T, 6]");
+  if (T && (fin_stats.ndim() != 2 || fin_stats.shape(0) != T || fin_stats.shape(1) != C))
+    throw std::invalid_argument("fin_stats must be [T, C]");
+  const int64_t J = did.size();
+  if (roots.size() != J) throw std::invalid_argument("did/roots length mismatch");
+  const int64_t n = n1 + T;
+  std::vector<int32_t> f(n), b(n);
+  std::vector<int64_t> l(n), r(n);
+  std::copy(feature.data(), feature.data() + n1, f.begin());
+  std::copy(tbin.data(), tbin.data() + n1, b.begin());
+  std::copy(left.data(), left.data() + n1, l.begin());
+  std::copy(right.data(), right.data() + n1, r.begin());
+  const int32_t* fi = T ? fin.data() : nullptr;
+  for (int64_t t = 0; t < T; ++t) {
+    const int32_t* R = fi + t * 6;
+    f[n1 + t] = R[0];
+    b[n1 + t] = R[1];
+    l[n1 + t] = R[0] >= 0 ? n1 + R[2] : -1;
+    r[n1 + t] = R[0] >= 0 ? n1 + R[3] : -1;
+  }
+  const int64_t* dp = did.data();
+  const int64_t* rp = roots.data();
+  for (int64_t j = 0; j < J; ++j) {
+    const int64_t d = dp[j], rt = n1 + rp[j];
+    if (d < 0 || d >= n1 || rt < n1 || rt >= n) throw std::out_of_range("bad deferred link");
+    if (f[rt] < 0) continue;
+    f[d] = f[rt];
+    b[d] = b[rt];
+    l[d] = l[rt];
+    r[d] = r[rt];
+  }
+  const int64_t* ns = nsamp.data();
+  const int64_t* st = stats.data();
+  const int64_t* fs = T ? fin_stats.data() : nullptr;
+  const bool thr = edges.ndim() == 2 && edges.size() > 0;
+  return assemble_core(
+      n, f.data(), b.data(), l.data(), r.data(),
+      [&](int64_t i) { return i < n1 ? ns[i] : (int64_t)fi[(i - n1) * 6 + 5]; },
+      [&](int64_t i, int64_t c) {
+        return i < n1 ? st[i * C + c] : fs[(i - n1) * C + c];
+      },
+      C, 0, thr ? edges.data() : nullptr, thr ? edges.shape(1) : 0, crit, n_threads);
 }
 
 // Node terms for every node: stats [N, C] class counts, or [N, 2] (count, sum).
@@ -567,7 +652,13 @@ PYBIND11_MODULE(_cpu, m) {
   m.def("preorder", &preorder);
   m.def("assemble", &assemble, py::arg("feature"), py::arg("tbin"), py::arg("left"),
         py::arg("right"), py::arg("nsamp"), py::arg("stats"), py::arg("root") = 0,
-        py::arg("edges") = py::array_t<double>(), py::arg("crit") = -1);
+        py::arg("edges") = py::array_t<double>(), py::arg("crit") = -1,
+        py::arg("n_threads") = 1);
+  m.def("assemble_tree", &assemble_tree, py::arg("feature"), py::arg("tbin"), py::arg("left"),
+        py::arg("right"), py::arg("nsamp"), py::arg("stats"), py::arg("fin"),
+        py::arg("fin_stats"), py::arg("did"), py::arg("roots"),
+        py::arg("edges") = py::array_t<double>(), py::arg("crit") = -1,
+        py::arg("n_threads") = 1);
   m.def("node_terms", &node_terms);
   m.def("xlog2x", &xlog2x_np);
 }

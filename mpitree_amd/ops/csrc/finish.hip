@@ -18,10 +18,12 @@
 //   checks, push the larger child first so the DFS stack stays O(log rows).
 //
 // Class counts travel on the DFS stack (known from the parent's split), so a
-// node needs five workgroup barriers. Node slots are handed out by one global
-// atomic counter, so the output is compact; the allocation order varies from
-// run to run but every link is explicit and the host re-numbers the final
-// tree into pre-order, so the fitted tree is bitwise deterministic.
+// node needs five workgroup barriers. Output is addressed by pre-order
+// position: a subtree of r rows has at most 2r - 1 nodes, so a node at
+// position p with n_left left rows puts its left child at p + 1 and its right
+// child at p + 2 n_left. Every position is fixed by row counts alone -- no
+// allocation counter, no renumbering -- and compacting the written positions
+// (assemble.hip) yields the tree in exact pre-order, bitwise deterministic.
 #include <type_traits>
 
 #include "common.h"
@@ -59,7 +61,7 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
     int32_t* __restrict__ job_counter, const int32_t* __restrict__ nbins, int F, int B, int C,
     int crit, int max_depth, int64_t mss, int64_t msl, const double* __restrict__ xtab,
     const float* __restrict__ xtabf, int xtab_n, int32_t* __restrict__ node_i32, int32_t* __restrict__ node_cnt,
-    int32_t* __restrict__ job_root, int32_t* __restrict__ node_counter, int tiny_rows,
+    int32_t* __restrict__ job_root, int tiny_rows,
     int64_t* __restrict__ tiny, int32_t* __restrict__ tiny_count, int64_t* __restrict__ prof) {
   // prof (optional): per workgroup {wall start, wall end, nodes, rows, cycles in
   // histogram, scan, partition, rest} -- the finisher's own phase profile
@@ -243,10 +245,10 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
     if (job >= J) break;
     if (prof && tid == 0) pr_t = (int64_t)clock64();
     const int64_t* jb = jobs + (int64_t)job * JW;
-    int32_t* ni = node_i32;  // node slots come from one global counter
+    int32_t* ni = node_i32;  // indexed by pre-order position (see launch_finish)
     int32_t* nc = node_cnt;
     if (tid == 0) {
-      const int r = atomicAdd(node_counter, 1);
+      const int r = (int)jb[3];
       s_root = r;
       job_root[job] = r;
       s_sp = 1;
@@ -598,7 +600,7 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
       if (tid == 0 && bf >= 0) {
         const int nl = s_lc;
         const int nr = m - nl;
-        const int lid = atomicAdd(node_counter, 2), rid = lid + 1;
+        const int lid = id + 1, rid = id + 2 * nl;  // left subtree owns 2 nl - 1 positions
         ni[(int64_t)id * 6 + 0] = bf;
         ni[(int64_t)id * 6 + 1] = bb;
         ni[(int64_t)id * 6 + 2] = lid;
@@ -696,7 +698,7 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
     const int64_t* __restrict__ tiny, const int32_t* __restrict__ tiny_count,
     int32_t* __restrict__ tiny_counter, int F, int C, int crit, int max_depth, int64_t mss,
     int64_t msl, const double* __restrict__ xtab, int32_t* __restrict__ node_i32,
-    int32_t* __restrict__ node_cnt, int32_t* __restrict__ node_counter) {
+    int32_t* __restrict__ node_cnt) {
   __shared__ double s_tab[kTinyRows + 1];
   __shared__ uint32_t s_codes[kTinyWaves][kTinyRows * kTinyStride];
   __shared__ unsigned long long s_mask[kTinyWaves][16];
@@ -840,10 +842,8 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
       if (!(bg > -__builtin_inf()) || bf < 0) continue;  // leaf: the creation record stands
       const unsigned long long LM = M & __ballot((uint32_t)my_bytes[bf] <= bb);
       const unsigned long long RM = M & ~LM;
-      int alloc = 0;
-      if (lane == 0) alloc = atomicAdd(node_counter, 2);
-      const int64_t ls = __builtin_amdgcn_readfirstlane(alloc), rs = ls + 1;
       const int nl = __popcll(LM), nr = __popcll(RM);
+      const int64_t ls = slot + 1, rs = slot + 2 * nl;  // pre-order position ranges
       int nzl = 0, nzr = 0;
 #pragma unroll
       for (int c = 0; c < kFinMaxC; ++c) {
@@ -901,8 +901,9 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                    const float* xtabf, int xtab_n,
                    int32_t* node_i32, int32_t* node_cnt, int32_t* job_root, int grid,
                    int tiny_rows, int64_t* tiny, int tiny_grid, int64_t* prof) {
-  // counter: int32 [4] = {job cursor, tiny count, tiny cursor, node count}, zeroed by
-  // the host; node slots are handed out by the last one (compact output)
+  // counter: int32 [4] = {job cursor, tiny count, tiny cursor, -}, zeroed by the
+  // host. node_i32 / node_cnt are indexed by pre-order position (jobs[j][3] is
+  // job j's root position); rows a fit never writes keep n = 0 (host memset).
   if (J <= 0) return;
   if (C > kFinMaxC) throw std::runtime_error("finisher supports at most 16 classes");
   if (F > kFinMaxF) throw std::runtime_error("finisher supports at most 256 features");
@@ -916,7 +917,7 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   hipLaunchKernelGGL((finish_cls_kernel<CT, C2>), dim3(grid), dim3(kFinThreads), lds, stream, \
                      (const uint32_t*)codes_rm, row_words, (const CT*)codes_fm, n_rows, buf0, \
                      buf1, y, rl, jobs, J, counter, nbins, F, B, C, crit, max_depth, mss,     \
-                     msl, xtab, xtabf, xtab_n, node_i32, node_cnt, job_root, counter + 3, tiny_rows, \
+                     msl, xtab, xtabf, xtab_n, node_i32, node_cnt, job_root, tiny_rows,           \
                      tiny, counter + 1, prof);
   if (code_bytes == 1) {
     if (C <= 2) {
@@ -937,7 +938,7 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
     hipLaunchKernelGGL(finish_tiny_kernel, dim3(tiny_grid), dim3(kTinyWaves * kWave), 0, stream,
                        (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,
                        counter + 1, counter + 2, F, C, crit, max_depth, mss, msl, xtab,
-                       node_i32, node_cnt, counter + 3);
+                       node_i32, node_cnt);
     MT_HIP_CHECK(hipGetLastError());
   }
 }

@@ -182,6 +182,24 @@ def xlog2x_table(device) -> torch.Tensor:
     return t
 
 
+_pinned: dict = {}
+
+
+def _pinned_copy(t: torch.Tensor, key: str) -> np.ndarray:
+    """Start an async D2H copy of ``t`` into a reusable pinned buffer; returns
+    the numpy view (valid after the stream is synchronised). Buffers grow
+    geometrically and are reused, so steady-state fits allocate nothing."""
+    n = t.numel()
+    buf = _pinned.get(key)
+    if buf is None or buf.numel() < n or buf.dtype != t.dtype:
+        cap = max(n, 2 * (buf.numel() if buf is not None and buf.dtype == t.dtype else 0), 1024)
+        buf = torch.empty(cap, dtype=t.dtype, pin_memory=True)
+        _pinned[key] = buf
+    view = buf[:n].view(t.shape)
+    view.copy_(t, non_blocking=True)
+    return view.numpy()
+
+
 def xlog2x_table_f32(device) -> torch.Tensor:
     """fp32 rounding of :func:`xlog2x_table` (the finisher's approximate pass)."""
     key = "f32:" + str(device)
@@ -356,28 +374,100 @@ class HipBackend:
     # finisher jobs index the x*log2(x) table with row counts: keep them below it
     max_finisher_rows = XTAB_N - 1
 
-    def finish_subtrees(self, starts, counts, depths, params, stats=None):
-        """Grow every job's subtree on the device; one compact node table out.
+    # ------------------------------------------------ pre-order position space
+    def begin_positions(self, P: int):
+        """Allocate the fit's position space: every node is written at its
+        pre-order position with holes (a subtree of r rows owns 2r - 1
+        positions); ``assemble_positions`` removes the holes on the device."""
+        if P >= 2**31 - 1:
+            raise ValueError("position space exceeds 2^31 (more than ~1e9 rows)")
+        self.P = int(P)
+        self.pos_rec = torch.zeros((self.P, 6), dtype=torch.int32, device=self.device)
+        dt = torch.int64 if self.reg else torch.int32
+        self.pos_st = torch.empty((self.P, self.C), dtype=dt, device=self.device)
 
-        Returns a dict of arrays (feature, bin, left, right, depth, nsamp,
-        stats) over all finisher nodes, child links indexing this table, and
-        ``roots[j]``: the row of job j's root.
+    def put_positions(self, pos, feature, tbin, lpos, rpos, depth, nsamp, stats):
+        """Write host-grown (level-wise) nodes into the position space."""
+        if len(pos) == 0:
+            return
+        rec = np.stack([feature, tbin, lpos, rpos, depth, nsamp], 1)
+        d_pos, d_rec, d_st = self.up(np.asarray(pos, np.int64), rec,
+                                     np.asarray(stats, np.int64))
+        self.pos_rec.index_copy_(0, d_pos, d_rec.reshape(-1, 6).to(torch.int32))
+        self.pos_st.index_copy_(0, d_pos, d_st.reshape(-1, self.C).to(self.pos_st.dtype))
+
+    def assemble_positions(self, edges: np.ndarray, crit: int, y_exp: int = 0) -> dict:
+        """Compact the position space into pre-ordered tree columns (numpy views
+        of one pinned host buffer, filled by a single D2H copy)."""
+        P, C = self.P, self.C
+        hip = self.hip
+        s = _stream()
+        tiles = hip.asm_tiles(P)
+        tile = torch.empty(max(tiles, 1), dtype=torch.int32, device=self.device)
+        total = torch.zeros(1, dtype=torch.int64, device=self.device)
+        rank = torch.empty(P, dtype=torch.int32, device=self.device)
+        hip.asm_rank(s, self.pos_rec.data_ptr(), P, tile.data_ptr(), total.data_ptr(),
+                     rank.data_ptr())
+        N = int(total.item())
+        # packed output: 8-byte columns first, then 4-byte columns (alignment)
+        cols8 = [("nsamp", torch.int64, 1), ("stats", torch.int64, C),
+                 ("threshold", torch.float64, 1), ("term", torch.float64, 1),
+                 ("impurity", torch.float64, 1)]
+        if self.reg:
+            cols8.append(("value", torch.float64, 1))
+        cols4 = [(k, torch.int32, 1) for k in ("feature", "bin", "left", "right", "depth")]
+        layout, off = [], 0
+        for name, dt, w in cols8 + cols4:
+            nbytes = N * w * (8 if dt in (torch.int64, torch.float64) else 4)
+            layout.append((name, dt, w, off, nbytes))
+            off += nbytes
+        dev = torch.empty(max(off, 8), dtype=torch.uint8, device=self.device)
+        ptrs = {name: dev.data_ptr() + o for name, dt, w, o, nb in layout}
+        d_edges = torch.from_numpy(np.ascontiguousarray(edges, np.float64)).to(self.device)
+        hip.asm_emit(s, self.pos_rec.data_ptr(), self.pos_st.data_ptr(), self.reg, P, C,
+                     rank.data_ptr(), d_edges.data_ptr(), int(edges.shape[1]),
+                     self.xtab.data_ptr(), XTAB_N, int(crit), int(y_exp), ptrs)
+        host = torch.empty(max(off, 8), dtype=torch.uint8, pin_memory=True)
+        host.copy_(dev, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        out = {}
+        for name, dt, w, o, nb in layout:
+            t = host[o : o + nb].view(dt)
+            out[name] = (t.view(N, w) if w > 1 else t).numpy()
+        self.pos_rec = self.pos_st = None
+        return out
+
+    def finish_subtrees(self, starts, counts, depths, params, stats=None, positions=None):
+        """Grow every job's subtree on the device.
+
+        With ``positions`` (the jobs' pre-order positions in the fit's position
+        space, see :meth:`begin_positions`) the nodes stay on the device and
+        ``None`` is returned. Without, the jobs get a private position space
+        and a compact node table comes back (the distributed merge format):
+        arrays feature, bin, left, right, depth, nsamp, stats with child links
+        indexing the table, and ``roots[j]``: the row of job j's root.
         """
         J = len(starts)
         starts = np.asarray(starts, np.int64)
         counts = np.asarray(counts, np.int64)
         depths = np.asarray(depths, np.int64)
-        order = np.argsort(-counts, kind="stable")  # largest first
-        st = np.asarray(stats, np.int64).reshape(J, self.C)
-        # {start, count, depth, -, row buffer, class counts[C]}
-        jobs = np.concatenate([np.stack([starts[order], counts[order], depths[order],
-                                         np.zeros(J, np.int64), np.zeros(J, np.int64)], 1),
-                               st[order]], 1)
-        total = int((2 * counts - 1).sum())  # a subtree of r rows has <= 2r-1 nodes
         C = self.C
+        table_mode = positions is None
+        span = 2 * counts - 1  # a subtree of r rows owns 2r - 1 positions
+        if table_mode:
+            positions = np.cumsum(span) - span
+            rec = torch.zeros((max(int(span.sum()), 1), 6), dtype=torch.int32, device=self.device)
+            cnt = torch.empty((rec.shape[0], C), dtype=torch.int32, device=self.device)
+        else:
+            rec, cnt = self.pos_rec, self.pos_st
+        positions = np.asarray(positions, np.int64)
+        order = np.argsort(-counts, kind="stable")  # largest first
+        st = np.asarray(stats, np.int64).reshape(J, C)
+        # {start, count, depth, root position, row buffer, class counts[C]}
+        jobs = np.concatenate([np.stack([starts[order], counts[order], depths[order],
+                                         positions[order], np.zeros(J, np.int64)], 1),
+                               st[order]], 1)
         (d_jobs,) = self.up(jobs)
-        node_i32 = torch.empty((total, 6), dtype=torch.int32, device=self.device)
-        node_cnt = torch.empty((total, C), dtype=torch.int32, device=self.device)
         job_root = torch.empty(J, dtype=torch.int32, device=self.device)
         counter = torch.zeros(4, dtype=torch.int32, device=self.device)
         tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
@@ -396,19 +486,32 @@ class HipBackend:
                         int(self.crit), md, int(params.min_samples_split),
                         int(max(1, params.min_samples_leaf)), self.xtab.data_ptr(),
                         self.xtabf.data_ptr(), XTAB_N,
-                        node_i32.data_ptr(), node_cnt.data_ptr(), job_root.data_ptr(), grid,
+                        rec.data_ptr(), cnt.data_ptr(), job_root.data_ptr(), grid,
                         tiny_rows, tiny.data_ptr(), 4 * N_CU,
                         0 if prof is None else prof.data_ptr())
         if prof is not None:
             self.last_finisher_prof = prof.cpu().numpy()
-        N = int(counter[3].item())
-        ni = node_i32[:N].cpu().numpy()
-        nc = node_cnt[:N].cpu().numpy()
-        roots = np.empty(J, np.int64)
-        roots[order] = job_root.cpu().numpy()
-        return dict(feature=ni[:, 0], bin=ni[:, 1], left=ni[:, 2].astype(np.int64),
-                    right=ni[:, 3].astype(np.int64), depth=ni[:, 4], nsamp=ni[:, 5].astype(np.int64),
-                    stats=nc.astype(np.int64), roots=roots)
+        if not table_mode:
+            return None
+        # compact the private position space into the merge table
+        P = rec.shape[0]
+        tiles = self.hip.asm_tiles(P)
+        tile = torch.empty(max(tiles, 1), dtype=torch.int32, device=self.device)
+        total = torch.zeros(1, dtype=torch.int64, device=self.device)
+        rank = torch.empty(P, dtype=torch.int32, device=self.device)
+        self.hip.asm_rank(_stream(), rec.data_ptr(), P, tile.data_ptr(), total.data_ptr(),
+                          rank.data_ptr())
+        live = torch.nonzero(rank >= 0).squeeze(1)  # ascending position = table row
+        r = rec[live]
+        inner = r[:, 0] >= 0
+        lk = torch.where(inner, rank[r[:, 2].long().clamp(min=0)], -1)
+        rk = torch.where(inner, rank[r[:, 3].long().clamp(min=0)], -1)
+        r = torch.stack([r[:, 0], r[:, 1], lk, rk, r[:, 4], r[:, 5]], 1)
+        ni = r.cpu().numpy()
+        nc = cnt[live].cpu().numpy().astype(np.int64)
+        roots = rank[torch.from_numpy(positions).to(self.device)].cpu().numpy().astype(np.int64)
+        return dict(feature=ni[:, 0], bin=ni[:, 1], left=ni[:, 2], right=ni[:, 3],
+                    depth=ni[:, 4], nsamp=ni[:, 5], stats=nc, roots=roots, i32=ni, cnt=nc)
 
     def sync(self):
         if self.timing:

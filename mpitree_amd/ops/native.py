@@ -51,3 +51,18 @@ def has_hip() -> bool:
         return True
     except ImportError:
         return False
+
+
+def host_threads() -> int:
+    """Host worker threads for native helpers: ``MPITREE_HOST_THREADS`` or the
+    CPUs this process may run on, capped at 16 (one GPU's share of a node)."""
+    import os
+
+    env = os.environ.get("MPITREE_HOST_THREADS")
+    if env:
+        return max(1, int(env))
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):  # pragma: no cover - non-Linux
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))

@@ -137,3 +137,26 @@ def test_gpu_tiny_subtree_wave_path(monkeypatch, tiny):
         clf = DecisionTreeClassifier(criterion=crit, device="cuda",
                                      min_samples_leaf=2 if crit == "gini" else 1).fit(X, y)
         assert clf.tree_arrays_.equal(ref), (tiny, crit)
+
+
+@pytest.mark.parametrize("regression", [False, True])
+def test_gpu_device_assembly_matches_host(monkeypatch, regression):
+    """Pre-order position space + device compaction == host renumbering."""
+    from mpitree_amd.core.fit import fit_tree
+
+    rng = np.random.default_rng(7)
+    n, F = 6000, 9
+    X = rng.integers(0, 40, size=(n, F)).astype(np.float32)
+    y = rng.normal(size=n) if regression else rng.integers(0, 3, size=n)
+    kw = dict(regression=regression, criterion=2 if regression else 0, max_depth=None,
+              min_samples_split=2, device="cuda", finisher_rows=None if regression else 700)
+    monkeypatch.setenv("MPITREE_DEVICE_ASSEMBLY", "1")
+    dev = fit_tree(X, y, **kw).arrays
+    monkeypatch.setenv("MPITREE_DEVICE_ASSEMBLY", "0")
+    host = fit_tree(X, y, **kw).arrays
+    assert dev.equal(host, check_impurity=False)
+    assert np.array_equal(dev.impurity, host.impurity, equal_nan=True)
+    if regression:
+        assert np.array_equal(dev.value, host.value)
+        assert np.array_equal(dev.meta["sum_fixed"], host.meta["sum_fixed"])
+    assert np.array_equal(dev.meta["term"], host.meta["term"])
