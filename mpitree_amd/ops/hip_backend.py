@@ -401,6 +401,10 @@ class HipBackend:
         of one pinned host buffer, filled by a single D2H copy)."""
         P, C = self.P, self.C
         hip = self.hip
+        done = getattr(self, "_side_done", None)
+        if done is not None:  # overlapped finisher batches must land first
+            torch.cuda.current_stream(self.device).wait_event(done)
+            self._side_done = None
         s = _stream()
         tiles = hip.asm_tiles(P)
         tile = torch.empty(max(tiles, 1), dtype=torch.int32, device=self.device)
@@ -437,7 +441,27 @@ class HipBackend:
         self.pos_rec = self.pos_st = None
         return out
 
-    def finish_subtrees(self, starts, counts, depths, params, stats=None, positions=None):
+    def finish_subtrees(self, starts, counts, depths, params, stats=None, positions=None,
+                        overlap=False):
+        """See :meth:`_finish_subtrees`; ``overlap`` runs the batch on a side
+        stream (after the rows' partition on the main stream) so later levels
+        and this batch share the GPU. :meth:`assemble_positions` joins it."""
+        if not overlap or positions is None:
+            return self._finish_subtrees(starts, counts, depths, params, stats, positions)
+        main = torch.cuda.current_stream(self.device)
+        if getattr(self, "side", None) is None:
+            self.side = torch.cuda.Stream(self.device)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        self.side.wait_event(ready)
+        with torch.cuda.stream(self.side):
+            self._finish_subtrees(starts, counts, depths, params, stats, positions)
+            done = torch.cuda.Event()
+            done.record(self.side)
+        self._side_done = done
+        return None
+
+    def _finish_subtrees(self, starts, counts, depths, params, stats=None, positions=None):
         """Grow every job's subtree on the device.
 
         With ``positions`` (the jobs' pre-order positions in the fit's position
@@ -475,7 +499,7 @@ class HipBackend:
         tiny_cap = int(counts.sum() // 2 + J + 1)
         tiny = torch.empty((tiny_cap, 8), dtype=torch.int64, device=self.device)
         md = -1 if params.max_depth is None else int(params.max_depth)
-        grid = int(min(J, 2 * N_CU))
+        grid = int(min(J, int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU))))
         prof = None
         if os.environ.get("MPITREE_FIN_PROF"):
             prof = torch.zeros((grid, 10), dtype=torch.int64, device=self.device)
