@@ -83,7 +83,8 @@ def _validate_X(X, allow_tensor=True):
             raise ValueError("Found array with 0 sample(s)")
         if not torch.is_floating_point(X):
             X = X.double()
-        if not bool(torch.isfinite(X).all()):
+        # device tensors are checked by the bin kernel (no extra pass / sync)
+        if not X.is_cuda and not bool(torch.isfinite(X).all()):
             raise ValueError("Input X contains NaN or infinity.")
         return X
     X = np.asarray(X)
@@ -244,6 +245,8 @@ def fit_tree(
         stats = dict(builder.stats)
     else:
         Xh = X.cpu().numpy() if _is_tensor(X) else X
+        if _is_tensor(X) and X.is_cuda and not np.isfinite(Xh).all():
+            raise ValueError("Input X contains NaN or infinity.")
         yh = yv.cpu().numpy() if _is_tensor(yv) else yv
         t0 = time.perf_counter()
         mapper = fit_bin_mapper(Xh, max_bins)

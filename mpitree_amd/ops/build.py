@@ -29,8 +29,8 @@ BUILD = PKG.parent / "build" / "native"
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 ARCH = os.environ.get("MPITREE_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["hist.hip", "split_scan.hip", "partition.hip", "predict_bin.hip", "misc.hip",
-               "finish.hip", "assemble.hip", "bindings.cpp"]
+HIP_SOURCES = ["hist.hip", "split_scan.hip", "partition.hip", "predict.hip", "misc.hip",
+               "finish.hip", "assemble.hip", "binning.hip", "bindings.cpp"]
 CPU_SOURCES = ["cpu_builder.cpp"]
 HEADERS = ["common.h", "criterion.h"]
 

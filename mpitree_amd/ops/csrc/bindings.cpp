@@ -52,6 +52,9 @@ struct AsmOut {
   double* value;
 };
 int asm_tiles(int64_t P);
+int edges_sample_rows(bool x64);
+void launch_edges(hipStream_t, const void*, bool, int64_t, int, int, int, void*, int32_t*,
+                  uint8_t*);
 void launch_asm_rank(hipStream_t, const int32_t*, int64_t, int32_t*, int64_t*, int32_t*);
 void launch_asm_emit(hipStream_t, const int32_t*, const void*, bool, int64_t, int,
                      const int32_t*, const double*, int, const double*, int, int, int,
@@ -135,6 +138,12 @@ PYBIND11_MODULE(_hip, m) {
                       P<int64_t>(tiny), tiny_grid, P<int64_t>(prof));
   });
   m.def("asm_tiles", &mt::asm_tiles);
+  m.def("edges_sample_rows", &mt::edges_sample_rows);
+  m.def("edges", [](uintptr_t s, uintptr_t X, bool x64, int64_t n, int F, int rows, int limit,
+                    uintptr_t edges, uintptr_t nbins, uintptr_t exact) {
+    mt::launch_edges(S(s), P<void>(X), x64, n, F, rows, limit, P<void>(edges), P<int32_t>(nbins),
+                     P<uint8_t>(exact));
+  });
   m.def("asm_rank", [](uintptr_t s, uintptr_t rec, int64_t npos, uintptr_t tile, uintptr_t total,
                        uintptr_t rank) {
     mt::launch_asm_rank(S(s), P<int32_t>(rec), npos, P<int32_t>(tile), P<int64_t>(total),

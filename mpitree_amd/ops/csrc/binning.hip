@@ -1,0 +1,366 @@
+// Feature binning on gfx950: bin edges and codes for the whole matrix.
+//
+// The reference re-derives candidate thresholds at every node with
+// ``np.unique(X[:, f])`` (mpitree/tree/decision_tree.py:73). Here binning is a
+// single up-front pass of two kernels:
+//
+// edges_kernel (one workgroup per feature): a deterministic strided row sample
+//   of the column is staged in LDS. Its distinct values are first collected in
+//   an LDS open-addressing hash set; when there are at most ``limit`` of them
+//   (tabular data: integers, categories, quantized values) the feature is in
+//   exact mode and its edges are those values, sorted. Otherwise the sample is
+//   bitonic-sorted in LDS and ``limit`` quantile edges are taken (duplicates
+//   dropped). Exactly the edges the host BinMapper would produce for the same
+//   sample.
+// bin_kernel (row tile x 16-feature tile): each thread bins 16 elements with
+//   16 independent branch-free lower_bound searches over LDS edges (ILP hides
+//   the LDS latency), verifies exact-mode values against their edge, flags
+//   non-finite input, and writes codes row-major (histogram gathers) and
+//   feature-major (partition's single-column reads) from an LDS tile.
+#include <type_traits>
+
+#include "common.h"
+
+namespace mt {
+
+template <typename XT>
+struct KeyOf {
+  using T = typename std::conditional<sizeof(XT) == 8, unsigned long long, uint32_t>::type;
+};
+
+template <typename XT>
+__device__ __forceinline__ typename KeyOf<XT>::T key_bits(XT v) {
+  if constexpr (sizeof(XT) == 8) {
+    return (unsigned long long)__double_as_longlong(v);
+  } else {
+    return __float_as_uint(v);
+  }
+}
+
+template <typename XT>
+__device__ __forceinline__ XT key_value(typename KeyOf<XT>::T k) {
+  if constexpr (sizeof(XT) == 8) {
+    return __longlong_as_double((long long)k);
+  } else {
+    return __uint_as_float(k);
+  }
+}
+
+constexpr int kEdgeThreads = 1024;
+constexpr int kEdgeHash = 2048;  // hash slots (exact mode needs <= limit <= 1024 keys)
+
+// One workgroup per feature. smem: sample [S] XT, hash [kEdgeHash] keys.
+// S = power of two >= s (padding +inf sorts last). Output: edges [F][limit]
+// (+inf padded), nbins [F], exact [F].
+template <typename XT>
+__global__ __launch_bounds__(kEdgeThreads) void edges_kernel(const XT* __restrict__ X, int64_t n,
+                                                             int F, int s, int S, int limit,
+                                                             XT* __restrict__ edges,
+                                                             int32_t* __restrict__ nbins,
+                                                             uint8_t* __restrict__ exact) {
+  using K = typename KeyOf<XT>::T;
+  extern __shared__ __align__(16) uint8_t smem[];
+  XT* key = reinterpret_cast<XT*>(smem);
+  K* hset = reinterpret_cast<K*>(smem + (size_t)S * sizeof(XT));
+  __shared__ int s_cnt, s_over;
+  __shared__ int w_sum[kEdgeThreads / kWave];
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x;
+  const K kEmpty = ~(K)0;  // a NaN pattern: never a (finite) data value
+  const bool use_hash = limit <= kEdgeHash / 2;
+  if (tid == 0) {
+    s_cnt = 0;
+    s_over = use_hash ? 0 : 1;
+  }
+  for (int i = tid; i < kEdgeHash; i += kEdgeThreads) hset[i] = kEmpty;
+  for (int i = tid; i < S; i += kEdgeThreads) {
+    XT v = __builtin_inf();
+    if (i < s) {
+      const int64_t row = (int64_t)i * n / s;  // deterministic strided sample
+      v = X[row * F + f];
+      if (v == (XT)0) v = (XT)0;  // -0 and +0 are one value (x <= t cannot tell them apart)
+    }
+    key[i] = v;
+  }
+  __syncthreads();
+  // ---- exact-mode probe: distinct values into the LDS hash set
+  if (use_hash) {
+    for (int i = tid; i < s && !s_over; i += kEdgeThreads) {
+      const K k = key_bits<XT>(key[i]);
+      uint32_t h = (uint32_t)(k ^ (k >> 29)) * 0x9E3779B1u;
+      int slot = (int)(h >> 21) & (kEdgeHash - 1);
+      for (int probe = 0; probe < kEdgeHash; ++probe) {
+        const K cur = atomicCAS(&hset[slot], kEmpty, k);
+        if (cur == kEmpty) {  // inserted a new distinct value
+          if (atomicAdd(&s_cnt, 1) + 1 > limit) s_over = 1;
+          break;
+        }
+        if (cur == k) break;
+        slot = (slot + 1) & (kEdgeHash - 1);
+      }
+    }
+  }
+  __syncthreads();
+  XT* out = edges + (int64_t)f * limit;
+  if (!s_over) {
+    // exact: sort the <= limit distinct values (compact them into key[] first)
+    const int m = s_cnt;
+    __syncthreads();
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+    for (int i = tid; i < kEdgeHash; i += kEdgeThreads) {
+      const K k = hset[i];
+      if (k != kEmpty) key[atomicAdd(&s_cnt, 1)] = key_value<XT>(k);
+    }
+    __syncthreads();
+    int M = 1;
+    while (M < m) M <<= 1;
+    for (int i = m + tid; i < M; i += kEdgeThreads) key[i] = __builtin_inf();
+    __syncthreads();
+    for (int k = 2; k <= M; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int q = tid; q < (M >> 1); q += kEdgeThreads) {
+          const int lo = ((q & ~(j - 1)) << 1) | (q & (j - 1));
+          const int hi = lo | j;
+          const XT a = key[lo], b = key[hi];
+          const bool up = (lo & k) == 0;
+          if ((a > b) == up) {
+            key[lo] = b;
+            key[hi] = a;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    for (int i = tid; i < limit; i += kEdgeThreads) out[i] = i < m ? key[i] : (XT)__builtin_inf();
+    if (tid == 0) {
+      nbins[f] = m;
+      exact[f] = 1;
+    }
+    return;
+  }
+  // ---- quantile mode: bitonic sort of the whole sample
+  for (int k = 2; k <= S; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int q = tid; q < (S >> 1); q += kEdgeThreads) {
+        const int lo = ((q & ~(j - 1)) << 1) | (q & (j - 1));
+        const int hi = lo | j;
+        const XT a = key[lo], b = key[hi];
+        const bool up = (lo & k) == 0;
+        if ((a > b) == up) {
+          key[lo] = b;
+          key[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // ordered compaction: out[0..) = value(i) for i in [0, R) with pick(i) true
+  __shared__ int s_base;
+  auto compact = [&](int R, auto pick, auto value) {
+    if (tid == 0) s_base = 0;
+    __syncthreads();
+    for (int b0 = 0; b0 < R; b0 += kEdgeThreads) {
+      const int i = b0 + tid;
+      const bool keep = i < R && pick(i);
+      const unsigned long long bal = __ballot(keep);
+      const int lane = lane_id();
+      const int wv = tid >> 6;
+      if (lane == 0) w_sum[wv] = __popcll(bal);
+      __syncthreads();
+      int off = s_base;
+      for (int w = 0; w < wv; ++w) off += w_sum[w];
+      const int pos = off + __popcll(bal & ((1ull << lane) - 1ull));
+      if (keep) out[pos] = value(i);
+      __syncthreads();
+      if (tid == kEdgeThreads - 1) s_base = pos + (keep ? 1 : 0);
+      __syncthreads();
+    }
+    return s_base;
+  };
+  // distinct values of the sorted sample
+  int cnt = 0;
+  for (int i = tid; i < s; i += kEdgeThreads) cnt += (i == 0 || key[i] != key[i - 1]) ? 1 : 0;
+  cnt = (int)wave_sum_u32((uint32_t)cnt);
+  if (lane_id() == 0) w_sum[tid >> 6] = cnt;
+  __syncthreads();
+  int distinct = 0;
+  for (int w = 0; w < kEdgeThreads / kWave; ++w) distinct += w_sum[w];
+  __syncthreads();
+  const bool is_exact = distinct <= limit;
+  int m;
+  if (is_exact) {
+    m = compact(
+        s, [&](int i) { return i == 0 || key[i] != key[i - 1]; }, [&](int i) { return key[i]; });
+  } else {
+    // quantile k (1..limit) is sample element ceil(k s / limit) - 1; keep first of runs
+    auto qi = [&](int k1) {
+      const int64_t q = ((int64_t)k1 * s + limit - 1) / limit - 1;
+      return (int)(q < s - 1 ? q : s - 1);
+    };
+    m = compact(
+        limit, [&](int k) { return k == 0 || key[qi(k)] != key[qi(k + 1)]; },
+        [&](int k) { return key[qi(k + 1)]; });
+  }
+  for (int i = m + tid; i < limit; i += kEdgeThreads) out[i] = (XT)__builtin_inf();
+  if (tid == 0) {
+    nbins[f] = m;
+    exact[f] = is_exact ? 1 : 0;
+  }
+}
+
+constexpr int kBinRows = 256;
+constexpr int kBinFt = 16;                          // features per tile
+constexpr int kBinPer = kBinRows * kBinFt / 256;    // elements per thread
+
+// grid = (row tiles, feature tiles). flags[f]: bit 0 = an exact-mode value
+// missed its edge (sample incomplete), bit 1 = non-finite value seen.
+template <typename XT, typename CodeT, bool kLds>
+__global__ __launch_bounds__(256) void bin_kernel(const XT* __restrict__ X, int64_t n, int F,
+                                                  const XT* __restrict__ edges, int Bmax,
+                                                  int steps0, const int32_t* __restrict__ nbins,
+                                                  const uint8_t* __restrict__ exact,
+                                                  CodeT* __restrict__ codes_rm, int row_elems,
+                                                  CodeT* __restrict__ codes_fm,
+                                                  int32_t* __restrict__ flags) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  __shared__ int s_flag[kBinFt];
+  __shared__ int32_t s_nb[kBinFt];
+  __shared__ uint8_t s_ex[kBinFt];
+  XT* s_edges = reinterpret_cast<XT*>(smem);  // [kBinFt][Bmax] when staged
+  CodeT* tile = reinterpret_cast<CodeT*>(smem + (kLds ? (size_t)kBinFt * Bmax * sizeof(XT) : 0));
+  const int64_t r0 = blockIdx.x * (int64_t)kBinRows;
+  const int rows = (int)min<int64_t>(kBinRows, n - r0);
+  const int f0 = blockIdx.y * kBinFt;
+  const int nf = min(kBinFt, F - f0);
+  if (threadIdx.x < kBinFt) {
+    s_flag[threadIdx.x] = 0;
+    s_nb[threadIdx.x] = threadIdx.x < nf ? nbins[f0 + threadIdx.x] : 1;
+    s_ex[threadIdx.x] = threadIdx.x < nf ? exact[f0 + threadIdx.x] : 0;
+  }
+  if constexpr (kLds) {
+    for (int e = threadIdx.x; e < nf * Bmax; e += 256) s_edges[e] = edges[(int64_t)f0 * Bmax + e];
+  }
+  __syncthreads();
+  // element e = threadIdx.x + 256 k -> (row e / 16, feature e % 16): a wave reads
+  // 4 rows x 16 consecutive features per step
+  XT v[kBinPer];
+  int pos[kBinPer], nb[kBinPer];
+  bool ok[kBinPer];
+#pragma unroll
+  for (int k = 0; k < kBinPer; ++k) {
+    const int e = threadIdx.x + 256 * k;
+    const int r = e / kBinFt, fl = e % kBinFt;
+    ok[k] = r < rows && fl < nf;
+    v[k] = ok[k] ? X[(r0 + r) * F + f0 + fl] : (XT)0;
+    nb[k] = s_nb[fl];
+    pos[k] = 0;  // number of edges < v (lower_bound)
+  }
+  for (int step = steps0; step > 0; step >>= 1) {
+#pragma unroll
+    for (int k = 0; k < kBinPer; ++k) {
+      const int fl = (threadIdx.x + 256 * k) % kBinFt;
+      const int p = pos[k] + step;
+      const XT* ed = kLds ? s_edges + fl * Bmax : edges + (int64_t)(f0 + fl) * Bmax;
+      if (p <= nb[k] && ed[p - 1] < v[k]) pos[k] = p;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kBinPer; ++k) {
+    const int e = threadIdx.x + 256 * k;
+    const int r = e / kBinFt, fl = e % kBinFt;
+    if (!ok[k]) continue;
+    const XT* ed = kLds ? s_edges + fl * Bmax : edges + (int64_t)(f0 + fl) * Bmax;
+    const int code = pos[k] < nb[k] ? pos[k] : nb[k] - 1;
+    int fg = 0;
+    if (s_ex[fl] && !(ed[code] == v[k])) fg |= 1;
+    if (!isfinite(v[k])) fg |= 2;
+    if (fg) atomicOr(&s_flag[fl], fg);
+    tile[r * kBinFt + fl] = (CodeT)code;
+  }
+  __syncthreads();
+  // row-major: this tile's codes of every row (+ zero padding after the last feature)
+  const int pad_end = (f0 + nf == F) ? row_elems : f0 + nf;
+  const int wcols = pad_end - f0;
+  for (int e = threadIdx.x; e < rows * wcols; e += 256) {
+    const int r = e / wcols;
+    const int c = e - r * wcols;
+    codes_rm[(r0 + r) * row_elems + f0 + c] = c < nf ? tile[r * kBinFt + c] : (CodeT)0;
+  }
+  // feature-major: kBinRows contiguous codes per feature
+  for (int e = threadIdx.x; e < nf * rows; e += 256) {
+    const int fl = e / rows;
+    const int r = e - fl * rows;
+    codes_fm[(int64_t)(f0 + fl) * n + r0 + r] = tile[r * kBinFt + fl];
+  }
+  if (threadIdx.x < nf && s_flag[threadIdx.x]) atomicOr(&flags[f0 + threadIdx.x], s_flag[threadIdx.x]);
+}
+
+int edges_sample_rows(bool x64) { return x64 ? 16384 : 32768; }
+
+void launch_edges(hipStream_t stream, const void* X, bool x64, int64_t n, int F, int s, int limit,
+                  void* edges, int32_t* nbins, uint8_t* exact) {
+  if (F <= 0) return;
+  int S = 1;
+  while (S < s) S <<= 1;
+  const int xb = x64 ? 8 : 4;
+  const size_t lds = (size_t)S * xb + (size_t)kEdgeHash * xb;
+  if (s > edges_sample_rows(x64)) throw std::runtime_error("edges sample exceeds LDS");
+#define MT_EDGES(XT)                                                                           \
+  MT_HIP_CHECK(hipFuncSetAttribute((const void*)edges_kernel<XT>,                              \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));     \
+  hipLaunchKernelGGL(edges_kernel<XT>, dim3(F), dim3(kEdgeThreads), lds, stream, (const XT*)X, \
+                     n, F, s, S, limit, (XT*)edges, nbins, exact);
+  if (x64) {
+    MT_EDGES(double)
+  } else {
+    MT_EDGES(float)
+  }
+#undef MT_EDGES
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_bin(hipStream_t stream, const void* X, bool x64, int64_t n, int F, const void* edges,
+                int Bmax, const int32_t* nbins, const uint8_t* exact, void* codes_rm,
+                int row_elems, void* codes_fm, int code_bytes, int32_t* flags) {
+  if (n <= 0) return;
+  const int xb = x64 ? 8 : 4;
+  const size_t edge_bytes = (size_t)kBinFt * Bmax * xb;
+  const bool lds_edges = edge_bytes <= 64 * 1024;
+  const size_t lds = (lds_edges ? edge_bytes : 0) + (size_t)kBinRows * kBinFt * code_bytes;
+  int steps0 = 1;
+  while (steps0 * 2 <= Bmax) steps0 *= 2;
+  dim3 grid((unsigned)((n + kBinRows - 1) / kBinRows), (unsigned)((F + kBinFt - 1) / kBinFt));
+#define MT_BIN(XT, CT, L)                                                                      \
+  {                                                                                            \
+    MT_HIP_CHECK(hipFuncSetAttribute((const void*)bin_kernel<XT, CT, L>,                       \
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));   \
+    hipLaunchKernelGGL((bin_kernel<XT, CT, L>), grid, dim3(256), lds, stream, (const XT*)X, n, \
+                       F, (const XT*)edges, Bmax, steps0, nbins, exact, (CT*)codes_rm,         \
+                       row_elems, (CT*)codes_fm, flags);                                       \
+  }
+#define MT_BIN2(XT, CT)      \
+  if (lds_edges) {           \
+    MT_BIN(XT, CT, true)     \
+  } else {                   \
+    MT_BIN(XT, CT, false)    \
+  }
+  if (x64) {
+    if (code_bytes == 1) {
+      MT_BIN2(double, uint8_t)
+    } else {
+      MT_BIN2(double, uint16_t)
+    }
+  } else {
+    if (code_bytes == 1) {
+      MT_BIN2(float, uint8_t)
+    } else {
+      MT_BIN2(float, uint16_t)
+    }
+  }
+#undef MT_BIN2
+#undef MT_BIN
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace mt

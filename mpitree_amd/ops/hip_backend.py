@@ -72,75 +72,58 @@ class _Uploader:
         return outs
 
 
-def gpu_bin_features(X: torch.Tensor, max_bins=256, sample_rows: int = 1 << 17):
+def gpu_bin_features(X: torch.Tensor, max_bins=256, sample_rows: int | None = None):
     """Bin a device feature matrix; returns (BinMapper, codes_rm, codes_fm, nbins_dev).
 
-    Edges come from a deterministic strided row sample sorted on the device;
-    features whose sample has at most ``max_bins`` distinct values are binned
-    in exact mode and verified by the bin kernel, falling back to the full
-    column when the sample missed a value.
+    Edges come from a deterministic strided row sample processed on the device
+    (binning.hip ``edges_kernel``): features whose sample has at most
+    ``max_bins`` distinct values are binned in exact mode and verified by the
+    bin kernel, which falls back to the full column when the sample missed a
+    value. The bin kernel also rejects non-finite input. Two small D2H reads
+    (edges + the verification flags) are the only host synchronisations.
     """
     hip = native.hip()
     n, F = X.shape
     dev = X.device
+    x64 = X.dtype == torch.float64
     limit = MAX_BINS_LIMIT if max_bins is None else int(max_bins)
-    if n > sample_rows:
-        ridx = (torch.arange(sample_rows, device=dev, dtype=torch.int64) * n) // sample_rows
-        S = X.index_select(0, ridx)
-    else:
-        S = X
-    s = S.shape[0]
-    srt = torch.sort(S, dim=0).values.t().contiguous()  # [F, s]
-    distinct = torch.ones((F, s), dtype=torch.bool, device=dev)
-    if s > 1:
-        distinct[:, 1:] = srt[:, 1:] != srt[:, :-1]
-    nuniq = distinct.sum(1)
-    exact = nuniq <= limit
-    # exact edges: distinct values compacted per row
-    pos = torch.cumsum(distinct, 1) - 1
-    width = limit + 1
-    pos = torch.where(distinct & exact[:, None], pos, torch.full_like(pos, limit))
-    edges = torch.full((F, width), float("inf"), dtype=X.dtype, device=dev)
-    edges.scatter_(1, pos, srt)
-    # quantile edges for the others
-    if (~exact).any():
-        k = torch.arange(1, limit + 1, device=dev, dtype=torch.int64)
-        qi = torch.clamp((k * s + limit - 1) // limit - 1, max=s - 1)
-        qv = srt[:, qi]  # [F, limit] sorted
-        qd = torch.ones_like(qv, dtype=torch.bool)
-        qd[:, 1:] = qv[:, 1:] != qv[:, :-1]
-        qpos = torch.cumsum(qd, 1) - 1
-        qpos = torch.where(qd & ~exact[:, None], qpos, torch.full_like(qpos, limit))
-        qedges = torch.full((F, width), float("inf"), dtype=X.dtype, device=dev)
-        qedges.scatter_(1, qpos, qv)
-        edges = torch.where(exact[:, None], edges, qedges)
-    edges = edges[:, :limit]
-    nb = torch.isfinite(edges).sum(1).to(torch.int32)
-    host_edges = edges.double().cpu().numpy()
-    host_nb = nb.cpu().numpy()
-    host_exact = exact.cpu().numpy()
+    s = min(n, int(sample_rows or hip.edges_sample_rows(x64)))
+    limit_eff = limit
+    edges = torch.empty((F, limit_eff), dtype=X.dtype, device=dev)
+    nb = torch.empty(F, dtype=torch.int32, device=dev)
+    exact = torch.empty(F, dtype=torch.uint8, device=dev)
+    hip.edges(_stream(), X.data_ptr(), x64, n, F, s, limit_eff, edges.data_ptr(), nb.data_ptr(),
+              exact.data_ptr())
+    # one packed D2H: edges (fp64), bin counts, exact flags
+    pack = torch.cat([edges.double().reshape(-1), nb.double(), exact.double()])
+    host = pack.cpu().numpy()
+    host_edges = host[: F * limit_eff].reshape(F, limit_eff).copy()
+    host_nb = host[F * limit_eff : F * limit_eff + F].astype(np.int64)
+    host_exact = host[F * limit_eff + F :].astype(bool)
 
-    def run_bin(edges_t, nb_t, exact_t):
-        bmax = int(nb_t.max().item()) if F else 1
+    def run_bin(edges_t, nb_t, exact_t, bmax):
         cb = 1 if bmax <= 256 else 2
         ctype = torch.uint8 if cb == 1 else torch.int16
         row_elems = ((F * cb + 3) // 4) * 4 // cb
         codes_rm = torch.empty((n, row_elems), dtype=ctype, device=dev)
         codes_fm = torch.empty((F, n), dtype=ctype, device=dev)
-        bad = torch.zeros(F, dtype=torch.int32, device=dev)
+        flags = torch.zeros(F, dtype=torch.int32, device=dev)
         et = edges_t[:, :bmax].contiguous()
-        hip.bin(_stream(), X.data_ptr(), X.dtype == torch.float64, n, F, et.data_ptr(), bmax,
-                nb_t.data_ptr(), exact_t.to(torch.uint8).contiguous().data_ptr(),
-                codes_rm.data_ptr(), row_elems, codes_fm.data_ptr(), cb, bad.data_ptr())
-        return codes_rm, codes_fm, bad, bmax
+        hip.bin(_stream(), X.data_ptr(), x64, n, F, et.data_ptr(), bmax, nb_t.data_ptr(),
+                exact_t.contiguous().data_ptr(), codes_rm.data_ptr(), row_elems,
+                codes_fm.data_ptr(), cb, flags.data_ptr())
+        return codes_rm, codes_fm, flags
 
-    codes_rm, codes_fm, bad, _ = run_bin(edges, nb, exact)
-    bad_h = bad.cpu().numpy()
-    if bad_h.any():
+    bmax = int(max(1, host_nb.max())) if F else 1
+    codes_rm, codes_fm, flags = run_bin(edges, nb, exact, bmax)
+    fl = flags.cpu().numpy()
+    if (fl & 2).any():
+        raise ValueError("Input X contains NaN or infinity.")
+    if (fl & 1).any():
         # the sample missed values of an "exact" feature: use the full column
-        for f in np.nonzero(bad_h)[0]:
+        for f in np.nonzero(fl & 1)[0]:
             col = X[:, f]
-            u = torch.unique(col)
+            u = torch.unique(torch.where(col == 0, torch.zeros_like(col), col))
             if u.numel() <= limit:
                 e = u
                 host_exact[f] = True
@@ -150,14 +133,21 @@ def gpu_bin_features(X: torch.Tensor, max_bins=256, sample_rows: int = 1 << 17):
                 qi = torch.clamp((k * n + limit - 1) // limit - 1, max=n - 1)
                 e = torch.unique(srtc[qi])
                 host_exact[f] = False
+            if e.numel() > edges.shape[1]:
+                wider = torch.full((F, e.numel()), float("inf"), dtype=X.dtype, device=dev)
+                wider[:, : edges.shape[1]] = edges
+                edges = wider
+                host_edges = np.concatenate(
+                    [host_edges, np.full((F, e.numel() - host_edges.shape[1]), np.inf)], 1)
             edges[f].fill_(float("inf"))
             edges[f, : e.numel()] = e
             host_edges[f] = np.inf
             host_edges[f, : e.numel()] = e.double().cpu().numpy()
             host_nb[f] = e.numel()
         nb = torch.from_numpy(host_nb.astype(np.int32)).to(dev)
-        exact = torch.from_numpy(host_exact).to(dev)
-        codes_rm, codes_fm, bad, _ = run_bin(edges, nb, exact)
+        exact = torch.from_numpy(host_exact.astype(np.uint8)).to(dev)
+        bmax = int(max(1, host_nb.max()))
+        codes_rm, codes_fm, flags = run_bin(edges, nb, exact, bmax)
     mapper = BinMapper(
         edges=[host_edges[f, : host_nb[f]].copy() for f in range(F)],
         exact=host_exact.astype(bool),

@@ -160,3 +160,32 @@ def test_gpu_device_assembly_matches_host(monkeypatch, regression):
         assert np.array_equal(dev.value, host.value)
         assert np.array_equal(dev.meta["sum_fixed"], host.meta["sum_fixed"])
     assert np.array_equal(dev.meta["term"], host.meta["term"])
+
+
+def test_gpu_edges_match_host_mapper():
+    """Device edges (hash-set exact mode, bitonic-sort quantiles) == host BinMapper."""
+    from mpitree_amd.core.binning import fit_bin_mapper
+    from mpitree_amd.ops.hip_backend import gpu_bin_features
+
+    rng = np.random.default_rng(3)
+    n = 20000  # below the device sample size: both sides see every row
+    X = np.stack([
+        rng.normal(size=n),                       # continuous -> quantiles
+        rng.integers(0, 7, size=n),               # 7 levels -> exact
+        rng.integers(0, 256, size=n),             # 256 levels -> exact at the limit
+        rng.integers(0, 300, size=n),             # 300 levels -> quantiles
+        np.where(rng.random(n) < 0.5, -0.0, 0.0),  # signed zeros are one value
+    ], 1).astype(np.float32)
+    host = fit_bin_mapper(X, 256)
+    mapper, codes_rm, codes_fm, nb = gpu_bin_features(torch.from_numpy(X).cuda(), 256)
+    for f in range(X.shape[1]):
+        assert bool(mapper.exact[f]) == bool(host.exact[f]), f
+        assert np.array_equal(mapper.edges[f], host.edges[f]), f
+    assert np.array_equal(codes_fm.cpu().numpy().T[:, :5], host.transform(X))
+
+
+def test_gpu_rejects_nonfinite_tensor():
+    X = torch.zeros((1000, 3), device="cuda")
+    X[17, 1] = float("nan")
+    with pytest.raises(ValueError, match="NaN or infinity"):
+        DecisionTreeClassifier(device="cuda").fit(X, torch.zeros(1000, device="cuda"))
