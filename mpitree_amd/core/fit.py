@@ -109,6 +109,15 @@ def _encode_labels(y, n):
     if _is_tensor(y):
         if y.dim() != 1 or y.shape[0] != n:
             raise ValueError("y must be 1-D with one label per row")
+        if not torch.is_floating_point(y) and y.dtype != torch.bool and n > 0:
+            # integer labels: a presence table instead of a sort (one small sync)
+            lo, hi = torch.stack(torch.aminmax(y)).tolist()
+            if hi - lo < (1 << 22):
+                yz = (y - lo).long() if lo else y.long()
+                present = torch.bincount(yz, minlength=hi - lo + 1) > 0
+                lut = torch.cumsum(present, 0, dtype=torch.int32) - 1
+                classes = (torch.nonzero(present).squeeze(1) + lo).to(y.dtype)
+                return classes.cpu().numpy(), lut[yz]
         classes, enc = torch.unique(y, return_inverse=True)
         return classes.cpu().numpy(), enc.to(torch.int32)
     y = np.asarray(y)

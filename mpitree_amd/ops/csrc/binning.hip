@@ -227,8 +227,11 @@ __global__ __launch_bounds__(256) void bin_kernel(const XT* __restrict__ X, int6
   __shared__ int s_flag[kBinFt];
   __shared__ int32_t s_nb[kBinFt];
   __shared__ uint8_t s_ex[kBinFt];
-  XT* s_edges = reinterpret_cast<XT*>(smem);  // [kBinFt][Bmax] when staged
-  CodeT* tile = reinterpret_cast<CodeT*>(smem + (kLds ? (size_t)kBinFt * Bmax * sizeof(XT) : 0));
+  // [kBinFt][ES] when staged; the odd row stride ES spreads the 16 features'
+  // concurrent searches over different LDS banks
+  const int ES = Bmax | 1;
+  XT* s_edges = reinterpret_cast<XT*>(smem);
+  CodeT* tile = reinterpret_cast<CodeT*>(smem + (kLds ? (size_t)kBinFt * ES * sizeof(XT) : 0));
   const int64_t r0 = blockIdx.x * (int64_t)kBinRows;
   const int rows = (int)min<int64_t>(kBinRows, n - r0);
   const int f0 = blockIdx.y * kBinFt;
@@ -239,7 +242,10 @@ __global__ __launch_bounds__(256) void bin_kernel(const XT* __restrict__ X, int6
     s_ex[threadIdx.x] = threadIdx.x < nf ? exact[f0 + threadIdx.x] : 0;
   }
   if constexpr (kLds) {
-    for (int e = threadIdx.x; e < nf * Bmax; e += 256) s_edges[e] = edges[(int64_t)f0 * Bmax + e];
+    for (int e = threadIdx.x; e < nf * Bmax; e += 256) {
+      const int fl = e / Bmax, b = e - fl * Bmax;
+      s_edges[fl * ES + b] = edges[(int64_t)f0 * Bmax + e];
+    }
   }
   __syncthreads();
   // element e = threadIdx.x + 256 k -> (row e / 16, feature e % 16): a wave reads
@@ -261,7 +267,7 @@ __global__ __launch_bounds__(256) void bin_kernel(const XT* __restrict__ X, int6
     for (int k = 0; k < kBinPer; ++k) {
       const int fl = (threadIdx.x + 256 * k) % kBinFt;
       const int p = pos[k] + step;
-      const XT* ed = kLds ? s_edges + fl * Bmax : edges + (int64_t)(f0 + fl) * Bmax;
+      const XT* ed = kLds ? s_edges + fl * ES : edges + (int64_t)(f0 + fl) * Bmax;
       if (p <= nb[k] && ed[p - 1] < v[k]) pos[k] = p;
     }
   }
@@ -270,7 +276,7 @@ __global__ __launch_bounds__(256) void bin_kernel(const XT* __restrict__ X, int6
     const int e = threadIdx.x + 256 * k;
     const int r = e / kBinFt, fl = e % kBinFt;
     if (!ok[k]) continue;
-    const XT* ed = kLds ? s_edges + fl * Bmax : edges + (int64_t)(f0 + fl) * Bmax;
+    const XT* ed = kLds ? s_edges + fl * ES : edges + (int64_t)(f0 + fl) * Bmax;
     const int code = pos[k] < nb[k] ? pos[k] : nb[k] - 1;
     int fg = 0;
     if (s_ex[fl] && !(ed[code] == v[k])) fg |= 1;
@@ -325,7 +331,7 @@ void launch_bin(hipStream_t stream, const void* X, bool x64, int64_t n, int F, c
                 int row_elems, void* codes_fm, int code_bytes, int32_t* flags) {
   if (n <= 0) return;
   const int xb = x64 ? 8 : 4;
-  const size_t edge_bytes = (size_t)kBinFt * Bmax * xb;
+  const size_t edge_bytes = (size_t)kBinFt * (Bmax | 1) * xb;
   const bool lds_edges = edge_bytes <= 64 * 1024;
   const size_t lds = (lds_edges ? edge_bytes : 0) + (size_t)kBinRows * kBinFt * code_bytes;
   int steps0 = 1;
