@@ -247,9 +247,16 @@ def fit_tree(
             finisher_rows = 0
         finisher_rows = min(int(finisher_rows), be.max_finisher_rows)
         params.finisher_rows = int(finisher_rows)
-        builder = LevelwiseBuilder(be, params, comm)
-        ta = builder.fit(hi - lo, C, F, edges=mapper.padded_edges(), y_exp=y_exp)
-        eng = "hip-levelwise"
+        from ..ops.device_grower import DeviceGrower, device_loop_supported
+
+        if device_loop_supported(be, params, comm):
+            builder = DeviceGrower(be, params)
+            ta = builder.fit(hi - lo, C, F, mapper.padded_edges(), y_exp)
+            eng = "hip-device-loop"
+        else:
+            builder = LevelwiseBuilder(be, params, comm)
+            ta = builder.fit(hi - lo, C, F, edges=mapper.padded_edges(), y_exp=y_exp)
+            eng = "hip-levelwise"
         timings.update(builder.timings)
         stats = dict(builder.stats)
     else:

@@ -16,14 +16,17 @@ namespace mt {
 int hist_feature_tile(int F_h, int B, int C, bool reg, int lds_budget);
 int64_t hist_slab_words(int F_h, int B, int C, bool reg);
 void launch_hist(hipStream_t, const void*, int, int64_t, const uint32_t*, const void*, int,
-                 const int64_t*, int, void*, void*, int, int, int, int, bool, int);
+                 const int64_t*, int, void*, void*, int, int, int, int, bool, int,
+                 const int32_t*);
 void launch_hist_reduce(hipStream_t, const int64_t*, int, int, const void*, void*, int, int, int,
-                        bool);
-void launch_hist_derive(hipStream_t, const int64_t*, int, const void*, void*, int64_t, bool);
+                        bool, const int32_t*);
+void launch_hist_derive(hipStream_t, const int64_t*, int, const void*, void*, int64_t, bool,
+                        const int32_t*);
 void launch_scan(hipStream_t, const void*, const int64_t*, int, const int32_t*, int, int, int,
-                 int, int, int, double*, int32_t*, int64_t*, const double*, int);
+                 int, int, int, double*, int32_t*, int64_t*, const double*, int,
+                 const int32_t*);
 void launch_partition(hipStream_t, const void*, int, int64_t, uint32_t*, uint32_t*, uint32_t,
-                      const int64_t*, int, const int64_t*, int32_t*);
+                      const int64_t*, int, const int64_t*, int32_t*, const int32_t*);
 void launch_seg_stats(hipStream_t, const uint32_t*, const void*, int, bool, const int64_t*, int,
                       void*, int);
 void launch_init_idx(hipStream_t, uint32_t*, const int32_t*, int, int64_t);
@@ -52,6 +55,32 @@ struct AsmOut {
   double* value;
 };
 int asm_tiles(int64_t P);
+struct LevelLists {
+  int64_t* pos;
+  int64_t* start;
+  int32_t* cnt;
+  int32_t* depth;
+  int32_t* stats;
+  int64_t* items;
+  int64_t* red;
+  int64_t* der;
+  int32_t* ctl;
+};
+struct PlanArgs {
+  LevelLists cur, nxt;
+  const int64_t* rec;
+  int64_t* split;
+  int64_t* pitems;
+  int32_t* cursors;
+  int32_t* pctl;
+  int32_t* pos_rec;
+  int32_t* pos_st;
+  int64_t* jobs;
+  int32_t* job_count;
+  int C, max_depth, n_cu;
+  int64_t mss, msl, fr;
+};
+void launch_grow_plan(hipStream_t, const PlanArgs&);
 int edges_sample_rows(bool x64);
 void launch_edges(hipStream_t, const void*, bool, int64_t, int, int, int, void*, int32_t*,
                   uint8_t*);
@@ -73,34 +102,46 @@ PYBIND11_MODULE(_hip, m) {
   m.def("hist_slab_words", &mt::hist_slab_words);
   m.def("hist", [](uintptr_t s, uintptr_t codes, int cb, int64_t rs, uintptr_t idx, uintptr_t y,
                    int lab_shift, uintptr_t items, int n_items, uintptr_t hist, uintptr_t slab,
-                   int F_h, int f_lo, int B, int C, bool reg, int lds) {
+                   int F_h, int f_lo, int B, int C, bool reg, int lds, uintptr_t dcount) {
     mt::launch_hist(S(s), P<void>(codes), cb, rs, P<uint32_t>(idx), P<void>(y), lab_shift,
                     P<int64_t>(items), n_items, P<void>(hist), P<void>(slab), F_h, f_lo, B, C,
-                    reg, lds);
-  });
+                    reg, lds, P<int32_t>(dcount));
+  }, "", py::arg("s"), py::arg("codes"), py::arg("cb"), py::arg("rs"), py::arg("idx"),
+     py::arg("y"), py::arg("lab_shift"), py::arg("items"), py::arg("n_items"), py::arg("hist"),
+     py::arg("slab"), py::arg("F_h"), py::arg("f_lo"), py::arg("B"), py::arg("C"), py::arg("reg"),
+     py::arg("lds"), py::arg("dcount") = 0);
   m.def("hist_reduce", [](uintptr_t s, uintptr_t red, int n, int max_k, uintptr_t slab,
-                          uintptr_t hist, int F_h, int B, int C, bool reg) {
+                          uintptr_t hist, int F_h, int B, int C, bool reg, uintptr_t dcount) {
     mt::launch_hist_reduce(S(s), P<int64_t>(red), n, max_k, P<void>(slab), P<void>(hist), F_h, B,
-                           C, reg);
-  });
+                           C, reg, P<int32_t>(dcount));
+  }, "", py::arg("s"), py::arg("red"), py::arg("n"), py::arg("max_k"), py::arg("slab"),
+     py::arg("hist"), py::arg("F_h"), py::arg("B"), py::arg("C"), py::arg("reg"),
+     py::arg("dcount") = 0);
   m.def("hist_derive", [](uintptr_t s, uintptr_t der, int n, uintptr_t prev, uintptr_t hist,
-                          int64_t E, bool is64) {
-    mt::launch_hist_derive(S(s), P<int64_t>(der), n, P<void>(prev), P<void>(hist), E, is64);
-  });
+                          int64_t E, bool is64, uintptr_t dcount) {
+    mt::launch_hist_derive(S(s), P<int64_t>(der), n, P<void>(prev), P<void>(hist), E, is64,
+                           P<int32_t>(dcount));
+  }, "", py::arg("s"), py::arg("der"), py::arg("n"), py::arg("prev"), py::arg("hist"),
+     py::arg("E"), py::arg("is64"), py::arg("dcount") = 0);
   m.def("scan", [](uintptr_t s, uintptr_t hist, uintptr_t nodes, int k, uintptr_t nbins, int F_h,
                    int f_lo, int B, int C, int crit, int msl, uintptr_t cost, uintptr_t bins,
-                   uintptr_t rec, uintptr_t xtab, int xtab_n) {
+                   uintptr_t rec, uintptr_t xtab, int xtab_n, uintptr_t dcount) {
     mt::launch_scan(S(s), P<void>(hist), P<int64_t>(nodes), k, P<int32_t>(nbins), F_h, f_lo, B, C,
                     crit, msl, P<double>(cost), P<int32_t>(bins), P<int64_t>(rec),
-                    P<double>(xtab), xtab_n);
-  });
+                    P<double>(xtab), xtab_n, P<int32_t>(dcount));
+  }, "", py::arg("s"), py::arg("hist"), py::arg("nodes"), py::arg("k"), py::arg("nbins"),
+     py::arg("F_h"), py::arg("f_lo"), py::arg("B"), py::arg("C"), py::arg("crit"), py::arg("msl"),
+     py::arg("cost"), py::arg("bins"), py::arg("rec"), py::arg("xtab"), py::arg("xtab_n"),
+     py::arg("dcount") = 0);
   m.def("partition", [](uintptr_t s, uintptr_t codes_fm, int cb, int64_t n_rows, uintptr_t idx,
                         uintptr_t tmp, uint32_t mask, uintptr_t items, int n_items,
-                        uintptr_t split, uintptr_t cursors) {
+                        uintptr_t split, uintptr_t cursors, uintptr_t dcount) {
     mt::launch_partition(S(s), P<void>(codes_fm), cb, n_rows, P<uint32_t>(idx),
                          P<uint32_t>(tmp), mask, P<int64_t>(items), n_items, P<int64_t>(split),
-                         P<int32_t>(cursors));
-  });
+                         P<int32_t>(cursors), P<int32_t>(dcount));
+  }, "", py::arg("s"), py::arg("codes_fm"), py::arg("cb"), py::arg("n_rows"), py::arg("idx"),
+     py::arg("tmp"), py::arg("mask"), py::arg("items"), py::arg("n_items"), py::arg("split"),
+     py::arg("cursors"), py::arg("dcount") = 0);
   m.def("seg_stats", [](uintptr_t s, uintptr_t idx, uintptr_t y, int lab_shift, bool reg,
                         uintptr_t items, int n_items, uintptr_t out, int C) {
     mt::launch_seg_stats(S(s), P<uint32_t>(idx), P<void>(y), lab_shift, reg, P<int64_t>(items),
@@ -138,6 +179,23 @@ PYBIND11_MODULE(_hip, m) {
                       P<int64_t>(tiny), tiny_grid, P<int64_t>(prof));
   });
   m.def("asm_tiles", &mt::asm_tiles);
+  // cur / nxt: dicts of device pointers {pos, start, cnt, depth, stats, items, red, der, ctl}
+  m.def("grow_plan", [](uintptr_t s, py::dict cur, py::dict nxt, uintptr_t rec, uintptr_t split,
+                        uintptr_t pitems, uintptr_t cursors, uintptr_t pctl, uintptr_t pos_rec,
+                        uintptr_t pos_st, uintptr_t jobs, uintptr_t job_count, int C,
+                        int max_depth, int n_cu, int64_t mss, int64_t msl, int64_t fr) {
+    auto lists = [](py::dict d) {
+      auto g = [&](const char* k) { return d[k].cast<uintptr_t>(); };
+      return mt::LevelLists{P<int64_t>(g("pos")),  P<int64_t>(g("start")), P<int32_t>(g("cnt")),
+                            P<int32_t>(g("depth")), P<int32_t>(g("stats")), P<int64_t>(g("items")),
+                            P<int64_t>(g("red")),  P<int64_t>(g("der")),   P<int32_t>(g("ctl"))};
+    };
+    mt::PlanArgs a{lists(cur),          lists(nxt),         P<int64_t>(rec),
+                   P<int64_t>(split),   P<int64_t>(pitems), P<int32_t>(cursors),
+                   P<int32_t>(pctl),    P<int32_t>(pos_rec), P<int32_t>(pos_st),
+                   P<int64_t>(jobs),    P<int32_t>(job_count), C, max_depth, n_cu, mss, msl, fr};
+    mt::launch_grow_plan(S(s), a);
+  });
   m.def("edges_sample_rows", &mt::edges_sample_rows);
   m.def("edges", [](uintptr_t s, uintptr_t X, bool x64, int64_t n, int F, int rows, int limit,
                     uintptr_t edges, uintptr_t nbins, uintptr_t exact) {

@@ -1,0 +1,370 @@
+// Device-driven level loop: the per-level planner.
+//
+// The reference grows depth-first with one Python recursion per node
+// (mpitree/tree/decision_tree.py:93-166). The level-wise engine batches a
+// whole depth into a few kernels, but a host-driven loop still pays a device
+// round trip and ~100 host numpy operations per level to turn the split
+// records into the next level's work lists. Here that bookkeeping runs on the
+// GPU: after scan/select, one workgroup (grow_plan_kernel) reads the level's
+// split records and writes
+//
+//   * every decided node into the pre-order position space (see assemble.hip):
+//     split nodes, and children that became leaves;
+//   * finisher jobs for children with at most ``finisher_rows`` rows;
+//   * the partition work list of this level's split nodes;
+//   * the next frontier, slot-ordered built-then-derived (the smaller child of
+//     a pair is built from rows, the larger derived as parent - sibling),
+//     with its histogram items / slab reductions / derive triples and counts.
+//
+// Every kernel of a level reads its work count from device memory (grids are
+// host-known upper bounds), so the host enqueues levels back to back with no
+// synchronisation and learns only at the end -- from one lagged 32-byte read
+// -- that the frontier is empty.
+#include "common.h"
+#include "criterion.h"
+
+namespace mt {
+
+constexpr int kPlanThreads = 1024;
+constexpr int kPlanWaves = kPlanThreads / kWave;
+
+// Level work lists (one set per level parity). ctl: int32
+// {0: K frontier nodes, 1: built nodes, 2: hist items, 3: slab reductions,
+//  4: derive triples, 5: split nodes, 6: partition items, 7: -}
+struct LevelLists {
+  int64_t* pos;     // [KMAX] pre-order position of each frontier slot
+  int64_t* start;   // [KMAX] row segment start
+  int32_t* cnt;     // [KMAX] rows
+  int32_t* depth;   // [KMAX]
+  int32_t* stats;   // [KMAX][C] class counts
+  int64_t* items;   // [IMAX][4] {slot, start, count, dest slab or -1}
+  int64_t* red;     // [KMAX][3] {slot, first slab, slabs}
+  int64_t* der;     // [KMAX][3] {slot, parent slot (previous level), sibling slot}
+  int32_t* ctl;     // [8]
+};
+
+struct PlanArgs {
+  LevelLists cur, nxt;
+  const int64_t* rec;  // [KMAX][5 + 2C] split records of the current level
+  int64_t* split;      // [KMAX][4] {start, count, feature, bin}
+  int64_t* pitems;     // [PMAX][3] {split j, start, count}
+  int32_t* cursors;    // [KMAX][2]
+  int32_t* pctl;       // [2] {split nodes, partition items} (aliases cur.ctl + 5)
+  int32_t* pos_rec;    // [P][6]
+  int32_t* pos_st;     // [P][C]
+  int64_t* jobs;       // [JMAX][5 + C] finisher jobs
+  int32_t* job_count;
+  int C, max_depth, n_cu;
+  int64_t mss, msl, fr;
+};
+
+__device__ __forceinline__ int plan_scan_excl(int v, int* s_w, int& total) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int incl = (int)wave_incl_scan_u32((uint32_t)v);
+  if (lane == kWave - 1) s_w[w] = incl;
+  __syncthreads();
+  int off = 0, tot = 0;
+  for (int k = 0; k < kPlanWaves; ++k) {
+    const int x = s_w[k];
+    off += k < w ? x : 0;
+    tot += x;
+  }
+  __syncthreads();
+  total = tot;
+  return off + incl - v;
+}
+
+// What happens to one frontier node and its children.
+struct Decision {
+  bool split;
+  int feature, bin;
+  int64_t nl, nr;
+  int fate[2];  // 0 leaf, 1 finisher job, 2 next frontier
+  int built;    // child index built from rows (-1 none), the other alive one is derived
+};
+
+__device__ Decision plan_decide(const PlanArgs& a, int i) {
+  const int C = a.C;
+  const int R = 5 + 2 * C;
+  const int64_t* r = a.rec + (int64_t)i * R;
+  Decision d;
+  const double gain = __longlong_as_double((long long)r[0]);
+  d.split = gain > -__builtin_inf();
+  d.feature = (int)r[1];
+  d.bin = (int)r[2];
+  const int64_t m = a.cur.cnt[i];
+  d.nl = r[3];
+  d.nr = m - d.nl;
+  d.fate[0] = d.fate[1] = 0;
+  d.built = -1;
+  if (!d.split) return d;
+  const int cd = a.cur.depth[i] + 1;
+  const bool depth_stop = a.max_depth >= 0 && cd >= a.max_depth;
+  for (int c = 0; c < 2; ++c) {
+    const int64_t cm = c == 0 ? d.nl : d.nr;
+    int nz = 0;
+    for (int k = 0; k < C; ++k) {
+      const int64_t lc = r[5 + k];
+      const int64_t v = c == 0 ? lc : (int64_t)a.cur.stats[(int64_t)i * C + k] - lc;
+      nz += v > 0;
+    }
+    const bool term = depth_stop || cm < a.mss || cm < 2 * a.msl || nz <= 1;
+    d.fate[c] = term ? 0 : ((a.fr > 0 && cm <= a.fr) ? 1 : 2);
+  }
+  if (d.fate[0] == 2 && d.fate[1] == 2)
+    d.built = d.nl <= d.nr ? 0 : 1;  // smaller child from rows (ties: left)
+  else if (d.fate[0] == 2)
+    d.built = 0;
+  else if (d.fate[1] == 2)
+    d.built = 1;
+  return d;
+}
+
+__global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
+  __shared__ int s_w[kPlanWaves];
+  __shared__ int s_carry[4];
+  __shared__ long long s_rows;
+  const int tid = threadIdx.x;
+  const int C = a.C;
+  const int K = a.cur.ctl[0];
+  // ---- pass 1: totals (built / derived next-frontier children, split nodes)
+  int nb_tot = 0, nd_tot = 0;
+  for (int b0 = 0; b0 < K; b0 += kPlanThreads) {
+    const int i = b0 + tid;
+    int nb = 0, nd = 0;
+    if (i < K) {
+      const Decision d = plan_decide(a, i);
+      nb = d.built >= 0 ? 1 : 0;
+      nd = (d.fate[0] == 2 && d.fate[1] == 2) ? 1 : 0;
+    }
+    int t;
+    plan_scan_excl(nb, s_w, t);
+    nb_tot += t;
+    plan_scan_excl(nd, s_w, t);
+    nd_tot += t;
+  }
+  const int NB = nb_tot;
+  // ---- pass 2: write decided nodes, jobs, split list, next frontier, derive list
+  if (tid == 0) {
+    s_carry[0] = 0;  // built slots
+    s_carry[1] = 0;  // derived slots
+    s_carry[2] = 0;  // split nodes
+    s_rows = 0;
+  }
+  __syncthreads();
+  long long built_rows = 0;
+  for (int b0 = 0; b0 < K; b0 += kPlanThreads) {
+    const int i = b0 + tid;
+    Decision d;
+    d.split = false;
+    d.built = -1;
+    d.fate[0] = d.fate[1] = 0;
+    if (i < K) d = plan_decide(a, i);
+    const int nb = d.built >= 0 ? 1 : 0;
+    const int nd = (d.fate[0] == 2 && d.fate[1] == 2) ? 1 : 0;
+    const int ns = d.split ? 1 : 0;
+    int tb, td, ts;
+    const int ob = plan_scan_excl(nb, s_w, tb) + s_carry[0];
+    const int od = plan_scan_excl(nd, s_w, td) + s_carry[1];
+    const int os = plan_scan_excl(ns, s_w, ts) + s_carry[2];
+    if (i < K) {
+      const int64_t pos = a.cur.pos[i];
+      const int64_t start = a.cur.start[i];
+      const int64_t m = a.cur.cnt[i];
+      const int depth = a.cur.depth[i];
+      const int32_t* st = a.cur.stats + (int64_t)i * C;
+      int32_t* P = a.pos_rec + pos * 6;
+      const int64_t* r = a.rec + (int64_t)i * (5 + 2 * C);
+      for (int k = 0; k < C; ++k) a.pos_st[pos * C + k] = st[k];
+      P[4] = depth;
+      P[5] = (int32_t)m;
+      if (!d.split) {
+        P[0] = -1;
+        P[1] = -1;
+        P[2] = -1;
+        P[3] = -1;
+      } else {
+        const int64_t cpos[2] = {pos + 1, pos + 2 * d.nl};
+        P[0] = d.feature;
+        P[1] = d.bin;
+        P[2] = (int32_t)cpos[0];
+        P[3] = (int32_t)cpos[1];
+        // partition list
+        int64_t* S = a.split + (int64_t)os * 4;
+        S[0] = start;
+        S[1] = m;
+        S[2] = d.feature;
+        S[3] = d.bin;
+        a.cursors[os * 2 + 0] = (int32_t)start;
+        a.cursors[os * 2 + 1] = (int32_t)(start + m);
+        const int cd = depth + 1;
+        int slot[2] = {-1, -1};
+        if (d.built >= 0) {
+          slot[d.built] = ob;
+          if (nd) slot[1 - d.built] = NB + od;
+        }
+        for (int c = 0; c < 2; ++c) {
+          const int64_t cm = c == 0 ? d.nl : d.nr;
+          const int64_t cs = c == 0 ? start : start + d.nl;
+          if (d.fate[c] == 0) {  // leaf: write it now
+            int32_t* Q = a.pos_rec + cpos[c] * 6;
+            Q[0] = -1;
+            Q[1] = -1;
+            Q[2] = -1;
+            Q[3] = -1;
+            Q[4] = cd;
+            Q[5] = (int32_t)cm;
+            for (int k = 0; k < C; ++k) {
+              const int64_t lc = r[5 + k];
+              a.pos_st[cpos[c] * C + k] = (int32_t)(c == 0 ? lc : st[k] - lc);
+            }
+          } else if (d.fate[c] == 1) {  // finisher job
+            const int j = atomicAdd(a.job_count, 1);
+            int64_t* J = a.jobs + (int64_t)j * (5 + C);
+            J[0] = cs;
+            J[1] = cm;
+            J[2] = cd;
+            J[3] = cpos[c];
+            J[4] = 0;
+            for (int k = 0; k < C; ++k) {
+              const int64_t lc = r[5 + k];
+              J[5 + k] = c == 0 ? lc : st[k] - lc;
+            }
+          } else {  // next frontier
+            const int sl = slot[c];
+            a.nxt.pos[sl] = cpos[c];
+            a.nxt.start[sl] = cs;
+            a.nxt.cnt[sl] = (int32_t)cm;
+            a.nxt.depth[sl] = cd;
+            for (int k = 0; k < C; ++k) {
+              const int64_t lc = r[5 + k];
+              a.nxt.stats[(int64_t)sl * C + k] = (int32_t)(c == 0 ? lc : st[k] - lc);
+            }
+            if (c == d.built) {
+              built_rows += cm;
+            } else {  // derived: parent slot i of this level, sibling built slot
+              int64_t* D = a.nxt.der + (int64_t)(sl - NB) * 3;
+              D[0] = sl;
+              D[1] = i;
+              D[2] = slot[d.built];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      s_carry[0] += tb;
+      s_carry[1] += td;
+      s_carry[2] += ts;
+    }
+    __syncthreads();
+  }
+  // total rows of built children -> histogram chunk size (about 2 items per CU)
+  {
+    long long v = built_rows;
+    for (int d = kWave / 2; d > 0; d >>= 1) v += __shfl_xor(v, d, kWave);
+    if (lane_id() == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&s_rows),
+                                  (unsigned long long)v);
+  }
+  __syncthreads();
+  const int ND = s_carry[1];
+  const int NS = s_carry[2];
+  const int K2 = NB + ND;
+  const long long total = s_rows;
+  long long chunk = (total + 2LL * a.n_cu - 1) / (2LL * a.n_cu);
+  chunk = chunk < 1024 ? 1024 : (chunk > 65535 ? 65535 : chunk);
+  // ---- pass 3: histogram items of the next level's built slots [0, NB)
+  if (tid == 0) {
+    s_carry[0] = 0;  // items
+    s_carry[1] = 0;  // slabs
+    s_carry[2] = 0;  // reductions
+  }
+  __syncthreads();
+  for (int b0 = 0; b0 < NB; b0 += kPlanThreads) {
+    const int sl = b0 + tid;
+    int64_t cnt = 0, kk = 0;
+    if (sl < NB) {
+      cnt = a.nxt.cnt[sl];
+      kk = (cnt + chunk - 1) / chunk;
+      if (kk < 1) kk = 1;
+    }
+    const int multi = kk > 1 ? 1 : 0;
+    int ti, tsl, tr;
+    const int oi = plan_scan_excl((int)kk, s_w, ti) + s_carry[0];
+    const int osl = plan_scan_excl(multi ? (int)kk : 0, s_w, tsl) + s_carry[1];
+    const int orr = plan_scan_excl(multi, s_w, tr) + s_carry[2];
+    if (sl < NB) {
+      const int64_t st0 = a.nxt.start[sl];
+      for (int64_t c = 0; c < kk; ++c) {
+        int64_t* it = a.nxt.items + (int64_t)(oi + c) * 4;
+        const int64_t c0 = c * chunk;
+        it[0] = sl;
+        it[1] = st0 + c0;
+        it[2] = (cnt - c0) < chunk ? (cnt - c0) : chunk;
+        it[3] = multi ? osl + c : -1;
+      }
+      if (multi) {
+        int64_t* rr = a.nxt.red + (int64_t)orr * 3;
+        rr[0] = sl;
+        rr[1] = osl;
+        rr[2] = kk;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      s_carry[0] += ti;
+      s_carry[1] += tsl;
+      s_carry[2] += tr;
+    }
+    __syncthreads();
+  }
+  const int n_items = s_carry[0];
+  const int n_red = s_carry[2];
+  // ---- pass 4: partition items of this level's split nodes (1024 rows each)
+  __syncthreads();
+  if (tid == 0) s_carry[3] = 0;
+  __syncthreads();
+  for (int b0 = 0; b0 < NS; b0 += kPlanThreads) {
+    const int j = b0 + tid;
+    int64_t cnt = 0, kk = 0;
+    if (j < NS) {
+      cnt = a.split[(int64_t)j * 4 + 1];
+      kk = (cnt + 1023) / 1024;
+      if (kk < 1) kk = 1;
+    }
+    int tp;
+    const int op = plan_scan_excl((int)kk, s_w, tp) + s_carry[3];
+    if (j < NS) {
+      const int64_t st0 = a.split[(int64_t)j * 4 + 0];
+      for (int64_t c = 0; c < kk; ++c) {
+        int64_t* it = a.pitems + (int64_t)(op + c) * 3;
+        const int64_t c0 = c * 1024;
+        it[0] = j;
+        it[1] = st0 + c0;
+        it[2] = (cnt - c0) < 1024 ? (cnt - c0) : 1024;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) s_carry[3] += tp;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    a.nxt.ctl[0] = K2;
+    a.nxt.ctl[1] = NB;
+    a.nxt.ctl[2] = n_items;
+    a.nxt.ctl[3] = n_red;
+    a.nxt.ctl[4] = ND;
+    a.nxt.ctl[5] = 0;
+    a.nxt.ctl[6] = 0;
+    a.pctl[0] = NS;
+    a.pctl[1] = s_carry[3];
+  }
+}
+
+void launch_grow_plan(hipStream_t stream, const PlanArgs& a) {
+  hipLaunchKernelGGL(grow_plan_kernel, dim3(1), dim3(kPlanThreads), 0, stream, a);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace mt

@@ -44,7 +44,9 @@ __global__ __launch_bounds__(kHistThreads) void hist_cls_lds_kernel(
     const uint32_t* __restrict__ codes, int64_t row_words, const uint32_t* __restrict__ idx,
     const int32_t* __restrict__ y, RowLab rl, const int64_t* __restrict__ items,
     uint32_t* __restrict__ hist, uint32_t* __restrict__ slab, int F_h, int f_lo, int B, int C,
-    int ft, int lane_shift) {
+    int ft, int lane_shift, const int32_t* __restrict__ dcount) {
+  // dcount (optional): device-side item count; the grid is an upper bound
+  if (dcount && (int)blockIdx.x >= *dcount) return;
   extern __shared__ uint32_t lds[];
   constexpr int cpw = 4 / sizeof(CodeT);  // codes per 32-bit word
   const int W = (C + 1) >> 1;
@@ -246,7 +248,9 @@ __global__ __launch_bounds__(256) void hist_reg_global_kernel(
 // the (zeroed) histogram.
 __global__ __launch_bounds__(256) void zero_slots_kernel(const int64_t* __restrict__ red,
                                                          uint32_t* __restrict__ hist,
-                                                         int64_t E) {
+                                                         int64_t E,
+                                                         const int32_t* __restrict__ dcount) {
+  if (dcount && (int)blockIdx.y >= *dcount) return;
   const int64_t slot = red[blockIdx.y * 3 + 0];
   if ((E & 3) == 0) {  // every slot base is 16-B aligned
     uint4* h = reinterpret_cast<uint4*>(hist + slot * E);
@@ -262,7 +266,9 @@ __global__ __launch_bounds__(256) void zero_slots_kernel(const int64_t* __restri
 
 __global__ __launch_bounds__(256) void hist_reduce_cls_kernel(
     const int64_t* __restrict__ red, const uint32_t* __restrict__ slab,
-    uint32_t* __restrict__ hist, int64_t Ep, int C, int W, int G) {
+    uint32_t* __restrict__ hist, int64_t Ep, int C, int W, int G,
+    const int32_t* __restrict__ dcount) {
+  if (dcount && (int)blockIdx.y >= *dcount) return;
   const int64_t slot = red[blockIdx.y * 3 + 0];
   const int64_t first = red[blockIdx.y * 3 + 1];
   const int64_t k = red[blockIdx.y * 3 + 2];
@@ -305,7 +311,9 @@ __global__ __launch_bounds__(256) void hist_reduce_reg_kernel(const int64_t* __r
 template <typename T>
 __global__ __launch_bounds__(256) void hist_derive_kernel(const int64_t* __restrict__ der,
                                                           const T* __restrict__ prev,
-                                                          T* __restrict__ hist, int64_t E) {
+                                                          T* __restrict__ hist, int64_t E,
+                                                          const int32_t* __restrict__ dcount) {
+  if (dcount && (int)blockIdx.y >= *dcount) return;
   const int64_t slot = der[blockIdx.y * 3 + 0];
   const int64_t ps = der[blockIdx.y * 3 + 1];
   const int64_t ss = der[blockIdx.y * 3 + 2];
@@ -377,7 +385,7 @@ int64_t hist_slab_words(int F_h, int B, int C, bool reg) {
 void launch_hist(hipStream_t stream, const void* codes, int code_bytes, int64_t row_stride_bytes,
                  const uint32_t* idx, const void* y, int lab_shift, const int64_t* items,
                  int n_items, void* hist, void* slab, int F_h, int f_lo, int B, int C, bool reg,
-                 int lds_budget) {
+                 int lds_budget, const int32_t* dcount) {
   if (n_items <= 0) return;
   const int ft = hist_feature_tile(F_h, B, C, reg, lds_budget);
   RowLab rl{lab_shift ? ((1u << lab_shift) - 1u) : 0xffffffffu, lab_shift};
@@ -446,7 +454,7 @@ void launch_hist(hipStream_t stream, const void* codes, int code_bytes, int64_t 
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));    \
   hipLaunchKernelGGL((hist_cls_lds_kernel<CT, V>), grid, dim3(kHistThreads), lds, stream,     \
                      (const uint32_t*)codes, row_words, idx, (const int32_t*)y, rl, items,    \
-                     (uint32_t*)hist, (uint32_t*)slab, F_h, f_lo, B, C, ft, shift);
+                     (uint32_t*)hist, (uint32_t*)slab, F_h, f_lo, B, C, ft, shift, dcount);
   if (code_bytes == 1) {
     if (vec4) {
       MT_CLS(uint8_t, 4)
@@ -465,7 +473,8 @@ void launch_hist(hipStream_t stream, const void* codes, int code_bytes, int64_t 
 }
 
 void launch_hist_reduce(hipStream_t stream, const int64_t* red, int n_red, int max_k,
-                        const void* slab, void* hist, int F_h, int B, int C, bool reg) {
+                        const void* slab, void* hist, int F_h, int B, int C, bool reg,
+                        const int32_t* dcount) {
   if (n_red <= 0) return;
   if (reg) {
     const int64_t E = (int64_t)F_h * B * 2;
@@ -480,28 +489,28 @@ void launch_hist_reduce(hipStream_t stream, const int64_t* red, int n_red, int m
   const int64_t Eu = (int64_t)F_h * B * C;
   hipLaunchKernelGGL(zero_slots_kernel, dim3((unsigned)std::min<int64_t>((Eu / 4 + 255) / 256, 256),
                                              n_red),
-                     dim3(256), 0, stream, red, (uint32_t*)hist, Eu);
+                     dim3(256), 0, stream, red, (uint32_t*)hist, Eu, dcount);
   MT_HIP_CHECK(hipGetLastError());
   const int G = 16;
   const int groups = (max_k + G - 1) / G;
   dim3 grid((unsigned)((Ep + 255) / 256), n_red, groups);
   hipLaunchKernelGGL(hist_reduce_cls_kernel, grid, dim3(256), 0, stream, red,
-                     (const uint32_t*)slab, (uint32_t*)hist, Ep, C, W, G);
+                     (const uint32_t*)slab, (uint32_t*)hist, Ep, C, W, G, dcount);
   MT_HIP_CHECK(hipGetLastError());
 }
 
 void launch_hist_derive(hipStream_t stream, const int64_t* der, int n_der, const void* prev,
-                        void* hist, int64_t E, bool is64) {
+                        void* hist, int64_t E, bool is64, const int32_t* dcount) {
   if (n_der <= 0) return;
   int gx = (int)std::min<int64_t>((E / 4 + 255) / 256, 256);
   if (gx < 1) gx = 1;
   dim3 grid(gx, n_der);
   if (is64)
     hipLaunchKernelGGL(hist_derive_kernel<int64_t>, grid, dim3(256), 0, stream, der,
-                       (const int64_t*)prev, (int64_t*)hist, E);
+                       (const int64_t*)prev, (int64_t*)hist, E, dcount);
   else
     hipLaunchKernelGGL(hist_derive_kernel<uint32_t>, grid, dim3(256), 0, stream, der,
-                       (const uint32_t*)prev, (uint32_t*)hist, E);
+                       (const uint32_t*)prev, (uint32_t*)hist, E, dcount);
   MT_HIP_CHECK(hipGetLastError());
 }
 

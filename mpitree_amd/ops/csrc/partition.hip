@@ -29,7 +29,9 @@ template <typename CodeT>
 __global__ __launch_bounds__(kPartThreads) void partition_kernel(
     const CodeT* __restrict__ codes_fm, int64_t n_rows, const uint32_t* __restrict__ idx,
     uint32_t* __restrict__ tmp, uint32_t mask, const int64_t* __restrict__ items,
-    const int64_t* __restrict__ split, int32_t* __restrict__ cursors) {
+    const int64_t* __restrict__ split, int32_t* __restrict__ cursors,
+    const int32_t* __restrict__ dcount) {
+  if (dcount && (int)blockIdx.x >= *dcount) return;  // device-side item count
   __shared__ uint32_t s_left[kPartThreads / kWave];
   __shared__ uint32_t s_right[kPartThreads / kWave];
   __shared__ int32_t s_base_l, s_base_r;
@@ -100,7 +102,9 @@ __global__ __launch_bounds__(kPartThreads) void partition_kernel(
 // idx[seg] = tmp[seg] for every chunk item
 __global__ __launch_bounds__(256) void copy_back_kernel(const uint32_t* __restrict__ tmp,
                                                         uint32_t* __restrict__ idx,
-                                                        const int64_t* __restrict__ items) {
+                                                        const int64_t* __restrict__ items,
+                                                        const int32_t* __restrict__ dcount) {
+  if (dcount && (int)blockIdx.x >= *dcount) return;
   const int64_t c0 = items[blockIdx.x * 3 + 1];
   const int64_t cn = items[blockIdx.x * 3 + 2];
   for (int64_t e = threadIdx.x; e < cn; e += blockDim.x) idx[c0 + e] = tmp[c0 + e];
@@ -188,16 +192,20 @@ __global__ __launch_bounds__(256) void init_idx_kernel(uint32_t* __restrict__ id
 
 void launch_partition(hipStream_t stream, const void* codes_fm, int code_bytes, int64_t n_rows,
                       uint32_t* idx, uint32_t* tmp, uint32_t mask, const int64_t* items,
-                      int n_items, const int64_t* split, int32_t* cursors) {
+                      int n_items, const int64_t* split, int32_t* cursors,
+                      const int32_t* dcount) {
   if (n_items <= 0) return;
   if (code_bytes == 1)
     hipLaunchKernelGGL(partition_kernel<uint8_t>, dim3(n_items), dim3(kPartThreads), 0, stream,
-                       (const uint8_t*)codes_fm, n_rows, idx, tmp, mask, items, split, cursors);
+                       (const uint8_t*)codes_fm, n_rows, idx, tmp, mask, items, split, cursors,
+                       dcount);
   else
     hipLaunchKernelGGL(partition_kernel<uint16_t>, dim3(n_items), dim3(kPartThreads), 0, stream,
-                       (const uint16_t*)codes_fm, n_rows, idx, tmp, mask, items, split, cursors);
+                       (const uint16_t*)codes_fm, n_rows, idx, tmp, mask, items, split, cursors,
+                       dcount);
   MT_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(copy_back_kernel, dim3(n_items), dim3(256), 0, stream, tmp, idx, items);
+  hipLaunchKernelGGL(copy_back_kernel, dim3(n_items), dim3(256), 0, stream, tmp, idx, items,
+                     dcount);
   MT_HIP_CHECK(hipGetLastError());
 }
 

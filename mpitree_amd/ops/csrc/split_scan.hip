@@ -30,7 +30,8 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
     const uint32_t* __restrict__ hist, const int64_t* __restrict__ nodes,
     const int32_t* __restrict__ nbins, int F_h, int f_lo, int B, int C, int crit, int msl,
     double* __restrict__ out_cost, int32_t* __restrict__ out_bin,
-    const double* __restrict__ xtab, int xtab_n) {
+    const double* __restrict__ xtab, int xtab_n, const int32_t* __restrict__ dcount) {
+  if (dcount && (int)blockIdx.x >= *dcount) return;  // device-side node count
   extern __shared__ uint32_t sm[];  // per wave: C class totals + C carries
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
@@ -213,7 +214,8 @@ __global__ __launch_bounds__(256) void scan_reg_kernel(
 __global__ __launch_bounds__(256) void select_kernel(
     const void* __restrict__ hist_v, const int64_t* __restrict__ nodes,
     const double* __restrict__ cost, const int32_t* __restrict__ bins, int F_h, int f_lo, int B,
-    int C, int crit, int64_t* __restrict__ rec) {
+    int C, int crit, int64_t* __restrict__ rec, const int32_t* __restrict__ dcount) {
+  if (dcount && (int)blockIdx.x >= *dcount) return;
   extern __shared__ int64_t cls[];  // [C] totals, then [C] left counts
   __shared__ double s_gain[4];
   __shared__ int s_feat[4], s_bin[4];
@@ -362,7 +364,8 @@ __global__ __launch_bounds__(256) void select_kernel(
 
 void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int k,
                  const int32_t* nbins, int F_h, int f_lo, int B, int C, int crit, int msl,
-                 double* cost, int32_t* bins, int64_t* rec, const double* xtab, int xtab_n) {
+                 double* cost, int32_t* bins, int64_t* rec, const double* xtab, int xtab_n,
+                 const int32_t* dcount) {
   if (k <= 0) return;
   dim3 grid(k, (F_h + 3) / 4);
   if (crit == kSquaredError) {
@@ -373,14 +376,15 @@ void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int
     MT_HIP_CHECK(hipFuncSetAttribute((const void*)scan_cls_kernel,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(scan_cls_kernel, grid, dim3(256), lds, stream, (const uint32_t*)hist,
-                       nodes, nbins, F_h, f_lo, B, C, crit, msl, cost, bins, xtab, xtab_n);
+                       nodes, nbins, F_h, f_lo, B, C, crit, msl, cost, bins, xtab, xtab_n,
+                       dcount);
   }
   MT_HIP_CHECK(hipGetLastError());
   const size_t sel_lds = crit == kSquaredError ? 16 : (size_t)2 * C * sizeof(int64_t);
   MT_HIP_CHECK(hipFuncSetAttribute((const void*)select_kernel,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)sel_lds));
   hipLaunchKernelGGL(select_kernel, dim3(k), dim3(256), sel_lds, stream, hist, nodes, cost, bins,
-                     F_h, f_lo, B, C, crit, rec);
+                     F_h, f_lo, B, C, crit, rec, dcount);
   MT_HIP_CHECK(hipGetLastError());
 }
 

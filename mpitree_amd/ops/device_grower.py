@@ -1,0 +1,211 @@
+"""Device-driven level-wise growth for single-GPU classification fits.
+
+The host-driven :class:`~mpitree_amd.core.levelwise.LevelwiseBuilder` reads
+every level's split records back and rebuilds the next level's work lists in
+numpy -- one device round trip and ~100 small host operations per level. Here
+the same algorithm runs with the planning on the GPU (``grow.hip``):
+
+per level, all on one stream and with device-side work counts
+    histogram items -> slab reduction -> sibling derivation -> scan/select
+    -> ``grow_plan_kernel`` (writes decided nodes into the pre-order position
+    space, appends finisher jobs, builds the partition list and the next
+    level's lists) -> partition + copy-back
+
+so the host only enqueues fixed-shape launches. Grids are host-known upper
+bounds (a level has at most ``min(2**L, n // (finisher_rows + 1) + 1)``
+frontier nodes, because frontier nodes hold more than ``finisher_rows`` rows);
+surplus workgroups exit on the device count. The host learns that the tree is
+finished from a lagged, pinned 32-byte read of the next level's counters, then
+sorts the device job list (largest first) and launches the subtree finisher;
+the position space is compacted by ``assemble.hip``. The resulting tree is
+bitwise identical to the host-driven builder's (tests/test_gpu_kernels.py).
+
+Reference parity: mpitree/tree/decision_tree.py:93-166 (growth),
+:63-91 (split search), :150-164 (recursion / stopping rules).
+"""
+
+from __future__ import annotations
+
+import os
+import time
+
+import numpy as np
+import torch
+
+from ..core.criterion import Criterion
+from ..models.tree_arrays import TreeArrays
+from . import hip_backend as hb
+
+__all__ = ["DeviceGrower", "device_loop_supported"]
+
+
+def device_loop_supported(be, params, comm) -> bool:
+    if os.environ.get("MPITREE_DEVICE_LOOP", "1") == "0":
+        return False
+    if getattr(comm, "world_size", 1) != 1 or be.reg:
+        return False
+    if params.finisher_rows <= 0 or not be.finisher_supported():
+        return False
+    # the planner drives the LDS histogram path only
+    return be.hip.hist_feature_tile(be.F, be.B, be.C, False, hb.LDS_BUDGET) > 0
+
+
+class DeviceGrower:
+    def __init__(self, be, params):
+        self.be = be
+        self.p = params
+        self.timings: dict = {}
+        self.stats: dict = {}
+
+    # ------------------------------------------------------------ buffers
+    def _lists(self, KMAX, IMAX, C, dev):
+        i64 = dict(dtype=torch.int64, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        return dict(
+            pos=torch.empty(KMAX, **i64), start=torch.empty(KMAX, **i64),
+            cnt=torch.empty(KMAX, **i32), depth=torch.empty(KMAX, **i32),
+            stats=torch.empty((KMAX, C), **i32), items=torch.empty((IMAX, 4), **i64),
+            red=torch.empty((KMAX, 3), **i64), der=torch.empty((KMAX, 3), **i64),
+            ctl=torch.zeros(8, **i32),
+        )
+
+    @staticmethod
+    def _ptrs(lists) -> dict:
+        return {k: v.data_ptr() for k, v in lists.items()}
+
+    # --------------------------------------------------------------- fit
+    def fit(self, n: int, n_classes: int, n_features: int, edges, y_exp: int = 0) -> TreeArrays:
+        be, p = self.be, self.p
+        hip = be.hip
+        dev = be.device
+        C, F, B = n_classes, n_features, be.B
+        fr = int(p.finisher_rows)
+        md = -1 if p.max_depth is None else int(p.max_depth)
+        mss, msl = int(p.min_samples_split), int(max(1, p.min_samples_leaf))
+        s = hb._stream
+        t0 = time.perf_counter()
+        root = be.segment_stats(np.array([0]), np.array([n]))[0]  # one small sync
+        be.begin_positions(2 * n - 1)
+        nz = int((root > 0).sum())
+        root_term = (md == 0) or n < mss or n < 2 * msl or nz <= 1
+        jobs_host = None
+        if root_term:
+            be.put_positions([0], [-1], [-1], [-1], [-1], [0], [n], root[None, :])
+        elif n <= fr:  # the whole tree is one finisher job
+            jobs_host = np.concatenate([[0, n, 0, 0, 0], root]).astype(np.int64)[None, :]
+        self.timings["stats"] = time.perf_counter() - t0
+        levels = 0
+        J = 0
+        t0 = time.perf_counter()
+        if not root_term and jobs_host is None:
+            KMAX = n // (fr + 1) + 2
+            IMAX = KMAX + n // 1024 + 2 * hb.N_CU + 16
+            PMAX = KMAX + n // 1024 + 16
+            JMAX = n // 2 + 2
+            R = 5 + 2 * C
+            sets = [self._lists(KMAX, IMAX, C, dev), self._lists(KMAX, IMAX, C, dev)]
+            ptrs = [self._ptrs(x) for x in sets]
+            E = F * B * C
+            hists = [torch.empty((KMAX, F, B, C), dtype=torch.int32, device=dev) for _ in range(2)]
+            sw = hip.hist_slab_words(F, B, C, False)
+            slab = torch.empty((IMAX, sw), dtype=torch.int32, device=dev)
+            rec = torch.empty((KMAX, R), dtype=torch.int64, device=dev)
+            cost = torch.empty((KMAX, F), dtype=torch.float64, device=dev)
+            bins = torch.empty((KMAX, F), dtype=torch.int32, device=dev)
+            ident = torch.arange(KMAX, dtype=torch.int64, device=dev)
+            split = torch.empty((KMAX, 4), dtype=torch.int64, device=dev)
+            pitems = torch.empty((PMAX, 3), dtype=torch.int64, device=dev)
+            cursors = torch.empty((KMAX, 2), dtype=torch.int32, device=dev)
+            jobs = torch.empty((JMAX, 5 + C), dtype=torch.int64, device=dev)
+            job_count = torch.zeros(1, dtype=torch.int32, device=dev)
+            # level 0: the root, built from rows (lists prepared on the host)
+            chunk = int(min(hb.MAX_ITEM_ROWS, max(1024, -(-n // (2 * hb.N_CU)))))
+            k = -(-n // chunk)
+            c0 = np.arange(k, dtype=np.int64) * chunk
+            items = np.stack([np.zeros(k, np.int64), c0, np.minimum(chunk, n - c0),
+                              np.arange(k) if k > 1 else np.full(k, -1)], 1)
+            a = sets[0]
+            a["pos"][:1].zero_()
+            a["start"][:1].zero_()
+            a["cnt"][:1].fill_(n)
+            a["depth"][:1].zero_()
+            a["stats"][:1].copy_(torch.from_numpy(root.astype(np.int32)).to(dev))
+            a["items"][:k].copy_(torch.from_numpy(items).to(dev))
+            if k > 1:
+                a["red"][:1].copy_(torch.tensor([[0, 0, k]], dtype=torch.int64, device=dev))
+            a["ctl"].copy_(torch.tensor([1, 1, k, 1 if k > 1 else 0, 0, 0, 0, 0],
+                                        dtype=torch.int32, device=dev))
+            pinned = torch.zeros((64, 9), dtype=torch.int32, pin_memory=True)
+            events = []
+            cb, rs = be.cb, be.row_elems * be.cb
+            # slabs per multi-item node: chunk >= max(1024, level rows / (2 CUs)), <= 65535
+            max_k = max(2 * hb.N_CU + 1, n // hb.MAX_ITEM_ROWS + 2)
+            lvl = 0
+            done_at = None
+            while True:
+                cur, nxt = ptrs[lvl % 2], ptrs[(lvl + 1) % 2]
+                H, Hp = hists[lvl % 2], hists[(lvl + 1) % 2]
+                kb = int(min(2 ** min(lvl, 40), KMAX))
+                ib = int(min(IMAX, kb + n // 1024 + 2 * hb.N_CU + 1))
+                ctl = cur["ctl"]
+                hip.hist(s(), be.codes_rm.data_ptr(), cb, rs, be.idx.data_ptr(), be.y.data_ptr(),
+                         be.lab_shift, cur["items"], ib, H.data_ptr(), slab.data_ptr(), F, 0, B, C,
+                         False, hb.LDS_BUDGET, dcount=ctl + 4 * 2)
+                hip.hist_reduce(s(), cur["red"], kb, max_k, slab.data_ptr(), H.data_ptr(),
+                                F, B, C, False, dcount=ctl + 4 * 3)
+                if lvl > 0:
+                    hip.hist_derive(s(), cur["der"], kb, Hp.data_ptr(), H.data_ptr(), E, False,
+                                    dcount=ctl + 4 * 4)
+                hip.scan(s(), H.data_ptr(), ident.data_ptr(), kb, be.nbins.data_ptr(), F, 0, B, C,
+                         int(be.crit), msl, cost.data_ptr(), bins.data_ptr(), rec.data_ptr(),
+                         be.xtab.data_ptr(), hb.XTAB_N, dcount=ctl)
+                hip.grow_plan(s(), cur, nxt, rec.data_ptr(), split.data_ptr(), pitems.data_ptr(),
+                              cursors.data_ptr(), ctl + 4 * 5, be.pos_rec.data_ptr(),
+                              be.pos_st.data_ptr(), jobs.data_ptr(), job_count.data_ptr(), C, md,
+                              hb.N_CU, mss, msl, fr)
+                pb = int(min(PMAX, n // 1024 + kb + 1))
+                hip.partition(s(), be.codes_fm.data_ptr(), cb, be.n, be.idx.data_ptr(),
+                              be.tmp.data_ptr(), be.row_mask, pitems.data_ptr(), pb,
+                              split.data_ptr(), cursors.data_ptr(), dcount=ctl + 4 * 6)
+                # lagged completion check: next level's frontier size + job count
+                slot = lvl % 64
+                pinned[slot, :8].copy_(sets[(lvl + 1) % 2]["ctl"], non_blocking=True)
+                pinned[slot, 8:9].copy_(job_count, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                events.append(ev)
+                lvl += 1
+                if lvl >= 2:
+                    events[lvl - 2].synchronize()
+                    row = pinned[(lvl - 2) % 64]
+                    if int(row[0]) == 0:
+                        done_at = lvl - 2
+                        break
+                if lvl > 4096:
+                    raise RuntimeError("device level loop did not terminate")
+            levels = done_at + 1
+            J = int(pinned[done_at % 64, 8])
+            self._keep = (sets, hists, slab, rec, cost, bins, split, pitems, cursors)
+            if J:
+                order = torch.argsort(jobs[:J, 1], descending=True, stable=True)
+                d_jobs = jobs[:J].index_select(0, order).contiguous()
+                be.launch_finisher(d_jobs, J, n, p, be.pos_rec, be.pos_st)
+        elif jobs_host is not None:
+            J = 1
+            (d_jobs,) = be.up(jobs_host)
+            be.launch_finisher(d_jobs.view(1, -1), 1, n, p, be.pos_rec, be.pos_st)
+        self.timings["levels"] = time.perf_counter() - t0
+        self.stats["levels"] = levels
+        self.stats["finisher_subtrees"] = J
+        t0 = time.perf_counter()
+        a = be.assemble_positions(edges, int(p.criterion), y_exp)
+        self.timings["assemble"] = time.perf_counter() - t0
+        st = a["stats"]
+        ta = TreeArrays(
+            feature=a["feature"], threshold=a["threshold"], threshold_bin=a["bin"],
+            left=a["left"], right=a["right"], depth=a["depth"], n_samples=a["nsamp"],
+            impurity=a["impurity"], count=st, value=None,
+        )
+        ta.meta["term"] = a["term"]
+        ta.meta["final"] = True
+        return ta

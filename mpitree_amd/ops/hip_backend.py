@@ -431,6 +431,38 @@ class HipBackend:
         self.pos_rec = self.pos_st = None
         return out
 
+    def launch_finisher(self, d_jobs, J: int, job_rows: int, params, rec, cnt):
+        """Launch the block + wave finisher kernels on ``J`` device jobs
+        (int64 [J][5 + C] = {start, count, depth, root position, buffer, counts},
+        largest first for load balance) writing into position space rec/cnt."""
+        if J <= 0:
+            return
+        C = self.C
+        counter = torch.zeros(4, dtype=torch.int32, device=self.device)
+        job_root = torch.empty(J, dtype=torch.int32, device=self.device)
+        tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
+        # every tiny subtree has >= 2 rows and they partition the job rows
+        tiny_cap = int(job_rows // 2 + J + 1)
+        tiny = torch.empty((tiny_cap, 8), dtype=torch.int64, device=self.device)
+        md = -1 if params.max_depth is None else int(params.max_depth)
+        grid = int(min(J, int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU))))
+        prof = None
+        if os.environ.get("MPITREE_FIN_PROF"):
+            prof = torch.zeros((grid, 10), dtype=torch.int64, device=self.device)
+        self.hip.finish(_stream(), self.codes_rm.data_ptr(), self.row_elems * self.cb // 4,
+                        self.codes_fm.data_ptr(), self.cb, self.n, self.idx.data_ptr(),
+                        self.tmp.data_ptr(), self.y.data_ptr(), self.lab_shift, d_jobs.data_ptr(),
+                        J, counter.data_ptr(), self.nbins.data_ptr(), self.F, self.B, C,
+                        int(self.crit), md, int(params.min_samples_split),
+                        int(max(1, params.min_samples_leaf)), self.xtab.data_ptr(),
+                        self.xtabf.data_ptr(), XTAB_N,
+                        rec.data_ptr(), cnt.data_ptr(), job_root.data_ptr(), grid,
+                        tiny_rows, tiny.data_ptr(), 4 * N_CU,
+                        0 if prof is None else prof.data_ptr())
+        self._fin_keep = (counter, job_root, tiny, d_jobs)
+        if prof is not None:
+            self.last_finisher_prof = prof.cpu().numpy()
+
     def finish_subtrees(self, starts, counts, depths, params, stats=None, positions=None,
                         overlap=False):
         """See :meth:`_finish_subtrees`; ``overlap`` runs the batch on a side
@@ -482,29 +514,7 @@ class HipBackend:
                                          positions[order], np.zeros(J, np.int64)], 1),
                                st[order]], 1)
         (d_jobs,) = self.up(jobs)
-        job_root = torch.empty(J, dtype=torch.int32, device=self.device)
-        counter = torch.zeros(4, dtype=torch.int32, device=self.device)
-        tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
-        # every tiny subtree has >= 2 rows and they partition the job rows
-        tiny_cap = int(counts.sum() // 2 + J + 1)
-        tiny = torch.empty((tiny_cap, 8), dtype=torch.int64, device=self.device)
-        md = -1 if params.max_depth is None else int(params.max_depth)
-        grid = int(min(J, int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU))))
-        prof = None
-        if os.environ.get("MPITREE_FIN_PROF"):
-            prof = torch.zeros((grid, 10), dtype=torch.int64, device=self.device)
-        self.hip.finish(_stream(), self.codes_rm.data_ptr(), self.row_elems * self.cb // 4,
-                        self.codes_fm.data_ptr(), self.cb, self.n, self.idx.data_ptr(),
-                        self.tmp.data_ptr(), self.y.data_ptr(), self.lab_shift, d_jobs.data_ptr(),
-                        J, counter.data_ptr(), self.nbins.data_ptr(), self.F, self.B, C,
-                        int(self.crit), md, int(params.min_samples_split),
-                        int(max(1, params.min_samples_leaf)), self.xtab.data_ptr(),
-                        self.xtabf.data_ptr(), XTAB_N,
-                        rec.data_ptr(), cnt.data_ptr(), job_root.data_ptr(), grid,
-                        tiny_rows, tiny.data_ptr(), 4 * N_CU,
-                        0 if prof is None else prof.data_ptr())
-        if prof is not None:
-            self.last_finisher_prof = prof.cpu().numpy()
+        self.launch_finisher(d_jobs, J, int(counts.sum()), params, rec, cnt)
         if not table_mode:
             return None
         # compact the private position space into the merge table

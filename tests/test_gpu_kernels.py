@@ -189,3 +189,25 @@ def test_gpu_rejects_nonfinite_tensor():
     X[17, 1] = float("nan")
     with pytest.raises(ValueError, match="NaN or infinity"):
         DecisionTreeClassifier(device="cuda").fit(X, torch.zeros(1000, device="cuda"))
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("max_depth", [None, 7])
+def test_gpu_device_loop_matches_host_loop(monkeypatch, seed, max_depth):
+    """Device-planned level loop (grow.hip) == host-driven level-wise builder."""
+    from mpitree_amd.core.fit import fit_tree
+
+    rng = np.random.default_rng(100 + seed)
+    n, F, C = 30000 + 7000 * seed, 11, 2 + seed
+    X = rng.integers(0, 60, size=(n, F)).astype(np.float32)
+    y = (X[:, 0] + X[:, 1] * (seed + 1) + rng.integers(0, 40, size=n)) % C
+    kw = dict(regression=False, criterion=seed % 2, max_depth=max_depth, min_samples_split=2,
+              device="cuda", finisher_rows=500)
+    monkeypatch.setenv("MPITREE_DEVICE_LOOP", "1")
+    r1 = fit_tree(X, y, **kw)
+    assert r1.engine == "hip-device-loop"
+    monkeypatch.setenv("MPITREE_DEVICE_LOOP", "0")
+    r2 = fit_tree(X, y, **kw)
+    assert r2.engine == "hip-levelwise"
+    assert r1.arrays.equal(r2.arrays)
+    assert np.array_equal(r1.arrays.meta["term"], r2.arrays.meta["term"])
