@@ -64,6 +64,7 @@ struct LevelLists {
   int64_t* items;
   int64_t* red;
   int64_t* der;
+  int64_t* tasks;
   int32_t* ctl;
 };
 struct PlanArgs {
@@ -81,6 +82,8 @@ struct PlanArgs {
   int64_t mss, msl, fr;
 };
 void launch_grow_plan(hipStream_t, const PlanArgs&);
+void launch_hist_reduce_tasks(hipStream_t, const int64_t*, int, const int64_t*, int, const void*,
+                              void*, int, int, int, const int32_t*, const int32_t*);
 int edges_sample_rows(bool x64);
 void launch_edges(hipStream_t, const void*, bool, int64_t, int, int, int, void*, int32_t*,
                   uint8_t*);
@@ -179,6 +182,13 @@ PYBIND11_MODULE(_hip, m) {
                       P<int64_t>(tiny), tiny_grid, P<int64_t>(prof));
   });
   m.def("asm_tiles", &mt::asm_tiles);
+  m.def("hist_reduce_tasks", [](uintptr_t s, uintptr_t red, int red_bound, uintptr_t tasks,
+                                int task_bound, uintptr_t slab, uintptr_t hist, int F_h, int B,
+                                int C, uintptr_t dred, uintptr_t dtasks) {
+    mt::launch_hist_reduce_tasks(S(s), P<int64_t>(red), red_bound, P<int64_t>(tasks), task_bound,
+                                 P<void>(slab), P<void>(hist), F_h, B, C, P<int32_t>(dred),
+                                 P<int32_t>(dtasks));
+  });
   // cur / nxt: dicts of device pointers {pos, start, cnt, depth, stats, items, red, der, ctl}
   m.def("grow_plan", [](uintptr_t s, py::dict cur, py::dict nxt, uintptr_t rec, uintptr_t split,
                         uintptr_t pitems, uintptr_t cursors, uintptr_t pctl, uintptr_t pos_rec,
@@ -188,7 +198,8 @@ PYBIND11_MODULE(_hip, m) {
       auto g = [&](const char* k) { return d[k].cast<uintptr_t>(); };
       return mt::LevelLists{P<int64_t>(g("pos")),  P<int64_t>(g("start")), P<int32_t>(g("cnt")),
                             P<int32_t>(g("depth")), P<int32_t>(g("stats")), P<int64_t>(g("items")),
-                            P<int64_t>(g("red")),  P<int64_t>(g("der")),   P<int32_t>(g("ctl"))};
+                            P<int64_t>(g("red")),  P<int64_t>(g("der")),   P<int64_t>(g("tasks")),
+                            P<int32_t>(g("ctl"))};
     };
     mt::PlanArgs a{lists(cur),          lists(nxt),         P<int64_t>(rec),
                    P<int64_t>(split),   P<int64_t>(pitems), P<int32_t>(cursors),

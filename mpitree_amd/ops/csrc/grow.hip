@@ -30,7 +30,7 @@ constexpr int kPlanWaves = kPlanThreads / kWave;
 
 // Level work lists (one set per level parity). ctl: int32
 // {0: K frontier nodes, 1: built nodes, 2: hist items, 3: slab reductions,
-//  4: derive triples, 5: split nodes, 6: partition items, 7: -}
+//  4: derive triples, 5: split nodes, 6: partition items, 7: reduction tasks}
 struct LevelLists {
   int64_t* pos;     // [KMAX] pre-order position of each frontier slot
   int64_t* start;   // [KMAX] row segment start
@@ -40,6 +40,7 @@ struct LevelLists {
   int64_t* items;   // [IMAX][4] {slot, start, count, dest slab or -1}
   int64_t* red;     // [KMAX][3] {slot, first slab, slabs}
   int64_t* der;     // [KMAX][3] {slot, parent slot (previous level), sibling slot}
+  int64_t* tasks;   // [TMAX][3] {slot, first slab, <= 16 slabs} slab-reduction tasks
   int32_t* ctl;     // [8]
 };
 
@@ -279,6 +280,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     s_carry[0] = 0;  // items
     s_carry[1] = 0;  // slabs
     s_carry[2] = 0;  // reductions
+    s_carry[3] = 0;  // reduction tasks
   }
   __syncthreads();
   for (int b0 = 0; b0 < NB; b0 += kPlanThreads) {
@@ -290,10 +292,12 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
       if (kk < 1) kk = 1;
     }
     const int multi = kk > 1 ? 1 : 0;
-    int ti, tsl, tr;
+    const int nt = multi ? (int)((kk + 15) / 16) : 0;
+    int ti, tsl, tr, tt;
     const int oi = plan_scan_excl((int)kk, s_w, ti) + s_carry[0];
     const int osl = plan_scan_excl(multi ? (int)kk : 0, s_w, tsl) + s_carry[1];
     const int orr = plan_scan_excl(multi, s_w, tr) + s_carry[2];
+    const int ot = plan_scan_excl(nt, s_w, tt) + s_carry[3];
     if (sl < NB) {
       const int64_t st0 = a.nxt.start[sl];
       for (int64_t c = 0; c < kk; ++c) {
@@ -309,6 +313,12 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
         rr[0] = sl;
         rr[1] = osl;
         rr[2] = kk;
+        for (int t = 0; t < nt; ++t) {
+          int64_t* tk = a.nxt.tasks + (int64_t)(ot + t) * 3;
+          tk[0] = sl;
+          tk[1] = osl + 16 * t;
+          tk[2] = (kk - 16 * t) < 16 ? (kk - 16 * t) : 16;
+        }
       }
     }
     __syncthreads();
@@ -316,11 +326,13 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
       s_carry[0] += ti;
       s_carry[1] += tsl;
       s_carry[2] += tr;
+      s_carry[3] += tt;
     }
     __syncthreads();
   }
   const int n_items = s_carry[0];
   const int n_red = s_carry[2];
+  const int n_tasks = s_carry[3];
   // ---- pass 4: partition items of this level's split nodes (1024 rows each)
   __syncthreads();
   if (tid == 0) s_carry[3] = 0;
@@ -357,6 +369,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     a.nxt.ctl[4] = ND;
     a.nxt.ctl[5] = 0;
     a.nxt.ctl[6] = 0;
+    a.nxt.ctl[7] = n_tasks;
     a.pctl[0] = NS;
     a.pctl[1] = s_carry[3];
   }

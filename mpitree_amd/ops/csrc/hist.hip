@@ -264,6 +264,9 @@ __global__ __launch_bounds__(256) void zero_slots_kernel(const int64_t* __restri
     hist[slot * E + e] = 0;
 }
 
+// With ``tasks`` (device-planned levels) each grid row is one task {slot,
+// first slab, slabs <= G} and z is 1; otherwise row y is reduction entry y and
+// z selects its group of G slabs.
 __global__ __launch_bounds__(256) void hist_reduce_cls_kernel(
     const int64_t* __restrict__ red, const uint32_t* __restrict__ slab,
     uint32_t* __restrict__ hist, int64_t Ep, int C, int W, int G,
@@ -496,6 +499,25 @@ void launch_hist_reduce(hipStream_t stream, const int64_t* red, int n_red, int m
   dim3 grid((unsigned)((Ep + 255) / 256), n_red, groups);
   hipLaunchKernelGGL(hist_reduce_cls_kernel, grid, dim3(256), 0, stream, red,
                      (const uint32_t*)slab, (uint32_t*)hist, Ep, C, W, G, dcount);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+// Device-planned reduction: zero the multi-item slots (red entries), then one
+// workgroup row per task {slot, first slab, <= 16 slabs} adds into them.
+void launch_hist_reduce_tasks(hipStream_t stream, const int64_t* red, int red_bound,
+                              const int64_t* tasks, int task_bound, const void* slab, void* hist,
+                              int F_h, int B, int C, const int32_t* dred, const int32_t* dtasks) {
+  if (red_bound <= 0 || task_bound <= 0) return;
+  const int W = (C + 1) / 2;
+  const int64_t Ep = (int64_t)F_h * B * W;
+  const int64_t Eu = (int64_t)F_h * B * C;
+  hipLaunchKernelGGL(zero_slots_kernel,
+                     dim3((unsigned)std::min<int64_t>((Eu / 4 + 255) / 256, 64), red_bound),
+                     dim3(256), 0, stream, red, (uint32_t*)hist, Eu, dred);
+  MT_HIP_CHECK(hipGetLastError());
+  dim3 grid((unsigned)((Ep + 255) / 256), task_bound, 1);
+  hipLaunchKernelGGL(hist_reduce_cls_kernel, grid, dim3(256), 0, stream, tasks,
+                     (const uint32_t*)slab, (uint32_t*)hist, Ep, C, W, 16, dtasks);
   MT_HIP_CHECK(hipGetLastError());
 }
 

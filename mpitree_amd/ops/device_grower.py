@@ -58,7 +58,7 @@ class DeviceGrower:
         self.stats: dict = {}
 
     # ------------------------------------------------------------ buffers
-    def _lists(self, KMAX, IMAX, C, dev):
+    def _lists(self, KMAX, IMAX, TMAX, C, dev):
         i64 = dict(dtype=torch.int64, device=dev)
         i32 = dict(dtype=torch.int32, device=dev)
         return dict(
@@ -66,7 +66,7 @@ class DeviceGrower:
             cnt=torch.empty(KMAX, **i32), depth=torch.empty(KMAX, **i32),
             stats=torch.empty((KMAX, C), **i32), items=torch.empty((IMAX, 4), **i64),
             red=torch.empty((KMAX, 3), **i64), der=torch.empty((KMAX, 3), **i64),
-            ctl=torch.zeros(8, **i32),
+            tasks=torch.empty((TMAX, 3), **i64), ctl=torch.zeros(8, **i32),
         )
 
     @staticmethod
@@ -103,7 +103,10 @@ class DeviceGrower:
             PMAX = KMAX + n // 1024 + 16
             JMAX = n // 2 + 2
             R = 5 + 2 * C
-            sets = [self._lists(KMAX, IMAX, C, dev), self._lists(KMAX, IMAX, C, dev)]
+            # multi-item nodes hold > max(1024, level rows / 512) rows each
+            RMAX = int(min(KMAX, max(2 * hb.N_CU + 1, n // 1024 + 1)))
+            TMAX = RMAX + IMAX // 16 + 16
+            sets = [self._lists(KMAX, IMAX, TMAX, C, dev), self._lists(KMAX, IMAX, TMAX, C, dev)]
             ptrs = [self._ptrs(x) for x in sets]
             E = F * B * C
             hists = [torch.empty((KMAX, F, B, C), dtype=torch.int32, device=dev) for _ in range(2)]
@@ -131,15 +134,17 @@ class DeviceGrower:
             a["depth"][:1].zero_()
             a["stats"][:1].copy_(torch.from_numpy(root.astype(np.int32)).to(dev))
             a["items"][:k].copy_(torch.from_numpy(items).to(dev))
+            nt = -(-k // 16) if k > 1 else 0
             if k > 1:
                 a["red"][:1].copy_(torch.tensor([[0, 0, k]], dtype=torch.int64, device=dev))
-            a["ctl"].copy_(torch.tensor([1, 1, k, 1 if k > 1 else 0, 0, 0, 0, 0],
+                t0s = np.arange(nt, dtype=np.int64) * 16
+                a["tasks"][:nt].copy_(torch.from_numpy(
+                    np.stack([np.zeros(nt, np.int64), t0s, np.minimum(16, k - t0s)], 1)).to(dev))
+            a["ctl"].copy_(torch.tensor([1, 1, k, 1 if k > 1 else 0, 0, 0, 0, nt],
                                         dtype=torch.int32, device=dev))
             pinned = torch.zeros((64, 9), dtype=torch.int32, pin_memory=True)
             events = []
             cb, rs = be.cb, be.row_elems * be.cb
-            # slabs per multi-item node: chunk >= max(1024, level rows / (2 CUs)), <= 65535
-            max_k = max(2 * hb.N_CU + 1, n // hb.MAX_ITEM_ROWS + 2)
             lvl = 0
             done_at = None
             while True:
@@ -151,8 +156,10 @@ class DeviceGrower:
                 hip.hist(s(), be.codes_rm.data_ptr(), cb, rs, be.idx.data_ptr(), be.y.data_ptr(),
                          be.lab_shift, cur["items"], ib, H.data_ptr(), slab.data_ptr(), F, 0, B, C,
                          False, hb.LDS_BUDGET, dcount=ctl + 4 * 2)
-                hip.hist_reduce(s(), cur["red"], kb, max_k, slab.data_ptr(), H.data_ptr(),
-                                F, B, C, False, dcount=ctl + 4 * 3)
+                rb = int(min(kb, RMAX))
+                hip.hist_reduce_tasks(s(), cur["red"], rb, cur["tasks"],
+                                      int(min(TMAX, rb + ib // 16 + 1)), slab.data_ptr(),
+                                      H.data_ptr(), F, B, C, ctl + 4 * 3, ctl + 4 * 7)
                 if lvl > 0:
                     hip.hist_derive(s(), cur["der"], kb, Hp.data_ptr(), H.data_ptr(), E, False,
                                     dcount=ctl + 4 * 4)
