@@ -18,6 +18,7 @@ level-wise engine on either device.
 
 from __future__ import annotations
 
+import logging
 import math
 import os
 import time
@@ -31,6 +32,7 @@ from .criterion import Criterion
 from .levelwise import GrowParams, LevelwiseBuilder, LocalComm
 from ..models.tree_arrays import TreeArrays
 from ..ops import native
+from ..utils.observability import logger, profiling, roctx_range
 
 __all__ = ["FitResult", "fit_tree", "resolve_device", "AUTO_GPU_MIN_CELLS"]
 
@@ -227,7 +229,8 @@ def fit_tree(
             Xd = Xd.double()
         Xd = Xd.contiguous()
         t0 = time.perf_counter()
-        mapper, codes_rm, codes_fm, nb = gpu_bin_features(Xd, max_bins)
+        with roctx_range("mpitree.bin"):
+            mapper, codes_rm, codes_fm, nb = gpu_bin_features(Xd, max_bins)
         yd = (yv if _is_tensor(yv) else torch.from_numpy(np.ascontiguousarray(yv))).to("cuda")
         lo, hi = comm.local_rows(n)
         if (lo, hi) != (0, n):  # data-parallel shard of a replicated input
@@ -239,6 +242,7 @@ def fit_tree(
         be = HipBackend()
         be.setup(codes_rm, codes_fm, yd, nb, n_bins=mapper.max_n_bins, n_classes=C,
                  criterion=crit)
+        be.timing = profiling()  # synchronised per-phase timers (host-driven loop)
         if finisher_rows is None:
             env = os.environ.get("MPITREE_FINISHER_ROWS")
             # ~2 subtree jobs per workgroup slot of the finisher grid
@@ -251,11 +255,13 @@ def fit_tree(
 
         if device_loop_supported(be, params, comm):
             builder = DeviceGrower(be, params)
-            ta = builder.fit(hi - lo, C, F, mapper.padded_edges(), y_exp)
+            with roctx_range("mpitree.grow"):
+                ta = builder.fit(hi - lo, C, F, mapper.padded_edges(), y_exp)
             eng = "hip-device-loop"
         else:
             builder = LevelwiseBuilder(be, params, comm)
-            ta = builder.fit(hi - lo, C, F, edges=mapper.padded_edges(), y_exp=y_exp)
+            with roctx_range("mpitree.grow"):
+                ta = builder.fit(hi - lo, C, F, edges=mapper.padded_edges(), y_exp=y_exp)
             eng = "hip-levelwise"
         timings.update(builder.timings)
         stats = dict(builder.stats)
@@ -298,5 +304,9 @@ def fit_tree(
     ta = _finalize(ta, mapper, regression, y_exp)
     timings["finalize"] = time.perf_counter() - t0
     timings["total"] = time.perf_counter() - t_start
+    if logger.isEnabledFor(logging.INFO):
+        logger.info("fit: engine=%s n=%d F=%d nodes=%d depth=%d %.3f ms", eng, n, F,
+                    ta.node_count, ta.max_depth, timings["total"] * 1e3)
+        logger.debug("fit timings (ms): %s", {k: round(v * 1e3, 3) for k, v in timings.items()})
     return FitResult(arrays=ta, classes=classes, n_features=F, mapper=mapper, y_scale_exp=y_exp,
                      engine=eng, timings=timings, stats=stats)

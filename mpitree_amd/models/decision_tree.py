@@ -24,6 +24,8 @@ Internally a fitted estimator holds flat arrays (:class:`TreeArrays`);
 
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 from sklearn.base import BaseEstimator, ClassifierMixin, RegressorMixin
@@ -324,7 +326,15 @@ class _ParallelMixin:
     WORLD_SIZE = _WorldAttr("size")
 
     def fit(self, X, y, *, data_sharded: bool = False):
+        """Collective fit. Failure handling the reference lacks (an exception
+        on one rank there deadlocks the others, ``decision_tree.py:446-477``):
+        every rank reports its status in one all-reduce after the fit, so an
+        error on any rank raises on all of them; a cross-rank digest check
+        (``MPITREE_CHECK_CONSISTENCY``, default on) verifies every rank holds
+        the same tree. Hangs are bounded by the process-group timeout
+        (``MPITREE_DIST_TIMEOUT`` seconds)."""
         from ..parallel.strategies import make_comm
+        from ..utils.observability import maybe_inject_fault, tree_digest
 
         comm, X, y = make_comm(
             getattr(self, "strategy", "auto"),
@@ -334,7 +344,37 @@ class _ParallelMixin:
             data_sharded=data_sharded,
             regression=self._regression,
         )
-        return self._fit_impl(X, y, comm=comm, **comm.fit_kwargs())
+        if getattr(comm, "world_size", 1) == 1:
+            return self._fit_impl(X, y, comm=comm, **comm.fit_kwargs())
+        # pre-flight: a rank that cannot start (bad input, injected fault) makes
+        # every rank raise instead of leaving the others blocked in a collective
+        error = None
+        try:
+            maybe_inject_fault(comm.rank)
+        except Exception as e:
+            error = e
+        self._raise_if_any_failed(comm, error)
+        try:
+            self._fit_impl(X, y, comm=comm, **comm.fit_kwargs())
+        except Exception as e:  # reported to every rank below
+            error = e
+        self._raise_if_any_failed(comm, error)
+        if os.environ.get("MPITREE_CHECK_CONSISTENCY", "1") != "0":
+            if not comm.check_consistent(tree_digest(self._arrays)):
+                raise RuntimeError("ranks built different trees (digest mismatch)")
+        return self
+
+
+    @staticmethod
+    def _raise_if_any_failed(comm, error):
+        from ..utils.observability import logger
+
+        if error is not None:
+            logger.error("rank %d: collective fit failed: %r", comm.rank, error)
+        if comm.any_failed(error is not None):
+            if error is not None:
+                raise error
+            raise RuntimeError("collective fit failed on another rank")
 
 
 class ParallelDecisionTreeClassifier(_ParallelMixin, DecisionTreeClassifier):

@@ -34,6 +34,7 @@ import torch
 
 from ..core.criterion import Criterion
 from ..models.tree_arrays import TreeArrays
+from ..utils.observability import profiling
 from . import hip_backend as hb
 
 __all__ = ["DeviceGrower", "device_loop_supported"]
@@ -68,6 +69,18 @@ class DeviceGrower:
             red=torch.empty((KMAX, 3), **i64), der=torch.empty((KMAX, 3), **i64),
             tasks=torch.empty((TMAX, 3), **i64), ctl=torch.zeros(8, **i32),
         )
+
+    def _level_profile(self, marks):
+        """Per-level device times (ms) from the HIP events (MPITREE_PROFILE=1)."""
+        names = ("hist", "derive", "scan", "plan", "partition")
+        marks[-1][-1].synchronize()
+        rows = []
+        for m in marks:
+            d = {k: m[i].elapsed_time(m[i + 1]) for i, k in enumerate(names) if i + 1 < len(m)}
+            rows.append(d)
+            for k, v in d.items():
+                self.timings["device_" + k] = self.timings.get("device_" + k, 0.0) + v / 1e3
+        self.stats["level_profile"] = rows
 
     @staticmethod
     def _ptrs(lists) -> dict:
@@ -147,7 +160,19 @@ class DeviceGrower:
             cb, rs = be.cb, be.row_elems * be.cb
             lvl = 0
             done_at = None
+            prof = profiling()
+            marks = []  # per level: events at start and after hist, derive, scan, plan, partition
+
+            def mark():
+                if prof:
+                    e = torch.cuda.Event(enable_timing=True)
+                    e.record()
+                    marks[-1].append(e)
+
             while True:
+                if prof:
+                    marks.append([])
+                    mark()
                 cur, nxt = ptrs[lvl % 2], ptrs[(lvl + 1) % 2]
                 H, Hp = hists[lvl % 2], hists[(lvl + 1) % 2]
                 kb = int(min(2 ** min(lvl, 40), KMAX))
@@ -160,20 +185,24 @@ class DeviceGrower:
                 hip.hist_reduce_tasks(s(), cur["red"], rb, cur["tasks"],
                                       int(min(TMAX, rb + ib // 16 + 1)), slab.data_ptr(),
                                       H.data_ptr(), F, B, C, ctl + 4 * 3, ctl + 4 * 7)
+                mark()
                 if lvl > 0:
                     hip.hist_derive(s(), cur["der"], kb, Hp.data_ptr(), H.data_ptr(), E, False,
                                     dcount=ctl + 4 * 4)
                 hip.scan(s(), H.data_ptr(), ident.data_ptr(), kb, be.nbins.data_ptr(), F, 0, B, C,
                          int(be.crit), msl, cost.data_ptr(), bins.data_ptr(), rec.data_ptr(),
                          be.xtab.data_ptr(), hb.XTAB_N, dcount=ctl)
+                mark()
                 hip.grow_plan(s(), cur, nxt, rec.data_ptr(), split.data_ptr(), pitems.data_ptr(),
                               cursors.data_ptr(), ctl + 4 * 5, be.pos_rec.data_ptr(),
                               be.pos_st.data_ptr(), jobs.data_ptr(), job_count.data_ptr(), C, md,
                               hb.N_CU, mss, msl, fr)
+                mark()
                 pb = int(min(PMAX, n // 1024 + kb + 1))
                 hip.partition(s(), be.codes_fm.data_ptr(), cb, be.n, be.idx.data_ptr(),
                               be.tmp.data_ptr(), be.row_mask, pitems.data_ptr(), pb,
                               split.data_ptr(), cursors.data_ptr(), dcount=ctl + 4 * 6)
+                mark()
                 # lagged completion check: next level's frontier size + job count
                 slot = lvl % 64
                 pinned[slot, :8].copy_(sets[(lvl + 1) % 2]["ctl"], non_blocking=True)
@@ -192,6 +221,8 @@ class DeviceGrower:
                     raise RuntimeError("device level loop did not terminate")
             levels = done_at + 1
             J = int(pinned[done_at % 64, 8])
+            if prof:
+                self._level_profile(marks[:levels])
             self._keep = (sets, hists, slab, rec, cost, bins, split, pitems, cursors)
             if J:
                 order = torch.argsort(jobs[:J, 1], descending=True, stable=True)

@@ -175,6 +175,11 @@ class DistComm(LocalComm):
                     left=out[:, 2], right=out[:, 3], depth=out[:, 4].astype(np.int32),
                     nsamp=out[:, 5], stats=out[:, 6:], roots=roots)
 
+    def any_failed(self, failed: bool) -> bool:
+        """All-reduce of a failure flag: True on every rank if any rank failed."""
+        return bool(self._all_reduce(np.array([1 if failed else 0]),
+                                     op=dist.ReduceOp.MAX)[0])
+
     def check_consistent(self, digest: int) -> bool:
         """Cross-rank check that every rank built the same tree."""
         a = self._all_gather(np.array([digest], dtype=np.int64))

@@ -202,3 +202,32 @@ def test_parallel_class_attributes_without_process_group():
     assert ParallelDecisionTreeClassifier.WORLD_SIZE == 1
     clf = ParallelDecisionTreeClassifier(max_depth=2)
     assert clf.WORLD_RANK == 0
+
+
+def test_tree_digest_and_logger():
+    import logging
+
+    from mpitree_amd import DecisionTreeClassifier
+    from mpitree_amd.utils.observability import logger, tree_digest
+
+    rng = np.random.default_rng(0)
+    X = rng.integers(0, 9, size=(300, 4))
+    y = rng.integers(0, 3, size=300)
+    a = DecisionTreeClassifier(device="cpu").fit(X, y).tree_arrays_
+    b = DecisionTreeClassifier(device="cpu").fit(X, y).tree_arrays_
+    c = DecisionTreeClassifier(max_depth=2, device="cpu").fit(X, y).tree_arrays_
+    assert tree_digest(a) == tree_digest(b) != tree_digest(c)
+    assert 0 <= tree_digest(a) < 2**63
+    assert logger.name == "mpitree" and logger.level == logging.NOTSET
+
+
+def test_fault_injection_helper(monkeypatch):
+    from mpitree_amd.utils.observability import InjectedFault, maybe_inject_fault
+
+    maybe_inject_fault(0)  # unset: no-op
+    monkeypatch.setenv("MPITREE_FAULT_RANK", "1")
+    maybe_inject_fault(0)
+    with pytest.raises(InjectedFault):
+        maybe_inject_fault(1)
+    monkeypatch.setenv("MPITREE_FAULT_AT", "level")
+    maybe_inject_fault(1)  # different site

@@ -115,3 +115,48 @@ def test_gpu_ranks_equal_serial(strategy, monkeypatch):
         assert str(o["engine"][0]).startswith("hip")
         for k in FIELDS:
             np.testing.assert_array_equal(o[k], getattr(ref, k))
+
+
+def _fault_rank(rank, world, fault_rank):
+    import os
+
+    from mpitree_amd import ParallelDecisionTreeClassifier
+    from mpitree_amd.utils.observability import InjectedFault
+
+    os.environ["MPITREE_FAULT_RANK"] = str(fault_rank)
+    X, y = _data(3)
+    kind = "ok"
+    try:
+        ParallelDecisionTreeClassifier(max_depth=4, strategy="feature", device="cpu").fit(X, y)
+    except InjectedFault:
+        kind = "injected"
+    except RuntimeError as e:
+        kind = "peer" if "another rank" in str(e) else f"other:{e}"
+    # the group is still usable afterwards: a clean fit succeeds on every rank
+    os.environ.pop("MPITREE_FAULT_RANK")
+    est = ParallelDecisionTreeClassifier(max_depth=4, strategy="feature", device="cpu").fit(X, y)
+    return {"kind": np.array([kind]), "nodes": np.array([est.tree_arrays_.node_count])}
+
+
+@pytest.mark.parametrize("fault_rank", [0, 1])
+def test_fault_on_one_rank_raises_everywhere(fault_rank):
+    outs = run_ranks(_fault_rank, 2, fault_rank)
+    kinds = [str(o["kind"][0]) for o in outs]
+    assert kinds[fault_rank] == "injected"
+    assert kinds[1 - fault_rank] == "peer"
+    assert outs[0]["nodes"][0] == outs[1]["nodes"][0] > 1
+
+
+def _digest_rank(rank, world):
+    from mpitree_amd.parallel.strategies import FeatureParallelComm
+
+    comm = FeatureParallelComm()
+    same = comm.check_consistent(12345)
+    differ = comm.check_consistent(1000 + rank)
+    return {"r": np.array([same, differ])}
+
+
+def test_cross_rank_digest_check():
+    outs = run_ranks(_digest_rank, 2)
+    for o in outs:
+        assert list(o["r"]) == [True, False]

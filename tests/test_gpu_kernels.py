@@ -211,3 +211,16 @@ def test_gpu_device_loop_matches_host_loop(monkeypatch, seed, max_depth):
     assert r2.engine == "hip-levelwise"
     assert r1.arrays.equal(r2.arrays)
     assert np.array_equal(r1.arrays.meta["term"], r2.arrays.meta["term"])
+
+
+def test_gpu_profile_mode_level_events(monkeypatch):
+    monkeypatch.setenv("MPITREE_PROFILE", "1")
+    rng = np.random.default_rng(5)
+    X = rng.integers(0, 50, size=(40000, 6)).astype(np.float32)
+    y = (X[:, 0] + rng.integers(0, 30, size=40000)) % 2
+    est = DecisionTreeClassifier(device="cuda").fit(X, y)
+    st = est.fit_stats_
+    assert st["engine"] == "hip-device-loop"
+    prof = st["level_profile"]
+    assert len(prof) == st["levels"] and all(v >= 0 for row in prof for v in row.values())
+    assert st["timings"]["device_hist"] > 0
