@@ -243,10 +243,11 @@ def fit_tree(
         be.setup(codes_rm, codes_fm, yd, nb, n_bins=mapper.max_n_bins, n_classes=C,
                  criterion=crit)
         be.timing = profiling()  # synchronised per-phase timers (host-driven loop)
+        env = os.environ.get("MPITREE_FINISHER_ROWS")
+        # ~2 subtree jobs per workgroup slot of the finisher grid
+        default_fr = int(env) if env else max(2048, n // 512)
         if finisher_rows is None:
-            env = os.environ.get("MPITREE_FINISHER_ROWS")
-            # ~2 subtree jobs per workgroup slot of the finisher grid
-            finisher_rows = int(env) if env else max(2048, n // 512)
+            finisher_rows = default_fr
         if not be.finisher_supported():
             finisher_rows = 0
         finisher_rows = min(int(finisher_rows), be.max_finisher_rows)
@@ -254,7 +255,9 @@ def fit_tree(
         from ..ops.device_grower import DeviceGrower, device_loop_supported
 
         if device_loop_supported(be, params, comm):
-            builder = DeviceGrower(be, params)
+            if comm.world_size > 1:  # the redundant top levels use the 1-GPU split point
+                params.finisher_rows = min(default_fr, be.max_finisher_rows)
+            builder = DeviceGrower(be, params, comm)
             with roctx_range("mpitree.grow"):
                 ta = builder.fit(hi - lo, C, F, mapper.padded_edges(), y_exp)
             eng = "hip-device-loop"

@@ -43,8 +43,15 @@ __all__ = ["DeviceGrower", "device_loop_supported"]
 def device_loop_supported(be, params, comm) -> bool:
     if os.environ.get("MPITREE_DEVICE_LOOP", "1") == "0":
         return False
-    if getattr(comm, "world_size", 1) != 1 or be.reg:
+    if be.reg:
         return False
+    if getattr(comm, "world_size", 1) != 1:
+        # replicated rows: every rank runs the (cheap) level loop, the finisher
+        # jobs are split across ranks and the finished nodes all-gathered
+        if getattr(comm, "kind", "") not in ("auto", "subtree"):
+            return False
+        if not getattr(comm, "rows_replicated", False):
+            return False
     if params.finisher_rows <= 0 or not be.finisher_supported():
         return False
     # the planner drives the LDS histogram path only
@@ -52,9 +59,10 @@ def device_loop_supported(be, params, comm) -> bool:
 
 
 class DeviceGrower:
-    def __init__(self, be, params):
+    def __init__(self, be, params, comm=None):
         self.be = be
         self.p = params
+        self.comm = comm
         self.timings: dict = {}
         self.stats: dict = {}
 
@@ -69,6 +77,34 @@ class DeviceGrower:
             red=torch.empty((KMAX, 3), **i64), der=torch.empty((KMAX, 3), **i64),
             tasks=torch.empty((TMAX, 3), **i64), ctl=torch.zeros(8, **i32),
         )
+
+    def _run_jobs(self, d_jobs, n: int):
+        """Finish the (largest-first) job list; with several ranks each takes a
+        serpentine share (0..P-1, P-1..0, ...) -- near-even row totals."""
+        be, comm = self.be, self.comm
+        if comm is not None and comm.world_size > 1:
+            P, r = comm.world_size, comm.rank
+            k = torch.arange(d_jobs.shape[0], device=d_jobs.device)
+            lap, off = k // P, k % P
+            owner = torch.where(lap % 2 == 0, off, P - 1 - off)
+            d_jobs = d_jobs[owner == r]
+        J = int(d_jobs.shape[0])
+        if J:
+            be.launch_finisher(d_jobs.contiguous(), J, n, self.p, be.pos_rec, be.pos_st)
+
+    def _exchange_nodes(self):
+        """Every rank ends with every finished node: compact the written
+        positions ({pos, record[6], counts[C]} int32 rows), all-gather them and
+        scatter into the local position space. Level nodes are written by all
+        ranks identically, so their duplicates are harmless."""
+        be, comm = self.be, self.comm
+        live = torch.nonzero(be.pos_rec[:, 5] > 0).squeeze(1)
+        rows = torch.cat([live.to(torch.int32)[:, None], be.pos_rec[live],
+                          be.pos_st[live].to(torch.int32)], 1)
+        allr = comm.all_gather_rows(rows)
+        pos = allr[:, 0].long()
+        be.pos_rec.index_copy_(0, pos, allr[:, 1:7].contiguous())
+        be.pos_st.index_copy_(0, pos, allr[:, 7:].to(be.pos_st.dtype).contiguous())
 
     def _level_profile(self, marks):
         """Per-level device times (ms) from the HIP events (MPITREE_PROFILE=1)."""
@@ -226,12 +262,15 @@ class DeviceGrower:
             self._keep = (sets, hists, slab, rec, cost, bins, split, pitems, cursors)
             if J:
                 order = torch.argsort(jobs[:J, 1], descending=True, stable=True)
-                d_jobs = jobs[:J].index_select(0, order).contiguous()
-                be.launch_finisher(d_jobs, J, n, p, be.pos_rec, be.pos_st)
+                self._run_jobs(jobs[:J].index_select(0, order), n)
         elif jobs_host is not None:
             J = 1
             (d_jobs,) = be.up(jobs_host)
-            be.launch_finisher(d_jobs.view(1, -1), 1, n, p, be.pos_rec, be.pos_st)
+            self._run_jobs(d_jobs.view(1, -1), n)
+        if self.comm is not None and self.comm.world_size > 1:
+            t1 = time.perf_counter()
+            self._exchange_nodes()
+            self.timings["exchange"] = time.perf_counter() - t1
         self.timings["levels"] = time.perf_counter() - t0
         self.stats["levels"] = levels
         self.stats["finisher_subtrees"] = J

@@ -180,6 +180,24 @@ class DistComm(LocalComm):
         return bool(self._all_reduce(np.array([1 if failed else 0]),
                                      op=dist.ReduceOp.MAX)[0])
 
+    def all_gather_rows(self, t):
+        """All-gather a [k, w] int32 device tensor with per-rank k; returns the
+        concatenation [sum k, w] on the tensor's device (padded exchange)."""
+        import torch
+
+        k = int(t.shape[0])
+        sizes = self._all_gather(np.array([k], dtype=np.int64)).reshape(-1)
+        kmax = int(max(1, sizes.max()))
+        w = int(t.shape[1])
+        buf = torch.zeros((kmax, w), dtype=t.dtype, device=self.device)
+        if k:
+            buf[:k].copy_(t.to(self.device))
+        out = torch.empty((self.world_size * kmax, w), dtype=t.dtype, device=self.device)
+        dist.all_gather_into_tensor(out, buf, group=self.group)
+        self.bytes_communicated += buf.numel() * buf.element_size() * self.world_size
+        parts = [out[r * kmax : r * kmax + int(sizes[r])] for r in range(self.world_size)]
+        return torch.cat(parts, 0).to(t.device)
+
     def check_consistent(self, digest: int) -> bool:
         """Cross-rank check that every rank built the same tree."""
         a = self._all_gather(np.array([digest], dtype=np.int64))
@@ -270,6 +288,11 @@ class SubtreeComm(DistComm):
 
 
 class AutoComm(FeatureParallelComm):
+    """``strategy="auto"`` with replicated rows. Single-GPU-per-rank fits that
+    the device-driven loop supports use the replicated-top / split-finisher
+    scheme (:class:`~mpitree_amd.ops.device_grower.DeviceGrower`); everything
+    else runs feature-parallel levels with load-balanced subtree finishing."""
+
     kind = "auto"
 
 
@@ -282,8 +305,12 @@ def make_comm(strategy: str, X, y, *, device="auto", data_sharded=False, regress
     P = dist.get_world_size()
     strategy = (strategy or "auto").lower()
     if strategy == "auto":
-        strategy = "feature" if (F >= P and not data_sharded) else (
-            "data" if data_sharded else "subtree")
+        if data_sharded:
+            strategy = "data"
+        elif F >= P:
+            return AutoComm(), X, y
+        else:
+            strategy = "subtree"
     if data_sharded and strategy != "data":
         raise ValueError("data_sharded=True requires strategy='data'")
     if strategy == "feature":

@@ -101,7 +101,7 @@ def _fit_rank_gpu(rank, world, strategy, seed, md):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("strategy", ["feature", "data", "subtree"])
+@pytest.mark.parametrize("strategy", ["feature", "data", "subtree", "auto"])
 def test_gpu_ranks_equal_serial(strategy, monkeypatch):
     # two ranks sharing one MI355X over gloo: exercises the HIP backend with
     # every strategy's collectives (RCCL itself needs one GPU per rank)
@@ -112,7 +112,9 @@ def test_gpu_ranks_equal_serial(strategy, monkeypatch):
     X, y = _data(4, n=5000, F=9, C=3)
     ref = DecisionTreeClassifier(device="cpu").fit(X, y).tree_arrays_
     for o in outs:
-        assert str(o["engine"][0]).startswith("hip")
+        eng = str(o["engine"][0])
+        # auto/subtree: replicated device level loop + split finisher + node exchange
+        assert eng == ("hip-device-loop" if strategy in ("auto", "subtree") else "hip-levelwise")
         for k in FIELDS:
             np.testing.assert_array_equal(o[k], getattr(ref, k))
 
