@@ -358,20 +358,24 @@ class _ParallelMixin:
             self._fit_impl(X, y, comm=comm, **comm.fit_kwargs())
         except Exception as e:  # reported to every rank below
             error = e
-        self._raise_if_any_failed(comm, error)
-        if os.environ.get("MPITREE_CHECK_CONSISTENCY", "1") != "0":
-            if not comm.check_consistent(tree_digest(self._arrays)):
-                raise RuntimeError("ranks built different trees (digest mismatch)")
+        # one all-gather of {failed, tree digest}: failure propagation + consistency
+        check = os.environ.get("MPITREE_CHECK_CONSISTENCY", "1") != "0"
+        digest = tree_digest(self._arrays) if (error is None and check) else 0
+        st = comm._all_gather(np.array([1 if error is not None else 0, digest], np.int64))
+        if st[:, 0].any():
+            self._raise_if_any_failed(comm, error, known_failed=True)
+        if check and not (st[:, 1] == st[0, 1]).all():
+            raise RuntimeError("ranks built different trees (digest mismatch)")
         return self
 
 
     @staticmethod
-    def _raise_if_any_failed(comm, error):
+    def _raise_if_any_failed(comm, error, known_failed=False):
         from ..utils.observability import logger
 
         if error is not None:
             logger.error("rank %d: collective fit failed: %r", comm.rank, error)
-        if comm.any_failed(error is not None):
+        if known_failed or comm.any_failed(error is not None):
             if error is not None:
                 raise error
             raise RuntimeError("collective fit failed on another rank")

@@ -65,16 +65,23 @@ def roctx_range(name: str):
 
 
 def tree_digest(ta) -> int:
-    """63-bit digest of the tree structure, thresholds and node statistics."""
-    h = hashlib.blake2b(digest_size=8)
-    for a in (ta.feature, ta.threshold_bin, ta.left, ta.right, ta.n_samples):
-        h.update(np.ascontiguousarray(a).tobytes())
-    h.update(np.ascontiguousarray(ta.threshold).view(np.int64).tobytes())
-    if ta.count is not None:
-        h.update(np.ascontiguousarray(ta.count).tobytes())
-    if ta.value is not None:
-        h.update(np.ascontiguousarray(ta.value).view(np.int64).tobytes())
-    return int.from_bytes(h.digest(), "little") & ((1 << 63) - 1)
+    """63-bit digest of the tree structure: split features and bins, child
+    links and node sizes (thresholds and statistics follow from these and the
+    shared bin edges). xxh3 over the arrays in place: ~0.3 ms for 200k nodes."""
+    parts = (ta.feature, ta.threshold_bin, ta.left, ta.right, ta.n_samples)
+    try:
+        import xxhash
+
+        h = xxhash.xxh3_64()
+        for a in parts:
+            h.update(memoryview(np.ascontiguousarray(a)).cast("B"))
+        d = h.intdigest()
+    except ImportError:  # pragma: no cover - xxhash ships with the image
+        h = hashlib.blake2b(digest_size=8)
+        for a in parts:
+            h.update(np.ascontiguousarray(a).tobytes())
+        d = int.from_bytes(h.digest(), "little")
+    return d & ((1 << 63) - 1)
 
 
 class InjectedFault(RuntimeError):
