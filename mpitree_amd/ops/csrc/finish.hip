@@ -24,6 +24,7 @@
 // child at p + 2 n_left. Every position is fixed by row counts alone -- no
 // allocation counter, no renumbering -- and compacting the written positions
 // (assemble.hip) yields the tree in exact pre-order, bitwise deterministic.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -44,6 +45,11 @@ constexpr int kFinChunk = 16;    // features per wave whose per-lane minima stay
 // Histogram row stride in words: >= B*W + 1 (the odd word staggers features over
 // LDS banks for the atomics), rounded to 4 so each feature row is 16-B aligned.
 __host__ __device__ inline int fin_fstride(int B, int W) { return ((B * W + 1) + 3) & ~3; }
+
+inline int getenv_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
 
 struct FinRowLab {
   uint32_t mask;
@@ -890,6 +896,205 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Tiny subtrees, C <= 2: presorted per-feature lane orders.
+//
+// A child's rows are a subset of its parent's, so the order of the subtree's
+// rows by each feature's code is computed once per tiny subtree (the 8-ballot
+// radix rank of finish_tiny_kernel, plus the lane's position among equal
+// codes) and stored in LDS. At every node of the subtree, sorted position k
+// holds lane order_f[k]; one packed DPP prefix sum of {in node, in node and
+// class 1} along the sorted order gives both left counts of the split "code
+// <= code of position k", which is a valid split where k is the last node row
+// of its code. The wave keeps each lane's best (gain, feature, cost, code) and
+// reduces once per node -- the same decision rule as the per-node kernel.
+//
+// LDS per wave: codes [64][cw] words (cw = ceil(F/4) | 1) + order [F][64] bytes.
+__global__ __launch_bounds__(256) void finish_tiny_sorted_kernel(
+    const uint32_t* __restrict__ codes_rm, int64_t row_words, const uint32_t* __restrict__ buf0,
+    const uint32_t* __restrict__ buf1, const int32_t* __restrict__ y, FinRowLab rl,
+    const int64_t* __restrict__ tiny, const int32_t* __restrict__ tiny_count,
+    int32_t* __restrict__ tiny_counter, int F, int C, int crit, int max_depth, int64_t mss,
+    int64_t msl, const double* __restrict__ xtab, int32_t* __restrict__ node_i32,
+    int32_t* __restrict__ node_cnt, int cw) {
+  extern __shared__ __align__(16) uint32_t dyn[];
+  __shared__ double s_tab[kTinyRows + 1];
+  __shared__ unsigned long long s_mask[kTinyWaves][16];
+  __shared__ int32_t s_dep[kTinyWaves][16], s_slot[kTinyWaves][16];
+  const int lane = lane_id();
+  const int wave = threadIdx.x >> 6;
+  const int per_wave_words = kWave * cw + (F * kWave + 3) / 4;
+  uint32_t* wbase = dyn + wave * per_wave_words;
+  uint32_t* my_codes = wbase + lane * cw;
+  const uint8_t* codes_b = reinterpret_cast<const uint8_t*>(wbase);  // [lane][cw*4]
+  uint8_t* order = reinterpret_cast<uint8_t*>(wbase + kWave * cw);   // [F][64]
+  const uint8_t* my_bytes = reinterpret_cast<const uint8_t*>(my_codes);
+  for (int i = threadIdx.x; i <= kTinyRows; i += blockDim.x) s_tab[i] = xtab[i];
+  __syncthreads();
+  const int K = *tiny_count;
+  const int nw = (int)min<int64_t>(row_words, (int64_t)cw);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (;;) {
+    int k = 0;
+    if (lane == 0) k = atomicAdd(tiny_counter, 1);
+    k = __builtin_amdgcn_readfirstlane(k);
+    if (k >= K) break;
+    const int64_t* rec = tiny + (int64_t)k * 8;
+    const int64_t start = rec[0];
+    const int m = (int)rec[1];
+    const int depth0 = (int)rec[2];
+    const uint32_t* src = rec[3] ? buf1 : buf0;
+    const int64_t root_slot = rec[4];
+    const bool act = lane < m;
+    int lab = 0;
+    if (act) {
+      const uint32_t ent = src[start + lane];
+      const uint32_t row = rl.shift ? (ent & rl.mask) : ent;
+      lab = rl.shift ? (int)(ent >> rl.shift) : y[row];
+      for (int i = 0; i < nw; ++i) my_codes[i] = codes_rm[(int64_t)row * row_words + i];
+    }
+    const unsigned long long R = m == 64 ? ~0ull : ((1ull << m) - 1ull);
+    const unsigned long long cm1 = C > 1 ? __ballot(act && lab == 1) : 0ull;
+    const unsigned long long cm0 = R & ~cm1;
+    // ---- presort: order_f[position] = lane, stable by lane among equal codes
+    for (int f = 0; f < F; ++f) {
+      const uint32_t code = my_bytes[f];
+      unsigned long long eq = R, gt = 0ull;
+#pragma unroll
+      for (int b = 7; b >= 0; --b) {
+        const unsigned long long bm = __ballot((code >> b) & 1u) & R;
+        if ((code >> b) & 1u) {
+          eq &= bm;
+        } else {
+          gt |= eq & bm;
+          eq &= ~bm;
+        }
+      }
+      const unsigned long long lt = R & ~gt & ~eq;
+      if (act) order[f * kWave + __popcll(lt) + __popcll(eq & below)] = (uint8_t)lane;
+    }
+    if (lane == 0) {
+      s_mask[wave][0] = R;
+      s_dep[wave][0] = depth0;
+      s_slot[wave][0] = (int32_t)root_slot;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    int sp = 1;
+    while (sp > 0) {
+      --sp;
+      const unsigned long long M = s_mask[wave][sp];
+      const int d = s_dep[wave][sp];
+      const int64_t slot = s_slot[wave][sp];
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const int mm = __popcll(M);
+      const uint32_t mc1 = (uint32_t)__popcll(M & cm1), mc0 = (uint32_t)mm - mc1;
+      const double pterm = crit == kEntropy
+                               ? s_tab[mm] - (s_tab[mc0] + s_tab[mc1])
+                               : gini_term(mm, (int64_t)mc0 * mc0 + (int64_t)mc1 * mc1);
+      double bg = -__builtin_inf(), bc = __builtin_inf();
+      int bf = 0x7fffffff;
+      uint32_t bb = 0xffffffffu;
+      for (int f = 0; f < F; ++f) {
+        // sorted position = lane; only positions < m hold rows of the subtree
+        const int s = act ? order[f * kWave + lane] : 0;
+        const bool in = act && ((M >> s) & 1ull);
+        const uint32_t code = codes_b[s * cw * 4 + f];
+        const uint32_t packed = (in ? 1u : 0u) | ((in && ((cm1 >> s) & 1ull)) ? 0x10000u : 0u);
+        const uint32_t incl = wave_incl_scan_dpp(packed);
+        const uint32_t ml = incl & 0xffffu, l1 = incl >> 16, l0 = ml - l1;
+        // the split "code <= mine" is taken at the last node row of each code
+        const unsigned long long inb = __ballot(in);
+        const unsigned long long after = inb & ~(below | (1ull << lane));
+        const int nxt = after ? __ffsll((long long)after) - 1 : lane;
+        const uint32_t ncode = (uint32_t)__shfl((int)code, nxt, kWave);
+        const bool last = in && (after == 0ull || ncode != code);
+        const int mr = mm - (int)ml;
+        double cost = __builtin_inf();
+        if (last && (int64_t)ml >= msl && (int64_t)mr >= msl) {
+          const uint32_t r0 = mc0 - l0, r1 = mc1 - l1;
+          if (crit == kEntropy) {
+            const double sl = s_tab[l0] + s_tab[l1];
+            const double sr = s_tab[r0] + s_tab[r1];
+            cost = (s_tab[ml] - sl) + (s_tab[mr] - sr);
+          } else {
+            cost = gini_term(ml, (int64_t)l0 * l0 + (int64_t)l1 * l1) +
+                   gini_term(mr, (int64_t)r0 * r0 + (int64_t)r1 * r1);
+          }
+        }
+        const double g = pterm - cost;
+        if (g > bg) {  // features ascend: strict > keeps the lowest
+          bg = g;
+          bf = f;
+          bc = cost;
+          bb = code;
+        }
+      }
+#pragma unroll
+      for (int dd = kWave / 2; dd > 0; dd >>= 1) {
+        const double og = __shfl_xor(bg, dd, kWave);
+        const int of = __shfl_xor(bf, dd, kWave);
+        const double oc = __shfl_xor(bc, dd, kWave);
+        const uint32_t ob = (uint32_t)__shfl_xor((int)bb, dd, kWave);
+        const bool take =
+            og > bg ||
+            (og == bg && (of < bf || (of == bf && (oc < bc || (oc == bc && ob < bb)))));
+        if (take) {
+          bg = og;
+          bf = of;
+          bc = oc;
+          bb = ob;
+        }
+      }
+      bf = __builtin_amdgcn_readfirstlane(bf);
+      bb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bb);
+      if (!(bg > -__builtin_inf()) || bf < 0) continue;  // leaf: the creation record stands
+      const unsigned long long LM = M & __ballot(act && (uint32_t)my_bytes[bf] <= bb);
+      const unsigned long long RM = M & ~LM;
+      const int nl = __popcll(LM), nr = __popcll(RM);
+      const int64_t ls = slot + 1, rs = slot + 2 * nl;  // pre-order position ranges
+      const int lc1 = __popcll(LM & cm1), rc1 = (int)mc1 - lc1;
+      const int lc0 = nl - lc1, rc0 = nr - rc1;
+      const int nzl = (lc0 > 0) + (lc1 > 0), nzr = (rc0 > 0) + (rc1 > 0);
+      const int cd = d + 1;
+      if (lane == 0) {
+        int32_t* P = node_i32 + slot * 6;
+        P[0] = bf;
+        P[1] = (int32_t)bb;
+        P[2] = (int32_t)ls;
+        P[3] = (int32_t)rs;
+        int32_t* L = node_i32 + ls * 6;
+        int32_t* Rr = node_i32 + rs * 6;
+        L[0] = -1; L[1] = -1; L[2] = -1; L[3] = -1; L[4] = cd; L[5] = nl;
+        Rr[0] = -1; Rr[1] = -1; Rr[2] = -1; Rr[3] = -1; Rr[4] = cd; Rr[5] = nr;
+        node_cnt[ls * C + 0] = lc0;
+        node_cnt[rs * C + 0] = rc0;
+        if (C > 1) {
+          node_cnt[ls * C + 1] = lc1;
+          node_cnt[rs * C + 1] = rc1;
+        }
+      }
+      const bool depth_stop = max_depth >= 0 && cd >= max_depth;
+      const bool tlf = depth_stop || nl < mss || nl < 2 * msl || nzl <= 1;
+      const bool trf = depth_stop || nr < mss || nr < 2 * msl || nzr <= 1;
+      const bool left_small = nl <= nr;
+      for (int pass = 0; pass < 2; ++pass) {
+        const bool is_left = (pass == 0) ? !left_small : left_small;
+        if (is_left ? tlf : trf) continue;
+        if (lane == 0) {
+          s_mask[wave][sp] = is_left ? LM : RM;
+          s_dep[wave][sp] = cd;
+          s_slot[wave][sp] = (int32_t)(is_left ? ls : rs);
+        }
+        ++sp;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
 int finish_lds_bytes(int F, int B, int C) { return F * fin_fstride(B, (C + 1) / 2) * 4; }
 int finish_max_classes() { return kFinMaxC; }
 
@@ -935,10 +1140,22 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
 #undef MT_FIN
   MT_HIP_CHECK(hipGetLastError());
   if (tiny_rows > 0) {
-    hipLaunchKernelGGL(finish_tiny_kernel, dim3(tiny_grid), dim3(kTinyWaves * kWave), 0, stream,
-                       (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,
-                       counter + 1, counter + 2, F, C, crit, max_depth, mss, msl, xtab,
-                       node_i32, node_cnt);
+    const bool sorted = C <= 2 && getenv_int("MPITREE_TINY_SORTED", 1) != 0;
+    if (sorted) {
+      const int cw = ((F + 3) / 4) | 1;  // odd row stride: lanes spread over LDS banks
+      const size_t lds = (size_t)kTinyWaves * (kWave * cw + (F * kWave + 3) / 4) * 4;
+      MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_tiny_sorted_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(finish_tiny_sorted_kernel, dim3(tiny_grid), dim3(kTinyWaves * kWave),
+                         lds, stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl,
+                         tiny, counter + 1, counter + 2, F, C, crit, max_depth, mss, msl, xtab,
+                         node_i32, node_cnt, cw);
+    } else {
+      hipLaunchKernelGGL(finish_tiny_kernel, dim3(tiny_grid), dim3(kTinyWaves * kWave), 0,
+                         stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,
+                         counter + 1, counter + 2, F, C, crit, max_depth, mss, msl, xtab,
+                         node_i32, node_cnt);
+    }
     MT_HIP_CHECK(hipGetLastError());
   }
 }
