@@ -9,17 +9,17 @@ from mpitree_amd.core import fit as fitmod
 from mpitree_amd.ops import hip_backend as hb
 
 keep = {}
-orig = hb.HipBackend.finish_subtrees
+orig = hb.HipBackend.launch_finisher
 
 
-def spy(self, *a, **k):
-    out = orig(self, *a, **k)
+def spy(self, d_jobs, J, *a, **k):
+    out = orig(self, d_jobs, J, *a, **k)
     keep["prof"] = self.last_finisher_prof
-    keep["counts"] = np.asarray(a[1])
+    keep["counts"] = d_jobs[:, 1].cpu().numpy()
     return out
 
 
-hb.HipBackend.finish_subtrees = spy
+hb.HipBackend.launch_finisher = spy
 X, y = make_classification(1_000_000, 64, seed=0)
 for _ in range(3):
     r = fitmod.fit_tree(X, y, regression=False, criterion=0, max_depth=None, min_samples_split=2,

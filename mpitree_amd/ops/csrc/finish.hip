@@ -75,7 +75,10 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
   // x*log2(x) table: fp64 entries (generic path) or, for C <= 2, twice as many
   // fp32 entries that drive the approximate first pass of the split scan
   __shared__ double s_tab[kFinTab];
+  // C <= 2 splits the same 8 KB: fp32 entries [0, kFinTab) in the first half,
+  // fp64 entries [0, kFinTab / 4) in the second (exact rescoring, node terms)
   float* const s_tabf = reinterpret_cast<float*>(s_tab);
+  double* const s_tabd = s_tab + kFinTab / 2;
   __shared__ int32_t s_nb[kFinMaxF];
   __shared__ float s_fmin[kFinMaxF];
   __shared__ float w_fmin[kFinWaves];
@@ -103,7 +106,8 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
   const int fstride = fin_fstride(B, W);
   constexpr int cpw = 4 / sizeof(CodeT);
   const int words = (F + cpw - 1) / cpw;
-  const int tn = min(kC2 ? 2 * kFinTab : kFinTab, xtab_n);
+  const int tn = min(kFinTab, xtab_n);
+  const int tnd = min(kFinTab / 4, xtab_n);  // C <= 2: fp64 entries kept in LDS
   const int JW = 5 + C;
   // 16-B row loads when the row stride allows it; lanes per row = pow2 >= words/vec
   const int vec = (row_words % 4) == 0 ? 4 : 1;
@@ -122,6 +126,7 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
   };
   if constexpr (kC2) {
     for (int i = tid; i < tn; i += kFinThreads) s_tabf[i] = xtabf[i];
+    for (int i = tid; i < tnd; i += kFinThreads) s_tabd[i] = xtab[i];
   } else {
     for (int i = tid; i < tn; i += kFinThreads) s_tab[i] = xtab[i];
   }
@@ -131,7 +136,9 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
   for (int e = tid; e < hist_q; e += kFinThreads) hist4[e] = make_uint4(0, 0, 0, 0);
 
   auto tl = [&](uint64_t x) -> double {
-    if constexpr (kC2) return x < (uint64_t)xtab_n ? __ldg(xtab + x) : xlog2x(x);
+    if constexpr (kC2)
+      return x < (uint64_t)tnd ? s_tabd[x]
+                               : (x < (uint64_t)xtab_n ? __ldg(xtab + x) : xlog2x(x));
     return x < (uint64_t)tn ? s_tab[x] : (x < (uint64_t)xtab_n ? __ldg(xtab + x) : xlog2x(x));
   };
 
@@ -212,7 +219,8 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
   // Exact (fp64, global table) best split of one feature: (cost, lowest bin).
   auto scan_c2 = [&](const uint32_t* h, int nb, uint32_t t0, uint32_t t1, int m,
                      double& best_cost, int& best_bin) {
-    auto lk = [&](uint32_t x) -> double { return __ldg(xtab + x); };
+    const bool small = m < tnd;  // wave-uniform: every count of the node is in LDS
+    auto lk = [&](uint32_t x) -> double { return small ? s_tabd[x] : __ldg(xtab + x); };
     uint32_t v[4], lp;
     load_c2(h, nb, v, lp);
     best_cost = __builtin_inf();
