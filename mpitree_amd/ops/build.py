@@ -30,7 +30,7 @@ EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 ARCH = os.environ.get("MPITREE_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["hist.hip", "split_scan.hip", "partition.hip", "predict.hip", "misc.hip",
-               "finish.hip", "assemble.hip", "binning.hip", "grow.hip",
+               "finish.hip", "finish_reg.hip", "assemble.hip", "binning.hip", "grow.hip",
                "bindings.cpp"]
 CPU_SOURCES = ["cpu_builder.cpp"]
 HEADERS = ["common.h", "criterion.h"]

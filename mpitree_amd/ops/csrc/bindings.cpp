@@ -66,6 +66,9 @@ struct LevelLists {
   int64_t* der;
   int64_t* tasks;
   int32_t* ctl;
+  int64_t* stats64;
+  int64_t* minmax;
+  int64_t* mitems;
 };
 struct PlanArgs {
   LevelLists cur, nxt;
@@ -76,12 +79,21 @@ struct PlanArgs {
   int32_t* pctl;
   int32_t* pos_rec;
   int32_t* pos_st;
+  int64_t* pos_st64;
+  int reg;
   int64_t* jobs;
   int32_t* job_count;
   int C, max_depth, n_cu;
   int64_t mss, msl, fr;
 };
 void launch_grow_plan(hipStream_t, const PlanArgs&);
+int finish_reg_lds_bytes(int B);
+void launch_finish_reg(hipStream_t, const void*, int64_t, const void*, int, int64_t, uint32_t*,
+                       uint32_t*, const int64_t*, const int64_t*, int, int32_t*, const int32_t*,
+                       int, int, int, int64_t, int64_t, int32_t*, int64_t*, int, int, int64_t*,
+                       int);
+void launch_seg_minmax(hipStream_t, const uint32_t*, const int64_t*, const int64_t*, int, int64_t*,
+                       const int32_t*);
 void launch_hist_reduce_tasks(hipStream_t, const int64_t*, int, const int64_t*, int, const void*,
                               void*, int, int, int, const int32_t*, const int32_t*);
 int edges_sample_rows(bool x64);
@@ -182,6 +194,24 @@ PYBIND11_MODULE(_hip, m) {
                       P<int64_t>(tiny), tiny_grid, P<int64_t>(prof));
   });
   m.def("asm_tiles", &mt::asm_tiles);
+  m.def("finish_reg_lds_bytes", &mt::finish_reg_lds_bytes);
+  m.def("finish_reg", [](uintptr_t s, uintptr_t codes_rm, int64_t row_words, uintptr_t codes_fm,
+                         int cb, int64_t n_rows, uintptr_t buf0, uintptr_t buf1, uintptr_t y,
+                         uintptr_t jobs, int J, uintptr_t counter, uintptr_t nbins, int F, int B,
+                         int max_depth, int64_t mss, int64_t msl, uintptr_t node_i32,
+                         uintptr_t node_st, int grid, int tiny_rows, uintptr_t tiny,
+                         int tiny_grid) {
+    mt::launch_finish_reg(S(s), P<void>(codes_rm), row_words, P<void>(codes_fm), cb, n_rows,
+                          P<uint32_t>(buf0), P<uint32_t>(buf1), P<int64_t>(y), P<int64_t>(jobs),
+                          J, P<int32_t>(counter), P<int32_t>(nbins), F, B, max_depth, mss, msl,
+                          P<int32_t>(node_i32), P<int64_t>(node_st), grid, tiny_rows,
+                          P<int64_t>(tiny), tiny_grid);
+  });
+  m.def("seg_minmax", [](uintptr_t s, uintptr_t idx, uintptr_t y, uintptr_t items, int n_items,
+                         uintptr_t out, uintptr_t dcount) {
+    mt::launch_seg_minmax(S(s), P<uint32_t>(idx), P<int64_t>(y), P<int64_t>(items), n_items,
+                          P<int64_t>(out), P<int32_t>(dcount));
+  });
   m.def("hist_reduce_tasks", [](uintptr_t s, uintptr_t red, int red_bound, uintptr_t tasks,
                                 int task_bound, uintptr_t slab, uintptr_t hist, int F_h, int B,
                                 int C, uintptr_t dred, uintptr_t dtasks) {
@@ -192,19 +222,22 @@ PYBIND11_MODULE(_hip, m) {
   // cur / nxt: dicts of device pointers {pos, start, cnt, depth, stats, items, red, der, ctl}
   m.def("grow_plan", [](uintptr_t s, py::dict cur, py::dict nxt, uintptr_t rec, uintptr_t split,
                         uintptr_t pitems, uintptr_t cursors, uintptr_t pctl, uintptr_t pos_rec,
-                        uintptr_t pos_st, uintptr_t jobs, uintptr_t job_count, int C,
-                        int max_depth, int n_cu, int64_t mss, int64_t msl, int64_t fr) {
+                        uintptr_t pos_st, uintptr_t pos_st64, int reg, uintptr_t jobs,
+                        uintptr_t job_count, int C, int max_depth, int n_cu, int64_t mss,
+                        int64_t msl, int64_t fr) {
     auto lists = [](py::dict d) {
       auto g = [&](const char* k) { return d[k].cast<uintptr_t>(); };
       return mt::LevelLists{P<int64_t>(g("pos")),  P<int64_t>(g("start")), P<int32_t>(g("cnt")),
                             P<int32_t>(g("depth")), P<int32_t>(g("stats")), P<int64_t>(g("items")),
                             P<int64_t>(g("red")),  P<int64_t>(g("der")),   P<int64_t>(g("tasks")),
-                            P<int32_t>(g("ctl"))};
+                            P<int32_t>(g("ctl")),  P<int64_t>(g("stats64")),
+                            P<int64_t>(g("minmax")), P<int64_t>(g("mitems"))};
     };
     mt::PlanArgs a{lists(cur),          lists(nxt),         P<int64_t>(rec),
                    P<int64_t>(split),   P<int64_t>(pitems), P<int32_t>(cursors),
                    P<int32_t>(pctl),    P<int32_t>(pos_rec), P<int32_t>(pos_st),
-                   P<int64_t>(jobs),    P<int32_t>(job_count), C, max_depth, n_cu, mss, msl, fr};
+                   P<int64_t>(pos_st64), reg, P<int64_t>(jobs), P<int32_t>(job_count), C,
+                   max_depth, n_cu, mss, msl, fr};
     mt::launch_grow_plan(S(s), a);
   });
   m.def("edges_sample_rows", &mt::edges_sample_rows);

@@ -1,0 +1,566 @@
+// Subtree finisher for regression trees (squared error) on gfx950.
+//
+// Same contract as the classification finisher (finish.hip): jobs are
+// deferred frontier nodes with at most ``finisher_rows`` rows, every node is
+// written at its pre-order position (a subtree of r rows owns 2r - 1
+// positions), children at p + 1 and p + 2 n_left. Differences:
+//
+// * statistics are {count, fixed-point target sum} (int64); a node whose
+//   targets are all equal is a leaf -- the reference-style stopping rule for
+//   regression -- checked from the min / max of its rows when it is popped;
+// * finish_reg_kernel (nodes above the tiny size): one 256-thread workgroup
+//   per job. A node's histogram {count u32, sum i64} per (feature, bin) is
+//   48 KB per 16 features, so features are processed in LDS tiles of 16: build
+//   the tile from the node's rows, wave-per-feature prefix scans (DPP for the
+//   counts, 64-bit shuffles for the sums), cost = -S_L^2/m_L - S_R^2/m_R with
+//   the shared mse_term, then the next tile. Ties: lowest bin, lowest feature.
+// * finish_tiny_reg_kernel (<= 64 rows): one wavefront per subtree with the
+//   presorted per-feature lane orders of finish_tiny_sorted_kernel; per node
+//   and feature one count scan and one 64-bit sum scan along the sorted order.
+#include <climits>
+#include <cstdlib>
+
+#include "common.h"
+#include "criterion.h"
+
+namespace mt {
+
+constexpr int kRegThreads = 256;
+constexpr int kRegWaves = kRegThreads / kWave;
+constexpr int kRegFT = 16;      // features per LDS tile
+constexpr int kRegStack = 40;
+constexpr int kRegTinyRows = 64;
+constexpr int kRegTinyWaves = 4;
+constexpr int kRegMaxF = 256;
+
+// Wave-wide min / max of int64 (every lane gets the result).
+__device__ __forceinline__ void wave_minmax_i64(long long& mn, long long& mx) {
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    const long long a = __shfl_xor(mn, d, kWave), b = __shfl_xor(mx, d, kWave);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+}
+
+// jobs: int64 [J][7] = {start, count, depth, root position, buffer, count, sum}
+// node_i32: [P][6] = {feature, bin, left pos, right pos, depth, n}; node_st: int64 [P][2]
+template <typename CodeT>
+__global__ __launch_bounds__(kRegThreads, 2) void finish_reg_kernel(
+    const uint32_t* __restrict__ codes_rm, int64_t row_words, const CodeT* __restrict__ codes_fm,
+    int64_t n_rows, uint32_t* __restrict__ buf0, uint32_t* __restrict__ buf1,
+    const int64_t* __restrict__ y, const int64_t* __restrict__ jobs, int J,
+    int32_t* __restrict__ job_counter, const int32_t* __restrict__ nbins, int F, int B,
+    int max_depth, int64_t mss, int64_t msl, int32_t* __restrict__ node_i32,
+    int64_t* __restrict__ node_st, int tiny_rows, int64_t* __restrict__ tiny,
+    int32_t* __restrict__ tiny_count) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  unsigned long long* t_sum = reinterpret_cast<unsigned long long*>(smem);  // [FT][B]
+  uint32_t* t_cnt = reinterpret_cast<uint32_t*>(smem + (size_t)kRegFT * B * 8);  // [FT][B]
+  __shared__ int32_t s_nb[kRegMaxF];
+  __shared__ int s_job, s_sp;
+  __shared__ int64_t s_st_start[kRegStack], s_st_sum[kRegStack];
+  __shared__ int32_t s_st_count[kRegStack], s_st_depth[kRegStack], s_st_id[kRegStack],
+      s_st_buf[kRegStack];
+  __shared__ int64_t s_start, s_sum;
+  __shared__ int32_t s_count, s_depth, s_id, s_buf;
+  __shared__ long long s_min, s_max;
+  __shared__ unsigned long long s_lsum;
+  __shared__ double w_gain[kRegWaves];
+  __shared__ int w_feat[kRegWaves], w_bin[kRegWaves];
+  __shared__ int s_lc, s_rc;
+
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = lane_id();
+  const int n_tiles = (F + kRegFT - 1) / kRegFT;
+  const int tile_words = kRegFT * B;  // per array
+  const bool vec4 = (row_words % 4) == 0 && sizeof(CodeT) == 1;
+  for (int f = tid; f < F; f += kRegThreads) s_nb[f] = min(B, nbins[f]);
+  __syncthreads();
+
+  for (;;) {
+    if (tid == 0) s_job = atomicAdd(job_counter, 1);
+    __syncthreads();
+    const int job = s_job;
+    if (job >= J) break;
+    const int64_t* jb = jobs + (int64_t)job * 7;
+    if (tid == 0) {
+      const int r = (int)jb[3];
+      int32_t* R = node_i32 + (int64_t)r * 6;
+      R[0] = -1;
+      R[1] = -1;
+      R[2] = -1;
+      R[3] = -1;
+      R[4] = (int32_t)jb[2];
+      R[5] = (int32_t)jb[1];
+      node_st[(int64_t)r * 2 + 0] = jb[5];
+      node_st[(int64_t)r * 2 + 1] = jb[6];
+      s_sp = 0;
+      if (jb[1] <= tiny_rows) {  // the whole job goes to a wavefront
+        const int t = atomicAdd(tiny_count, 1);
+        int64_t* tr = tiny + (int64_t)t * 8;
+        tr[0] = jb[0];
+        tr[1] = jb[1];
+        tr[2] = jb[2];
+        tr[3] = jb[4];
+        tr[4] = r;
+      } else {
+        s_sp = 1;
+        s_st_start[0] = jb[0];
+        s_st_count[0] = (int32_t)jb[1];
+        s_st_depth[0] = (int32_t)jb[2];
+        s_st_id[0] = r;
+        s_st_buf[0] = (int32_t)jb[4];
+        s_st_sum[0] = jb[6];
+      }
+    }
+    __syncthreads();
+    while (s_sp > 0) {
+      __syncthreads();
+      if (tid == 0) {
+        const int sp = --s_sp;
+        s_start = s_st_start[sp];
+        s_count = s_st_count[sp];
+        s_depth = s_st_depth[sp];
+        s_id = s_st_id[sp];
+        s_buf = s_st_buf[sp];
+        s_sum = s_st_sum[sp];
+        s_min = LLONG_MAX;
+        s_max = LLONG_MIN;
+        s_lc = 0;
+        s_rc = 0;
+        s_lsum = 0ull;
+      }
+      __syncthreads();
+      const int64_t start = s_start;
+      const int m = s_count;
+      const int depth = s_depth;
+      const int id = s_id;
+      const int64_t S = s_sum;
+      uint32_t* __restrict__ src = s_buf ? buf1 : buf0;
+      uint32_t* __restrict__ dst = s_buf ? buf0 : buf1;
+      const double pterm = mse_term(m, S);
+      double bg = -__builtin_inf();
+      int bfeat = 0x7fffffff, bbin = -1;
+      bool pure = false;
+      for (int t = 0; t < n_tiles; ++t) {
+        const int f0 = t * kRegFT;
+        const int nf = min(kRegFT, F - f0);
+        {  // clear the tile (sums then counts are contiguous: 12 B per (feature, bin))
+          uint4* z = reinterpret_cast<uint4*>(smem);
+          const int q = tile_words * 12 / 16;
+          for (int e = tid; e < q; e += kRegThreads) z[e] = make_uint4(0, 0, 0, 0);
+        }
+        __syncthreads();
+        long long mn = LLONG_MAX, mx = LLONG_MIN;
+        for (int r = tid; r < m; r += kRegThreads) {
+          const uint32_t row = src[start + r];
+          const long long yv = y[row];
+          if (t == 0) {
+            mn = yv < mn ? yv : mn;
+            mx = yv > mx ? yv : mx;
+          }
+          uint32_t w[4];
+          const uint32_t* rp = codes_rm + (int64_t)row * row_words;
+          if (vec4) {
+            const uint4 v = *reinterpret_cast<const uint4*>(rp + f0 / 4);
+            w[0] = v.x;
+            w[1] = v.y;
+            w[2] = v.z;
+            w[3] = v.w;
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w[k] = 0u;
+          }
+#pragma unroll
+          for (int fl = 0; fl < kRegFT; ++fl) {
+            if (fl < nf) {
+              uint32_t code;
+              if (vec4) {
+                code = (w[fl >> 2] >> ((fl & 3) * 8)) & 0xffu;
+              } else {
+                const CodeT* cp = reinterpret_cast<const CodeT*>(rp);
+                code = (uint32_t)cp[f0 + fl];
+              }
+              atomicAdd(&t_cnt[fl * B + (int)code], 1u);
+              atomicAdd(&t_sum[fl * B + (int)code], (unsigned long long)yv);
+            }
+          }
+        }
+        if (t == 0) {
+          wave_minmax_i64(mn, mx);
+          if (lane == 0) {
+            atomicMin(&s_min, mn);
+            atomicMax(&s_max, mx);
+          }
+        }
+        __syncthreads();
+        if (t == 0 && s_min == s_max) {
+          pure = true;  // all targets equal: a leaf (its record already stands)
+          break;
+        }
+        // ---- scan the tile: wave w takes features f0 + w, f0 + w + 4, ...
+        for (int fl = wave; fl < nf; fl += kRegWaves) {
+          const int f = f0 + fl;
+          const int nb = s_nb[f];
+          const int b0 = lane * 4;
+          uint32_t cn[4];
+          long long cs[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int b = b0 + k;
+            cn[k] = b < nb ? t_cnt[fl * B + b] : 0u;
+            cs[k] = b < nb ? (long long)t_sum[fl * B + b] : 0ll;
+          }
+          uint32_t pn[4];
+          long long ps[4];
+          pn[0] = cn[0];
+          ps[0] = cs[0];
+#pragma unroll
+          for (int k = 1; k < 4; ++k) {
+            pn[k] = pn[k - 1] + cn[k];
+            ps[k] = ps[k - 1] + cs[k];
+          }
+          const uint32_t en = wave_incl_scan_dpp(pn[3]) - pn[3];
+          const long long es = (long long)wave_incl_scan_i64((int64_t)ps[3]) - ps[3];
+          double best_cost = __builtin_inf();
+          int best_bin = 0x7fffffff;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int64_t ml = (int64_t)(en + pn[k]);
+            const int64_t sl = (int64_t)(es + ps[k]);
+            const int64_t mr = (int64_t)m - ml;
+            if (b0 + k < nb && cn[k] > 0 && ml >= msl && mr >= msl) {
+              const double cost = mse_term(ml, sl) + mse_term(mr, S - sl);
+              if (cost < best_cost) {
+                best_cost = cost;
+                best_bin = b0 + k;
+              }
+            }
+          }
+          wave_argmin_dpp(best_cost, best_bin);  // lanes own ascending bins (B <= 256)
+          if (best_cost < __builtin_inf()) {
+            const double g = pterm - best_cost;
+            if (g > bg) {  // features ascend within a wave: strict > keeps the lowest
+              bg = g;
+              bfeat = f;
+              bbin = best_bin;
+            }
+          }
+        }
+        __syncthreads();  // every wave is done with the tile before it is cleared
+      }
+      if (lane == 0) {
+        w_gain[wave] = bg;
+        w_feat[wave] = bfeat;
+        w_bin[wave] = bbin;
+      }
+      __syncthreads();
+      int bf, bb;
+      {
+        double g = w_gain[0];
+        bf = w_feat[0];
+        bb = w_bin[0];
+        for (int w = 1; w < kRegWaves; ++w) {
+          if (w_gain[w] > g || (w_gain[w] == g && w_feat[w] < bf)) {
+            g = w_gain[w];
+            bf = w_feat[w];
+            bb = w_bin[w];
+          }
+        }
+        if (!(g > -__builtin_inf()) || pure) bf = -1;
+      }
+      if (bf >= 0) {
+        // ---- partition rows src -> dst; left targets summed on the way
+        const CodeT* col = codes_fm + (int64_t)bf * n_rows;
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        unsigned long long lsum = 0ull;
+        for (int r0 = 0; r0 < m; r0 += kRegThreads) {
+          const int r = r0 + tid;
+          const bool valid = r < m;
+          const uint32_t ent = valid ? src[start + r] : 0u;
+          const bool go = valid && (uint32_t)col[ent] <= (uint32_t)bb;
+          if (go) lsum += (unsigned long long)y[ent];
+          const unsigned long long bl = __ballot(go);
+          const unsigned long long br = __ballot(valid && !go);
+          int basel = 0, baser = 0;
+          if (lane == 0) {
+            const int nl = __popcll(bl), nr = __popcll(br);
+            basel = nl ? atomicAdd(&s_lc, nl) : 0;
+            baser = nr ? atomicAdd(&s_rc, nr) : 0;
+          }
+          basel = __builtin_amdgcn_readfirstlane(basel);
+          baser = __builtin_amdgcn_readfirstlane(baser);
+          if (valid) {
+            if (go)
+              dst[start + basel + __popcll(bl & lt)] = ent;
+            else
+              dst[start + m - 1 - (baser + __popcll(br & lt))] = ent;
+          }
+        }
+        lsum = (unsigned long long)wave_sum_i64((int64_t)lsum);
+        if (lane == 0) atomicAdd(&s_lsum, lsum);
+      }
+      __syncthreads();
+      if (tid == 0 && bf >= 0) {
+        const int nl = s_lc;
+        const int nr = m - nl;
+        const int64_t sl = (int64_t)s_lsum, sr = S - sl;
+        const int lid = id + 1, rid = id + 2 * nl;
+        int32_t* P = node_i32 + (int64_t)id * 6;
+        P[0] = bf;
+        P[1] = bb;
+        P[2] = lid;
+        P[3] = rid;
+        const int cd = depth + 1;
+        int32_t* L = node_i32 + (int64_t)lid * 6;
+        int32_t* Rr = node_i32 + (int64_t)rid * 6;
+        L[0] = -1; L[1] = -1; L[2] = -1; L[3] = -1; L[4] = cd; L[5] = nl;
+        Rr[0] = -1; Rr[1] = -1; Rr[2] = -1; Rr[3] = -1; Rr[4] = cd; Rr[5] = nr;
+        node_st[(int64_t)lid * 2 + 0] = nl;
+        node_st[(int64_t)lid * 2 + 1] = sl;
+        node_st[(int64_t)rid * 2 + 0] = nr;
+        node_st[(int64_t)rid * 2 + 1] = sr;
+        const bool depth_stop = max_depth >= 0 && cd >= max_depth;
+        const bool tlf = depth_stop || nl < mss || nl < 2 * msl;
+        const bool trf = depth_stop || nr < mss || nr < 2 * msl;
+        const bool left_small = nl <= nr;
+        for (int pass = 0; pass < 2; ++pass) {
+          const bool is_left = (pass == 0) ? !left_small : left_small;
+          if (is_left ? tlf : trf) continue;
+          const int cm = is_left ? nl : nr;
+          const int64_t cstart = is_left ? start : start + nl;
+          if (cm <= tiny_rows) {
+            const int t = atomicAdd(tiny_count, 1);
+            int64_t* tr = tiny + (int64_t)t * 8;
+            tr[0] = cstart;
+            tr[1] = cm;
+            tr[2] = cd;
+            tr[3] = s_buf ^ 1;
+            tr[4] = is_left ? lid : rid;
+            continue;
+          }
+          const int sp = s_sp++;
+          s_st_start[sp] = cstart;
+          s_st_count[sp] = cm;
+          s_st_depth[sp] = cd;
+          s_st_id[sp] = is_left ? lid : rid;
+          s_st_buf[sp] = s_buf ^ 1;
+          s_st_sum[sp] = is_left ? sl : sr;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Tiny regression subtrees (<= 64 rows): presorted lane orders per feature.
+// LDS per wave: codes [64][cw] words, order [F][64] bytes, targets [64] int64.
+__global__ __launch_bounds__(256) void finish_tiny_reg_kernel(
+    const uint32_t* __restrict__ codes_rm, int64_t row_words, const uint32_t* __restrict__ buf0,
+    const uint32_t* __restrict__ buf1, const int64_t* __restrict__ y,
+    const int64_t* __restrict__ tiny, const int32_t* __restrict__ tiny_count,
+    int32_t* __restrict__ tiny_counter, int F, int max_depth, int64_t mss, int64_t msl,
+    int32_t* __restrict__ node_i32, int64_t* __restrict__ node_st, int cw) {
+  extern __shared__ __align__(16) uint32_t dyn[];
+  __shared__ unsigned long long s_mask[kRegTinyWaves][16];
+  __shared__ int32_t s_dep[kRegTinyWaves][16], s_slot[kRegTinyWaves][16];
+  const int lane = lane_id();
+  const int wave = threadIdx.x >> 6;
+  const int per_wave_words = kWave * cw + (F * kWave + 3) / 4 + 2 * kWave;
+  uint32_t* wbase = dyn + wave * per_wave_words;
+  uint32_t* my_codes = wbase + lane * cw;
+  const uint8_t* codes_b = reinterpret_cast<const uint8_t*>(wbase);
+  uint8_t* order = reinterpret_cast<uint8_t*>(wbase + kWave * cw);
+  long long* s_y = reinterpret_cast<long long*>(wbase + kWave * cw + (F * kWave + 3) / 4);
+  const uint8_t* my_bytes = reinterpret_cast<const uint8_t*>(my_codes);
+  const int K = *tiny_count;
+  const int nw = (int)min<int64_t>(row_words, (int64_t)cw);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (;;) {
+    int k = 0;
+    if (lane == 0) k = atomicAdd(tiny_counter, 1);
+    k = __builtin_amdgcn_readfirstlane(k);
+    if (k >= K) break;
+    const int64_t* rec = tiny + (int64_t)k * 8;
+    const int64_t start = rec[0];
+    const int m = (int)rec[1];
+    const int depth0 = (int)rec[2];
+    const uint32_t* src = rec[3] ? buf1 : buf0;
+    const int64_t root_slot = rec[4];
+    const bool act = lane < m;
+    long long yv = 0;
+    if (act) {
+      const uint32_t row = src[start + lane];
+      yv = y[row];
+      for (int i = 0; i < nw; ++i) my_codes[i] = codes_rm[(int64_t)row * row_words + i];
+    }
+    s_y[lane] = yv;
+    const unsigned long long R = m == 64 ? ~0ull : ((1ull << m) - 1ull);
+    for (int f = 0; f < F; ++f) {
+      const uint32_t code = my_bytes[f];
+      unsigned long long eq = R, gt = 0ull;
+#pragma unroll
+      for (int b = 7; b >= 0; --b) {
+        const unsigned long long bm = __ballot((code >> b) & 1u) & R;
+        if ((code >> b) & 1u) {
+          eq &= bm;
+        } else {
+          gt |= eq & bm;
+          eq &= ~bm;
+        }
+      }
+      const unsigned long long lt = R & ~gt & ~eq;
+      if (act) order[f * kWave + __popcll(lt) + __popcll(eq & below)] = (uint8_t)lane;
+    }
+    if (lane == 0) {
+      s_mask[wave][0] = R;
+      s_dep[wave][0] = depth0;
+      s_slot[wave][0] = (int32_t)root_slot;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    int sp = 1;
+    while (sp > 0) {
+      --sp;
+      const unsigned long long M = s_mask[wave][sp];
+      const int d = s_dep[wave][sp];
+      const int64_t slot = s_slot[wave][sp];
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const bool mine = (M >> lane) & 1ull;
+      const int mm = __popcll(M);
+      const int64_t S = wave_sum_i64(mine ? (int64_t)yv : 0);
+      long long mn = mine ? yv : LLONG_MAX, mx = mine ? yv : LLONG_MIN;
+      wave_minmax_i64(mn, mx);
+      if (mn == mx) continue;  // all targets equal: leaf (record written at creation)
+      const double pterm = mse_term(mm, S);
+      double bg = -__builtin_inf(), bc = __builtin_inf();
+      int bf = 0x7fffffff;
+      uint32_t bb = 0xffffffffu;
+      for (int f = 0; f < F; ++f) {
+        const int s = act ? order[f * kWave + lane] : 0;
+        const bool in = act && ((M >> s) & 1ull);
+        const uint32_t code = codes_b[s * cw * 4 + f];
+        const uint32_t ml = wave_incl_scan_dpp(in ? 1u : 0u);
+        const int64_t sl = wave_incl_scan_i64(in ? (int64_t)s_y[s] : 0);
+        const unsigned long long inb = __ballot(in);
+        const unsigned long long after = inb & ~(below | (1ull << lane));
+        const int nxt = after ? __ffsll((long long)after) - 1 : lane;
+        const uint32_t ncode = (uint32_t)__shfl((int)code, nxt, kWave);
+        const bool last = in && (after == 0ull || ncode != code);
+        const int mr = mm - (int)ml;
+        double cost = __builtin_inf();
+        if (last && (int64_t)ml >= msl && (int64_t)mr >= msl)
+          cost = mse_term(ml, sl) + mse_term(mr, S - sl);
+        const double g = pterm - cost;
+        if (g > bg) {
+          bg = g;
+          bf = f;
+          bc = cost;
+          bb = code;
+        }
+      }
+#pragma unroll
+      for (int dd = kWave / 2; dd > 0; dd >>= 1) {
+        const double og = __shfl_xor(bg, dd, kWave);
+        const int of = __shfl_xor(bf, dd, kWave);
+        const double oc = __shfl_xor(bc, dd, kWave);
+        const uint32_t ob = (uint32_t)__shfl_xor((int)bb, dd, kWave);
+        const bool take =
+            og > bg ||
+            (og == bg && (of < bf || (of == bf && (oc < bc || (oc == bc && ob < bb)))));
+        if (take) {
+          bg = og;
+          bf = of;
+          bc = oc;
+          bb = ob;
+        }
+      }
+      bf = __builtin_amdgcn_readfirstlane(bf);
+      bb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bb);
+      if (!(bg > -__builtin_inf()) || bf < 0) continue;
+      const unsigned long long LM = M & __ballot(act && (uint32_t)my_bytes[bf] <= bb);
+      const unsigned long long RM = M & ~LM;
+      const int nl = __popcll(LM), nr = __popcll(RM);
+      const int64_t ls = slot + 1, rs = slot + 2 * nl;
+      const int64_t SL = wave_sum_i64(((LM >> lane) & 1ull) ? (int64_t)yv : 0);
+      const int cd = d + 1;
+      if (lane == 0) {
+        int32_t* P = node_i32 + slot * 6;
+        P[0] = bf;
+        P[1] = (int32_t)bb;
+        P[2] = (int32_t)ls;
+        P[3] = (int32_t)rs;
+        int32_t* L = node_i32 + ls * 6;
+        int32_t* Rr = node_i32 + rs * 6;
+        L[0] = -1; L[1] = -1; L[2] = -1; L[3] = -1; L[4] = cd; L[5] = nl;
+        Rr[0] = -1; Rr[1] = -1; Rr[2] = -1; Rr[3] = -1; Rr[4] = cd; Rr[5] = nr;
+        node_st[ls * 2 + 0] = nl;
+        node_st[ls * 2 + 1] = SL;
+        node_st[rs * 2 + 0] = nr;
+        node_st[rs * 2 + 1] = S - SL;
+      }
+      const bool depth_stop = max_depth >= 0 && cd >= max_depth;
+      const bool tlf = depth_stop || nl < mss || nl < 2 * msl;
+      const bool trf = depth_stop || nr < mss || nr < 2 * msl;
+      const bool left_small = nl <= nr;
+      for (int pass = 0; pass < 2; ++pass) {
+        const bool is_left = (pass == 0) ? !left_small : left_small;
+        if (is_left ? tlf : trf) continue;
+        if (lane == 0) {
+          s_mask[wave][sp] = is_left ? LM : RM;
+          s_dep[wave][sp] = cd;
+          s_slot[wave][sp] = (int32_t)(is_left ? ls : rs);
+        }
+        ++sp;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+int finish_reg_lds_bytes(int B) { return kRegFT * B * 12; }
+
+// counter: int32 [4] = {job cursor, tiny count, tiny cursor, -}, zeroed by the host.
+void launch_finish_reg(hipStream_t stream, const void* codes_rm, int64_t row_words,
+                       const void* codes_fm, int code_bytes, int64_t n_rows, uint32_t* buf0,
+                       uint32_t* buf1, const int64_t* y, const int64_t* jobs, int J,
+                       int32_t* counter, const int32_t* nbins, int F, int B, int max_depth,
+                       int64_t mss, int64_t msl, int32_t* node_i32, int64_t* node_st, int grid,
+                       int tiny_rows, int64_t* tiny, int tiny_grid) {
+  if (J <= 0) return;
+  if (F > kRegMaxF) throw std::runtime_error("regression finisher supports at most 256 features");
+  if (code_bytes != 1) tiny_rows = 0;
+  tiny_rows = std::min(tiny_rows, kRegTinyRows);
+  const size_t lds = (size_t)finish_reg_lds_bytes(B);
+#define MT_FR(CT)                                                                           \
+  MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_reg_kernel<CT>,                      \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));  \
+  hipLaunchKernelGGL(finish_reg_kernel<CT>, dim3(grid), dim3(kRegThreads), lds, stream,     \
+                     (const uint32_t*)codes_rm, row_words, (const CT*)codes_fm, n_rows, buf0, \
+                     buf1, y, jobs, J, counter, nbins, F, B, max_depth, mss, msl, node_i32,  \
+                     node_st, tiny_rows, tiny, counter + 1);
+  if (code_bytes == 1) {
+    MT_FR(uint8_t)
+  } else {
+    MT_FR(uint16_t)
+  }
+#undef MT_FR
+  MT_HIP_CHECK(hipGetLastError());
+  if (tiny_rows > 0) {
+    const int cw = ((F + 3) / 4) | 1;
+    const size_t tl = (size_t)kRegTinyWaves * (kWave * cw + (F * kWave + 3) / 4 + 2 * kWave) * 4;
+    MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_tiny_reg_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl));
+    hipLaunchKernelGGL(finish_tiny_reg_kernel, dim3(tiny_grid), dim3(kRegTinyWaves * kWave), tl,
+                       stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, tiny,
+                       counter + 1, counter + 2, F, max_depth, mss, msl, node_i32, node_st, cw);
+    MT_HIP_CHECK(hipGetLastError());
+  }
+}
+
+}  // namespace mt

@@ -20,6 +20,8 @@
 // host-known upper bounds), so the host enqueues levels back to back with no
 // synchronisation and learns only at the end -- from one lagged 32-byte read
 // -- that the frontier is empty.
+#include <climits>
+
 #include "common.h"
 #include "criterion.h"
 
@@ -30,18 +32,22 @@ constexpr int kPlanWaves = kPlanThreads / kWave;
 
 // Level work lists (one set per level parity). ctl: int32
 // {0: K frontier nodes, 1: built nodes, 2: hist items, 3: slab reductions,
-//  4: derive triples, 5: split nodes, 6: partition items, 7: reduction tasks}
+//  4: derive triples, 5: split nodes, 6: partition items, 7: reduction tasks,
+//  8: min/max items (regression), 9-15: -}
 struct LevelLists {
   int64_t* pos;     // [KMAX] pre-order position of each frontier slot
   int64_t* start;   // [KMAX] row segment start
   int32_t* cnt;     // [KMAX] rows
   int32_t* depth;   // [KMAX]
-  int32_t* stats;   // [KMAX][C] class counts
+  int32_t* stats;   // [KMAX][C] class counts (classification)
   int64_t* items;   // [IMAX][4] {slot, start, count, dest slab or -1}
   int64_t* red;     // [KMAX][3] {slot, first slab, slabs}
   int64_t* der;     // [KMAX][3] {slot, parent slot (previous level), sibling slot}
   int64_t* tasks;   // [TMAX][3] {slot, first slab, <= 16 slabs} slab-reduction tasks
-  int32_t* ctl;     // [8]
+  int32_t* ctl;     // [16]
+  int64_t* stats64; // [KMAX][2] {count, fixed-point target sum} (regression)
+  int64_t* minmax;  // [KMAX][2] target min / max of the slot's rows (regression)
+  int64_t* mitems;  // [MMAX][3] {slot, start, count} min/max work items (regression)
 };
 
 struct PlanArgs {
@@ -52,7 +58,9 @@ struct PlanArgs {
   int32_t* cursors;    // [KMAX][2]
   int32_t* pctl;       // [2] {split nodes, partition items} (aliases cur.ctl + 5)
   int32_t* pos_rec;    // [P][6]
-  int32_t* pos_st;     // [P][C]
+  int32_t* pos_st;     // [P][C] class counts (classification)
+  int64_t* pos_st64;   // [P][2] {count, sum} (regression)
+  int reg;
   int64_t* jobs;       // [JMAX][5 + C] finisher jobs
   int32_t* job_count;
   int C, max_depth, n_cu;
@@ -84,13 +92,33 @@ struct Decision {
   int built;    // child index built from rows (-1 none), the other alive one is derived
 };
 
+__device__ __forceinline__ int plan_rec_width(const PlanArgs& a) {
+  return a.reg ? 7 : 5 + 2 * a.C;
+}
+
+// Statistic k of child c (0 left, 1 right) of frontier node i: class counts,
+// or {count, fixed-point sum} for regression (the record's left sum at r[5]).
+__device__ __forceinline__ int64_t plan_child_stat(const PlanArgs& a, int i, const int64_t* r,
+                                                   const int64_t nl, int c, int k) {
+  if (a.reg) {
+    const int64_t* st = a.cur.stats64 + (int64_t)i * 2;
+    if (k == 0) return c == 0 ? nl : st[0] - nl;
+    return c == 0 ? r[5] : st[1] - r[5];
+  }
+  const int64_t lc = r[5 + k];
+  return c == 0 ? lc : (int64_t)a.cur.stats[(int64_t)i * a.C + k] - lc;
+}
+
 __device__ Decision plan_decide(const PlanArgs& a, int i) {
   const int C = a.C;
-  const int R = 5 + 2 * C;
+  const int R = plan_rec_width(a);
   const int64_t* r = a.rec + (int64_t)i * R;
   Decision d;
   const double gain = __longlong_as_double((long long)r[0]);
   d.split = gain > -__builtin_inf();
+  // regression: a node whose targets are all equal is a leaf (purity is only
+  // known once its rows are partitioned, so it is checked one level later)
+  if (a.reg && a.cur.minmax[(int64_t)i * 2] == a.cur.minmax[(int64_t)i * 2 + 1]) d.split = false;
   d.feature = (int)r[1];
   d.bin = (int)r[2];
   const int64_t m = a.cur.cnt[i];
@@ -103,11 +131,10 @@ __device__ Decision plan_decide(const PlanArgs& a, int i) {
   const bool depth_stop = a.max_depth >= 0 && cd >= a.max_depth;
   for (int c = 0; c < 2; ++c) {
     const int64_t cm = c == 0 ? d.nl : d.nr;
-    int nz = 0;
-    for (int k = 0; k < C; ++k) {
-      const int64_t lc = r[5 + k];
-      const int64_t v = c == 0 ? lc : (int64_t)a.cur.stats[(int64_t)i * C + k] - lc;
-      nz += v > 0;
+    int nz = 2;  // regression: purity is checked when the child is scanned
+    if (!a.reg) {
+      nz = 0;
+      for (int k = 0; k < C; ++k) nz += plan_child_stat(a, i, r, d.nl, c, k) > 0;
     }
     const bool term = depth_stop || cm < a.mss || cm < 2 * a.msl || nz <= 1;
     d.fate[c] = term ? 0 : ((a.fr > 0 && cm <= a.fr) ? 1 : 2);
@@ -173,10 +200,14 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
       const int64_t start = a.cur.start[i];
       const int64_t m = a.cur.cnt[i];
       const int depth = a.cur.depth[i];
-      const int32_t* st = a.cur.stats + (int64_t)i * C;
       int32_t* P = a.pos_rec + pos * 6;
-      const int64_t* r = a.rec + (int64_t)i * (5 + 2 * C);
-      for (int k = 0; k < C; ++k) a.pos_st[pos * C + k] = st[k];
+      const int64_t* r = a.rec + (int64_t)i * plan_rec_width(a);
+      if (a.reg) {
+        a.pos_st64[pos * 2 + 0] = a.cur.stats64[(int64_t)i * 2 + 0];
+        a.pos_st64[pos * 2 + 1] = a.cur.stats64[(int64_t)i * 2 + 1];
+      } else {
+        for (int k = 0; k < C; ++k) a.pos_st[pos * C + k] = a.cur.stats[(int64_t)i * C + k];
+      }
       P[4] = depth;
       P[5] = (int32_t)m;
       if (!d.split) {
@@ -215,9 +246,12 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
             Q[3] = -1;
             Q[4] = cd;
             Q[5] = (int32_t)cm;
-            for (int k = 0; k < C; ++k) {
-              const int64_t lc = r[5 + k];
-              a.pos_st[cpos[c] * C + k] = (int32_t)(c == 0 ? lc : st[k] - lc);
+            if (a.reg) {
+              a.pos_st64[cpos[c] * 2 + 0] = plan_child_stat(a, i, r, d.nl, c, 0);
+              a.pos_st64[cpos[c] * 2 + 1] = plan_child_stat(a, i, r, d.nl, c, 1);
+            } else {
+              for (int k = 0; k < C; ++k)
+                a.pos_st[cpos[c] * C + k] = (int32_t)plan_child_stat(a, i, r, d.nl, c, k);
             }
           } else if (d.fate[c] == 1) {  // finisher job
             const int j = atomicAdd(a.job_count, 1);
@@ -227,19 +261,21 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
             J[2] = cd;
             J[3] = cpos[c];
             J[4] = 0;
-            for (int k = 0; k < C; ++k) {
-              const int64_t lc = r[5 + k];
-              J[5 + k] = c == 0 ? lc : st[k] - lc;
-            }
+            for (int k = 0; k < C; ++k) J[5 + k] = plan_child_stat(a, i, r, d.nl, c, k);
           } else {  // next frontier
             const int sl = slot[c];
             a.nxt.pos[sl] = cpos[c];
             a.nxt.start[sl] = cs;
             a.nxt.cnt[sl] = (int32_t)cm;
             a.nxt.depth[sl] = cd;
-            for (int k = 0; k < C; ++k) {
-              const int64_t lc = r[5 + k];
-              a.nxt.stats[(int64_t)sl * C + k] = (int32_t)(c == 0 ? lc : st[k] - lc);
+            if (a.reg) {
+              a.nxt.stats64[(int64_t)sl * 2 + 0] = plan_child_stat(a, i, r, d.nl, c, 0);
+              a.nxt.stats64[(int64_t)sl * 2 + 1] = plan_child_stat(a, i, r, d.nl, c, 1);
+              a.nxt.minmax[(int64_t)sl * 2 + 0] = LLONG_MAX;
+              a.nxt.minmax[(int64_t)sl * 2 + 1] = LLONG_MIN;
+            } else {
+              for (int k = 0; k < C; ++k)
+                a.nxt.stats[(int64_t)sl * C + k] = (int32_t)plan_child_stat(a, i, r, d.nl, c, k);
             }
             if (c == d.built) {
               built_rows += cm;
@@ -361,7 +397,39 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     if (tid == 0) s_carry[3] += tp;
     __syncthreads();
   }
+  // ---- pass 5 (regression): min/max work items over every next-frontier slot
+  int n_mitems = 0;
+  if (a.reg) {
+    __syncthreads();
+    if (tid == 0) s_carry[0] = 0;
+    __syncthreads();
+    for (int b0 = 0; b0 < K2; b0 += kPlanThreads) {
+      const int sl = b0 + tid;
+      int64_t cnt = 0, kk = 0;
+      if (sl < K2) {
+        cnt = a.nxt.cnt[sl];
+        kk = (cnt + 4095) / 4096;
+        if (kk < 1) kk = 1;
+      }
+      int tm;
+      const int om = plan_scan_excl((int)kk, s_w, tm) + s_carry[0];
+      if (sl < K2) {
+        const int64_t st0 = a.nxt.start[sl];
+        for (int64_t c = 0; c < kk; ++c) {
+          int64_t* it = a.nxt.mitems + (int64_t)(om + c) * 3;
+          it[0] = sl;
+          it[1] = st0 + c * 4096;
+          it[2] = (cnt - c * 4096) < 4096 ? (cnt - c * 4096) : 4096;
+        }
+      }
+      __syncthreads();
+      if (tid == 0) s_carry[0] += tm;
+      __syncthreads();
+    }
+    n_mitems = s_carry[0];
+  }
   if (tid == 0) {
+    a.nxt.ctl[8] = n_mitems;
     a.nxt.ctl[0] = K2;
     a.nxt.ctl[1] = NB;
     a.nxt.ctl[2] = n_items;

@@ -145,7 +145,8 @@ __global__ __launch_bounds__(kHistThreads) void hist_reg_lds_kernel(
     const CodeT* __restrict__ codes, int64_t row_words, const uint32_t* __restrict__ idx,
     const int64_t* __restrict__ y, const int64_t* __restrict__ items,
     int64_t* __restrict__ hist, int64_t* __restrict__ slab, int F_h, int f_lo, int B, int ft,
-    int lane_shift) {
+    int lane_shift, const int32_t* __restrict__ dcount) {
+  if (dcount && (int)blockIdx.x >= *dcount) return;
   extern __shared__ uint32_t lds[];
   constexpr int cpw = 4 / sizeof(CodeT);
   const int t0 = blockIdx.y * ft;
@@ -298,7 +299,9 @@ __global__ __launch_bounds__(256) void hist_reduce_cls_kernel(
 __global__ __launch_bounds__(256) void hist_reduce_reg_kernel(const int64_t* __restrict__ red,
                                                               const int64_t* __restrict__ slab,
                                                               int64_t* __restrict__ hist,
-                                                              int64_t E) {
+                                                              int64_t E,
+                                                              const int32_t* __restrict__ dcount) {
+  if (dcount && (int)blockIdx.y >= *dcount) return;
   const int64_t slot = red[blockIdx.y * 3 + 0];
   const int64_t first = red[blockIdx.y * 3 + 1];
   const int64_t k = red[blockIdx.y * 3 + 2];
@@ -430,7 +433,7 @@ void launch_hist(hipStream_t stream, const void* codes, int code_bytes, int64_t 
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));    \
   hipLaunchKernelGGL(hist_reg_lds_kernel<CT>, grid, dim3(kHistThreads), lds, stream,          \
                      (const CT*)codes, row_words, idx, (const int64_t*)y, items,              \
-                     (int64_t*)hist, (int64_t*)slab, F_h, f_lo, B, ft, shift);
+                     (int64_t*)hist, (int64_t*)slab, F_h, f_lo, B, ft, shift, dcount);
     if (code_bytes == 1) {
       MT_REG(uint8_t)
     } else {
@@ -483,7 +486,7 @@ void launch_hist_reduce(hipStream_t stream, const int64_t* red, int n_red, int m
     const int64_t E = (int64_t)F_h * B * 2;
     int gx = (int)std::min<int64_t>((E + 255) / 256, 1024);
     hipLaunchKernelGGL(hist_reduce_reg_kernel, dim3(gx, n_red), dim3(256), 0, stream, red,
-                       (const int64_t*)slab, (int64_t*)hist, E);
+                       (const int64_t*)slab, (int64_t*)hist, E, dcount);
     MT_HIP_CHECK(hipGetLastError());
     return;
   }

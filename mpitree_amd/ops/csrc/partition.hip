@@ -15,6 +15,8 @@
 // harmless: every statistic downstream is an integer (or fixed-point) sum.
 // Permutation entries may carry the class label in their top bits
 // (``row | label << shift``, see hist.hip); ``mask`` extracts the row.
+#include <climits>
+
 #include "common.h"
 
 namespace mt {
@@ -188,6 +190,43 @@ __global__ __launch_bounds__(256) void init_idx_kernel(uint32_t* __restrict__ id
                                                        int lab_shift, int64_t n) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < n) idx[i] = lab_shift ? ((uint32_t)i | ((uint32_t)y[i] << lab_shift)) : (uint32_t)i;
+}
+
+// Regression purity: per frontier slot min / max of the fixed-point targets
+// over its rows. items: int64 [n][3] {slot, start, count}; out: int64 [slot][2]
+// initialised to {INT64_MAX, INT64_MIN} by the planner.
+__global__ __launch_bounds__(256) void seg_minmax_kernel(const uint32_t* __restrict__ idx,
+                                                         const int64_t* __restrict__ y,
+                                                         const int64_t* __restrict__ items,
+                                                         int64_t* __restrict__ out,
+                                                         const int32_t* __restrict__ dcount) {
+  if (dcount && (int)blockIdx.x >= *dcount) return;
+  const int64_t s = items[blockIdx.x * 3 + 0];
+  const int64_t c0 = items[blockIdx.x * 3 + 1];
+  const int64_t cn = items[blockIdx.x * 3 + 2];
+  long long mn = LLONG_MAX, mx = LLONG_MIN;
+  for (int64_t e = threadIdx.x; e < cn; e += blockDim.x) {
+    const long long v = y[idx[c0 + e]];
+    mn = v < mn ? v : mn;
+    mx = v > mx ? v : mx;
+  }
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    const long long a = __shfl_xor(mn, d, kWave), b = __shfl_xor(mx, d, kWave);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if (lane_id() == 0) {
+    atomicMin(reinterpret_cast<long long*>(out + s * 2), mn);
+    atomicMax(reinterpret_cast<long long*>(out + s * 2 + 1), mx);
+  }
+}
+
+void launch_seg_minmax(hipStream_t stream, const uint32_t* idx, const int64_t* y,
+                       const int64_t* items, int n_items, int64_t* out, const int32_t* dcount) {
+  if (n_items <= 0) return;
+  hipLaunchKernelGGL(seg_minmax_kernel, dim3(n_items), dim3(256), 0, stream, idx, y, items, out,
+                     dcount);
+  MT_HIP_CHECK(hipGetLastError());
 }
 
 void launch_partition(hipStream_t stream, const void* codes_fm, int code_bytes, int64_t n_rows,

@@ -142,7 +142,9 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
 __global__ __launch_bounds__(256) void scan_reg_kernel(
     const int64_t* __restrict__ hist, const int64_t* __restrict__ nodes,
     const int32_t* __restrict__ nbins, int F_h, int f_lo, int B, int msl,
-    double* __restrict__ out_cost, int32_t* __restrict__ out_bin) {
+    double* __restrict__ out_cost, int32_t* __restrict__ out_bin,
+    const int32_t* __restrict__ dcount) {
+  if (dcount && (int)blockIdx.x >= *dcount) return;
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
   const int f = blockIdx.y * 4 + wave;
@@ -370,7 +372,7 @@ void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int
   dim3 grid(k, (F_h + 3) / 4);
   if (crit == kSquaredError) {
     hipLaunchKernelGGL(scan_reg_kernel, grid, dim3(256), 0, stream, (const int64_t*)hist, nodes,
-                       nbins, F_h, f_lo, B, msl, cost, bins);
+                       nbins, F_h, f_lo, B, msl, cost, bins, dcount);
   } else {
     size_t lds = (size_t)4 * 2 * C * sizeof(uint32_t);
     MT_HIP_CHECK(hipFuncSetAttribute((const void*)scan_cls_kernel,

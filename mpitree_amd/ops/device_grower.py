@@ -43,8 +43,6 @@ __all__ = ["DeviceGrower", "device_loop_supported"]
 def device_loop_supported(be, params, comm) -> bool:
     if os.environ.get("MPITREE_DEVICE_LOOP", "1") == "0":
         return False
-    if be.reg:
-        return False
     if getattr(comm, "world_size", 1) != 1:
         # replicated rows: every rank runs the (cheap) level loop, the finisher
         # jobs are split across ranks and the finished nodes all-gathered
@@ -55,7 +53,7 @@ def device_loop_supported(be, params, comm) -> bool:
     if params.finisher_rows <= 0 or not be.finisher_supported():
         return False
     # the planner drives the LDS histogram path only
-    return be.hip.hist_feature_tile(be.F, be.B, be.C, False, hb.LDS_BUDGET) > 0
+    return be.hip.hist_feature_tile(be.F, be.B, be.C, bool(be.reg), hb.LDS_BUDGET) > 0
 
 
 class DeviceGrower:
@@ -67,15 +65,19 @@ class DeviceGrower:
         self.stats: dict = {}
 
     # ------------------------------------------------------------ buffers
-    def _lists(self, KMAX, IMAX, TMAX, C, dev):
+    def _lists(self, KMAX, IMAX, TMAX, MMAX, C, reg, dev):
         i64 = dict(dtype=torch.int64, device=dev)
         i32 = dict(dtype=torch.int32, device=dev)
+        k_reg = KMAX if reg else 1
         return dict(
             pos=torch.empty(KMAX, **i64), start=torch.empty(KMAX, **i64),
             cnt=torch.empty(KMAX, **i32), depth=torch.empty(KMAX, **i32),
-            stats=torch.empty((KMAX, C), **i32), items=torch.empty((IMAX, 4), **i64),
+            stats=torch.empty((1 if reg else KMAX, C), **i32),
+            items=torch.empty((IMAX, 4), **i64),
             red=torch.empty((KMAX, 3), **i64), der=torch.empty((KMAX, 3), **i64),
-            tasks=torch.empty((TMAX, 3), **i64), ctl=torch.zeros(8, **i32),
+            tasks=torch.empty((TMAX, 3), **i64), ctl=torch.zeros(16, **i32),
+            stats64=torch.empty((k_reg, 2), **i64), minmax=torch.empty((k_reg, 2), **i64),
+            mitems=torch.empty((MMAX if reg else 1, 3), **i64),
         )
 
     def _run_jobs(self, d_jobs, n: int):
@@ -98,12 +100,13 @@ class DeviceGrower:
         scatter into the local position space. Level nodes are written by all
         ranks identically, so their duplicates are harmless."""
         be, comm = self.be, self.comm
+        dt = torch.int64 if be.reg else torch.int32  # regression sums need 64 bits
         live = torch.nonzero(be.pos_rec[:, 5] > 0).squeeze(1)
-        rows = torch.cat([live.to(torch.int32)[:, None], be.pos_rec[live],
-                          be.pos_st[live].to(torch.int32)], 1)
+        rows = torch.cat([live.to(dt)[:, None], be.pos_rec[live].to(dt),
+                          be.pos_st[live].to(dt)], 1)
         allr = comm.all_gather_rows(rows)
         pos = allr[:, 0].long()
-        be.pos_rec.index_copy_(0, pos, allr[:, 1:7].contiguous())
+        be.pos_rec.index_copy_(0, pos, allr[:, 1:7].to(torch.int32).contiguous())
         be.pos_st.index_copy_(0, pos, allr[:, 7:].to(be.pos_st.dtype).contiguous())
 
     def _level_profile(self, marks):
@@ -127,16 +130,22 @@ class DeviceGrower:
         be, p = self.be, self.p
         hip = be.hip
         dev = be.device
-        C, F, B = n_classes, n_features, be.B
+        reg = bool(be.reg)
+        C, F, B = (2 if reg else n_classes), n_features, be.B
         fr = int(p.finisher_rows)
         md = -1 if p.max_depth is None else int(p.max_depth)
         mss, msl = int(p.min_samples_split), int(max(1, p.min_samples_leaf))
         s = hb._stream
         t0 = time.perf_counter()
-        root = be.segment_stats(np.array([0]), np.array([n]))[0]  # one small sync
+        root_full = be.segment_stats(np.array([0]), np.array([n]))[0]  # one small sync
         be.begin_positions(2 * n - 1)
-        nz = int((root > 0).sum())
-        root_term = (md == 0) or n < mss or n < 2 * msl or nz <= 1
+        if reg:  # {count, sum, min, max}: a root with equal targets is a leaf
+            root = root_full[:2]
+            pure = root_full[2] == root_full[3]
+        else:
+            root = root_full
+            pure = int((root > 0).sum()) <= 1
+        root_term = (md == 0) or n < mss or n < 2 * msl or pure
         jobs_host = None
         if root_term:
             be.put_positions([0], [-1], [-1], [-1], [-1], [0], [n], root[None, :])
@@ -151,16 +160,18 @@ class DeviceGrower:
             IMAX = KMAX + n // 1024 + 2 * hb.N_CU + 16
             PMAX = KMAX + n // 1024 + 16
             JMAX = n // 2 + 2
-            R = 5 + 2 * C
+            R = 7 if reg else 5 + 2 * C
             # multi-item nodes hold > max(1024, level rows / 512) rows each
             RMAX = int(min(KMAX, max(2 * hb.N_CU + 1, n // 1024 + 1)))
             TMAX = RMAX + IMAX // 16 + 16
-            sets = [self._lists(KMAX, IMAX, TMAX, C, dev), self._lists(KMAX, IMAX, TMAX, C, dev)]
+            MMAX = KMAX + n // 4096 + 16
+            sets = [self._lists(KMAX, IMAX, TMAX, MMAX, C, reg, dev) for _ in range(2)]
             ptrs = [self._ptrs(x) for x in sets]
             E = F * B * C
-            hists = [torch.empty((KMAX, F, B, C), dtype=torch.int32, device=dev) for _ in range(2)]
-            sw = hip.hist_slab_words(F, B, C, False)
-            slab = torch.empty((IMAX, sw), dtype=torch.int32, device=dev)
+            hdt = torch.int64 if reg else torch.int32
+            hists = [torch.empty((KMAX, F, B, C), dtype=hdt, device=dev) for _ in range(2)]
+            sw = hip.hist_slab_words(F, B, C, reg)
+            slab = torch.empty((IMAX, sw), dtype=hdt, device=dev)
             rec = torch.empty((KMAX, R), dtype=torch.int64, device=dev)
             cost = torch.empty((KMAX, F), dtype=torch.float64, device=dev)
             bins = torch.empty((KMAX, F), dtype=torch.int32, device=dev)
@@ -181,7 +192,12 @@ class DeviceGrower:
             a["start"][:1].zero_()
             a["cnt"][:1].fill_(n)
             a["depth"][:1].zero_()
-            a["stats"][:1].copy_(torch.from_numpy(root.astype(np.int32)).to(dev))
+            if reg:
+                a["stats64"][:1].copy_(torch.from_numpy(root.astype(np.int64)[None, :]).to(dev))
+                a["minmax"][:1].copy_(torch.from_numpy(root_full[2:4].astype(np.int64)[None, :])
+                                      .to(dev))
+            else:
+                a["stats"][:1].copy_(torch.from_numpy(root.astype(np.int32)).to(dev))
             a["items"][:k].copy_(torch.from_numpy(items).to(dev))
             nt = -(-k // 16) if k > 1 else 0
             if k > 1:
@@ -189,9 +205,9 @@ class DeviceGrower:
                 t0s = np.arange(nt, dtype=np.int64) * 16
                 a["tasks"][:nt].copy_(torch.from_numpy(
                     np.stack([np.zeros(nt, np.int64), t0s, np.minimum(16, k - t0s)], 1)).to(dev))
-            a["ctl"].copy_(torch.tensor([1, 1, k, 1 if k > 1 else 0, 0, 0, 0, nt],
+            a["ctl"].copy_(torch.tensor([1, 1, k, 1 if k > 1 else 0, 0, 0, 0, nt] + [0] * 8,
                                         dtype=torch.int32, device=dev))
-            pinned = torch.zeros((64, 9), dtype=torch.int32, pin_memory=True)
+            pinned = torch.zeros((64, 17), dtype=torch.int32, pin_memory=True)
             events = []
             cb, rs = be.cb, be.row_elems * be.cb
             lvl = 0
@@ -216,14 +232,18 @@ class DeviceGrower:
                 ctl = cur["ctl"]
                 hip.hist(s(), be.codes_rm.data_ptr(), cb, rs, be.idx.data_ptr(), be.y.data_ptr(),
                          be.lab_shift, cur["items"], ib, H.data_ptr(), slab.data_ptr(), F, 0, B, C,
-                         False, hb.LDS_BUDGET, dcount=ctl + 4 * 2)
+                         reg, hb.LDS_BUDGET, dcount=ctl + 4 * 2)
                 rb = int(min(kb, RMAX))
-                hip.hist_reduce_tasks(s(), cur["red"], rb, cur["tasks"],
-                                      int(min(TMAX, rb + ib // 16 + 1)), slab.data_ptr(),
-                                      H.data_ptr(), F, B, C, ctl + 4 * 3, ctl + 4 * 7)
+                if reg:  # slabs summed straight into the slot
+                    hip.hist_reduce(s(), cur["red"], rb, 1, slab.data_ptr(), H.data_ptr(), F, B, C,
+                                    True, dcount=ctl + 4 * 3)
+                else:
+                    hip.hist_reduce_tasks(s(), cur["red"], rb, cur["tasks"],
+                                          int(min(TMAX, rb + ib // 16 + 1)), slab.data_ptr(),
+                                          H.data_ptr(), F, B, C, ctl + 4 * 3, ctl + 4 * 7)
                 mark()
                 if lvl > 0:
-                    hip.hist_derive(s(), cur["der"], kb, Hp.data_ptr(), H.data_ptr(), E, False,
+                    hip.hist_derive(s(), cur["der"], kb, Hp.data_ptr(), H.data_ptr(), E, reg,
                                     dcount=ctl + 4 * 4)
                 hip.scan(s(), H.data_ptr(), ident.data_ptr(), kb, be.nbins.data_ptr(), F, 0, B, C,
                          int(be.crit), msl, cost.data_ptr(), bins.data_ptr(), rec.data_ptr(),
@@ -231,18 +251,23 @@ class DeviceGrower:
                 mark()
                 hip.grow_plan(s(), cur, nxt, rec.data_ptr(), split.data_ptr(), pitems.data_ptr(),
                               cursors.data_ptr(), ctl + 4 * 5, be.pos_rec.data_ptr(),
-                              be.pos_st.data_ptr(), jobs.data_ptr(), job_count.data_ptr(), C, md,
-                              hb.N_CU, mss, msl, fr)
+                              0 if reg else be.pos_st.data_ptr(),
+                              be.pos_st.data_ptr() if reg else 0, int(reg), jobs.data_ptr(),
+                              job_count.data_ptr(), C, md, hb.N_CU, mss, msl, fr)
                 mark()
                 pb = int(min(PMAX, n // 1024 + kb + 1))
                 hip.partition(s(), be.codes_fm.data_ptr(), cb, be.n, be.idx.data_ptr(),
                               be.tmp.data_ptr(), be.row_mask, pitems.data_ptr(), pb,
                               split.data_ptr(), cursors.data_ptr(), dcount=ctl + 4 * 6)
+                if reg:  # purity of the next frontier, read by the next planner
+                    hip.seg_minmax(s(), be.idx.data_ptr(), be.y.data_ptr(), nxt["mitems"],
+                                   int(min(MMAX, 2 * kb + n // 4096 + 1)), nxt["minmax"],
+                                   nxt["ctl"] + 4 * 8)
                 mark()
                 # lagged completion check: next level's frontier size + job count
                 slot = lvl % 64
-                pinned[slot, :8].copy_(sets[(lvl + 1) % 2]["ctl"], non_blocking=True)
-                pinned[slot, 8:9].copy_(job_count, non_blocking=True)
+                pinned[slot, :16].copy_(sets[(lvl + 1) % 2]["ctl"], non_blocking=True)
+                pinned[slot, 16:17].copy_(job_count, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record()
                 events.append(ev)
@@ -256,7 +281,7 @@ class DeviceGrower:
                 if lvl > 4096:
                     raise RuntimeError("device level loop did not terminate")
             levels = done_at + 1
-            J = int(pinned[done_at % 64, 8])
+            J = int(pinned[done_at % 64, 16])
             if prof:
                 self._level_profile(marks[:levels])
             self._keep = (sets, hists, slab, rec, cost, bins, split, pitems, cursors)
@@ -281,8 +306,11 @@ class DeviceGrower:
         ta = TreeArrays(
             feature=a["feature"], threshold=a["threshold"], threshold_bin=a["bin"],
             left=a["left"], right=a["right"], depth=a["depth"], n_samples=a["nsamp"],
-            impurity=a["impurity"], count=st, value=None,
+            impurity=a["impurity"], count=None if reg else st,
+            value=a["value"] if reg else None,
         )
         ta.meta["term"] = a["term"]
+        if reg:
+            ta.meta["sum_fixed"] = st[:, 1]
         ta.meta["final"] = True
         return ta

@@ -357,9 +357,13 @@ class HipBackend:
 
     # -------------------------------------------------------------- finisher
     def finisher_supported(self) -> bool:
-        if self.reg or self.cb != 1 or self.C > 16 or self.B > 256:
+        if self.B > 256 or self.F > 256:
             return False
-        return self.hip.finish_lds_bytes(self.F, self.B, self.C) <= 150 * 1024 and self.F <= 256
+        if self.reg:  # feature-tiled LDS histograms: any F
+            return True
+        if self.cb != 1 or self.C > 16:
+            return False
+        return self.hip.finish_lds_bytes(self.F, self.B, self.C) <= 150 * 1024
 
     # finisher jobs index the x*log2(x) table with row counts: keep them below it
     max_finisher_rows = XTAB_N - 1
@@ -439,6 +443,9 @@ class HipBackend:
             return
         C = self.C
         counter = torch.zeros(4, dtype=torch.int32, device=self.device)
+        if self.reg:
+            self._launch_finisher_reg(d_jobs, J, job_rows, params, rec, cnt, counter)
+            return
         job_root = torch.empty(J, dtype=torch.int32, device=self.device)
         tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
         # every tiny subtree has >= 2 rows and they partition the job rows
@@ -462,6 +469,20 @@ class HipBackend:
         self._fin_keep = (counter, job_root, tiny, d_jobs)
         if prof is not None:
             self.last_finisher_prof = prof.cpu().numpy()
+
+    def _launch_finisher_reg(self, d_jobs, J, job_rows, params, rec, st64, counter):
+        tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
+        tiny = torch.empty((int(job_rows // 2 + J + 1), 8), dtype=torch.int64, device=self.device)
+        md = -1 if params.max_depth is None else int(params.max_depth)
+        grid = int(min(J, int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU))))
+        self.hip.finish_reg(_stream(), self.codes_rm.data_ptr(), self.row_elems * self.cb // 4,
+                            self.codes_fm.data_ptr(), self.cb, self.n, self.idx.data_ptr(),
+                            self.tmp.data_ptr(), self.y.data_ptr(), d_jobs.data_ptr(), J,
+                            counter.data_ptr(), self.nbins.data_ptr(), self.F, self.B, md,
+                            int(params.min_samples_split), int(max(1, params.min_samples_leaf)),
+                            rec.data_ptr(), st64.data_ptr(), grid, tiny_rows, tiny.data_ptr(),
+                            4 * N_CU)
+        self._fin_keep = (counter, tiny, d_jobs)
 
     def finish_subtrees(self, starts, counts, depths, params, stats=None, positions=None,
                         overlap=False):
@@ -503,7 +524,8 @@ class HipBackend:
         if table_mode:
             positions = np.cumsum(span) - span
             rec = torch.zeros((max(int(span.sum()), 1), 6), dtype=torch.int32, device=self.device)
-            cnt = torch.empty((rec.shape[0], C), dtype=torch.int32, device=self.device)
+            cnt = torch.empty((rec.shape[0], C), device=self.device,
+                              dtype=torch.int64 if self.reg else torch.int32)
         else:
             rec, cnt = self.pos_rec, self.pos_st
         positions = np.asarray(positions, np.int64)

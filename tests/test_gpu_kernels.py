@@ -224,3 +224,28 @@ def test_gpu_profile_mode_level_events(monkeypatch):
     prof = st["level_profile"]
     assert len(prof) == st["levels"] and all(v >= 0 for row in prof for v in row.values())
     assert st["timings"]["device_hist"] > 0
+
+
+@pytest.mark.parametrize("seed", range(3))
+@pytest.mark.parametrize("max_depth", [None, 9])
+def test_gpu_regression_device_loop_matches_host(monkeypatch, seed, max_depth):
+    """Regression: device loop + regression finisher == host loop == numpy oracle."""
+    from mpitree_amd.core.fit import fit_tree
+
+    rng = np.random.default_rng(300 + seed)
+    n, F = 20000 + 5000 * seed, 7
+    X = rng.integers(0, 40, size=(n, F)).astype(np.float32)
+    # repeated target values so that pure (all-equal) nodes occur
+    y = np.round(X[:, 0] * 0.5 + X[:, 1] * (seed + 1) + rng.integers(0, 5, size=n), 1)
+    kw = dict(regression=True, criterion=2, max_depth=max_depth, min_samples_split=2,
+              device="cuda", finisher_rows=400)
+    monkeypatch.setenv("MPITREE_DEVICE_LOOP", "1")
+    r1 = fit_tree(X, y, **kw)
+    assert r1.engine == "hip-device-loop"
+    monkeypatch.setenv("MPITREE_DEVICE_LOOP", "0")
+    r2 = fit_tree(X, y, **kw)
+    assert r2.engine == "hip-levelwise"
+    assert r1.arrays.equal(r2.arrays)
+    assert np.array_equal(r1.arrays.value, r2.arrays.value)
+    r3 = fit_tree(X, y, **{**kw, "device": "cpu"})
+    assert r1.arrays.equal(r3.arrays)
