@@ -26,7 +26,7 @@ void launch_scan(hipStream_t, const void*, const int64_t*, int, const int32_t*, 
                  int, int, int, double*, int32_t*, int64_t*, const double*, int,
                  const int32_t*);
 void launch_partition(hipStream_t, const void*, int, int64_t, uint32_t*, uint32_t*, uint32_t,
-                      const int64_t*, int, const int64_t*, int32_t*, const int32_t*);
+                      const int64_t*, int, const int64_t*, int32_t*, const int32_t*, bool);
 void launch_seg_stats(hipStream_t, const uint32_t*, const void*, int, bool, const int64_t*, int,
                       void*, int);
 void launch_init_idx(hipStream_t, uint32_t*, const int32_t*, int, int64_t);
@@ -81,12 +81,14 @@ struct PlanArgs {
   int32_t* pos_st;
   int64_t* pos_st64;
   int reg;
+  int out_buf;
   int64_t* jobs;
   int32_t* job_count;
   int C, max_depth, n_cu;
   int64_t mss, msl, fr;
 };
 void launch_grow_plan(hipStream_t, const PlanArgs&);
+void launch_grow_init(hipStream_t, const LevelLists&, int64_t, int64_t, int, int, const int64_t*);
 int finish_reg_lds_bytes(int B);
 void launch_finish_reg(hipStream_t, const void*, int64_t, const void*, int, int64_t, uint32_t*,
                        uint32_t*, const int64_t*, const int64_t*, int, int32_t*, const int32_t*,
@@ -150,13 +152,13 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("dcount") = 0);
   m.def("partition", [](uintptr_t s, uintptr_t codes_fm, int cb, int64_t n_rows, uintptr_t idx,
                         uintptr_t tmp, uint32_t mask, uintptr_t items, int n_items,
-                        uintptr_t split, uintptr_t cursors, uintptr_t dcount) {
+                        uintptr_t split, uintptr_t cursors, uintptr_t dcount, bool copy_back) {
     mt::launch_partition(S(s), P<void>(codes_fm), cb, n_rows, P<uint32_t>(idx),
                          P<uint32_t>(tmp), mask, P<int64_t>(items), n_items, P<int64_t>(split),
-                         P<int32_t>(cursors), P<int32_t>(dcount));
+                         P<int32_t>(cursors), P<int32_t>(dcount), copy_back);
   }, "", py::arg("s"), py::arg("codes_fm"), py::arg("cb"), py::arg("n_rows"), py::arg("idx"),
      py::arg("tmp"), py::arg("mask"), py::arg("items"), py::arg("n_items"), py::arg("split"),
-     py::arg("cursors"), py::arg("dcount") = 0);
+     py::arg("cursors"), py::arg("dcount") = 0, py::arg("copy_back") = true);
   m.def("seg_stats", [](uintptr_t s, uintptr_t idx, uintptr_t y, int lab_shift, bool reg,
                         uintptr_t items, int n_items, uintptr_t out, int C) {
     mt::launch_seg_stats(S(s), P<uint32_t>(idx), P<void>(y), lab_shift, reg, P<int64_t>(items),
@@ -219,10 +221,21 @@ PYBIND11_MODULE(_hip, m) {
                                  P<void>(slab), P<void>(hist), F_h, B, C, P<int32_t>(dred),
                                  P<int32_t>(dtasks));
   });
+  m.def("grow_init", [](uintptr_t s, py::dict lists, int64_t n, int64_t chunk, int C, int reg,
+                        uintptr_t root) {
+    auto g = [&](const char* k) { return lists[k].cast<uintptr_t>(); };
+    mt::LevelLists L{P<int64_t>(g("pos")),  P<int64_t>(g("start")), P<int32_t>(g("cnt")),
+                     P<int32_t>(g("depth")), P<int32_t>(g("stats")), P<int64_t>(g("items")),
+                     P<int64_t>(g("red")),  P<int64_t>(g("der")),   P<int64_t>(g("tasks")),
+                     P<int32_t>(g("ctl")),  P<int64_t>(g("stats64")), P<int64_t>(g("minmax")),
+                     P<int64_t>(g("mitems"))};
+    mt::launch_grow_init(S(s), L, n, chunk, C, reg, P<int64_t>(root));
+  });
   // cur / nxt: dicts of device pointers {pos, start, cnt, depth, stats, items, red, der, ctl}
   m.def("grow_plan", [](uintptr_t s, py::dict cur, py::dict nxt, uintptr_t rec, uintptr_t split,
                         uintptr_t pitems, uintptr_t cursors, uintptr_t pctl, uintptr_t pos_rec,
-                        uintptr_t pos_st, uintptr_t pos_st64, int reg, uintptr_t jobs,
+                        uintptr_t pos_st, uintptr_t pos_st64, int reg, int out_buf,
+                        uintptr_t jobs,
                         uintptr_t job_count, int C, int max_depth, int n_cu, int64_t mss,
                         int64_t msl, int64_t fr) {
     auto lists = [](py::dict d) {
@@ -236,7 +249,7 @@ PYBIND11_MODULE(_hip, m) {
     mt::PlanArgs a{lists(cur),          lists(nxt),         P<int64_t>(rec),
                    P<int64_t>(split),   P<int64_t>(pitems), P<int32_t>(cursors),
                    P<int32_t>(pctl),    P<int32_t>(pos_rec), P<int32_t>(pos_st),
-                   P<int64_t>(pos_st64), reg, P<int64_t>(jobs), P<int32_t>(job_count), C,
+                   P<int64_t>(pos_st64), reg, out_buf, P<int64_t>(jobs), P<int32_t>(job_count), C,
                    max_depth, n_cu, mss, msl, fr};
     mt::launch_grow_plan(S(s), a);
   });

@@ -61,6 +61,7 @@ struct PlanArgs {
   int32_t* pos_st;     // [P][C] class counts (classification)
   int64_t* pos_st64;   // [P][2] {count, sum} (regression)
   int reg;
+  int out_buf;         // row buffer (0 idx, 1 tmp) this level's partition writes
   int64_t* jobs;       // [JMAX][5 + C] finisher jobs
   int32_t* job_count;
   int C, max_depth, n_cu;
@@ -152,7 +153,27 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
   __shared__ int s_w[kPlanWaves];
   __shared__ int s_carry[4];
   __shared__ long long s_rows;
+  // cooperative expansion of per-node work items: node j of the current chunk
+  // owns items [s_off[j], s_off[j + 1]); every thread writes items, found by a
+  // binary search over the offsets, so one large node does not serialise a pass
+  __shared__ int s_off[kPlanThreads + 1];
+  __shared__ long long s_pa[kPlanThreads], s_pb[kPlanThreads];
+  __shared__ int s_pc[kPlanThreads];
   const int tid = threadIdx.x;
+  auto expand = [&](int o_local, int total, auto emit) {
+    s_off[tid] = o_local;
+    if (tid == 0) s_off[kPlanThreads] = total;
+    __syncthreads();
+    for (int it = tid; it < total; it += kPlanThreads) {
+      int lo = 0, hi = kPlanThreads;  // last j with s_off[j] <= it
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (s_off[mid] <= it) lo = mid; else hi = mid;
+      }
+      emit(lo, it - s_off[lo]);
+    }
+    __syncthreads();
+  };
   const int C = a.C;
   const int K = a.cur.ctl[0];
   // ---- pass 1: totals (built / derived next-frontier children, split nodes)
@@ -260,7 +281,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
             J[1] = cm;
             J[2] = cd;
             J[3] = cpos[c];
-            J[4] = 0;
+            J[4] = a.out_buf;  // the child's rows live where this level partitions to
             for (int k = 0; k < C; ++k) J[5 + k] = plan_child_stat(a, i, r, d.nl, c, k);
           } else {  // next frontier
             const int sl = slot[c];
@@ -330,20 +351,25 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     const int multi = kk > 1 ? 1 : 0;
     const int nt = multi ? (int)((kk + 15) / 16) : 0;
     int ti, tsl, tr, tt;
-    const int oi = plan_scan_excl((int)kk, s_w, ti) + s_carry[0];
+    const int oi_l = plan_scan_excl((int)kk, s_w, ti);
+    const int oi = oi_l + s_carry[0];
     const int osl = plan_scan_excl(multi ? (int)kk : 0, s_w, tsl) + s_carry[1];
     const int orr = plan_scan_excl(multi, s_w, tr) + s_carry[2];
     const int ot = plan_scan_excl(nt, s_w, tt) + s_carry[3];
+    s_pa[tid] = sl < NB ? a.nxt.start[sl] : 0;
+    s_pb[tid] = cnt;
+    s_pc[tid] = multi ? osl : -1;
+    const int ibase = s_carry[0];
+    expand(oi_l, ti, [&](int j, int c) {
+      int64_t* it = a.nxt.items + (int64_t)(ibase + s_off[j] + c) * 4;
+      const int64_t c0 = (int64_t)c * chunk;
+      const int64_t cn = s_pb[j] - c0;
+      it[0] = b0 + j;
+      it[1] = s_pa[j] + c0;
+      it[2] = cn < chunk ? cn : chunk;
+      it[3] = s_pc[j] >= 0 ? s_pc[j] + c : -1;
+    });
     if (sl < NB) {
-      const int64_t st0 = a.nxt.start[sl];
-      for (int64_t c = 0; c < kk; ++c) {
-        int64_t* it = a.nxt.items + (int64_t)(oi + c) * 4;
-        const int64_t c0 = c * chunk;
-        it[0] = sl;
-        it[1] = st0 + c0;
-        it[2] = (cnt - c0) < chunk ? (cnt - c0) : chunk;
-        it[3] = multi ? osl + c : -1;
-      }
       if (multi) {
         int64_t* rr = a.nxt.red + (int64_t)orr * 3;
         rr[0] = sl;
@@ -382,17 +408,18 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
       if (kk < 1) kk = 1;
     }
     int tp;
-    const int op = plan_scan_excl((int)kk, s_w, tp) + s_carry[3];
-    if (j < NS) {
-      const int64_t st0 = a.split[(int64_t)j * 4 + 0];
-      for (int64_t c = 0; c < kk; ++c) {
-        int64_t* it = a.pitems + (int64_t)(op + c) * 3;
-        const int64_t c0 = c * 1024;
-        it[0] = j;
-        it[1] = st0 + c0;
-        it[2] = (cnt - c0) < 1024 ? (cnt - c0) : 1024;
-      }
-    }
+    const int op_l = plan_scan_excl((int)kk, s_w, tp);
+    s_pa[tid] = j < NS ? a.split[(int64_t)j * 4 + 0] : 0;
+    s_pb[tid] = cnt;
+    const int pbase = s_carry[3];
+    expand(op_l, tp, [&](int jj, int c) {
+      int64_t* it = a.pitems + (int64_t)(pbase + s_off[jj] + c) * 3;
+      const int64_t c0 = (int64_t)c * 1024;
+      const int64_t cn = s_pb[jj] - c0;
+      it[0] = b0 + jj;
+      it[1] = s_pa[jj] + c0;
+      it[2] = cn < 1024 ? cn : 1024;
+    });
     __syncthreads();
     if (tid == 0) s_carry[3] += tp;
     __syncthreads();
@@ -412,16 +439,18 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
         if (kk < 1) kk = 1;
       }
       int tm;
-      const int om = plan_scan_excl((int)kk, s_w, tm) + s_carry[0];
-      if (sl < K2) {
-        const int64_t st0 = a.nxt.start[sl];
-        for (int64_t c = 0; c < kk; ++c) {
-          int64_t* it = a.nxt.mitems + (int64_t)(om + c) * 3;
-          it[0] = sl;
-          it[1] = st0 + c * 4096;
-          it[2] = (cnt - c * 4096) < 4096 ? (cnt - c * 4096) : 4096;
-        }
-      }
+      const int om_l = plan_scan_excl((int)kk, s_w, tm);
+      s_pa[tid] = sl < K2 ? a.nxt.start[sl] : 0;
+      s_pb[tid] = cnt;
+      const int mbase = s_carry[0];
+      expand(om_l, tm, [&](int j, int c) {
+        int64_t* it = a.nxt.mitems + (int64_t)(mbase + s_off[j] + c) * 3;
+        const int64_t c0 = (int64_t)c * 4096;
+        const int64_t cn = s_pb[j] - c0;
+        it[0] = b0 + j;
+        it[1] = s_pa[j] + c0;
+        it[2] = cn < 4096 ? cn : 4096;
+      });
       __syncthreads();
       if (tid == 0) s_carry[0] += tm;
       __syncthreads();
@@ -441,6 +470,59 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     a.pctl[0] = NS;
     a.pctl[1] = s_carry[3];
   }
+}
+
+// Level 0 (the root, built from rows) in one launch: root stats come from a
+// small device array (classification: C counts; regression: count, sum, min, max).
+__global__ __launch_bounds__(256) void grow_init_kernel(LevelLists L, int64_t n, int64_t chunk,
+                                                        int C, int reg,
+                                                        const int64_t* __restrict__ root) {
+  const int64_t k = (n + chunk - 1) / chunk;
+  const int64_t nt = k > 1 ? (k + 15) / 16 : 0;
+  for (int64_t i = threadIdx.x; i < k; i += blockDim.x) {
+    int64_t* it = L.items + i * 4;
+    it[0] = 0;
+    it[1] = i * chunk;
+    it[2] = (n - i * chunk) < chunk ? (n - i * chunk) : chunk;
+    it[3] = k > 1 ? i : -1;
+  }
+  for (int64_t t = threadIdx.x; t < nt; t += blockDim.x) {
+    int64_t* tk = L.tasks + t * 3;
+    tk[0] = 0;
+    tk[1] = 16 * t;
+    tk[2] = (k - 16 * t) < 16 ? (k - 16 * t) : 16;
+  }
+  if (threadIdx.x == 0) {
+    L.pos[0] = 0;
+    L.start[0] = 0;
+    L.cnt[0] = (int32_t)n;
+    L.depth[0] = 0;
+    if (reg) {
+      L.stats64[0] = root[0];
+      L.stats64[1] = root[1];
+      L.minmax[0] = root[2];
+      L.minmax[1] = root[3];
+    } else {
+      for (int c = 0; c < C; ++c) L.stats[c] = (int32_t)root[c];
+    }
+    if (k > 1) {
+      L.red[0] = 0;
+      L.red[1] = 0;
+      L.red[2] = k;
+    }
+    for (int i = 0; i < 16; ++i) L.ctl[i] = 0;
+    L.ctl[0] = 1;
+    L.ctl[1] = 1;
+    L.ctl[2] = (int32_t)k;
+    L.ctl[3] = k > 1 ? 1 : 0;
+    L.ctl[7] = (int32_t)nt;
+  }
+}
+
+void launch_grow_init(hipStream_t stream, const LevelLists& L, int64_t n, int64_t chunk, int C,
+                      int reg, const int64_t* root) {
+  hipLaunchKernelGGL(grow_init_kernel, dim3(1), dim3(256), 0, stream, L, n, chunk, C, reg, root);
+  MT_HIP_CHECK(hipGetLastError());
 }
 
 void launch_grow_plan(hipStream_t stream, const PlanArgs& a) {

@@ -232,7 +232,7 @@ void launch_seg_minmax(hipStream_t stream, const uint32_t* idx, const int64_t* y
 void launch_partition(hipStream_t stream, const void* codes_fm, int code_bytes, int64_t n_rows,
                       uint32_t* idx, uint32_t* tmp, uint32_t mask, const int64_t* items,
                       int n_items, const int64_t* split, int32_t* cursors,
-                      const int32_t* dcount) {
+                      const int32_t* dcount, bool copy_back) {
   if (n_items <= 0) return;
   if (code_bytes == 1)
     hipLaunchKernelGGL(partition_kernel<uint8_t>, dim3(n_items), dim3(kPartThreads), 0, stream,
@@ -243,6 +243,7 @@ void launch_partition(hipStream_t stream, const void* codes_fm, int code_bytes, 
                        (const uint16_t*)codes_fm, n_rows, idx, tmp, mask, items, split, cursors,
                        dcount);
   MT_HIP_CHECK(hipGetLastError());
+  if (!copy_back) return;  // device loop: levels alternate the two row buffers
   hipLaunchKernelGGL(copy_back_kernel, dim3(n_items), dim3(256), 0, stream, tmp, idx, items,
                      dcount);
   MT_HIP_CHECK(hipGetLastError());

@@ -181,35 +181,14 @@ class DeviceGrower:
             cursors = torch.empty((KMAX, 2), dtype=torch.int32, device=dev)
             jobs = torch.empty((JMAX, 5 + C), dtype=torch.int64, device=dev)
             job_count = torch.zeros(1, dtype=torch.int32, device=dev)
-            # level 0: the root, built from rows (lists prepared on the host)
+            # level 0: the root, built from rows (one init launch; root stats H2D)
             chunk = int(min(hb.MAX_ITEM_ROWS, max(1024, -(-n // (2 * hb.N_CU)))))
-            k = -(-n // chunk)
-            c0 = np.arange(k, dtype=np.int64) * chunk
-            items = np.stack([np.zeros(k, np.int64), c0, np.minimum(chunk, n - c0),
-                              np.arange(k) if k > 1 else np.full(k, -1)], 1)
-            a = sets[0]
-            a["pos"][:1].zero_()
-            a["start"][:1].zero_()
-            a["cnt"][:1].fill_(n)
-            a["depth"][:1].zero_()
-            if reg:
-                a["stats64"][:1].copy_(torch.from_numpy(root.astype(np.int64)[None, :]).to(dev))
-                a["minmax"][:1].copy_(torch.from_numpy(root_full[2:4].astype(np.int64)[None, :])
-                                      .to(dev))
-            else:
-                a["stats"][:1].copy_(torch.from_numpy(root.astype(np.int32)).to(dev))
-            a["items"][:k].copy_(torch.from_numpy(items).to(dev))
-            nt = -(-k // 16) if k > 1 else 0
-            if k > 1:
-                a["red"][:1].copy_(torch.tensor([[0, 0, k]], dtype=torch.int64, device=dev))
-                t0s = np.arange(nt, dtype=np.int64) * 16
-                a["tasks"][:nt].copy_(torch.from_numpy(
-                    np.stack([np.zeros(nt, np.int64), t0s, np.minimum(16, k - t0s)], 1)).to(dev))
-            a["ctl"].copy_(torch.tensor([1, 1, k, 1 if k > 1 else 0, 0, 0, 0, nt] + [0] * 8,
-                                        dtype=torch.int32, device=dev))
+            (d_root,) = be.up(root_full.astype(np.int64))
+            hip.grow_init(s(), ptrs[0], n, chunk, C, int(reg), d_root.data_ptr())
             pinned = torch.zeros((64, 17), dtype=torch.int32, pin_memory=True)
             events = []
             cb, rs = be.cb, be.row_elems * be.cb
+            bufs = (be.idx.data_ptr(), be.tmp.data_ptr())
             lvl = 0
             done_at = None
             prof = profiling()
@@ -230,7 +209,9 @@ class DeviceGrower:
                 kb = int(min(2 ** min(lvl, 40), KMAX))
                 ib = int(min(IMAX, kb + n // 1024 + 2 * hb.N_CU + 1))
                 ctl = cur["ctl"]
-                hip.hist(s(), be.codes_rm.data_ptr(), cb, rs, be.idx.data_ptr(), be.y.data_ptr(),
+                # rows alternate between the two permutation buffers level by level
+                src, dst = bufs[lvl % 2], bufs[(lvl + 1) % 2]
+                hip.hist(s(), be.codes_rm.data_ptr(), cb, rs, src, be.y.data_ptr(),
                          be.lab_shift, cur["items"], ib, H.data_ptr(), slab.data_ptr(), F, 0, B, C,
                          reg, hb.LDS_BUDGET, dcount=ctl + 4 * 2)
                 rb = int(min(kb, RMAX))
@@ -252,15 +233,16 @@ class DeviceGrower:
                 hip.grow_plan(s(), cur, nxt, rec.data_ptr(), split.data_ptr(), pitems.data_ptr(),
                               cursors.data_ptr(), ctl + 4 * 5, be.pos_rec.data_ptr(),
                               0 if reg else be.pos_st.data_ptr(),
-                              be.pos_st.data_ptr() if reg else 0, int(reg), jobs.data_ptr(),
+                              be.pos_st.data_ptr() if reg else 0, int(reg), (lvl + 1) % 2,
+                              jobs.data_ptr(),
                               job_count.data_ptr(), C, md, hb.N_CU, mss, msl, fr)
                 mark()
                 pb = int(min(PMAX, n // 1024 + kb + 1))
-                hip.partition(s(), be.codes_fm.data_ptr(), cb, be.n, be.idx.data_ptr(),
-                              be.tmp.data_ptr(), be.row_mask, pitems.data_ptr(), pb,
-                              split.data_ptr(), cursors.data_ptr(), dcount=ctl + 4 * 6)
+                hip.partition(s(), be.codes_fm.data_ptr(), cb, be.n, src, dst, be.row_mask,
+                              pitems.data_ptr(), pb, split.data_ptr(), cursors.data_ptr(),
+                              dcount=ctl + 4 * 6, copy_back=False)
                 if reg:  # purity of the next frontier, read by the next planner
-                    hip.seg_minmax(s(), be.idx.data_ptr(), be.y.data_ptr(), nxt["mitems"],
+                    hip.seg_minmax(s(), dst, be.y.data_ptr(), nxt["mitems"],
                                    int(min(MMAX, 2 * kb + n // 4096 + 1)), nxt["minmax"],
                                    nxt["ctl"] + 4 * 8)
                 mark()
