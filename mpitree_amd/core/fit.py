@@ -204,14 +204,13 @@ def fit_tree(
     if int(min_samples_leaf) < 1:
         raise ValueError("min_samples_leaf must be >= 1")
     dev = resolve_device(device, X)
-    if regression:
-        yv, y_exp = _encode_targets(y, n)
-        classes = None
-        C = 0
-    else:
-        classes, yv = _encode_labels(y, n)
-        y_exp = 0
-        C = len(classes)
+    classes, yv, y_exp, C = None, None, 0, 0
+    if dev != "cuda":  # the GPU path encodes labels alongside binning (gpu_prepare)
+        if regression:
+            yv, y_exp = _encode_targets(y, n)
+        else:
+            classes, yv = _encode_labels(y, n)
+            C = len(classes)
     comm = comm or LocalComm()
     params = GrowParams(
         criterion=crit,
@@ -221,7 +220,8 @@ def fit_tree(
     )
     timings = {}
     if dev == "cuda":
-        from ..ops.hip_backend import HipBackend, gpu_bin_features
+        from ..ops.gpu_prepare import prepare
+        from ..ops.hip_backend import HipBackend
 
         Xd = X if _is_tensor(X) else torch.from_numpy(np.ascontiguousarray(X))
         Xd = Xd.to("cuda")
@@ -230,13 +230,18 @@ def fit_tree(
         Xd = Xd.contiguous()
         t0 = time.perf_counter()
         with roctx_range("mpitree.bin"):
-            mapper, codes_rm, codes_fm, nb = gpu_bin_features(Xd, max_bins)
-        yd = (yv if _is_tensor(yv) else torch.from_numpy(np.ascontiguousarray(yv))).to("cuda")
+            prep = prepare(Xd, y, regression=regression, max_bins=max_bins,
+                           encode_labels=_encode_labels, encode_targets=_encode_targets,
+                           exponent=fixed_point_exponent)
+        mapper, codes_rm, codes_fm, nb = prep.mapper, prep.codes_rm, prep.codes_fm, prep.nbins
+        yd, classes, y_exp, root = prep.y, prep.classes, prep.y_exp, prep.root
+        C = 0 if regression else len(classes)
         lo, hi = comm.local_rows(n)
         if (lo, hi) != (0, n):  # data-parallel shard of a replicated input
             codes_rm = codes_rm[lo:hi].contiguous()
             codes_fm = codes_fm[:, lo:hi].contiguous()
             yd = yd[lo:hi]
+            root = None
         yd = yd.contiguous()
         timings["bin"] = time.perf_counter() - t0
         be = HipBackend()
@@ -259,7 +264,8 @@ def fit_tree(
                 params.finisher_rows = min(default_fr, be.max_finisher_rows)
             builder = DeviceGrower(be, params, comm)
             with roctx_range("mpitree.grow"):
-                ta = builder.fit(hi - lo, C, F, mapper.padded_edges(), y_exp)
+                ta = builder.fit(hi - lo, C, F, mapper, y_exp, root=root,
+                                 d_edges=prep.d_edges64)
             eng = "hip-device-loop"
         else:
             builder = LevelwiseBuilder(be, params, comm)

@@ -445,7 +445,6 @@ class LevelwiseBuilder:
             impurity=a["impurity"], count=None if reg else st,
             value=a["value"] if reg else None,
         )
-        ta.meta["term"] = a["term"]
         if reg:
             ta.meta["sum_fixed"] = st[:, 1]
         ta.meta["final"] = True  # thresholds, impurity and values are filled in

@@ -103,30 +103,53 @@ __global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __
   }
 }
 
-struct AsmOut {
-  int32_t* feature;   // [N]
-  int32_t* bin;       // [N]
-  int32_t* left;      // [N]
-  int32_t* right;     // [N]
-  int32_t* depth;     // [N]
-  int64_t* nsamp;     // [N]
-  int64_t* stats;     // [N][C]
-  double* threshold;  // [N]
-  double* term;       // [N]
-  double* impurity;   // [N]
-  double* value;      // [N] (regression) or null
+// Output columns, packed back to back for one D2H; the node count N is read
+// from the device (asm_offsets_kernel's total), so the emit launch needs no
+// host round trip. 8-byte columns first (alignment), then 4-byte columns:
+//   nsamp i64 [N] | stats i64 [N][C] | threshold f64 [N] | impurity f64 [N]
+//   | value f64 [N] (regression) | feature, bin, left, right, depth i32 [N]
+struct AsmCols {
+  int64_t* nsamp;
+  int64_t* stats;
+  double* threshold;
+  double* impurity;
+  double* value;
+  int32_t* feature;
+  int32_t* bin;
+  int32_t* left;
+  int32_t* right;
+  int32_t* depth;
 };
+
+__device__ inline AsmCols asm_cols(uint8_t* base, int64_t N, int C, bool reg) {
+  AsmCols o;
+  int64_t* p8 = reinterpret_cast<int64_t*>(base);
+  o.nsamp = p8;
+  o.stats = p8 + N;
+  o.threshold = reinterpret_cast<double*>(p8 + N * (1 + C));
+  o.impurity = o.threshold + N;
+  o.value = reg ? o.impurity + N : nullptr;
+  int32_t* p4 = reinterpret_cast<int32_t*>(o.impurity + N * (reg ? 2 : 1));
+  o.feature = p4;
+  o.bin = p4 + N;
+  o.left = p4 + 2 * N;
+  o.right = p4 + 3 * N;
+  o.depth = p4 + 4 * N;
+  return o;
+}
 
 // StatT: int32 class counts (classification) or int64 {count, fixed-point sum}.
 template <typename StatT>
 __global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
     const int32_t* __restrict__ rec, const StatT* __restrict__ st, int64_t P, int C,
     const int32_t* __restrict__ rank, const double* __restrict__ edges, int EB,
-    const double* __restrict__ xtab, int xtab_n, int crit, int y_exp, AsmOut o) {
+    const double* __restrict__ xtab, int xtab_n, int crit, int y_exp,
+    const int64_t* __restrict__ total, uint8_t* __restrict__ base) {
   const int64_t p = (int64_t)blockIdx.x * kAsmThreads + threadIdx.x;
   if (p >= P) return;
   const int j = rank[p];
   if (j < 0) return;
+  const AsmCols o = asm_cols(base, *total, C, crit == kSquaredError);
   const int32_t* R = rec + p * 6;
   const int f = R[0];
   const int b = R[1];
@@ -149,14 +172,12 @@ __global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
     return x < (int64_t)xtab_n ? xtab[x] : xlog2x((uint64_t)x);
   };
   const StatT* s = st + p * C;
-  double term;
   if (crit == kSquaredError) {
     const int64_t cnt = (int64_t)s[0], sum = (int64_t)s[1];
     o.stats[(int64_t)j * C + 0] = cnt;
     o.stats[(int64_t)j * C + 1] = sum;
-    term = mse_term(cnt, sum);
     o.impurity[j] = __builtin_nan("");
-    if (o.value) o.value[j] = ldexp((double)sum / (double)(n > 1 ? n : 1), -y_exp);
+    o.value[j] = ldexp((double)sum / (double)(n > 1 ? n : 1), -y_exp);
   } else {
     double acc = 0.0;
     int64_t m = 0, sq = 0;
@@ -167,10 +188,9 @@ __global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
       m += v;
       sq += v * v;
     }
-    term = crit == kEntropy ? T(m) - acc : gini_term(m, sq);
+    const double term = crit == kEntropy ? T(m) - acc : gini_term(m, sq);
     o.impurity[j] = n > 0 ? term / (double)n : 0.0;
   }
-  o.term[j] = term;
 }
 
 void launch_asm_rank(hipStream_t stream, const int32_t* rec, int64_t P, int32_t* tile,
@@ -187,19 +207,22 @@ void launch_asm_rank(hipStream_t stream, const int32_t* rec, int64_t P, int32_t*
 
 int asm_tiles(int64_t P) { return (int)((P + kAsmTile - 1) / kAsmTile); }
 
+int64_t asm_node_bytes(int C, bool reg) { return 8 * (1 + C + 2 + (reg ? 1 : 0)) + 4 * 5; }
+
 void launch_asm_emit(hipStream_t stream, const int32_t* rec, const void* st, bool st64,
                      int64_t P, int C, const int32_t* rank, const double* edges, int EB,
-                     const double* xtab, int xtab_n, int crit, int y_exp, const AsmOut& o) {
+                     const double* xtab, int xtab_n, int crit, int y_exp, const int64_t* total,
+                     uint8_t* base) {
   const int64_t blocks = (P + kAsmThreads - 1) / kAsmThreads;
   if (blocks == 0) return;
   if (st64)
     hipLaunchKernelGGL(asm_emit_kernel<int64_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
                        stream, rec, (const int64_t*)st, P, C, rank, edges, EB, xtab, xtab_n, crit,
-                       y_exp, o);
+                       y_exp, total, base);
   else
     hipLaunchKernelGGL(asm_emit_kernel<int32_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
                        stream, rec, (const int32_t*)st, P, C, rank, edges, EB, xtab, xtab_n, crit,
-                       y_exp, o);
+                       y_exp, total, base);
   MT_HIP_CHECK(hipGetLastError());
 }
 

@@ -32,28 +32,17 @@ void launch_seg_stats(hipStream_t, const uint32_t*, const void*, int, bool, cons
 void launch_init_idx(hipStream_t, uint32_t*, const int32_t*, int, int64_t);
 void launch_predict(hipStream_t, const void*, bool, int64_t, int, const void*, const double*,
                     int32_t*);
-void launch_bin(hipStream_t, const void*, bool, int64_t, int, const void*, int, const int32_t*,
-                const uint8_t*, void*, int, void*, int, int32_t*);
+void launch_bin(hipStream_t, const void*, bool, int64_t, int, const void*, int, int,
+                const int32_t*, const uint8_t*, void*, int, void*, int, int32_t*);
 void launch_xlog2x(hipStream_t, double*, int64_t);
+void launch_label_count(hipStream_t, const int64_t*, int64_t, int64_t, int, uint32_t*);
+void launch_label_encode(hipStream_t, const int64_t*, int64_t, int64_t, const int64_t*, int32_t*);
 void launch_finish(hipStream_t, const void*, int64_t, const void*, int, int64_t, uint32_t*,
                    uint32_t*, const int32_t*, int, const int64_t*, int, int32_t*, const int32_t*,
                    int, int, int, int, int, int64_t, int64_t, const double*, const float*, int,
                    int32_t*,
                    int32_t*, int32_t*, int, int, int64_t*, int, int64_t*);
 int finish_lds_bytes(int F, int B, int C);
-struct AsmOut {
-  int32_t* feature;
-  int32_t* bin;
-  int32_t* left;
-  int32_t* right;
-  int32_t* depth;
-  int64_t* nsamp;
-  int64_t* stats;
-  double* threshold;
-  double* term;
-  double* impurity;
-  double* value;
-};
 int asm_tiles(int64_t P);
 struct LevelLists {
   int64_t* pos;
@@ -88,8 +77,11 @@ struct PlanArgs {
   int64_t mss, msl, fr;
 };
 void launch_grow_plan(hipStream_t, const PlanArgs&);
-void launch_grow_init(hipStream_t, const LevelLists&, int64_t, int64_t, int, int, const int64_t*);
+void launch_grow_init(hipStream_t, const LevelLists&, int64_t, int64_t, int, int, const int64_t*,
+                      int32_t*);
 int finish_reg_lds_bytes(int B);
+int job_sort_max();
+void launch_job_sort(hipStream_t, const int64_t*, int, int, int64_t*, int32_t*);
 void launch_finish_reg(hipStream_t, const void*, int64_t, const void*, int, int64_t, uint32_t*,
                        uint32_t*, const int64_t*, const int64_t*, int, int32_t*, const int32_t*,
                        int, int, int, int64_t, int64_t, int32_t*, int64_t*, int, int, int64_t*,
@@ -100,11 +92,12 @@ void launch_hist_reduce_tasks(hipStream_t, const int64_t*, int, const int64_t*, 
                               void*, int, int, int, const int32_t*, const int32_t*);
 int edges_sample_rows(bool x64);
 void launch_edges(hipStream_t, const void*, bool, int64_t, int, int, int, void*, int32_t*,
-                  uint8_t*);
+                  uint8_t*, double*);
 void launch_asm_rank(hipStream_t, const int32_t*, int64_t, int32_t*, int64_t*, int32_t*);
+int64_t asm_node_bytes(int C, bool reg);
 void launch_asm_emit(hipStream_t, const int32_t*, const void*, bool, int64_t, int,
                      const int32_t*, const double*, int, const double*, int, int, int,
-                     const AsmOut&);
+                     const int64_t*, uint8_t*);
 }  // namespace mt
 
 template <typename T>
@@ -172,13 +165,19 @@ PYBIND11_MODULE(_hip, m) {
     mt::launch_predict(S(s), P<void>(X), x64, n, F, P<void>(nodes), P<double>(thr),
                        P<int32_t>(leaf));
   });
-  m.def("bin", [](uintptr_t s, uintptr_t X, bool x64, int64_t n, int F, uintptr_t edges, int Bmax,
-                  uintptr_t nbins, uintptr_t exact, uintptr_t codes_rm, int row_elems,
-                  uintptr_t codes_fm, int cb, uintptr_t bad) {
-    mt::launch_bin(S(s), P<void>(X), x64, n, F, P<void>(edges), Bmax, P<int32_t>(nbins),
-                   P<uint8_t>(exact), P<void>(codes_rm), row_elems, P<void>(codes_fm), cb,
-                   P<int32_t>(bad));
-  });
+  m.def(
+      "bin",
+      [](uintptr_t s, uintptr_t X, bool x64, int64_t n, int F, uintptr_t edges, int Bmax,
+         uintptr_t nbins, uintptr_t exact, uintptr_t codes_rm, int row_elems, uintptr_t codes_fm,
+         int cb, uintptr_t bad, int estride) {
+        mt::launch_bin(S(s), P<void>(X), x64, n, F, P<void>(edges), Bmax,
+                       estride > 0 ? estride : Bmax, P<int32_t>(nbins), P<uint8_t>(exact),
+                       P<void>(codes_rm), row_elems, P<void>(codes_fm), cb, P<int32_t>(bad));
+      },
+      py::arg("s"), py::arg("X"), py::arg("x64"), py::arg("n"), py::arg("F"), py::arg("edges"),
+      py::arg("Bmax"), py::arg("nbins"), py::arg("exact"), py::arg("codes_rm"),
+      py::arg("row_elems"), py::arg("codes_fm"), py::arg("cb"), py::arg("bad"),
+      py::arg("estride") = 0);
   m.def("finish_lds_bytes", &mt::finish_lds_bytes);
   m.def("finish", [](uintptr_t s, uintptr_t codes_rm, int64_t row_words, uintptr_t codes_fm,
                      int cb, int64_t n_rows, uintptr_t idx, uintptr_t tmp, uintptr_t y,
@@ -221,15 +220,20 @@ PYBIND11_MODULE(_hip, m) {
                                  P<void>(slab), P<void>(hist), F_h, B, C, P<int32_t>(dred),
                                  P<int32_t>(dtasks));
   });
+  m.def("job_sort_max", &mt::job_sort_max);
+  m.def("job_sort", [](uintptr_t s, uintptr_t jobs, int J, int W, uintptr_t out,
+                       uintptr_t counters) {
+    mt::launch_job_sort(S(s), P<int64_t>(jobs), J, W, P<int64_t>(out), P<int32_t>(counters));
+  });
   m.def("grow_init", [](uintptr_t s, py::dict lists, int64_t n, int64_t chunk, int C, int reg,
-                        uintptr_t root) {
+                        uintptr_t root, uintptr_t job_count) {
     auto g = [&](const char* k) { return lists[k].cast<uintptr_t>(); };
     mt::LevelLists L{P<int64_t>(g("pos")),  P<int64_t>(g("start")), P<int32_t>(g("cnt")),
                      P<int32_t>(g("depth")), P<int32_t>(g("stats")), P<int64_t>(g("items")),
                      P<int64_t>(g("red")),  P<int64_t>(g("der")),   P<int64_t>(g("tasks")),
                      P<int32_t>(g("ctl")),  P<int64_t>(g("stats64")), P<int64_t>(g("minmax")),
                      P<int64_t>(g("mitems"))};
-    mt::launch_grow_init(S(s), L, n, chunk, C, reg, P<int64_t>(root));
+    mt::launch_grow_init(S(s), L, n, chunk, C, reg, P<int64_t>(root), P<int32_t>(job_count));
   });
   // cur / nxt: dicts of device pointers {pos, start, cnt, depth, stats, items, red, der, ctl}
   m.def("grow_plan", [](uintptr_t s, py::dict cur, py::dict nxt, uintptr_t rec, uintptr_t split,
@@ -254,30 +258,36 @@ PYBIND11_MODULE(_hip, m) {
     mt::launch_grow_plan(S(s), a);
   });
   m.def("edges_sample_rows", &mt::edges_sample_rows);
-  m.def("edges", [](uintptr_t s, uintptr_t X, bool x64, int64_t n, int F, int rows, int limit,
-                    uintptr_t edges, uintptr_t nbins, uintptr_t exact) {
-    mt::launch_edges(S(s), P<void>(X), x64, n, F, rows, limit, P<void>(edges), P<int32_t>(nbins),
-                     P<uint8_t>(exact));
-  });
+  m.def(
+      "edges",
+      [](uintptr_t s, uintptr_t X, bool x64, int64_t n, int F, int rows, int limit,
+         uintptr_t edges, uintptr_t nbins, uintptr_t exact, uintptr_t pack) {
+        mt::launch_edges(S(s), P<void>(X), x64, n, F, rows, limit, P<void>(edges),
+                         P<int32_t>(nbins), P<uint8_t>(exact), P<double>(pack));
+      },
+      py::arg("s"), py::arg("X"), py::arg("x64"), py::arg("n"), py::arg("F"), py::arg("rows"),
+      py::arg("limit"), py::arg("edges"), py::arg("nbins"), py::arg("exact"),
+      py::arg("pack") = 0);
   m.def("asm_rank", [](uintptr_t s, uintptr_t rec, int64_t npos, uintptr_t tile, uintptr_t total,
                        uintptr_t rank) {
     mt::launch_asm_rank(S(s), P<int32_t>(rec), npos, P<int32_t>(tile), P<int64_t>(total),
                         P<int32_t>(rank));
   });
+  m.def("asm_node_bytes", &mt::asm_node_bytes);
   m.def("asm_emit", [](uintptr_t s, uintptr_t rec, uintptr_t st, bool st64, int64_t npos, int C,
                        uintptr_t rank, uintptr_t edges, int EB, uintptr_t xtab, int xtab_n,
-                       int crit, int y_exp, py::dict out) {
-    auto ptr = [&](const char* k) -> uintptr_t {
-      return out.contains(k) ? out[k].cast<uintptr_t>() : (uintptr_t)0;
-    };
-    mt::AsmOut o{P<int32_t>(ptr("feature")),  P<int32_t>(ptr("bin")),
-                 P<int32_t>(ptr("left")),     P<int32_t>(ptr("right")),
-                 P<int32_t>(ptr("depth")),    P<int64_t>(ptr("nsamp")),
-                 P<int64_t>(ptr("stats")),    P<double>(ptr("threshold")),
-                 P<double>(ptr("term")),      P<double>(ptr("impurity")),
-                 P<double>(ptr("value"))};
+                       int crit, int y_exp, uintptr_t total, uintptr_t base) {
     mt::launch_asm_emit(S(s), P<int32_t>(rec), P<void>(st), st64, npos, C, P<int32_t>(rank),
-                        P<double>(edges), EB, P<double>(xtab), xtab_n, crit, y_exp, o);
+                        P<double>(edges), EB, P<double>(xtab), xtab_n, crit, y_exp,
+                        P<int64_t>(total), P<uint8_t>(base));
+  });
+  m.def("label_count", [](uintptr_t s, uintptr_t y, int64_t n, int64_t lo, int R,
+                          uintptr_t counts) {
+    mt::launch_label_count(S(s), P<int64_t>(y), n, lo, R, P<uint32_t>(counts));
+  });
+  m.def("label_encode", [](uintptr_t s, uintptr_t y, int64_t n, int64_t lo, uintptr_t lut,
+                           uintptr_t out) {
+    mt::launch_label_encode(S(s), P<int64_t>(y), n, lo, P<int64_t>(lut), P<int32_t>(out));
   });
   m.def("xlog2x_device", [](uintptr_t s, uintptr_t out, int64_t n) {
     mt::launch_xlog2x(S(s), P<double>(out), n);

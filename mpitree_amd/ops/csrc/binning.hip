@@ -218,7 +218,7 @@ constexpr int kBinPer = kBinRows * kBinFt / 256;    // elements per thread
 template <typename XT, typename CodeT, bool kLds>
 __global__ __launch_bounds__(256) void bin_kernel(const XT* __restrict__ X, int64_t n, int F,
                                                   const XT* __restrict__ edges, int Bmax,
-                                                  int steps0, const int32_t* __restrict__ nbins,
+                                                  int estride, int steps0, const int32_t* __restrict__ nbins,
                                                   const uint8_t* __restrict__ exact,
                                                   CodeT* __restrict__ codes_rm, int row_elems,
                                                   CodeT* __restrict__ codes_fm,
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(256) void bin_kernel(const XT* __restrict__ X, int6
   if constexpr (kLds) {
     for (int e = threadIdx.x; e < nf * Bmax; e += 256) {
       const int fl = e / Bmax, b = e - fl * Bmax;
-      s_edges[fl * ES + b] = edges[(int64_t)f0 * Bmax + e];
+      s_edges[fl * ES + b] = edges[(int64_t)(f0 + fl) * estride + b];
     }
   }
   __syncthreads();
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256) void bin_kernel(const XT* __restrict__ X, int6
     for (int k = 0; k < kBinPer; ++k) {
       const int fl = (threadIdx.x + 256 * k) % kBinFt;
       const int p = pos[k] + step;
-      const XT* ed = kLds ? s_edges + fl * ES : edges + (int64_t)(f0 + fl) * Bmax;
+      const XT* ed = kLds ? s_edges + fl * ES : edges + (int64_t)(f0 + fl) * estride;
       if (p <= nb[k] && ed[p - 1] < v[k]) pos[k] = p;
     }
   }
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void bin_kernel(const XT* __restrict__ X, int6
     const int e = threadIdx.x + 256 * k;
     const int r = e / kBinFt, fl = e % kBinFt;
     if (!ok[k]) continue;
-    const XT* ed = kLds ? s_edges + fl * ES : edges + (int64_t)(f0 + fl) * Bmax;
+    const XT* ed = kLds ? s_edges + fl * ES : edges + (int64_t)(f0 + fl) * estride;
     const int code = pos[k] < nb[k] ? pos[k] : nb[k] - 1;
     int fg = 0;
     if (s_ex[fl] && !(ed[code] == v[k])) fg |= 1;
@@ -304,8 +304,28 @@ __global__ __launch_bounds__(256) void bin_kernel(const XT* __restrict__ X, int6
 
 int edges_sample_rows(bool x64) { return x64 ? 16384 : 32768; }
 
+// The host's view of the edges in one fp64 array: [F][limit] edges, then the
+// F bin counts, then the F exact flags -- a single D2H instead of a gather.
+template <typename XT>
+__global__ __launch_bounds__(256) void edges_pack_kernel(const XT* __restrict__ edges,
+                                                         const int32_t* __restrict__ nbins,
+                                                         const uint8_t* __restrict__ exact, int F,
+                                                         int limit, double* __restrict__ pack) {
+  const int64_t E = (int64_t)F * limit;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < E + 2 * F; i += (int64_t)gridDim.x * 256) {
+    double v;
+    if (i < E)
+      v = (double)edges[i];
+    else if (i < E + F)
+      v = (double)nbins[i - E];
+    else
+      v = (double)exact[i - E - F];
+    pack[i] = v;
+  }
+}
+
 void launch_edges(hipStream_t stream, const void* X, bool x64, int64_t n, int F, int s, int limit,
-                  void* edges, int32_t* nbins, uint8_t* exact) {
+                  void* edges, int32_t* nbins, uint8_t* exact, double* pack) {
   if (F <= 0) return;
   int S = 1;
   while (S < s) S <<= 1;
@@ -316,7 +336,13 @@ void launch_edges(hipStream_t stream, const void* X, bool x64, int64_t n, int F,
   MT_HIP_CHECK(hipFuncSetAttribute((const void*)edges_kernel<XT>,                              \
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));     \
   hipLaunchKernelGGL(edges_kernel<XT>, dim3(F), dim3(kEdgeThreads), lds, stream, (const XT*)X, \
-                     n, F, s, S, limit, (XT*)edges, nbins, exact);
+                     n, F, s, S, limit, (XT*)edges, nbins, exact);                             \
+  if (pack) {                                                                                  \
+    const int64_t tot = (int64_t)F * limit + 2 * F;                                            \
+    const int g = (int)std::min<int64_t>((tot + 255) / 256, 1024);                             \
+    hipLaunchKernelGGL(edges_pack_kernel<XT>, dim3(g), dim3(256), 0, stream, (const XT*)edges, \
+                       nbins, exact, F, limit, pack);                                          \
+  }
   if (x64) {
     MT_EDGES(double)
   } else {
@@ -327,7 +353,7 @@ void launch_edges(hipStream_t stream, const void* X, bool x64, int64_t n, int F,
 }
 
 void launch_bin(hipStream_t stream, const void* X, bool x64, int64_t n, int F, const void* edges,
-                int Bmax, const int32_t* nbins, const uint8_t* exact, void* codes_rm,
+                int Bmax, int estride, const int32_t* nbins, const uint8_t* exact, void* codes_rm,
                 int row_elems, void* codes_fm, int code_bytes, int32_t* flags) {
   if (n <= 0) return;
   const int xb = x64 ? 8 : 4;
@@ -342,7 +368,7 @@ void launch_bin(hipStream_t stream, const void* X, bool x64, int64_t n, int F, c
     MT_HIP_CHECK(hipFuncSetAttribute((const void*)bin_kernel<XT, CT, L>,                       \
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));   \
     hipLaunchKernelGGL((bin_kernel<XT, CT, L>), grid, dim3(256), lds, stream, (const XT*)X, n, \
-                       F, (const XT*)edges, Bmax, steps0, nbins, exact, (CT*)codes_rm,         \
+                       F, (const XT*)edges, Bmax, estride, steps0, nbins, exact, (CT*)codes_rm, \
                        row_elems, (CT*)codes_fm, flags);                                       \
   }
 #define MT_BIN2(XT, CT)      \

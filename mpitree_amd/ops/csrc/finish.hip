@@ -32,15 +32,15 @@
 
 namespace mt {
 
-constexpr int kFinThreads = 256;
+constexpr int kFinThreads = 512;
 constexpr int kFinWaves = kFinThreads / kWave;
 constexpr int kFinStack = 40;    // >= log2(max job rows) + 2
 constexpr int kFinMaxC = 16;     // classes supported by the finisher
 constexpr int kFinTab = 1024;    // LDS x*log2(x) entries
 constexpr int kFinUnroll = 4;    // row gathers in flight per lane
 constexpr int kFinMaxF = 256;    // features (the LDS histogram bounds F far lower)
-constexpr int kFinPair = 2;      // features scanned together per wave (latency hiding)
-constexpr int kFinChunk = 16;    // features per wave whose per-lane minima stay in registers
+constexpr int kFinPair = 1;      // features scanned together per wave (latency hiding)
+constexpr int kFinChunk = 8;     // features per wave whose per-lane minima stay in registers
 
 // Histogram row stride in words: >= B*W + 1 (the odd word staggers features over
 // LDS banks for the atomics), rounded to 4 so each feature row is 16-B aligned.
@@ -60,7 +60,7 @@ struct FinRowLab {
 // node_i32: [slots][6] = {feature, bin, left, right, depth, n}; node_cnt: [slots][C]
 
 template <typename CodeT, bool kC2>
-__global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
+__global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))) void finish_cls_kernel(
     const uint32_t* __restrict__ codes_rm, int64_t row_words, const CodeT* __restrict__ codes_fm,
     int64_t n_rows, uint32_t* __restrict__ buf0, uint32_t* __restrict__ buf1,
     const int32_t* __restrict__ y, FinRowLab rl, const int64_t* __restrict__ jobs, int J,
@@ -114,14 +114,17 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
   int lane_shift = 0;
   while ((1 << lane_shift) * vec < words && lane_shift < 6) ++lane_shift;
 
-  int64_t pr_nodes = 0, pr_rows = 0, pr_c[5] = {0, 0, 0, 0, 0};
-  const int64_t pr_wall0 = prof ? (int64_t)wall_clock64() : 0;
-  int64_t pr_t = 0;
+  // profile counters live in LDS (thread 0 only): no VGPRs on the hot path
+  __shared__ int64_t s_pr[9];  // {wall0, nodes, rows, cycles[5], last clock}
+  if (prof && tid == 0) {
+    s_pr[0] = (int64_t)wall_clock64();
+    for (int k = 1; k < 9; ++k) s_pr[k] = 0;
+  }
   auto mark = [&](int k) {
     if (prof && tid == 0) {
       const int64_t t = (int64_t)clock64();
-      pr_c[k] += t - pr_t;
-      pr_t = t;
+      s_pr[3 + k] += t - s_pr[8];
+      s_pr[8] = t;
     }
   };
   if constexpr (kC2) {
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
     __syncthreads();
     const int job = s_job;
     if (job >= J) break;
-    if (prof && tid == 0) pr_t = (int64_t)clock64();
+    if (prof && tid == 0) s_pr[8] = (int64_t)clock64();
     const int64_t* jb = jobs + (int64_t)job * JW;
     int32_t* ni = node_i32;  // indexed by pre-order position (see launch_finish)
     int32_t* nc = node_cnt;
@@ -321,8 +324,10 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
       const int depth = s_depth;
       const int id = s_id;
       mark(3);
-      pr_nodes += 1;
-      pr_rows += m;
+      if (prof && tid == 0) {
+        s_pr[1] += 1;
+        s_pr[2] += m;
+      }
       uint32_t* __restrict__ src = s_buf ? buf1 : buf0;
       uint32_t* __restrict__ dst = s_buf ? buf0 : buf1;
       // ---- histogram of this node's rows (all features): VEC words per lane,
@@ -667,11 +672,11 @@ __global__ __launch_bounds__(kFinThreads, 2) void finish_cls_kernel(
   }
   if (prof && tid == 0) {
     int64_t* P = prof + (int64_t)blockIdx.x * 10;
-    P[0] = pr_wall0;
+    P[0] = s_pr[0];
     P[1] = (int64_t)wall_clock64();
-    P[2] = pr_nodes;
-    P[3] = pr_rows;
-    for (int k = 0; k < 5; ++k) P[4 + k] = pr_c[k];
+    P[2] = s_pr[1];
+    P[3] = s_pr[2];
+    for (int k = 0; k < 5; ++k) P[4 + k] = s_pr[3 + k];
     P[9] = s_cand_total;
   }
 }

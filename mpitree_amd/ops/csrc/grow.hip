@@ -467,6 +467,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     a.nxt.ctl[5] = 0;
     a.nxt.ctl[6] = 0;
     a.nxt.ctl[7] = n_tasks;
+    a.nxt.ctl[9] = atomicAdd(a.job_count, 0);  // finisher jobs so far (host's lagged read)
     a.pctl[0] = NS;
     a.pctl[1] = s_carry[3];
   }
@@ -476,7 +477,8 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
 // small device array (classification: C counts; regression: count, sum, min, max).
 __global__ __launch_bounds__(256) void grow_init_kernel(LevelLists L, int64_t n, int64_t chunk,
                                                         int C, int reg,
-                                                        const int64_t* __restrict__ root) {
+                                                        const int64_t* __restrict__ root,
+                                                        int32_t* __restrict__ job_count) {
   const int64_t k = (n + chunk - 1) / chunk;
   const int64_t nt = k > 1 ? (k + 15) / 16 : 0;
   for (int64_t i = threadIdx.x; i < k; i += blockDim.x) {
@@ -493,6 +495,7 @@ __global__ __launch_bounds__(256) void grow_init_kernel(LevelLists L, int64_t n,
     tk[2] = (k - 16 * t) < 16 ? (k - 16 * t) : 16;
   }
   if (threadIdx.x == 0) {
+    *job_count = 0;
     L.pos[0] = 0;
     L.start[0] = 0;
     L.cnt[0] = (int32_t)n;
@@ -520,8 +523,63 @@ __global__ __launch_bounds__(256) void grow_init_kernel(LevelLists L, int64_t n,
 }
 
 void launch_grow_init(hipStream_t stream, const LevelLists& L, int64_t n, int64_t chunk, int C,
-                      int reg, const int64_t* root) {
-  hipLaunchKernelGGL(grow_init_kernel, dim3(1), dim3(256), 0, stream, L, n, chunk, C, reg, root);
+                      int reg, const int64_t* root, int32_t* job_count) {
+  hipLaunchKernelGGL(grow_init_kernel, dim3(1), dim3(256), 0, stream, L, n, chunk, C, reg, root,
+                     job_count);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+// Finisher job order: largest subtree first (stable), so the persistent
+// finisher workgroups start the long jobs early. One workgroup bitonic-sorts
+// 32-bit keys {0xFFFF - rows : 16, index : 13} in LDS and gathers the rows;
+// it also zeroes the finisher's work counters.
+constexpr int kSortMax = 8192;
+
+__global__ __launch_bounds__(1024) void job_sort_kernel(const int64_t* __restrict__ jobs, int J,
+                                                        int W, int64_t* __restrict__ out,
+                                                        int32_t* __restrict__ counters) {
+  __shared__ uint32_t key[kSortMax];
+  int N2 = 1;
+  while (N2 < J) N2 <<= 1;
+  for (int i = threadIdx.x; i < N2; i += 1024) {
+    uint32_t k = 0xFFFFFFFFu;
+    if (i < J) {
+      const int64_t c = jobs[(int64_t)i * W + 1];
+      const uint32_t cc = c > 0xFFFF ? 0xFFFFu : (uint32_t)c;
+      k = ((0xFFFFu - cc) << 13) | (uint32_t)i;
+    }
+    key[i] = k;
+  }
+  if (threadIdx.x < 4) counters[threadIdx.x] = 0;
+  __syncthreads();
+  for (int size = 2; size <= N2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < N2; i += 1024) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const uint32_t a = key[i], b = key[j];
+          const bool up = (i & size) == 0;
+          if ((a > b) == up) {
+            key[i] = b;
+            key[j] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int e = threadIdx.x; e < J * W; e += 1024) {
+    const int r = e / W, c = e - r * W;
+    out[e] = jobs[(int64_t)(key[r] & 0x1FFFu) * W + c];
+  }
+}
+
+int job_sort_max() { return kSortMax; }
+
+void launch_job_sort(hipStream_t stream, const int64_t* jobs, int J, int W, int64_t* out,
+                     int32_t* counters) {
+  if (J > kSortMax) throw std::runtime_error("job_sort: too many jobs for one workgroup");
+  hipLaunchKernelGGL(job_sort_kernel, dim3(1), dim3(1024), 0, stream, jobs, J, W, out, counters);
   MT_HIP_CHECK(hipGetLastError());
 }
 

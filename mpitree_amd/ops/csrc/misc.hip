@@ -2,6 +2,8 @@
 #include "common.h"
 #include "criterion.h"
 
+#include <algorithm>
+
 namespace mt {
 
 __global__ void xlog2x_kernel(double* __restrict__ out, int64_t n) {
@@ -14,6 +16,65 @@ void launch_xlog2x(hipStream_t stream, double* out, int64_t n) {
   if (n <= 0) return;
   hipLaunchKernelGGL(xlog2x_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, out,
                      n);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+// ---- device-resident class labels (core/fit.py prepare path) --------------
+// The reference encodes labels with np.unique on every rank
+// (mpitree/tree/decision_tree.py:418-421); here an int64 label column on the
+// GPU is counted over its [lo, lo + R) range and re-coded through a LUT, so
+// the classes, the root class counts and the int32 codes cost one small D2H.
+constexpr int kLabLds = 8192;
+
+__global__ __launch_bounds__(256) void label_count_kernel(const int64_t* __restrict__ y,
+                                                          int64_t n, int64_t lo, int R,
+                                                          uint32_t* __restrict__ counts) {
+  __shared__ uint32_t h[kLabLds];
+  const bool lds = R <= kLabLds;
+  if (lds)
+    for (int i = threadIdx.x; i < R; i += 256) h[i] = 0;
+  __syncthreads();
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int v = (int)(y[i] - lo);
+    if (lds)
+      atomicAdd(&h[v], 1u);
+    else
+      atomicAdd(&counts[v], 1u);
+  }
+  if (lds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < R; i += 256)
+      if (h[i]) atomicAdd(&counts[i], h[i]);
+  }
+}
+
+__global__ __launch_bounds__(256) void label_encode_kernel(const int64_t* __restrict__ y,
+                                                           int64_t n, int64_t lo,
+                                                           const int64_t* __restrict__ lut,
+                                                           int32_t* __restrict__ out) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    out[i] = (int32_t)lut[y[i] - lo];
+}
+
+static unsigned label_grid(int64_t n) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 2048));
+}
+
+void launch_label_count(hipStream_t stream, const int64_t* y, int64_t n, int64_t lo, int R,
+                        uint32_t* counts) {
+  MT_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(uint32_t) * (size_t)R, stream));
+  if (n <= 0) return;
+  // LDS-privatised histograms: fewer, fuller blocks; global atomics otherwise
+  const unsigned g = R <= kLabLds ? std::min(label_grid(n), 512u) : label_grid(n);
+  hipLaunchKernelGGL(label_count_kernel, dim3(g), dim3(256), 0, stream, y, n, lo, R, counts);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_label_encode(hipStream_t stream, const int64_t* y, int64_t n, int64_t lo,
+                         const int64_t* lut, int32_t* out) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(label_encode_kernel, dim3(label_grid(n)), dim3(256), 0, stream, y, n, lo,
+                     lut, out);
   MT_HIP_CHECK(hipGetLastError());
 }
 

@@ -39,6 +39,8 @@ from . import hip_backend as hb
 
 __all__ = ["DeviceGrower", "device_loop_supported"]
 
+_WORKSPACES: dict = {}  # (device, n, F, B, C, reg, fr) -> level-loop buffers
+
 
 def device_loop_supported(be, params, comm) -> bool:
     if os.environ.get("MPITREE_DEVICE_LOOP", "1") == "0":
@@ -80,7 +82,7 @@ class DeviceGrower:
             mitems=torch.empty((MMAX if reg else 1, 3), **i64),
         )
 
-    def _run_jobs(self, d_jobs, n: int):
+    def _run_jobs(self, d_jobs, n: int, counter=None):
         """Finish the (largest-first) job list; with several ranks each takes a
         serpentine share (0..P-1, P-1..0, ...) -- near-even row totals."""
         be, comm = self.be, self.comm
@@ -90,9 +92,11 @@ class DeviceGrower:
             lap, off = k // P, k % P
             owner = torch.where(lap % 2 == 0, off, P - 1 - off)
             d_jobs = d_jobs[owner == r]
+            counter = None
         J = int(d_jobs.shape[0])
         if J:
-            be.launch_finisher(d_jobs.contiguous(), J, n, self.p, be.pos_rec, be.pos_st)
+            be.launch_finisher(d_jobs.contiguous(), J, n, self.p, be.pos_rec, be.pos_st,
+                               counter)
 
     def _exchange_nodes(self):
         """Every rank ends with every finished node: compact the written
@@ -126,7 +130,23 @@ class DeviceGrower:
         return {k: v.data_ptr() for k, v in lists.items()}
 
     # --------------------------------------------------------------- fit
-    def fit(self, n: int, n_classes: int, n_features: int, edges, y_exp: int = 0) -> TreeArrays:
+    def _workspace(self, key, make):
+        """Level-loop buffers, reused by consecutive fits of one shape (the
+        allocations and pinned buffers cost more host time than a level)."""
+        ws = _WORKSPACES.pop(key, None)
+        if ws is None:
+            ws = make()
+        _WORKSPACES[key] = ws  # most recently used last
+        while len(_WORKSPACES) > 2:
+            _WORKSPACES.pop(next(iter(_WORKSPACES)))
+        return ws
+
+    def fit(self, n: int, n_classes: int, n_features: int, edges, y_exp: int = 0,
+            root=None, d_edges=None) -> TreeArrays:
+        """Grow the tree. ``edges``: host edge table ``[F, W]`` or a BinMapper
+        (only materialised when ``d_edges``, the device copy, is absent);
+        ``root``: root statistics when the caller already has them
+        (gpu_prepare), which saves a device round trip."""
         be, p = self.be, self.p
         hip = be.hip
         dev = be.device
@@ -137,7 +157,10 @@ class DeviceGrower:
         mss, msl = int(p.min_samples_split), int(max(1, p.min_samples_leaf))
         s = hb._stream
         t0 = time.perf_counter()
-        root_full = be.segment_stats(np.array([0]), np.array([n]))[0]  # one small sync
+        if root is None:
+            root_full = be.segment_stats(np.array([0]), np.array([n]))[0]  # one small sync
+        else:
+            root_full = np.asarray(root, dtype=np.int64)
         be.begin_positions(2 * n - 1)
         if reg:  # {count, sum, min, max}: a root with equal targets is a leaf
             root = root_full[:2]
@@ -165,27 +188,47 @@ class DeviceGrower:
             RMAX = int(min(KMAX, max(2 * hb.N_CU + 1, n // 1024 + 1)))
             TMAX = RMAX + IMAX // 16 + 16
             MMAX = KMAX + n // 4096 + 16
-            sets = [self._lists(KMAX, IMAX, TMAX, MMAX, C, reg, dev) for _ in range(2)]
-            ptrs = [self._ptrs(x) for x in sets]
             E = F * B * C
             hdt = torch.int64 if reg else torch.int32
-            hists = [torch.empty((KMAX, F, B, C), dtype=hdt, device=dev) for _ in range(2)]
-            sw = hip.hist_slab_words(F, B, C, reg)
-            slab = torch.empty((IMAX, sw), dtype=hdt, device=dev)
-            rec = torch.empty((KMAX, R), dtype=torch.int64, device=dev)
-            cost = torch.empty((KMAX, F), dtype=torch.float64, device=dev)
-            bins = torch.empty((KMAX, F), dtype=torch.int32, device=dev)
-            ident = torch.arange(KMAX, dtype=torch.int64, device=dev)
-            split = torch.empty((KMAX, 4), dtype=torch.int64, device=dev)
-            pitems = torch.empty((PMAX, 3), dtype=torch.int64, device=dev)
-            cursors = torch.empty((KMAX, 2), dtype=torch.int32, device=dev)
-            jobs = torch.empty((JMAX, 5 + C), dtype=torch.int64, device=dev)
-            job_count = torch.zeros(1, dtype=torch.int32, device=dev)
+            W = 7 if reg else 5 + C  # finisher job row width
+
+            def make():
+                i64 = dict(dtype=torch.int64, device=dev)
+                return dict(
+                    sets=[self._lists(KMAX, IMAX, TMAX, MMAX, C, reg, dev) for _ in range(2)],
+                    hists=[torch.empty((KMAX, F, B, C), dtype=hdt, device=dev)
+                           for _ in range(2)],
+                    slab=torch.empty((IMAX, hip.hist_slab_words(F, B, C, reg)), dtype=hdt,
+                                     device=dev),
+                    rec=torch.empty((KMAX, R), **i64),
+                    cost=torch.empty((KMAX, F), dtype=torch.float64, device=dev),
+                    bins=torch.empty((KMAX, F), dtype=torch.int32, device=dev),
+                    ident=torch.arange(KMAX, **i64),
+                    split=torch.empty((KMAX, 4), **i64),
+                    pitems=torch.empty((PMAX, 3), **i64),
+                    cursors=torch.empty((KMAX, 2), dtype=torch.int32, device=dev),
+                    jobs=torch.empty((JMAX, W), **i64),
+                    jobs_sorted=torch.empty((min(JMAX, hip.job_sort_max()), W), **i64),
+                    job_count=torch.zeros(1, dtype=torch.int32, device=dev),
+                    fin_counter=torch.zeros(4, dtype=torch.int32, device=dev),
+                    root=torch.empty(4 if reg else C, **i64),
+                    root_host=torch.empty(4 if reg else C, dtype=torch.int64, pin_memory=True),
+                    pinned=torch.zeros((64, 16), dtype=torch.int32, pin_memory=True),
+                )
+
+            ws = self._workspace((str(dev), n, F, B, C, reg, fr), make)
+            sets, hists, slab, rec = ws["sets"], ws["hists"], ws["slab"], ws["rec"]
+            cost, bins, ident, split = ws["cost"], ws["bins"], ws["ident"], ws["split"]
+            pitems, cursors, jobs, job_count = (ws["pitems"], ws["cursors"], ws["jobs"],
+                                                ws["job_count"])
+            pinned = ws["pinned"]
+            ptrs = [self._ptrs(x) for x in sets]
             # level 0: the root, built from rows (one init launch; root stats H2D)
             chunk = int(min(hb.MAX_ITEM_ROWS, max(1024, -(-n // (2 * hb.N_CU)))))
-            (d_root,) = be.up(root_full.astype(np.int64))
-            hip.grow_init(s(), ptrs[0], n, chunk, C, int(reg), d_root.data_ptr())
-            pinned = torch.zeros((64, 17), dtype=torch.int32, pin_memory=True)
+            ws["root_host"].numpy()[: root_full.size] = root_full
+            ws["root"].copy_(ws["root_host"], non_blocking=True)
+            hip.grow_init(s(), ptrs[0], n, chunk, C, int(reg), ws["root"].data_ptr(),
+                          job_count.data_ptr())
             events = []
             cb, rs = be.cb, be.row_elems * be.cb
             bufs = (be.idx.data_ptr(), be.tmp.data_ptr())
@@ -248,8 +291,7 @@ class DeviceGrower:
                 mark()
                 # lagged completion check: next level's frontier size + job count
                 slot = lvl % 64
-                pinned[slot, :16].copy_(sets[(lvl + 1) % 2]["ctl"], non_blocking=True)
-                pinned[slot, 16:17].copy_(job_count, non_blocking=True)
+                pinned[slot].copy_(sets[(lvl + 1) % 2]["ctl"], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record()
                 events.append(ev)
@@ -263,13 +305,20 @@ class DeviceGrower:
                 if lvl > 4096:
                     raise RuntimeError("device level loop did not terminate")
             levels = done_at + 1
-            J = int(pinned[done_at % 64, 16])
+            J = int(pinned[done_at % 64, 9])  # ctl[9]: finisher jobs appended
             if prof:
                 self._level_profile(marks[:levels])
-            self._keep = (sets, hists, slab, rec, cost, bins, split, pitems, cursors)
             if J:
-                order = torch.argsort(jobs[:J, 1], descending=True, stable=True)
-                self._run_jobs(jobs[:J].index_select(0, order), n)
+                counter = None
+                if J <= hip.job_sort_max():  # one-workgroup sort, zeroes the counters too
+                    d_jobs = ws["jobs_sorted"][:J]
+                    counter = ws["fin_counter"]
+                    hip.job_sort(s(), jobs.data_ptr(), J, W, d_jobs.data_ptr(),
+                                 counter.data_ptr())
+                else:
+                    order = torch.argsort(jobs[:J, 1], descending=True, stable=True)
+                    d_jobs = jobs[:J].index_select(0, order)
+                self._run_jobs(d_jobs, n, counter)
         elif jobs_host is not None:
             J = 1
             (d_jobs,) = be.up(jobs_host)
@@ -282,7 +331,9 @@ class DeviceGrower:
         self.stats["levels"] = levels
         self.stats["finisher_subtrees"] = J
         t0 = time.perf_counter()
-        a = be.assemble_positions(edges, int(p.criterion), y_exp)
+        if d_edges is None and not isinstance(edges, np.ndarray):
+            edges = edges.padded_edges()
+        a = be.assemble_positions(edges, int(p.criterion), y_exp, d_edges=d_edges)
         self.timings["assemble"] = time.perf_counter() - t0
         st = a["stats"]
         ta = TreeArrays(
@@ -291,7 +342,6 @@ class DeviceGrower:
             impurity=a["impurity"], count=None if reg else st,
             value=a["value"] if reg else None,
         )
-        ta.meta["term"] = a["term"]
         if reg:
             ta.meta["sum_fixed"] = st[:, 1]
         ta.meta["final"] = True

@@ -1,0 +1,168 @@
+"""Device-side fit preparation: binning plus label / target encoding.
+
+The reference prepares a fit on the host of every rank (``np.unique`` class
+discovery, ``mpitree/tree/decision_tree.py:418-421``; no binning -- it scans
+raw values). Here a fit on the GPU needs, before the first tree level:
+
+* the feature bin edges, codes and verification flags (``DeviceBinning``),
+* the class list and int32 label codes (or the fixed-point regression
+  targets and their exponent),
+* the root node's statistics (class counts, or {count, sum, min, max}).
+
+Every host decision among these needs a small device read; issued one by one
+they cost ~6 synchronisations with host work in between, during which the
+GPU idles. :func:`prepare` interleaves them into two synchronisations: the
+edge table travels with the label range (or target scale), and the bin
+kernel's flags travel with the class counts (or target root stats). The root
+statistics then come for free and the device level loop starts without
+another round trip.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import native
+from .hip_backend import DeviceBinning, _pinned_copy, _stream, _uploader
+
+__all__ = ["Prepared", "prepare"]
+
+_LUT_MAX = 1 << 22  # label ranges beyond this fall back to torch.unique
+
+
+@dataclass
+class Prepared:
+    mapper: object
+    codes_rm: torch.Tensor
+    codes_fm: torch.Tensor
+    nbins: torch.Tensor
+    y: torch.Tensor  # int32 class codes or int64 fixed-point targets (device)
+    classes: np.ndarray | None
+    y_exp: int
+    root: np.ndarray | None  # root statistics when known without another sync
+    d_edges64: torch.Tensor | None  # device fp64 edge table [F, W] (None: use host edges)
+
+
+def _np_dtype(dt: torch.dtype):
+    return torch.empty(0, dtype=dt).numpy().dtype
+
+
+class _Labels:
+    """Classification labels: device int tensors take the two-sync path."""
+
+    def __init__(self, y, n, dev, encode_fallback):
+        self.y, self.n, self.dev = y, n, dev
+        self.fallback = encode_fallback
+        self.dev_path = (
+            torch.is_tensor(y) and y.is_cuda and y.dim() == 1 and y.shape[0] == n and n > 0
+            and not torch.is_floating_point(y) and y.dtype != torch.bool
+        )
+        if self.dev_path:
+            self.yl = (y if y.dtype == torch.int64 else y.long()).contiguous()
+            self._mm = _pinned_copy(torch.stack(torch.aminmax(self.yl)), "prep.lab.mm")
+
+    def after_first_sync(self):
+        if not self.dev_path:
+            return
+        lo, hi = int(self._mm[0]), int(self._mm[1])
+        R = hi - lo + 1
+        if R > _LUT_MAX:
+            self.dev_path = False
+            return
+        self.lo, self.R = lo, R
+        self.counts = torch.empty(R, dtype=torch.int32, device=self.dev)
+        native.hip().label_count(_stream(), self.yl.data_ptr(), self.n, lo, R,
+                                 self.counts.data_ptr())
+        self._counts = _pinned_copy(self.counts, "prep.lab.counts")
+
+    def finish(self):
+        """(classes, int32 device codes, root class counts)."""
+        if not self.dev_path:
+            classes, enc = self.fallback(self.y, self.n)
+            if torch.is_tensor(enc):
+                return classes, enc.to(self.dev).to(torch.int32).contiguous(), None
+            root = np.bincount(enc, minlength=len(classes)).astype(np.int64)
+            d = torch.from_numpy(np.ascontiguousarray(enc, np.int32)).to(self.dev)
+            return classes, d, root
+        counts = np.array(self._counts, dtype=np.int64)
+        present = counts > 0
+        idx = np.nonzero(present)[0]
+        classes = (idx + self.lo).astype(_np_dtype(self.y.dtype))
+        if self.lo == 0 and present.all():
+            enc = self.yl.to(torch.int32)
+        else:
+            (d_lut,) = _uploader(self.dev)(np.cumsum(present) - 1)
+            enc = torch.empty(self.n, dtype=torch.int32, device=self.dev)
+            native.hip().label_encode(_stream(), self.yl.data_ptr(), self.n, self.lo,
+                                      d_lut.data_ptr(), enc.data_ptr())
+        return classes, enc, counts[present]
+
+
+class _Targets:
+    """Regression targets as fixed-point int64 (exponent chosen from max |y|)."""
+
+    def __init__(self, y, n, dev, encode_fallback, exponent):
+        self.y, self.n, self.dev = y, n, dev
+        self.fallback, self.exponent = encode_fallback, exponent
+        self.dev_path = torch.is_tensor(y) and y.is_cuda and y.dim() == 1 and y.shape[0] == n
+        if self.dev_path and n > 0:
+            self.yd = y.double()
+            st = torch.stack([self.yd.abs().max(), torch.isfinite(self.yd).all().double()])
+            self._st = _pinned_copy(st, "prep.reg.st")
+        elif self.dev_path:
+            self.dev_path = False
+
+    def after_first_sync(self):
+        if not self.dev_path:
+            return
+        if not self._st[1]:
+            raise ValueError("Input y contains NaN or infinity.")
+        self.e = self.exponent(float(self._st[0]), self.n)
+        scale = torch.tensor(float(self.e), dtype=torch.float64, device=self.dev)
+        self.yi = torch.round(torch.ldexp(self.yd, scale)).long()
+        mn, mx = torch.aminmax(self.yi)
+        self._root = _pinned_copy(torch.stack([self.yi.sum(), mn, mx]), "prep.reg.root")
+
+    def finish(self):
+        """(int64 device targets, exponent, root {count, sum, min, max})."""
+        if not self.dev_path:
+            yi, e = self.fallback(self.y, self.n)
+            if torch.is_tensor(yi):
+                return yi.to(self.dev).contiguous(), e, None
+            root = None
+            if yi.size:
+                root = np.array([yi.size, int(yi.sum()), int(yi.min()), int(yi.max())], np.int64)
+            return torch.from_numpy(np.ascontiguousarray(yi)).to(self.dev), e, root
+        r = np.array(self._root, dtype=np.int64)
+        return self.yi.contiguous(), self.e, np.array([self.n, r[0], r[1], r[2]], np.int64)
+
+
+def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
+            encode_targets, exponent) -> Prepared:
+    """Bin ``Xd`` (device, fp32/fp64) and encode ``y`` with two host syncs.
+
+    ``encode_labels`` / ``encode_targets`` are the host encoders of
+    ``core/fit.py``, used for host arrays and unusual label dtypes.
+    """
+    n = Xd.shape[0]
+    dev = Xd.device
+    stream = torch.cuda.current_stream(dev)
+    lab = (_Targets(y, n, dev, encode_targets, exponent) if regression
+           else _Labels(y, n, dev, encode_labels))
+    binning = DeviceBinning(Xd, max_bins)
+    stream.synchronize()  # sync 1: edge table + label range / target scale
+    binning.launch_bin()
+    lab.after_first_sync()
+    stream.synchronize()  # sync 2: bin flags + class counts / target root stats
+    mapper, codes_rm, codes_fm, nb = binning.finish()
+    if regression:
+        yenc, y_exp, root = lab.finish()
+        classes = None
+    else:
+        classes, yenc, root = lab.finish()
+        y_exp = 0
+    return Prepared(mapper=mapper, codes_rm=codes_rm, codes_fm=codes_fm, nbins=nb, y=yenc,
+                    classes=classes, y_exp=y_exp, root=root, d_edges64=binning.d_edges64)

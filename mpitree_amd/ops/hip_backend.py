@@ -72,56 +72,121 @@ class _Uploader:
         return outs
 
 
-def gpu_bin_features(X: torch.Tensor, max_bins=256, sample_rows: int | None = None):
-    """Bin a device feature matrix; returns (BinMapper, codes_rm, codes_fm, nbins_dev).
+_workspaces: dict = {}
 
-    Edges come from a deterministic strided row sample processed on the device
-    (binning.hip ``edges_kernel``): features whose sample has at most
-    ``max_bins`` distinct values are binned in exact mode and verified by the
-    bin kernel, which falls back to the full column when the sample missed a
-    value. The bin kernel also rejects non-finite input. Two small D2H reads
-    (edges + the verification flags) are the only host synchronisations.
+
+def _workspace(device, name: str, nbytes: int) -> torch.Tensor:
+    """A reusable uint8 device scratch buffer per (device, name), grown
+    geometrically: steady-state fits of one shape allocate nothing. Reuse is
+    safe because every user enqueues on the one current stream."""
+    key = (str(device), name)
+    buf = _workspaces.get(key)
+    if buf is None or buf.numel() < nbytes:
+        cap = max(int(nbytes), int(1.25 * buf.numel()) if buf is not None else 0, 256)
+        buf = _workspaces[key] = torch.empty(cap, dtype=torch.uint8, device=device)
+    return buf
+
+
+_uploaders: dict = {}
+
+
+def _uploader(device) -> _Uploader:
+    """One staging ring per device, shared by every fit (pinned allocations
+    are expensive; the ring's events keep reuse safe)."""
+    key = str(device)
+    u = _uploaders.get(key)
+    if u is None:
+        u = _uploaders[key] = _Uploader(device)
+    return u
+
+
+class DeviceBinning:
+    """Bin a device feature matrix in three host steps around two syncs.
+
+    ``__init__`` enqueues the edges kernel (binning.hip ``edges_kernel``: a
+    deterministic strided row sample per feature, exact mode when the sample
+    has at most ``max_bins`` distinct values) and one D2H of the packed edge
+    table. After the caller synchronises, :meth:`launch_bin` enqueues the bin
+    kernel and the D2H of its flags, and builds the host ``BinMapper`` while
+    the kernel runs. After the next sync :meth:`finish` rejects non-finite
+    input and, when an exact-mode sample missed a value, re-bins the affected
+    features from their full columns. Callers batch their own small reads
+    into the same two syncs (``core/fit.py``); :func:`gpu_bin_features` is
+    the stand-alone form.
     """
-    hip = native.hip()
-    n, F = X.shape
-    dev = X.device
-    x64 = X.dtype == torch.float64
-    limit = MAX_BINS_LIMIT if max_bins is None else int(max_bins)
-    s = min(n, int(sample_rows or hip.edges_sample_rows(x64)))
-    limit_eff = limit
-    edges = torch.empty((F, limit_eff), dtype=X.dtype, device=dev)
-    nb = torch.empty(F, dtype=torch.int32, device=dev)
-    exact = torch.empty(F, dtype=torch.uint8, device=dev)
-    hip.edges(_stream(), X.data_ptr(), x64, n, F, s, limit_eff, edges.data_ptr(), nb.data_ptr(),
-              exact.data_ptr())
-    # one packed D2H: edges (fp64), bin counts, exact flags
-    pack = torch.cat([edges.double().reshape(-1), nb.double(), exact.double()])
-    host = pack.cpu().numpy()
-    host_edges = host[: F * limit_eff].reshape(F, limit_eff).copy()
-    host_nb = host[F * limit_eff : F * limit_eff + F].astype(np.int64)
-    host_exact = host[F * limit_eff + F :].astype(bool)
 
-    def run_bin(edges_t, nb_t, exact_t, bmax):
-        cb = 1 if bmax <= 256 else 2
+    def __init__(self, X: torch.Tensor, max_bins=256, sample_rows: int | None = None):
+        hip = self.hip = native.hip()
+        self.X = X
+        n, F = self.n, self.F = X.shape
+        dev = self.dev = X.device
+        self.x64 = X.dtype == torch.float64
+        self.limit = MAX_BINS_LIMIT if max_bins is None else int(max_bins)
+        s = min(n, int(sample_rows or hip.edges_sample_rows(self.x64)))
+        L = self.limit
+        self.edges = torch.empty((F, L), dtype=X.dtype, device=dev)
+        self.nb = torch.empty(F, dtype=torch.int32, device=dev)
+        self.exact = torch.empty(F, dtype=torch.uint8, device=dev)
+        # fp64 [F*L edges | F counts | F exact flags]: the host's copy in one D2H
+        self.pack = torch.empty(F * L + 2 * F, dtype=torch.float64, device=dev)
+        hip.edges(_stream(), X.data_ptr(), self.x64, n, F, s, L, self.edges.data_ptr(),
+                  self.nb.data_ptr(), self.exact.data_ptr(), pack=self.pack.data_ptr())
+        self._host_pack = _pinned_copy(self.pack, "bin.pack")
+        # the code buffers' shapes are known up front for <= 256 bins
+        self._codes = self._alloc_codes(1) if L <= 256 else None
+
+    def _alloc_codes(self, cb):
+        n, F = self.n, self.F
         ctype = torch.uint8 if cb == 1 else torch.int16
         row_elems = ((F * cb + 3) // 4) * 4 // cb
-        codes_rm = torch.empty((n, row_elems), dtype=ctype, device=dev)
-        codes_fm = torch.empty((F, n), dtype=ctype, device=dev)
-        flags = torch.zeros(F, dtype=torch.int32, device=dev)
-        et = edges_t[:, :bmax].contiguous()
-        hip.bin(_stream(), X.data_ptr(), x64, n, F, et.data_ptr(), bmax, nb_t.data_ptr(),
-                exact_t.contiguous().data_ptr(), codes_rm.data_ptr(), row_elems,
-                codes_fm.data_ptr(), cb, flags.data_ptr())
+        codes_rm = torch.empty((n, row_elems), dtype=ctype, device=self.dev)
+        codes_fm = torch.empty((F, n), dtype=ctype, device=self.dev)
+        flags = torch.zeros(self.F, dtype=torch.int32, device=self.dev)
+        return cb, row_elems, codes_rm, codes_fm, flags
+
+    def _run_bin(self, edges_t, nb_t, exact_t, bmax):
+        cb = 1 if bmax <= 256 else 2
+        if self._codes is None or self._codes[0] != cb:
+            self._codes = self._alloc_codes(cb)
+        cb, row_elems, codes_rm, codes_fm, flags = self._codes
+        self._codes = None  # buffers belong to this pass
+        self.hip.bin(_stream(), self.X.data_ptr(), self.x64, self.n, self.F, edges_t.data_ptr(),
+                     bmax, nb_t.data_ptr(), exact_t.data_ptr(), codes_rm.data_ptr(), row_elems,
+                     codes_fm.data_ptr(), cb, flags.data_ptr(), estride=int(edges_t.stride(0)))
         return codes_rm, codes_fm, flags
 
-    bmax = int(max(1, host_nb.max())) if F else 1
-    codes_rm, codes_fm, flags = run_bin(edges, nb, exact, bmax)
-    fl = flags.cpu().numpy()
-    if (fl & 2).any():
-        raise ValueError("Input X contains NaN or infinity.")
-    if (fl & 1).any():
-        # the sample missed values of an "exact" feature: use the full column
-        for f in np.nonzero(fl & 1)[0]:
+    def launch_bin(self):
+        """Enqueue the bin kernel (after a sync covering ``__init__``'s copy)."""
+        F, L = self.F, self.limit
+        host = self._host_pack
+        self.host_edges = host[: F * L].reshape(F, L).copy()
+        self.host_nb = host[F * L : F * L + F].astype(np.int64)
+        self.host_exact = host[F * L + F :].astype(bool)
+        self.bmax = int(max(1, self.host_nb.max())) if F else 1
+        self.codes_rm, self.codes_fm, flags = self._run_bin(self.edges, self.nb, self.exact,
+                                                            self.bmax)
+        self._host_flags = _pinned_copy(flags, "bin.flags")
+        he, hn = self.host_edges, self.host_nb
+        self.mapper = BinMapper(edges=[he[f, : hn[f]].copy() for f in range(F)],
+                                exact=self.host_exact.copy(), max_bins=L)
+
+    def finish(self):
+        """(mapper, codes_rm, codes_fm, nbins_dev) after a sync covering the flags copy."""
+        fl = np.array(self._host_flags)
+        if (fl & 2).any():
+            raise ValueError("Input X contains NaN or infinity.")
+        if (fl & 1).any():
+            self._refit_missed(np.nonzero(fl & 1)[0])
+        self.d_edges64 = None if (fl & 1).any() else self.pack[: self.F * self.limit].view(
+            self.F, self.limit)
+        return self.mapper, self.codes_rm, self.codes_fm, self.nb
+
+    def _refit_missed(self, feats):
+        """The sample missed values of an "exact" feature: use the full column."""
+        X, dev, n, limit = self.X, self.dev, self.n, self.limit
+        edges, host_edges = self.edges, self.host_edges
+        host_nb, host_exact = self.host_nb, self.host_exact
+        for f in feats:
             col = X[:, f]
             u = torch.unique(torch.where(col == 0, torch.zeros_like(col), col))
             if u.numel() <= limit:
@@ -134,26 +199,40 @@ def gpu_bin_features(X: torch.Tensor, max_bins=256, sample_rows: int | None = No
                 e = torch.unique(srtc[qi])
                 host_exact[f] = False
             if e.numel() > edges.shape[1]:
-                wider = torch.full((F, e.numel()), float("inf"), dtype=X.dtype, device=dev)
+                wider = torch.full((self.F, e.numel()), float("inf"), dtype=X.dtype, device=dev)
                 wider[:, : edges.shape[1]] = edges
                 edges = wider
                 host_edges = np.concatenate(
-                    [host_edges, np.full((F, e.numel() - host_edges.shape[1]), np.inf)], 1)
+                    [host_edges, np.full((self.F, e.numel() - host_edges.shape[1]), np.inf)], 1)
             edges[f].fill_(float("inf"))
             edges[f, : e.numel()] = e
             host_edges[f] = np.inf
             host_edges[f, : e.numel()] = e.double().cpu().numpy()
             host_nb[f] = e.numel()
-        nb = torch.from_numpy(host_nb.astype(np.int32)).to(dev)
+        self.nb = torch.from_numpy(host_nb.astype(np.int32)).to(dev)
         exact = torch.from_numpy(host_exact.astype(np.uint8)).to(dev)
         bmax = int(max(1, host_nb.max()))
-        codes_rm, codes_fm, flags = run_bin(edges, nb, exact, bmax)
-    mapper = BinMapper(
-        edges=[host_edges[f, : host_nb[f]].copy() for f in range(F)],
-        exact=host_exact.astype(bool),
-        max_bins=limit,
-    )
-    return mapper, codes_rm, codes_fm, nb
+        self.codes_rm, self.codes_fm, flags = self._run_bin(edges, self.nb, exact, bmax)
+        if (flags.cpu().numpy() & 2).any():  # pragma: no cover - caught by the first pass
+            raise ValueError("Input X contains NaN or infinity.")
+        self.mapper = BinMapper(
+            edges=[host_edges[f, : host_nb[f]].copy() for f in range(self.F)],
+            exact=host_exact.astype(bool),
+            max_bins=limit,
+        )
+
+
+def gpu_bin_features(X: torch.Tensor, max_bins=256, sample_rows: int | None = None):
+    """Bin a device feature matrix; returns (BinMapper, codes_rm, codes_fm, nbins_dev).
+
+    Stand-alone form of :class:`DeviceBinning` (two host synchronisations:
+    the packed edge table and the bin kernel's verification flags).
+    """
+    job = DeviceBinning(X, max_bins, sample_rows)
+    torch.cuda.current_stream(X.device).synchronize()
+    job.launch_bin()
+    torch.cuda.current_stream(X.device).synchronize()
+    return job.finish()
 
 
 XTAB_N = 1 << 16
@@ -209,7 +288,7 @@ class HipBackend:
         self.hip = native.hip()
         self.device = torch.device(device) if device is not None else torch.device(
             "cuda", torch.cuda.current_device())
-        self.up = _Uploader(self.device)
+        self.up = _uploader(self.device)
         self.timing = False
 
     # ---------------------------------------------------------------- setup
@@ -375,10 +454,14 @@ class HipBackend:
         positions); ``assemble_positions`` removes the holes on the device."""
         if P >= 2**31 - 1:
             raise ValueError("position space exceeds 2^31 (more than ~1e9 rows)")
-        self.P = int(P)
-        self.pos_rec = torch.zeros((self.P, 6), dtype=torch.int32, device=self.device)
+        self.P = P = int(P)
+        # reused device scratch: only the records need clearing (n = 0 marks a hole)
+        rec = _workspace(self.device, "pos_rec", P * 24)
+        self.pos_rec = rec[: P * 24].view(torch.int32).view(P, 6)
+        self.pos_rec.zero_()
         dt = torch.int64 if self.reg else torch.int32
-        self.pos_st = torch.empty((self.P, self.C), dtype=dt, device=self.device)
+        sb = P * self.C * (8 if self.reg else 4)
+        self.pos_st = _workspace(self.device, "pos_st", sb)[:sb].view(dt).view(P, self.C)
 
     def put_positions(self, pos, feature, tbin, lpos, rpos, depth, nsamp, stats):
         """Write host-grown (level-wise) nodes into the position space."""
@@ -390,9 +473,13 @@ class HipBackend:
         self.pos_rec.index_copy_(0, d_pos, d_rec.reshape(-1, 6).to(torch.int32))
         self.pos_st.index_copy_(0, d_pos, d_st.reshape(-1, self.C).to(self.pos_st.dtype))
 
-    def assemble_positions(self, edges: np.ndarray, crit: int, y_exp: int = 0) -> dict:
+    def assemble_positions(self, edges, crit: int, y_exp: int = 0, d_edges=None) -> dict:
         """Compact the position space into pre-ordered tree columns (numpy views
-        of one pinned host buffer, filled by a single D2H copy)."""
+        of one pinned host buffer). ``d_edges``: the device fp64 edge table
+        ``[F, W]`` (any row stride); otherwise ``edges`` (host ``[F, W]``) is
+        uploaded. Rank -> emit run back to back (the emit kernel lays the
+        columns out from the device node count), then two small host waits:
+        the node count, and the single D2H of the columns."""
         P, C = self.P, self.C
         hip = self.hip
         done = getattr(self, "_side_done", None)
@@ -400,49 +487,51 @@ class HipBackend:
             torch.cuda.current_stream(self.device).wait_event(done)
             self._side_done = None
         s = _stream()
+        if d_edges is None:
+            d_edges = torch.from_numpy(np.ascontiguousarray(edges, np.float64)).to(self.device)
         tiles = hip.asm_tiles(P)
-        tile = torch.empty(max(tiles, 1), dtype=torch.int32, device=self.device)
-        total = torch.zeros(1, dtype=torch.int64, device=self.device)
-        rank = torch.empty(P, dtype=torch.int32, device=self.device)
-        hip.asm_rank(s, self.pos_rec.data_ptr(), P, tile.data_ptr(), total.data_ptr(),
-                     rank.data_ptr())
-        N = int(total.item())
-        # packed output: 8-byte columns first, then 4-byte columns (alignment)
+        bpn = int(hip.asm_node_bytes(C, self.reg))
+        al = lambda x: (x + 255) // 256 * 256  # noqa: E731
+        o_total = al(max(tiles, 1) * 4)
+        o_rank = o_total + 256
+        o_out = o_rank + al(P * 4)
+        ws = _workspace(self.device, "asm", o_out + P * bpn)
+        base = ws.data_ptr()
+        total = ws[o_total : o_total + 8].view(torch.int64)
+        hip.asm_rank(s, self.pos_rec.data_ptr(), P, base, base + o_total, base + o_rank)
+        hip.asm_emit(s, self.pos_rec.data_ptr(), self.pos_st.data_ptr(), self.reg, P, C,
+                     base + o_rank, d_edges.data_ptr(), int(d_edges.stride(0)),
+                     self.xtab.data_ptr(), XTAB_N, int(crit), int(y_exp), base + o_total,
+                     base + o_out)
+        h_total = _pinned_copy(total, "asm.total")
+        torch.cuda.current_stream(self.device).synchronize()
+        N = int(h_total[0])
+        host = torch.empty(max(N * bpn, 8), dtype=torch.uint8, pin_memory=True)
+        host[: N * bpn].copy_(ws[o_out : o_out + N * bpn], non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
         cols8 = [("nsamp", torch.int64, 1), ("stats", torch.int64, C),
-                 ("threshold", torch.float64, 1), ("term", torch.float64, 1),
-                 ("impurity", torch.float64, 1)]
+                 ("threshold", torch.float64, 1), ("impurity", torch.float64, 1)]
         if self.reg:
             cols8.append(("value", torch.float64, 1))
         cols4 = [(k, torch.int32, 1) for k in ("feature", "bin", "left", "right", "depth")]
-        layout, off = [], 0
+        out, o = {}, 0
         for name, dt, w in cols8 + cols4:
-            nbytes = N * w * (8 if dt in (torch.int64, torch.float64) else 4)
-            layout.append((name, dt, w, off, nbytes))
-            off += nbytes
-        dev = torch.empty(max(off, 8), dtype=torch.uint8, device=self.device)
-        ptrs = {name: dev.data_ptr() + o for name, dt, w, o, nb in layout}
-        d_edges = torch.from_numpy(np.ascontiguousarray(edges, np.float64)).to(self.device)
-        hip.asm_emit(s, self.pos_rec.data_ptr(), self.pos_st.data_ptr(), self.reg, P, C,
-                     rank.data_ptr(), d_edges.data_ptr(), int(edges.shape[1]),
-                     self.xtab.data_ptr(), XTAB_N, int(crit), int(y_exp), ptrs)
-        host = torch.empty(max(off, 8), dtype=torch.uint8, pin_memory=True)
-        host.copy_(dev, non_blocking=True)
-        torch.cuda.current_stream(self.device).synchronize()
-        out = {}
-        for name, dt, w, o, nb in layout:
+            nb = N * w * (8 if dt in (torch.int64, torch.float64) else 4)
             t = host[o : o + nb].view(dt)
             out[name] = (t.view(N, w) if w > 1 else t).numpy()
+            o += nb
         self.pos_rec = self.pos_st = None
         return out
 
-    def launch_finisher(self, d_jobs, J: int, job_rows: int, params, rec, cnt):
+    def launch_finisher(self, d_jobs, J: int, job_rows: int, params, rec, cnt, counter=None):
         """Launch the block + wave finisher kernels on ``J`` device jobs
         (int64 [J][5 + C] = {start, count, depth, root position, buffer, counts},
         largest first for load balance) writing into position space rec/cnt."""
         if J <= 0:
             return
         C = self.C
-        counter = torch.zeros(4, dtype=torch.int32, device=self.device)
+        if counter is None:  # four int32 work cursors, zero at launch
+            counter = torch.zeros(4, dtype=torch.int32, device=self.device)
         if self.reg:
             self._launch_finisher_reg(d_jobs, J, job_rows, params, rec, cnt, counter)
             return

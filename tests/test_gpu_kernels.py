@@ -159,7 +159,6 @@ def test_gpu_device_assembly_matches_host(monkeypatch, regression):
     if regression:
         assert np.array_equal(dev.value, host.value)
         assert np.array_equal(dev.meta["sum_fixed"], host.meta["sum_fixed"])
-    assert np.array_equal(dev.meta["term"], host.meta["term"])
 
 
 def test_gpu_edges_match_host_mapper():
@@ -182,6 +181,68 @@ def test_gpu_edges_match_host_mapper():
         assert bool(mapper.exact[f]) == bool(host.exact[f]), f
         assert np.array_equal(mapper.edges[f], host.edges[f]), f
     assert np.array_equal(codes_fm.cpu().numpy().T[:, :5], host.transform(X))
+
+
+@pytest.mark.parametrize("labels", ["int64", "int32-gaps", "negative", "float", "host"])
+def test_gpu_label_prepare_paths(labels):
+    """Device label encoding (range count + LUT, gpu_prepare) == host np.unique,
+    and the tree equals the one grown from host labels."""
+    from mpitree_amd.core.fit import fit_tree
+
+    rng = np.random.default_rng(11)
+    n = 20000
+    X = rng.integers(0, 30, size=(n, 5)).astype(np.float32)
+    base = (X[:, 0] + rng.integers(0, 9, size=n)) % 3
+    yh = {"int64": base, "int32-gaps": np.array([3, 7, 100])[base.astype(int)],
+          "negative": base.astype(int) - 5, "float": base * 0.5, "host": base}[labels]
+    if labels == "int32-gaps":
+        yh = yh.astype(np.int32)
+    yd = yh if labels == "host" else torch.from_numpy(np.ascontiguousarray(yh)).cuda()
+    kw = dict(regression=False, criterion=0, max_depth=None, min_samples_split=2,
+              device="cuda")
+    r_dev = fit_tree(torch.from_numpy(X).cuda(), yd, **kw)
+    r_cpu = fit_tree(X, yh, **{**kw, "device": "cpu"})
+    assert np.array_equal(r_dev.classes, np.unique(yh))
+    assert r_dev.classes.dtype == np.unique(yh).dtype
+    assert r_dev.arrays.equal(r_cpu.arrays, check_impurity=False)
+
+
+def test_gpu_regression_prepare_device_targets():
+    """Fixed-point targets and root stats computed on the device == host path."""
+    from mpitree_amd.core.fit import fit_tree
+
+    rng = np.random.default_rng(12)
+    n = 30000
+    X = rng.integers(0, 40, size=(n, 6)).astype(np.float32)
+    y = X[:, 0] * 0.25 + rng.normal(size=n)
+    kw = dict(regression=True, criterion=2, max_depth=None, min_samples_split=2, device="cuda")
+    a = fit_tree(torch.from_numpy(X).cuda(), torch.from_numpy(y).cuda(), **kw)
+    b = fit_tree(X, y, **kw)
+    assert a.y_scale_exp == b.y_scale_exp
+    assert a.arrays.equal(b.arrays, check_impurity=False)
+    assert np.array_equal(a.arrays.value, b.arrays.value)
+    with pytest.raises(ValueError, match="NaN or infinity"):
+        yb = torch.from_numpy(y).cuda()
+        yb[5] = float("inf")
+        fit_tree(torch.from_numpy(X).cuda(), yb, **kw)
+
+
+def test_gpu_job_sort_kernel_matches_torch_order(monkeypatch):
+    """The one-workgroup job sort and the torch argsort fallback give the same tree."""
+    from mpitree_amd.core.fit import fit_tree
+    from mpitree_amd.ops import native
+
+    rng = np.random.default_rng(13)
+    n = 50000
+    X = rng.integers(0, 50, size=(n, 7)).astype(np.float32)
+    y = (X[:, 1] + rng.integers(0, 20, size=n)) % 2
+    kw = dict(regression=False, criterion=1, max_depth=None, min_samples_split=2,
+              device="cuda", finisher_rows=300)
+    a = fit_tree(X, y, **kw)
+    assert a.stats["finisher_subtrees"] > 1
+    monkeypatch.setattr(native.hip(), "job_sort_max", lambda: 0)
+    b = fit_tree(X, y, **kw)
+    assert a.arrays.equal(b.arrays)
 
 
 def test_gpu_rejects_nonfinite_tensor():
@@ -210,7 +271,7 @@ def test_gpu_device_loop_matches_host_loop(monkeypatch, seed, max_depth):
     r2 = fit_tree(X, y, **kw)
     assert r2.engine == "hip-levelwise"
     assert r1.arrays.equal(r2.arrays)
-    assert np.array_equal(r1.arrays.meta["term"], r2.arrays.meta["term"])
+    assert np.array_equal(r1.arrays.impurity, r2.arrays.impurity)
 
 
 def test_gpu_profile_mode_level_events(monkeypatch):
