@@ -1,0 +1,22 @@
+"""One flagship fit after a warmup -- a small trace for PMC counter runs.
+
+rocprofv3 --pmc SQ_INSTS_VALU ... --kernel-trace --output-format csv -- python3 bench/pmc_fit.py
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from mpitree_amd import DecisionTreeClassifier  # noqa: E402
+from mpitree_amd.utils.datasets import make_classification  # noqa: E402
+
+n = int(os.environ.get("PMC_N", 1_000_000))
+F = int(os.environ.get("PMC_F", 64))
+X, y = make_classification(n, F, seed=0, device=torch.device("cuda", 0))
+est = DecisionTreeClassifier(device="cuda")
+est.fit(X, y)
+torch.cuda.synchronize()
+est.fit(X, y)
+torch.cuda.synchronize()
+print(est.fit_stats_.get("node_count"))

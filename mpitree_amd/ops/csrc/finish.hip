@@ -913,198 +913,309 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
 // Tiny subtrees, C <= 2: presorted per-feature lane orders.
 //
 // A child's rows are a subset of its parent's, so the order of the subtree's
-// rows by each feature's code is computed once per tiny subtree (the 8-ballot
-// radix rank of finish_tiny_kernel, plus the lane's position among equal
-// codes) and stored in LDS. At every node of the subtree, sorted position k
-// holds lane order_f[k]; one packed DPP prefix sum of {in node, in node and
-// class 1} along the sorted order gives both left counts of the split "code
-// <= code of position k", which is a valid split where k is the last node row
-// of its code. The wave keeps each lane's best (gain, feature, cost, code) and
-// reduces once per node -- the same decision rule as the per-node kernel.
+// rows by each feature's code is computed once per tiny subtree (an 8-ballot
+// MSB-first radix rank, stable by lane) and stored in LDS as 16-bit entries
+// srt[f][k] = {code : 8, run end : 1, -, lane : 6} for sorted position k.
+// At every node of the subtree lane k reads srt[f][k] (64 consecutive
+// halfwords: conflict-free); one packed DPP prefix sum of {in node, in node and
+// class 1} along the sorted order gives both left counts of the split "code <=
+// code at k". Splits are scored at the ends of equal-code runs of the subtree
+// order: a run holding node rows yields exactly the reference candidate (the
+// last node row of that code); a run without node rows repeats the previous
+// partition with a larger code and never wins the (gain, feature, cost, code)
+// order. Costs come from a per-launch table H[a][b] = T(a) - (T(a-b) + T(b))
+// (entropy) or gini_term(a, (a-b)^2 + b^2), a <= 64 -- two lookups and one add
+// per candidate, bitwise equal to the six-lookup form. Two features are scanned
+// per iteration (independent DPP chains); the wave reduces once per node.
 //
-// LDS per wave: codes [64][cw] words (cw = ceil(F/4) | 1) + order [F][64] bytes.
+// LDS per wave: srt [F][64] halfwords + 64 flag bytes (tiny_wave_bytes); per
+// workgroup: the H table (tiny_h_entries doubles).
+constexpr int kTinyH = (kTinyRows + 1) * (kTinyRows + 2) / 2;  // triangular a <= 64, b <= a
+__device__ __forceinline__ int tiny_h_idx(int a, int b) { return ((a * (a + 1)) >> 1) + b; }
+
+// H table for one criterion (entropy from the shared x*log2(x) values).
+__device__ __forceinline__ void tiny_fill_h(double* __restrict__ H, const double* __restrict__ xtab,
+                                            int crit) {
+  for (int i = threadIdx.x; i < kTinyH; i += blockDim.x) {
+    int a = 0;
+    while (tiny_h_idx(a + 1, 0) <= i) ++a;
+    const int b = i - tiny_h_idx(a, 0);
+    H[i] = crit == kEntropy ? xtab[a] - (xtab[a - b] + xtab[b])
+                            : gini_term(a, (int64_t)(a - b) * (a - b) + (int64_t)b * b);
+  }
+}
+
+// Lane l's value from lane l ^ J (DPP within rows, swizzle, bpermute across halves).
+template <int J>
+__device__ __forceinline__ uint32_t lane_xor_u32(uint32_t v) {
+  if constexpr (J == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // quad [1,0,3,2]
+  } else if constexpr (J == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // quad [2,3,0,1]
+  } else if constexpr (J == 4) {
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x101F);  // xor 4 (bit mode)
+  } else if constexpr (J == 8) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  } else if constexpr (J == 16) {
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x401F);  // xor 16
+  } else {
+    return (uint32_t)__shfl_xor((int)v, 32, kWave);
+  }
+}
+
+typedef unsigned short mt_u16x2 __attribute__((ext_vector_type(2)));
+
+template <int K, int J>
+__device__ __forceinline__ uint32_t bitonic_step_pk(uint32_t v, int lane) {
+  const uint32_t p = lane_xor_u32<J>(v);
+  const mt_u16x2 a = __builtin_bit_cast(mt_u16x2, v), b = __builtin_bit_cast(mt_u16x2, p);
+  const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(a, b));
+  const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(a, b));
+  const bool keep_min = ((lane & K) == 0) == ((lane & J) == 0);
+  return keep_min ? lo : hi;
+}
+
+// Ascending bitonic sort of 64 lanes, two independent 16-bit keys per lane.
+__device__ __forceinline__ uint32_t bitonic64_pk_u16(uint32_t v, int lane) {
+  v = bitonic_step_pk<2, 1>(v, lane);
+  v = bitonic_step_pk<4, 2>(v, lane);
+  v = bitonic_step_pk<4, 1>(v, lane);
+  v = bitonic_step_pk<8, 4>(v, lane);
+  v = bitonic_step_pk<8, 2>(v, lane);
+  v = bitonic_step_pk<8, 1>(v, lane);
+  v = bitonic_step_pk<16, 8>(v, lane);
+  v = bitonic_step_pk<16, 4>(v, lane);
+  v = bitonic_step_pk<16, 2>(v, lane);
+  v = bitonic_step_pk<16, 1>(v, lane);
+  v = bitonic_step_pk<32, 16>(v, lane);
+  v = bitonic_step_pk<32, 8>(v, lane);
+  v = bitonic_step_pk<32, 4>(v, lane);
+  v = bitonic_step_pk<32, 2>(v, lane);
+  v = bitonic_step_pk<32, 1>(v, lane);
+  v = bitonic_step_pk<64, 32>(v, lane);
+  v = bitonic_step_pk<64, 16>(v, lane);
+  v = bitonic_step_pk<64, 8>(v, lane);
+  v = bitonic_step_pk<64, 4>(v, lane);
+  v = bitonic_step_pk<64, 2>(v, lane);
+  v = bitonic_step_pk<64, 1>(v, lane);
+  return v;
+}
+
+__host__ __device__ inline int tiny_wave_bytes(int F) { return F * kWave * 2 + kWave; }
+
+struct TinyOut {
+  int32_t* node_i32;
+  int32_t* node_cnt;
+};
+
+__device__ __forceinline__ void tiny_sorted_subtree(
+    const uint32_t* __restrict__ codes_rm, int64_t row_words, const uint32_t* __restrict__ src,
+    const int32_t* __restrict__ y, FinRowLab rl, int64_t start, int m, int depth0,
+    int64_t root_slot, int F, int C, int crit, int max_depth, int64_t mss, int64_t msl,
+    const double* __restrict__ H, const uint32_t* __restrict__ Hrow, uint16_t* __restrict__ srt,
+    uint8_t* __restrict__ flag,
+    unsigned long long* __restrict__ st_mask, int32_t* __restrict__ st_dep,
+    int32_t* __restrict__ st_slot, TinyOut out) {
+  const int lane = lane_id();
+  const unsigned long long below = (1ull << lane) - 1ull;
+  const bool act = lane < m;
+  uint32_t row = 0;
+  int lab = 0;
+  if (act) {
+    const uint32_t ent = src[start + lane];
+    row = rl.shift ? (ent & rl.mask) : ent;
+    lab = rl.shift ? (int)(ent >> rl.shift) : y[row];
+  }
+  const unsigned long long R = m == 64 ? ~0ull : ((1ull << m) - 1ull);
+  const unsigned long long cm1 = C > 1 ? __ballot(act && lab == 1) : 0ull;
+  const int mslw = (int)(msl < 65 ? msl : 65);
+  // ---- presort: srt[f][position] = {code, run end, lane}. Keys {code : 8,
+  // lane : 8} are unique, so a bitonic network over the wave sorts them stably;
+  // two features share a 32-bit register (packed 16-bit min / max).
+  const uint32_t* rowp = codes_rm + (int64_t)row * row_words;
+  const int nwords = (F + 3) >> 2;
+  for (int w = 0; w < nwords; ++w) {
+    const uint32_t word = act ? rowp[w] : 0u;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int f = w * 4 + 2 * h;
+      if (f >= F) break;
+      const uint32_t ka = ((word >> (16 * h)) & 0xffu) << 8 | (uint32_t)lane;
+      const uint32_t kb = ((word >> (16 * h + 8)) & 0xffu) << 8 | (uint32_t)lane;
+      uint32_t v = act ? (ka | (kb << 16)) : 0xffffffffu;
+      v = bitonic64_pk_u16(v, lane);
+      const uint32_t nv = (uint32_t)__shfl_down((int)v, 1, kWave);
+      const bool endl = lane == m - 1;
+      const uint32_t ea = (endl || ((nv >> 8) & 0xffu) != ((v >> 8) & 0xffu)) ? 0x80u : 0u;
+      const uint32_t eb = (endl || (nv >> 24) != (v >> 24)) ? 0x80u : 0u;
+      // positions past the subtree: lane 63 (never a row there, so no node
+      // bits), no run end -- the scan loop needs no activity test
+      srt[f * kWave + lane] = act ? (uint16_t)((v & 0xffffu) | ea) : (uint16_t)0xff3fu;
+      if (f + 1 < F) srt[(f + 1) * kWave + lane] = act ? (uint16_t)((v >> 16) | eb) : (uint16_t)0xff3fu;
+    }
+  }
+  if (lane == 0) {
+    st_mask[0] = R;
+    st_dep[0] = depth0;
+    st_slot[0] = (int32_t)root_slot;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  int sp = 1;
+  while (sp > 0) {
+    --sp;
+    const unsigned long long M = st_mask[sp];
+    const int d = st_dep[sp];
+    const int64_t slot = st_slot[sp];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int mm = __popcll(M);
+    const int mc1 = __popcll(M & cm1);
+    const double pterm = H[tiny_h_idx(mm, mc1)];
+    double bg = -__builtin_inf(), bc = __builtin_inf();
+    int bf = 0x7fffffff;
+    uint32_t bb = 0xffffffffu;
+    // this lane's row in the node: {in : 8, in and class 1 : 8}, fetched per
+    // feature at sorted position k with one ds_bpermute from lane srt[f][k]
+    const bool lin = act && ((M >> lane) & 1ull);
+    const int nodebits = lin ? (1 | ((((cm1 >> lane) & 1ull) != 0ull) ? 0x100 : 0)) : 0;
+    // split cost at this lane's sorted position from the left counts (ml, l1)
+    const char* Hb = reinterpret_cast<const char*>(H);
+    // H[tri(a) + b] by byte offset; Hrow[a] = 8 tri(a) (an LDS lookup is cheaper
+    // than the multiply on the VALU-bound path)
+    auto hval = [&](int a, int b) -> double {
+      return *reinterpret_cast<const double*>(Hb + Hrow[a] + ((uint32_t)b << 3));
+    };
+    auto cost_of = [&](uint32_t v, int ml, int l1) -> double {
+      const int mr = mm - ml, r1 = mc1 - l1;
+      const bool ok = (v & 0x80u) && ml >= mslw && mr >= mslw;
+      const double c = hval(ml, l1) + hval(mr, r1);
+      return ok ? c : __builtin_inf();
+    };
+    auto take = [&](int f, double cost, uint32_t v) {
+      const double g = pterm - cost;
+      const bool better = g > bg;  // features ascend: strict > keeps the lowest
+      bg = better ? g : bg;
+      bf = better ? f : bf;
+      bc = better ? cost : bc;
+      bb = better ? (v >> 8) : bb;
+    };
+    // two features per DPP scan: {in, class 1} counts of feature a in the low
+    // 16 bits, of feature b in the high 16 (every field <= 64)
+    for (int f = 0; f < F; f += 2) {
+      const bool two = f + 1 < F;
+      const uint32_t va = srt[f * kWave + lane];
+      const uint32_t vb = two ? (uint32_t)srt[(f + 1) * kWave + lane] : 0u;
+      const uint32_t xa = (uint32_t)__shfl(nodebits, (int)(va & 0x3fu), kWave);
+      const uint32_t xb = (uint32_t)__shfl(nodebits, (int)(vb & 0x3fu), kWave);
+      const uint32_t incl = wave_incl_scan_dpp(xa | (xb << 16));
+      const double ca = cost_of(va, (int)(incl & 0xffu), (int)((incl >> 8) & 0xffu));
+      const double cb = cost_of(vb, (int)((incl >> 16) & 0xffu), (int)(incl >> 24));
+      take(f, ca, va);
+      if (two) take(f + 1, cb, vb);
+    }
+#pragma unroll
+    for (int dd = kWave / 2; dd > 0; dd >>= 1) {
+      const double og = __shfl_xor(bg, dd, kWave);
+      const int of = __shfl_xor(bf, dd, kWave);
+      const double oc = __shfl_xor(bc, dd, kWave);
+      const uint32_t ob = (uint32_t)__shfl_xor((int)bb, dd, kWave);
+      const bool tk =
+          og > bg || (og == bg && (of < bf || (of == bf && (oc < bc || (oc == bc && ob < bb)))));
+      if (tk) {
+        bg = og;
+        bf = of;
+        bc = oc;
+        bb = ob;
+      }
+    }
+    bf = __builtin_amdgcn_readfirstlane(bf);
+    bb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bb);
+    if (!(bg > -__builtin_inf()) || bf < 0) continue;  // leaf: the creation record stands
+    // left rows: sorted positions of feature bf with code <= bb, scattered back to lanes
+    {
+      const uint32_t v = srt[bf * kWave + lane];
+      if (act) flag[v & 0x3fu] = (uint8_t)((v >> 8) <= bb);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    const unsigned long long LM = M & __ballot(act && flag[lane]);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long RM = M & ~LM;
+    const int nl = __popcll(LM), nr = __popcll(RM);
+    const int64_t ls = slot + 1, rs = slot + 2 * nl;  // pre-order position ranges
+    const int lc1 = __popcll(LM & cm1), rc1 = (int)mc1 - lc1;
+    (void)bc;
+    const int lc0 = nl - lc1, rc0 = nr - rc1;
+    const int nzl = (lc0 > 0) + (lc1 > 0), nzr = (rc0 > 0) + (rc1 > 0);
+    const int cd = d + 1;
+    if (lane == 0) {
+      int32_t* P = out.node_i32 + slot * 6;
+      P[0] = bf;
+      P[1] = (int32_t)bb;
+      P[2] = (int32_t)ls;
+      P[3] = (int32_t)rs;
+      int32_t* L = out.node_i32 + ls * 6;
+      int32_t* Rr = out.node_i32 + rs * 6;
+      L[0] = -1; L[1] = -1; L[2] = -1; L[3] = -1; L[4] = cd; L[5] = nl;
+      Rr[0] = -1; Rr[1] = -1; Rr[2] = -1; Rr[3] = -1; Rr[4] = cd; Rr[5] = nr;
+      out.node_cnt[ls * C + 0] = lc0;
+      out.node_cnt[rs * C + 0] = rc0;
+      if (C > 1) {
+        out.node_cnt[ls * C + 1] = lc1;
+        out.node_cnt[rs * C + 1] = rc1;
+      }
+    }
+    const bool depth_stop = max_depth >= 0 && cd >= max_depth;
+    const bool tlf = depth_stop || nl < mss || nl < 2 * msl || nzl <= 1;
+    const bool trf = depth_stop || nr < mss || nr < 2 * msl || nzr <= 1;
+    const bool left_small = nl <= nr;
+    for (int pass = 0; pass < 2; ++pass) {
+      const bool is_left = (pass == 0) ? !left_small : left_small;
+      if (is_left ? tlf : trf) continue;
+      if (lane == 0) {
+        st_mask[sp] = is_left ? LM : RM;
+        st_dep[sp] = cd;
+        st_slot[sp] = (int32_t)(is_left ? ls : rs);
+      }
+      ++sp;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 __global__ __launch_bounds__(256) void finish_tiny_sorted_kernel(
     const uint32_t* __restrict__ codes_rm, int64_t row_words, const uint32_t* __restrict__ buf0,
     const uint32_t* __restrict__ buf1, const int32_t* __restrict__ y, FinRowLab rl,
     const int64_t* __restrict__ tiny, const int32_t* __restrict__ tiny_count,
     int32_t* __restrict__ tiny_counter, int F, int C, int crit, int max_depth, int64_t mss,
     int64_t msl, const double* __restrict__ xtab, int32_t* __restrict__ node_i32,
-    int32_t* __restrict__ node_cnt, int cw) {
+    int32_t* __restrict__ node_cnt) {
   extern __shared__ __align__(16) uint32_t dyn[];
-  __shared__ double s_tab[kTinyRows + 1];
+  __shared__ double s_h[kTinyH];
+  __shared__ uint32_t s_hrow[kTinyRows + 1];
   __shared__ unsigned long long s_mask[kTinyWaves][16];
   __shared__ int32_t s_dep[kTinyWaves][16], s_slot[kTinyWaves][16];
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
-  const int per_wave_words = kWave * cw + (F * kWave + 3) / 4;
-  uint32_t* wbase = dyn + wave * per_wave_words;
-  uint32_t* my_codes = wbase + lane * cw;
-  const uint8_t* codes_b = reinterpret_cast<const uint8_t*>(wbase);  // [lane][cw*4]
-  uint8_t* order = reinterpret_cast<uint8_t*>(wbase + kWave * cw);   // [F][64]
-  const uint8_t* my_bytes = reinterpret_cast<const uint8_t*>(my_codes);
-  for (int i = threadIdx.x; i <= kTinyRows; i += blockDim.x) s_tab[i] = xtab[i];
+  uint8_t* wbase = reinterpret_cast<uint8_t*>(dyn) + (size_t)wave * tiny_wave_bytes(F);
+  uint16_t* srt = reinterpret_cast<uint16_t*>(wbase);
+  uint8_t* flag = wbase + F * kWave * 2;
+  tiny_fill_h(s_h, xtab, crit);
+  for (int a = threadIdx.x; a <= kTinyRows; a += blockDim.x) s_hrow[a] = 8u * (uint32_t)tiny_h_idx(a, 0);
   __syncthreads();
   const int K = *tiny_count;
-  const int nw = (int)min<int64_t>(row_words, (int64_t)cw);
-  const unsigned long long below = (1ull << lane) - 1ull;
   for (;;) {
     int k = 0;
     if (lane == 0) k = atomicAdd(tiny_counter, 1);
     k = __builtin_amdgcn_readfirstlane(k);
     if (k >= K) break;
     const int64_t* rec = tiny + (int64_t)k * 8;
-    const int64_t start = rec[0];
-    const int m = (int)rec[1];
-    const int depth0 = (int)rec[2];
-    const uint32_t* src = rec[3] ? buf1 : buf0;
-    const int64_t root_slot = rec[4];
-    const bool act = lane < m;
-    int lab = 0;
-    if (act) {
-      const uint32_t ent = src[start + lane];
-      const uint32_t row = rl.shift ? (ent & rl.mask) : ent;
-      lab = rl.shift ? (int)(ent >> rl.shift) : y[row];
-      for (int i = 0; i < nw; ++i) my_codes[i] = codes_rm[(int64_t)row * row_words + i];
-    }
-    const unsigned long long R = m == 64 ? ~0ull : ((1ull << m) - 1ull);
-    const unsigned long long cm1 = C > 1 ? __ballot(act && lab == 1) : 0ull;
-    const unsigned long long cm0 = R & ~cm1;
-    // ---- presort: order_f[position] = lane, stable by lane among equal codes
-    for (int f = 0; f < F; ++f) {
-      const uint32_t code = my_bytes[f];
-      unsigned long long eq = R, gt = 0ull;
-#pragma unroll
-      for (int b = 7; b >= 0; --b) {
-        const unsigned long long bm = __ballot((code >> b) & 1u) & R;
-        if ((code >> b) & 1u) {
-          eq &= bm;
-        } else {
-          gt |= eq & bm;
-          eq &= ~bm;
-        }
-      }
-      const unsigned long long lt = R & ~gt & ~eq;
-      if (act) order[f * kWave + __popcll(lt) + __popcll(eq & below)] = (uint8_t)lane;
-    }
-    if (lane == 0) {
-      s_mask[wave][0] = R;
-      s_dep[wave][0] = depth0;
-      s_slot[wave][0] = (int32_t)root_slot;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    int sp = 1;
-    while (sp > 0) {
-      --sp;
-      const unsigned long long M = s_mask[wave][sp];
-      const int d = s_dep[wave][sp];
-      const int64_t slot = s_slot[wave][sp];
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      const int mm = __popcll(M);
-      const uint32_t mc1 = (uint32_t)__popcll(M & cm1), mc0 = (uint32_t)mm - mc1;
-      const double pterm = crit == kEntropy
-                               ? s_tab[mm] - (s_tab[mc0] + s_tab[mc1])
-                               : gini_term(mm, (int64_t)mc0 * mc0 + (int64_t)mc1 * mc1);
-      double bg = -__builtin_inf(), bc = __builtin_inf();
-      int bf = 0x7fffffff;
-      uint32_t bb = 0xffffffffu;
-      for (int f = 0; f < F; ++f) {
-        // sorted position = lane; only positions < m hold rows of the subtree
-        const int s = act ? order[f * kWave + lane] : 0;
-        const bool in = act && ((M >> s) & 1ull);
-        const uint32_t code = codes_b[s * cw * 4 + f];
-        const uint32_t packed = (in ? 1u : 0u) | ((in && ((cm1 >> s) & 1ull)) ? 0x10000u : 0u);
-        const uint32_t incl = wave_incl_scan_dpp(packed);
-        const uint32_t ml = incl & 0xffffu, l1 = incl >> 16, l0 = ml - l1;
-        // the split "code <= mine" is taken at the last node row of each code
-        const unsigned long long inb = __ballot(in);
-        const unsigned long long after = inb & ~(below | (1ull << lane));
-        const int nxt = after ? __ffsll((long long)after) - 1 : lane;
-        const uint32_t ncode = (uint32_t)__shfl((int)code, nxt, kWave);
-        const bool last = in && (after == 0ull || ncode != code);
-        const int mr = mm - (int)ml;
-        double cost = __builtin_inf();
-        if (last && (int64_t)ml >= msl && (int64_t)mr >= msl) {
-          const uint32_t r0 = mc0 - l0, r1 = mc1 - l1;
-          if (crit == kEntropy) {
-            const double sl = s_tab[l0] + s_tab[l1];
-            const double sr = s_tab[r0] + s_tab[r1];
-            cost = (s_tab[ml] - sl) + (s_tab[mr] - sr);
-          } else {
-            cost = gini_term(ml, (int64_t)l0 * l0 + (int64_t)l1 * l1) +
-                   gini_term(mr, (int64_t)r0 * r0 + (int64_t)r1 * r1);
-          }
-        }
-        const double g = pterm - cost;
-        if (g > bg) {  // features ascend: strict > keeps the lowest
-          bg = g;
-          bf = f;
-          bc = cost;
-          bb = code;
-        }
-      }
-#pragma unroll
-      for (int dd = kWave / 2; dd > 0; dd >>= 1) {
-        const double og = __shfl_xor(bg, dd, kWave);
-        const int of = __shfl_xor(bf, dd, kWave);
-        const double oc = __shfl_xor(bc, dd, kWave);
-        const uint32_t ob = (uint32_t)__shfl_xor((int)bb, dd, kWave);
-        const bool take =
-            og > bg ||
-            (og == bg && (of < bf || (of == bf && (oc < bc || (oc == bc && ob < bb)))));
-        if (take) {
-          bg = og;
-          bf = of;
-          bc = oc;
-          bb = ob;
-        }
-      }
-      bf = __builtin_amdgcn_readfirstlane(bf);
-      bb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bb);
-      if (!(bg > -__builtin_inf()) || bf < 0) continue;  // leaf: the creation record stands
-      const unsigned long long LM = M & __ballot(act && (uint32_t)my_bytes[bf] <= bb);
-      const unsigned long long RM = M & ~LM;
-      const int nl = __popcll(LM), nr = __popcll(RM);
-      const int64_t ls = slot + 1, rs = slot + 2 * nl;  // pre-order position ranges
-      const int lc1 = __popcll(LM & cm1), rc1 = (int)mc1 - lc1;
-      const int lc0 = nl - lc1, rc0 = nr - rc1;
-      const int nzl = (lc0 > 0) + (lc1 > 0), nzr = (rc0 > 0) + (rc1 > 0);
-      const int cd = d + 1;
-      if (lane == 0) {
-        int32_t* P = node_i32 + slot * 6;
-        P[0] = bf;
-        P[1] = (int32_t)bb;
-        P[2] = (int32_t)ls;
-        P[3] = (int32_t)rs;
-        int32_t* L = node_i32 + ls * 6;
-        int32_t* Rr = node_i32 + rs * 6;
-        L[0] = -1; L[1] = -1; L[2] = -1; L[3] = -1; L[4] = cd; L[5] = nl;
-        Rr[0] = -1; Rr[1] = -1; Rr[2] = -1; Rr[3] = -1; Rr[4] = cd; Rr[5] = nr;
-        node_cnt[ls * C + 0] = lc0;
-        node_cnt[rs * C + 0] = rc0;
-        if (C > 1) {
-          node_cnt[ls * C + 1] = lc1;
-          node_cnt[rs * C + 1] = rc1;
-        }
-      }
-      const bool depth_stop = max_depth >= 0 && cd >= max_depth;
-      const bool tlf = depth_stop || nl < mss || nl < 2 * msl || nzl <= 1;
-      const bool trf = depth_stop || nr < mss || nr < 2 * msl || nzr <= 1;
-      const bool left_small = nl <= nr;
-      for (int pass = 0; pass < 2; ++pass) {
-        const bool is_left = (pass == 0) ? !left_small : left_small;
-        if (is_left ? tlf : trf) continue;
-        if (lane == 0) {
-          s_mask[wave][sp] = is_left ? LM : RM;
-          s_dep[wave][sp] = cd;
-          s_slot[wave][sp] = (int32_t)(is_left ? ls : rs);
-        }
-        ++sp;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
+    tiny_sorted_subtree(codes_rm, row_words, rec[3] ? buf1 : buf0, y, rl, rec[0], (int)rec[1],
+                        (int)rec[2], rec[4], F, C, crit, max_depth, mss, msl, s_h, s_hrow, srt, flag,
+                        s_mask[wave], s_dep[wave], s_slot[wave], TinyOut{node_i32, node_cnt});
   }
 }
 
@@ -1155,14 +1266,13 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   if (tiny_rows > 0) {
     const bool sorted = C <= 2 && getenv_int("MPITREE_TINY_SORTED", 1) != 0;
     if (sorted) {
-      const int cw = ((F + 3) / 4) | 1;  // odd row stride: lanes spread over LDS banks
-      const size_t lds = (size_t)kTinyWaves * (kWave * cw + (F * kWave + 3) / 4) * 4;
+      const size_t lds = (size_t)kTinyWaves * tiny_wave_bytes(F);
       MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_tiny_sorted_kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       hipLaunchKernelGGL(finish_tiny_sorted_kernel, dim3(tiny_grid), dim3(kTinyWaves * kWave),
                          lds, stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl,
                          tiny, counter + 1, counter + 2, F, C, crit, max_depth, mss, msl, xtab,
-                         node_i32, node_cnt, cw);
+                         node_i32, node_cnt);
     } else {
       hipLaunchKernelGGL(finish_tiny_kernel, dim3(tiny_grid), dim3(kTinyWaves * kWave), 0,
                          stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,
