@@ -12,6 +12,9 @@ Single GPU: ``python bench.py``. Multi-GPU (one process per GPU, RCCL):
 ``torchrun --nproc-per-node N bench.py --gpus N``; every rank holds the full
 data (the reference's ParallelDecisionTreeClassifier contract) and the total
 work is fixed, so scaling is "strong".
+
+``MPITREE_BENCH_BACKEND=gloo`` rehearses the multi-rank path with ranks
+sharing the visible GPUs (collectives over gloo instead of RCCL).
 """
 
 from __future__ import annotations
@@ -23,6 +26,12 @@ import sys
 import time
 
 import torch
+
+
+# BASELINE.json's headline metric and the configuration this script runs
+METRIC = "tree fit wall-clock (s) + samples/sec, 1M\u00d764 synthetic at 1/2/4/8 GPUs"
+CONFIG = "1M\u00d764 synthetic, feature-parallel split search, RCCL all-reduce on 8\u00d7MI355X"
+CONFIG_REG = "1M\u00d764 regression tree (MSE split criterion) on 8\u00d7MI355X"
 
 
 def main(argv=None):
@@ -47,7 +56,11 @@ def main(argv=None):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    backend = os.environ.get("MPITREE_BENCH_BACKEND", "nccl")
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend != "nccl":  # rehearsal: ranks may share a GPU
+        local %= max(1, torch.cuda.device_count())
+        os.environ["LOCAL_RANK"] = str(local)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     md = None if a.max_depth < 0 else a.max_depth
@@ -62,7 +75,7 @@ def main(argv=None):
 
         from mpitree_amd.parallel.process_group import init_distributed
 
-        init_distributed(backend="nccl")
+        init_distributed(backend=backend)
         cls = ParallelDecisionTreeRegressor if a.regression else ParallelDecisionTreeClassifier
         est = cls(max_depth=md, criterion=crit, device="cuda", strategy=a.strategy)
     else:
@@ -91,7 +104,7 @@ def main(argv=None):
     if rank == 0:
         value = a.n / dt
         out = {
-            "metric": "fit_samples_per_sec",
+            "metric": METRIC,
             "value": round(value, 1),
             "unit": "samples/s",
             "n_gpus": world,
@@ -102,9 +115,12 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "fp32-features/int32-hist/fp64-criterion",
+            "dtype": "fp32",
+            "dtype_detail": "fp32 features (exact data-value thresholds), int32 histogram "
+                            "counts, fp64 split criterion",
             "data": "synthetic (on-device, 256-level quantized features, random-init labels)",
             "config": {
+                "name": CONFIG if not a.regression else CONFIG_REG,
                 "model": f"DecisionTree{'Regressor' if a.regression else 'Classifier'}"
                          f"(criterion={crit}, max_depth={md})",
                 "n_samples": a.n,

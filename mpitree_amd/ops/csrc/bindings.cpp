@@ -4,6 +4,8 @@
 // current HIP stream handle, so no PyTorch headers are compiled here: the
 // extension builds in seconds with hipcc and calls cost one pybind hop.
 #include <hip/hip_runtime.h>
+#include <cstring>
+
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 
@@ -75,6 +77,7 @@ struct PlanArgs {
   int32_t* job_count;
   int C, max_depth, n_cu;
   int64_t mss, msl, fr;
+  int32_t* host_ctl;
 };
 void launch_grow_plan(hipStream_t, const PlanArgs&);
 void launch_grow_init(hipStream_t, const LevelLists&, int64_t, int64_t, int, int, const int64_t*,
@@ -241,7 +244,7 @@ PYBIND11_MODULE(_hip, m) {
                         uintptr_t pos_st, uintptr_t pos_st64, int reg, int out_buf,
                         uintptr_t jobs,
                         uintptr_t job_count, int C, int max_depth, int n_cu, int64_t mss,
-                        int64_t msl, int64_t fr) {
+                        int64_t msl, int64_t fr, uintptr_t host_ctl) {
     auto lists = [](py::dict d) {
       auto g = [&](const char* k) { return d[k].cast<uintptr_t>(); };
       return mt::LevelLists{P<int64_t>(g("pos")),  P<int64_t>(g("start")), P<int32_t>(g("cnt")),
@@ -254,9 +257,23 @@ PYBIND11_MODULE(_hip, m) {
                    P<int64_t>(split),   P<int64_t>(pitems), P<int32_t>(cursors),
                    P<int32_t>(pctl),    P<int32_t>(pos_rec), P<int32_t>(pos_st),
                    P<int64_t>(pos_st64), reg, out_buf, P<int64_t>(jobs), P<int32_t>(job_count), C,
-                   max_depth, n_cu, mss, msl, fr};
+                   max_depth, n_cu, mss, msl, fr, P<int32_t>(host_ctl)};
     mt::launch_grow_plan(S(s), a);
   });
+  // Host-mapped, fine-grained (coherent) memory the kernels can store into
+  // directly: the level loop's termination counters travel without a copy.
+  m.def("host_alloc", [](size_t nbytes) {
+    void* p = nullptr;
+    MT_HIP_CHECK(hipHostMalloc(&p, nbytes, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(p, 0, nbytes);
+    return reinterpret_cast<uintptr_t>(p);
+  });
+  m.def("host_device_ptr", [](uintptr_t p) {
+    void* d = nullptr;
+    MT_HIP_CHECK(hipHostGetDevicePointer(&d, reinterpret_cast<void*>(p), 0));
+    return reinterpret_cast<uintptr_t>(d);
+  });
+  m.def("host_free", [](uintptr_t p) { MT_HIP_CHECK(hipHostFree(reinterpret_cast<void*>(p))); });
   m.def("edges_sample_rows", &mt::edges_sample_rows);
   m.def(
       "edges",

@@ -302,6 +302,141 @@ __global__ __launch_bounds__(256) void bin_kernel(const XT* __restrict__ X, int6
   if (threadIdx.x < nf && s_flag[threadIdx.x]) atomicOr(&flags[f0 + threadIdx.x], s_flag[threadIdx.x]);
 }
 
+// Row-streaming bin kernel for the common case (fp32 X, <= 256 bins, F % 4 == 0):
+// each workgroup keeps the edges of up to 64 features resident in LDS and
+// streams a contiguous row range in batches of kBrU x (512 / (nf / 4)) rows.
+// A thread owns one float4 (4 consecutive features) of a row per pass, so X
+// is read as whole 16-byte-aligned row segments, the row-major codes leave as
+// one 4-byte store per thread, and the feature-major codes are transposed
+// through a small LDS tile and written as 16-byte runs. The next batch's
+// loads are issued before the current batch is searched (register double
+// buffering) to keep enough bytes in flight per CU for HBM3E.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int kBrThreads = 512;
+constexpr int kBrFt = 64;  // features per tile (LDS: 64 x 257 x 4 B of edges)
+constexpr int kBrU = 4;    // passes per batch
+
+__global__ __launch_bounds__(kBrThreads) void bin_rows_kernel(
+    const float* __restrict__ X, int64_t n, int F, const float* __restrict__ edges, int Bmax,
+    int estride, int steps0, const int32_t* __restrict__ nbins, const uint8_t* __restrict__ exact,
+    uint8_t* __restrict__ codes_rm, int row_elems, uint8_t* __restrict__ codes_fm,
+    int32_t* __restrict__ flags, int64_t rows_per_block, int fm_vec) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  __shared__ int s_flag[kBrFt];
+  const int ES = Bmax | 1;
+  const int f0 = blockIdx.y * kBrFt;
+  const int nf = min(kBrFt, F - f0);  // multiple of 4
+  const int tpr = nf >> 2;            // threads per row
+  const int rp = kBrThreads / tpr;    // rows per pass
+  const int batch = kBrU * rp;
+  float* s_edges = reinterpret_cast<float*>(smem);
+  uint8_t* tile = smem + (((size_t)nf * ES * 4 + 15) & ~(size_t)15);  // [batch][nf]
+  const int tid = threadIdx.x;
+  if (tid < kBrFt) s_flag[tid] = 0;
+  for (int e = tid; e < nf * Bmax; e += kBrThreads) {
+    const int fl = e / Bmax, b = e - fl * Bmax;
+    s_edges[fl * ES + b] = edges[(int64_t)(f0 + fl) * estride + b];
+  }
+  const int rs = tid / tpr;  // row slot within a pass
+  const int q = tid - rs * tpr;
+  const bool active = rs < rp;
+  int nb[4], ex[4], fg[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int f = f0 + 4 * q + j;
+    nb[j] = active ? nbins[f] : 1;
+    ex[j] = active ? exact[f] : 0;
+    fg[j] = 0;
+  }
+  __syncthreads();
+  const int64_t rbeg = blockIdx.x * rows_per_block;
+  const int64_t rend = min<int64_t>(n, rbeg + rows_per_block);
+  fm_vec = fm_vec && ((rbeg | batch) & 15) == 0;
+  auto load = [&](int64_t b0, float4* v) {
+#pragma unroll
+    for (int u = 0; u < kBrU; ++u) {
+      const int64_t r = b0 + u * rp + rs;
+      if (active && r < rend) {
+        const f32x4 t = __builtin_nontemporal_load(
+            reinterpret_cast<const f32x4*>(X + r * F + f0 + 4 * q));
+        v[u] = make_float4(t[0], t[1], t[2], t[3]);
+      } else {
+        v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  };
+  float4 cur[kBrU], nxt[kBrU];
+  if (rbeg < rend) load(rbeg, cur);
+  for (int64_t b0 = rbeg; b0 < rend; b0 += batch) {
+    if (b0 + batch < rend) load(b0 + batch, nxt);
+    float v[kBrU * 4];
+    int pos[kBrU * 4];
+#pragma unroll
+    for (int u = 0; u < kBrU; ++u) {
+      v[4 * u + 0] = cur[u].x;
+      v[4 * u + 1] = cur[u].y;
+      v[4 * u + 2] = cur[u].z;
+      v[4 * u + 3] = cur[u].w;
+    }
+#pragma unroll
+    for (int k = 0; k < kBrU * 4; ++k) pos[k] = 0;
+    for (int step = steps0; step > 0; step >>= 1) {
+#pragma unroll
+      for (int k = 0; k < kBrU * 4; ++k) {
+        const int j = k & 3;
+        const int p = pos[k] + step;
+        if (p <= nb[j] && s_edges[(4 * q + j) * ES + p - 1] < v[k]) pos[k] = p;
+      }
+    }
+    const int rows = (int)min<int64_t>(batch, rend - b0);
+#pragma unroll
+    for (int u = 0; u < kBrU; ++u) {
+      const int rl = u * rp + rs;
+      uint32_t word = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = 4 * u + j;
+        const int code = pos[k] < nb[j] ? pos[k] : nb[j] - 1;
+        if (ex[j] && !(s_edges[(4 * q + j) * ES + code] == v[k])) fg[j] |= 1;
+        if (!isfinite(v[k])) fg[j] |= 2;
+        word |= (uint32_t)code << (8 * j);
+      }
+      if (active && rl < rows) {
+        *reinterpret_cast<uint32_t*>(codes_rm + (b0 + rl) * row_elems + f0 + 4 * q) = word;
+        *reinterpret_cast<uint32_t*>(tile + rl * nf + 4 * q) = word;
+      }
+    }
+    __syncthreads();
+    // feature-major: each feature's `rows` codes are contiguous at codes_fm[f * n + b0]
+    const int chunks = (rows + 15) >> 4;
+    for (int e = tid; e < nf * chunks; e += kBrThreads) {
+      const int fl = e % nf, c = e / nf;
+      uint8_t* dst = codes_fm + (int64_t)(f0 + fl) * n + b0 + 16 * c;
+      const int m = min(16, rows - 16 * c);
+      if (fm_vec && m == 16) {
+        uint32_t w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          w[i] = (uint32_t)tile[(16 * c + 4 * i) * nf + fl] |
+                 ((uint32_t)tile[(16 * c + 4 * i + 1) * nf + fl] << 8) |
+                 ((uint32_t)tile[(16 * c + 4 * i + 2) * nf + fl] << 16) |
+                 ((uint32_t)tile[(16 * c + 4 * i + 3) * nf + fl] << 24);
+        *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+      } else {
+        for (int i = 0; i < m; ++i) dst[i] = tile[(16 * c + i) * nf + fl];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kBrU; ++u) cur[u] = nxt[u];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (active && fg[j]) atomicOr(&s_flag[4 * q + j], fg[j]);
+  __syncthreads();
+  if (tid < nf && s_flag[tid]) atomicOr(&flags[f0 + tid], s_flag[tid]);
+}
+
 int edges_sample_rows(bool x64) { return x64 ? 16384 : 32768; }
 
 // The host's view of the edges in one fp64 array: [F][limit] edges, then the
@@ -362,6 +497,27 @@ void launch_bin(hipStream_t stream, const void* X, bool x64, int64_t n, int F, c
   const size_t lds = (lds_edges ? edge_bytes : 0) + (size_t)kBinRows * kBinFt * code_bytes;
   int steps0 = 1;
   while (steps0 * 2 <= Bmax) steps0 *= 2;
+  if (!x64 && code_bytes == 1 && Bmax <= 256 && (F & 3) == 0 && (row_elems & 3) == 0 &&
+      ((uintptr_t)X & 15) == 0 && ((uintptr_t)codes_rm & 3) == 0) {
+    const int tiles = (F + kBrFt - 1) / kBrFt;
+    const int nf = std::min(kBrFt, F);
+    const int batch = kBrU * (kBrThreads / (nf / 4));
+    const int64_t nbatch = (n + batch - 1) / batch;
+    const int64_t want = std::max<int64_t>(1, 2 * 256 / tiles);  // ~2 workgroups per CU
+    const int64_t per = (nbatch + want - 1) / want;
+    const int64_t rpb = per * batch;
+    const unsigned gx = (unsigned)((n + rpb - 1) / rpb);
+    const size_t lds2 = (((size_t)nf * (Bmax | 1) * 4 + 15) & ~(size_t)15) + (size_t)batch * nf;
+    const int fm_vec = ((n & 15) == 0 && ((uintptr_t)codes_fm & 15) == 0) ? 1 : 0;
+    MT_HIP_CHECK(hipFuncSetAttribute((const void*)bin_rows_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+    hipLaunchKernelGGL(bin_rows_kernel, dim3(gx, (unsigned)tiles), dim3(kBrThreads), lds2, stream,
+                       (const float*)X, n, F, (const float*)edges, Bmax, estride, steps0, nbins,
+                       exact, (uint8_t*)codes_rm, row_elems, (uint8_t*)codes_fm, flags, rpb,
+                       fm_vec);
+    MT_HIP_CHECK(hipGetLastError());
+    return;
+  }
   dim3 grid((unsigned)((n + kBinRows - 1) / kBinRows), (unsigned)((F + kBinFt - 1) / kBinFt));
 #define MT_BIN(XT, CT, L)                                                                      \
   {                                                                                            \

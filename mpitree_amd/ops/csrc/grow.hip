@@ -66,6 +66,7 @@ struct PlanArgs {
   int32_t* job_count;
   int C, max_depth, n_cu;
   int64_t mss, msl, fr;
+  int32_t* host_ctl;   // [2] host-mapped {next frontier size, jobs so far} or null
 };
 
 __device__ __forceinline__ int plan_scan_excl(int v, int* s_w, int& total) {
@@ -467,9 +468,15 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     a.nxt.ctl[5] = 0;
     a.nxt.ctl[6] = 0;
     a.nxt.ctl[7] = n_tasks;
-    a.nxt.ctl[9] = atomicAdd(a.job_count, 0);  // finisher jobs so far (host's lagged read)
+    const int jobs_so_far = atomicAdd(a.job_count, 0);
+    a.nxt.ctl[9] = jobs_so_far;  // finisher jobs so far
     a.pctl[0] = NS;
     a.pctl[1] = s_carry[3];
+    if (a.host_ctl) {  // the host's lagged termination read, stored straight to host memory
+      __hip_atomic_store(a.host_ctl + 1, jobs_so_far, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(a.host_ctl, K2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+    }
   }
 }
 
@@ -529,24 +536,28 @@ void launch_grow_init(hipStream_t stream, const LevelLists& L, int64_t n, int64_
   MT_HIP_CHECK(hipGetLastError());
 }
 
-// Finisher job order: largest subtree first (stable), so the persistent
-// finisher workgroups start the long jobs early. One workgroup bitonic-sorts
-// 32-bit keys {0xFFFF - rows : 16, index : 13} in LDS and gathers the rows;
-// it also zeroes the finisher's work counters.
+// Finisher job order: largest subtree first, ties by root position -- a total
+// order independent of the planner's (atomic, racy) append order, so every
+// rank of a multi-GPU fit derives the same job list and job ownership. One
+// workgroup bitonic-sorts 64-bit keys {0xFFFF - rows : 16, root position : 31,
+// index : 13} in LDS and gathers the rows; it also zeroes the finisher's work
+// counters.
 constexpr int kSortMax = 8192;
 
 __global__ __launch_bounds__(1024) void job_sort_kernel(const int64_t* __restrict__ jobs, int J,
                                                         int W, int64_t* __restrict__ out,
                                                         int32_t* __restrict__ counters) {
-  __shared__ uint32_t key[kSortMax];
+  extern __shared__ __align__(16) uint8_t smem[];
+  uint64_t* key = reinterpret_cast<uint64_t*>(smem);  // [kSortMax]
   int N2 = 1;
   while (N2 < J) N2 <<= 1;
   for (int i = threadIdx.x; i < N2; i += 1024) {
-    uint32_t k = 0xFFFFFFFFu;
+    uint64_t k = ~0ull;
     if (i < J) {
       const int64_t c = jobs[(int64_t)i * W + 1];
-      const uint32_t cc = c > 0xFFFF ? 0xFFFFu : (uint32_t)c;
-      k = ((0xFFFFu - cc) << 13) | (uint32_t)i;
+      const uint64_t cc = c > 0xFFFF ? 0xFFFFull : (uint64_t)c;
+      const uint64_t pos = (uint64_t)jobs[(int64_t)i * W + 3] & 0x7FFFFFFFull;
+      k = ((0xFFFFull - cc) << 44) | (pos << 13) | (uint64_t)i;
     }
     key[i] = k;
   }
@@ -557,7 +568,7 @@ __global__ __launch_bounds__(1024) void job_sort_kernel(const int64_t* __restric
       for (int i = threadIdx.x; i < N2; i += 1024) {
         const int j = i ^ stride;
         if (j > i) {
-          const uint32_t a = key[i], b = key[j];
+          const uint64_t a = key[i], b = key[j];
           const bool up = (i & size) == 0;
           if ((a > b) == up) {
             key[i] = b;
@@ -570,7 +581,7 @@ __global__ __launch_bounds__(1024) void job_sort_kernel(const int64_t* __restric
   }
   for (int e = threadIdx.x; e < J * W; e += 1024) {
     const int r = e / W, c = e - r * W;
-    out[e] = jobs[(int64_t)(key[r] & 0x1FFFu) * W + c];
+    out[e] = jobs[(int64_t)(key[r] & 0x1FFFull) * W + c];
   }
 }
 
@@ -579,7 +590,12 @@ int job_sort_max() { return kSortMax; }
 void launch_job_sort(hipStream_t stream, const int64_t* jobs, int J, int W, int64_t* out,
                      int32_t* counters) {
   if (J > kSortMax) throw std::runtime_error("job_sort: too many jobs for one workgroup");
-  hipLaunchKernelGGL(job_sort_kernel, dim3(1), dim3(1024), 0, stream, jobs, J, W, out, counters);
+  int N2 = 1;
+  while (N2 < J) N2 <<= 1;
+  const int lds = N2 * (int)sizeof(uint64_t);
+  MT_HIP_CHECK(hipFuncSetAttribute((const void*)job_sort_kernel,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, kSortMax * 8));
+  hipLaunchKernelGGL(job_sort_kernel, dim3(1), dim3(1024), lds, stream, jobs, J, W, out, counters);
   MT_HIP_CHECK(hipGetLastError());
 }
 

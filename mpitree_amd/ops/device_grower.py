@@ -15,7 +15,7 @@ so the host only enqueues fixed-shape launches. Grids are host-known upper
 bounds (a level has at most ``min(2**L, n // (finisher_rows + 1) + 1)``
 frontier nodes, because frontier nodes hold more than ``finisher_rows`` rows);
 surplus workgroups exit on the device count. The host learns that the tree is
-finished from a lagged, pinned 32-byte read of the next level's counters, then
+finished from a lagged read of host-mapped counters the planner stores, then
 sorts the device job list (largest first) and launches the subtree finisher;
 the position space is compacted by ``assemble.hip``. The resulting tree is
 bitwise identical to the host-driven builder's (tests/test_gpu_kernels.py).
@@ -40,6 +40,21 @@ from . import hip_backend as hb
 __all__ = ["DeviceGrower", "device_loop_supported"]
 
 _WORKSPACES: dict = {}  # (device, n, F, B, C, reg, fr) -> level-loop buffers
+_HOST_CTL: dict = {}  # device index -> (device pointer, numpy view [64, 16] int32)
+
+
+def _host_ctl(hip, dev):
+    """Host-mapped coherent slots the planner stores each level's {next frontier
+    size, finisher jobs} into (no copy kernel, no pinned D2H per level)."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    ent = _HOST_CTL.get(key)
+    if ent is None:
+        import ctypes
+
+        hptr = hip.host_alloc(64 * 16 * 4)
+        view = np.ctypeslib.as_array((ctypes.c_int32 * (64 * 16)).from_address(hptr))
+        ent = _HOST_CTL[key] = (hip.host_device_ptr(hptr), view.reshape(64, 16))
+    return ent
 
 
 def device_loop_supported(be, params, comm) -> bool:
@@ -93,19 +108,29 @@ class DeviceGrower:
             owner = torch.where(lap % 2 == 0, off, P - 1 - off)
             d_jobs = d_jobs[owner == r]
             counter = None
+            # positions the (replicated) level loop decided: every rank has
+            # them, so the exchange sends only what this rank's finisher grew
+            self._pre_live = be.pos_rec[:, 5] > 0
         J = int(d_jobs.shape[0])
         if J:
             be.launch_finisher(d_jobs.contiguous(), J, n, self.p, be.pos_rec, be.pos_st,
                                counter)
 
     def _exchange_nodes(self):
-        """Every rank ends with every finished node: compact the written
-        positions ({pos, record[6], counts[C]} int32 rows), all-gather them and
-        scatter into the local position space. Level nodes are written by all
-        ranks identically, so their duplicates are harmless."""
+        """Every rank ends with every finished node: compact the positions this
+        rank's finisher wrote ({pos, record[6], counts[C]} rows), all-gather
+        them and scatter into the local position space. Level nodes are on
+        every rank already and every job has one owner (the job order is a
+        total order, see ``job_sort_kernel``), so each position has exactly
+        one writer."""
         be, comm = self.be, self.comm
         dt = torch.int64 if be.reg else torch.int32  # regression sums need 64 bits
-        live = torch.nonzero(be.pos_rec[:, 5] > 0).squeeze(1)
+        grown = be.pos_rec[:, 5] > 0
+        pre = getattr(self, "_pre_live", None)
+        if pre is not None:
+            grown &= ~pre
+            self._pre_live = None
+        live = torch.nonzero(grown).squeeze(1)
         rows = torch.cat([live.to(dt)[:, None], be.pos_rec[live].to(dt),
                           be.pos_st[live].to(dt)], 1)
         allr = comm.all_gather_rows(rows)
@@ -213,7 +238,6 @@ class DeviceGrower:
                     fin_counter=torch.zeros(4, dtype=torch.int32, device=dev),
                     root=torch.empty(4 if reg else C, **i64),
                     root_host=torch.empty(4 if reg else C, dtype=torch.int64, pin_memory=True),
-                    pinned=torch.zeros((64, 16), dtype=torch.int32, pin_memory=True),
                 )
 
             ws = self._workspace((str(dev), n, F, B, C, reg, fr), make)
@@ -221,7 +245,7 @@ class DeviceGrower:
             cost, bins, ident, split = ws["cost"], ws["bins"], ws["ident"], ws["split"]
             pitems, cursors, jobs, job_count = (ws["pitems"], ws["cursors"], ws["jobs"],
                                                 ws["job_count"])
-            pinned = ws["pinned"]
+            hctl_dev, hctl = _host_ctl(hip, dev)
             ptrs = [self._ptrs(x) for x in sets]
             # level 0: the root, built from rows (one init launch; root stats H2D)
             chunk = int(min(hb.MAX_ITEM_ROWS, max(1024, -(-n // (2 * hb.N_CU)))))
@@ -278,7 +302,8 @@ class DeviceGrower:
                               0 if reg else be.pos_st.data_ptr(),
                               be.pos_st.data_ptr() if reg else 0, int(reg), (lvl + 1) % 2,
                               jobs.data_ptr(),
-                              job_count.data_ptr(), C, md, hb.N_CU, mss, msl, fr)
+                              job_count.data_ptr(), C, md, hb.N_CU, mss, msl, fr,
+                              hctl_dev + (lvl % 64) * 64)
                 mark()
                 pb = int(min(PMAX, n // 1024 + kb + 1))
                 hip.partition(s(), be.codes_fm.data_ptr(), cb, be.n, src, dst, be.row_mask,
@@ -289,23 +314,21 @@ class DeviceGrower:
                                    int(min(MMAX, 2 * kb + n // 4096 + 1)), nxt["minmax"],
                                    nxt["ctl"] + 4 * 8)
                 mark()
-                # lagged completion check: next level's frontier size + job count
-                slot = lvl % 64
-                pinned[slot].copy_(sets[(lvl + 1) % 2]["ctl"], non_blocking=True)
+                # lagged completion check: the planner stored the next level's
+                # frontier size + job count into host slot lvl % 64
                 ev = torch.cuda.Event()
                 ev.record()
                 events.append(ev)
                 lvl += 1
                 if lvl >= 2:
                     events[lvl - 2].synchronize()
-                    row = pinned[(lvl - 2) % 64]
-                    if int(row[0]) == 0:
+                    if int(hctl[(lvl - 2) % 64, 0]) == 0:
                         done_at = lvl - 2
                         break
                 if lvl > 4096:
                     raise RuntimeError("device level loop did not terminate")
             levels = done_at + 1
-            J = int(pinned[done_at % 64, 9])  # ctl[9]: finisher jobs appended
+            J = int(hctl[done_at % 64, 1])  # finisher jobs appended
             if prof:
                 self._level_profile(marks[:levels])
             if J:
@@ -316,7 +339,9 @@ class DeviceGrower:
                     hip.job_sort(s(), jobs.data_ptr(), J, W, d_jobs.data_ptr(),
                                  counter.data_ptr())
                 else:
-                    order = torch.argsort(jobs[:J, 1], descending=True, stable=True)
+                    # largest first, ties by root position (the kernel's total order)
+                    order = torch.argsort(jobs[:J, 1] * (1 << 32) - jobs[:J, 3],
+                                          descending=True)
                     d_jobs = jobs[:J].index_select(0, order)
                 self._run_jobs(d_jobs, n, counter)
         elif jobs_host is not None:

@@ -119,6 +119,54 @@ def test_gpu_ranks_equal_serial(strategy, monkeypatch):
             np.testing.assert_array_equal(o[k], getattr(ref, k))
 
 
+def _fit_rank_gpu_large(rank, world, regression):
+    import torch
+
+    from mpitree_amd import ParallelDecisionTreeClassifier, ParallelDecisionTreeRegressor
+    from mpitree_amd.utils.datasets import make_classification, make_regression
+
+    dev = torch.device("cuda", 0)
+    if regression:
+        X, y = make_regression(200_000, 16, levels=64, seed=5, device=dev)
+        cls = ParallelDecisionTreeRegressor
+    else:
+        X, y = make_classification(300_000, 16, seed=5, device=dev)
+        cls = ParallelDecisionTreeClassifier
+    outs = {}
+    for it in range(2):  # repeated fits: the job split must not depend on append order
+        est = cls(strategy="auto", device="cuda").fit(X, y)
+        ta = est.tree_arrays_
+        for k in FIELDS:
+            outs[f"{k}{it}"] = getattr(ta, k)
+        outs[f"engine{it}"] = np.array([est.fit_stats_["engine"]])
+    return outs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("regression", [False, True])
+def test_gpu_ranks_equal_single_gpu_at_scale(regression):
+    """Thousands of finisher jobs (many with equal row counts) split over two
+    ranks: every rank, every repeat, equals the single-GPU device-loop tree."""
+    import torch
+
+    from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
+    from mpitree_amd.utils.datasets import make_classification, make_regression
+
+    outs = run_ranks(_fit_rank_gpu_large, 2, regression, start_method="spawn")
+    dev = torch.device("cuda", 0)
+    if regression:
+        X, y = make_regression(200_000, 16, levels=64, seed=5, device=dev)
+        ref = DecisionTreeRegressor(device="cuda").fit(X, y).tree_arrays_
+    else:
+        X, y = make_classification(300_000, 16, seed=5, device=dev)
+        ref = DecisionTreeClassifier(device="cuda").fit(X, y).tree_arrays_
+    for o in outs:
+        for it in range(2):
+            assert str(o[f"engine{it}"][0]) == "hip-device-loop"
+            for k in FIELDS:
+                np.testing.assert_array_equal(o[f"{k}{it}"], getattr(ref, k), err_msg=k)
+
+
 def _fault_rank(rank, world, fault_rank):
     import os
 
