@@ -78,6 +78,7 @@ struct PlanArgs {
   int C, max_depth, n_cu;
   int64_t mss, msl, fr;
   int32_t* host_ctl;
+  int32_t host_tag;
 };
 void launch_grow_plan(hipStream_t, const PlanArgs&);
 void launch_grow_init(hipStream_t, const LevelLists&, int64_t, int64_t, int, int, const int64_t*,
@@ -244,7 +245,7 @@ PYBIND11_MODULE(_hip, m) {
                         uintptr_t pos_st, uintptr_t pos_st64, int reg, int out_buf,
                         uintptr_t jobs,
                         uintptr_t job_count, int C, int max_depth, int n_cu, int64_t mss,
-                        int64_t msl, int64_t fr, uintptr_t host_ctl) {
+                        int64_t msl, int64_t fr, uintptr_t host_ctl, int host_tag) {
     auto lists = [](py::dict d) {
       auto g = [&](const char* k) { return d[k].cast<uintptr_t>(); };
       return mt::LevelLists{P<int64_t>(g("pos")),  P<int64_t>(g("start")), P<int32_t>(g("cnt")),
@@ -257,7 +258,7 @@ PYBIND11_MODULE(_hip, m) {
                    P<int64_t>(split),   P<int64_t>(pitems), P<int32_t>(cursors),
                    P<int32_t>(pctl),    P<int32_t>(pos_rec), P<int32_t>(pos_st),
                    P<int64_t>(pos_st64), reg, out_buf, P<int64_t>(jobs), P<int32_t>(job_count), C,
-                   max_depth, n_cu, mss, msl, fr, P<int32_t>(host_ctl)};
+                   max_depth, n_cu, mss, msl, fr, P<int32_t>(host_ctl), host_tag};
     mt::launch_grow_plan(S(s), a);
   });
   // Host-mapped, fine-grained (coherent) memory the kernels can store into

@@ -66,7 +66,8 @@ struct PlanArgs {
   int32_t* job_count;
   int C, max_depth, n_cu;
   int64_t mss, msl, fr;
-  int32_t* host_ctl;   // [2] host-mapped {next frontier size, jobs so far} or null
+  int32_t* host_ctl;   // [3] host-mapped {next frontier size, jobs so far, tag} or null
+  int32_t host_tag;    // written last: the host polls it to know the slot is complete
 };
 
 __device__ __forceinline__ int plan_scan_excl(int v, int* s_w, int& total) {
@@ -476,6 +477,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
       __hip_atomic_store(a.host_ctl + 1, jobs_so_far, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(a.host_ctl, K2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __threadfence_system();
+      __hip_atomic_store(a.host_ctl + 2, a.host_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }

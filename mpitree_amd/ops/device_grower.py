@@ -41,6 +41,25 @@ __all__ = ["DeviceGrower", "device_loop_supported"]
 
 _WORKSPACES: dict = {}  # (device, n, F, B, C, reg, fr) -> level-loop buffers
 _HOST_CTL: dict = {}  # device index -> (device pointer, numpy view [64, 16] int32)
+_FIT_SEQ = [0]  # per-process fit counter: tags host slots so stale values never match
+POLL_TIMEOUT_S = float(os.environ.get("MPITREE_POLL_TIMEOUT", "120"))
+
+
+def _wait_slot(hctl, slot: int, tag: int):
+    """Spin until the planner's store of ``tag`` into host slot ``slot`` lands
+    (coherent host memory: no event, no stream sync, no driver call)."""
+    row = hctl[slot]
+    if row[2] == tag:
+        return
+    t_end = time.perf_counter() + POLL_TIMEOUT_S
+    k = 0
+    while row[2] != tag:
+        k += 1
+        if (k & 0xFFFF) == 0:
+            if time.perf_counter() > t_end:
+                raise RuntimeError("device level loop: planner result never arrived "
+                                   f"(slot {slot}, tag {tag}); the GPU stream is stuck")
+            time.sleep(0)
 
 
 def _host_ctl(hip, dev):
@@ -246,6 +265,8 @@ class DeviceGrower:
             pitems, cursors, jobs, job_count = (ws["pitems"], ws["cursors"], ws["jobs"],
                                                 ws["job_count"])
             hctl_dev, hctl = _host_ctl(hip, dev)
+            _FIT_SEQ[0] = (_FIT_SEQ[0] + 1) % (1 << 18)
+            tag0 = _FIT_SEQ[0] << 12
             ptrs = [self._ptrs(x) for x in sets]
             # level 0: the root, built from rows (one init launch; root stats H2D)
             chunk = int(min(hb.MAX_ITEM_ROWS, max(1024, -(-n // (2 * hb.N_CU)))))
@@ -253,7 +274,6 @@ class DeviceGrower:
             ws["root"].copy_(ws["root_host"], non_blocking=True)
             hip.grow_init(s(), ptrs[0], n, chunk, C, int(reg), ws["root"].data_ptr(),
                           job_count.data_ptr())
-            events = []
             cb, rs = be.cb, be.row_elems * be.cb
             bufs = (be.idx.data_ptr(), be.tmp.data_ptr())
             lvl = 0
@@ -303,7 +323,7 @@ class DeviceGrower:
                               be.pos_st.data_ptr() if reg else 0, int(reg), (lvl + 1) % 2,
                               jobs.data_ptr(),
                               job_count.data_ptr(), C, md, hb.N_CU, mss, msl, fr,
-                              hctl_dev + (lvl % 64) * 64)
+                              hctl_dev + (lvl % 64) * 64, tag0 + (lvl % 4096) + 1)
                 mark()
                 pb = int(min(PMAX, n // 1024 + kb + 1))
                 hip.partition(s(), be.codes_fm.data_ptr(), cb, be.n, src, dst, be.row_mask,
@@ -316,12 +336,9 @@ class DeviceGrower:
                 mark()
                 # lagged completion check: the planner stored the next level's
                 # frontier size + job count into host slot lvl % 64
-                ev = torch.cuda.Event()
-                ev.record()
-                events.append(ev)
                 lvl += 1
                 if lvl >= 2:
-                    events[lvl - 2].synchronize()
+                    _wait_slot(hctl, (lvl - 2) % 64, tag0 + ((lvl - 2) % 4096) + 1)
                     if int(hctl[(lvl - 2) % 64, 0]) == 0:
                         done_at = lvl - 2
                         break
