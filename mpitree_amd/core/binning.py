@@ -19,7 +19,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-__all__ = ["BinMapper", "quantile_edges", "fit_bin_mapper"]
+__all__ = ["BinMapper", "TableBinMapper", "quantile_edges", "fit_bin_mapper"]
 
 MAX_BINS_LIMIT = 65536
 
@@ -72,6 +72,40 @@ class BinMapper:
             np.minimum(c, len(e) - 1, out=c)
             codes[:, f] = c
         return codes
+
+
+class TableBinMapper(BinMapper):
+    """A :class:`BinMapper` over a padded edge table ``[F, W]`` plus bin counts
+    (the device binner's host copy). The per-feature edge arrays are sliced on
+    first use: a device fit only needs ``max_n_bins`` before its level loop,
+    so no host work sits between the fit's sync and the first tree kernels."""
+
+    def __init__(self, table: np.ndarray, n_bins: np.ndarray, exact: np.ndarray, max_bins: int):
+        self._table = table
+        self._nb = np.asarray(n_bins, dtype=np.int64)
+        self._edges = None
+        self.exact = exact
+        self.max_bins = max_bins
+
+    @property
+    def edges(self) -> list:
+        if self._edges is None:
+            self._edges = [self._table[f, : self._nb[f]].copy() for f in range(self._nb.size)]
+        return self._edges
+
+    @property
+    def n_features(self) -> int:
+        return int(self._nb.size)
+
+    @property
+    def n_bins(self) -> np.ndarray:
+        return self._nb.astype(np.int32)
+
+    def padded_edges(self, dtype=np.float64) -> np.ndarray:
+        bmax = self.max_n_bins
+        out = np.array(self._table[:, :bmax], dtype=dtype)
+        out[np.arange(bmax)[None, :] >= self._nb[:, None]] = np.inf
+        return out
 
 
 def fit_bin_mapper(X: np.ndarray, max_bins=256, sample: int | None = None, seed: int = 0):

@@ -32,6 +32,7 @@ from .criterion import Criterion
 from .levelwise import GrowParams, LevelwiseBuilder, LocalComm
 from ..models.tree_arrays import TreeArrays
 from ..ops import native
+from ..utils.debug import check_device_inputs, debug_enabled, validate_tree
 from ..utils.observability import logger, profiling, roctx_range
 
 __all__ = ["FitResult", "fit_tree", "resolve_device", "AUTO_GPU_MIN_CELLS"]
@@ -244,6 +245,8 @@ def fit_tree(
             root = None
         yd = yd.contiguous()
         timings["bin"] = time.perf_counter() - t0
+        if debug_enabled():
+            check_device_inputs(codes_rm, codes_fm, nb, yd, C, regression)
         be = HipBackend()
         be.setup(codes_rm, codes_fm, yd, nb, n_bins=mapper.max_n_bins, n_classes=C,
                  criterion=crit)
@@ -312,6 +315,9 @@ def fit_tree(
     t0 = time.perf_counter()
     ta = _finalize(ta, mapper, regression, y_exp)
     timings["finalize"] = time.perf_counter() - t0
+    if debug_enabled():
+        sharded = getattr(comm, "sharded", False)  # then n is this rank's rows only
+        validate_tree(ta, n_rows=None if sharded else n, n_features=F, n_bins=mapper.n_bins)
     timings["total"] = time.perf_counter() - t_start
     if logger.isEnabledFor(logging.INFO):
         logger.info("fit: engine=%s n=%d F=%d nodes=%d depth=%d %.3f ms", eng, n, F,

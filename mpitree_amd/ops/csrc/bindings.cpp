@@ -37,7 +37,7 @@ void launch_predict(hipStream_t, const void*, bool, int64_t, int, const void*, c
 void launch_bin(hipStream_t, const void*, bool, int64_t, int, const void*, int, int,
                 const int32_t*, const uint8_t*, void*, int, void*, int, int32_t*);
 void launch_xlog2x(hipStream_t, double*, int64_t);
-void launch_label_count(hipStream_t, const int64_t*, int64_t, int64_t, int, uint32_t*);
+void launch_label_count(hipStream_t, const int64_t*, int64_t, int64_t, int, uint32_t*, bool);
 void launch_label_encode(hipStream_t, const int64_t*, int64_t, int64_t, const int64_t*, int32_t*);
 void launch_finish(hipStream_t, const void*, int64_t, const void*, int, int64_t, uint32_t*,
                    uint32_t*, const int32_t*, int, const int64_t*, int, int32_t*, const int32_t*,
@@ -300,9 +300,10 @@ PYBIND11_MODULE(_hip, m) {
                         P<int64_t>(total), P<uint8_t>(base));
   });
   m.def("label_count", [](uintptr_t s, uintptr_t y, int64_t n, int64_t lo, int R,
-                          uintptr_t counts) {
-    mt::launch_label_count(S(s), P<int64_t>(y), n, lo, R, P<uint32_t>(counts));
-  });
+                          uintptr_t counts, bool checked) {
+    mt::launch_label_count(S(s), P<int64_t>(y), n, lo, R, P<uint32_t>(counts), checked);
+  }, py::arg("s"), py::arg("y"), py::arg("n"), py::arg("lo"), py::arg("R"), py::arg("counts"),
+     py::arg("checked") = false);
   m.def("label_encode", [](uintptr_t s, uintptr_t y, int64_t n, int64_t lo, uintptr_t lut,
                            uintptr_t out) {
     mt::launch_label_encode(S(s), P<int64_t>(y), n, lo, P<int64_t>(lut), P<int32_t>(out));

@@ -28,19 +28,29 @@ constexpr int kLabLds = 8192;
 
 __global__ __launch_bounds__(256) void label_count_kernel(const int64_t* __restrict__ y,
                                                           int64_t n, int64_t lo, int R,
-                                                          uint32_t* __restrict__ counts) {
+                                                          uint32_t* __restrict__ counts,
+                                                          bool checked) {
+  // checked: the range is a guess made before the labels' min/max reached the
+  // host -- out-of-range labels are tallied in counts[R] instead of indexed
   __shared__ uint32_t h[kLabLds];
   const bool lds = R <= kLabLds;
   if (lds)
     for (int i = threadIdx.x; i < R; i += 256) h[i] = 0;
   __syncthreads();
+  uint32_t oob = 0;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const int v = (int)(y[i] - lo);
+    const int64_t d = y[i] - lo;
+    if (checked && (d < 0 || d >= R)) {
+      ++oob;
+      continue;
+    }
+    const int v = (int)d;
     if (lds)
       atomicAdd(&h[v], 1u);
     else
       atomicAdd(&counts[v], 1u);
   }
+  if (checked && oob) atomicAdd(&counts[R], oob);
   if (lds) {
     __syncthreads();
     for (int i = threadIdx.x; i < R; i += 256)
@@ -61,12 +71,15 @@ static unsigned label_grid(int64_t n) {
 }
 
 void launch_label_count(hipStream_t stream, const int64_t* y, int64_t n, int64_t lo, int R,
-                        uint32_t* counts) {
-  MT_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(uint32_t) * (size_t)R, stream));
+                        uint32_t* counts, bool checked) {
+  // checked: counts has R + 1 entries, the last one counts labels outside the range
+  MT_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(uint32_t) * (size_t)(R + (checked ? 1 : 0)),
+                              stream));
   if (n <= 0) return;
   // LDS-privatised histograms: fewer, fuller blocks; global atomics otherwise
   const unsigned g = R <= kLabLds ? std::min(label_grid(n), 512u) : label_grid(n);
-  hipLaunchKernelGGL(label_count_kernel, dim3(g), dim3(256), 0, stream, y, n, lo, R, counts);
+  hipLaunchKernelGGL(label_count_kernel, dim3(g), dim3(256), 0, stream, y, n, lo, R, counts,
+                     checked);
   MT_HIP_CHECK(hipGetLastError());
 }
 

@@ -120,6 +120,30 @@ class DeviceGrower:
         """Finish the (largest-first) job list; with several ranks each takes a
         serpentine share (0..P-1, P-1..0, ...) -- near-even row totals."""
         be, comm = self.be, self.comm
+        sim = int(os.environ.get("MPITREE_SIM_RANKS", "0"))
+        if comm is not None and comm.world_size > 1:
+            sim = 0
+        if sim > 1:
+            # diagnostic (MPITREE_SIM_RANKS=P, one process): time rank 0's
+            # serpentine share alone on the GPU, then finish the rest so the
+            # tree stays complete -- the per-rank finisher critical path of a
+            # P-GPU fit, measured on one GPU
+            k = torch.arange(d_jobs.shape[0], device=d_jobs.device)
+            lap, off = k // sim, k % sim
+            owner = torch.where(lap % 2 == 0, off, sim - 1 - off)
+            mine, rest = d_jobs[owner == 0].contiguous(), d_jobs[owner != 0].contiguous()
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            ev[0].record()
+            be.launch_finisher(mine, int(mine.shape[0]), n, self.p, be.pos_rec, be.pos_st)
+            ev[1].record()
+            keep = be._fin_keep
+            if rest.shape[0]:
+                be.launch_finisher(rest, int(rest.shape[0]), n, self.p, be.pos_rec, be.pos_st)
+            ev[2].record()
+            be._fin_keep = (keep, be._fin_keep)
+            self._sim_events = ev  # read after the assembly's sync
+            self.stats["sim_rank0_jobs"] = int(mine.shape[0])
+            return
         if comm is not None and comm.world_size > 1:
             P, r = comm.world_size, comm.rank
             k = torch.arange(d_jobs.shape[0], device=d_jobs.device)
@@ -377,6 +401,12 @@ class DeviceGrower:
             edges = edges.padded_edges()
         a = be.assemble_positions(edges, int(p.criterion), y_exp, d_edges=d_edges)
         self.timings["assemble"] = time.perf_counter() - t0
+        ev = getattr(self, "_sim_events", None)
+        if ev is not None:
+            ev[2].synchronize()
+            self.stats["sim_rank0_finisher_ms"] = ev[0].elapsed_time(ev[1])
+            self.stats["sim_rest_finisher_ms"] = ev[1].elapsed_time(ev[2])
+            self._sim_events = None
         st = a["stats"]
         ta = TreeArrays(
             feature=a["feature"], threshold=a["threshold"], threshold_bin=a["bin"],

@@ -11,11 +11,15 @@ raw values). Here a fit on the GPU needs, before the first tree level:
 
 Every host decision among these needs a small device read; issued one by one
 they cost ~6 synchronisations with host work in between, during which the
-GPU idles. :func:`prepare` interleaves them into two synchronisations: the
-edge table travels with the label range (or target scale), and the bin
-kernel's flags travel with the class counts (or target root stats). The root
-statistics then come for free and the device level loop starts without
-another round trip.
+GPU idles. :func:`prepare` batches them: with at most 256 bins the bin
+kernel is enqueued right behind the edges kernel (it reads the bin counts on
+the device), and the class counts are taken speculatively over [0, 8192) with
+an out-of-range tally, so a classification fit on integer labels needs ONE
+synchronisation (edge table, bin flags and class counts in one wait). Labels
+outside the guess, more than 256 bins and regression targets (whose
+fixed-point exponent depends on max |y|) take a second one. The root
+statistics come for free and the device level loop starts without another
+round trip.
 """
 
 from __future__ import annotations
@@ -31,6 +35,7 @@ from .hip_backend import DeviceBinning, _pinned_copy, _stream, _uploader
 __all__ = ["Prepared", "prepare"]
 
 _LUT_MAX = 1 << 22  # label ranges beyond this fall back to torch.unique
+_SPEC_R = 8192  # guessed label range [0, _SPEC_R) (the count kernel's LDS histogram)
 
 
 @dataclass
@@ -60,23 +65,38 @@ class _Labels:
             torch.is_tensor(y) and y.is_cuda and y.dim() == 1 and y.shape[0] == n and n > 0
             and not torch.is_floating_point(y) and y.dtype != torch.bool
         )
+        self._counts = None
         if self.dev_path:
             self.yl = (y if y.dtype == torch.int64 else y.long()).contiguous()
-            self._mm = _pinned_copy(torch.stack(torch.aminmax(self.yl)), "prep.lab.mm")
+            # speculate that the labels lie in [0, _SPEC_R): the counts (and an
+            # out-of-range tally) then arrive with the fit's first sync
+            self.spec = torch.empty(_SPEC_R + 1, dtype=torch.int32, device=dev)
+            native.hip().label_count(_stream(), self.yl.data_ptr(), n, 0, _SPEC_R,
+                                     self.spec.data_ptr(), checked=True)
+            self._spec = _pinned_copy(self.spec, "prep.lab.spec")
+            self.enc0 = self.yl.to(torch.int32)  # the codes when the labels are 0..C-1
 
-    def after_first_sync(self):
+    def after_first_sync(self) -> bool:
+        """True when the labels need another device round (outside the guess)."""
         if not self.dev_path:
-            return
-        lo, hi = int(self._mm[0]), int(self._mm[1])
+            return False
+        if int(self._spec[_SPEC_R]) == 0:
+            self.lo, self.R = 0, _SPEC_R
+            self._counts = self._spec[:_SPEC_R]
+            return False
+        self.enc0 = None
+        mm = torch.stack(torch.aminmax(self.yl)).cpu().numpy()  # one extra sync
+        lo, hi = int(mm[0]), int(mm[1])
         R = hi - lo + 1
         if R > _LUT_MAX:
             self.dev_path = False
-            return
+            return False
         self.lo, self.R = lo, R
         self.counts = torch.empty(R, dtype=torch.int32, device=self.dev)
         native.hip().label_count(_stream(), self.yl.data_ptr(), self.n, lo, R,
                                  self.counts.data_ptr())
         self._counts = _pinned_copy(self.counts, "prep.lab.counts")
+        return True
 
     def finish(self):
         """(classes, int32 device codes, root class counts)."""
@@ -91,7 +111,10 @@ class _Labels:
         present = counts > 0
         idx = np.nonzero(present)[0]
         classes = (idx + self.lo).astype(_np_dtype(self.y.dtype))
-        if self.lo == 0 and present.all():
+        last = int(idx[-1]) if idx.size else -1
+        if self.lo == 0 and last + 1 == idx.size and self.enc0 is not None:
+            enc = self.enc0
+        elif self.lo == 0 and present.all():
             enc = self.yl.to(torch.int32)
         else:
             (d_lut,) = _uploader(self.dev)(np.cumsum(present) - 1)
@@ -115,9 +138,10 @@ class _Targets:
         elif self.dev_path:
             self.dev_path = False
 
-    def after_first_sync(self):
+    def after_first_sync(self) -> bool:
+        """True: the fixed-point targets need another sync (always, on the device path)."""
         if not self.dev_path:
-            return
+            return False
         if not self._st[1]:
             raise ValueError("Input y contains NaN or infinity.")
         self.e = self.exponent(float(self._st[0]), self.n)
@@ -125,6 +149,7 @@ class _Targets:
         self.yi = torch.round(torch.ldexp(self.yd, scale)).long()
         mn, mx = torch.aminmax(self.yi)
         self._root = _pinned_copy(torch.stack([self.yi.sum(), mn, mx]), "prep.reg.root")
+        return True
 
     def finish(self):
         """(int64 device targets, exponent, root {count, sum, min, max})."""
@@ -153,10 +178,13 @@ def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
     lab = (_Targets(y, n, dev, encode_targets, exponent) if regression
            else _Labels(y, n, dev, encode_labels))
     binning = DeviceBinning(Xd, max_bins)
-    stream.synchronize()  # sync 1: edge table + label range / target scale
-    binning.launch_bin()
-    lab.after_first_sync()
-    stream.synchronize()  # sync 2: bin flags + class counts / target root stats
+    if binning.early:  # <= 256 bins: codes, flags and edges all land by sync 1
+        binning.launch_bin_early()
+    stream.synchronize()  # sync 1: edge table (+ bin flags) + label counts / target scale
+    need2 = lab.after_first_sync()
+    binning.launch_bin()  # host tables; enqueues the bin kernel unless already done
+    if need2 or not binning.early:
+        stream.synchronize()  # sync 2: bin flags / class counts / target root stats
     mapper, codes_rm, codes_fm, nb = binning.finish()
     if regression:
         yenc, y_exp, root = lab.finish()

@@ -14,7 +14,7 @@ import os
 import numpy as np
 import torch
 
-from ..core.binning import BinMapper, MAX_BINS_LIMIT
+from ..core.binning import MAX_BINS_LIMIT, BinMapper, TableBinMapper
 from ..core.criterion import Criterion
 from . import native
 
@@ -155,20 +155,39 @@ class DeviceBinning:
                      codes_fm.data_ptr(), cb, flags.data_ptr(), estride=int(edges_t.stride(0)))
         return codes_rm, codes_fm, flags
 
-    def launch_bin(self):
-        """Enqueue the bin kernel (after a sync covering ``__init__``'s copy)."""
+    @property
+    def early(self) -> bool:
+        """At most 256 bins: one code byte whatever the per-feature counts, so
+        the bin kernel can be enqueued before the edge table reaches the host."""
+        return self.limit <= 256
+
+    def launch_bin_early(self):
+        """Enqueue the bin kernel straight after the edges kernel (``early``):
+        it reads the bin counts from the device, so the fit's first sync covers
+        edges, codes and flags together."""
+        self.codes_rm, self.codes_fm, flags = self._run_bin(self.edges, self.nb, self.exact,
+                                                            self.limit)
+        self._host_flags = _pinned_copy(flags, "bin.flags")
+        self._launched = True
+
+    def host_tables(self):
+        """Host edge table and ``BinMapper`` (after a sync covering ``__init__``'s copy)."""
         F, L = self.F, self.limit
         host = self._host_pack
         self.host_edges = host[: F * L].reshape(F, L).copy()
         self.host_nb = host[F * L : F * L + F].astype(np.int64)
         self.host_exact = host[F * L + F :].astype(bool)
         self.bmax = int(max(1, self.host_nb.max())) if F else 1
-        self.codes_rm, self.codes_fm, flags = self._run_bin(self.edges, self.nb, self.exact,
-                                                            self.bmax)
-        self._host_flags = _pinned_copy(flags, "bin.flags")
-        he, hn = self.host_edges, self.host_nb
-        self.mapper = BinMapper(edges=[he[f, : hn[f]].copy() for f in range(F)],
-                                exact=self.host_exact.copy(), max_bins=L)
+        self.mapper = TableBinMapper(self.host_edges, self.host_nb, self.host_exact.copy(), L)
+
+    def launch_bin(self):
+        """Enqueue the bin kernel (after a sync covering ``__init__``'s copy)."""
+        self.host_tables()
+        if not getattr(self, "_launched", False):
+            self.codes_rm, self.codes_fm, flags = self._run_bin(self.edges, self.nb, self.exact,
+                                                                self.bmax)
+            self._host_flags = _pinned_copy(flags, "bin.flags")
+            self._launched = True
 
     def finish(self):
         """(mapper, codes_rm, codes_fm, nbins_dev) after a sync covering the flags copy."""

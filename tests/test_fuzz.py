@@ -1,0 +1,159 @@
+"""Property-based (hypothesis) fuzzing of every builder against the
+reference-semantics oracle (``core/reference.py``: exact thresholds, first
+minimum-cost threshold, lowest feature on ties, leaf on empty children --
+``mpitree/tree/decision_tree.py:53-166``) and of the GPU path against the
+host path (shapes including n = 1, F not a multiple of a tile,
+heavy ties, one class, every stopping rule)."""
+
+import os
+
+import numpy as np
+import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
+from mpitree_amd.core.backend_numpy import NumpyBackend
+from mpitree_amd.core.binning import fit_bin_mapper
+from mpitree_amd.core.criterion import Criterion
+from mpitree_amd.core.levelwise import GrowParams, LevelwiseBuilder
+from mpitree_amd.core.reference import fit_reference
+from mpitree_amd.ops import native
+
+
+@st.composite
+def problems(draw, max_n=60, regression=False):
+    n = draw(st.integers(1, max_n))
+    F = draw(st.integers(1, 5))
+    levels = draw(st.integers(1, 7))
+    seed = draw(st.integers(0, 2**31 - 1))
+    rng = np.random.default_rng(seed)
+    X = rng.integers(0, levels, size=(n, F)).astype(np.float64) * 0.5 - 1.0
+    if regression:
+        y = rng.integers(-20, 20, size=n).astype(np.float64) / 4.0
+        C = 0
+    else:
+        C = draw(st.integers(1, 4))
+        y = rng.integers(0, C, size=n)
+    hp = dict(
+        crit=Criterion.SQUARED_ERROR if regression else draw(
+            st.sampled_from([Criterion.ENTROPY, Criterion.GINI])),
+        md=draw(st.sampled_from([None, 0, 1, 2, 4])),
+        mss=draw(st.integers(2, 6)),
+        msl=draw(st.integers(1, 3)),
+    )
+    return X, y, C, hp
+
+
+def _oracle(X, y, C, hp):
+    mapper = fit_bin_mapper(X)
+    codes = mapper.transform(X)
+    if hp["crit"] == Criterion.SQUARED_ERROR:
+        from mpitree_amd.core.fit import _encode_targets
+
+        yv, _ = _encode_targets(y, len(y))
+        C = 0
+    else:
+        _, yv = np.unique(y, return_inverse=True)
+        C = int(yv.max()) + 1
+    ref = fit_reference(codes, yv, n_classes=C, n_bins=mapper.max_n_bins, criterion=hp["crit"],
+                        max_depth=hp["md"], min_samples_split=hp["mss"],
+                        min_samples_leaf=hp["msl"])
+    return mapper, codes, yv, C, ref
+
+
+def _params(hp, fr=0):
+    return GrowParams(criterion=hp["crit"], max_depth=hp["md"], min_samples_split=hp["mss"],
+                      min_samples_leaf=hp["msl"], finisher_rows=fr)
+
+
+FUZZ = settings(max_examples=60, deadline=None,
+                suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+
+
+@FUZZ
+@given(problems(), st.sampled_from([0, 3, 17]))
+def test_fuzz_levelwise_numpy_vs_oracle(prob, fr):
+    X, y, C, hp = prob
+    mapper, codes, yv, C, ref = _oracle(X, y, C, hp)
+    be = NumpyBackend()
+    be.setup(codes, yv, n_bins=mapper.max_n_bins, n_classes=C, criterion=hp["crit"])
+    ta = LevelwiseBuilder(be, _params(hp, fr)).fit(len(yv), C, X.shape[1])
+    assert ta.equal(ref)
+
+
+@pytest.mark.skipif(not native.has_cpu(), reason="native module not built")
+@FUZZ
+@given(problems())
+def test_fuzz_native_vs_oracle(prob):
+    from mpitree_amd.ops.cpu_builder import fit_native
+
+    X, y, C, hp = prob
+    mapper, codes, yv, C, ref = _oracle(X, y, C, hp)
+    assert fit_native(codes, yv, mapper, C, _params(hp), n_threads=1).equal(ref)
+
+
+@pytest.mark.skipif(not native.has_cpu(), reason="native module not built")
+@FUZZ
+@given(problems(regression=True))
+def test_fuzz_regression_native_vs_oracle(prob):
+    from mpitree_amd.ops.cpu_builder import fit_native
+
+    X, y, C, hp = prob
+    mapper, codes, yv, C, ref = _oracle(X, y, C, hp)
+    ta = fit_native(codes, yv, mapper, 0, _params(hp), n_threads=1)
+    assert ta.equal(ref)
+    assert np.array_equal(ta.meta["sum_fixed"], ref.meta["sum_fixed"])
+
+
+@FUZZ
+@given(problems())
+def test_fuzz_estimator_predict_consistent(prob):
+    """Training rows land in leaves whose counts include their label."""
+    X, y, C, hp = prob
+    clf = DecisionTreeClassifier(criterion=hp["crit"].name.lower(), max_depth=hp["md"],
+                                 min_samples_split=hp["mss"], min_samples_leaf=hp["msl"],
+                                 device="cpu").fit(X, y)
+    proba = clf.predict_proba(X)
+    assert proba.shape == (len(y), len(clf.classes_))
+    idx = np.searchsorted(clf.classes_, y)
+    assert (proba[np.arange(len(y)), idx] > 0).all()
+    assert clf.predict(X).shape == (len(y),)
+
+
+# ---------------------------------------------------------------- GPU vs host
+def _gpu_vs_cpu(prob, fr, regression):
+    X, y, C, hp = prob
+    kw = dict(max_depth=hp["md"], min_samples_split=hp["mss"], min_samples_leaf=hp["msl"])
+    if regression:
+        mk = lambda d: DecisionTreeRegressor(device=d, **kw)  # noqa: E731
+    else:
+        mk = lambda d: DecisionTreeClassifier(criterion=hp["crit"].name.lower(),  # noqa: E731
+                                              device=d, **kw)
+    old = os.environ.get("MPITREE_FINISHER_ROWS")
+    os.environ["MPITREE_FINISHER_ROWS"] = str(fr)
+    try:
+        g = mk("cuda").fit(X, y)
+    finally:
+        if old is None:
+            os.environ.pop("MPITREE_FINISHER_ROWS", None)
+        else:
+            os.environ["MPITREE_FINISHER_ROWS"] = old
+    c = mk("cpu").fit(X, y)
+    assert g.fit_stats_["engine"].startswith("hip")
+    assert g._arrays.equal(c._arrays, check_impurity=False)
+    np.testing.assert_array_equal(g.predict(X), c.predict(X))
+
+
+@pytest.mark.gpu
+@settings(max_examples=40, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(problems(max_n=300), st.sampled_from([2, 9, 64, 4096]))
+def test_fuzz_gpu_matches_host(prob, fr):
+    _gpu_vs_cpu(prob, fr, False)
+
+
+@pytest.mark.gpu
+@settings(max_examples=25, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(problems(max_n=300, regression=True), st.sampled_from([2, 9, 4096]))
+def test_fuzz_gpu_regression_matches_host(prob, fr):
+    _gpu_vs_cpu(prob, fr, True)
