@@ -537,7 +537,7 @@ class HipBackend:
         for name, dt, w in cols8 + cols4:
             nb = N * w * (8 if dt in (torch.int64, torch.float64) else 4)
             t = host[o : o + nb].view(dt)
-            out[name] = (t.view(N, w) if w > 1 else t).numpy()
+            out[name] = (t.view(N, w) if (w > 1 or name == "stats") else t).numpy()
             o += nb
         self.pos_rec = self.pos_st = None
         return out
