@@ -131,6 +131,13 @@ class NumpyBackend:
         return out
 
     # ------------------------------------------------------------ partition
+    # row permutation (level checkpoints, utils/level_checkpoint.py)
+    def get_rows(self) -> np.ndarray:
+        return self.idx.copy()
+
+    def set_rows(self, rows) -> None:
+        self.idx[:] = np.asarray(rows, dtype=self.idx.dtype)
+
     def partition(self, starts, counts, features, bins, need_counts=True):
         """Move each split node's rows so left rows come first; return local left counts."""
         nl = np.zeros(len(starts), dtype=np.int64)

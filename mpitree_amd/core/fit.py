@@ -160,6 +160,19 @@ def _encode_targets(y, n):
     return np.round(np.ldexp(y, e)).astype(np.int64), e
 
 
+def _level_checkpoint(path, codes, y, params, n_classes):
+    """A LevelCheckpoint for ``fit(..., checkpoint=path)`` (None: no checkpointing)."""
+    if path is None:
+        return None
+    from ..utils.level_checkpoint import LevelCheckpoint, problem_signature
+
+    if isinstance(path, LevelCheckpoint):  # tests pass a configured instance
+        if not path.signature:
+            path.signature = problem_signature(codes, y, params, n_classes)
+        return path
+    return LevelCheckpoint(path, problem_signature(codes, y, params, n_classes))
+
+
 def _finalize(ta: TreeArrays, mapper: BinMapper, regression: bool, y_exp: int) -> TreeArrays:
     if ta.meta.pop("final", False):  # device assembly produced finished columns
         return ta
@@ -193,6 +206,7 @@ def fit_tree(
     comm=None,
     finisher_rows=None,
     engine: str | None = None,
+    checkpoint=None,
 ) -> FitResult:
     t_start = time.perf_counter()
     X = _validate_X(X)
@@ -262,7 +276,8 @@ def fit_tree(
         params.finisher_rows = int(finisher_rows)
         from ..ops.device_grower import DeviceGrower, device_loop_supported
 
-        if device_loop_supported(be, params, comm):
+        ckpt = _level_checkpoint(checkpoint, codes_rm, yd, params, C)
+        if ckpt is None and device_loop_supported(be, params, comm):
             if comm.world_size > 1:  # the redundant top levels use the 1-GPU split point
                 params.finisher_rows = min(default_fr, be.max_finisher_rows)
             builder = DeviceGrower(be, params, comm)
@@ -271,7 +286,7 @@ def fit_tree(
                                  d_edges=prep.d_edges64)
             eng = "hip-device-loop"
         else:
-            builder = LevelwiseBuilder(be, params, comm)
+            builder = LevelwiseBuilder(be, params, comm, checkpoint=ckpt)
             with roctx_range("mpitree.grow"):
                 ta = builder.fit(hi - lo, C, F, edges=mapper.padded_edges(), y_exp=y_exp)
             eng = "hip-levelwise"
@@ -291,6 +306,7 @@ def fit_tree(
         timings["bin"] = time.perf_counter() - t0
         use_native = (
             engine in (None, "native") and comm.world_size == 1 and native.has_cpu()
+            and checkpoint is None  # the native builder is depth-first: no level state
         )
         if use_native:
             from ..ops.cpu_builder import fit_native
@@ -304,7 +320,9 @@ def fit_tree(
             be = NumpyBackend()
             be.setup(codes, yh, n_bins=mapper.max_n_bins, n_classes=C, criterion=crit)
             params.finisher_rows = int(finisher_rows or 0)
-            builder = LevelwiseBuilder(be, params, comm)
+            builder = LevelwiseBuilder(be, params, comm,
+                                       checkpoint=_level_checkpoint(checkpoint, codes, yh,
+                                                                    params, C))
             ta = builder.fit(hi - lo, C, F, edges=mapper.padded_edges())
             eng = "numpy-levelwise"
             timings.update(builder.timings)

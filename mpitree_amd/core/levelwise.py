@@ -85,6 +85,9 @@ class LocalComm:
         return {}
 
 
+_DEFERRED = ("id", "start", "count", "m", "depth", "pos")
+
+
 class _Table:
     """Growing node table (unordered ids; pre-ordered at the end)."""
 
@@ -160,10 +163,14 @@ def _host_threads() -> int:
 class LevelwiseBuilder:
     """Drive one fit through ``backend`` with communication hooks ``comm``."""
 
-    def __init__(self, backend, params: GrowParams, comm=None):
+    def __init__(self, backend, params: GrowParams, comm=None, checkpoint=None):
         self.be = backend
         self.p = params
         self.comm = comm or LocalComm()
+        # LevelCheckpoint (utils/level_checkpoint.py): state saved after every level
+        self.ckpt = checkpoint
+        if checkpoint is not None and self.comm.world_size != 1:
+            raise ValueError("level checkpoints are supported for single-process fits")
         self.timings: dict = {}
         self.stats: dict = {}
 
@@ -200,6 +207,9 @@ class LevelwiseBuilder:
         f_lo, f_hi = comm.feature_range(n_features)
         F_h = f_hi - f_lo
         tab = _Table(C)
+        state = self.ckpt.load() if self.ckpt is not None else None
+        if state is not None:
+            return self._resume(state, tab, n_local, C, F_h, f_lo, f_hi, reg)
 
         t0 = time.perf_counter()
         st = comm.reduce_stats(be.segment_stats(np.array([0]), np.array([n_local])), reg)
@@ -214,7 +224,7 @@ class LevelwiseBuilder:
         # backend lays the tree out on the device and compacts it in one pass.
         self._device_asm = (
             hasattr(be, "begin_positions") and comm.world_size == 1 and edges is not None
-            and os.environ.get("MPITREE_DEVICE_ASSEMBLY", "1") != "0"
+            and os.environ.get("MPITREE_DEVICE_ASSEMBLY", "1") != "0" and self.ckpt is None
         )
         # MPITREE_FIN_OVERLAP=1 launches each level's finisher batch at once on a
         # side stream (it then competes with the level kernels for CUs)
@@ -234,9 +244,23 @@ class LevelwiseBuilder:
         )
         if self._terminal(np.zeros(1), np.array([m_root]), rstats, minmax)[0]:
             fr = {k: v[:0] for k, v in fr.items()}
-        deferred = {k: [] for k in ("id", "start", "count", "m", "depth", "pos")}
+        deferred = {k: [] for k in _DEFERRED}
+        return self._grow(tab, fr, deferred, 0, C, F_h, f_lo, f_hi, reg)
+
+    def _resume(self, state, tab, n_local, C, F_h, f_lo, f_hi, reg) -> TreeArrays:
+        """Continue a fit from its last saved level (utils/level_checkpoint.py)."""
+        self._device_asm = self._overlap = False
+        ck = self.ckpt
+        ck.restore_table(state, tab)
+        self.be.set_rows(state["rows"])
+        fr = ck.restore_frontier(state)
+        deferred = ck.restore_deferred(state, _DEFERRED)
+        self.stats["resumed_from_level"] = int(state["level"][0])
+        return self._grow(tab, fr, deferred, int(state["level"][0]), C, F_h, f_lo, f_hi, reg)
+
+    def _grow(self, tab, fr, deferred, levels, C, F_h, f_lo, f_hi, reg) -> TreeArrays:
+        p, be, comm = self.p, self.be, self.comm
         prev_hist = None
-        levels = 0
         while fr["id"].size:
             levels += 1
             K = fr["id"].size
@@ -350,6 +374,8 @@ class LevelwiseBuilder:
                 sib=sib[keep_idx],
             )
             prev_hist = hist
+            if self.ckpt is not None:
+                self.ckpt.save(levels, tab, fr, deferred, be.get_rows())
         self.stats["levels"] = levels
         if deferred["id"]:
             d = {k: np.concatenate(v) for k, v in deferred.items()}
@@ -363,6 +389,9 @@ class LevelwiseBuilder:
         t0 = time.perf_counter()
         ta = self._to_arrays(tab)
         self.timings["assemble"] = time.perf_counter() - t0
+        if self.ckpt is not None:
+            self.stats["checkpoint_levels_saved"] = self.ckpt.saved_levels
+            self.ckpt.clear()
         return ta
 
     # ------------------------------------------------------------ finisher

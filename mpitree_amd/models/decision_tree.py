@@ -107,8 +107,14 @@ class _BaseTree(BaseEstimator):
         self._device_tree = None
         return self
 
-    def fit(self, X, y):
-        """Grow the tree on ``X`` (n, F) and targets ``y`` (n,)."""
+    def fit(self, X, y, *, checkpoint=None):
+        """Grow the tree on ``X`` (n, F) and targets ``y`` (n,).
+
+        ``checkpoint``: a file path; the level-wise builder saves its state
+        there after every level and a re-run of the same fit resumes from the
+        last saved level (``utils/level_checkpoint.py``; single process)."""
+        if checkpoint is not None:
+            return self._fit_impl(X, y, checkpoint=checkpoint)
         return self._fit_impl(X, y)
 
     # ------------------------------------------------------------ tree views

@@ -1,0 +1,132 @@
+"""Level-granular checkpoint / resume of a tree fit.
+
+The reference's only checkpoint is the pickled estimator *after* a fit
+(``mpitree/tree/_base.py:22-57``); a fit that dies restarts from the root.
+``fit(X, y, checkpoint=path)`` runs the level-wise builder
+(:class:`~mpitree_amd.core.levelwise.LevelwiseBuilder`) and, after every
+completed level, atomically writes the grower's state to ``path``:
+
+* the node table grown so far (features, bins, links, depths, row counts,
+  class counts / target sums, pre-order positions),
+* the frontier (start, count, rows, depth, position of every open node) and
+  the subtrees deferred to the finisher,
+* the row permutation (rows grouped by frontier node),
+* a signature of the problem (shapes, hyperparameters, a digest of a strided
+  sample of the binned features and targets), so a checkpoint is never
+  resumed against different data.
+
+A later ``fit`` with the same ``path`` and problem resumes after the last
+saved level; its tree is identical to an uninterrupted fit's (the sibling
+subtraction of the resumed level is replaced by histogram builds, which give
+the same integer histograms). The file is removed when the fit completes.
+Single-process fits only (the state is per rank).
+"""
+
+from __future__ import annotations
+
+import hashlib
+import os
+
+import numpy as np
+
+__all__ = ["LevelCheckpoint", "problem_signature"]
+
+_TAB = ("feature", "tbin", "left", "right", "depth", "nsamp", "stats", "pos")
+_FR = ("id", "pos", "start", "count", "m", "depth")
+
+
+def problem_signature(codes, y, params, n_classes: int) -> str:
+    """Digest of the fit's inputs (strided sample of codes / targets) and params."""
+    h = hashlib.sha256()
+    n = int(codes.shape[0])
+    step = max(1, n // 4096)
+
+    def host(a):
+        try:
+            import torch
+
+            if torch.is_tensor(a):
+                return a[::step].cpu().numpy()
+        except ImportError:  # pragma: no cover
+            pass
+        return np.asarray(a)[::step]
+
+    h.update(repr((tuple(codes.shape), int(n_classes), int(params.criterion), params.max_depth,
+                   params.min_samples_split, params.min_samples_leaf)).encode())
+    h.update(np.ascontiguousarray(host(codes)).tobytes())
+    h.update(np.ascontiguousarray(host(y)).tobytes())
+    return h.hexdigest()
+
+
+class LevelCheckpoint:
+    """One fit's checkpoint file (``path``, ``.npz``)."""
+
+    def __init__(self, path, signature: str = ""):
+        self.path = os.fspath(path)
+        self.signature = signature
+        self.fail_after_level = None  # tests: raise after saving this level
+        self.saved_levels = 0
+        self.resumed_from = None
+
+    # ---------------------------------------------------------------- save
+    def save(self, level: int, tab, fr: dict, deferred: dict, rows: np.ndarray) -> None:
+        arrs = {"sig": np.frombuffer(self.signature.encode(), np.uint8),
+                "level": np.array([level], np.int64), "tab_n": np.array([tab.n], np.int64),
+                "rows": rows}
+        for k in _TAB:
+            arrs["tab_" + k] = getattr(tab, k)[: tab.n]
+        for k in _FR:
+            arrs["fr_" + k] = np.asarray(fr[k])
+        for k, parts in deferred.items():
+            arrs["def_" + k] = (np.concatenate(parts) if parts
+                                else np.zeros(0, np.int64))
+        tmp = self.path + ".tmp.npz"
+        np.savez(tmp, **arrs)
+        os.replace(tmp, self.path)  # atomic: a crash leaves the previous level
+        self.saved_levels += 1
+        if self.fail_after_level is not None and level >= self.fail_after_level:
+            raise CheckpointInterrupt(f"interrupted after level {level} (test hook)")
+
+    # ---------------------------------------------------------------- load
+    def load(self):
+        """The saved state as a dict, or None (no file / different problem)."""
+        if not os.path.exists(self.path):
+            return None
+        with np.load(self.path, allow_pickle=False) as z:
+            if bytes(z["sig"]).decode() != self.signature:
+                return None
+            st = {k: z[k] for k in z.files}
+        self.resumed_from = int(st["level"][0])
+        return st
+
+    def restore_table(self, st, tab) -> None:
+        n = int(st["tab_n"][0])
+        tab._grow(n)
+        for k in _TAB:
+            getattr(tab, k)[:n] = st["tab_" + k]
+        tab.n = n
+
+    @staticmethod
+    def restore_frontier(st) -> dict:
+        fr = {k: np.asarray(st["fr_" + k], np.int64) for k in _FR}
+        K = fr["id"].size
+        fr["src"] = np.full(K, -1, np.int64)  # resumed level: every histogram is built
+        fr["sib"] = np.full(K, -1, np.int64)
+        return fr
+
+    @staticmethod
+    def restore_deferred(st, keys) -> dict:
+        out = {}
+        for k in keys:
+            a = st.get("def_" + k)
+            out[k] = [np.asarray(a, np.int64)] if a is not None and a.size else []
+        return out
+
+    def clear(self) -> None:
+        for p in (self.path, self.path + ".tmp.npz"):
+            if os.path.exists(p):
+                os.remove(p)
+
+
+class CheckpointInterrupt(RuntimeError):
+    """Raised by the ``fail_after_level`` test hook after a checkpoint write."""
