@@ -118,7 +118,8 @@ def main(argv=None):
             "dtype": "fp32",
             "dtype_detail": "fp32 features (exact data-value thresholds), int32 histogram "
                             "counts, fp64 split criterion",
-            "data": "synthetic (on-device, 256-level quantized features, random-init labels)",
+            "data": "synthetic (generated on device: 256-level quantized features, labels from "
+                    "a random linear + interaction score with Gaussian noise)",
             "config": {
                 "name": CONFIG if not a.regression else CONFIG_REG,
                 "model": f"DecisionTree{'Regressor' if a.regression else 'Classifier'}"

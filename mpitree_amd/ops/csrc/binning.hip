@@ -259,7 +259,9 @@ __global__ __launch_bounds__(256) void bin_kernel(const XT* __restrict__ X, int6
     const int r = e / kBinFt, fl = e % kBinFt;
     ok[k] = r < rows && fl < nf;
     v[k] = ok[k] ? X[(r0 + r) * F + f0 + fl] : (XT)0;
-    nb[k] = s_nb[fl];
+    // no search for padding elements: with global edges (kLds false) a lane of
+    // a feature past F would read edges rows beyond the table
+    nb[k] = ok[k] ? s_nb[fl] : 0;
     pos[k] = 0;  // number of edges < v (lower_bound)
   }
   for (int step = steps0; step > 0; step >>= 1) {

@@ -32,8 +32,11 @@
 
 namespace mt {
 
-constexpr int kFinThreads = 512;
-constexpr int kFinWaves = kFinThreads / kWave;
+// threads per finisher workgroup: 512 (two per CU); 1024 (one per CU, twice the
+// waves per job) targets ranks of a multi-GPU fit, which finish ~1/P of the jobs
+// and are bound by per-job latency rather than throughput (bench/sim_ranks.py)
+constexpr int kFinThreadsSmall = 512;
+constexpr int kFinThreadsBig = 1024;
 constexpr int kFinStack = 40;    // >= log2(max job rows) + 2
 constexpr int kFinMaxC = 16;     // classes supported by the finisher
 constexpr int kFinTab = 1024;    // LDS x*log2(x) entries
@@ -59,7 +62,7 @@ struct FinRowLab {
 // jobs: int64 [J][5 + C] = {start, count, depth, base, buffer, counts[C]}
 // node_i32: [slots][6] = {feature, bin, left, right, depth, n}; node_cnt: [slots][C]
 
-template <typename CodeT, bool kC2>
+template <typename CodeT, bool kC2, int kFinThreads>
 __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))) void finish_cls_kernel(
     const uint32_t* __restrict__ codes_rm, int64_t row_words, const CodeT* __restrict__ codes_fm,
     int64_t n_rows, uint32_t* __restrict__ buf0, uint32_t* __restrict__ buf1,
@@ -71,6 +74,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
     int64_t* __restrict__ tiny, int32_t* __restrict__ tiny_count, int64_t* __restrict__ prof) {
   // prof (optional): per workgroup {wall start, wall end, nodes, rows, cycles in
   // histogram, scan, partition, rest} -- the finisher's own phase profile
+  constexpr int kFinWaves = kFinThreads / kWave;
   extern __shared__ __align__(16) uint32_t hist[];  // [F][B*W + 1] packed class pairs
   // x*log2(x) table: fp64 entries (generic path) or, for C <= 2, twice as many
   // fp32 entries that drive the approximate first pass of the split scan
@@ -1229,7 +1233,8 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                    int max_depth, int64_t mss, int64_t msl, const double* xtab,
                    const float* xtabf, int xtab_n,
                    int32_t* node_i32, int32_t* node_cnt, int32_t* job_root, int grid,
-                   int tiny_rows, int64_t* tiny, int tiny_grid, int64_t* prof) {
+                   int tiny_rows, int64_t* tiny, int tiny_grid, int64_t* prof, int fin_threads,
+                   int n_cu) {
   // counter: int32 [4] = {job cursor, tiny count, tiny cursor, -}, zeroed by the
   // host. node_i32 / node_cnt are indexed by pre-order position (jobs[j][3] is
   // job j's root position); rows a fit never writes keep n = 0 (host memset).
@@ -1240,14 +1245,24 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   tiny_rows = std::min(tiny_rows, kTinyRows);
   FinRowLab rl{lab_shift ? ((1u << lab_shift) - 1u) : 0xffffffffu, lab_shift};
   const size_t lds = (size_t)finish_lds_bytes(F, B, C);
-#define MT_FIN(CT, C2)                                                                        \
-  MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_cls_kernel<CT, C2>,                    \
+  // fin_threads: 1024 selects the one-workgroup-per-CU variant (MPITREE_FIN_THREADS,
+  // opt-in while it is being measured), anything else the 512-thread kernel
+  const bool big = fin_threads == kFinThreadsBig;
+  if (big) grid = std::min(grid, n_cu);
+#define MT_FIN_NT(CT, C2, NT)                                                                 \
+  MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_cls_kernel<CT, C2, NT>,                \
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));    \
-  hipLaunchKernelGGL((finish_cls_kernel<CT, C2>), dim3(grid), dim3(kFinThreads), lds, stream, \
+  hipLaunchKernelGGL((finish_cls_kernel<CT, C2, NT>), dim3(grid), dim3(NT), lds, stream,      \
                      (const uint32_t*)codes_rm, row_words, (const CT*)codes_fm, n_rows, buf0, \
                      buf1, y, rl, jobs, J, counter, nbins, F, B, C, crit, max_depth, mss,     \
-                     msl, xtab, xtabf, xtab_n, node_i32, node_cnt, job_root, tiny_rows,           \
+                     msl, xtab, xtabf, xtab_n, node_i32, node_cnt, job_root, tiny_rows,       \
                      tiny, counter + 1, prof);
+#define MT_FIN(CT, C2)                   \
+  if (big) {                             \
+    MT_FIN_NT(CT, C2, kFinThreadsBig)    \
+  } else {                               \
+    MT_FIN_NT(CT, C2, kFinThreadsSmall)  \
+  }
   if (code_bytes == 1) {
     if (C <= 2) {
       MT_FIN(uint8_t, true)
@@ -1262,6 +1277,7 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
     }
   }
 #undef MT_FIN
+#undef MT_FIN_NT
   MT_HIP_CHECK(hipGetLastError());
   if (tiny_rows > 0) {
     const bool sorted = C <= 2 && getenv_int("MPITREE_TINY_SORTED", 1) != 0;

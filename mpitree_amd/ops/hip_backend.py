@@ -589,7 +589,8 @@ class HipBackend:
                         self.xtabf.data_ptr(), XTAB_N,
                         rec.data_ptr(), cnt.data_ptr(), job_root.data_ptr(), grid,
                         tiny_rows, tiny.data_ptr(), 4 * N_CU,
-                        0 if prof is None else prof.data_ptr())
+                        0 if prof is None else prof.data_ptr(),
+                        int(os.environ.get("MPITREE_FIN_THREADS", 0)), N_CU)
         self._fin_keep = (counter, job_root, tiny, d_jobs)
         if prof is not None:
             self.last_finisher_prof = prof.cpu().numpy()

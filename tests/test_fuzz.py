@@ -67,7 +67,9 @@ def _params(hp, fr=0):
                       min_samples_leaf=hp["msl"], finisher_rows=fr)
 
 
-FUZZ = settings(max_examples=60, deadline=None,
+# derandomized: every run (here, on the GPU box, at round end) draws the same
+# examples, so a failure is reproducible and a pass means the same coverage
+FUZZ = settings(max_examples=60, deadline=None, derandomize=True,
                 suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
 
 
@@ -146,14 +148,16 @@ def _gpu_vs_cpu(prob, fr, regression):
 
 
 @pytest.mark.gpu
-@settings(max_examples=40, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@settings(max_examples=40, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow])
 @given(problems(max_n=300), st.sampled_from([2, 9, 64, 4096]))
 def test_fuzz_gpu_matches_host(prob, fr):
     _gpu_vs_cpu(prob, fr, False)
 
 
 @pytest.mark.gpu
-@settings(max_examples=25, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@settings(max_examples=25, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.too_slow])
 @given(problems(max_n=300, regression=True), st.sampled_from([2, 9, 4096]))
 def test_fuzz_gpu_regression_matches_host(prob, fr):
     _gpu_vs_cpu(prob, fr, True)
