@@ -352,14 +352,17 @@ class _ParallelMixin:
         )
         if getattr(comm, "world_size", 1) == 1:
             return self._fit_impl(X, y, comm=comm, **comm.fit_kwargs())
-        # pre-flight: a rank that cannot start (bad input, injected fault) makes
-        # every rank raise instead of leaving the others blocked in a collective
+        # pre-flight (fault injection / MPITREE_PREFLIGHT=1): a rank that cannot
+        # start makes every rank raise instead of leaving the others blocked in a
+        # collective. Off by default: every rank validates the same replicated
+        # input identically, and the check costs a host-synchronising all-reduce
         error = None
-        try:
-            maybe_inject_fault(comm.rank)
-        except Exception as e:
-            error = e
-        self._raise_if_any_failed(comm, error)
+        if os.environ.get("MPITREE_FAULT_RANK") or os.environ.get("MPITREE_PREFLIGHT") == "1":
+            try:
+                maybe_inject_fault(comm.rank)
+            except Exception as e:
+                error = e
+            self._raise_if_any_failed(comm, error)
         try:
             self._fit_impl(X, y, comm=comm, **comm.fit_kwargs())
         except Exception as e:  # reported to every rank below
