@@ -7,6 +7,7 @@ One JSON line per config (wall-clock per fit, samples/s, tree size):
   sweep       the notebook's published workload (experiments.ipynb:198-209):
               X = arange(n)[:, None], y = arange(n) (every sample its own
               class), n = 1..241 step 10; CPU, compared with time_data.csv
+  sweep_gpu   the same workload fitted on one MI355X
   100k        100k x 32 synthetic classification, max_depth=12, 1 GPU
   1m          1M x 64 synthetic classification (flagship; bench.py), 1 GPU
   1m_reg      1M x 64 regression tree (squared error), 1 GPU
@@ -92,6 +93,27 @@ def run_sweep(reps):
     return out
 
 
+def run_sweep_gpu(reps):
+    """The published workload on one MI355X (device tensors in, tree out)."""
+    import torch
+
+    from mpitree_amd import DecisionTreeClassifier
+
+    pub = _published()
+    out = []
+    for i, n in enumerate(range(1, 242, 10)):
+        X = torch.arange(n, dtype=torch.float32, device="cuda").reshape(-1, 1)
+        y = torch.arange(n, device="cuda")
+        est = DecisionTreeClassifier(device="cuda")
+        med, best = _time(lambda: est.fit(X, y), reps, sync=torch.cuda.synchronize)
+        row = {"config": f"sweep_gpu_n={n}", "ms_median": med * 1e3, "ms_best": best * 1e3,
+               "nodes": est.tree_arrays_.node_count, "engine": est.fit_stats_["engine"]}
+        if pub:
+            row["reference_k8_ms"] = pub[8][i]
+        out.append(row)
+    return out
+
+
 def _gpu_fit(n, F, reps, md=None, regression=False, classes=2, seed=0):
     import torch
 
@@ -113,7 +135,8 @@ def _gpu_fit(n, F, reps, md=None, regression=False, classes=2, seed=0):
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("names", nargs="*", default=["iris", "sweep", "100k", "1m", "1m_reg", "10m"])
+    ap.add_argument("names", nargs="*", default=["iris", "sweep", "sweep_gpu", "100k", "1m", "1m_reg",
+                                                         "10m"])
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args(argv)
     for name in a.names:
@@ -121,6 +144,8 @@ def main(argv=None):
             rows = run_iris(max(a.reps, 20))
         elif name == "sweep":
             rows = run_sweep(max(a.reps, 20))
+        elif name == "sweep_gpu":
+            rows = run_sweep_gpu(max(a.reps, 10))
         elif name == "100k":
             rows = [{"config": "100k x 32 classification, max_depth=12, 1 GPU",
                      **_gpu_fit(100_000, 32, a.reps, md=12)}]
