@@ -980,22 +980,31 @@ __device__ __forceinline__ uint32_t bitonic_step_pk(uint32_t v, int lane) {
 }
 
 // Ascending bitonic sort of 64 lanes, two independent 16-bit keys per lane.
-__device__ __forceinline__ uint32_t bitonic64_pk_u16(uint32_t v, int lane) {
+// lg (wave-uniform) = ceil(log2(active lanes)): every lane >= 2^lg holds the
+// all-ones key, so the stages that merge blocks larger than 2^lg are skipped --
+// after stage 2^lg lanes [0, 2^lg) are ascending and the rest are equal maxima
+// (a 32-row subtree runs 15 of the 21 steps, a 16-row one 10).
+__device__ __forceinline__ uint32_t bitonic64_pk_u16(uint32_t v, int lane, int lg) {
   v = bitonic_step_pk<2, 1>(v, lane);
+  if (lg < 2) return v;
   v = bitonic_step_pk<4, 2>(v, lane);
   v = bitonic_step_pk<4, 1>(v, lane);
+  if (lg < 3) return v;
   v = bitonic_step_pk<8, 4>(v, lane);
   v = bitonic_step_pk<8, 2>(v, lane);
   v = bitonic_step_pk<8, 1>(v, lane);
+  if (lg < 4) return v;
   v = bitonic_step_pk<16, 8>(v, lane);
   v = bitonic_step_pk<16, 4>(v, lane);
   v = bitonic_step_pk<16, 2>(v, lane);
   v = bitonic_step_pk<16, 1>(v, lane);
+  if (lg < 5) return v;
   v = bitonic_step_pk<32, 16>(v, lane);
   v = bitonic_step_pk<32, 8>(v, lane);
   v = bitonic_step_pk<32, 4>(v, lane);
   v = bitonic_step_pk<32, 2>(v, lane);
   v = bitonic_step_pk<32, 1>(v, lane);
+  if (lg < 6) return v;
   v = bitonic_step_pk<64, 32>(v, lane);
   v = bitonic_step_pk<64, 16>(v, lane);
   v = bitonic_step_pk<64, 8>(v, lane);
@@ -1038,6 +1047,8 @@ __device__ __forceinline__ void tiny_sorted_subtree(
   // two features share a 32-bit register (packed 16-bit min / max).
   const uint32_t* rowp = codes_rm + (int64_t)row * row_words;
   const int nwords = (F + 3) >> 2;
+  int lg = 1;  // sort network size 2^lg >= m (m >= 2)
+  while ((1 << lg) < m) ++lg;
   for (int w = 0; w < nwords; ++w) {
     const uint32_t word = act ? rowp[w] : 0u;
 #pragma unroll
@@ -1047,7 +1058,7 @@ __device__ __forceinline__ void tiny_sorted_subtree(
       const uint32_t ka = ((word >> (16 * h)) & 0xffu) << 8 | (uint32_t)lane;
       const uint32_t kb = ((word >> (16 * h + 8)) & 0xffu) << 8 | (uint32_t)lane;
       uint32_t v = act ? (ka | (kb << 16)) : 0xffffffffu;
-      v = bitonic64_pk_u16(v, lane);
+      v = bitonic64_pk_u16(v, lane, lg);
       const uint32_t nv = (uint32_t)__shfl_down((int)v, 1, kWave);
       const bool endl = lane == m - 1;
       const uint32_t ea = (endl || ((nv >> 8) & 0xffu) != ((v >> 8) & 0xffu)) ? 0x80u : 0u;
