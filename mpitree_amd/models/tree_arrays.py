@@ -52,7 +52,9 @@ class TreeArrays:
 
     @property
     def n_leaves(self) -> int:
-        return int((self.feature < 0).sum())
+        # every internal node has two children, so N = 2 L - 1 (O(1); a
+        # (feature < 0).sum() over a 187k-node flagship tree costs ~130 us)
+        return (self.node_count + 1) // 2 if self.node_count else 0
 
     def equal(self, other: "TreeArrays", *, check_impurity: bool = True) -> bool:
         names = ["feature", "threshold_bin", "left", "right", "depth", "n_samples"]

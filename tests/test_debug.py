@@ -68,3 +68,12 @@ def test_debug_gpu_fit_checks_inputs_and_tree(debug_env):
     assert clf.fit_stats_["engine"].startswith("hip")
     validate_tree(clf._arrays, n_rows=50_000, n_features=16)
     assert torch.cuda.is_available()
+
+
+def test_leaf_count_identity():
+    """n_leaves uses N = 2L - 1 (every internal node has two children)."""
+    for seed in range(4):
+        rng = np.random.default_rng(seed)
+        X, y = random_problem(rng, 300 + 50 * seed, 4, 3, 6)
+        ta = DecisionTreeClassifier(max_depth=[None, 0, 3, 5][seed], device="cpu").fit(X, y)._arrays
+        assert ta.n_leaves == int((ta.feature < 0).sum())
