@@ -203,6 +203,9 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         const uint32_t l0 = lp[q] & 0xffffu, l1 = lp[q] >> 16;
         const uint32_t ml = l0 + l1, mr = (uint32_t)m - ml;
         ok[q][k] = v[q][k] != 0u && (int64_t)ml >= msl && (int64_t)mr >= msl;
+        // every bin looks its terms up, empty ones included: redirecting empty
+        // bins to one broadcast entry measured slower (the selects cost more VALU
+        // than the bank conflicts they remove)
         tv[q][k][0] = lk(ml);
         tv[q][k][1] = lk(l0);
         tv[q][k][2] = lk(l1);
