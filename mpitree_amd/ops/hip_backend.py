@@ -565,18 +565,29 @@ class HipBackend:
         if J <= 0:
             return
         C = self.C
-        if counter is None:  # four int32 work cursors, zero at launch
-            counter = torch.zeros(4, dtype=torch.int32, device=self.device)
+        if counter is None:  # eight int32 work cursors, zero at launch
+            counter = torch.zeros(8, dtype=torch.int32, device=self.device)
         if self.reg:
             self._launch_finisher_reg(d_jobs, J, job_rows, params, rec, cnt, counter)
             return
         job_root = torch.empty(J, dtype=torch.int32, device=self.device)
         tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
-        # every tiny subtree has >= 2 rows and they partition the job rows
-        tiny_cap = int(job_rows // 2 + J + 1)
+        # every tiny subtree has >= 2 rows and they partition the job rows; with
+        # the in-kernel queue (opt-in, C <= 2) a job's records sit at its start
+        # row / 2, and tq lists the published ones (zeroed). Measured on the
+        # 1M x 64 flagship: finisher + tiny kernel 1647 us -> 1571 us in-kernel,
+        # but the fit itself 3.845 ms (off) vs 3.873 / 3.896 ms (on): within
+        # noise, so the spin-waiting consumer stays off by default.
+        queue = (C <= 2 and self.cb == 1 and tiny_rows > 0
+                 and os.environ.get("MPITREE_TINY_QUEUE", "0") == "1")
+        tiny_cap = int(max(job_rows, self.n if queue else 0) // 2 + J + 1)
         tiny = torch.empty((tiny_cap, 8), dtype=torch.int64, device=self.device)
         md = -1 if params.max_depth is None else int(params.max_depth)
         grid = int(min(J, int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU))))
+        # every consumer wave's last claim lands past the records: room for
+        # 16 waves per workgroup
+        tq = (torch.zeros(tiny_cap + 16 * grid, dtype=torch.int32, device=self.device)
+              if queue else None)
         prof = None
         if os.environ.get("MPITREE_FIN_PROF"):
             prof = torch.zeros((grid, 10), dtype=torch.int64, device=self.device)
@@ -590,8 +601,9 @@ class HipBackend:
                         rec.data_ptr(), cnt.data_ptr(), job_root.data_ptr(), grid,
                         tiny_rows, tiny.data_ptr(), 4 * N_CU,
                         0 if prof is None else prof.data_ptr(),
-                        int(os.environ.get("MPITREE_FIN_THREADS", 0)), N_CU)
-        self._fin_keep = (counter, job_root, tiny, d_jobs)
+                        int(os.environ.get("MPITREE_FIN_THREADS", 0)), N_CU,
+                        0 if tq is None else tq.data_ptr())
+        self._fin_keep = (counter, job_root, tiny, d_jobs, tq)
         if prof is not None:
             self.last_finisher_prof = prof.cpu().numpy()
 

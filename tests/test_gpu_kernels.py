@@ -139,6 +139,19 @@ def test_gpu_tiny_subtree_wave_path(monkeypatch, tiny):
         assert clf.tree_arrays_.equal(ref), (tiny, crit)
 
 
+@pytest.mark.parametrize("crit", ["entropy", "gini"])
+def test_gpu_tiny_queue_matches_oracle(monkeypatch, crit):
+    # opt-in in-kernel tiny-subtree queue (binary labels: the sorted wave path)
+    monkeypatch.setenv("MPITREE_TINY_QUEUE", "1")
+    monkeypatch.setenv("MPITREE_FINISHER_ROWS", "2000")
+    rng = np.random.default_rng(5)
+    n, F, C = 20000, 8, 2
+    X, y = random_problem(rng, n, F, C, levels=40)
+    ref = oracle(X, y, Criterion.ENTROPY if crit == "entropy" else Criterion.GINI, None)
+    clf = DecisionTreeClassifier(criterion=crit, device="cuda").fit(X, y)
+    assert clf.tree_arrays_.equal(ref), crit
+
+
 @pytest.mark.parametrize("regression", [False, True])
 def test_gpu_device_assembly_matches_host(monkeypatch, regression):
     """Pre-order position space + device compaction == host renumbering."""
