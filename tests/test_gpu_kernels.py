@@ -196,6 +196,30 @@ def test_gpu_edges_match_host_mapper():
     assert np.array_equal(codes_fm.cpu().numpy().T[:, :5], host.transform(X))
 
 
+@pytest.mark.parametrize("F", [4, 12, 64, 68, 132])
+def test_gpu_bin_cols_matches_bin_rows(monkeypatch, F):
+    """Column-search bin kernel (opt-in) == row-search kernel == host transform,
+    both code layouts, ragged row count, an exact feature the sample misses."""
+    from mpitree_amd.ops.hip_backend import gpu_bin_features
+
+    rng = np.random.default_rng(F)
+    n = 70001  # > the device edge sample: exact features can be missed
+    X = rng.normal(size=(n, F)).astype(np.float32)
+    X[:, 1] = rng.integers(0, 200, size=n)
+    X[rng.integers(0, n), 1] = 1000.0  # one rare level: the refit path
+    X[:, 2] = rng.integers(0, 3, size=n)
+    X[:, 3] = np.round(X[:, 3], 1)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MPITREE_BIN_COLS", mode)
+        mapper, rm, fm, _ = gpu_bin_features(torch.from_numpy(X).cuda(), 256)
+        out[mode] = (rm.cpu().numpy()[:, :F], fm.cpu().numpy())
+    host = mapper.transform(X)
+    for mode in ("1", "0"):
+        np.testing.assert_array_equal(out[mode][0], host)
+        np.testing.assert_array_equal(out[mode][1].T, host)
+
+
 @pytest.mark.parametrize("labels", ["int64", "int32-gaps", "negative", "float", "host"])
 def test_gpu_label_prepare_paths(labels):
     """Device label encoding (range count + LUT, gpu_prepare) == host np.unique,
