@@ -19,7 +19,7 @@ int hist_feature_tile(int F_h, int B, int C, bool reg, int lds_budget);
 int64_t hist_slab_words(int F_h, int B, int C, bool reg);
 void launch_hist(hipStream_t, const void*, int, int64_t, const uint32_t*, const void*, int,
                  const int64_t*, int, void*, void*, int, int, int, int, bool, int,
-                 const int32_t*);
+                 const int32_t*, const int64_t*, int, const int32_t*);
 void launch_hist_reduce(hipStream_t, const int64_t*, int, int, const void*, void*, int, int, int,
                         bool, const int32_t*);
 void launch_hist_derive(hipStream_t, const int64_t*, int, const void*, void*, int64_t, bool,
@@ -93,7 +93,7 @@ void launch_finish_reg(hipStream_t, const void*, int64_t, const void*, int, int6
 void launch_seg_minmax(hipStream_t, const uint32_t*, const int64_t*, const int64_t*, int, int64_t*,
                        const int32_t*);
 void launch_hist_reduce_tasks(hipStream_t, const int64_t*, int, const int64_t*, int, const void*,
-                              void*, int, int, int, const int32_t*, const int32_t*);
+                              void*, int, int, int, const int32_t*, const int32_t*, bool);
 int edges_sample_rows(bool x64);
 void launch_edges(hipStream_t, const void*, bool, int64_t, int, int, int, void*, int32_t*,
                   uint8_t*, double*);
@@ -116,14 +116,17 @@ PYBIND11_MODULE(_hip, m) {
   m.def("hist_slab_words", &mt::hist_slab_words);
   m.def("hist", [](uintptr_t s, uintptr_t codes, int cb, int64_t rs, uintptr_t idx, uintptr_t y,
                    int lab_shift, uintptr_t items, int n_items, uintptr_t hist, uintptr_t slab,
-                   int F_h, int f_lo, int B, int C, bool reg, int lds, uintptr_t dcount) {
+                   int F_h, int f_lo, int B, int C, bool reg, int lds, uintptr_t dcount,
+                   uintptr_t zred, int zred_bound, uintptr_t zcount) {
     mt::launch_hist(S(s), P<void>(codes), cb, rs, P<uint32_t>(idx), P<void>(y), lab_shift,
                     P<int64_t>(items), n_items, P<void>(hist), P<void>(slab), F_h, f_lo, B, C,
-                    reg, lds, P<int32_t>(dcount));
+                    reg, lds, P<int32_t>(dcount), P<int64_t>(zred), zred_bound,
+                    P<int32_t>(zcount));
   }, "", py::arg("s"), py::arg("codes"), py::arg("cb"), py::arg("rs"), py::arg("idx"),
      py::arg("y"), py::arg("lab_shift"), py::arg("items"), py::arg("n_items"), py::arg("hist"),
      py::arg("slab"), py::arg("F_h"), py::arg("f_lo"), py::arg("B"), py::arg("C"), py::arg("reg"),
-     py::arg("lds"), py::arg("dcount") = 0);
+     py::arg("lds"), py::arg("dcount") = 0, py::arg("zred") = 0, py::arg("zred_bound") = 0,
+     py::arg("zcount") = 0);
   m.def("hist_reduce", [](uintptr_t s, uintptr_t red, int n, int max_k, uintptr_t slab,
                           uintptr_t hist, int F_h, int B, int C, bool reg, uintptr_t dcount) {
     mt::launch_hist_reduce(S(s), P<int64_t>(red), n, max_k, P<void>(slab), P<void>(hist), F_h, B,
@@ -228,11 +231,13 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("hist_reduce_tasks", [](uintptr_t s, uintptr_t red, int red_bound, uintptr_t tasks,
                                 int task_bound, uintptr_t slab, uintptr_t hist, int F_h, int B,
-                                int C, uintptr_t dred, uintptr_t dtasks) {
+                                int C, uintptr_t dred, uintptr_t dtasks, bool zero) {
     mt::launch_hist_reduce_tasks(S(s), P<int64_t>(red), red_bound, P<int64_t>(tasks), task_bound,
                                  P<void>(slab), P<void>(hist), F_h, B, C, P<int32_t>(dred),
-                                 P<int32_t>(dtasks));
-  });
+                                 P<int32_t>(dtasks), zero);
+  }, "", py::arg("s"), py::arg("red"), py::arg("red_bound"), py::arg("tasks"),
+     py::arg("task_bound"), py::arg("slab"), py::arg("hist"), py::arg("F_h"), py::arg("B"),
+     py::arg("C"), py::arg("dred"), py::arg("dtasks"), py::arg("zero") = true);
   m.def("job_sort_max", &mt::job_sort_max);
   m.def("job_sort", [](uintptr_t s, uintptr_t jobs, int J, int W, uintptr_t out,
                        uintptr_t counters) {

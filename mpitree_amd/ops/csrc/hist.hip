@@ -44,7 +44,25 @@ __global__ __launch_bounds__(kHistThreads) void hist_cls_lds_kernel(
     const uint32_t* __restrict__ codes, int64_t row_words, const uint32_t* __restrict__ idx,
     const int32_t* __restrict__ y, RowLab rl, const int64_t* __restrict__ items,
     uint32_t* __restrict__ hist, uint32_t* __restrict__ slab, int F_h, int f_lo, int B, int C,
-    int ft, int lane_shift, const int32_t* __restrict__ dcount) {
+    int ft, int lane_shift, const int32_t* __restrict__ dcount, const int64_t* __restrict__ zred,
+    const int32_t* __restrict__ zcount, int64_t zE) {
+  // zred (optional, device-planned levels): zero the multi-item slots {slot, -, -}
+  // [*zcount] that the following slab reduction adds into -- one launch less per
+  // level. This kernel writes single-item slots and slabs only, never a zred slot.
+  // The zeroing is spread over the active workgroups (at least one).
+  if (zred) {
+    const int act = max(1, dcount ? min(*dcount, (int)gridDim.x) : (int)gridDim.x);
+    if ((int)blockIdx.x < act) {
+      const int64_t per = zE >> 2;  // uint4 per slot (zE % 4 == 0, host-checked)
+      const int64_t total = (int64_t)(*zcount) * per;
+      const int64_t stride = (int64_t)act * gridDim.y * blockDim.x;
+      for (int64_t i = ((int64_t)blockIdx.x * gridDim.y + blockIdx.y) * blockDim.x + threadIdx.x;
+           i < total; i += stride) {
+        const int64_t z = i / per;
+        reinterpret_cast<uint4*>(hist + zred[z * 3] * zE)[i - z * per] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
   // dcount (optional): device-side item count; the grid is an upper bound
   if (dcount && (int)blockIdx.x >= *dcount) return;
   extern __shared__ uint32_t lds[];
@@ -391,9 +409,21 @@ int64_t hist_slab_words(int F_h, int B, int C, bool reg) {
 void launch_hist(hipStream_t stream, const void* codes, int code_bytes, int64_t row_stride_bytes,
                  const uint32_t* idx, const void* y, int lab_shift, const int64_t* items,
                  int n_items, void* hist, void* slab, int F_h, int f_lo, int B, int C, bool reg,
-                 int lds_budget, const int32_t* dcount) {
+                 int lds_budget, const int32_t* dcount, const int64_t* zred, int zred_bound,
+                 const int32_t* zcount) {
+  // zred / zcount (classification, optional): the multi-item slots to zero before
+  // the slab reduction (launch_hist_reduce_tasks with zero = false) -- fused into
+  // the LDS histogram kernel, else a zero_slots_kernel launch here
   if (n_items <= 0) return;
   const int ft = hist_feature_tile(F_h, B, C, reg, lds_budget);
+  const int64_t Eu = (int64_t)F_h * B * C;
+  const bool fuse_zero = zred && zred_bound > 0 && !reg && ft != 0 && (Eu & 3) == 0;
+  if (zred && zred_bound > 0 && !fuse_zero) {
+    hipLaunchKernelGGL(zero_slots_kernel,
+                       dim3((unsigned)std::min<int64_t>((Eu / 4 + 255) / 256, 64), zred_bound),
+                       dim3(256), 0, stream, zred, (uint32_t*)hist, Eu, zcount);
+    MT_HIP_CHECK(hipGetLastError());
+  }
   RowLab rl{lab_shift ? ((1u << lab_shift) - 1u) : 0xffffffffu, lab_shift};
   if (ft == 0) {
     dim3 grid(n_items);
@@ -460,7 +490,8 @@ void launch_hist(hipStream_t stream, const void* codes, int code_bytes, int64_t 
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));    \
   hipLaunchKernelGGL((hist_cls_lds_kernel<CT, V>), grid, dim3(kHistThreads), lds, stream,     \
                      (const uint32_t*)codes, row_words, idx, (const int32_t*)y, rl, items,    \
-                     (uint32_t*)hist, (uint32_t*)slab, F_h, f_lo, B, C, ft, shift, dcount);
+                     (uint32_t*)hist, (uint32_t*)slab, F_h, f_lo, B, C, ft, shift, dcount,   \
+                     fuse_zero ? zred : nullptr, zcount, Eu);
   if (code_bytes == 1) {
     if (vec4) {
       MT_CLS(uint8_t, 4)
@@ -509,15 +540,18 @@ void launch_hist_reduce(hipStream_t stream, const int64_t* red, int n_red, int m
 // workgroup row per task {slot, first slab, <= 16 slabs} adds into them.
 void launch_hist_reduce_tasks(hipStream_t stream, const int64_t* red, int red_bound,
                               const int64_t* tasks, int task_bound, const void* slab, void* hist,
-                              int F_h, int B, int C, const int32_t* dred, const int32_t* dtasks) {
+                              int F_h, int B, int C, const int32_t* dred, const int32_t* dtasks,
+                              bool zero) {
   if (red_bound <= 0 || task_bound <= 0) return;
   const int W = (C + 1) / 2;
   const int64_t Ep = (int64_t)F_h * B * W;
   const int64_t Eu = (int64_t)F_h * B * C;
-  hipLaunchKernelGGL(zero_slots_kernel,
-                     dim3((unsigned)std::min<int64_t>((Eu / 4 + 255) / 256, 64), red_bound),
-                     dim3(256), 0, stream, red, (uint32_t*)hist, Eu, dred);
-  MT_HIP_CHECK(hipGetLastError());
+  if (zero) {  // else launch_hist already zeroed the slots (zred)
+    hipLaunchKernelGGL(zero_slots_kernel,
+                       dim3((unsigned)std::min<int64_t>((Eu / 4 + 255) / 256, 64), red_bound),
+                       dim3(256), 0, stream, red, (uint32_t*)hist, Eu, dred);
+    MT_HIP_CHECK(hipGetLastError());
+  }
   dim3 grid((unsigned)((Ep + 255) / 256), task_bound, 1);
   hipLaunchKernelGGL(hist_reduce_cls_kernel, grid, dim3(256), 0, stream, tasks,
                      (const uint32_t*)slab, (uint32_t*)hist, Ep, C, W, 16, dtasks);

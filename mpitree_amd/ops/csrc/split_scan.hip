@@ -364,6 +364,12 @@ __global__ __launch_bounds__(256) void select_kernel(
   }
 }
 
+// The select stays a launch of its own. Fusing it into scan_cls_kernel (the
+// last of a node's feature-group workgroups runs it, behind an agent-scope
+// release / acquire on a per-node counter) was measured on the 1M x 64
+// flagship: the scan went from ~19 to ~82 us per level -- every workgroup's
+// agent-scope release writes back its XCD's L2 -- against the ~6 us launch
+// it saves.
 void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int k,
                  const int32_t* nbins, int F_h, int f_lo, int B, int C, int crit, int msl,
                  double* cost, int32_t* bins, int64_t* rec, const double* xtab, int xtab_n,

@@ -322,17 +322,22 @@ class DeviceGrower:
                 ctl = cur["ctl"]
                 # rows alternate between the two permutation buffers level by level
                 src, dst = bufs[lvl % 2], bufs[(lvl + 1) % 2]
+                rb = int(min(kb, RMAX))
+                # classification: the hist launch also zeroes the slots the slab
+                # reduction adds into (one launch less per level)
                 hip.hist(s(), be.codes_rm.data_ptr(), cb, rs, src, be.y.data_ptr(),
                          be.lab_shift, cur["items"], ib, H.data_ptr(), slab.data_ptr(), F, 0, B, C,
-                         reg, hb.LDS_BUDGET, dcount=ctl + 4 * 2)
-                rb = int(min(kb, RMAX))
+                         reg, hb.LDS_BUDGET, dcount=ctl + 4 * 2,
+                         zred=0 if reg else cur["red"], zred_bound=0 if reg else rb,
+                         zcount=0 if reg else ctl + 4 * 3)
                 if reg:  # slabs summed straight into the slot
                     hip.hist_reduce(s(), cur["red"], rb, 1, slab.data_ptr(), H.data_ptr(), F, B, C,
                                     True, dcount=ctl + 4 * 3)
                 else:
                     hip.hist_reduce_tasks(s(), cur["red"], rb, cur["tasks"],
                                           int(min(TMAX, rb + ib // 16 + 1)), slab.data_ptr(),
-                                          H.data_ptr(), F, B, C, ctl + 4 * 3, ctl + 4 * 7)
+                                          H.data_ptr(), F, B, C, ctl + 4 * 3, ctl + 4 * 7,
+                                          zero=False)
                 mark()
                 if lvl > 0:
                     hip.hist_derive(s(), cur["der"], kb, Hp.data_ptr(), H.data_ptr(), E, reg,
