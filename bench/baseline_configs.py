@@ -135,8 +135,8 @@ def _gpu_fit(n, F, reps, md=None, regression=False, classes=2, seed=0):
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("names", nargs="*", default=["iris", "sweep", "sweep_gpu", "100k", "1m", "1m_reg",
-                                                         "10m"])
+    ap.add_argument("names", nargs="*",
+                    default=["iris", "sweep", "sweep_gpu", "100k", "1m", "1m_reg", "10m"])
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args(argv)
     for name in a.names:

@@ -1,4 +1,4 @@
-import cProfile, pstats, sys, time, torch
+import cProfile, pstats, sys, torch
 sys.path.insert(0, '.')
 from mpitree_amd import DecisionTreeClassifier
 from mpitree_amd.utils.datasets import make_classification

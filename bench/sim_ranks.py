@@ -33,7 +33,6 @@ def main():
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--regression", action="store_true")
-    ap.add_argument("--fin-threads", default="0", help="MPITREE_FIN_THREADS values to sweep")
     a = ap.parse_args()
     from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
     from mpitree_amd.utils.datasets import make_classification, make_regression
@@ -45,10 +44,7 @@ def main():
     else:
         X, y = make_classification(a.n, a.features, n_classes=2, seed=0, device=dev)
         est = DecisionTreeClassifier(device="cuda")
-    combos = [(ft, fr) for ft in a.fin_threads.split(",") for fr in a.fr.split(",")]
-    for ft, fr in combos:
-        os.environ["MPITREE_FIN_THREADS"] = ft
-        fr = int(fr)
+    for fr in [int(v) for v in a.fr.split(",")]:
         os.environ["MPITREE_FINISHER_ROWS"] = str(fr)
         for P in [int(v) for v in a.ranks.split(",")]:
             os.environ["MPITREE_SIM_RANKS"] = str(P)
@@ -65,7 +61,8 @@ def main():
                     rest.append(st.get("sim_rest_finisher_ms", 0.0))
             st = est.fit_stats_
             T = float(np.median(ts))
-            out = dict(fin_threads=int(ft), fr=fr, P=P, fit_ms=round(T, 3), rank0_fin_ms=round(float(np.median(r0)), 3),
+            out = dict(fr=fr, P=P, fit_ms=round(T, 3),
+                       rank0_fin_ms=round(float(np.median(r0)), 3),
                        rest_fin_ms=round(float(np.median(rest)), 3),
                        est_rank_ms=round(T - float(np.median(rest)), 3),
                        levels=st.get("levels"), jobs=st.get("finisher_subtrees"),

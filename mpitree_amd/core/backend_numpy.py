@@ -153,6 +153,9 @@ class NumpyBackend:
         k = len(starts)
         if self.reg:
             out = np.zeros((k, 4), dtype=np.int64)
+            # an empty (row-shard) segment must not pull the cross-rank min / max
+            out[:, 2] = np.iinfo(np.int64).max
+            out[:, 3] = np.iinfo(np.int64).min
             for j, (st, ct) in enumerate(zip(starts, counts)):
                 yn = self.y[self.idx[st : st + ct]]
                 if ct:

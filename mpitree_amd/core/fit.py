@@ -219,14 +219,34 @@ def fit_tree(
     if int(min_samples_leaf) < 1:
         raise ValueError("min_samples_leaf must be >= 1")
     dev = resolve_device(device, X)
+    comm = comm or LocalComm()
     classes, yv, y_exp, C = None, None, 0, 0
-    if dev != "cuda":  # the GPU path encodes labels alongside binning (gpu_prepare)
+    sharded = bool(getattr(comm, "sharded", False))
+    g_mapper = None
+    if sharded:  # row shards: every rank must agree on bins, labels and the target scale
+        from ..parallel.agreement import global_bin_mapper, global_classes, global_target_scale
+
+        g_mapper = global_bin_mapper(comm, X, max_bins)
+        if regression:
+            absmax, n_tot = global_target_scale(comm, y)
+            y_exp = fixed_point_exponent(absmax, n_tot)
+            yh = np.asarray(y.detach().cpu().numpy() if _is_tensor(y) else y, np.float64).ravel()
+            if yh.shape[0] != n:
+                raise ValueError("y must be 1-D with one target per row")
+            yv = np.round(np.ldexp(yh, y_exp)).astype(np.int64)
+        else:
+            classes = global_classes(comm, y)
+            yh = np.asarray(y.detach().cpu().numpy() if _is_tensor(y) else y).ravel()
+            if yh.shape[0] != n:
+                raise ValueError("y must be 1-D with one label per row")
+            yv = np.searchsorted(classes, yh).astype(np.int32)
+            C = len(classes)
+    elif dev != "cuda":  # the GPU path encodes labels alongside binning (gpu_prepare)
         if regression:
             yv, y_exp = _encode_targets(y, n)
         else:
             classes, yv = _encode_labels(y, n)
             C = len(classes)
-    comm = comm or LocalComm()
     params = GrowParams(
         criterion=crit,
         max_depth=None if max_depth is None else int(max_depth),
@@ -245,9 +265,14 @@ def fit_tree(
         Xd = Xd.contiguous()
         t0 = time.perf_counter()
         with roctx_range("mpitree.bin"):
-            prep = prepare(Xd, y, regression=regression, max_bins=max_bins,
-                           encode_labels=_encode_labels, encode_targets=_encode_targets,
-                           exponent=fixed_point_exponent)
+            if g_mapper is not None:  # globally agreed edges / encodings (row shards)
+                from ..ops.gpu_prepare import prepare_with_mapper
+
+                prep = prepare_with_mapper(Xd, yv, g_mapper, classes, y_exp)
+            else:
+                prep = prepare(Xd, y, regression=regression, max_bins=max_bins,
+                               encode_labels=_encode_labels, encode_targets=_encode_targets,
+                               exponent=fixed_point_exponent)
         mapper, codes_rm, codes_fm, nb = prep.mapper, prep.codes_rm, prep.codes_fm, prep.nbins
         yd, classes, y_exp, root = prep.y, prep.classes, prep.y_exp, prep.root
         C = 0 if regression else len(classes)
@@ -298,7 +323,7 @@ def fit_tree(
             raise ValueError("Input X contains NaN or infinity.")
         yh = yv.cpu().numpy() if _is_tensor(yv) else yv
         t0 = time.perf_counter()
-        mapper = fit_bin_mapper(Xh, max_bins)
+        mapper = g_mapper if g_mapper is not None else fit_bin_mapper(Xh, max_bins)
         codes = mapper.transform(Xh)
         lo, hi = comm.local_rows(n)
         if (lo, hi) != (0, n):

@@ -226,9 +226,6 @@ class LevelwiseBuilder:
             hasattr(be, "begin_positions") and comm.world_size == 1 and edges is not None
             and os.environ.get("MPITREE_DEVICE_ASSEMBLY", "1") != "0" and self.ckpt is None
         )
-        # MPITREE_FIN_OVERLAP=1 launches each level's finisher batch at once on a
-        # side stream (it then competes with the level kernels for CUs)
-        self._overlap = self._device_asm and os.environ.get("MPITREE_FIN_OVERLAP", "0") == "1"
         if self._device_asm:
             be.begin_positions(2 * m_root - 1)
         # frontier columns
@@ -249,7 +246,7 @@ class LevelwiseBuilder:
 
     def _resume(self, state, tab, n_local, C, F_h, f_lo, f_hi, reg) -> TreeArrays:
         """Continue a fit from its last saved level (utils/level_checkpoint.py)."""
-        self._device_asm = self._overlap = False
+        self._device_asm = False
         ck = self.ckpt
         ck.restore_table(state, tab)
         self.be.set_rows(state["rows"])
@@ -270,14 +267,6 @@ class LevelwiseBuilder:
                 if small.any():
                     for key in deferred:
                         deferred[key].append(fr[key][small])
-                    if self._device_asm and self._overlap:  # start now, beside later levels
-                        t0 = time.perf_counter()
-                        sids = fr["id"][small]
-                        be.finish_subtrees(fr["start"][small], fr["count"][small],
-                                           fr["depth"][small], p, stats=tab.stats[sids],
-                                           positions=fr["pos"][small], overlap=True)
-                        self.timings["finisher"] = (self.timings.get("finisher", 0.0)
-                                                    + time.perf_counter() - t0)
                     keep = ~small
                     # derived nodes whose built sibling was deferred: build from rows
                     sib = fr["sib"]
@@ -379,12 +368,9 @@ class LevelwiseBuilder:
         self.stats["levels"] = levels
         if deferred["id"]:
             d = {k: np.concatenate(v) for k, v in deferred.items()}
-            if self._device_asm and self._overlap:  # already running on the side stream
-                self._deferred_ids = np.asarray(d["id"], np.int64)
-            else:
-                t0 = time.perf_counter()
-                self._finish(tab, d)
-                self._tick("finisher", t0)
+            t0 = time.perf_counter()
+            self._finish(tab, d)
+            self._tick("finisher", t0)
             self.stats["finisher_subtrees"] = int(d["id"].size)
         t0 = time.perf_counter()
         ta = self._to_arrays(tab)

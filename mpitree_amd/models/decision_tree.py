@@ -31,7 +31,7 @@ import torch
 from sklearn.base import BaseEstimator, ClassifierMixin, RegressorMixin
 from sklearn.utils.validation import check_is_fitted
 
-from ..core.criterion import Criterion, parse_criterion
+from ..core.criterion import parse_criterion
 from ..core.fit import fit_tree
 from .tree_arrays import TreeArrays
 

@@ -43,7 +43,7 @@ void launch_finish(hipStream_t, const void*, int64_t, const void*, int, int64_t,
                    uint32_t*, const int32_t*, int, const int64_t*, int, int32_t*, const int32_t*,
                    int, int, int, int, int, int64_t, int64_t, const double*, const float*, int,
                    int32_t*,
-                   int32_t*, int32_t*, int, int, int64_t*, int, int64_t*, int, int, int32_t*);
+                   int32_t*, int32_t*, int, int, int64_t*, int, int64_t*);
 int finish_lds_bytes(int F, int B, int C);
 int asm_tiles(int64_t P);
 struct LevelLists {
@@ -193,23 +193,20 @@ PYBIND11_MODULE(_hip, m) {
                      uintptr_t xtab, uintptr_t xtabf, int xtab_n, uintptr_t node_i32,
                      uintptr_t node_cnt,
                      uintptr_t job_nodes, int grid, int tiny_rows, uintptr_t tiny,
-                     int tiny_grid, uintptr_t prof, int fin_threads, int n_cu,
-                     uintptr_t tq) {
+                     int tiny_grid, uintptr_t prof) {
     mt::launch_finish(S(s), P<void>(codes_rm), row_words, P<void>(codes_fm), cb, n_rows,
                       P<uint32_t>(idx), P<uint32_t>(tmp), P<int32_t>(y), lab_shift,
                       P<int64_t>(jobs), J, P<int32_t>(counter), P<int32_t>(nbins), F, B, C, crit,
                       max_depth, mss, msl, P<double>(xtab), P<float>(xtabf), xtab_n, P<int32_t>(node_i32),
                       P<int32_t>(node_cnt), P<int32_t>(job_nodes), grid, tiny_rows,
-                      P<int64_t>(tiny), tiny_grid, P<int64_t>(prof), fin_threads, n_cu,
-                      P<int32_t>(tq));
+                      P<int64_t>(tiny), tiny_grid, P<int64_t>(prof));
   }, py::arg("s"), py::arg("codes_rm"), py::arg("row_words"), py::arg("codes_fm"), py::arg("cb"),
      py::arg("n_rows"), py::arg("idx"), py::arg("tmp"), py::arg("y"), py::arg("lab_shift"),
      py::arg("jobs"), py::arg("J"), py::arg("counter"), py::arg("nbins"), py::arg("F"),
      py::arg("B"), py::arg("C"), py::arg("crit"), py::arg("max_depth"), py::arg("mss"),
      py::arg("msl"), py::arg("xtab"), py::arg("xtabf"), py::arg("xtab_n"), py::arg("node_i32"),
      py::arg("node_cnt"), py::arg("job_nodes"), py::arg("grid"), py::arg("tiny_rows"),
-     py::arg("tiny"), py::arg("tiny_grid"), py::arg("prof"), py::arg("fin_threads") = 0,
-     py::arg("n_cu") = 256, py::arg("tq") = 0);
+     py::arg("tiny"), py::arg("tiny_grid"), py::arg("prof"));
   m.def("asm_tiles", &mt::asm_tiles);
   m.def("finish_reg_lds_bytes", &mt::finish_reg_lds_bytes);
   m.def("finish_reg", [](uintptr_t s, uintptr_t codes_rm, int64_t row_words, uintptr_t codes_fm,

@@ -440,171 +440,6 @@ __global__ __launch_bounds__(kBrThreads) void bin_rows_kernel(
   if (tid < nf && s_flag[tid]) atomicOr(&flags[f0 + tid], s_flag[tid]);
 }
 
-// Column-search variant of bin_rows_kernel (same inputs, outputs and flags):
-// one 1024-thread workgroup per CU stages each batch of X through LDS so that
-// every lower-bound search of a wavefront runs on ONE feature's edges. In
-// bin_rows_kernel the 64 lanes search 16 different features, whose candidate
-// positions p (multiples of the step) land in the same LDS banks: the PMC run
-// counted 75% bank conflicts (profiles/pmc_counters.md). Here all lanes probe
-// one feature, so a probe level touches at most 2^level consecutive edges:
-// same-address broadcasts and distinct banks up to level 6. The X tile is
-// written row by row (stride nf + 1 words: conflict-free) and read column by
-// column (lane = row: conflict-free); codes go to a byte tile (stride nf + 4)
-// that both output layouts are written from, as in bin_rows_kernel.
-constexpr int kBcThreads = 1024;
-constexpr int kBcWaves = kBcThreads / 64;
-constexpr int kBcChains = 8;  // independent searches in flight per lane
-
-__host__ __device__ inline int bc_rows(int nf) { return kBrU * (kBcThreads / (nf >> 2)); }
-__host__ __device__ inline size_t bc_edge_bytes(int nf, int Bmax) {
-  return ((size_t)nf * (Bmax | 1) * 4 + 15) & ~(size_t)15;
-}
-__host__ __device__ inline size_t bc_x_bytes(int nf) {
-  return ((size_t)bc_rows(nf) * (nf + 1) * 4 + 15) & ~(size_t)15;
-}
-inline size_t bc_lds_bytes(int nf, int Bmax) {
-  return bc_edge_bytes(nf, Bmax) + bc_x_bytes(nf) + (size_t)bc_rows(nf) * (nf + 4);
-}
-
-__global__ __launch_bounds__(kBcThreads) void bin_cols_kernel(
-    const float* __restrict__ X, int64_t n, int F, const float* __restrict__ edges, int Bmax,
-    int estride, int steps0, const int32_t* __restrict__ nbins, const uint8_t* __restrict__ exact,
-    uint8_t* __restrict__ codes_rm, int row_elems, uint8_t* __restrict__ codes_fm,
-    int32_t* __restrict__ flags, int64_t rows_per_block, int fm_vec) {
-  extern __shared__ __align__(16) uint8_t smem[];
-  __shared__ int s_flag[kBrFt];
-  __shared__ int s_nb[kBrFt];
-  __shared__ int s_ex[kBrFt];
-  const int ES = Bmax | 1;
-  const int f0 = blockIdx.y * kBrFt;
-  const int nf = min(kBrFt, F - f0);  // multiple of 4
-  const int tpr = nf >> 2;
-  const int rp = kBcThreads / tpr;
-  const int batch = kBrU * rp;  // == bc_rows(nf)
-  const int XS = nf + 1;        // X tile row stride (words)
-  const int TS = nf + 4;        // code tile row stride (bytes)
-  float* s_edges = reinterpret_cast<float*>(smem);
-  float* xs = reinterpret_cast<float*>(smem + bc_edge_bytes(nf, Bmax));
-  uint8_t* tile = smem + bc_edge_bytes(nf, Bmax) + bc_x_bytes(nf);
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63;
-  if (tid < kBrFt) {
-    s_flag[tid] = 0;
-    s_nb[tid] = tid < nf ? nbins[f0 + tid] : 1;
-    s_ex[tid] = tid < nf ? exact[f0 + tid] : 0;
-  }
-  for (int e = tid; e < nf * Bmax; e += kBcThreads) {
-    const int fl = e / Bmax, b = e - fl * Bmax;
-    s_edges[fl * ES + b] = edges[(int64_t)(f0 + fl) * estride + b];
-  }
-  const int rs = tid / tpr;
-  const int q = tid - rs * tpr;
-  const bool active = rs < rp;
-  const int groups = (batch + 63) >> 6;
-  const int ntasks = nf * groups;  // (feature, 64-row group) searches per batch
-  const int64_t rbeg = blockIdx.x * rows_per_block;
-  const int64_t rend = min<int64_t>(n, rbeg + rows_per_block);
-  fm_vec = fm_vec && ((rbeg | batch) & 15) == 0;
-  auto load = [&](int64_t b0, float4* v) {
-#pragma unroll
-    for (int u = 0; u < kBrU; ++u) {
-      const int64_t r = b0 + u * rp + rs;
-      if (active && r < rend) {
-        const f32x4 t = __builtin_nontemporal_load(
-            reinterpret_cast<const f32x4*>(X + r * F + f0 + 4 * q));
-        v[u] = make_float4(t[0], t[1], t[2], t[3]);
-      } else {
-        v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-    }
-  };
-  auto stage = [&](const float4* v) {
-#pragma unroll
-    for (int u = 0; u < kBrU; ++u) {
-      if (!active) continue;
-      float* d = xs + (u * rp + rs) * XS + 4 * q;
-      d[0] = v[u].x;
-      d[1] = v[u].y;
-      d[2] = v[u].z;
-      d[3] = v[u].w;
-    }
-  };
-  float4 cur[kBrU];
-  if (rbeg < rend) {
-    load(rbeg, cur);
-    stage(cur);
-  }
-  __syncthreads();
-  for (int64_t b0 = rbeg; b0 < rend; b0 += batch) {
-    const bool more = b0 + batch < rend;
-    if (more) load(b0 + batch, cur);  // in flight during the search
-    const int rows = (int)min<int64_t>(batch, rend - b0);
-    for (int t0 = wave; t0 < ntasks; t0 += kBcWaves * kBcChains) {
-      float v[kBcChains];
-      int pos[kBcChains], fl[kBcChains], r[kBcChains], nbf[kBcChains];
-#pragma unroll
-      for (int i = 0; i < kBcChains; ++i) {
-        const int t = t0 + kBcWaves * i;  // wave-uniform
-        fl[i] = t < ntasks ? t % nf : 0;
-        r[i] = (t < ntasks ? t / nf : 0) * 64 + lane;
-        v[i] = xs[(r[i] < batch ? r[i] : 0) * XS + fl[i]];
-        nbf[i] = s_nb[fl[i]];
-        pos[i] = 0;
-      }
-      for (int step = steps0; step > 0; step >>= 1) {
-#pragma unroll
-        for (int i = 0; i < kBcChains; ++i) {
-          const int p = pos[i] + step;
-          if (p <= nbf[i] && s_edges[fl[i] * ES + p - 1] < v[i]) pos[i] = p;
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < kBcChains; ++i) {
-        const int t = t0 + kBcWaves * i;
-        if (t >= ntasks) continue;
-        const int code = pos[i] < nbf[i] ? pos[i] : nbf[i] - 1;
-        const bool ok = r[i] < rows;
-        int fg = 0;
-        if (ok && s_ex[fl[i]] && !(s_edges[fl[i] * ES + code] == v[i])) fg |= 1;
-        if (ok && !isfinite(v[i])) fg |= 2;
-        if (fg) atomicOr(&s_flag[fl[i]], fg);
-        if (ok) tile[r[i] * TS + fl[i]] = (uint8_t)code;
-      }
-    }
-    __syncthreads();
-    // row-major: one 4-byte word (4 features) per thread and row
-#pragma unroll
-    for (int u = 0; u < kBrU; ++u) {
-      const int rl = u * rp + rs;
-      if (active && rl < rows)
-        *reinterpret_cast<uint32_t*>(codes_rm + (b0 + rl) * row_elems + f0 + 4 * q) =
-            *reinterpret_cast<const uint32_t*>(tile + rl * TS + 4 * q);
-    }
-    // feature-major: each feature's `rows` codes are contiguous at codes_fm[f * n + b0]
-    const int chunks = (rows + 15) >> 4;
-    for (int e = tid; e < nf * chunks; e += kBcThreads) {
-      const int f = e % nf, c = e / nf;
-      uint8_t* dst = codes_fm + (int64_t)(f0 + f) * n + b0 + 16 * c;
-      const int m = min(16, rows - 16 * c);
-      if (fm_vec && m == 16) {
-        uint32_t w[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          w[i] = (uint32_t)tile[(16 * c + 4 * i) * TS + f] |
-                 ((uint32_t)tile[(16 * c + 4 * i + 1) * TS + f] << 8) |
-                 ((uint32_t)tile[(16 * c + 4 * i + 2) * TS + f] << 16) |
-                 ((uint32_t)tile[(16 * c + 4 * i + 3) * TS + f] << 24);
-        *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
-      } else {
-        for (int i = 0; i < m; ++i) dst[i] = tile[(16 * c + i) * TS + f];
-      }
-    }
-    if (more) stage(cur);  // the search above was the last reader of xs
-    __syncthreads();
-  }
-  if (tid < nf && s_flag[tid]) atomicOr(&flags[f0 + tid], s_flag[tid]);
-}
-
 int edges_sample_rows(bool x64) { return x64 ? 16384 : 32768; }
 
 // The host's view of the edges in one fp64 array: [F][limit] edges, then the
@@ -669,32 +504,6 @@ void launch_bin(hipStream_t stream, const void* X, bool x64, int64_t n, int F, c
       ((uintptr_t)X & 15) == 0 && ((uintptr_t)codes_rm & 3) == 0) {
     const int tiles = (F + kBrFt - 1) / kBrFt;
     const int nf = std::min(kBrFt, F);
-    // column-search kernel (opt-in, MPITREE_BIN_COLS=1): one 1024-thread
-    // workgroup per CU, if the last (narrowest) tile fits too. Measured on the
-    // 1M x 64 flagship: 336 us vs 241 us for bin_rows_kernel. One resident
-    // workgroup per CU serialises its batch phases (load / search / store)
-    // behind the barriers, and sorted-order edges still put a lane-divergent
-    // probe level's candidates (spaced 256 / 2^level apart) in a few banks.
-    const int nf_last = F - (tiles - 1) * kBrFt;
-    const size_t lds_c = std::max(bc_lds_bytes(nf, Bmax), bc_lds_bytes(nf_last, Bmax));
-    const char* bc_env = std::getenv("MPITREE_BIN_COLS");
-    if (bc_env && bc_env[0] == '1' && lds_c <= 150 * 1024) {
-      const int batch = bc_rows(nf);
-      const int64_t nbatch = (n + batch - 1) / batch;
-      const int64_t want = std::max<int64_t>(1, 256 / tiles);
-      const int64_t per = (nbatch + want - 1) / want;
-      const int64_t rpb = per * batch;
-      const unsigned gx = (unsigned)((n + rpb - 1) / rpb);
-      const int fm_vec = ((n & 15) == 0 && ((uintptr_t)codes_fm & 15) == 0) ? 1 : 0;
-      MT_HIP_CHECK(hipFuncSetAttribute((const void*)bin_cols_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c));
-      hipLaunchKernelGGL(bin_cols_kernel, dim3(gx, (unsigned)tiles), dim3(kBcThreads), lds_c,
-                         stream, (const float*)X, n, F, (const float*)edges, Bmax, estride, steps0,
-                         nbins, exact, (uint8_t*)codes_rm, row_elems, (uint8_t*)codes_fm, flags,
-                         rpb, fm_vec);
-      MT_HIP_CHECK(hipGetLastError());
-      return;
-    }
     const int batch = kBrU * (kBrThreads / (nf / 4));
     const int64_t nbatch = (n + batch - 1) / batch;
     const int64_t want = std::max<int64_t>(1, 2 * 256 / tiles);  // ~2 workgroups per CU

@@ -32,11 +32,9 @@
 
 namespace mt {
 
-// threads per finisher workgroup: 512 (two per CU); 1024 (one per CU, twice the
-// waves per job) targets ranks of a multi-GPU fit, which finish ~1/P of the jobs
-// and are bound by per-job latency rather than throughput (bench/sim_ranks.py)
+// threads per finisher workgroup: 512 (two per CU). A 1024-thread variant and an
+// in-kernel tiny-subtree queue were measured slower (profiles/kernel_experiments.md)
 constexpr int kFinThreadsSmall = 512;
-constexpr int kFinThreadsBig = 1024;
 constexpr int kFinStack = 40;    // >= log2(max job rows) + 2
 constexpr int kFinMaxC = 16;     // classes supported by the finisher
 constexpr int kFinTab = 1024;    // LDS x*log2(x) entries
@@ -59,13 +57,6 @@ struct FinRowLab {
   int shift;
 };
 
-// Tiny-subtree queue consumer of the block finisher (defined with the tiny kernels).
-__device__ void drain_tiny_queue(uint8_t* lds, int nw, const int32_t* tq, int32_t* ctr, int J,
-                                 const int64_t* tiny, const uint32_t* codes_rm, int64_t row_words,
-                                 const uint32_t* buf0, const uint32_t* buf1, const int32_t* y,
-                                 FinRowLab rl, int F, int C, int crit, int max_depth, int64_t mss,
-                                 int64_t msl, const double* xtab, int32_t* node_i32,
-                                 int32_t* node_cnt);
 
 // jobs: int64 [J][5 + C] = {start, count, depth, base, buffer, counts[C]}
 // node_i32: [slots][6] = {feature, bin, left, right, depth, n}; node_cnt: [slots][C]
@@ -79,8 +70,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
     int crit, int max_depth, int64_t mss, int64_t msl, const double* __restrict__ xtab,
     const float* __restrict__ xtabf, int xtab_n, int32_t* __restrict__ node_i32, int32_t* __restrict__ node_cnt,
     int32_t* __restrict__ job_root, int tiny_rows,
-    int64_t* __restrict__ tiny, int32_t* __restrict__ tiny_count, int64_t* __restrict__ prof,
-    int tiny_queue, int32_t* __restrict__ tq) {
+    int64_t* __restrict__ tiny, int32_t* __restrict__ tiny_count, int64_t* __restrict__ prof) {
   // prof (optional): per workgroup {wall start, wall end, nodes, rows, cycles in
   // histogram, scan, partition, rest} -- the finisher's own phase profile
   constexpr int kFinWaves = kFinThreads / kWave;
@@ -108,12 +98,6 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
   __shared__ double w_gain[kFinWaves];
   __shared__ int w_feat[kFinWaves], w_bin[kFinWaves];
   __shared__ int s_bf, s_bb;
-  // tiny_queue > 0 (see launch_finish): a job's tiny records go to its own slice
-  // tiny[start / 2 ...] (a job of c rows has at most c / 2 tiny subtrees of >= 2
-  // rows; jobs own disjoint row ranges) and are published to the queue tq when
-  // the job ends; a workgroup that finds the job list empty drains the queue
-  __shared__ int s_tiny_n;
-  __shared__ int64_t s_tiny_base;
   __shared__ int s_lc, s_rc;
   __shared__ int s_cand_total;
   if (threadIdx.x == 0) s_cand_total = 0;
@@ -296,8 +280,6 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
       s_st_depth[0] = (int32_t)jb[2];
       s_st_id[0] = r;
       s_st_buf[0] = (int32_t)jb[4];
-      s_tiny_n = 0;
-      s_tiny_base = jb[0] >> 1;
       int32_t* R = ni + (int64_t)r * 6;
       R[0] = -1;
       R[1] = -1;
@@ -306,7 +288,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
       R[4] = (int32_t)jb[2];
       R[5] = (int32_t)jb[1];
       if (jb[1] <= tiny_rows) {  // the whole job is tiny: one wave finishes it
-        const int64_t t = tiny_queue ? s_tiny_base + s_tiny_n++ : atomicAdd(tiny_count, 1);
+        const int64_t t = atomicAdd(tiny_count, 1);
         int64_t* tr = tiny + t * 8;
         tr[0] = jb[0];
         tr[1] = jb[1];
@@ -671,8 +653,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           if (is_left ? tlf : trf) continue;
           const int cm_rows = is_left ? nl : nr;
           if (cm_rows <= tiny_rows) {  // hand the tiny subtree to a wavefront
-            const int64_t t =
-                tiny_queue ? s_tiny_base + s_tiny_n++ : atomicAdd(tiny_count, 1);
+            const int64_t t = atomicAdd(tiny_count, 1);
             int64_t* tr = tiny + t * 8;
             tr[0] = is_left ? start : start + nl;
             tr[1] = cm_rows;
@@ -693,29 +674,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
       }
       __syncthreads();
     }
-    if (tiny_queue > 0) {  // kernel-uniform: publish this job's tiny records
-      // every wave's row writes and thread 0's records reach memory (each
-      // XCD's L2 is written back) before any queue entry names them
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      __syncthreads();
-      if (tid == 0) {
-        const int n = s_tiny_n;
-        if (n > 0) {
-          const int base = atomicAdd(job_counter + 4, n);
-          for (int i = 0; i < n; ++i)
-            __hip_atomic_store(tq + base + i, (int32_t)(s_tiny_base + i) + 1, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __hip_atomic_fetch_add(job_counter + 6, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
     mark(3);
-  }
-  if constexpr (kC2) {
-    if (tiny_queue > 0)
-      drain_tiny_queue(reinterpret_cast<uint8_t*>(hist), tiny_queue, tq, job_counter, J, tiny,
-                       codes_rm, row_words, buf0, buf1, y, rl, F, C, crit, max_depth, mss, msl,
-                       xtab, node_i32, node_cnt);
   }
   if (prof && tid == 0) {
     int64_t* P = prof + (int64_t)blockIdx.x * 10;
@@ -1287,87 +1246,6 @@ __global__ __launch_bounds__(256) void finish_tiny_sorted_kernel(
   }
 }
 
-// Consumer LDS (the block finisher's histogram, free once the job list is
-// empty): the H table and its row offsets, then per wave srt [F][64] halfwords,
-// 64 flag bytes and the DFS stack (16 masks, depths, positions).
-constexpr int kQueueHBytes = ((kTinyH * 8 + (kTinyRows + 1) * 4) + 15) & ~15;
-__host__ __device__ inline int queue_wave_bytes(int F) { return tiny_wave_bytes(F) + 16 * 16; }
-constexpr int64_t kQueueSpinCap = 1ll << 24;  // polls (~4 s): a bound, never reached
-
-// Every wave claims the next queue slot and waits until a finished job has
-// published a record there, or until every job is done and the slot is past
-// the last record. Only workgroups whose job list is exhausted get here, so
-// every job still open is running on a resident workgroup and will publish:
-// the waits end. Records and rows come from other workgroups (other XCDs'
-// L2s): they are read with agent-scope (sc1) loads after the producer's
-// release; codes, labels and the H table are read-only here.
-__device__ void drain_tiny_queue(uint8_t* lds, int nw, const int32_t* tq, int32_t* ctr, int J,
-                                 const int64_t* tiny, const uint32_t* codes_rm, int64_t row_words,
-                                 const uint32_t* buf0, const uint32_t* buf1, const int32_t* y,
-                                 FinRowLab rl, int F, int C, int crit, int max_depth, int64_t mss,
-                                 int64_t msl, const double* xtab, int32_t* node_i32,
-                                 int32_t* node_cnt) {
-  __syncthreads();  // the histogram is no longer read
-  double* H = reinterpret_cast<double*>(lds);
-  uint32_t* Hrow = reinterpret_cast<uint32_t*>(lds + kTinyH * 8);
-  tiny_fill_h(H, xtab, crit);
-  for (int a = threadIdx.x; a <= kTinyRows; a += blockDim.x) Hrow[a] = 8u * (uint32_t)tiny_h_idx(a, 0);
-  __syncthreads();
-  const int wave = threadIdx.x >> 6;
-  if (wave >= nw) return;
-  const int lane = lane_id();
-  uint8_t* wb = lds + kQueueHBytes + (size_t)wave * queue_wave_bytes(F);
-  uint16_t* srt = reinterpret_cast<uint16_t*>(wb);
-  uint8_t* flag = wb + F * kWave * 2;
-  unsigned long long* st_mask = reinterpret_cast<unsigned long long*>(wb + tiny_wave_bytes(F));
-  int32_t* st_dep = reinterpret_cast<int32_t*>(st_mask + 16);
-  int32_t* st_slot = st_dep + 16;
-  int32_t* q = const_cast<int32_t*>(tq);
-  int64_t* rq = const_cast<int64_t*>(tiny);
-  for (;;) {
-    int k = 0;
-    if (lane == 0) k = atomicAdd(ctr + 5, 1);
-    k = __builtin_amdgcn_readfirstlane(k);
-    int v = 0;
-    for (int64_t spin = 0;; ++spin) {
-      v = __builtin_amdgcn_readfirstlane(
-          __hip_atomic_load(q + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      if (v) break;
-      const int done = __builtin_amdgcn_readfirstlane(
-          __hip_atomic_load(ctr + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      if (done >= J) {  // every record is published: slot k is one or none
-        const int total = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(ctr + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if (k >= total) break;
-        continue;
-      }
-      if (spin >= kQueueSpinCap) {  // unreachable bound: flag it, never hang
-        if (lane == 0) atomicOr(ctr + 7, 1);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    if (!v) return;
-    int64_t* rec = rq + (int64_t)(v - 1) * 8;
-    int64_t r[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i)
-      r[i] = __builtin_amdgcn_readfirstlane(
-          (int)__hip_atomic_load(rec + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    tiny_sorted_subtree(codes_rm, row_words, r[3] ? buf1 : buf0, y, rl, r[0], (int)r[1],
-                        (int)r[2], r[4], F, C, crit, max_depth, mss, msl, H, Hrow, srt, flag,
-                        st_mask, st_dep, st_slot, TinyOut{node_i32, node_cnt}, true);
-  }
-}
-
-// Consumer waves of the block finisher's tiny queue: what fits in the
-// histogram LDS of F x B x C, at most one per wave (0: the tiny kernel runs).
-int finish_tiny_queue_waves(int F, int B, int C, int threads) {
-  const int avail = F * fin_fstride(B, (C + 1) / 2) * 4 - kQueueHBytes;
-  if (avail <= 0) return 0;
-  return std::min(threads / kWave, avail / queue_wave_bytes(F));
-}
-
 int finish_lds_bytes(int F, int B, int C) { return F * fin_fstride(B, (C + 1) / 2) * 4; }
 int finish_max_classes() { return kFinMaxC; }
 
@@ -1378,10 +1256,8 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                    int max_depth, int64_t mss, int64_t msl, const double* xtab,
                    const float* xtabf, int xtab_n,
                    int32_t* node_i32, int32_t* node_cnt, int32_t* job_root, int grid,
-                   int tiny_rows, int64_t* tiny, int tiny_grid, int64_t* prof, int fin_threads,
-                   int n_cu, int32_t* tq) {
-  // counter: int32 [8] = {job cursor, tiny count, tiny cursor, -, queue count,
-  // queue cursor, jobs done, queue error}, zeroed by the
+                   int tiny_rows, int64_t* tiny, int tiny_grid, int64_t* prof) {
+  // counter: int32 [8] = {job cursor, tiny count, tiny cursor, -...}, zeroed by the
   // host. node_i32 / node_cnt are indexed by pre-order position (jobs[j][3] is
   // job j's root position); rows a fit never writes keep n = 0 (host memset).
   if (J <= 0) return;
@@ -1391,18 +1267,6 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   tiny_rows = std::min(tiny_rows, kTinyRows);
   FinRowLab rl{lab_shift ? ((1u << lab_shift) - 1u) : 0xffffffffu, lab_shift};
   const size_t lds = (size_t)finish_lds_bytes(F, B, C);
-  // fin_threads: 1024 selects the one-workgroup-per-CU variant (MPITREE_FIN_THREADS,
-  // opt-in while it is being measured), anything else the 512-thread kernel
-  const bool big = fin_threads == kFinThreadsBig;
-  // tiny subtrees (C <= 2, sorted wave path) through the in-kernel queue when
-  // the caller passes one (tq: int32, zeroed, >= n_rows / 2 + J entries; tiny
-  // must then hold n_rows / 2 + J records), else the follow-up tiny kernel
-  int tiny_queue = 0;
-  if (tq != nullptr && tiny_rows > 0 && C <= 2 && getenv_int("MPITREE_TINY_SORTED", 1) != 0) {
-    tiny_queue = finish_tiny_queue_waves(F, B, C, big ? kFinThreadsBig : kFinThreadsSmall);
-    if (tiny_queue < 2) tiny_queue = 0;
-  }
-  if (big) grid = std::min(grid, n_cu);
 #define MT_FIN_NT(CT, C2, NT)                                                                 \
   MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_cls_kernel<CT, C2, NT>,                \
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));    \
@@ -1410,13 +1274,8 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                      (const uint32_t*)codes_rm, row_words, (const CT*)codes_fm, n_rows, buf0, \
                      buf1, y, rl, jobs, J, counter, nbins, F, B, C, crit, max_depth, mss,     \
                      msl, xtab, xtabf, xtab_n, node_i32, node_cnt, job_root, tiny_rows,       \
-                     tiny, counter + 1, prof, tiny_queue, tq);
-#define MT_FIN(CT, C2)                   \
-  if (big) {                             \
-    MT_FIN_NT(CT, C2, kFinThreadsBig)    \
-  } else {                               \
-    MT_FIN_NT(CT, C2, kFinThreadsSmall)  \
-  }
+                     tiny, counter + 1, prof);
+#define MT_FIN(CT, C2) MT_FIN_NT(CT, C2, kFinThreadsSmall)
   if (code_bytes == 1) {
     if (C <= 2) {
       MT_FIN(uint8_t, true)
@@ -1433,7 +1292,7 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
 #undef MT_FIN
 #undef MT_FIN_NT
   MT_HIP_CHECK(hipGetLastError());
-  if (tiny_rows > 0 && tiny_queue == 0) {
+  if (tiny_rows > 0) {
     const bool sorted = C <= 2 && getenv_int("MPITREE_TINY_SORTED", 1) != 0;
     if (sorted) {
       const size_t lds = (size_t)kTinyWaves * tiny_wave_bytes(F);

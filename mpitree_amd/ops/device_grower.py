@@ -32,7 +32,6 @@ import time
 import numpy as np
 import torch
 
-from ..core.criterion import Criterion
 from ..models.tree_arrays import TreeArrays
 from ..utils.observability import profiling
 from . import hip_backend as hb

@@ -194,3 +194,30 @@ def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
         y_exp = 0
     return Prepared(mapper=mapper, codes_rm=codes_rm, codes_fm=codes_fm, nbins=nb, y=yenc,
                     classes=classes, y_exp=y_exp, root=root, d_edges64=binning.d_edges64)
+
+
+def prepare_with_mapper(Xd: torch.Tensor, y_enc, mapper, classes, y_exp: int) -> Prepared:
+    """Bin ``Xd`` with a given (globally agreed) ``BinMapper`` and upload the
+    already-encoded targets ``y_enc`` (int32 class codes / int64 fixed-point).
+    Used by row-sharded data-parallel fits (``parallel/agreement.py``)."""
+    dev = Xd.device
+    hip = native.hip()
+    F = Xd.shape[1]
+    table = mapper.padded_edges(np.float64)
+    W = table.shape[1]
+    edges = torch.from_numpy(table).to(dev)
+    edges_x = edges.to(Xd.dtype).contiguous()
+    nb = torch.from_numpy(mapper.n_bins.astype(np.int32)).to(dev)
+    exact = torch.from_numpy(np.asarray(mapper.exact, np.uint8)).to(dev)
+    job = DeviceBinning.__new__(DeviceBinning)  # the bin pass alone (no edges kernel)
+    job.hip, job.X, job.dev = hip, Xd, dev
+    job.n, job.F = Xd.shape
+    job.x64 = Xd.dtype == torch.float64
+    job._codes = None
+    codes_rm, codes_fm, flags = job._run_bin(edges_x, nb, exact, max(1, W))
+    if (flags.cpu().numpy() & 2).any():
+        raise ValueError("Input X contains NaN or infinity.")
+    yd = torch.as_tensor(np.ascontiguousarray(y_enc)).to(dev)
+    del F
+    return Prepared(mapper=mapper, codes_rm=codes_rm, codes_fm=codes_fm, nbins=nb, y=yd,
+                    classes=classes, y_exp=int(y_exp), root=None, d_edges64=edges)

@@ -517,10 +517,6 @@ class HipBackend:
         the node count, and the single D2H of the columns."""
         P, C = self.P, self.C
         hip = self.hip
-        done = getattr(self, "_side_done", None)
-        if done is not None:  # overlapped finisher batches must land first
-            torch.cuda.current_stream(self.device).wait_event(done)
-            self._side_done = None
         s = _stream()
         if d_edges is None:
             d_edges = torch.from_numpy(np.ascontiguousarray(edges, np.float64)).to(self.device)
@@ -572,22 +568,11 @@ class HipBackend:
             return
         job_root = torch.empty(J, dtype=torch.int32, device=self.device)
         tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
-        # every tiny subtree has >= 2 rows and they partition the job rows; with
-        # the in-kernel queue (opt-in, C <= 2) a job's records sit at its start
-        # row / 2, and tq lists the published ones (zeroed). Measured on the
-        # 1M x 64 flagship: finisher + tiny kernel 1647 us -> 1571 us in-kernel,
-        # but the fit itself 3.845 ms (off) vs 3.873 / 3.896 ms (on): within
-        # noise, so the spin-waiting consumer stays off by default.
-        queue = (C <= 2 and self.cb == 1 and tiny_rows > 0
-                 and os.environ.get("MPITREE_TINY_QUEUE", "0") == "1")
-        tiny_cap = int(max(job_rows, self.n if queue else 0) // 2 + J + 1)
-        tiny = torch.empty((tiny_cap, 8), dtype=torch.int64, device=self.device)
+        # every tiny subtree has >= 2 rows and they partition the job rows
+        tiny = torch.empty((int(job_rows // 2 + J + 1), 8), dtype=torch.int64,
+                           device=self.device)
         md = -1 if params.max_depth is None else int(params.max_depth)
         grid = int(min(J, int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU))))
-        # every consumer wave's last claim lands past the records: room for
-        # 16 waves per workgroup
-        tq = (torch.zeros(tiny_cap + 16 * grid, dtype=torch.int32, device=self.device)
-              if queue else None)
         prof = None
         if os.environ.get("MPITREE_FIN_PROF"):
             prof = torch.zeros((grid, 10), dtype=torch.int64, device=self.device)
@@ -600,10 +585,8 @@ class HipBackend:
                         self.xtabf.data_ptr(), XTAB_N,
                         rec.data_ptr(), cnt.data_ptr(), job_root.data_ptr(), grid,
                         tiny_rows, tiny.data_ptr(), 4 * N_CU,
-                        0 if prof is None else prof.data_ptr(),
-                        int(os.environ.get("MPITREE_FIN_THREADS", 0)), N_CU,
-                        0 if tq is None else tq.data_ptr())
-        self._fin_keep = (counter, job_root, tiny, d_jobs, tq)
+                        0 if prof is None else prof.data_ptr())
+        self._fin_keep = (counter, job_root, tiny, d_jobs)
         if prof is not None:
             self.last_finisher_prof = prof.cpu().numpy()
 
@@ -621,25 +604,9 @@ class HipBackend:
                             4 * N_CU)
         self._fin_keep = (counter, tiny, d_jobs)
 
-    def finish_subtrees(self, starts, counts, depths, params, stats=None, positions=None,
-                        overlap=False):
-        """See :meth:`_finish_subtrees`; ``overlap`` runs the batch on a side
-        stream (after the rows' partition on the main stream) so later levels
-        and this batch share the GPU. :meth:`assemble_positions` joins it."""
-        if not overlap or positions is None:
-            return self._finish_subtrees(starts, counts, depths, params, stats, positions)
-        main = torch.cuda.current_stream(self.device)
-        if getattr(self, "side", None) is None:
-            self.side = torch.cuda.Stream(self.device)
-        ready = torch.cuda.Event()
-        ready.record(main)
-        self.side.wait_event(ready)
-        with torch.cuda.stream(self.side):
-            self._finish_subtrees(starts, counts, depths, params, stats, positions)
-            done = torch.cuda.Event()
-            done.record(self.side)
-        self._side_done = done
-        return None
+    def finish_subtrees(self, starts, counts, depths, params, stats=None, positions=None):
+        """See :meth:`_finish_subtrees`."""
+        return self._finish_subtrees(starts, counts, depths, params, stats, positions)
 
     def _finish_subtrees(self, starts, counts, depths, params, stats=None, positions=None):
         """Grow every job's subtree on the device.

@@ -11,9 +11,9 @@ completed level, atomically writes the grower's state to ``path``:
 * the frontier (start, count, rows, depth, position of every open node) and
   the subtrees deferred to the finisher,
 * the row permutation (rows grouped by frontier node),
-* a signature of the problem (shapes, hyperparameters, a digest of a strided
-  sample of the binned features and targets), so a checkpoint is never
-  resumed against different data.
+* a signature of the problem (shapes, hyperparameters, an xxh3-128 digest of
+  every binned feature code and target), so a checkpoint is never resumed
+  against different data.
 
 A later ``fit`` with the same ``path`` and problem resumes after the last
 saved level; its tree is identical to an uninterrupted fit's (the sibling
@@ -24,7 +24,6 @@ Single-process fits only (the state is per rank).
 
 from __future__ import annotations
 
-import hashlib
 import os
 
 import numpy as np
@@ -36,25 +35,28 @@ _FR = ("id", "pos", "start", "count", "m", "depth")
 
 
 def problem_signature(codes, y, params, n_classes: int) -> str:
-    """Digest of the fit's inputs (strided sample of codes / targets) and params."""
-    h = hashlib.sha256()
-    n = int(codes.shape[0])
-    step = max(1, n // 4096)
+    """Digest of the fit's full inputs (every binned code and target) and params.
+
+    xxh3-128 over the whole buffers (device tensors are copied to the host
+    once); a checkpoint written for different data never matches."""
+    import xxhash
+
+    h = xxhash.xxh3_128()
 
     def host(a):
         try:
             import torch
 
             if torch.is_tensor(a):
-                return a[::step].cpu().numpy()
+                return a.detach().cpu().numpy()
         except ImportError:  # pragma: no cover
             pass
-        return np.asarray(a)[::step]
+        return np.asarray(a)
 
     h.update(repr((tuple(codes.shape), int(n_classes), int(params.criterion), params.max_depth,
                    params.min_samples_split, params.min_samples_leaf)).encode())
-    h.update(np.ascontiguousarray(host(codes)).tobytes())
-    h.update(np.ascontiguousarray(host(y)).tobytes())
+    for a in (codes, y):
+        h.update(memoryview(np.ascontiguousarray(host(a))).cast("B"))
     return h.hexdigest()
 
 

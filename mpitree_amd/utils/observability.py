@@ -65,10 +65,12 @@ def roctx_range(name: str):
 
 
 def tree_digest(ta) -> int:
-    """63-bit digest of the tree structure: split features and bins, child
-    links and node sizes (thresholds and statistics follow from these and the
-    shared bin edges). xxh3 over the arrays in place: ~0.3 ms for 200k nodes."""
-    parts = (ta.feature, ta.threshold_bin, ta.left, ta.right, ta.n_samples)
+    """63-bit digest of the tree: split features, bins and threshold values,
+    child links and node sizes. Thresholds are hashed too, so ranks that
+    disagree on bin edges (e.g. row shards binned apart) cannot match.
+    xxh3 over the arrays in place: ~0.3 ms for 200k nodes."""
+    thr = np.nan_to_num(np.asarray(ta.threshold, dtype=np.float64), nan=0.0)
+    parts = (ta.feature, ta.threshold_bin, ta.left, ta.right, ta.n_samples, thr)
     try:
         import xxhash
 

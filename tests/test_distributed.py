@@ -210,3 +210,70 @@ def test_cross_rank_digest_check():
     outs = run_ranks(_digest_rank, 2)
     for o in outs:
         assert list(o["r"]) == [True, False]
+
+
+def _sharded_data(seed, regression):
+    """Shards with different value and label sets: rank 0 sees feature values
+    0..7 and labels {0, 1}; rank 1 sees 4..15 and labels {1, 2, 5}."""
+    rng = np.random.default_rng(seed)
+    n = 400
+    X0 = rng.integers(0, 8, size=(n, 4)).astype(np.float64)
+    X1 = rng.integers(4, 16, size=(n, 4)).astype(np.float64) + 0.5
+    s0, s1 = X0 @ [1, -1, 0.5, 0], X1 @ [1, -1, 0.5, 0]
+    if regression:
+        return [X0, X1], [s0 * 0.25, s1 * 3.0]
+    y0 = (s0 > 2).astype(np.int64)
+    y1 = np.choose(np.digitize(s1, [0, 5]), [1, 2, 5])
+    return [X0, X1], [y0, y1]
+
+
+def _fit_sharded(rank, world, regression):
+    from mpitree_amd import ParallelDecisionTreeClassifier, ParallelDecisionTreeRegressor
+    from mpitree_amd.utils.observability import tree_digest
+
+    Xs, ys = _sharded_data(5, regression)
+    cls = ParallelDecisionTreeRegressor if regression else ParallelDecisionTreeClassifier
+    est = cls(strategy="data", device="cpu").fit(Xs[rank], ys[rank], data_sharded=True)
+    ta = est.tree_arrays_
+    out = {k: getattr(ta, k) for k in FIELDS}
+    out["threshold"] = ta.threshold
+    out["value"] = ta.value if regression else ta.count
+    out["digest"] = np.array([tree_digest(ta)])
+    if not regression:
+        out["classes"] = est.classes_
+    return out
+
+
+@pytest.mark.parametrize("regression", [False, True])
+def test_data_sharded_agrees_with_concatenated_fit(regression):
+    """shards must agree on bin edges, classes and the fixed-point
+    scale; the tree equals the single-process fit of the concatenated data."""
+    from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
+
+    outs = run_ranks(_fit_sharded, 2, regression)
+    Xs, ys = _sharded_data(5, regression)
+    X, y = np.concatenate(Xs), np.concatenate(ys)
+    cls = DecisionTreeRegressor if regression else DecisionTreeClassifier
+    ref = cls(device="cpu").fit(X, y)
+    ta = ref.tree_arrays_
+    for o in outs:
+        assert o["digest"][0] == outs[0]["digest"][0]
+        for k in FIELDS:
+            np.testing.assert_array_equal(o[k], getattr(ta, k), err_msg=k)
+        np.testing.assert_array_equal(o["threshold"], ta.threshold)
+        if regression:
+            np.testing.assert_allclose(o["value"], ta.value, rtol=1e-12)
+        else:
+            np.testing.assert_array_equal(o["classes"], ref.classes_)
+            np.testing.assert_array_equal(o["value"], ta.count)
+
+
+def test_tree_digest_covers_thresholds():
+    from mpitree_amd import DecisionTreeClassifier
+    from mpitree_amd.utils.observability import tree_digest
+
+    X = np.array([[0.0], [1.0], [2.0], [3.0]])
+    y = np.array([0, 0, 1, 1])
+    a = DecisionTreeClassifier(device="cpu").fit(X, y).tree_arrays_
+    b = DecisionTreeClassifier(device="cpu").fit(X * 10, y).tree_arrays_
+    assert tree_digest(a) != tree_digest(b)  # same structure, different thresholds

@@ -139,19 +139,6 @@ def test_gpu_tiny_subtree_wave_path(monkeypatch, tiny):
         assert clf.tree_arrays_.equal(ref), (tiny, crit)
 
 
-@pytest.mark.parametrize("crit", ["entropy", "gini"])
-def test_gpu_tiny_queue_matches_oracle(monkeypatch, crit):
-    # opt-in in-kernel tiny-subtree queue (binary labels: the sorted wave path)
-    monkeypatch.setenv("MPITREE_TINY_QUEUE", "1")
-    monkeypatch.setenv("MPITREE_FINISHER_ROWS", "2000")
-    rng = np.random.default_rng(5)
-    n, F, C = 20000, 8, 2
-    X, y = random_problem(rng, n, F, C, levels=40)
-    ref = oracle(X, y, Criterion.ENTROPY if crit == "entropy" else Criterion.GINI, None)
-    clf = DecisionTreeClassifier(criterion=crit, device="cuda").fit(X, y)
-    assert clf.tree_arrays_.equal(ref), crit
-
-
 @pytest.mark.parametrize("regression", [False, True])
 def test_gpu_device_assembly_matches_host(monkeypatch, regression):
     """Pre-order position space + device compaction == host renumbering."""
@@ -194,30 +181,6 @@ def test_gpu_edges_match_host_mapper():
         assert bool(mapper.exact[f]) == bool(host.exact[f]), f
         assert np.array_equal(mapper.edges[f], host.edges[f]), f
     assert np.array_equal(codes_fm.cpu().numpy().T[:, :5], host.transform(X))
-
-
-@pytest.mark.parametrize("F", [4, 12, 64, 68, 132])
-def test_gpu_bin_cols_matches_bin_rows(monkeypatch, F):
-    """Column-search bin kernel (opt-in) == row-search kernel == host transform,
-    both code layouts, ragged row count, an exact feature the sample misses."""
-    from mpitree_amd.ops.hip_backend import gpu_bin_features
-
-    rng = np.random.default_rng(F)
-    n = 70001  # > the device edge sample: exact features can be missed
-    X = rng.normal(size=(n, F)).astype(np.float32)
-    X[:, 1] = rng.integers(0, 200, size=n)
-    X[rng.integers(0, n), 1] = 1000.0  # one rare level: the refit path
-    X[:, 2] = rng.integers(0, 3, size=n)
-    X[:, 3] = np.round(X[:, 3], 1)
-    out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("MPITREE_BIN_COLS", mode)
-        mapper, rm, fm, _ = gpu_bin_features(torch.from_numpy(X).cuda(), 256)
-        out[mode] = (rm.cpu().numpy()[:, :F], fm.cpu().numpy())
-    host = mapper.transform(X)
-    for mode in ("1", "0"):
-        np.testing.assert_array_equal(out[mode][0], host)
-        np.testing.assert_array_equal(out[mode][1].T, host)
 
 
 @pytest.mark.parametrize("labels", ["int64", "int32-gaps", "negative", "float", "host"])

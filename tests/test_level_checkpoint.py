@@ -76,3 +76,22 @@ def test_gpu_resume_equals_device_loop(tmp_path):
     assert res.fit_stats_["engine"] == "hip-levelwise"
     assert res._arrays.equal(ref._arrays, check_impurity=False)
     assert torch.cuda.is_available()
+
+
+def test_signature_covers_every_row():
+    """a change to any single row must change the signature."""
+    from mpitree_amd.core.levelwise import GrowParams
+    from mpitree_amd.utils.level_checkpoint import problem_signature
+
+    rng = np.random.default_rng(0)
+    codes = rng.integers(0, 8, size=(20000, 3)).astype(np.uint8)
+    y = rng.integers(0, 2, size=20000).astype(np.int32)
+    p = GrowParams()
+    base = problem_signature(codes, y, p, 2)
+    for r in (1, 4097, 19999):
+        c2 = codes.copy()
+        c2[r, 1] ^= 1
+        assert problem_signature(c2, y, p, 2) != base
+        y2 = y.copy()
+        y2[r] ^= 1
+        assert problem_signature(codes, y2, p, 2) != base

@@ -5,7 +5,7 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-AB=${1:-MPITREE_BIN_COLS}
+AB=${1:-MPITREE_DEVICE_ASSEMBLY}
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gputests.log 2>&1
 timeout -k 10 120 python -u bench.py --steps 20 --warmup 3 > gpurun_out/bench_on.log 2>&1
 env "$AB=0" timeout -k 10 120 python -u bench.py --steps 20 --warmup 3 > gpurun_out/bench_off.log 2>&1
