@@ -293,7 +293,9 @@ def fit_tree(
         env = os.environ.get("MPITREE_FINISHER_ROWS")
         # ~2 subtree jobs per workgroup slot of the finisher grid
         default_fr = int(env) if env else max(2048, n // 512)
-        if finisher_rows is None:
+        if finisher_rows is None or (comm.world_size > 1 and comm.kind == "data"):
+            # data-parallel GPU ranks finish subtrees on their owners (rows sent
+            # there first), so the finisher applies as on one GPU
             finisher_rows = default_fr
         if not be.finisher_supported():
             finisher_rows = 0

@@ -10,6 +10,7 @@
 #include <pybind11/pybind11.h>
 
 #include "common.h"
+#include "grow.h"
 #include "criterion.h"
 
 namespace py = pybind11;
@@ -46,42 +47,11 @@ void launch_finish(hipStream_t, const void*, int64_t, const void*, int, int64_t,
                    int32_t*, int32_t*, int, int, int64_t*, int, int64_t*);
 int finish_lds_bytes(int F, int B, int C);
 int asm_tiles(int64_t P);
-struct LevelLists {
-  int64_t* pos;
-  int64_t* start;
-  int32_t* cnt;
-  int32_t* depth;
-  int32_t* stats;
-  int64_t* items;
-  int64_t* red;
-  int64_t* der;
-  int64_t* tasks;
-  int32_t* ctl;
-  int64_t* stats64;
-  int64_t* minmax;
-  int64_t* mitems;
-};
-struct PlanArgs {
-  LevelLists cur, nxt;
-  const int64_t* rec;
-  int64_t* split;
-  int64_t* pitems;
-  int32_t* cursors;
-  int32_t* pctl;
-  int32_t* pos_rec;
-  int32_t* pos_st;
-  int64_t* pos_st64;
-  int reg;
-  int out_buf;
-  int64_t* jobs;
-  int32_t* job_count;
-  int C, max_depth, n_cu;
-  int64_t mss, msl, fr;
-  int32_t* host_ctl;
-  int32_t host_tag;
-};
 void launch_grow_plan(hipStream_t, const PlanArgs&);
-void launch_grow_init(hipStream_t, const LevelLists&, int64_t, int64_t, int, int, const int64_t*,
+void launch_fp_combine(hipStream_t, const int64_t*, int, int, int, const int32_t*, int64_t*);
+void launch_grow_dp_fixup(hipStream_t, const PlanArgs&);
+void launch_grow_init(hipStream_t, const LevelLists&, int64_t, int64_t, int64_t, int, int,
+                      const int64_t*,
                       int32_t*);
 int finish_reg_lds_bytes(int B);
 int job_sort_max();
@@ -240,37 +210,59 @@ PYBIND11_MODULE(_hip, m) {
                        uintptr_t counters) {
     mt::launch_job_sort(S(s), P<int64_t>(jobs), J, W, P<int64_t>(out), P<int32_t>(counters));
   });
-  m.def("grow_init", [](uintptr_t s, py::dict lists, int64_t n, int64_t chunk, int C, int reg,
-                        uintptr_t root, uintptr_t job_count) {
-    auto g = [&](const char* k) { return lists[k].cast<uintptr_t>(); };
-    mt::LevelLists L{P<int64_t>(g("pos")),  P<int64_t>(g("start")), P<int32_t>(g("cnt")),
-                     P<int32_t>(g("depth")), P<int32_t>(g("stats")), P<int64_t>(g("items")),
-                     P<int64_t>(g("red")),  P<int64_t>(g("der")),   P<int64_t>(g("tasks")),
-                     P<int32_t>(g("ctl")),  P<int64_t>(g("stats64")), P<int64_t>(g("minmax")),
-                     P<int64_t>(g("mitems"))};
-    mt::launch_grow_init(S(s), L, n, chunk, C, reg, P<int64_t>(root), P<int32_t>(job_count));
+  // level lists: dicts of device pointers {pos, start, cnt, depth, stats, items, red, der,
+  // tasks, ctl, stats64, minmax, mitems, gcnt, src}
+  auto lists = [](py::dict d) {
+    auto g = [&](const char* k) { return d[k].cast<uintptr_t>(); };
+    return mt::LevelLists{P<int64_t>(g("pos")),     P<int64_t>(g("start")), P<int32_t>(g("cnt")),
+                          P<int32_t>(g("depth")),   P<int32_t>(g("stats")), P<int64_t>(g("items")),
+                          P<int64_t>(g("red")),     P<int64_t>(g("der")),   P<int64_t>(g("tasks")),
+                          P<int32_t>(g("ctl")),     P<int64_t>(g("stats64")),
+                          P<int64_t>(g("minmax")),  P<int64_t>(g("mitems")),
+                          P<int32_t>(g("gcnt")),    P<int32_t>(g("src"))};
+  };
+  m.def("grow_init", [lists](uintptr_t s, py::dict L, int64_t n, int64_t n_global, int64_t chunk,
+                             int C, int reg, uintptr_t root, uintptr_t job_count) {
+    mt::launch_grow_init(S(s), lists(L), n, n_global, chunk, C, reg, P<int64_t>(root),
+                         P<int32_t>(job_count));
   });
-  // cur / nxt: dicts of device pointers {pos, start, cnt, depth, stats, items, red, der, ctl}
-  m.def("grow_plan", [](uintptr_t s, py::dict cur, py::dict nxt, uintptr_t rec, uintptr_t split,
-                        uintptr_t pitems, uintptr_t cursors, uintptr_t pctl, uintptr_t pos_rec,
-                        uintptr_t pos_st, uintptr_t pos_st64, int reg, int out_buf,
-                        uintptr_t jobs,
-                        uintptr_t job_count, int C, int max_depth, int n_cu, int64_t mss,
-                        int64_t msl, int64_t fr, uintptr_t host_ctl, int host_tag) {
-    auto lists = [](py::dict d) {
-      auto g = [&](const char* k) { return d[k].cast<uintptr_t>(); };
-      return mt::LevelLists{P<int64_t>(g("pos")),  P<int64_t>(g("start")), P<int32_t>(g("cnt")),
-                            P<int32_t>(g("depth")), P<int32_t>(g("stats")), P<int64_t>(g("items")),
-                            P<int64_t>(g("red")),  P<int64_t>(g("der")),   P<int64_t>(g("tasks")),
-                            P<int32_t>(g("ctl")),  P<int64_t>(g("stats64")),
-                            P<int64_t>(g("minmax")), P<int64_t>(g("mitems"))};
-    };
-    mt::PlanArgs a{lists(cur),          lists(nxt),         P<int64_t>(rec),
-                   P<int64_t>(split),   P<int64_t>(pitems), P<int32_t>(cursors),
-                   P<int32_t>(pctl),    P<int32_t>(pos_rec), P<int32_t>(pos_st),
-                   P<int64_t>(pos_st64), reg, out_buf, P<int64_t>(jobs), P<int32_t>(job_count), C,
-                   max_depth, n_cu, mss, msl, fr, P<int32_t>(host_ctl), host_tag};
-    mt::launch_grow_plan(S(s), a);
+  auto plan_args = [lists](py::dict cur, py::dict nxt, uintptr_t rec, uintptr_t split,
+                           uintptr_t pitems, uintptr_t cursors, uintptr_t pctl, uintptr_t pos_rec,
+                           uintptr_t pos_st, uintptr_t pos_st64, int reg, int out_buf,
+                           uintptr_t jobs, uintptr_t job_count, int C, int max_depth, int n_cu,
+                           int64_t mss, int64_t msl, int64_t fr, uintptr_t host_ctl, int host_tag,
+                           int dp) {
+    return mt::PlanArgs{lists(cur),          lists(nxt),         P<int64_t>(rec),
+                        P<int64_t>(split),   P<int64_t>(pitems), P<int32_t>(cursors),
+                        P<int32_t>(pctl),    P<int32_t>(pos_rec), P<int32_t>(pos_st),
+                        P<int64_t>(pos_st64), reg, out_buf, P<int64_t>(jobs),
+                        P<int32_t>(job_count), C, max_depth, n_cu, mss, msl, fr,
+                        P<int32_t>(host_ctl), host_tag, dp};
+  };
+  m.def("grow_plan", [plan_args](uintptr_t s, py::dict cur, py::dict nxt, uintptr_t rec,
+                                 uintptr_t split, uintptr_t pitems, uintptr_t cursors,
+                                 uintptr_t pctl, uintptr_t pos_rec, uintptr_t pos_st,
+                                 uintptr_t pos_st64, int reg, int out_buf, uintptr_t jobs,
+                                 uintptr_t job_count, int C, int max_depth, int n_cu, int64_t mss,
+                                 int64_t msl, int64_t fr, uintptr_t host_ctl, int host_tag,
+                                 int dp, bool fixup) {
+    const mt::PlanArgs a = plan_args(cur, nxt, rec, split, pitems, cursors, pctl, pos_rec, pos_st,
+                                     pos_st64, reg, out_buf, jobs, job_count, C, max_depth, n_cu,
+                                     mss, msl, fr, host_ctl, host_tag, dp);
+    if (fixup)
+      mt::launch_grow_dp_fixup(S(s), a);
+    else
+      mt::launch_grow_plan(S(s), a);
+  }, py::arg("s"), py::arg("cur"), py::arg("nxt"), py::arg("rec"), py::arg("split"),
+     py::arg("pitems"), py::arg("cursors"), py::arg("pctl"), py::arg("pos_rec"),
+     py::arg("pos_st"), py::arg("pos_st64"), py::arg("reg"), py::arg("out_buf"), py::arg("jobs"),
+     py::arg("job_count"), py::arg("C"), py::arg("max_depth"), py::arg("n_cu"), py::arg("mss"),
+     py::arg("msl"), py::arg("fr"), py::arg("host_ctl"), py::arg("host_tag"), py::arg("dp") = 0,
+     py::arg("fixup") = false);
+  m.def("fp_combine", [](uintptr_t s, uintptr_t g, int nranks, int KB, int R, uintptr_t dcount,
+                         uintptr_t rec) {
+    mt::launch_fp_combine(S(s), P<int64_t>(g), nranks, KB, R, P<int32_t>(dcount),
+                          P<int64_t>(rec));
   });
   // Host-mapped, fine-grained (coherent) memory the kernels can store into
   // directly: the level loop's termination counters travel without a copy.

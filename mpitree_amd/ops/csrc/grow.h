@@ -1,0 +1,54 @@
+// Level-loop work lists and planner arguments (grow.hip), shared with the
+// host bindings.
+#pragma once
+#include <cstdint>
+
+namespace mt {
+
+// Level work lists (one set per level parity). ctl: int32
+// {0: K frontier nodes, 1: built nodes, 2: hist items, 3: slab reductions,
+//  4: derive triples, 5: split nodes, 6: partition items, 7: reduction tasks,
+//  8: min/max items (regression), 9-15: -}
+struct LevelLists {
+  int64_t* pos;     // [KMAX] pre-order position of each frontier slot
+  int64_t* start;   // [KMAX] row segment start
+  int32_t* cnt;     // [KMAX] rows
+  int32_t* depth;   // [KMAX]
+  int32_t* stats;   // [KMAX][C] class counts (classification)
+  int64_t* items;   // [IMAX][4] {slot, start, count, dest slab or -1}
+  int64_t* red;     // [KMAX][3] {slot, first slab, slabs}
+  int64_t* der;     // [KMAX][3] {slot, parent slot (previous level), sibling slot}
+  int64_t* tasks;   // [TMAX][3] {slot, first slab, <= 16 slabs} slab-reduction tasks
+  int32_t* ctl;     // [16]
+  int64_t* stats64; // [KMAX][2] {count, fixed-point target sum} (regression)
+  int64_t* minmax;  // [KMAX][2] target min / max of the slot's rows (regression)
+  int64_t* mitems;  // [MMAX][3] {slot, start, count} min/max work items (regression)
+  // global row count of each slot (decisions, positions, job sizes). Row-replicated
+  // fits alias it to cnt; row-sharded (data-parallel) fits keep this rank's local
+  // segment in start / cnt, filled after the partition by grow_dp_fixup_kernel
+  int32_t* gcnt;    // [KMAX]
+  int32_t* src;     // [KMAX] 2 * (parent's split index) + side (data-parallel only)
+};
+
+struct PlanArgs {
+  LevelLists cur, nxt;
+  const int64_t* rec;  // [KMAX][5 + 2C] split records of the current level
+  int64_t* split;      // [KMAX][4] {start, count, feature, bin}
+  int64_t* pitems;     // [PMAX][3] {split j, start, count}
+  int32_t* cursors;    // [KMAX][2]
+  int32_t* pctl;       // [2] {split nodes, partition items} (aliases cur.ctl + 5)
+  int32_t* pos_rec;    // [P][6]
+  int32_t* pos_st;     // [P][C] class counts (classification)
+  int64_t* pos_st64;   // [P][2] {count, sum} (regression)
+  int reg;
+  int out_buf;         // row buffer (0 idx, 1 tmp) this level's partition writes
+  int64_t* jobs;       // [JMAX][5 + C] finisher jobs
+  int32_t* job_count;
+  int C, max_depth, n_cu;
+  int64_t mss, msl, fr;
+  int32_t* host_ctl;   // [3] host-mapped {next frontier size, jobs so far, tag} or null
+  int32_t host_tag;    // written last: the host polls it to know the slot is complete
+  int dp;              // rows sharded across ranks: local segments fixed up after partition
+};
+
+}  // namespace mt

@@ -24,51 +24,12 @@
 
 #include "common.h"
 #include "criterion.h"
+#include "grow.h"
 
 namespace mt {
 
 constexpr int kPlanThreads = 1024;
 constexpr int kPlanWaves = kPlanThreads / kWave;
-
-// Level work lists (one set per level parity). ctl: int32
-// {0: K frontier nodes, 1: built nodes, 2: hist items, 3: slab reductions,
-//  4: derive triples, 5: split nodes, 6: partition items, 7: reduction tasks,
-//  8: min/max items (regression), 9-15: -}
-struct LevelLists {
-  int64_t* pos;     // [KMAX] pre-order position of each frontier slot
-  int64_t* start;   // [KMAX] row segment start
-  int32_t* cnt;     // [KMAX] rows
-  int32_t* depth;   // [KMAX]
-  int32_t* stats;   // [KMAX][C] class counts (classification)
-  int64_t* items;   // [IMAX][4] {slot, start, count, dest slab or -1}
-  int64_t* red;     // [KMAX][3] {slot, first slab, slabs}
-  int64_t* der;     // [KMAX][3] {slot, parent slot (previous level), sibling slot}
-  int64_t* tasks;   // [TMAX][3] {slot, first slab, <= 16 slabs} slab-reduction tasks
-  int32_t* ctl;     // [16]
-  int64_t* stats64; // [KMAX][2] {count, fixed-point target sum} (regression)
-  int64_t* minmax;  // [KMAX][2] target min / max of the slot's rows (regression)
-  int64_t* mitems;  // [MMAX][3] {slot, start, count} min/max work items (regression)
-};
-
-struct PlanArgs {
-  LevelLists cur, nxt;
-  const int64_t* rec;  // [KMAX][5 + 2C] split records of the current level
-  int64_t* split;      // [KMAX][4] {start, count, feature, bin}
-  int64_t* pitems;     // [PMAX][3] {split j, start, count}
-  int32_t* cursors;    // [KMAX][2]
-  int32_t* pctl;       // [2] {split nodes, partition items} (aliases cur.ctl + 5)
-  int32_t* pos_rec;    // [P][6]
-  int32_t* pos_st;     // [P][C] class counts (classification)
-  int64_t* pos_st64;   // [P][2] {count, sum} (regression)
-  int reg;
-  int out_buf;         // row buffer (0 idx, 1 tmp) this level's partition writes
-  int64_t* jobs;       // [JMAX][5 + C] finisher jobs
-  int32_t* job_count;
-  int C, max_depth, n_cu;
-  int64_t mss, msl, fr;
-  int32_t* host_ctl;   // [3] host-mapped {next frontier size, jobs so far, tag} or null
-  int32_t host_tag;    // written last: the host polls it to know the slot is complete
-};
 
 __device__ __forceinline__ int plan_scan_excl(int v, int* s_w, int& total) {
   const int lane = lane_id(), w = threadIdx.x >> 6;
@@ -99,6 +60,12 @@ __device__ __forceinline__ int plan_rec_width(const PlanArgs& a) {
   return a.reg ? 7 : 5 + 2 * a.C;
 }
 
+// finisher job row: {start, rows, depth, root position, buffer, stats[C]}; data-parallel
+// fits append {local rows, 2 * split index + side} (start / local rows set after partition)
+__device__ __forceinline__ int plan_job_width(const PlanArgs& a) {
+  return 5 + a.C + (a.dp ? 2 : 0);
+}
+
 // Statistic k of child c (0 left, 1 right) of frontier node i: class counts,
 // or {count, fixed-point sum} for regression (the record's left sum at r[5]).
 __device__ __forceinline__ int64_t plan_child_stat(const PlanArgs& a, int i, const int64_t* r,
@@ -124,7 +91,7 @@ __device__ Decision plan_decide(const PlanArgs& a, int i) {
   if (a.reg && a.cur.minmax[(int64_t)i * 2] == a.cur.minmax[(int64_t)i * 2 + 1]) d.split = false;
   d.feature = (int)r[1];
   d.bin = (int)r[2];
-  const int64_t m = a.cur.cnt[i];
+  const int64_t m = a.cur.gcnt[i];
   d.nl = r[3];
   d.nr = m - d.nl;
   d.fate[0] = d.fate[1] = 0;
@@ -151,32 +118,158 @@ __device__ Decision plan_decide(const PlanArgs& a, int i) {
   return d;
 }
 
-__global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
-  __shared__ int s_w[kPlanWaves];
-  __shared__ int s_carry[4];
-  __shared__ long long s_rows;
+// Workgroup-shared scratch of the planner and the data-parallel fixup kernel.
+struct PlanShared {
+  int w[kPlanWaves];
+  int carry[4];
+  long long rows;
   // cooperative expansion of per-node work items: node j of the current chunk
-  // owns items [s_off[j], s_off[j + 1]); every thread writes items, found by a
+  // owns items [off[j], off[j + 1]); every thread writes items, found by a
   // binary search over the offsets, so one large node does not serialise a pass
-  __shared__ int s_off[kPlanThreads + 1];
-  __shared__ long long s_pa[kPlanThreads], s_pb[kPlanThreads];
-  __shared__ int s_pc[kPlanThreads];
+  int off[kPlanThreads + 1];
+  long long pa[kPlanThreads], pb[kPlanThreads];
+  int pc[kPlanThreads];
+};
+
+template <typename Emit>
+__device__ __forceinline__ void plan_expand(PlanShared& sh, int o_local, int total, Emit emit) {
   const int tid = threadIdx.x;
-  auto expand = [&](int o_local, int total, auto emit) {
-    s_off[tid] = o_local;
-    if (tid == 0) s_off[kPlanThreads] = total;
-    __syncthreads();
-    for (int it = tid; it < total; it += kPlanThreads) {
-      int lo = 0, hi = kPlanThreads;  // last j with s_off[j] <= it
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (s_off[mid] <= it) lo = mid; else hi = mid;
+  sh.off[tid] = o_local;
+  if (tid == 0) sh.off[kPlanThreads] = total;
+  __syncthreads();
+  for (int it = tid; it < total; it += kPlanThreads) {
+    int lo = 0, hi = kPlanThreads;  // last j with off[j] <= it
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (sh.off[mid] <= it) lo = mid; else hi = mid;
+    }
+    emit(lo, it - sh.off[lo]);
+  }
+  __syncthreads();
+}
+
+// Histogram items of the next level's built slots [0, NB) (about 2 items per CU
+// over the level's built rows), slab reductions and reduction tasks -> nxt.ctl.
+__device__ void plan_hist_items(const PlanArgs& a, PlanShared& sh, int NB) {
+  const int tid = threadIdx.x;
+  long long built_rows = 0;
+  for (int sl = tid; sl < NB; sl += kPlanThreads) built_rows += a.nxt.cnt[sl];
+  if (tid == 0) sh.rows = 0;
+  __syncthreads();
+  {
+    long long v = built_rows;
+    for (int d = kWave / 2; d > 0; d >>= 1) v += __shfl_xor(v, d, kWave);
+    if (lane_id() == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&sh.rows),
+                                  (unsigned long long)v);
+  }
+  __syncthreads();
+  const long long total = sh.rows;
+  long long chunk = (total + 2LL * a.n_cu - 1) / (2LL * a.n_cu);
+  chunk = chunk < 1024 ? 1024 : (chunk > 65535 ? 65535 : chunk);
+  if (tid == 0) {
+    sh.carry[0] = 0;  // items
+    sh.carry[1] = 0;  // slabs
+    sh.carry[2] = 0;  // reductions
+    sh.carry[3] = 0;  // reduction tasks
+  }
+  __syncthreads();
+  for (int b0 = 0; b0 < NB; b0 += kPlanThreads) {
+    const int sl = b0 + tid;
+    int64_t cnt = 0, kk = 0;
+    if (sl < NB) {
+      cnt = a.nxt.cnt[sl];
+      kk = (cnt + chunk - 1) / chunk;
+      if (kk < 1) kk = 1;
+    }
+    const int multi = kk > 1 ? 1 : 0;
+    const int nt = multi ? (int)((kk + 15) / 16) : 0;
+    int ti, tsl, tr, tt;
+    const int oi_l = plan_scan_excl((int)kk, sh.w, ti);
+    const int osl = plan_scan_excl(multi ? (int)kk : 0, sh.w, tsl) + sh.carry[1];
+    const int orr = plan_scan_excl(multi, sh.w, tr) + sh.carry[2];
+    const int ot = plan_scan_excl(nt, sh.w, tt) + sh.carry[3];
+    sh.pa[tid] = sl < NB ? a.nxt.start[sl] : 0;
+    sh.pb[tid] = cnt;
+    sh.pc[tid] = multi ? osl : -1;
+    const int ibase = sh.carry[0];
+    plan_expand(sh, oi_l, ti, [&](int j, int c) {
+      int64_t* it = a.nxt.items + (int64_t)(ibase + sh.off[j] + c) * 4;
+      const int64_t c0 = (int64_t)c * chunk;
+      const int64_t cn = sh.pb[j] - c0;
+      it[0] = b0 + j;
+      it[1] = sh.pa[j] + c0;
+      it[2] = cn < chunk ? cn : chunk;
+      it[3] = sh.pc[j] >= 0 ? sh.pc[j] + c : -1;
+    });
+    if (sl < NB && multi) {
+      int64_t* rr = a.nxt.red + (int64_t)orr * 3;
+      rr[0] = sl;
+      rr[1] = osl;
+      rr[2] = kk;
+      for (int t = 0; t < nt; ++t) {
+        int64_t* tk = a.nxt.tasks + (int64_t)(ot + t) * 3;
+        tk[0] = sl;
+        tk[1] = osl + 16 * t;
+        tk[2] = (kk - 16 * t) < 16 ? (kk - 16 * t) : 16;
       }
-      emit(lo, it - s_off[lo]);
     }
     __syncthreads();
-  };
+    if (tid == 0) {
+      sh.carry[0] += ti;
+      sh.carry[1] += tsl;
+      sh.carry[2] += tr;
+      sh.carry[3] += tt;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    a.nxt.ctl[2] = sh.carry[0];
+    a.nxt.ctl[3] = sh.carry[2];
+    a.nxt.ctl[7] = sh.carry[3];
+  }
+  __syncthreads();
+}
+
+// Regression: min/max work items (4096 rows) over every next-frontier slot -> nxt.ctl[8].
+__device__ void plan_minmax_items(const PlanArgs& a, PlanShared& sh, int K2) {
+  const int tid = threadIdx.x;
+  __syncthreads();
+  if (tid == 0) sh.carry[0] = 0;
+  __syncthreads();
+  for (int b0 = 0; b0 < K2; b0 += kPlanThreads) {
+    const int sl = b0 + tid;
+    int64_t cnt = 0, kk = 0;
+    if (sl < K2) {
+      cnt = a.nxt.cnt[sl];
+      kk = (cnt + 4095) / 4096;
+      if (kk < 1) kk = 1;
+    }
+    int tm;
+    const int om_l = plan_scan_excl((int)kk, sh.w, tm);
+    sh.pa[tid] = sl < K2 ? a.nxt.start[sl] : 0;
+    sh.pb[tid] = cnt;
+    const int mbase = sh.carry[0];
+    plan_expand(sh, om_l, tm, [&](int j, int c) {
+      int64_t* it = a.nxt.mitems + (int64_t)(mbase + sh.off[j] + c) * 3;
+      const int64_t c0 = (int64_t)c * 4096;
+      const int64_t cn = sh.pb[j] - c0;
+      it[0] = b0 + j;
+      it[1] = sh.pa[j] + c0;
+      it[2] = cn < 4096 ? cn : 4096;
+    });
+    __syncthreads();
+    if (tid == 0) sh.carry[0] += tm;
+    __syncthreads();
+  }
+  if (tid == 0) a.nxt.ctl[8] = sh.carry[0];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
+  __shared__ PlanShared sh;
+  const int tid = threadIdx.x;
   const int C = a.C;
+  const int JW = plan_job_width(a);
   const int K = a.cur.ctl[0];
   // ---- pass 1: totals (built / derived next-frontier children, split nodes)
   int nb_tot = 0, nd_tot = 0;
@@ -189,21 +282,20 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
       nd = (d.fate[0] == 2 && d.fate[1] == 2) ? 1 : 0;
     }
     int t;
-    plan_scan_excl(nb, s_w, t);
+    plan_scan_excl(nb, sh.w, t);
     nb_tot += t;
-    plan_scan_excl(nd, s_w, t);
+    plan_scan_excl(nd, sh.w, t);
     nd_tot += t;
   }
   const int NB = nb_tot;
-  // ---- pass 2: write decided nodes, jobs, split list, next frontier, derive list
   if (tid == 0) {
-    s_carry[0] = 0;  // built slots
-    s_carry[1] = 0;  // derived slots
-    s_carry[2] = 0;  // split nodes
-    s_rows = 0;
+    sh.carry[0] = 0;  // built slots
+    sh.carry[1] = 0;  // derived slots
+    sh.carry[2] = 0;  // split nodes
+    a.nxt.ctl[10] = atomicAdd(a.job_count, 0);  // jobs before this level (dp fixup)
   }
   __syncthreads();
-  long long built_rows = 0;
+  // ---- pass 2: write decided nodes, jobs, split list, next frontier, derive list
   for (int b0 = 0; b0 < K; b0 += kPlanThreads) {
     const int i = b0 + tid;
     Decision d;
@@ -215,13 +307,14 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     const int nd = (d.fate[0] == 2 && d.fate[1] == 2) ? 1 : 0;
     const int ns = d.split ? 1 : 0;
     int tb, td, ts;
-    const int ob = plan_scan_excl(nb, s_w, tb) + s_carry[0];
-    const int od = plan_scan_excl(nd, s_w, td) + s_carry[1];
-    const int os = plan_scan_excl(ns, s_w, ts) + s_carry[2];
+    const int ob = plan_scan_excl(nb, sh.w, tb) + sh.carry[0];
+    const int od = plan_scan_excl(nd, sh.w, td) + sh.carry[1];
+    const int os = plan_scan_excl(ns, sh.w, ts) + sh.carry[2];
     if (i < K) {
       const int64_t pos = a.cur.pos[i];
       const int64_t start = a.cur.start[i];
-      const int64_t m = a.cur.cnt[i];
+      const int64_t m = a.cur.gcnt[i];      // global rows (decisions, positions)
+      const int64_t mloc = a.cur.cnt[i];    // this rank's segment (== m unless dp)
       const int depth = a.cur.depth[i];
       int32_t* P = a.pos_rec + pos * 6;
       const int64_t* r = a.rec + (int64_t)i * plan_rec_width(a);
@@ -244,14 +337,14 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
         P[1] = d.bin;
         P[2] = (int32_t)cpos[0];
         P[3] = (int32_t)cpos[1];
-        // partition list
+        // partition list (this rank's rows of the node)
         int64_t* S = a.split + (int64_t)os * 4;
         S[0] = start;
-        S[1] = m;
+        S[1] = mloc;
         S[2] = d.feature;
         S[3] = d.bin;
         a.cursors[os * 2 + 0] = (int32_t)start;
-        a.cursors[os * 2 + 1] = (int32_t)(start + m);
+        a.cursors[os * 2 + 1] = (int32_t)(start + mloc);
         const int cd = depth + 1;
         int slot[2] = {-1, -1};
         if (d.built >= 0) {
@@ -278,18 +371,24 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
             }
           } else if (d.fate[c] == 1) {  // finisher job
             const int j = atomicAdd(a.job_count, 1);
-            int64_t* J = a.jobs + (int64_t)j * (5 + C);
-            J[0] = cs;
+            int64_t* J = a.jobs + (int64_t)j * JW;
+            J[0] = a.dp ? 0 : cs;
             J[1] = cm;
             J[2] = cd;
             J[3] = cpos[c];
             J[4] = a.out_buf;  // the child's rows live where this level partitions to
             for (int k = 0; k < C; ++k) J[5 + k] = plan_child_stat(a, i, r, d.nl, c, k);
+            if (a.dp) {
+              J[5 + C] = 0;
+              J[6 + C] = 2 * os + c;
+            }
           } else {  // next frontier
             const int sl = slot[c];
             a.nxt.pos[sl] = cpos[c];
-            a.nxt.start[sl] = cs;
-            a.nxt.cnt[sl] = (int32_t)cm;
+            a.nxt.start[sl] = a.dp ? 0 : cs;
+            a.nxt.cnt[sl] = (int32_t)(a.dp ? 0 : cm);
+            a.nxt.gcnt[sl] = (int32_t)cm;
+            a.nxt.src[sl] = 2 * os + c;
             a.nxt.depth[sl] = cd;
             if (a.reg) {
               a.nxt.stats64[(int64_t)sl * 2 + 0] = plan_child_stat(a, i, r, d.nl, c, 0);
@@ -300,9 +399,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
               for (int k = 0; k < C; ++k)
                 a.nxt.stats[(int64_t)sl * C + k] = (int32_t)plan_child_stat(a, i, r, d.nl, c, k);
             }
-            if (c == d.built) {
-              built_rows += cm;
-            } else {  // derived: parent slot i of this level, sibling built slot
+            if (c != d.built) {  // derived: parent slot i of this level, sibling built slot
               int64_t* D = a.nxt.der + (int64_t)(sl - NB) * 3;
               D[0] = sl;
               D[1] = i;
@@ -314,92 +411,22 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     }
     __syncthreads();
     if (tid == 0) {
-      s_carry[0] += tb;
-      s_carry[1] += td;
-      s_carry[2] += ts;
+      sh.carry[0] += tb;
+      sh.carry[1] += td;
+      sh.carry[2] += ts;
     }
     __syncthreads();
   }
-  // total rows of built children -> histogram chunk size (about 2 items per CU)
-  {
-    long long v = built_rows;
-    for (int d = kWave / 2; d > 0; d >>= 1) v += __shfl_xor(v, d, kWave);
-    if (lane_id() == 0) atomicAdd(reinterpret_cast<unsigned long long*>(&s_rows),
-                                  (unsigned long long)v);
-  }
-  __syncthreads();
-  const int ND = s_carry[1];
-  const int NS = s_carry[2];
+  const int ND = sh.carry[1];
+  const int NS = sh.carry[2];
   const int K2 = NB + ND;
-  const long long total = s_rows;
-  long long chunk = (total + 2LL * a.n_cu - 1) / (2LL * a.n_cu);
-  chunk = chunk < 1024 ? 1024 : (chunk > 65535 ? 65535 : chunk);
-  // ---- pass 3: histogram items of the next level's built slots [0, NB)
-  if (tid == 0) {
-    s_carry[0] = 0;  // items
-    s_carry[1] = 0;  // slabs
-    s_carry[2] = 0;  // reductions
-    s_carry[3] = 0;  // reduction tasks
-  }
+  __threadfence_block();  // nxt.start / cnt written above are read by other threads below
   __syncthreads();
-  for (int b0 = 0; b0 < NB; b0 += kPlanThreads) {
-    const int sl = b0 + tid;
-    int64_t cnt = 0, kk = 0;
-    if (sl < NB) {
-      cnt = a.nxt.cnt[sl];
-      kk = (cnt + chunk - 1) / chunk;
-      if (kk < 1) kk = 1;
-    }
-    const int multi = kk > 1 ? 1 : 0;
-    const int nt = multi ? (int)((kk + 15) / 16) : 0;
-    int ti, tsl, tr, tt;
-    const int oi_l = plan_scan_excl((int)kk, s_w, ti);
-    const int oi = oi_l + s_carry[0];
-    const int osl = plan_scan_excl(multi ? (int)kk : 0, s_w, tsl) + s_carry[1];
-    const int orr = plan_scan_excl(multi, s_w, tr) + s_carry[2];
-    const int ot = plan_scan_excl(nt, s_w, tt) + s_carry[3];
-    s_pa[tid] = sl < NB ? a.nxt.start[sl] : 0;
-    s_pb[tid] = cnt;
-    s_pc[tid] = multi ? osl : -1;
-    const int ibase = s_carry[0];
-    expand(oi_l, ti, [&](int j, int c) {
-      int64_t* it = a.nxt.items + (int64_t)(ibase + s_off[j] + c) * 4;
-      const int64_t c0 = (int64_t)c * chunk;
-      const int64_t cn = s_pb[j] - c0;
-      it[0] = b0 + j;
-      it[1] = s_pa[j] + c0;
-      it[2] = cn < chunk ? cn : chunk;
-      it[3] = s_pc[j] >= 0 ? s_pc[j] + c : -1;
-    });
-    if (sl < NB) {
-      if (multi) {
-        int64_t* rr = a.nxt.red + (int64_t)orr * 3;
-        rr[0] = sl;
-        rr[1] = osl;
-        rr[2] = kk;
-        for (int t = 0; t < nt; ++t) {
-          int64_t* tk = a.nxt.tasks + (int64_t)(ot + t) * 3;
-          tk[0] = sl;
-          tk[1] = osl + 16 * t;
-          tk[2] = (kk - 16 * t) < 16 ? (kk - 16 * t) : 16;
-        }
-      }
-    }
-    __syncthreads();
-    if (tid == 0) {
-      s_carry[0] += ti;
-      s_carry[1] += tsl;
-      s_carry[2] += tr;
-      s_carry[3] += tt;
-    }
-    __syncthreads();
-  }
-  const int n_items = s_carry[0];
-  const int n_red = s_carry[2];
-  const int n_tasks = s_carry[3];
+  // ---- pass 3: histogram items of the next level's built slots (dp: after the partition)
+  if (!a.dp) plan_hist_items(a, sh, NB);
   // ---- pass 4: partition items of this level's split nodes (1024 rows each)
   __syncthreads();
-  if (tid == 0) s_carry[3] = 0;
+  if (tid == 0) sh.carry[3] = 0;
   __syncthreads();
   for (int b0 = 0; b0 < NS; b0 += kPlanThreads) {
     const int j = b0 + tid;
@@ -410,69 +437,36 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
       if (kk < 1) kk = 1;
     }
     int tp;
-    const int op_l = plan_scan_excl((int)kk, s_w, tp);
-    s_pa[tid] = j < NS ? a.split[(int64_t)j * 4 + 0] : 0;
-    s_pb[tid] = cnt;
-    const int pbase = s_carry[3];
-    expand(op_l, tp, [&](int jj, int c) {
-      int64_t* it = a.pitems + (int64_t)(pbase + s_off[jj] + c) * 3;
+    const int op_l = plan_scan_excl((int)kk, sh.w, tp);
+    sh.pa[tid] = j < NS ? a.split[(int64_t)j * 4 + 0] : 0;
+    sh.pb[tid] = cnt;
+    const int pbase = sh.carry[3];
+    plan_expand(sh, op_l, tp, [&](int jj, int c) {
+      int64_t* it = a.pitems + (int64_t)(pbase + sh.off[jj] + c) * 3;
       const int64_t c0 = (int64_t)c * 1024;
-      const int64_t cn = s_pb[jj] - c0;
+      const int64_t cn = sh.pb[jj] - c0;
       it[0] = b0 + jj;
-      it[1] = s_pa[jj] + c0;
+      it[1] = sh.pa[jj] + c0;
       it[2] = cn < 1024 ? cn : 1024;
     });
     __syncthreads();
-    if (tid == 0) s_carry[3] += tp;
+    if (tid == 0) sh.carry[3] += tp;
     __syncthreads();
   }
+  const int n_pitems = sh.carry[3];
   // ---- pass 5 (regression): min/max work items over every next-frontier slot
-  int n_mitems = 0;
-  if (a.reg) {
-    __syncthreads();
-    if (tid == 0) s_carry[0] = 0;
-    __syncthreads();
-    for (int b0 = 0; b0 < K2; b0 += kPlanThreads) {
-      const int sl = b0 + tid;
-      int64_t cnt = 0, kk = 0;
-      if (sl < K2) {
-        cnt = a.nxt.cnt[sl];
-        kk = (cnt + 4095) / 4096;
-        if (kk < 1) kk = 1;
-      }
-      int tm;
-      const int om_l = plan_scan_excl((int)kk, s_w, tm);
-      s_pa[tid] = sl < K2 ? a.nxt.start[sl] : 0;
-      s_pb[tid] = cnt;
-      const int mbase = s_carry[0];
-      expand(om_l, tm, [&](int j, int c) {
-        int64_t* it = a.nxt.mitems + (int64_t)(mbase + s_off[j] + c) * 3;
-        const int64_t c0 = (int64_t)c * 4096;
-        const int64_t cn = s_pb[j] - c0;
-        it[0] = b0 + j;
-        it[1] = s_pa[j] + c0;
-        it[2] = cn < 4096 ? cn : 4096;
-      });
-      __syncthreads();
-      if (tid == 0) s_carry[0] += tm;
-      __syncthreads();
-    }
-    n_mitems = s_carry[0];
-  }
+  if (a.reg && !a.dp) plan_minmax_items(a, sh, K2);
   if (tid == 0) {
-    a.nxt.ctl[8] = n_mitems;
+    if (!a.reg) a.nxt.ctl[8] = 0;
     a.nxt.ctl[0] = K2;
     a.nxt.ctl[1] = NB;
-    a.nxt.ctl[2] = n_items;
-    a.nxt.ctl[3] = n_red;
     a.nxt.ctl[4] = ND;
     a.nxt.ctl[5] = 0;
     a.nxt.ctl[6] = 0;
-    a.nxt.ctl[7] = n_tasks;
     const int jobs_so_far = atomicAdd(a.job_count, 0);
     a.nxt.ctl[9] = jobs_so_far;  // finisher jobs so far
     a.pctl[0] = NS;
-    a.pctl[1] = s_carry[3];
+    a.pctl[1] = n_pitems;
     if (a.host_ctl) {  // the host's lagged termination read, stored straight to host memory
       __hip_atomic_store(a.host_ctl + 1, jobs_so_far, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(a.host_ctl, K2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -482,10 +476,86 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
   }
 }
 
+// Data-parallel levels: after this rank's partition, every next-frontier slot
+// and every job appended this level learns its local row segment from its
+// parent's split cursors (left child: [start, cursor0), right: [cursor0, end)),
+// then the next level's histogram (and regression min/max) work items are built
+// from the local counts. One workgroup, like the planner.
+__global__ __launch_bounds__(kPlanThreads) void grow_dp_fixup_kernel(PlanArgs a) {
+  __shared__ PlanShared sh;
+  const int tid = threadIdx.x;
+  const int K2 = a.nxt.ctl[0];
+  const int NB = a.nxt.ctl[1];
+  const int j0 = a.nxt.ctl[10], j1 = a.nxt.ctl[9];
+  const int C = a.C;
+  const int JW = plan_job_width(a);
+  auto seg = [&](int src, int64_t& st, int64_t& cn) {
+    const int j = src >> 1, c = src & 1;
+    const int64_t s0 = a.split[(int64_t)j * 4 + 0];
+    const int64_t ml = a.split[(int64_t)j * 4 + 1];
+    const int64_t nl = (int64_t)a.cursors[j * 2 + 0] - s0;
+    st = c ? s0 + nl : s0;
+    cn = c ? ml - nl : nl;
+  };
+  for (int sl = tid; sl < K2; sl += kPlanThreads) {
+    int64_t st, cn;
+    seg(a.nxt.src[sl], st, cn);
+    a.nxt.start[sl] = st;
+    a.nxt.cnt[sl] = (int32_t)cn;
+  }
+  for (int t = j0 + tid; t < j1; t += kPlanThreads) {
+    int64_t* J = a.jobs + (int64_t)t * JW;
+    int64_t st, cn;
+    seg((int)J[6 + C], st, cn);
+    J[0] = st;
+    J[5 + C] = cn;
+  }
+  __threadfence_block();
+  __syncthreads();
+  plan_hist_items(a, sh, NB);
+  if (a.reg) plan_minmax_items(a, sh, K2);
+}
+
+// Feature-parallel levels: every rank scanned its own feature block; the
+// all-gathered records g[P][KB][R] are reduced per node to the best split
+// (max gain; ties to the lowest rank = the lowest feature, as select_kernel
+// breaks ties within a rank), written to rec[K][R].
+__global__ __launch_bounds__(256) void fp_combine_kernel(const int64_t* __restrict__ g, int P,
+                                                         int KB, int R,
+                                                         const int32_t* __restrict__ dcount,
+                                                         int64_t* __restrict__ rec) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *dcount || i >= KB) return;
+  int best = 0;
+  double bg = __longlong_as_double((long long)g[(int64_t)i * R]);
+  for (int r = 1; r < P; ++r) {
+    const double gr = __longlong_as_double((long long)g[((int64_t)r * KB + i) * R]);
+    if (gr > bg) {
+      bg = gr;
+      best = r;
+    }
+  }
+  const int64_t* src = g + ((int64_t)best * KB + i) * R;
+  for (int k = 0; k < R; ++k) rec[(int64_t)i * R + k] = src[k];
+}
+
+void launch_fp_combine(hipStream_t stream, const int64_t* g, int P, int KB, int R,
+                       const int32_t* dcount, int64_t* rec) {
+  if (KB <= 0) return;
+  hipLaunchKernelGGL(fp_combine_kernel, dim3((KB + 255) / 256), dim3(256), 0, stream, g, P, KB,
+                     R, dcount, rec);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_grow_dp_fixup(hipStream_t stream, const PlanArgs& a) {
+  hipLaunchKernelGGL(grow_dp_fixup_kernel, dim3(1), dim3(kPlanThreads), 0, stream, a);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
 // Level 0 (the root, built from rows) in one launch: root stats come from a
 // small device array (classification: C counts; regression: count, sum, min, max).
-__global__ __launch_bounds__(256) void grow_init_kernel(LevelLists L, int64_t n, int64_t chunk,
-                                                        int C, int reg,
+__global__ __launch_bounds__(256) void grow_init_kernel(LevelLists L, int64_t n, int64_t n_global,
+                                                        int64_t chunk, int C, int reg,
                                                         const int64_t* __restrict__ root,
                                                         int32_t* __restrict__ job_count) {
   const int64_t k = (n + chunk - 1) / chunk;
@@ -507,7 +577,9 @@ __global__ __launch_bounds__(256) void grow_init_kernel(LevelLists L, int64_t n,
     *job_count = 0;
     L.pos[0] = 0;
     L.start[0] = 0;
-    L.cnt[0] = (int32_t)n;
+    L.cnt[0] = (int32_t)n;  // this rank's rows (all of them unless row-sharded)
+    L.gcnt[0] = (int32_t)n_global;
+    L.src[0] = 0;
     L.depth[0] = 0;
     if (reg) {
       L.stats64[0] = root[0];
@@ -531,10 +603,10 @@ __global__ __launch_bounds__(256) void grow_init_kernel(LevelLists L, int64_t n,
   }
 }
 
-void launch_grow_init(hipStream_t stream, const LevelLists& L, int64_t n, int64_t chunk, int C,
-                      int reg, const int64_t* root, int32_t* job_count) {
-  hipLaunchKernelGGL(grow_init_kernel, dim3(1), dim3(256), 0, stream, L, n, chunk, C, reg, root,
-                     job_count);
+void launch_grow_init(hipStream_t stream, const LevelLists& L, int64_t n, int64_t n_global,
+                      int64_t chunk, int C, int reg, const int64_t* root, int32_t* job_count) {
+  hipLaunchKernelGGL(grow_init_kernel, dim3(1), dim3(256), 0, stream, L, n, n_global, chunk, C,
+                     reg, root, job_count);
   MT_HIP_CHECK(hipGetLastError());
 }
 

@@ -20,8 +20,30 @@ sorts the device job list (largest first) and launches the subtree finisher;
 the position space is compacted by ``assemble.hip``. The resulting tree is
 bitwise identical to the host-driven builder's (tests/test_gpu_kernels.py).
 
+Multi-GPU (one process per GPU, RCCL over xGMI; collectives are enqueued on
+the stream between the level kernels, never a host round trip):
+
+* feature-parallel (``strategy="feature"`` / ``"auto"``): rows replicated,
+  every rank builds and scans histograms of its own contiguous feature block
+  only; one ``all_gather_into_tensor`` of the per-node split records per level
+  feeds ``fp_combine_kernel`` (max gain, ties to the lowest feature), after
+  which the planner and partition run identically on every rank;
+* data-parallel (``strategy="data"``): rows sharded, the built (smaller-child)
+  histograms of each level are summed with one ``all_reduce`` (integer counts:
+  exact, order independent); local row segments are fixed up after the
+  partition (``grow_dp_fixup_kernel``); regression purity takes one min/max
+  all-reduce per level;
+* subtree jobs (nodes of at most ``finisher_rows`` rows) are split across
+  ranks (serpentine over the largest-first job order); data-parallel ranks
+  first send each job's rows to its owner (one ``all_to_all``); one
+  all-gather of the finished nodes leaves every rank with the full tree.
+
+Every mode produces the single-GPU tree bit for bit (tests/test_gpu_kernels.py,
+tests/test_distributed.py).
+
 Reference parity: mpitree/tree/decision_tree.py:93-166 (growth),
-:63-91 (split search), :150-164 (recursion / stopping rules).
+:63-91 (split search), :150-164 (recursion / stopping rules), :446-477
+(subtree task parallelism, here the job split + node all-gather).
 """
 
 from __future__ import annotations
@@ -79,11 +101,7 @@ def device_loop_supported(be, params, comm) -> bool:
     if os.environ.get("MPITREE_DEVICE_LOOP", "1") == "0":
         return False
     if getattr(comm, "world_size", 1) != 1:
-        # replicated rows: every rank runs the (cheap) level loop, the finisher
-        # jobs are split across ranks and the finished nodes all-gathered
-        if getattr(comm, "kind", "") not in ("auto", "subtree"):
-            return False
-        if not getattr(comm, "rows_replicated", False):
+        if getattr(comm, "kind", "") not in ("auto", "subtree", "feature", "data"):
             return False
     if params.finisher_rows <= 0 or not be.finisher_supported():
         return False
@@ -113,11 +131,20 @@ class DeviceGrower:
             tasks=torch.empty((TMAX, 3), **i64), ctl=torch.zeros(16, **i32),
             stats64=torch.empty((k_reg, 2), **i64), minmax=torch.empty((k_reg, 2), **i64),
             mitems=torch.empty((MMAX if reg else 1, 3), **i64),
+            gcnt=torch.empty(KMAX, **i32), src=torch.empty(KMAX, **i32),
         )
 
+    @staticmethod
+    def _owners(J: int, P: int, device) -> torch.Tensor:
+        """Serpentine job owners over the largest-first order (0..P-1, P-1..0, ...):
+        near-even row totals, identical on every rank (the order is total)."""
+        k = torch.arange(J, device=device)
+        lap, off = k // P, k % P
+        return torch.where(lap % 2 == 0, off, P - 1 - off)
+
     def _run_jobs(self, d_jobs, n: int, counter=None):
-        """Finish the (largest-first) job list; with several ranks each takes a
-        serpentine share (0..P-1, P-1..0, ...) -- near-even row totals."""
+        """Finish the (largest-first) job list; with several ranks each takes its
+        serpentine share."""
         be, comm = self.be, self.comm
         sim = int(os.environ.get("MPITREE_SIM_RANKS", "0"))
         if comm is not None and comm.world_size > 1:
@@ -127,9 +154,7 @@ class DeviceGrower:
             # serpentine share alone on the GPU, then finish the rest so the
             # tree stays complete -- the per-rank finisher critical path of a
             # P-GPU fit, measured on one GPU
-            k = torch.arange(d_jobs.shape[0], device=d_jobs.device)
-            lap, off = k // sim, k % sim
-            owner = torch.where(lap % 2 == 0, off, sim - 1 - off)
+            owner = self._owners(d_jobs.shape[0], sim, d_jobs.device)
             mine, rest = d_jobs[owner == 0].contiguous(), d_jobs[owner != 0].contiguous()
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             ev[0].record()
@@ -144,19 +169,84 @@ class DeviceGrower:
             self.stats["sim_rank0_jobs"] = int(mine.shape[0])
             return
         if comm is not None and comm.world_size > 1:
-            P, r = comm.world_size, comm.rank
-            k = torch.arange(d_jobs.shape[0], device=d_jobs.device)
-            lap, off = k // P, k % P
-            owner = torch.where(lap % 2 == 0, off, P - 1 - off)
-            d_jobs = d_jobs[owner == r]
+            owner = self._owners(d_jobs.shape[0], comm.world_size, d_jobs.device)
+            d_jobs = d_jobs[owner == comm.rank]
             counter = None
-            # positions the (replicated) level loop decided: every rank has
-            # them, so the exchange sends only what this rank's finisher grew
-            self._pre_live = be.pos_rec[:, 5] > 0
         J = int(d_jobs.shape[0])
         if J:
             be.launch_finisher(d_jobs.contiguous(), J, n, self.p, be.pos_rec, be.pos_st,
                                counter)
+
+    def _dp_finish(self, d_jobs, W: int):
+        """Data-parallel subtree finishing: each job's rows are spread over the
+        ranks; every rank sends its share of job j to owner(j) (one all_to_all of
+        row-major codes + targets), the owner lays its jobs' rows out
+        contiguously and runs the finisher on them (into the shared position
+        space). Jobs: int64 [J][W] = {local start, rows, depth, pos, buffer,
+        stats[C], local rows, src}."""
+        be, comm, p = self.be, self.comm, self.p
+        dev = be.device
+        P, r = comm.world_size, comm.rank
+        C = be.C
+        J = int(d_jobs.shape[0])
+        owner = self._owners(J, P, dev)
+        lstart, lcnt = d_jobs[:, 0], d_jobs[:, 5 + C]
+        # every rank's local rows per job: [P, J]
+        allc = torch.empty(P * J, dtype=torch.int64, device=dev)
+        comm.all_gather_device(allc, lcnt.contiguous())
+        allc = allc.view(P, J)
+        # this rank's rows, grouped by destination (job order within a destination)
+        order = torch.argsort(owner, stable=True)
+        cnt_o = lcnt[order]
+        seg_id = torch.repeat_interleave(torch.arange(J, device=dev), cnt_o)
+        seg_first = torch.cumsum(cnt_o, 0) - cnt_o
+        pos_in = torch.arange(seg_id.numel(), device=dev) - seg_first[seg_id]
+        jsel = order[seg_id]
+        ent_i = be.idx[lstart[jsel] + pos_in]
+        ent_t = be.tmp[lstart[jsel] + pos_in]
+        ent = torch.where(d_jobs[jsel, 4] == 0, ent_i, ent_t)
+        rows = (ent.long() & be.row_mask)
+        send_counts = torch.zeros(P, dtype=torch.int64, device=dev).index_add_(0, owner, lcnt)
+        recv_counts = allc[:, owner == r].sum(1)  # from each source rank
+        sc = send_counts.cpu().tolist()  # one host sync per fit (the all_to_all needs the splits)
+        rc = recv_counts.cpu().tolist()
+        R_tot = int(sum(rc))
+        codes_s = be.codes_rm.index_select(0, rows)
+        y_s = be.y.index_select(0, rows)
+        codes_r = torch.empty((R_tot,) + tuple(be.codes_rm.shape[1:]), dtype=be.codes_rm.dtype,
+                              device=dev)
+        y_r = torch.empty(R_tot, dtype=be.y.dtype, device=dev)
+        comm.all_to_all_device(codes_r, codes_s, rc, sc)
+        comm.all_to_all_device(y_r, y_s, rc, sc)
+        self.stats["dp_rows_exchanged"] = int(sum(sc))
+        mine = torch.nonzero(owner == r).squeeze(1)  # owned jobs, in job order
+        Jm = int(mine.numel())
+        if Jm == 0:
+            return
+        cm = allc[:, mine]                       # [P, Jm] rows of each owned job per source
+        gcount = cm.sum(0)                       # == d_jobs[mine, 1]
+        new_start = torch.cumsum(gcount, 0) - gcount
+        # segment (s, j): source block offset + prefix within the block -> new position
+        blk = torch.cumsum(recv_counts, 0) - recv_counts
+        within = torch.cumsum(cm, 1) - cm        # offset of job j inside source s's block
+        dst_off = new_start[None, :] + (torch.cumsum(cm, 0) - cm)
+        src_off = blk[:, None] + within
+        flat = cm.reshape(-1)
+        sid = torch.repeat_interleave(torch.arange(flat.numel(), device=dev), flat)
+        first = torch.cumsum(flat, 0) - flat
+        k = torch.arange(sid.numel(), device=dev) - first[sid]
+        perm = torch.empty(R_tot, dtype=torch.int64, device=dev)
+        perm[dst_off.reshape(-1)[sid] + k] = src_off.reshape(-1)[sid] + k
+        codes_rm = codes_r.index_select(0, perm)
+        y_loc = y_r.index_select(0, perm).contiguous()
+        codes_fm = codes_rm[:, : be.F].t().contiguous()
+        be2 = hb.HipBackend(dev)
+        be2.setup(codes_rm, codes_fm, y_loc, be.nbins, n_bins=be.B, n_classes=C,
+                  criterion=be.crit)
+        jobs2 = torch.cat([new_start[:, None], d_jobs[mine, 1:5], d_jobs[mine, 5:5 + C]], 1)
+        jobs2[:, 4] = 0  # rows in be2.idx
+        be2.launch_finisher(jobs2.contiguous(), Jm, R_tot, p, be.pos_rec, be.pos_st)
+        self._dp_keep = (be2, codes_r, y_r, jobs2)
 
     def _exchange_nodes(self):
         """Every rank ends with every finished node: compact the positions this
@@ -208,13 +298,28 @@ class DeviceGrower:
             _WORKSPACES.pop(next(iter(_WORKSPACES)))
         return ws
 
+    def _mode(self, F: int):
+        """(feature-parallel?, data-parallel?, f_lo, f_hi) of this rank."""
+        comm = self.comm
+        P = getattr(comm, "world_size", 1)
+        kind = getattr(comm, "kind", "local")
+        if P <= 1:
+            return False, False, 0, F
+        if kind == "data":
+            return False, True, 0, F
+        if kind in ("feature", "auto") and F >= P:
+            lo, hi = comm.feature_range(F)
+            return True, False, int(lo), int(hi)
+        return False, False, 0, F  # subtree: replicated levels, split finisher
+
     def fit(self, n: int, n_classes: int, n_features: int, edges, y_exp: int = 0,
             root=None, d_edges=None) -> TreeArrays:
-        """Grow the tree. ``edges``: host edge table ``[F, W]`` or a BinMapper
-        (only materialised when ``d_edges``, the device copy, is absent);
-        ``root``: root statistics when the caller already has them
-        (gpu_prepare), which saves a device round trip."""
-        be, p = self.be, self.p
+        """Grow the tree. ``n``: this rank's rows (all rows unless data-parallel);
+        ``edges``: host edge table ``[F, W]`` or a BinMapper (only materialised
+        when ``d_edges``, the device copy, is absent); ``root``: root statistics
+        when the caller already has them (gpu_prepare), which saves a device
+        round trip."""
+        be, p, comm = self.be, self.p, self.comm
         hip = be.hip
         dev = be.device
         reg = bool(be.reg)
@@ -222,12 +327,19 @@ class DeviceGrower:
         fr = int(p.finisher_rows)
         md = -1 if p.max_depth is None else int(p.max_depth)
         mss, msl = int(p.min_samples_split), int(max(1, p.min_samples_leaf))
+        fp, dp, f_lo, f_hi = self._mode(F)
+        F_h = f_hi - f_lo
+        P = getattr(comm, "world_size", 1)
         s = hb._stream
         t0 = time.perf_counter()
+        n_loc = int(n)
         if root is None:
-            root_full = be.segment_stats(np.array([0]), np.array([n]))[0]  # one small sync
+            root_full = be.segment_stats(np.array([0]), np.array([n_loc]))[0]  # one small sync
         else:
             root_full = np.asarray(root, dtype=np.int64)
+        if dp:  # global root statistics and row count (one small host collective)
+            root_full = comm.reduce_stats(np.asarray(root_full, np.int64)[None, :], reg)[0]
+        n = int(root_full[0]) if reg else int(np.sum(root_full))  # global rows
         be.begin_positions(2 * n - 1)
         if reg:  # {count, sum, min, max}: a root with equal targets is a leaf
             root = root_full[:2]
@@ -236,40 +348,43 @@ class DeviceGrower:
             root = root_full
             pure = int((root > 0).sum()) <= 1
         root_term = (md == 0) or n < mss or n < 2 * msl or pure
+        W = 5 + C + (2 if dp else 0)  # finisher job row width (dp: + local rows, src)
         jobs_host = None
         if root_term:
             be.put_positions([0], [-1], [-1], [-1], [-1], [0], [n], root[None, :])
         elif n <= fr:  # the whole tree is one finisher job
-            jobs_host = np.concatenate([[0, n, 0, 0, 0], root]).astype(np.int64)[None, :]
+            row = [0, n, 0, 0, 0] + list(root) + ([n_loc, 0] if dp else [])
+            jobs_host = np.asarray(row, np.int64)[None, :]
         self.timings["stats"] = time.perf_counter() - t0
         levels = 0
         J = 0
         t0 = time.perf_counter()
+        comm_bytes = []
         if not root_term and jobs_host is None:
             KMAX = n // (fr + 1) + 2
-            IMAX = KMAX + n // 1024 + 2 * hb.N_CU + 16
-            PMAX = KMAX + n // 1024 + 16
+            IMAX = KMAX + n_loc // 1024 + 2 * hb.N_CU + 16
+            PMAX = KMAX + n_loc // 1024 + 16
             JMAX = n // 2 + 2
             R = 7 if reg else 5 + 2 * C
             # multi-item nodes hold > max(1024, level rows / 512) rows each
-            RMAX = int(min(KMAX, max(2 * hb.N_CU + 1, n // 1024 + 1)))
+            RMAX = int(min(KMAX, max(2 * hb.N_CU + 1, n_loc // 1024 + 1)))
             TMAX = RMAX + IMAX // 16 + 16
-            MMAX = KMAX + n // 4096 + 16
-            E = F * B * C
+            MMAX = KMAX + n_loc // 4096 + 16
+            E = F_h * B * C
             hdt = torch.int64 if reg else torch.int32
-            W = 7 if reg else 5 + C  # finisher job row width
 
             def make():
                 i64 = dict(dtype=torch.int64, device=dev)
                 return dict(
                     sets=[self._lists(KMAX, IMAX, TMAX, MMAX, C, reg, dev) for _ in range(2)],
-                    hists=[torch.empty((KMAX, F, B, C), dtype=hdt, device=dev)
+                    hists=[torch.empty((KMAX, F_h, B, C), dtype=hdt, device=dev)
                            for _ in range(2)],
-                    slab=torch.empty((IMAX, hip.hist_slab_words(F, B, C, reg)), dtype=hdt,
+                    slab=torch.empty((IMAX, hip.hist_slab_words(F_h, B, C, reg)), dtype=hdt,
                                      device=dev),
                     rec=torch.empty((KMAX, R), **i64),
-                    cost=torch.empty((KMAX, F), dtype=torch.float64, device=dev),
-                    bins=torch.empty((KMAX, F), dtype=torch.int32, device=dev),
+                    grec=torch.empty((P * KMAX * R) if fp else 1, **i64),
+                    cost=torch.empty((KMAX, F_h), dtype=torch.float64, device=dev),
+                    bins=torch.empty((KMAX, F_h), dtype=torch.int32, device=dev),
                     ident=torch.arange(KMAX, **i64),
                     split=torch.empty((KMAX, 4), **i64),
                     pitems=torch.empty((PMAX, 3), **i64),
@@ -282,7 +397,7 @@ class DeviceGrower:
                     root_host=torch.empty(4 if reg else C, dtype=torch.int64, pin_memory=True),
                 )
 
-            ws = self._workspace((str(dev), n, F, B, C, reg, fr), make)
+            ws = self._workspace((str(dev), n, n_loc, F, f_lo, F_h, B, C, reg, fr, dp), make)
             sets, hists, slab, rec = ws["sets"], ws["hists"], ws["slab"], ws["rec"]
             cost, bins, ident, split = ws["cost"], ws["bins"], ws["ident"], ws["split"]
             pitems, cursors, jobs, job_count = (ws["pitems"], ws["cursors"], ws["jobs"],
@@ -292,10 +407,10 @@ class DeviceGrower:
             tag0 = _FIT_SEQ[0] << 12
             ptrs = [self._ptrs(x) for x in sets]
             # level 0: the root, built from rows (one init launch; root stats H2D)
-            chunk = int(min(hb.MAX_ITEM_ROWS, max(1024, -(-n // (2 * hb.N_CU)))))
+            chunk = int(min(hb.MAX_ITEM_ROWS, max(1024, -(-n_loc // (2 * hb.N_CU)))))
             ws["root_host"].numpy()[: root_full.size] = root_full
             ws["root"].copy_(ws["root_host"], non_blocking=True)
-            hip.grow_init(s(), ptrs[0], n, chunk, C, int(reg), ws["root"].data_ptr(),
+            hip.grow_init(s(), ptrs[0], n_loc, n, chunk, C, int(reg), ws["root"].data_ptr(),
                           job_count.data_ptr())
             cb, rs = be.cb, be.row_elems * be.cb
             bufs = (be.idx.data_ptr(), be.tmp.data_ptr())
@@ -310,14 +425,25 @@ class DeviceGrower:
                     e.record()
                     marks[-1].append(e)
 
+            def plan(cur, nxt, lvl, fixup=False):
+                hip.grow_plan(s(), cur, nxt, rec.data_ptr(), split.data_ptr(), pitems.data_ptr(),
+                              cursors.data_ptr(), cur["ctl"] + 4 * 5, be.pos_rec.data_ptr(),
+                              0 if reg else be.pos_st.data_ptr(),
+                              be.pos_st.data_ptr() if reg else 0, int(reg), (lvl + 1) % 2,
+                              jobs.data_ptr(), job_count.data_ptr(), C, md, hb.N_CU, mss, msl,
+                              fr, 0 if fixup else hctl_dev + (lvl % 64) * 64,
+                              tag0 + (lvl % 4096) + 1, dp=int(dp), fixup=fixup)
+
             while True:
+                b0 = getattr(comm, "bytes_communicated", 0)
                 if prof:
                     marks.append([])
                     mark()
                 cur, nxt = ptrs[lvl % 2], ptrs[(lvl + 1) % 2]
+                nxt_t = sets[(lvl + 1) % 2]
                 H, Hp = hists[lvl % 2], hists[(lvl + 1) % 2]
                 kb = int(min(2 ** min(lvl, 40), KMAX))
-                ib = int(min(IMAX, kb + n // 1024 + 2 * hb.N_CU + 1))
+                ib = int(min(IMAX, kb + n_loc // 1024 + 2 * hb.N_CU + 1))
                 ctl = cur["ctl"]
                 # rows alternate between the two permutation buffers level by level
                 src, dst = bufs[lvl % 2], bufs[(lvl + 1) % 2]
@@ -325,43 +451,58 @@ class DeviceGrower:
                 # classification: the hist launch also zeroes the slots the slab
                 # reduction adds into (one launch less per level)
                 hip.hist(s(), be.codes_rm.data_ptr(), cb, rs, src, be.y.data_ptr(),
-                         be.lab_shift, cur["items"], ib, H.data_ptr(), slab.data_ptr(), F, 0, B, C,
-                         reg, hb.LDS_BUDGET, dcount=ctl + 4 * 2,
+                         be.lab_shift, cur["items"], ib, H.data_ptr(), slab.data_ptr(), F_h, f_lo,
+                         B, C, reg, hb.LDS_BUDGET, dcount=ctl + 4 * 2,
                          zred=0 if reg else cur["red"], zred_bound=0 if reg else rb,
                          zcount=0 if reg else ctl + 4 * 3)
                 if reg:  # slabs summed straight into the slot
-                    hip.hist_reduce(s(), cur["red"], rb, 1, slab.data_ptr(), H.data_ptr(), F, B, C,
-                                    True, dcount=ctl + 4 * 3)
+                    hip.hist_reduce(s(), cur["red"], rb, 1, slab.data_ptr(), H.data_ptr(), F_h, B,
+                                    C, True, dcount=ctl + 4 * 3)
                 else:
                     hip.hist_reduce_tasks(s(), cur["red"], rb, cur["tasks"],
                                           int(min(TMAX, rb + ib // 16 + 1)), slab.data_ptr(),
-                                          H.data_ptr(), F, B, C, ctl + 4 * 3, ctl + 4 * 7,
+                                          H.data_ptr(), F_h, B, C, ctl + 4 * 3, ctl + 4 * 7,
                                           zero=False)
+                if dp:  # sum the built slots' histograms over the row shards
+                    if lvl >= 2:  # built slots <= splits of the previous level (lagged read)
+                        nbb = int(hctl[(lvl - 2) % 64, 0])
+                    else:
+                        nbb = 1
+                    nbb = max(1, min(nbb, KMAX))
+                    comm.all_reduce_device(H[:nbb])
                 mark()
                 if lvl > 0:
                     hip.hist_derive(s(), cur["der"], kb, Hp.data_ptr(), H.data_ptr(), E, reg,
                                     dcount=ctl + 4 * 4)
-                hip.scan(s(), H.data_ptr(), ident.data_ptr(), kb, be.nbins.data_ptr(), F, 0, B, C,
-                         int(be.crit), msl, cost.data_ptr(), bins.data_ptr(), rec.data_ptr(),
-                         be.xtab.data_ptr(), hb.XTAB_N, dcount=ctl)
+                hip.scan(s(), H.data_ptr(), ident.data_ptr(), kb, be.nbins.data_ptr(), F_h, f_lo,
+                         B, C, int(be.crit), msl, cost.data_ptr(), bins.data_ptr(),
+                         rec.data_ptr(), be.xtab.data_ptr(), hb.XTAB_N, dcount=ctl)
+                if fp:  # every rank's best split of each node -> the global best
+                    g = ws["grec"][: P * kb * R]
+                    comm.all_gather_device(g, rec[:kb].reshape(-1))
+                    hip.fp_combine(s(), g.data_ptr(), P, kb, R, ctl, rec.data_ptr())
                 mark()
-                hip.grow_plan(s(), cur, nxt, rec.data_ptr(), split.data_ptr(), pitems.data_ptr(),
-                              cursors.data_ptr(), ctl + 4 * 5, be.pos_rec.data_ptr(),
-                              0 if reg else be.pos_st.data_ptr(),
-                              be.pos_st.data_ptr() if reg else 0, int(reg), (lvl + 1) % 2,
-                              jobs.data_ptr(),
-                              job_count.data_ptr(), C, md, hb.N_CU, mss, msl, fr,
-                              hctl_dev + (lvl % 64) * 64, tag0 + (lvl % 4096) + 1)
+                plan(cur, nxt, lvl)
                 mark()
-                pb = int(min(PMAX, n // 1024 + kb + 1))
+                pb = int(min(PMAX, n_loc // 1024 + kb + 1))
                 hip.partition(s(), be.codes_fm.data_ptr(), cb, be.n, src, dst, be.row_mask,
                               pitems.data_ptr(), pb, split.data_ptr(), cursors.data_ptr(),
                               dcount=ctl + 4 * 6, copy_back=False)
+                if dp:  # local segments of the next frontier / new jobs, then its work items
+                    plan(cur, nxt, lvl, fixup=True)
                 if reg:  # purity of the next frontier, read by the next planner
+                    kbn = int(min(2 * kb, KMAX))
                     hip.seg_minmax(s(), dst, be.y.data_ptr(), nxt["mitems"],
-                                   int(min(MMAX, 2 * kb + n // 4096 + 1)), nxt["minmax"],
+                                   int(min(MMAX, 2 * kb + n_loc // 4096 + 1)), nxt["minmax"],
                                    nxt["ctl"] + 4 * 8)
+                    if dp:  # global min / max: one MAX all-reduce of (-min, max)
+                        mm = nxt_t["minmax"][:kbn]
+                        mm[:, 0].neg_()
+                        comm.all_reduce_device(mm, op=torch.distributed.ReduceOp.MAX)
+                        mm[:, 0].neg_()
                 mark()
+                if comm is not None and P > 1:
+                    comm_bytes.append(int(getattr(comm, "bytes_communicated", 0) - b0))
                 # lagged completion check: the planner stored the next level's
                 # frontier size + job count into host slot lvl % 64
                 lvl += 1
@@ -376,6 +517,8 @@ class DeviceGrower:
             J = int(hctl[done_at % 64, 1])  # finisher jobs appended
             if prof:
                 self._level_profile(marks[:levels])
+            if P > 1:  # positions the (replicated) level loop decided: on every rank already
+                self._pre_live = be.pos_rec[:, 5] > 0
             if J:
                 counter = None
                 if J <= hip.job_sort_max():  # one-workgroup sort, zeroes the counters too
@@ -388,15 +531,28 @@ class DeviceGrower:
                     order = torch.argsort(jobs[:J, 1] * (1 << 32) - jobs[:J, 3],
                                           descending=True)
                     d_jobs = jobs[:J].index_select(0, order)
-                self._run_jobs(d_jobs, n, counter)
+                if dp:
+                    self._dp_finish(d_jobs, W)
+                else:
+                    self._run_jobs(d_jobs, n, counter)
         elif jobs_host is not None:
             J = 1
             (d_jobs,) = be.up(jobs_host)
-            self._run_jobs(d_jobs.view(1, -1), n)
-        if self.comm is not None and self.comm.world_size > 1:
+            if P > 1:
+                self._pre_live = be.pos_rec[:, 5] > 0
+            if dp:
+                self._dp_finish(d_jobs.view(1, -1), W)
+            else:
+                self._run_jobs(d_jobs.view(1, -1), n)
+        if comm is not None and P > 1:
             t1 = time.perf_counter()
+            b0 = comm.bytes_communicated
             self._exchange_nodes()
             self.timings["exchange"] = time.perf_counter() - t1
+            self.stats["comm_bytes_per_level"] = comm_bytes
+            self.stats["comm_bytes_exchange"] = int(comm.bytes_communicated - b0)
+            self.stats["mode"] = "data" if dp else ("feature" if fp else "replicated")
+            self.stats["feature_block"] = [f_lo, f_hi]
         self.timings["levels"] = time.perf_counter() - t0
         self.stats["levels"] = levels
         self.stats["finisher_subtrees"] = J
@@ -411,6 +567,7 @@ class DeviceGrower:
             self.stats["sim_rank0_finisher_ms"] = ev[0].elapsed_time(ev[1])
             self.stats["sim_rest_finisher_ms"] = ev[1].elapsed_time(ev[2])
             self._sim_events = None
+        self._dp_keep = None
         st = a["stats"]
         ta = TreeArrays(
             feature=a["feature"], threshold=a["threshold"], threshold_bin=a["bin"],

@@ -198,6 +198,46 @@ class DistComm(LocalComm):
         parts = [out[r * kmax : r * kmax + int(sizes[r])] for r in range(self.world_size)]
         return torch.cat(parts, 0).to(t.device)
 
+    # ------------------------------------------- device-resident collectives
+    # The device level loop enqueues these between its kernels: with RCCL the
+    # collective runs on the process group's stream ordered after the current
+    # stream's kernels and the current stream waits for it -- no host sync.
+    # A gloo group (CPU rehearsal of GPU ranks) stages through host memory.
+    def _staged(self, t: torch.Tensor) -> bool:
+        return t.device.type != self.device.type
+
+    def all_gather_device(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        """``out[r * inp.numel():...] = inp`` of rank r (flat, same dtype)."""
+        if self._staged(inp):
+            o = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_gather_into_tensor(o, inp.cpu(), group=self.group)
+            out.copy_(o)
+        else:
+            dist.all_gather_into_tensor(out, inp, group=self.group)
+        self.bytes_communicated += inp.numel() * inp.element_size() * self.world_size
+
+    def all_reduce_device(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> None:
+        if self._staged(t):
+            h = t.cpu()
+            dist.all_reduce(h, op=op, group=self.group)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op, group=self.group)
+        self.bytes_communicated += t.numel() * t.element_size()
+
+    def all_to_all_device(self, out: torch.Tensor, inp: torch.Tensor, out_splits: list,
+                          in_splits: list) -> None:
+        """Rows (dim 0) of ``inp`` go to ranks by ``in_splits``; ``out`` receives by
+        ``out_splits`` (host lists, one entry per rank)."""
+        if self._staged(inp):
+            o = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
+            out.copy_(o)
+        else:
+            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+        row = inp[0].numel() * inp.element_size() if inp.dim() > 1 else inp.element_size()
+        self.bytes_communicated += int(sum(in_splits)) * row
+
     def check_consistent(self, digest: int) -> bool:
         """Cross-rank check that every rank built the same tree."""
         a = self._all_gather(np.array([digest], dtype=np.int64))

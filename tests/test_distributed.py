@@ -112,14 +112,14 @@ def test_gpu_ranks_equal_serial(strategy, monkeypatch):
     X, y = _data(4, n=5000, F=9, C=3)
     ref = DecisionTreeClassifier(device="cpu").fit(X, y).tree_arrays_
     for o in outs:
-        eng = str(o["engine"][0])
-        # auto/subtree: replicated device level loop + split finisher + node exchange
-        assert eng == ("hip-device-loop" if strategy in ("auto", "subtree") else "hip-levelwise")
+        # every strategy runs the device level loop (feature / data / replicated
+        # levels, split finisher, node exchange)
+        assert str(o["engine"][0]) == "hip-device-loop"
         for k in FIELDS:
             np.testing.assert_array_equal(o[k], getattr(ref, k))
 
 
-def _fit_rank_gpu_large(rank, world, regression):
+def _fit_rank_gpu_large(rank, world, regression, strategy="auto"):
     import torch
 
     from mpitree_amd import ParallelDecisionTreeClassifier, ParallelDecisionTreeRegressor
@@ -134,25 +134,30 @@ def _fit_rank_gpu_large(rank, world, regression):
         cls = ParallelDecisionTreeClassifier
     outs = {}
     for it in range(2):  # repeated fits: the job split must not depend on append order
-        est = cls(strategy="auto", device="cuda").fit(X, y)
+        est = cls(strategy=strategy, device="cuda").fit(X, y)
         ta = est.tree_arrays_
         for k in FIELDS:
             outs[f"{k}{it}"] = getattr(ta, k)
         outs[f"engine{it}"] = np.array([est.fit_stats_["engine"]])
+        outs[f"mode{it}"] = np.array([est.fit_stats_.get("mode", "")])
+        outs[f"bytes{it}"] = np.array(est.fit_stats_.get("comm_bytes_per_level", [0]))
     return outs
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("regression", [False, True])
-def test_gpu_ranks_equal_single_gpu_at_scale(regression):
+@pytest.mark.parametrize("strategy", ["auto", "data", "subtree"])
+def test_gpu_ranks_equal_single_gpu_at_scale(regression, strategy):
     """Thousands of finisher jobs (many with equal row counts) split over two
-    ranks: every rank, every repeat, equals the single-GPU device-loop tree."""
+    ranks; feature-parallel (auto), data-parallel and replicated levels: every
+    rank, every repeat, equals the single-GPU device-loop tree."""
     import torch
 
     from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
     from mpitree_amd.utils.datasets import make_classification, make_regression
 
-    outs = run_ranks(_fit_rank_gpu_large, 2, regression, start_method="spawn")
+    outs = run_ranks(_fit_rank_gpu_large, 2, regression, strategy, start_method="spawn")
+    want = {"auto": "feature", "data": "data", "subtree": "replicated"}[strategy]
     dev = torch.device("cuda", 0)
     if regression:
         X, y = make_regression(200_000, 16, levels=64, seed=5, device=dev)
@@ -163,6 +168,9 @@ def test_gpu_ranks_equal_single_gpu_at_scale(regression):
     for o in outs:
         for it in range(2):
             assert str(o[f"engine{it}"][0]) == "hip-device-loop"
+            assert str(o[f"mode{it}"][0]) == want
+            if want != "replicated":
+                assert o[f"bytes{it}"].sum() > 0  # per-level collectives ran
             for k in FIELDS:
                 np.testing.assert_array_equal(o[f"{k}{it}"], getattr(ref, k), err_msg=k)
 
