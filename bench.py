@@ -11,7 +11,13 @@ subtree finishing and the host copy of the tree arrays.
 Single GPU: ``python bench.py``. Multi-GPU (one process per GPU, RCCL):
 ``torchrun --nproc-per-node N bench.py --gpus N``; every rank holds the full
 data (the reference's ParallelDecisionTreeClassifier contract) and the total
-work is fixed, so scaling is "strong".
+work is fixed, so scaling is "strong". ``--strategy auto`` (default) runs the
+feature-parallel device level loop (each rank builds and scans F/N features,
+one RCCL all-gather of split records per level) and splits the subtree
+finisher jobs across ranks; ``--strategy data`` runs row-sharded histograms
+with one RCCL all-reduce per level (BASELINE config 4:
+``--n 10000000 --features 128 --strategy data``). The JSON line reports the
+level loop that actually ran (``config.level_loop``) and the bytes moved.
 
 ``MPITREE_BENCH_BACKEND=gloo`` rehearses the multi-rank path with ranks
 sharing the visible GPUs (collectives over gloo instead of RCCL).
@@ -32,6 +38,7 @@ import torch
 METRIC = "tree fit wall-clock (s) + samples/sec, 1M\u00d764 synthetic at 1/2/4/8 GPUs"
 CONFIG = "1M\u00d764 synthetic, feature-parallel split search, RCCL all-reduce on 8\u00d7MI355X"
 CONFIG_REG = "1M\u00d764 regression tree (MSE split criterion) on 8\u00d7MI355X"
+CONFIG_10M = "10M\u00d7128 synthetic, data-parallel histogram all-reduce, 288 GB HBM sizing, 8 GPUs"
 
 
 def main(argv=None):
@@ -101,6 +108,18 @@ def main(argv=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     stats = est.fit_stats_
+    mode = stats.get("mode", "single-gpu")
+    if world > 1:
+        parallelism = {"feature": f"fp{world}", "data": f"dp{world}",
+                       "replicated": f"subtree{world}"}.get(mode, f"{a.strategy}{world}")
+    else:
+        parallelism = "single"
+    if a.regression:
+        cfg_name = CONFIG_REG
+    elif a.n >= 10_000_000 and a.features >= 128:
+        cfg_name = CONFIG_10M
+    else:
+        cfg_name = CONFIG
     if rank == 0:
         value = a.n / dt
         out = {
@@ -121,7 +140,7 @@ def main(argv=None):
             "data": "synthetic (generated on device: 256-level quantized features, labels from "
                     "a random linear + interaction score with Gaussian noise)",
             "config": {
-                "name": CONFIG if not a.regression else CONFIG_REG,
+                "name": cfg_name,
                 "model": f"DecisionTree{'Regressor' if a.regression else 'Classifier'}"
                          f"(criterion={crit}, max_depth={md})",
                 "n_samples": a.n,
@@ -129,7 +148,13 @@ def main(argv=None):
                 "n_classes": None if a.regression else a.classes,
                 "global_batch": a.n,
                 "seq_len": a.features,
-                "parallelism": f"{a.strategy}{world}" if world > 1 else "single",
+                "parallelism": parallelism,
+                "strategy": a.strategy,
+                "engine": stats.get("engine"),
+                "level_loop": mode,
+                "feature_block": stats.get("feature_block"),
+                "comm_bytes": int(sum(stats.get("comm_bytes_per_level", [])))
+                + int(stats.get("comm_bytes_exchange", 0)),
                 "tree_nodes": stats.get("node_count"),
                 "tree_depth": stats.get("max_depth"),
             },

@@ -175,6 +175,64 @@ def test_gpu_ranks_equal_single_gpu_at_scale(regression, strategy):
                 np.testing.assert_array_equal(o[f"{k}{it}"], getattr(ref, k), err_msg=k)
 
 
+def _fit_rank_rccl(rank, world, strategy, regression):
+    import torch
+    import torch.distributed as dist
+
+    from mpitree_amd import ParallelDecisionTreeClassifier, ParallelDecisionTreeRegressor
+    from mpitree_amd.utils.datasets import make_classification, make_regression
+
+    assert dist.get_backend() == "nccl"
+    dev = torch.device("cuda", rank)
+    if regression:
+        X, y = make_regression(200_000, 16, levels=64, seed=5, device=dev)
+        cls = ParallelDecisionTreeRegressor
+    else:
+        X, y = make_classification(300_000, 16, seed=5, device=dev)
+        cls = ParallelDecisionTreeClassifier
+    est = cls(strategy=strategy, device="cuda").fit(X, y)
+    ta = est.tree_arrays_
+    out = {k: getattr(ta, k) for k in FIELDS}
+    out["mode"] = np.array([est.fit_stats_.get("mode", "")])
+    return out
+
+
+def _gpus() -> int:
+    try:
+        import torch
+
+        return torch.cuda.device_count()
+    except Exception:  # pragma: no cover
+        return 0
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(_gpus() < 2, reason="RCCL needs one GPU per rank (>= 2 visible)")
+@pytest.mark.parametrize("strategy,regression", [("auto", False), ("data", False),
+                                                 ("auto", True), ("data", True)])
+def test_rccl_ranks_equal_single_gpu(strategy, regression):
+    """Real RCCL (nccl backend, device_id init, on-stream collectives over xGMI):
+    2 ranks on 2 GPUs build the single-GPU tree bit for bit."""
+    import torch
+
+    from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
+    from mpitree_amd.utils.datasets import make_classification, make_regression
+
+    outs = run_ranks(_fit_rank_rccl, 2, strategy, regression, start_method="spawn",
+                     backend="nccl")
+    dev = torch.device("cuda", 0)
+    if regression:
+        X, y = make_regression(200_000, 16, levels=64, seed=5, device=dev)
+        ref = DecisionTreeRegressor(device="cuda").fit(X, y).tree_arrays_
+    else:
+        X, y = make_classification(300_000, 16, seed=5, device=dev)
+        ref = DecisionTreeClassifier(device="cuda").fit(X, y).tree_arrays_
+    for o in outs:
+        assert str(o["mode"][0]) == ("data" if strategy == "data" else "feature")
+        for k in FIELDS:
+            np.testing.assert_array_equal(o[k], getattr(ref, k), err_msg=k)
+
+
 def _fault_rank(rank, world, fault_rank):
     import os
 
