@@ -12,7 +12,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .criterion import Criterion, entropy_term, gini_term, mse_term
+from .criterion import Criterion, entropy_term, gini_term, mse_term, tie_round
 
 __all__ = ["NumpyBackend"]
 
@@ -109,6 +109,7 @@ class NumpyBackend:
                 else:
                     cost = gini_term(L) + gini_term(tot - L)
                     pt = float(gini_term(tot[0, 0]))
+                cost = tie_round(cost, m)
                 nonempty = hs.sum(-1) > 0
             valid = nonempty & (mL >= msl) & (m - mL >= msl)
             cost = np.where(valid, cost, np.inf)

@@ -10,7 +10,9 @@ values use quantile edges drawn from the data (every edge is a data value and
 ``x <= edges[b]`` <=> ``code <= b`` still holds), bounding the histogram size
 that the gfx950 kernels work on.
 
-Codes are ``uint8`` when every feature fits in 256 bins, else ``uint16``.
+Codes are ``uint8`` when every feature fits in 256 bins, ``uint16`` up to
+65536 and ``uint32`` beyond (``max_bins=None``, the default, keeps every
+unique value of every feature, as the reference does).
 """
 
 from __future__ import annotations
@@ -52,7 +54,8 @@ class BinMapper:
 
     @property
     def code_dtype(self):
-        return np.uint8 if self.max_n_bins <= 256 else np.uint16
+        b = self.max_n_bins
+        return np.uint8 if b <= 256 else (np.uint16 if b <= 65536 else np.uint32)
 
     def padded_edges(self, dtype=np.float64) -> np.ndarray:
         """[F, Bmax] edge table padded with +inf (what the kernels search)."""
@@ -111,16 +114,16 @@ class TableBinMapper(BinMapper):
 def fit_bin_mapper(X: np.ndarray, max_bins=256, sample: int | None = None, seed: int = 0):
     """Compute per-feature edges on the host.
 
-    ``max_bins=None`` requests exact mode for every feature (up to 65536
-    unique values). ``sample`` limits the rows used for quantile features;
-    exact features are always detected on the full column.
+    ``max_bins=None`` requests exact mode for every feature (every unique
+    value is an edge, however many). ``sample`` limits the rows used for
+    quantile features; exact features are always detected on the full column.
     """
     X = np.asarray(X)
     if X.ndim != 2:
         raise ValueError("X must be 2-D")
-    limit = MAX_BINS_LIMIT if max_bins is None else int(max_bins)
-    if not 2 <= limit <= MAX_BINS_LIMIT:
-        raise ValueError(f"max_bins must be in [2, {MAX_BINS_LIMIT}]")
+    if max_bins is not None and not 2 <= int(max_bins) <= MAX_BINS_LIMIT:
+        raise ValueError(f"max_bins must be None or in [2, {MAX_BINS_LIMIT}]")
+    limit = np.iinfo(np.int64).max if max_bins is None else int(max_bins)
     n, F = X.shape
     edges, exact = [], np.zeros(F, dtype=bool)
     rows = None
@@ -134,11 +137,6 @@ def fit_bin_mapper(X: np.ndarray, max_bins=256, sample: int | None = None, seed:
             edges.append(u)
             exact[f] = True
             continue
-        if max_bins is None:
-            raise ValueError(
-                f"feature {f} has {u.shape[0]} unique values; exact mode supports "
-                f"at most {MAX_BINS_LIMIT}"
-            )
         src = np.sort(col[rows]) if rows is not None else np.sort(col)
         edges.append(quantile_edges(src, limit))
-    return BinMapper(edges=edges, exact=exact, max_bins=limit)
+    return BinMapper(edges=edges, exact=exact, max_bins=max_bins)

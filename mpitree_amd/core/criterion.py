@@ -16,6 +16,7 @@ import numpy as np
 __all__ = [
     "Criterion",
     "xlog2x",
+    "tie_round",
     "entropy_term",
     "gini_term",
     "mse_term",
@@ -112,6 +113,18 @@ def gini_term(counts: np.ndarray, axis: int = -1) -> np.ndarray:
     with np.errstate(invalid="ignore", divide="ignore"):
         out = num / m.astype(np.float64)
     return np.where(m > 0, out, 0.0)
+
+
+def tie_round(cost, m) -> np.ndarray:
+    """Canonical ties (``criterion.h`` ``tie_unit``/``tie_round``): a node's
+    candidate costs on a grid of ``2^-32 * (T(m) + m)``, so mathematically equal
+    costs compare equal and the first candidate (lowest threshold, then lowest
+    feature -- the reference's rule, ``decision_tree.py:88-90, 140``) wins."""
+    unit = (xlog2x(np.asarray(m, dtype=np.int64)) + np.asarray(m, dtype=np.float64)) \
+        * 2.3283064365386963e-10
+    inv = 1.0 / unit
+    with np.errstate(invalid="ignore"):
+        return np.rint(np.asarray(cost, dtype=np.float64) * inv) * unit
 
 
 def mse_term(m, s_fixed) -> np.ndarray:

@@ -201,7 +201,7 @@ def fit_tree(
     max_depth,
     min_samples_split,
     min_samples_leaf=1,
-    max_bins=256,
+    max_bins=None,
     device="auto",
     comm=None,
     finisher_rows=None,

@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .criterion import Criterion, entropy_term, gini_term, mse_term
+from .criterion import Criterion, entropy_term, gini_term, mse_term, tie_round
 from ..models.tree_arrays import TreeArrays
 
 __all__ = ["best_split_dense", "fit_reference"]
@@ -57,7 +57,7 @@ def best_split_dense(hist, crit, parent_term, m_total, min_samples_leaf=1, hist_
         R = tot - L
         mL = L.sum(-1)
         mR = m_total - mL
-        cost = _terms(crit, L) + _terms(crit, R)
+        cost = tie_round(_terms(crit, L) + _terms(crit, R), m_total)
         nonempty = cnt.sum(-1) > 0
     valid = nonempty & (mL >= max(1, min_samples_leaf)) & (mR >= max(1, min_samples_leaf))
     cost = np.where(valid, cost, np.inf)

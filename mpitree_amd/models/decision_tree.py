@@ -64,7 +64,7 @@ class _BaseTree(BaseEstimator):
         min_samples_split: int = 2,
         criterion: str = "entropy",
         min_samples_leaf: int = 1,
-        max_bins: int | None = 256,
+        max_bins: int | None = None,
         device: str = "auto",
     ):
         self.max_depth = max_depth
@@ -192,7 +192,7 @@ class _BaseTree(BaseEstimator):
         self.__dict__.update(state)
         # parameters added by this framework default when loading reference pickles
         defaults = {"criterion": "squared_error" if self._regression else "entropy",
-                    "min_samples_leaf": 1, "max_bins": 256, "device": "auto"}
+                    "min_samples_leaf": 1, "max_bins": None, "device": "auto"}
         for k, v in defaults.items():
             self.__dict__.setdefault(k, v)
         if tree is not None:
@@ -226,10 +226,12 @@ class DecisionTreeClassifier(_BaseTree, ClassifierMixin):
         Nodes with fewer rows become leaves.
     criterion : {"entropy", "gini"}, default="entropy"
     min_samples_leaf : int, default=1
-    max_bins : int or None, default=256
-        Features with at most this many unique values use every unique value
-        as a threshold (the reference's exact search); others use quantile
-        bins. ``None`` forces exact thresholds (up to 65536 unique values).
+    max_bins : int or None, default=None
+        ``None`` (default): every unique value of a feature is a candidate
+        threshold, exactly the reference's search (``decision_tree.py:73``).
+        An int opts into quantile binning: features with at most this many
+        unique values stay exact, others get ``max_bins`` quantile edges
+        (every edge a data value).
     device : {"auto", "cpu", "cuda"}, default="auto"
     """
 
@@ -274,7 +276,7 @@ class DecisionTreeRegressor(_BaseTree, RegressorMixin):
         min_samples_split: int = 2,
         criterion: str = "squared_error",
         min_samples_leaf: int = 1,
-        max_bins: int | None = 256,
+        max_bins: int | None = None,
         device: str = "auto",
     ):
         super().__init__(
@@ -400,7 +402,7 @@ class ParallelDecisionTreeClassifier(_ParallelMixin, DecisionTreeClassifier):
         min_samples_split: int = 2,
         criterion: str = "entropy",
         min_samples_leaf: int = 1,
-        max_bins: int | None = 256,
+        max_bins: int | None = None,
         device: str = "auto",
         strategy: str = "auto",
     ):
@@ -425,7 +427,7 @@ class ParallelDecisionTreeRegressor(_ParallelMixin, DecisionTreeRegressor):
         min_samples_split: int = 2,
         criterion: str = "squared_error",
         min_samples_leaf: int = 1,
-        max_bins: int | None = 256,
+        max_bins: int | None = None,
         device: str = "auto",
         strategy: str = "auto",
     ):

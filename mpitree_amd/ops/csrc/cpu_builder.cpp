@@ -84,6 +84,8 @@ py::dict build_tree(py::array codes, py::array y, py::array_t<int32_t> nbins, in
   if (codes.ndim() != 2) throw std::invalid_argument("codes must be 2-D");
   if (py::isinstance<py::array_t<uint8_t>>(codes))
     return build_impl<uint8_t>(codes, y, nbins, C, crit, max_depth, mss, msl, n_threads);
+  if (py::isinstance<py::array_t<uint32_t>>(codes))  // exact mode, > 65536 unique values
+    return build_impl<uint32_t>(codes, y, nbins, C, crit, max_depth, mss, msl, n_threads);
   return build_impl<uint16_t>(codes, y, nbins, C, crit, max_depth, mss, msl, n_threads);
 }
 

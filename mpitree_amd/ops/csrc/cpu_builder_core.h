@@ -92,12 +92,15 @@ struct Builder {
     std::vector<int64_t> L(np, 0), R(np);
     double best_cost = std::numeric_limits<double>::infinity();
     int best_b = -1;
+    const double tu = tie_unit(xlog2x((uint64_t)m), m);  // canonical ties (criterion.h)
+    const double tinv = 1.0 / tu;
     auto eval = [&](int b, int64_t ml) {
       const int64_t mr = m - ml;
       if (ml < p.msl || mr < p.msl || ml <= 0 || mr <= 0) return;
       for (int i = 0; i < np; ++i) R[i] = tot[i] - L[i];
-      const double cost = term_cls(L.data(), present.data(), np, ml) +
-                          term_cls(R.data(), present.data(), np, mr);
+      const double cost = tie_round(term_cls(L.data(), present.data(), np, ml) +
+                                        term_cls(R.data(), present.data(), np, mr),
+                                    tinv, tu);
       if (cost < best_cost) {
         best_cost = cost;
         best_b = b;

@@ -17,6 +17,7 @@
 // hipcc, so the host oracle, the host builder and the device kernels produce
 // identical bits (tests/test_criterion.py checks the numpy mirror as well).
 #pragma once
+#include <math.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -90,6 +91,27 @@ MT_HD double xlog2x(uint64_t x) {
 MT_HD double gini_term(int64_t m, int64_t sumsq) {
   if (m <= 0) return 0.0;
   return (double)(m * m - sumsq) / (double)m;
+}
+
+// Canonical ties (every classification engine). Splits whose costs are
+// mathematically equal can still round differently -- e.g. left/right counts
+// [1,2]/[6,1] vs [4,3]/[3,0]: T(3)+T(7)-T(6)-2 == T(7)-8-T(3) since
+// T(6) = 2T(3)+6 -- so each node's candidate costs are compared on a grid of
+// 2^-32 * (T(m) + m): such ties become exact and the first candidate in
+// (feature, threshold) order wins everywhere, which is the reference's stated
+// rule (np.argmin over thresholds, np.argmax over features;
+// mpitree/tree/decision_tree.py:88-90, 140). rint is round-half-even on host
+// and device; the multiply / rint / multiply sequence is the same IEEE ops.
+MT_HD double tie_unit(double tm, int64_t m) {
+  return (tm + (double)m) * 2.3283064365386963e-10;  // 2^-32
+}
+
+MT_HD double tie_round(double cost, double inv_unit, double unit) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_rint(cost * inv_unit) * unit;
+#else
+  return rint(cost * inv_unit) * unit;
+#endif
 }
 
 // Squared-error term: -(S^2)/m with S the fixed-point target sum.

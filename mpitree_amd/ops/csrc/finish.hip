@@ -234,6 +234,8 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
     load_c2(h, nb, v, lp);
     best_cost = __builtin_inf();
     best_bin = 0x7fffffff;
+    const double tu = tie_unit(lk((uint32_t)m), (int64_t)m);
+    const double tinv = 1.0 / tu;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       lp += v[k];
@@ -252,6 +254,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           const int64_t qr = (int64_t)r0 * r0 + (int64_t)r1 * r1;
           cost = gini_term(ml, ql) + gini_term(mr, qr);
         }
+        cost = tie_round(cost, tinv, tu);
         if (cost < best_cost) {
           best_cost = cost;
           best_bin = lane * 4 + k;
@@ -475,6 +478,8 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         const uint32_t* h = hist + f * fstride;
         double best_cost = __builtin_inf();
         int best_bin = 0x7fffffff;
+        const double tu = tie_unit(tl((uint64_t)m), (int64_t)m);
+        const double tinv = 1.0 / tu;
         const int b0 = lane * 4;
         uint32_t mL[4] = {0, 0, 0, 0}, ne[4] = {0, 0, 0, 0};
         double sL[4] = {0.0, 0.0, 0.0, 0.0}, sR[4] = {0.0, 0.0, 0.0, 0.0};
@@ -528,6 +533,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
               cost = (tl((uint64_t)ml) - sL[k]) + (tl((uint64_t)mr) - sR[k]);
             else
               cost = gini_term(ml, qL[k]) + gini_term(mr, qR[k]);
+            cost = tie_round(cost, tinv, tu);
             if (cost < best_cost) {
               best_cost = cost;
               best_bin = b;
@@ -792,6 +798,8 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
         }
       }
       const double pterm = crit == kEntropy ? s_tab[mm] - acc : gini_term(mm, sq);
+      const double tu = tie_unit(s_tab[mm], (int64_t)mm);
+      const double tinv = 1.0 / tu;
       const bool inm = (M >> lane) & 1ull;
       double bg = -__builtin_inf(), bc = __builtin_inf();
       int bf = 0x7fffffff;
@@ -839,6 +847,7 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
             }
             cost = gini_term(ml, ql) + gini_term(mr, qr);
           }
+          cost = tie_round(cost, tinv, tu);
         }
         // per-lane running best; features ascend, so strict > keeps the lowest
         const double g = pterm - cost;
@@ -1099,6 +1108,8 @@ __device__ __forceinline__ void tiny_sorted_subtree(
     const int mm = __popcll(M);
     const int mc1 = __popcll(M & cm1);
     const double pterm = H[tiny_h_idx(mm, mc1)];
+    const double tu = tie_unit(xlog2x((uint64_t)mm), (int64_t)mm);
+    const double tinv = 1.0 / tu;
     double bg = -__builtin_inf(), bc = __builtin_inf();
     int bf = 0x7fffffff;
     uint32_t bb = 0xffffffffu;
@@ -1116,7 +1127,7 @@ __device__ __forceinline__ void tiny_sorted_subtree(
     auto cost_of = [&](uint32_t v, int ml, int l1) -> double {
       const int mr = mm - ml, r1 = mc1 - l1;
       const bool ok = (v & 0x80u) && ml >= mslw && mr >= mslw;
-      const double c = hval(ml, l1) + hval(mr, r1);
+      const double c = tie_round(hval(ml, l1) + hval(mr, r1), tinv, tu);
       return ok ? c : __builtin_inf();
     };
     auto take = [&](int f, double cost, uint32_t v) {

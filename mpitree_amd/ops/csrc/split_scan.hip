@@ -63,6 +63,8 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
 
   double best_cost = __builtin_inf();
   int best_bin = 0x7fffffff;
+  const double tu = tie_unit(tlog((uint64_t)m, xtab, xtab_n), (int64_t)m);
+  const double tinv = 1.0 / tu;
   for (int base = 0; base < nb; base += kChunk) {
     const int b0 = base + lane * kBinsPerLane;
     uint32_t mL[kBinsPerLane];
@@ -121,6 +123,7 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
                  (tlog((uint64_t)mr, xtab, xtab_n) - sR[k]);
         else
           cost = gini_term(ml, qL[k]) + gini_term(mr, qR[k]);
+        cost = tie_round(cost, tinv, tu);
         if (cost < best_cost) {
           best_cost = cost;
           best_bin = b;

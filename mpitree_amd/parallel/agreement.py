@@ -27,7 +27,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ..core.binning import MAX_BINS_LIMIT, BinMapper, quantile_edges
+from ..core.binning import BinMapper, quantile_edges
 
 __all__ = ["global_classes", "global_target_scale", "global_bin_mapper"]
 
@@ -73,7 +73,7 @@ def global_target_scale(comm, y_local) -> tuple[float, int]:
 
 def global_bin_mapper(comm, X_local, max_bins) -> BinMapper:
     """One ``BinMapper`` agreed by every rank from their local feature values."""
-    limit = MAX_BINS_LIMIT if max_bins is None else int(max_bins)
+    limit = np.iinfo(np.int64).max if max_bins is None else int(max_bins)
     if torch.is_tensor(X_local):
         F = int(X_local.shape[1])
         cols = [torch.unique(X_local[:, f].double()).cpu().numpy() for f in range(F)]
@@ -94,9 +94,6 @@ def global_bin_mapper(comm, X_local, max_bins) -> BinMapper:
         if all_exact[f] and u.size <= limit:
             edges.append(u)
             exact[f] = True
-        elif max_bins is None:
-            raise ValueError(f"feature {f}: exact thresholds over row-sharded data support at "
-                             f"most {MAX_BINS_LIMIT} unique values per feature")
         else:
             edges.append(quantile_edges(u, limit))
-    return BinMapper(edges=edges, exact=exact, max_bins=limit)
+    return BinMapper(edges=edges, exact=exact, max_bins=max_bins)
