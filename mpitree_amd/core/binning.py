@@ -132,7 +132,7 @@ def fit_bin_mapper(X: np.ndarray, max_bins=256, sample: int | None = None, seed:
         rows = np.sort(rng.choice(n, size=sample, replace=False))
     for f in range(F):
         col = np.asarray(X[:, f], dtype=np.float64)
-        u = np.unique(col)
+        u = np.unique(col) + 0.0  # -0.0 and 0.0 are one value: print it as 0.0
         if u.shape[0] <= limit:
             edges.append(u)
             exact[f] = True

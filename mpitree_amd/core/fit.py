@@ -192,6 +192,35 @@ def _finalize(ta: TreeArrays, mapper: BinMapper, regression: bool, y_exp: int) -
     return ta
 
 
+def _fit_exact_gpu(Xd, yd, classes, C, crit, params, comm, timings, t_bin, t_start, F):
+    """Classification with every unique value a threshold on continuous
+    features: level-wise growth over presorted per-feature lists
+    (``ops/exact_backend.py``). Multi-rank fits run it replicated on each rank
+    (every rank holds all rows and builds the same tree)."""
+    from ..ops.exact_backend import ExactHipBackend
+
+    be = ExactHipBackend()
+    be.setup_exact(Xd, yd.to(torch.int32), C, crit)
+    timings["bin"] = time.perf_counter() - t_bin
+    params.finisher_rows = 0
+    builder = LevelwiseBuilder(be, params, LocalComm())
+    dummy_edges = np.zeros((F, 1))  # thresholds come from the device unique-value table
+    with roctx_range("mpitree.grow"):
+        ta = builder.fit(Xd.shape[0], C, F, edges=dummy_edges)
+    timings.update(builder.timings)
+    stats = dict(builder.stats)
+    stats["thresholds"] = "exact (presorted lists)"
+    if comm.world_size > 1:
+        stats["strategy"] = comm.kind
+        stats["mode"] = "replicated-exact"
+    ta = _finalize(ta, None, False, 0)
+    timings["total"] = time.perf_counter() - t_start
+    # the exact engine's "bins" are value ranks; the unique values stay on the device
+    mapper = BinMapper(edges=[], exact=np.ones(F, bool), max_bins=None)
+    return FitResult(arrays=ta, classes=classes, n_features=F, mapper=mapper, y_scale_exp=0,
+                     engine="hip-exact", timings=timings, stats=stats)
+
+
 def fit_tree(
     X,
     y,
@@ -270,12 +299,25 @@ def fit_tree(
 
                 prep = prepare_with_mapper(Xd, yv, g_mapper, classes, y_exp)
             else:
-                prep = prepare(Xd, y, regression=regression, max_bins=max_bins,
+                # max_bins=None (exact): bin at 256 first -- one code byte, the
+                # histogram engines -- and take the presorted exact engine only
+                # when some feature turns out to have more than 256 values
+                prep = prepare(Xd, y, regression=regression,
+                               max_bins=256 if max_bins is None else max_bins,
                                encode_labels=_encode_labels, encode_targets=_encode_targets,
                                exponent=fixed_point_exponent)
         mapper, codes_rm, codes_fm, nb = prep.mapper, prep.codes_rm, prep.codes_fm, prep.nbins
         yd, classes, y_exp, root = prep.y, prep.classes, prep.y_exp, prep.root
         C = 0 if regression else len(classes)
+        from ..ops.exact_backend import exact_supported, needs_exact
+
+        if max_bins is None and g_mapper is None and needs_exact(mapper):
+            if exact_supported(n, C, regression) and checkpoint is None:
+                return _fit_exact_gpu(Xd, yd, classes, C, crit, params, comm, timings, t0,
+                                      t_start, F)
+            logger.warning("exact thresholds on > 256-value features are not available on "
+                           "the GPU for this fit (regression, >= 2^24 rows, > 256 classes or "
+                           "a level checkpoint): using 256 quantile bins per feature")
         lo, hi = comm.local_rows(n)
         if (lo, hi) != (0, n):  # data-parallel shard of a replicated input
             codes_rm = codes_rm[lo:hi].contiguous()

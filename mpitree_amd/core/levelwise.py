@@ -350,8 +350,9 @@ class LevelwiseBuilder:
             new_pos[keep_idx] = np.arange(keep_idx.size)
             src = np.full(2 * S, -1, np.int64)
             sib = np.full(2 * S, -1, np.int64)
-            src[2 * both + big[both]] = split[both]
-            sib[2 * both + big[both]] = new_pos[2 * both + 1 - big[both]]
+            if getattr(be, "derives", True):  # else every node is built from its rows
+                src[2 * both + big[both]] = split[both]
+                sib[2 * both + big[both]] = new_pos[2 * both + 1 - big[both]]
             fr = dict(
                 id=cids[keep_idx],
                 pos=cpos[keep_idx],

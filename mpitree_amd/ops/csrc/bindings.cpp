@@ -48,6 +48,13 @@ void launch_finish(hipStream_t, const void*, int64_t, const void*, int, int64_t,
 int finish_lds_bytes(int F, int B, int C);
 int asm_tiles(int64_t P);
 void launch_grow_plan(hipStream_t, const PlanArgs&);
+void ex_scan_level(hipStream_t, const uint64_t*, int64_t, const int64_t*, int, const int64_t*,
+                   const int64_t*, int, int, int, int, int64_t, const double*, int, int32_t*,
+                   int32_t*, int32_t*, unsigned long long*, int64_t*);
+void ex_partition_level(hipStream_t, const uint64_t*, uint64_t*, int64_t, const int64_t*, int,
+                        const int64_t*, const int64_t*, int, int, uint8_t*, int32_t*, int32_t*,
+                        int32_t*);
+int ex_chunk();
 void launch_fp_combine(hipStream_t, const int64_t*, int, int, int, const int32_t*, int64_t*);
 void launch_grow_dp_fixup(hipStream_t, const PlanArgs&);
 void launch_grow_init(hipStream_t, const LevelLists&, int64_t, int64_t, int64_t, int, int,
@@ -259,6 +266,24 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("job_count"), py::arg("C"), py::arg("max_depth"), py::arg("n_cu"), py::arg("mss"),
      py::arg("msl"), py::arg("fr"), py::arg("host_ctl"), py::arg("host_tag"), py::arg("dp") = 0,
      py::arg("fixup") = false);
+  m.def("ex_chunk", &mt::ex_chunk);
+  m.def("ex_scan_level", [](uintptr_t s, uintptr_t E, int64_t n, uintptr_t items, int NI,
+                            uintptr_t ifirst, uintptr_t seg, int K, int F, int C, int crit,
+                            int64_t msl, uintptr_t xtab, int xtab_n, uintptr_t tot,
+                            uintptr_t carry, uintptr_t slot_tot, uintptr_t best, uintptr_t rec) {
+    mt::ex_scan_level(S(s), P<uint64_t>(E), n, P<int64_t>(items), NI, P<int64_t>(ifirst),
+                      P<int64_t>(seg), K, F, C, crit, msl, P<double>(xtab), xtab_n,
+                      P<int32_t>(tot), P<int32_t>(carry), P<int32_t>(slot_tot),
+                      P<unsigned long long>(best), P<int64_t>(rec));
+  });
+  m.def("ex_partition_level", [](uintptr_t s, uintptr_t E, uintptr_t D, int64_t n,
+                                 uintptr_t pitems, int NP, uintptr_t pfirst, uintptr_t split,
+                                 int Sn, int F, uintptr_t flag, uintptr_t lc, uintptr_t lcar,
+                                 uintptr_t nl) {
+    mt::ex_partition_level(S(s), P<uint64_t>(E), P<uint64_t>(D), n, P<int64_t>(pitems), NP,
+                           P<int64_t>(pfirst), P<int64_t>(split), Sn, F, P<uint8_t>(flag),
+                           P<int32_t>(lc), P<int32_t>(lcar), P<int32_t>(nl));
+  });
   m.def("fp_combine", [](uintptr_t s, uintptr_t g, int nranks, int KB, int R, uintptr_t dcount,
                          uintptr_t rec) {
     mt::launch_fp_combine(S(s), P<int64_t>(g), nranks, KB, R, P<int32_t>(dcount),

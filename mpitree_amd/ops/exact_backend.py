@@ -1,0 +1,183 @@
+"""Exact-threshold GPU backend for continuous features (``ops/csrc/exact.hip``).
+
+The histogram engines are exact only while a feature has at most 256 unique
+values. The reference's search (``mpitree/tree/decision_tree.py:73-90``) takes
+*every* unique value as a candidate, and with ``max_bins=None`` (the default)
+so does this framework: when some feature has more than 256 values the GPU
+fit runs this backend under the level-wise grower
+(:class:`~mpitree_amd.core.levelwise.LevelwiseBuilder`).
+
+Layout: every feature keeps its rows sorted by value, grouped by frontier
+node (``E[f][p] = rank << 32 | label << 24 | row``, uint64). A level scans
+the frontier's segments -- class prefix counts at every position, the shared
+integer-form cost at every value boundary -- and stably partitions the split
+nodes' segments of every feature into the other list buffer. Rows that reach
+a leaf are never touched again. Thresholds are the sorted unique values
+(``uniq[f][rank]``), i.e. data values, exactly like ``np.unique``.
+
+Limits: classification, fewer than 2^24 rows, at most 256 classes (the label
+lives in 8 bits of each entry).
+"""
+
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..core.criterion import Criterion
+from . import hip_backend as hb
+from .hip_backend import HipBackend, XTAB_N, unpack_records
+
+__all__ = ["ExactHipBackend", "exact_supported", "needs_exact"]
+
+MAX_ROWS = 1 << 24
+MAX_CLASSES = 256
+
+
+def exact_supported(n: int, C: int, regression: bool) -> bool:
+    return (not regression) and n < MAX_ROWS and 1 <= C <= MAX_CLASSES
+
+
+def needs_exact(mapper) -> bool:
+    """A binned fit cannot be exact: some feature kept quantile edges."""
+    ex = np.asarray(getattr(mapper, "exact", []), dtype=bool)
+    return bool(ex.size) and not bool(ex.all())
+
+
+class _Frontier:
+    """What the grower's ``alloc_hist`` / ``build_hist`` hand to ``scan``: the
+    list segments of the level's frontier slots (no histogram is stored)."""
+
+    def __init__(self, K: int):
+        self.starts = np.zeros(K, np.int64)
+        self.counts = np.zeros(K, np.int64)
+
+
+class ExactHipBackend(HipBackend):
+    """Level-wise backend over presorted feature lists (no histograms)."""
+
+    name = "hip-exact"
+    derives = False  # every frontier node is scanned from its own segment
+
+    def setup_exact(self, X: torch.Tensor, y_codes: torch.Tensor, n_classes: int,
+                    criterion: Criterion):
+        n, F = X.shape
+        if not exact_supported(n, n_classes, criterion == Criterion.SQUARED_ERROR):
+            raise ValueError("exact GPU engine: classification with < 2^24 rows and "
+                             "<= 256 classes")
+        dev = self.device
+        self.n, self.F, self.C = int(n), int(F), int(n_classes)
+        self.crit = criterion
+        self.reg = False
+        self.chunk = int(self.hip.ex_chunk())
+        # per feature: values sorted (stable), dense ranks, unique-value table
+        xt = X.t().contiguous()
+        vals, order = torch.sort(xt, dim=1, stable=True)
+        del xt
+        new = torch.ones_like(vals, dtype=torch.bool)
+        new[:, 1:] = vals[:, 1:] != vals[:, :-1]
+        rank = torch.cumsum(new, 1, dtype=torch.int64) - 1
+        nb = rank[:, -1] + 1
+        self.B = int(nb.max())
+        uniq = torch.full((F, self.B), float("inf"), dtype=torch.float64, device=dev)
+        uniq.scatter_(1, rank, vals.double())
+        self.uniq = uniq + 0.0  # -0.0 -> +0.0, as np.unique prints it
+        self.nbins = nb.to(torch.int32)
+        lab = y_codes.to(torch.int64)[order]
+        e = (rank << 32) | (lab << 24) | order.to(torch.int64)
+        del vals, order, rank, new, lab
+        self.E = [e.contiguous(), torch.empty_like(e)]
+        self.cur = 0
+        self.flag = torch.empty(n, dtype=torch.uint8, device=dev)
+        self.xtab = hb.xlog2x_table(dev)
+        self.xtabf = hb.xlog2x_table_f32(dev)
+        self.y = y_codes
+
+    # the level-wise grower's histogram hooks: only the segments matter here
+    def alloc_hist(self, slots: int, F_h: int | None = None):
+        return _Frontier(max(int(slots), 1))
+
+    def build_hist(self, hist, slots, starts, counts, f_lo=0, f_hi=None):
+        hist.starts[np.asarray(slots)] = starts
+        hist.counts[np.asarray(slots)] = counts
+
+    def derive_hist(self, hist, prev_hist, slots, parent_slots, sibling_slots):
+        raise RuntimeError("exact backend builds every node from its segment")
+
+    def finisher_supported(self) -> bool:
+        return False
+
+    def _chunks(self, starts, counts):
+        """Chunk items {id, segment start, chunk start, chunk count} + first item per id."""
+        ch = self.chunk
+        k = np.maximum(1, -(-counts // ch))
+        ids = np.repeat(np.arange(counts.size), k)
+        first = np.concatenate([[0], np.cumsum(k)])
+        off = (np.arange(ids.size) - first[:-1][ids]) * ch
+        items = np.stack([ids, starts[ids], starts[ids] + off,
+                          np.maximum(0, np.minimum(ch, counts[ids] - off))], 1)
+        return items, first
+
+    def scan(self, hist, slots, min_samples_leaf=1, f_lo=0, f_hi=None):
+        slots = np.asarray(slots, np.int64)
+        K = slots.size
+        starts, counts = hist.starts[slots], hist.counts[slots]
+        items, first = self._chunks(starts, counts)
+        NI = items.shape[0]
+        F, C = self.F, self.C
+        d_items, d_first, d_seg = self.up(items, first, np.stack([starts, counts], 1))
+        dev = self.device
+        tot = torch.empty((NI, F, C), dtype=torch.int32, device=dev)
+        carry = torch.empty_like(tot)
+        slot_tot = torch.empty((K, C), dtype=torch.int32, device=dev)
+        best = torch.empty((K, F), dtype=torch.int64, device=dev)
+        rec = torch.empty((K, 5 + 2 * C), dtype=torch.int64, device=dev)
+        self.hip.ex_scan_level(hb._stream(), self.E[self.cur].data_ptr(), self.n,
+                               d_items.data_ptr(), NI, d_first.data_ptr(), d_seg.data_ptr(), K,
+                               F, C, int(self.crit), int(max(1, min_samples_leaf)),
+                               self.xtab.data_ptr(), XTAB_N, tot.data_ptr(), carry.data_ptr(),
+                               slot_tot.data_ptr(), best.data_ptr(), rec.data_ptr())
+        self.last_rec = rec
+        return unpack_records(rec.cpu().numpy(), C, False)
+
+    def partition(self, starts, counts, features, bins, need_counts=True):
+        S = len(starts)
+        if S == 0:
+            return np.zeros(0, dtype=np.int64)
+        starts = np.asarray(starts, np.int64)
+        counts = np.asarray(counts, np.int64)
+        split = np.stack([starts, counts, np.asarray(features, np.int64),
+                          np.asarray(bins, np.int64)], 1)
+        pitems, pfirst = self._chunks(starts, counts)
+        NP = pitems.shape[0]
+        d_items, d_first, d_split = self.up(pitems, pfirst, split)
+        dev = self.device
+        lc = torch.empty((NP, self.F), dtype=torch.int32, device=dev)
+        lcar = torch.empty_like(lc)
+        nl = torch.empty(S, dtype=torch.int32, device=dev)
+        src, dst = self.E[self.cur], self.E[1 - self.cur]
+        self.hip.ex_partition_level(hb._stream(), src.data_ptr(), dst.data_ptr(), self.n,
+                                    d_items.data_ptr(), NP, d_first.data_ptr(),
+                                    d_split.data_ptr(), S, self.F, self.flag.data_ptr(),
+                                    lc.data_ptr(), lcar.data_ptr(), nl.data_ptr())
+        self.cur = 1 - self.cur  # every next-level node lives in the list just written
+        self._keep_p = (d_items, d_first, d_split, lc, lcar)
+        if not need_counts:
+            self._keep_nl = nl
+            return None
+        return nl.cpu().numpy().astype(np.int64)
+
+    def segment_stats(self, starts, counts):
+        e0 = self.E[self.cur][0]
+        out = np.zeros((len(starts), self.C), dtype=np.int64)
+        for j, (s, c) in enumerate(zip(np.asarray(starts), np.asarray(counts))):
+            lab = ((e0[int(s): int(s) + int(c)] >> 24) & 0xFF)
+            out[j] = torch.bincount(lab, minlength=self.C).cpu().numpy()[: self.C]
+        return out
+
+    def get_rows(self):  # pragma: no cover - level checkpoints use the binned engines
+        raise RuntimeError("level checkpoints are not supported by the exact engine")
+
+    def assemble_positions(self, edges, crit: int, y_exp: int = 0, d_edges=None) -> dict:
+        # thresholds straight from the device unique-value table (rank -> value)
+        return super().assemble_positions(None, crit, y_exp, d_edges=self.uniq)

@@ -310,3 +310,35 @@ def test_gpu_regression_device_loop_matches_host(monkeypatch, seed, max_depth):
     assert np.array_equal(r1.arrays.value, r2.arrays.value)
     r3 = fit_tree(X, y, **{**kw, "device": "cpu"})
     assert r1.arrays.equal(r3.arrays)
+
+
+@pytest.mark.parametrize("crit", ["entropy", "gini"])
+@pytest.mark.parametrize("shape", [(3000, 3, 2, None), (20000, 6, 3, None), (5000, 4, 5, 6)])
+def test_gpu_exact_engine_matches_host(crit, shape):
+    """Continuous features (> 256 unique values) with the exact default: the
+    presorted-list engine (exact.hip) builds the host builder's tree bit for bit."""
+    n, F, C, md = shape
+    rng = np.random.default_rng(n + F)
+    X = np.round(rng.normal(size=(n, F)), 4).astype(np.float32)
+    X[:, 0] = np.round(X[:, 0], 1)  # many ties on one feature
+    s = X[:, 0] + 0.7 * X[:, 1] + rng.normal(scale=0.8, size=n)
+    y = np.digitize(s, np.quantile(s, np.linspace(0, 1, C + 1)[1:-1]))
+    g = DecisionTreeClassifier(criterion=crit, max_depth=md, device="cuda").fit(X, y)
+    assert g.fit_stats_["engine"] == "hip-exact"
+    h = DecisionTreeClassifier(criterion=crit, max_depth=md, device="cpu").fit(X, y)
+    assert g.tree_arrays_.equal(h.tree_arrays_)
+    np.testing.assert_array_equal(g.tree_arrays_.threshold, h.tree_arrays_.threshold)
+    assert g.export_text(precision=17) == h.export_text(precision=17)
+    np.testing.assert_array_equal(g.predict(X), h.predict(X))
+
+
+def test_gpu_exact_engine_device_tensors_and_quantile_optin():
+    rng = np.random.default_rng(7)
+    X = torch.from_numpy(rng.normal(size=(50000, 8)).astype(np.float32)).cuda()
+    y = (X[:, 0] + X[:, 1] * X[:, 2] > 0).long()
+    g = DecisionTreeClassifier(max_depth=10, device="cuda").fit(X, y)
+    assert g.fit_stats_["engine"] == "hip-exact"
+    acc = float((g.predict(X) == y).float().mean())
+    assert acc > 0.9
+    q = DecisionTreeClassifier(max_depth=10, max_bins=256, device="cuda").fit(X, y)
+    assert q.fit_stats_["engine"].startswith("hip-") and q.fit_stats_["engine"] != "hip-exact"
