@@ -10,6 +10,9 @@ One JSON line per config (wall-clock per fit, samples/s, tree size):
   sweep_gpu   the same workload fitted on one MI355X
   100k        100k x 32 synthetic classification, max_depth=12, 1 GPU
   1m          1M x 64 synthetic classification (flagship; bench.py), 1 GPU
+  1m_exact    1M x 64 continuous (randn) features: every unique value a threshold
+              (the reference's search; the presorted-list exact engine), 1 GPU
+  100k_exact  100k x 32 continuous, max_depth=12, exact engine, 1 GPU
   1m_reg      1M x 64 regression tree (squared error), 1 GPU
   10m         10M x 128 synthetic classification, 1 GPU (the 8-GPU
               data-parallel run is bench.py under torchrun)
@@ -114,7 +117,7 @@ def run_sweep_gpu(reps):
     return out
 
 
-def _gpu_fit(n, F, reps, md=None, regression=False, classes=2, seed=0):
+def _gpu_fit(n, F, reps, md=None, regression=False, classes=2, seed=0, levels=256):
     import torch
 
     from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
@@ -124,7 +127,7 @@ def _gpu_fit(n, F, reps, md=None, regression=False, classes=2, seed=0):
         X, y = make_regression(n, F, seed=seed)
         est = DecisionTreeRegressor(max_depth=md, device="cuda")
     else:
-        X, y = make_classification(n, F, n_classes=classes, seed=seed)
+        X, y = make_classification(n, F, n_classes=classes, seed=seed, levels=levels)
         est = DecisionTreeClassifier(max_depth=md, device="cuda")
     med, best = _time(lambda: est.fit(X, y), reps, sync=torch.cuda.synchronize)
     st = est.fit_stats_
@@ -152,6 +155,14 @@ def main(argv=None):
         elif name == "1m":
             rows = [{"config": "1M x 64 classification, full depth, 1 GPU",
                      **_gpu_fit(1_000_000, 64, a.reps)}]
+        elif name == "1m_exact":
+            rows = [{"config": "1M x 64 continuous (randn) classification, exact thresholds, "
+                               "full depth, 1 GPU",
+                     **_gpu_fit(1_000_000, 64, max(2, a.reps // 2), levels=None)}]
+        elif name == "100k_exact":
+            rows = [{"config": "100k x 32 continuous (randn) classification, exact thresholds, "
+                               "max_depth=12, 1 GPU",
+                     **_gpu_fit(100_000, 32, a.reps, md=12, levels=None)}]
         elif name == "1m_reg":
             rows = [{"config": "1M x 64 regression (squared_error), full depth, 1 GPU",
                      **_gpu_fit(1_000_000, 64, a.reps, regression=True)}]

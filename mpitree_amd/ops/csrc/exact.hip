@@ -211,6 +211,138 @@ __global__ __launch_bounds__(kExThreads) void ex_scan_kernel(
   }
 }
 
+// Two classes (the common case): one block scan of the class-1 prefix gives
+// every position's four side counts. Entropy costs are first scored in fp32
+// (hardware log2) -- |fp32 - exact| <= 2^-17.5 T(m) over the six terms and
+// their sums -- and only positions within 2^-16 (T(m) + m) of the chunk's fp32
+// minimum (twice that error plus one tie-rounding unit) are re-scored exactly
+// in fp64 with the shared xlog2x: the chunk's exact (tie-rounded) best is among
+// them. Gini is exact integer arithmetic plus two divisions: scored directly.
+__device__ __forceinline__ float ex_t32(uint32_t x) {
+  const float xf = (float)x;
+  return x <= 1u ? 0.0f : xf * __log2f(xf);
+}
+
+template <int CRIT>
+__global__ __launch_bounds__(kExThreads) void ex_scan_c2_kernel(
+    const uint64_t* __restrict__ E, int64_t n, const int64_t* __restrict__ items,
+    const int64_t* __restrict__ seg, const int32_t* __restrict__ carry,
+    const int32_t* __restrict__ slot_tot, int F, int64_t msl,
+    unsigned long long* __restrict__ best) {
+  __shared__ uint32_t s_w[kExThreads / kWave];
+  __shared__ uint32_t s_first[kExThreads];
+  __shared__ unsigned long long s_min[kExThreads / kWave];
+  __shared__ float s_fmin[kExThreads / kWave];
+  const int64_t it = blockIdx.x;
+  const int f = blockIdx.y;
+  const int64_t slot = items[it * 4 + 0], sstart = items[it * 4 + 1];
+  const int64_t c0 = items[it * 4 + 2], cn = items[it * 4 + 3];
+  const int64_t m = seg[slot * 2 + 1];
+  const uint64_t* L = E + (int64_t)f * n;
+  const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const int64_t p0 = c0 + (int64_t)tid * kExPer;
+  uint64_t e[kExPer];
+  uint32_t run = 0;
+  uint32_t pre[kExPer];
+#pragma unroll
+  for (int k = 0; k < kExPer; ++k) {
+    const int64_t p = p0 + k;
+    e[k] = (p - c0) < cn ? L[p] : ~0ull;
+    run += (e[k] != ~0ull && ex_lab(e[k]) == 1) ? 1u : 0u;
+    pre[k] = run;
+  }
+  s_first[tid] = ex_rank(e[0]);
+  uint32_t total;
+  const uint32_t excl = ex_block_excl(run, s_w, total);  // (its barriers order s_first too)
+  const int64_t pn = p0 + kExPer;
+  uint32_t next_rank = 0xFFFFFFFFu;
+  if (tid + 1 < kExThreads && (pn - c0) < cn)
+    next_rank = s_first[tid + 1];
+  else if ((pn - sstart) < m)
+    next_rank = ex_rank(L[pn]);
+  const int32_t* car = carry + (it * F + f) * 2;
+  const uint32_t base1 = (uint32_t)car[1] + excl;
+  const int64_t t0 = slot_tot[slot * 2 + 0], t1 = slot_tot[slot * 2 + 1];
+  bool valid[kExPer];
+  int64_t l1[kExPer];
+#pragma unroll
+  for (int k = 0; k < kExPer; ++k) {
+    const int64_t pos = p0 + k - sstart;
+    const int64_t ml = pos + 1, mr = m - ml;
+    const uint32_t nr = k + 1 < kExPer ? ex_rank(e[k + 1]) : next_rank;
+    valid[k] = (p0 + k - c0) < cn && mr > 0 && nr != ex_rank(e[k]) && ml >= msl && mr >= msl;
+    l1[k] = (int64_t)(base1 + pre[k]);
+  }
+  const double tm = xlog2x((uint64_t)m);
+  const double tu = tie_unit(tm, m);
+  const double tinv = 1.0 / tu;
+  auto exact_key = [&](int k) -> unsigned long long {
+    const int64_t pos = p0 + k - sstart;
+    const int64_t ml = pos + 1, mr = m - ml;
+    const int64_t L1 = l1[k], L0 = ml - L1, R1 = t1 - L1, R0 = t0 - L0;
+    double cost;
+    if (CRIT == kEntropy) {
+      const double sl = xlog2x((uint64_t)L0) + xlog2x((uint64_t)L1);
+      const double sr = xlog2x((uint64_t)R0) + xlog2x((uint64_t)R1);
+      cost = (xlog2x((uint64_t)ml) - sl) + (xlog2x((uint64_t)mr) - sr);
+    } else {
+      cost = gini_term(ml, L0 * L0 + L1 * L1) + gini_term(mr, R0 * R0 + R1 * R1);
+    }
+    double q = __builtin_rint(cost * tinv);
+    q = q < 0.0 ? 0.0 : q;
+    return ((unsigned long long)q << 24) | (unsigned long long)pos;
+  };
+  unsigned long long mine = ~0ull;
+  if (CRIT == kEntropy) {
+    float c32[kExPer];
+    float lmin = __builtin_inff();
+#pragma unroll
+    for (int k = 0; k < kExPer; ++k) {
+      const uint32_t ml = (uint32_t)(p0 + k - sstart + 1), mr = (uint32_t)(m - ml);
+      const uint32_t L1 = (uint32_t)l1[k], L0 = ml - L1;
+      const uint32_t R1 = (uint32_t)t1 - L1, R0 = (uint32_t)t0 - L0;
+      const float c = (ex_t32(ml) - (ex_t32(L0) + ex_t32(L1))) +
+                      (ex_t32(mr) - (ex_t32(R0) + ex_t32(R1)));
+      c32[k] = valid[k] ? c : __builtin_inff();
+      lmin = fminf(lmin, c32[k]);
+    }
+    lmin = wave_min_f32_dpp(lmin);
+    if (lane == 0) s_fmin[wave] = lmin;
+    __syncthreads();
+    float bmin = s_fmin[0];
+#pragma unroll
+    for (int w = 1; w < kExThreads / kWave; ++w) bmin = fminf(bmin, s_fmin[w]);
+    const float thr = bmin + (float)((tm + (double)m) * 0x1p-16);
+#pragma unroll
+    for (int k = 0; k < kExPer; ++k) {
+      if (valid[k] && c32[k] <= thr) {  // (thr is +inf when the chunk has no candidate)
+        const unsigned long long key = exact_key(k);
+        mine = key < mine ? key : mine;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kExPer; ++k) {
+      if (valid[k]) {
+        const unsigned long long key = exact_key(k);
+        mine = key < mine ? key : mine;
+      }
+    }
+  }
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    const unsigned long long o = __shfl_xor(mine, d, kWave);
+    mine = o < mine ? o : mine;
+  }
+  if (lane == 0) s_min[wave] = mine;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long b = s_min[0];
+    for (int w = 1; w < kExThreads / kWave; ++w) b = s_min[w] < b ? s_min[w] : b;
+    if (b != ~0ull) atomicMin(best + slot * F + f, b);
+  }
+}
+
 // Per slot: best feature and the winning split's record
 // rec: int64 [K][5 + 2C] = {gain bits, feature, threshold rank, n_left, m, left[C], total[C]}.
 __global__ __launch_bounds__(kExThreads) void ex_select_kernel(
@@ -411,8 +543,15 @@ void ex_scan_level(hipStream_t stream, const uint64_t* E, int64_t n, const int64
                      dim3(kExThreads), 0, stream, tot, ifirst, K, F, C, carry, slot_tot);
   MT_HIP_CHECK(hipGetLastError());
   MT_HIP_CHECK(hipMemsetAsync(best, 0xFF, (size_t)K * F * sizeof(unsigned long long), stream));
-  hipLaunchKernelGGL(ex_scan_kernel, dim3(NI, F), dim3(kExThreads), 0, stream, E, n, items, seg,
-                     carry, slot_tot, F, C, crit, msl, xtab, xtab_n, best);
+  if (C == 2 && crit == kEntropy)
+    hipLaunchKernelGGL(ex_scan_c2_kernel<kEntropy>, dim3(NI, F), dim3(kExThreads), 0, stream, E,
+                       n, items, seg, carry, slot_tot, F, msl, best);
+  else if (C == 2)
+    hipLaunchKernelGGL(ex_scan_c2_kernel<kGini>, dim3(NI, F), dim3(kExThreads), 0, stream, E, n,
+                       items, seg, carry, slot_tot, F, msl, best);
+  else
+    hipLaunchKernelGGL(ex_scan_kernel, dim3(NI, F), dim3(kExThreads), 0, stream, E, n, items,
+                       seg, carry, slot_tot, F, C, crit, msl, xtab, xtab_n, best);
   MT_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(ex_select_kernel, dim3(K), dim3(kExThreads), 0, stream, E, n, seg, ifirst,
                      carry, slot_tot, best, F, C, crit, xtab, xtab_n, rec);

@@ -1,8 +1,8 @@
 """Deterministic synthetic tabular data generated directly in device memory.
 
 Features are quantized to ``levels`` distinct values per column (default
-256), so every feature is binned in exact mode and GPU fits are exactly the
-reference's split semantics. Labels come from a random linear score plus a
+256; ``levels=None`` gives continuous N(0, 1) features, for the exact
+presorted-list engine). Labels come from a random linear score plus a
 sparse interaction term and Gaussian noise, which makes trees grow deep and
 wide like on real tabular data.
 """
@@ -15,6 +15,8 @@ __all__ = ["make_classification", "make_regression"]
 
 
 def _features(n, F, levels, gen, device, dtype):
+    if levels is None:  # continuous: every value distinct (exact-threshold engine)
+        return torch.randn((n, F), generator=gen, device=device, dtype=dtype)
     X = torch.randint(0, levels, (n, F), generator=gen, device=device, dtype=torch.int32)
     return X.to(dtype)
 
@@ -22,7 +24,7 @@ def _features(n, F, levels, gen, device, dtype):
 def _score(X, gen, device, noise, levels):
     n, F = X.shape
     w = torch.randn(F, generator=gen, device=device)
-    Xc = X.float() / max(levels - 1, 1) - 0.5
+    Xc = X.float() * 0.25 if levels is None else X.float() / max(levels - 1, 1) - 0.5
     s = Xc @ w
     k = min(F, 8)
     s = s + 2.0 * (Xc[:, :k:2] * Xc[:, 1:k:2]).sum(1) if k >= 2 else s
