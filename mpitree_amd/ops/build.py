@@ -33,7 +33,7 @@ HIP_SOURCES = ["hist.hip", "split_scan.hip", "partition.hip", "predict.hip", "mi
                "finish.hip", "finish_reg.hip", "assemble.hip", "binning.hip", "grow.hip",
                "exact.hip", "bindings.cpp"]
 CPU_SOURCES = ["cpu_builder.cpp"]
-HEADERS = ["common.h", "criterion.h", "cpu_builder_core.h", "grow.h"]
+HEADERS = ["common.h", "criterion.h", "cpu_builder_core.h", "grow.h", "tiny_sort.h"]
 
 
 def _pybind_includes() -> list[str]:

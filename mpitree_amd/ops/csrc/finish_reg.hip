@@ -22,6 +22,7 @@
 
 #include "common.h"
 #include "criterion.h"
+#include "tiny_sort.h"
 
 namespace mt {
 
@@ -356,29 +357,84 @@ __global__ __launch_bounds__(kRegThreads, 2) void finish_reg_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Tiny regression subtrees (<= 64 rows): presorted lane orders per feature.
-// LDS per wave: codes [64][cw] words, order [F][64] bytes, targets [64] int64.
+// Tiny regression subtrees (<= 64 rows): one wavefront per subtree, one row
+// per lane, presorted per-feature lane orders (the bitonic network of
+// finish_tiny_sorted_kernel): srt[f][k] = {code : 8, run end : 1, -, lane : 6}
+// for sorted position k, computed once per subtree (a child's rows are a
+// subset of its parent's, so the order never changes).
+//
+// Per node, the split cost -(S_L^2 / m_L + S_R^2 / m_R) needs two fp64
+// divisions and an int64 prefix per candidate; the exact form is the shared
+// mse_term and must stay bit-identical to the host builders. So every feature
+// is first scored in fp32 (one packed count scan, one fp32 target-sum scan, two
+// v_rcp_f32 per position), and only features whose fp32 minimum lies within
+// the fp32 error bound of the node's fp32 minimum are re-scored exactly (int64
+// DPP prefix, mse_term). Bound, with A = sum |y| over the node: each converted
+// target carries 2^-24 relative error, a 64-term fp32 prefix <= 65 * 2^-24 A,
+// so S_L, S_R are off by <= 2^-17.9 A and each term S^2/m by <= 2^-16.9 A^2
+// (+ 2^-22 A^2 of rounding in the square, reciprocal and product): the cost by
+// <= 2^-15.8 A^2. A feature can hold the exact optimum (or a candidate whose
+// gain rounds equal to it) only if its fp32 minimum is within twice that of
+// the node's; the threshold uses 2^-13 A^2. Every candidate of a re-scored
+// feature is compared exactly, with the (gain, feature, cost, code) order of
+// the block finisher, so the tree is the host builder's bit for bit.
+constexpr int kRegTinyStack = 16;
+constexpr int kRegSmallNode = 16;  // nodes of 3..16 rows: one lane per feature
+
+__host__ __device__ inline int reg_tiny_wave_bytes(int F) {
+  // srt [F][64] u16 | targets [64] int64 | per-feature fp32 minima [F] | flags [64]
+  return F * kWave * 2 + kWave * 8 + ((F * 4 + 15) & ~15) + kWave;
+}
+
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ int64_t dpp_i64_zero(int64_t v) {
+  const uint64_t x = (uint64_t)v;
+  const uint32_t lo = dpp_u32<CTRL, ROW_MASK>(0u, (uint32_t)x);
+  const uint32_t hi = dpp_u32<CTRL, ROW_MASK>(0u, (uint32_t)(x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Inclusive wave64 prefix sums in DPP steps (int64 exact, fp32 approximate).
+__device__ __forceinline__ int64_t wave_incl_scan_i64_dpp(int64_t v) {
+  v += dpp_i64_zero<kDppRowShr + 1>(v);
+  v += dpp_i64_zero<kDppRowShr + 2>(v);
+  v += dpp_i64_zero<kDppRowShr + 4>(v);
+  v += dpp_i64_zero<kDppRowShr + 8>(v);
+  v += dpp_i64_zero<kDppRowBcast15, 0xa>(v);
+  v += dpp_i64_zero<kDppRowBcast31, 0xc>(v);
+  return v;
+}
+
+__device__ __forceinline__ float wave_incl_scan_f32_dpp(float v) {
+  auto add = [](float x, uint32_t o) { return x + __uint_as_float(o); };
+  v = add(v, dpp_u32<kDppRowShr + 1>(0u, __float_as_uint(v)));
+  v = add(v, dpp_u32<kDppRowShr + 2>(0u, __float_as_uint(v)));
+  v = add(v, dpp_u32<kDppRowShr + 4>(0u, __float_as_uint(v)));
+  v = add(v, dpp_u32<kDppRowShr + 8>(0u, __float_as_uint(v)));
+  v = add(v, dpp_u32<kDppRowBcast15, 0xa>(0u, __float_as_uint(v)));
+  v = add(v, dpp_u32<kDppRowBcast31, 0xc>(0u, __float_as_uint(v)));
+  return v;
+}
+
 __global__ __launch_bounds__(256) void finish_tiny_reg_kernel(
     const uint32_t* __restrict__ codes_rm, int64_t row_words, const uint32_t* __restrict__ buf0,
     const uint32_t* __restrict__ buf1, const int64_t* __restrict__ y,
     const int64_t* __restrict__ tiny, const int32_t* __restrict__ tiny_count,
     int32_t* __restrict__ tiny_counter, int F, int max_depth, int64_t mss, int64_t msl,
-    int32_t* __restrict__ node_i32, int64_t* __restrict__ node_st, int cw) {
-  extern __shared__ __align__(16) uint32_t dyn[];
-  __shared__ unsigned long long s_mask[kRegTinyWaves][16];
-  __shared__ int32_t s_dep[kRegTinyWaves][16], s_slot[kRegTinyWaves][16];
+    int32_t* __restrict__ node_i32, int64_t* __restrict__ node_st) {
+  extern __shared__ __align__(16) uint8_t dyn_reg[];
+  __shared__ unsigned long long s_mask[kRegTinyWaves][kRegTinyStack];
+  __shared__ int32_t s_dep[kRegTinyWaves][kRegTinyStack], s_slot[kRegTinyWaves][kRegTinyStack];
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
-  const int per_wave_words = kWave * cw + (F * kWave + 3) / 4 + 2 * kWave;
-  uint32_t* wbase = dyn + wave * per_wave_words;
-  uint32_t* my_codes = wbase + lane * cw;
-  const uint8_t* codes_b = reinterpret_cast<const uint8_t*>(wbase);
-  uint8_t* order = reinterpret_cast<uint8_t*>(wbase + kWave * cw);
-  long long* s_y = reinterpret_cast<long long*>(wbase + kWave * cw + (F * kWave + 3) / 4);
-  const uint8_t* my_bytes = reinterpret_cast<const uint8_t*>(my_codes);
+  uint8_t* wb = dyn_reg + (size_t)wave * reg_tiny_wave_bytes(F);
+  uint16_t* srt = reinterpret_cast<uint16_t*>(wb);
+  long long* s_y = reinterpret_cast<long long*>(wb + F * kWave * 2);
+  float* s_fmin = reinterpret_cast<float*>(wb + F * kWave * 2 + kWave * 8);
+  uint8_t* flag = wb + F * kWave * 2 + kWave * 8 + ((F * 4 + 15) & ~15);
   const int K = *tiny_count;
-  const int nw = (int)min<int64_t>(row_words, (int64_t)cw);
-  const unsigned long long below = (1ull << lane) - 1ull;
+  const int nwords = (F + 3) >> 2;
+  const int mslw = (int)(msl < 65 ? msl : 65);
   for (;;) {
     int k = 0;
     if (lane == 0) k = atomicAdd(tiny_counter, 1);
@@ -391,32 +447,40 @@ __global__ __launch_bounds__(256) void finish_tiny_reg_kernel(
     const uint32_t* src = rec[3] ? buf1 : buf0;
     const int64_t root_slot = rec[4];
     const bool act = lane < m;
+    uint32_t row = 0;
     long long yv = 0;
     if (act) {
-      const uint32_t row = src[start + lane];
+      row = src[start + lane];
       yv = y[row];
-      for (int i = 0; i < nw; ++i) my_codes[i] = codes_rm[(int64_t)row * row_words + i];
     }
+    const float yf = (float)yv;
     s_y[lane] = yv;
-    const unsigned long long R = m == 64 ? ~0ull : ((1ull << m) - 1ull);
-    for (int f = 0; f < F; ++f) {
-      const uint32_t code = my_bytes[f];
-      unsigned long long eq = R, gt = 0ull;
+    // ---- presort: keys {code : 8, lane : 8} are unique, so the network is stable
+    const uint32_t* rowp = codes_rm + (int64_t)row * row_words;
+    int lg = 1;
+    while ((1 << lg) < m) ++lg;
+    for (int w = 0; w < nwords; ++w) {
+      const uint32_t word = act ? rowp[w] : 0u;
 #pragma unroll
-      for (int b = 7; b >= 0; --b) {
-        const unsigned long long bm = __ballot((code >> b) & 1u) & R;
-        if ((code >> b) & 1u) {
-          eq &= bm;
-        } else {
-          gt |= eq & bm;
-          eq &= ~bm;
-        }
+      for (int h = 0; h < 2; ++h) {
+        const int f = w * 4 + 2 * h;
+        if (f >= F) break;
+        const uint32_t ka = ((word >> (16 * h)) & 0xffu) << 8 | (uint32_t)lane;
+        const uint32_t kb = ((word >> (16 * h + 8)) & 0xffu) << 8 | (uint32_t)lane;
+        uint32_t v = act ? (ka | (kb << 16)) : 0xffffffffu;
+        v = bitonic64_pk_u16(v, lane, lg);
+        const uint32_t nv = (uint32_t)__shfl_down((int)v, 1, kWave);
+        const bool endl = lane == m - 1;
+        const uint32_t ea = (endl || ((nv >> 8) & 0xffu) != ((v >> 8) & 0xffu)) ? 0x80u : 0u;
+        const uint32_t eb = (endl || (nv >> 24) != (v >> 24)) ? 0x80u : 0u;
+        // positions past the subtree: lane 63 (never a node row there), no run end
+        srt[f * kWave + lane] = act ? (uint16_t)((v & 0xffffu) | ea) : (uint16_t)0xff3fu;
+        if (f + 1 < F)
+          srt[(f + 1) * kWave + lane] = act ? (uint16_t)((v >> 16) | eb) : (uint16_t)0xff3fu;
       }
-      const unsigned long long lt = R & ~gt & ~eq;
-      if (act) order[f * kWave + __popcll(lt) + __popcll(eq & below)] = (uint8_t)lane;
     }
     if (lane == 0) {
-      s_mask[wave][0] = R;
+      s_mask[wave][0] = m == 64 ? ~0ull : ((1ull << m) - 1ull);
       s_dep[wave][0] = depth0;
       s_slot[wave][0] = (int32_t)root_slot;
     }
@@ -430,59 +494,223 @@ __global__ __launch_bounds__(256) void finish_tiny_reg_kernel(
       const int64_t slot = s_slot[wave][sp];
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      const bool mine = (M >> lane) & 1ull;
+      const bool mine = act && ((M >> lane) & 1ull);
       const int mm = __popcll(M);
       const int64_t S = wave_sum_i64(mine ? (int64_t)yv : 0);
       long long mn = mine ? yv : LLONG_MAX, mx = mine ? yv : LLONG_MIN;
       wave_minmax_i64(mn, mx);
       if (mn == mx) continue;  // all targets equal: leaf (record written at creation)
-      const double pterm = mse_term(mm, S);
-      double bg = -__builtin_inf(), bc = __builtin_inf();
-      int bf = 0x7fffffff;
+      int bf = -1;
       uint32_t bb = 0xffffffffu;
-      for (int f = 0; f < F; ++f) {
-        const int s = act ? order[f * kWave + lane] : 0;
-        const bool in = act && ((M >> s) & 1ull);
-        const uint32_t code = codes_b[s * cw * 4 + f];
-        const uint32_t ml = wave_incl_scan_dpp(in ? 1u : 0u);
-        const int64_t sl = wave_incl_scan_i64(in ? (int64_t)s_y[s] : 0);
-        const unsigned long long inb = __ballot(in);
-        const unsigned long long after = inb & ~(below | (1ull << lane));
-        const int nxt = after ? __ffsll((long long)after) - 1 : lane;
-        const uint32_t ncode = (uint32_t)__shfl((int)code, nxt, kWave);
-        const bool last = in && (after == 0ull || ncode != code);
-        const int mr = mm - (int)ml;
-        double cost = __builtin_inf();
-        if (last && (int64_t)ml >= msl && (int64_t)mr >= msl)
-          cost = mse_term(ml, sl) + mse_term(mr, S - sl);
-        const double g = pterm - cost;
-        if (g > bg) {
-          bg = g;
-          bf = f;
-          bc = cost;
-          bb = code;
+      unsigned long long LM = 0ull;
+      if (mm == 2) {
+        // Two rows (about half the internal nodes of a subtree grown to single
+        // rows): the only partition is {a} | {b}, so every feature whose codes
+        // differ scores the same cost bit for bit (fp64 addition commutes) and
+        // the lowest such feature wins, at the smaller code -- no scans.
+        const int a = __ffsll((long long)M) - 1, b = 63 - __clzll((long long)M);
+        if (msl <= 1) {
+          const uint32_t ra = (uint32_t)__builtin_amdgcn_readlane((int)row, a);
+          const uint32_t rb = (uint32_t)__builtin_amdgcn_readlane((int)row, b);
+          for (int w0 = 0; w0 < nwords; w0 += kWave) {
+            const int w = w0 + lane;
+            uint32_t x = 0u, wa = 0u;
+            if (w < nwords) {
+              wa = codes_rm[(int64_t)ra * row_words + w];
+              x = wa ^ codes_rm[(int64_t)rb * row_words + w];
+            }
+            const unsigned long long nz = __ballot(x != 0u);
+            if (nz) {
+              const int wl = __ffsll((long long)nz) - 1;
+              const uint32_t xw = (uint32_t)__builtin_amdgcn_readlane((int)x, wl);
+              const uint32_t aw = (uint32_t)__builtin_amdgcn_readlane((int)wa, wl);
+              const int byte = (__ffs((int)xw) - 1) >> 3;
+              const int f = (w0 + wl) * 4 + byte;
+              if (f < F) {  // (bytes past F are row padding)
+                const uint32_t ca = (aw >> (8 * byte)) & 0xffu;
+                const uint32_t cb = ca ^ ((xw >> (8 * byte)) & 0xffu);
+                bf = f;
+                bb = ca < cb ? ca : cb;
+                LM = ca < cb ? (1ull << a) : (1ull << b);
+              }
+              break;
+            }
+          }
         }
-      }
+        if (bf < 0) continue;  // identical rows (or min_samples_leaf > 1): leaf
+      } else if (mm <= kRegSmallNode) {
+        // Small node: one lane per feature. Lane f reads the node rows' codes of
+        // feature f (coalesced bytes of each row) and scores every distinct
+        // code as a threshold from the exact int64 left sums -- mm^2 integer
+        // steps and mm exact costs per lane instead of a wave scan per feature.
+        // Same exact costs and the same (gain, feature, cost, code) order.
+        uint32_t rj[kRegSmallNode];
+        int64_t yj[kRegSmallNode];
+        unsigned long long rest = M;
 #pragma unroll
-      for (int dd = kWave / 2; dd > 0; dd >>= 1) {
-        const double og = __shfl_xor(bg, dd, kWave);
-        const int of = __shfl_xor(bf, dd, kWave);
-        const double oc = __shfl_xor(bc, dd, kWave);
-        const uint32_t ob = (uint32_t)__shfl_xor((int)bb, dd, kWave);
-        const bool take =
-            og > bg ||
-            (og == bg && (of < bf || (of == bf && (oc < bc || (oc == bc && ob < bb)))));
-        if (take) {
-          bg = og;
-          bf = of;
-          bc = oc;
-          bb = ob;
+        for (int t = 0; t < kRegSmallNode; ++t) {
+          const int j = rest ? __ffsll((long long)rest) - 1 : 0;
+          rest &= rest - 1ull;
+          rj[t] = (uint32_t)__builtin_amdgcn_readlane((int)row, j);
+          yj[t] = (int64_t)s_y[j];
         }
+        const double pterm = mse_term(mm, S);
+        double bg = -__builtin_inf(), bc = __builtin_inf();
+        bf = 0x7fffffff;
+        const uint8_t* cb8 = reinterpret_cast<const uint8_t*>(codes_rm);
+        const int64_t rb = row_words * 4;
+        for (int f0 = 0; f0 < F; f0 += kWave) {
+          const int f = f0 + lane;
+          uint32_t code[kRegSmallNode];
+#pragma unroll
+          for (int t = 0; t < kRegSmallNode; ++t)
+            code[t] = (t < mm && f < F) ? (uint32_t)cb8[(int64_t)rj[t] * rb + f] : 0xffffu;
+          if (f < F) {
+#pragma unroll
+            for (int i = 0; i < kRegSmallNode; ++i) {
+              if (i >= mm) break;
+              const uint32_t c = code[i];
+              int ml = 0;
+              int64_t sl = 0;
+#pragma unroll
+              for (int t = 0; t < kRegSmallNode; ++t) {
+                const bool le = code[t] <= c;  // (padding entries are 0xffff: never)
+                ml += le ? 1 : 0;
+                sl += le ? yj[t] : 0;
+              }
+              const int mr = mm - ml;
+              if (ml >= mslw && mr >= mslw) {
+                const double cost = mse_term(ml, sl) + mse_term(mr, S - sl);
+                const double g = pterm - cost;
+                if (g > bg || (g == bg && (f < bf || (f == bf && (cost < bc ||
+                                                               (cost == bc && c < bb)))))) {
+                  bg = g;
+                  bf = f;
+                  bc = cost;
+                  bb = c;
+                }
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int dd = kWave / 2; dd > 0; dd >>= 1) {
+          const double og = __shfl_xor(bg, dd, kWave);
+          const int of = __shfl_xor(bf, dd, kWave);
+          const double oc = __shfl_xor(bc, dd, kWave);
+          const uint32_t ob = (uint32_t)__shfl_xor((int)bb, dd, kWave);
+          const bool take =
+              og > bg ||
+              (og == bg && (of < bf || (of == bf && (oc < bc || (oc == bc && ob < bb)))));
+          if (take) {
+            bg = og;
+            bf = of;
+            bc = oc;
+            bb = ob;
+          }
+        }
+        bf = __builtin_amdgcn_readfirstlane(bf);
+        bb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bb);
+        if (!(bg > -__builtin_inf()) || bf < 0 || bf >= F) continue;
+        {
+          const uint32_t v = srt[bf * kWave + lane];
+          if (act) flag[v & 0x3fu] = (uint8_t)((v >> 8) <= bb);
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+        }
+        LM = M & __ballot(act && flag[lane]);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      } else {
+        // ---- pass 1: fp32 minimum cost of every feature
+        const float ym = mine ? yf : 0.0f;
+        const float Sf = (float)S;
+        const float Af = __uint_as_float((uint32_t)__builtin_amdgcn_readlane(
+            (int)__float_as_uint(wave_incl_scan_f32_dpp(fabsf(ym))), 63));
+        const float fmm = (float)mm;
+        float nmin = __builtin_inff();
+        auto approx = [&](uint32_t v, uint32_t ml, float sl) -> float {
+          const float fl = (float)ml, fr = fmm - fl, sr = Sf - sl;
+          const bool ok = (v & 0x80u) && (int)ml >= mslw && mm - (int)ml >= mslw;
+          const float c = -((sl * sl) * __builtin_amdgcn_rcpf(fl) +
+                            (sr * sr) * __builtin_amdgcn_rcpf(fr));
+          return ok ? c : __builtin_inff();
+        };
+        for (int f = 0; f < F; f += 2) {
+          const bool two = f + 1 < F;
+          const uint32_t va = srt[f * kWave + lane];
+          const uint32_t vb = two ? (uint32_t)srt[(f + 1) * kWave + lane] : 0xff3fu;
+          const uint32_t sa = va & 0x3fu, sb = vb & 0x3fu;
+          const uint32_t ia = (uint32_t)(M >> sa) & 1u, ib = (uint32_t)(M >> sb) & 1u;
+          const float ya = __shfl(ym, (int)sa, kWave), yb = __shfl(ym, (int)sb, kWave);
+          const uint32_t cnt = wave_incl_scan_dpp(ia | (ib << 16));
+          const float sla = wave_incl_scan_f32_dpp(ya), slb = wave_incl_scan_f32_dpp(yb);
+          const float fa = wave_min_f32_dpp(approx(va, cnt & 0xffffu, sla));
+          const float fb = wave_min_f32_dpp(approx(vb, cnt >> 16, slb));
+          if (lane == 0) {
+            s_fmin[f] = fa;
+            if (two) s_fmin[f + 1] = fb;
+          }
+          nmin = fminf(nmin, two ? fminf(fa, fb) : fa);
+        }
+        if (!(nmin < __builtin_inff())) continue;  // no admissible split: leaf
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const float thr = nmin + 0x1p-13f * (Af * Af);
+        // ---- pass 2: exact costs of the features that can hold the optimum
+        const double pterm = mse_term(mm, S);
+        double bg = -__builtin_inf(), bc = __builtin_inf();
+        bf = 0x7fffffff;
+        for (int f = 0; f < F; ++f) {
+          if (!(s_fmin[f] <= thr)) continue;  // wave-uniform
+          const uint32_t v = srt[f * kWave + lane];
+          const uint32_t s = v & 0x3fu;
+          const uint32_t in = (uint32_t)(M >> s) & 1u;
+          const int64_t ys = in ? (int64_t)s_y[s] : 0;
+          const int ml = (int)wave_incl_scan_dpp(in);
+          const int64_t sl = wave_incl_scan_i64_dpp(ys);
+          const int mr = mm - ml;
+          double cost = __builtin_inf();
+          if ((v & 0x80u) && ml >= mslw && mr >= mslw)
+            cost = mse_term(ml, sl) + mse_term(mr, S - sl);
+          const double g = pterm - cost;
+          if (g > bg) {  // features ascend: strict > keeps the lowest
+            bg = g;
+            bf = f;
+            bc = cost;
+            bb = v >> 8;
+          }
+        }
+#pragma unroll
+        for (int dd = kWave / 2; dd > 0; dd >>= 1) {
+          const double og = __shfl_xor(bg, dd, kWave);
+          const int of = __shfl_xor(bf, dd, kWave);
+          const double oc = __shfl_xor(bc, dd, kWave);
+          const uint32_t ob = (uint32_t)__shfl_xor((int)bb, dd, kWave);
+          const bool take =
+              og > bg ||
+              (og == bg && (of < bf || (of == bf && (oc < bc || (oc == bc && ob < bb)))));
+          if (take) {
+            bg = og;
+            bf = of;
+            bc = oc;
+            bb = ob;
+          }
+        }
+        bf = __builtin_amdgcn_readfirstlane(bf);
+        bb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bb);
+        if (!(bg > -__builtin_inf()) || bf < 0) continue;
+        // left rows: sorted positions of feature bf with code <= bb, scattered back to lanes
+        {
+          const uint32_t v = srt[bf * kWave + lane];
+          if (act) flag[v & 0x3fu] = (uint8_t)((v >> 8) <= bb);
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+        }
+        LM = M & __ballot(act && flag[lane]);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
       }
-      bf = __builtin_amdgcn_readfirstlane(bf);
-      bb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bb);
-      if (!(bg > -__builtin_inf()) || bf < 0) continue;
-      const unsigned long long LM = M & __ballot(act && (uint32_t)my_bytes[bf] <= bb);
       const unsigned long long RM = M & ~LM;
       const int nl = __popcll(LM), nr = __popcll(RM);
       const int64_t ls = slot + 1, rs = slot + 2 * nl;
@@ -552,13 +780,12 @@ void launch_finish_reg(hipStream_t stream, const void* codes_rm, int64_t row_wor
 #undef MT_FR
   MT_HIP_CHECK(hipGetLastError());
   if (tiny_rows > 0) {
-    const int cw = ((F + 3) / 4) | 1;
-    const size_t tl = (size_t)kRegTinyWaves * (kWave * cw + (F * kWave + 3) / 4 + 2 * kWave) * 4;
+    const size_t tl = (size_t)kRegTinyWaves * reg_tiny_wave_bytes(F);
     MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_tiny_reg_kernel,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl));
     hipLaunchKernelGGL(finish_tiny_reg_kernel, dim3(tiny_grid), dim3(kRegTinyWaves * kWave), tl,
                        stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, tiny,
-                       counter + 1, counter + 2, F, max_depth, mss, msl, node_i32, node_st, cw);
+                       counter + 1, counter + 2, F, max_depth, mss, msl, node_i32, node_st);
     MT_HIP_CHECK(hipGetLastError());
   }
 }

@@ -315,6 +315,31 @@ def test_gpu_regression_device_loop_matches_host(monkeypatch, seed, max_depth):
     assert r1.arrays.equal(r3.arrays)
 
 
+@pytest.mark.parametrize("kind", ["gauss", "mixed_scale", "cancel"])
+def test_gpu_regression_tiny_prefilter_matches_host(kind):
+    """Continuous targets (every row its own leaf): the tiny regression kernel's
+    fp32 prefilter + exact rescoring gives the host builder's tree bit for bit,
+    also for targets spanning many magnitudes and for sums that cancel."""
+    from mpitree_amd.core.fit import fit_tree
+
+    rng = np.random.default_rng({"gauss": 1, "mixed_scale": 2, "cancel": 3}[kind])
+    n, F = 30000, 9
+    X = rng.integers(0, 256, size=(n, F)).astype(np.float32)
+    base = X[:, 0] / 64.0 + np.sin(X[:, 1] / 20.0)
+    if kind == "gauss":
+        y = base + rng.normal(size=n)
+    elif kind == "mixed_scale":
+        y = base * 10.0 ** rng.integers(-3, 7, size=n) * rng.choice([-1.0, 1.0], size=n)
+    else:  # large opposite-sign pairs: node sums far below sum |y|
+        y = 1e6 * rng.choice([-1.0, 1.0], size=n) + rng.normal(size=n)
+    kw = dict(regression=True, criterion=2, max_depth=None, min_samples_split=2)
+    g = fit_tree(X, y, device="cuda", **kw)
+    assert g.engine == "hip-device-loop"
+    h = fit_tree(X, y, device="cpu", **kw)
+    assert g.arrays.equal(h.arrays)
+    assert np.array_equal(g.arrays.value, h.arrays.value)
+
+
 @pytest.mark.parametrize("crit", ["entropy", "gini"])
 @pytest.mark.parametrize("shape", [(3000, 3, 2, None), (20000, 6, 3, None), (5000, 4, 5, 6)])
 def test_gpu_exact_engine_matches_host(crit, shape):
