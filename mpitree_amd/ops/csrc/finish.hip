@@ -884,6 +884,9 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
       const unsigned long long LM = M & __ballot((uint32_t)my_bytes[bf] <= bb);
       const unsigned long long RM = M & ~LM;
       const int nl = __popcll(LM), nr = __popcll(RM);
+      // a split always leaves rows on both sides; anything else is a kernel bug --
+      // stop here instead of re-splitting into positions outside the subtree
+      if (nl == 0 || nr == 0) continue;
       const int64_t ls = slot + 1, rs = slot + 2 * nl;  // pre-order position ranges
       int nzl = 0, nzr = 0;
 #pragma unroll
@@ -952,6 +955,7 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
 //
 // LDS per wave: srt [F][64] halfwords + 64 flag bytes (tiny_wave_bytes); per
 // workgroup: the H table (tiny_h_entries doubles).
+constexpr int kTinySmallNode = 16;  // nodes of 3..16 rows: one lane per feature
 constexpr int kTinyH = (kTinyRows + 1) * (kTinyRows + 2) / 2;  // triangular a <= 64, b <= a
 __device__ __forceinline__ int tiny_h_idx(int a, int b) { return ((a * (a + 1)) >> 1) + b; }
 
@@ -1004,26 +1008,30 @@ __device__ __forceinline__ void tiny_sorted_subtree(
   // two features share a 32-bit register (packed 16-bit min / max).
   const uint32_t* rowp = codes_rm + (int64_t)row * row_words;
   const int nwords = (F + 3) >> 2;
-  int lg = 1;  // sort network size 2^lg >= m (m >= 2)
-  while ((1 << lg) < m) ++lg;
-  for (int w = 0; w < nwords; ++w) {
-    const uint32_t word = act ? rowp[w] : 0u;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int f = w * 4 + 2 * h;
-      if (f >= F) break;
-      const uint32_t ka = ((word >> (16 * h)) & 0xffu) << 8 | (uint32_t)lane;
-      const uint32_t kb = ((word >> (16 * h + 8)) & 0xffu) << 8 | (uint32_t)lane;
-      uint32_t v = act ? (ka | (kb << 16)) : 0xffffffffu;
-      v = bitonic64_pk_u16(v, lane, lg);
-      const uint32_t nv = (uint32_t)__shfl_down((int)v, 1, kWave);
-      const bool endl = lane == m - 1;
-      const uint32_t ea = (endl || ((nv >> 8) & 0xffu) != ((v >> 8) & 0xffu)) ? 0x80u : 0u;
-      const uint32_t eb = (endl || (nv >> 24) != (v >> 24)) ? 0x80u : 0u;
-      // positions past the subtree: lane 63 (never a row there, so no node
-      // bits), no run end -- the scan loop needs no activity test
-      srt[f * kWave + lane] = act ? (uint16_t)((v & 0xffffu) | ea) : (uint16_t)0xff3fu;
-      if (f + 1 < F) srt[(f + 1) * kWave + lane] = act ? (uint16_t)((v >> 16) | eb) : (uint16_t)0xff3fu;
+  // subtrees of at most kTinySmallNode rows never scan (every node takes the
+  // lane-per-feature path below), so they skip the presort
+  if (m > kTinySmallNode) {
+    int lg = 1;  // sort network size 2^lg >= m (m >= 2)
+    while ((1 << lg) < m) ++lg;
+    for (int w = 0; w < nwords; ++w) {
+      const uint32_t word = act ? rowp[w] : 0u;
+  #pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int f = w * 4 + 2 * h;
+        if (f >= F) break;
+        const uint32_t ka = ((word >> (16 * h)) & 0xffu) << 8 | (uint32_t)lane;
+        const uint32_t kb = ((word >> (16 * h + 8)) & 0xffu) << 8 | (uint32_t)lane;
+        uint32_t v = act ? (ka | (kb << 16)) : 0xffffffffu;
+        v = bitonic64_pk_u16(v, lane, lg);
+        const uint32_t nv = (uint32_t)__shfl_down((int)v, 1, kWave);
+        const bool endl = lane == m - 1;
+        const uint32_t ea = (endl || ((nv >> 8) & 0xffu) != ((v >> 8) & 0xffu)) ? 0x80u : 0u;
+        const uint32_t eb = (endl || (nv >> 24) != (v >> 24)) ? 0x80u : 0u;
+        // positions past the subtree: lane 63 (never a row there, so no node
+        // bits), no run end -- the scan loop needs no activity test
+        srt[f * kWave + lane] = act ? (uint16_t)((v & 0xffffu) | ea) : (uint16_t)0xff3fu;
+        if (f + 1 < F) srt[(f + 1) * kWave + lane] = act ? (uint16_t)((v >> 16) | eb) : (uint16_t)0xff3fu;
+      }
     }
   }
   if (lane == 0) {
@@ -1046,81 +1054,207 @@ __device__ __forceinline__ void tiny_sorted_subtree(
     const double pterm = H[tiny_h_idx(mm, mc1)];
     const double tu = tie_unit(xlog2x((uint64_t)mm), (int64_t)mm);
     const double tinv = 1.0 / tu;
-    double bg = -__builtin_inf(), bc = __builtin_inf();
-    int bf = 0x7fffffff;
-    uint32_t bb = 0xffffffffu;
-    // this lane's row in the node: {in : 8, in and class 1 : 8}, fetched per
-    // feature at sorted position k with one ds_bpermute from lane srt[f][k]
-    const bool lin = act && ((M >> lane) & 1ull);
-    const int nodebits = lin ? (1 | ((((cm1 >> lane) & 1ull) != 0ull) ? 0x100 : 0)) : 0;
-    // split cost at this lane's sorted position from the left counts (ml, l1)
     const char* Hb = reinterpret_cast<const char*>(H);
     // H[tri(a) + b] by byte offset; Hrow[a] = 8 tri(a) (an LDS lookup is cheaper
     // than the multiply on the VALU-bound path)
     auto hval = [&](int a, int b) -> double {
       return *reinterpret_cast<const double*>(Hb + Hrow[a] + ((uint32_t)b << 3));
     };
-    auto cost_of = [&](uint32_t v, int ml, int l1) -> double {
-      const int mr = mm - ml, r1 = mc1 - l1;
-      const bool ok = (v & 0x80u) && ml >= mslw && mr >= mslw;
-      const double c = tie_round(hval(ml, l1) + hval(mr, r1), tinv, tu);
-      return ok ? c : __builtin_inf();
-    };
-    auto take = [&](int f, double cost, uint32_t v) {
-      const double g = pterm - cost;
-      const bool better = g > bg;  // features ascend: strict > keeps the lowest
-      bg = better ? g : bg;
-      bf = better ? f : bf;
-      bc = better ? cost : bc;
-      bb = better ? (v >> 8) : bb;
-    };
-    // two features per DPP scan: {in, class 1} counts of feature a in the low
-    // 16 bits, of feature b in the high 16 (every field <= 64)
-    for (int f = 0; f < F; f += 2) {
-      const bool two = f + 1 < F;
-      const uint32_t va = srt[f * kWave + lane];
-      const uint32_t vb = two ? (uint32_t)srt[(f + 1) * kWave + lane] : 0u;
-      const uint32_t xa = (uint32_t)__shfl(nodebits, (int)(va & 0x3fu), kWave);
-      const uint32_t xb = (uint32_t)__shfl(nodebits, (int)(vb & 0x3fu), kWave);
-      const uint32_t incl = wave_incl_scan_dpp(xa | (xb << 16));
-      const double ca = cost_of(va, (int)(incl & 0xffu), (int)((incl >> 8) & 0xffu));
-      const double cb = cost_of(vb, (int)((incl >> 16) & 0xffu), (int)(incl >> 24));
-      take(f, ca, va);
-      if (two) take(f + 1, cb, vb);
-    }
-#pragma unroll
-    for (int dd = kWave / 2; dd > 0; dd >>= 1) {
-      const double og = __shfl_xor(bg, dd, kWave);
-      const int of = __shfl_xor(bf, dd, kWave);
-      const double oc = __shfl_xor(bc, dd, kWave);
-      const uint32_t ob = (uint32_t)__shfl_xor((int)bb, dd, kWave);
-      const bool tk =
-          og > bg || (og == bg && (of < bf || (of == bf && (oc < bc || (oc == bc && ob < bb)))));
-      if (tk) {
-        bg = og;
-        bf = of;
-        bc = oc;
-        bb = ob;
+    int bf = -1;
+    uint32_t bb = 0xffffffffu;
+    unsigned long long LM = 0ull;
+    if (mm == 2) {
+      // Two rows of different classes (pure nodes are never pushed): the only
+      // partition is {a} | {b}, which costs 0 (entropy and gini) for every
+      // feature whose codes differ, so the lowest such feature wins at the
+      // smaller code -- no scans.
+      const int a = __ffsll((long long)M) - 1, b = 63 - __clzll((long long)M);
+      if (mslw <= 1) {
+        const uint32_t ra = (uint32_t)__builtin_amdgcn_readlane((int)row, a);
+        const uint32_t rb = (uint32_t)__builtin_amdgcn_readlane((int)row, b);
+        for (int w0 = 0; w0 < nwords; w0 += kWave) {
+          const int w = w0 + lane;
+          uint32_t x = 0u, wa = 0u;
+          if (w < nwords) {
+            wa = codes_rm[(int64_t)ra * row_words + w];
+            x = wa ^ codes_rm[(int64_t)rb * row_words + w];
+          }
+          const unsigned long long nz = __ballot(x != 0u);
+          if (nz) {
+            const int wl = __ffsll((long long)nz) - 1;
+            const uint32_t xw = (uint32_t)__builtin_amdgcn_readlane((int)x, wl);
+            const uint32_t aw = (uint32_t)__builtin_amdgcn_readlane((int)wa, wl);
+            const int byte = (__ffs((int)xw) - 1) >> 3;
+            const int f = (w0 + wl) * 4 + byte;
+            if (f < F) {  // (bytes past F are row padding)
+              const uint32_t ca = (aw >> (8 * byte)) & 0xffu;
+              const uint32_t cb = ca ^ ((xw >> (8 * byte)) & 0xffu);
+              bf = f;
+              bb = ca < cb ? ca : cb;
+              LM = ca < cb ? (1ull << a) : (1ull << b);
+            }
+            break;
+          }
+        }
       }
-    }
-    bf = __builtin_amdgcn_readfirstlane(bf);
-    bb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bb);
-    if (!(bg > -__builtin_inf()) || bf < 0) continue;  // leaf: the creation record stands
-    // left rows: sorted positions of feature bf with code <= bb, scattered back to lanes
-    {
-      const uint32_t v = srt[bf * kWave + lane];
-      if (act) flag[v & 0x3fu] = (uint8_t)((v >> 8) <= bb);
+      if (bf < 0) continue;  // identical rows (or min_samples_leaf > 1): leaf
+    } else if (mm <= kTinySmallNode) {
+      // Small node: one lane per feature. Lane f reads the node rows' codes of
+      // feature f (coalesced bytes of each row, L2-resident) and scores every
+      // distinct code as a threshold from the left counts {rows, class-1 rows}
+      // -- mm^2 integer steps and mm table costs per lane instead of a wave
+      // scan per feature pair; same tie-rounded costs and the same
+      // (gain, feature, cost, code) order as the scan below.
+      uint32_t rj[kTinySmallNode], lj[kTinySmallNode];
+      unsigned long long rest = M;
+#pragma unroll
+      for (int t = 0; t < kTinySmallNode; ++t) {
+        const int j = rest ? __ffsll((long long)rest) - 1 : 0;
+        rest &= rest - 1ull;
+        rj[t] = (uint32_t)__builtin_amdgcn_readlane((int)row, j);
+        lj[t] = 1u | ((uint32_t)((cm1 >> j) & 1ull) << 16);  // {row, class-1 row}
+      }
+      double bg = -__builtin_inf(), bc = __builtin_inf();
+      bf = 0x7fffffff;
+      const uint8_t* cb8 = reinterpret_cast<const uint8_t*>(codes_rm);
+      const int64_t rbytes = row_words * 4;
+      uint32_t code[kTinySmallNode];
+      for (int f0 = 0; f0 < F; f0 += kWave) {
+        const int f = f0 + lane;
+#pragma unroll
+        for (int t = 0; t < kTinySmallNode; ++t)
+          code[t] = (t < mm && f < F) ? (uint32_t)cb8[(int64_t)rj[t] * rbytes + f] : 0xffffu;
+        if (f < F) {
+#pragma unroll
+          for (int i = 0; i < kTinySmallNode; ++i) {
+            if (i >= mm) break;
+            const uint32_t c = code[i];
+            uint32_t acc = 0u;
+#pragma unroll
+            for (int t = 0; t < kTinySmallNode; ++t) acc += code[t] <= c ? lj[t] : 0u;
+            const int ml = (int)(acc & 0xffffu), l1 = (int)(acc >> 16);
+            const int mr = mm - ml, r1 = mc1 - l1;
+            if (ml >= mslw && mr >= mslw) {
+              const double cost = tie_round(hval(ml, l1) + hval(mr, r1), tinv, tu);
+              const double g = pterm - cost;
+              if (g > bg || (g == bg && (f < bf || (f == bf && (cost < bc ||
+                                                             (cost == bc && c < bb)))))) {
+                bg = g;
+                bf = f;
+                bc = cost;
+                bb = c;
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int dd = kWave / 2; dd > 0; dd >>= 1) {
+        const double og = __shfl_xor(bg, dd, kWave);
+        const int of = __shfl_xor(bf, dd, kWave);
+        const double oc = __shfl_xor(bc, dd, kWave);
+        const uint32_t ob = (uint32_t)__shfl_xor((int)bb, dd, kWave);
+        const bool tk =
+            og > bg || (og == bg && (of < bf || (of == bf && (oc < bc || (oc == bc && ob < bb)))));
+        if (tk) {
+          bg = og;
+          bf = of;
+          bc = oc;
+          bb = ob;
+        }
+      }
+      bf = __builtin_amdgcn_readfirstlane(bf);
+      bb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bb);
+      if (!(bg > -__builtin_inf()) || bf < 0 || bf >= F) continue;
+      // left rows from lane bf's codes of the node rows
+      const int f0w = bf & ~(kWave - 1);
+      if (F > kWave) {  // code[] holds the last chunk: reload the winning one
+#pragma unroll
+        for (int t = 0; t < kTinySmallNode; ++t)
+          code[t] = (t < mm && f0w + lane < F) ? (uint32_t)cb8[(int64_t)rj[t] * rbytes + f0w + lane]
+                                              : 0xffffu;
+      }
+      rest = M;
+#pragma unroll
+      for (int t = 0; t < kTinySmallNode; ++t) {
+        if (t >= mm) break;
+        const int j = __ffsll((long long)rest) - 1;
+        rest &= rest - 1ull;
+        const uint32_t ct = (uint32_t)__builtin_amdgcn_readlane((int)code[t], bf - f0w);
+        if (ct <= bb) LM |= 1ull << j;
+      }
+    } else {
+      double bg = -__builtin_inf(), bc = __builtin_inf();
+      bf = 0x7fffffff;
+      // this lane's row in the node: {in : 8, in and class 1 : 8}, fetched per
+      // feature at sorted position k with one ds_bpermute from lane srt[f][k]
+      const bool lin = act && ((M >> lane) & 1ull);
+      const int nodebits = lin ? (1 | ((((cm1 >> lane) & 1ull) != 0ull) ? 0x100 : 0)) : 0;
+      // split cost at this lane's sorted position from the left counts (ml, l1)
+      auto cost_of = [&](uint32_t v, int ml, int l1) -> double {
+        const int mr = mm - ml, r1 = mc1 - l1;
+        const bool ok = (v & 0x80u) && ml >= mslw && mr >= mslw;
+        const double c = tie_round(hval(ml, l1) + hval(mr, r1), tinv, tu);
+        return ok ? c : __builtin_inf();
+      };
+      auto take = [&](int f, double cost, uint32_t v) {
+        const double g = pterm - cost;
+        const bool better = g > bg;  // features ascend: strict > keeps the lowest
+        bg = better ? g : bg;
+        bf = better ? f : bf;
+        bc = better ? cost : bc;
+        bb = better ? (v >> 8) : bb;
+      };
+      // two features per DPP scan: {in, class 1} counts of feature a in the low
+      // 16 bits, of feature b in the high 16 (every field <= 64)
+      for (int f = 0; f < F; f += 2) {
+        const bool two = f + 1 < F;
+        const uint32_t va = srt[f * kWave + lane];
+        const uint32_t vb = two ? (uint32_t)srt[(f + 1) * kWave + lane] : 0u;
+        const uint32_t xa = (uint32_t)__shfl(nodebits, (int)(va & 0x3fu), kWave);
+        const uint32_t xb = (uint32_t)__shfl(nodebits, (int)(vb & 0x3fu), kWave);
+        const uint32_t incl = wave_incl_scan_dpp(xa | (xb << 16));
+        const double ca = cost_of(va, (int)(incl & 0xffu), (int)((incl >> 8) & 0xffu));
+        const double cb = cost_of(vb, (int)((incl >> 16) & 0xffu), (int)(incl >> 24));
+        take(f, ca, va);
+        if (two) take(f + 1, cb, vb);
+      }
+#pragma unroll
+      for (int dd = kWave / 2; dd > 0; dd >>= 1) {
+        const double og = __shfl_xor(bg, dd, kWave);
+        const int of = __shfl_xor(bf, dd, kWave);
+        const double oc = __shfl_xor(bc, dd, kWave);
+        const uint32_t ob = (uint32_t)__shfl_xor((int)bb, dd, kWave);
+        const bool tk =
+            og > bg || (og == bg && (of < bf || (of == bf && (oc < bc || (oc == bc && ob < bb)))));
+        if (tk) {
+          bg = og;
+          bf = of;
+          bc = oc;
+          bb = ob;
+        }
+      }
+      bf = __builtin_amdgcn_readfirstlane(bf);
+      bb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bb);
+      if (!(bg > -__builtin_inf()) || bf < 0) continue;  // leaf: the creation record stands
+      // left rows: sorted positions of feature bf with code <= bb, scattered back to lanes
+      {
+        const uint32_t v = srt[bf * kWave + lane];
+        if (act) flag[v & 0x3fu] = (uint8_t)((v >> 8) <= bb);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+      LM = M & __ballot(act && flag[lane]);
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
     }
-    const unsigned long long LM = M & __ballot(act && flag[lane]);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
     const unsigned long long RM = M & ~LM;
     const int nl = __popcll(LM), nr = __popcll(RM);
+    // a split always leaves rows on both sides; anything else is a kernel bug --
+    // stop here instead of re-splitting into positions outside the subtree
+    if (nl == 0 || nr == 0) continue;
     const int64_t ls = slot + 1, rs = slot + 2 * nl;  // pre-order position ranges
     const int lc1 = __popcll(LM & cm1), rc1 = (int)mc1 - lc1;
-    (void)bc;
     const int lc0 = nl - lc1, rc0 = nr - rc1;
     const int nzl = (lc0 > 0) + (lc1 > 0), nzr = (rc0 > 0) + (rc1 > 0);
     const int cd = d + 1;

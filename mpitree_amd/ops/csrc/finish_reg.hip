@@ -713,6 +713,9 @@ __global__ __launch_bounds__(256) void finish_tiny_reg_kernel(
       }
       const unsigned long long RM = M & ~LM;
       const int nl = __popcll(LM), nr = __popcll(RM);
+      // a split always leaves rows on both sides; anything else is a kernel bug --
+      // stop here instead of re-splitting into positions outside the subtree
+      if (nl == 0 || nr == 0) continue;
       const int64_t ls = slot + 1, rs = slot + 2 * nl;
       const int64_t SL = wave_sum_i64(((LM >> lane) & 1ull) ? (int64_t)yv : 0);
       const int cd = d + 1;

@@ -315,6 +315,18 @@ def test_gpu_regression_device_loop_matches_host(monkeypatch, seed, max_depth):
     assert r1.arrays.equal(r3.arrays)
 
 
+@pytest.mark.parametrize("F", [100, 128])
+def test_gpu_many_features_tiny_paths_match_host(F):
+    """F > 64: the tiny kernels' lane-per-feature small-node path walks several
+    64-feature chunks (the winning chunk's codes decide the partition)."""
+    from mpitree_amd.utils.datasets import make_classification
+
+    X, y = make_classification(60000, F, seed=F, device=torch.device("cuda"))
+    g = DecisionTreeClassifier(device="cuda").fit(X, y)
+    h = DecisionTreeClassifier(device="cpu").fit(X.cpu().numpy(), y.cpu().numpy())
+    assert g.tree_arrays_.equal(h.tree_arrays_)
+
+
 @pytest.mark.parametrize("kind", ["gauss", "mixed_scale", "cancel"])
 def test_gpu_regression_tiny_prefilter_matches_host(kind):
     """Continuous targets (every row its own leaf): the tiny regression kernel's
