@@ -326,6 +326,7 @@ __global__ __launch_bounds__(kBrThreads) void bin_rows_kernel(
     int32_t* __restrict__ flags, int64_t rows_per_block, int fm_vec) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ int s_flag[kBrFt];
+  __shared__ int s_aff[kBrFt];  // edges are e0, e0 + 1, ..., e0 + nb - 1 (integers)
   const int ES = Bmax | 1;
   const int f0 = blockIdx.y * kBrFt;
   const int nf = min(kBrFt, F - f0);  // multiple of 4
@@ -335,10 +336,25 @@ __global__ __launch_bounds__(kBrThreads) void bin_rows_kernel(
   float* s_edges = reinterpret_cast<float*>(smem);
   uint8_t* tile = smem + (((size_t)nf * ES * 4 + 15) & ~(size_t)15);  // [batch][nf]
   const int tid = threadIdx.x;
-  if (tid < kBrFt) s_flag[tid] = 0;
+  if (tid < kBrFt) {
+    s_flag[tid] = 0;
+    s_aff[tid] = 1;
+  }
   for (int e = tid; e < nf * Bmax; e += kBrThreads) {
     const int fl = e / Bmax, b = e - fl * Bmax;
     s_edges[fl * ES + b] = edges[(int64_t)(f0 + fl) * estride + b];
+  }
+  __syncthreads();
+  // Consecutive-integer edges (integer-coded / quantized / categorical columns
+  // with every value present): the code is v - e0, one subtraction instead of
+  // an 8-step search through LDS. Exact in fp32 while |e0| + nb < 2^24.
+  for (int e = tid; e < nf * Bmax; e += kBrThreads) {
+    const int fl = e / Bmax, b = e - fl * Bmax;
+    if (b < nbins[f0 + fl]) {
+      const float e0 = s_edges[fl * ES];
+      const float eb = s_edges[fl * ES + b];
+      if (!(eb == e0 + (float)b) || !(fabsf(e0) < 8388608.0f) || e0 != rintf(e0)) s_aff[fl] = 0;
+    }
   }
   const int rs = tid / tpr;  // row slot within a pass
   const int q = tid - rs * tpr;
@@ -352,6 +368,13 @@ __global__ __launch_bounds__(kBrThreads) void bin_rows_kernel(
     fg[j] = 0;
   }
   __syncthreads();
+  bool aff[4];
+  float e0[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    aff[j] = active && s_aff[4 * q + j] != 0;
+    e0[j] = s_edges[(4 * q + j) * ES];
+  }
   const int64_t rbeg = blockIdx.x * rows_per_block;
   const int64_t rend = min<int64_t>(n, rbeg + rows_per_block);
   fm_vec = fm_vec && ((rbeg | batch) & 15) == 0;
@@ -381,14 +404,25 @@ __global__ __launch_bounds__(kBrThreads) void bin_rows_kernel(
       v[4 * u + 2] = cur[u].z;
       v[4 * u + 3] = cur[u].w;
     }
+    bool hit[kBrU * 4];
+    bool need = false;
 #pragma unroll
-    for (int k = 0; k < kBrU * 4; ++k) pos[k] = 0;
-    for (int step = steps0; step > 0; step >>= 1) {
+    for (int k = 0; k < kBrU * 4; ++k) {
+      const int j = k & 3;
+      const float d = v[k] - e0[j];
+      const int c = (int)d;  // v_cvt_i32_f32 saturates; NaN -> 0 (the checks reject both)
+      hit[k] = aff[j] && d == (float)c && c >= 0 && c < nb[j];
+      pos[k] = hit[k] ? c : 0;
+      need |= active && !hit[k];
+    }
+    if (__ballot(need)) {  // some value is not an integer edge: lower_bound search
+      for (int step = steps0; step > 0; step >>= 1) {
 #pragma unroll
-      for (int k = 0; k < kBrU * 4; ++k) {
-        const int j = k & 3;
-        const int p = pos[k] + step;
-        if (p <= nb[j] && s_edges[(4 * q + j) * ES + p - 1] < v[k]) pos[k] = p;
+        for (int k = 0; k < kBrU * 4; ++k) {
+          const int j = k & 3;
+          const int p = pos[k] + step;
+          if (!hit[k] && p <= nb[j] && s_edges[(4 * q + j) * ES + p - 1] < v[k]) pos[k] = p;
+        }
       }
     }
     const int rows = (int)min<int64_t>(batch, rend - b0);
@@ -400,7 +434,7 @@ __global__ __launch_bounds__(kBrThreads) void bin_rows_kernel(
       for (int j = 0; j < 4; ++j) {
         const int k = 4 * u + j;
         const int code = pos[k] < nb[j] ? pos[k] : nb[j] - 1;
-        if (ex[j] && !(s_edges[(4 * q + j) * ES + code] == v[k])) fg[j] |= 1;
+        if (ex[j] && !hit[k] && !(s_edges[(4 * q + j) * ES + code] == v[k])) fg[j] |= 1;
         if (!isfinite(v[k])) fg[j] |= 2;
         word |= (uint32_t)code << (8 * j);
       }

@@ -186,6 +186,33 @@ def test_gpu_edges_match_host_mapper():
     assert np.array_equal(codes_fm.cpu().numpy().T[:, :5], host.transform(X))
 
 
+def test_gpu_bin_rows_consecutive_integer_edges():
+    """Row-streaming binning (F % 4 == 0): columns whose edges are consecutive
+    integers take the subtraction path; every other column the LDS search.
+    Both code layouts equal the host BinMapper's transform."""
+    from mpitree_amd.core.binning import fit_bin_mapper
+    from mpitree_amd.ops.hip_backend import gpu_bin_features
+
+    rng = np.random.default_rng(11)
+    n = 20000
+    cols = [
+        rng.integers(0, 256, size=n),              # 0..255: consecutive
+        rng.integers(1000, 1100, size=n),          # offset range: consecutive
+        rng.integers(-50, 50, size=n),             # negative start: consecutive
+        2 * rng.integers(0, 100, size=n),          # even values: gaps -> search
+        rng.integers(0, 100, size=n) + 0.5,        # half-integers -> search
+        rng.normal(size=n),                        # quantiles -> search
+        rng.integers(0, 3, size=n),                # 3 levels: consecutive
+        np.full(n, 7.0),                           # constant: one edge
+    ]
+    X = np.stack(cols, 1).astype(np.float32)
+    host = fit_bin_mapper(X, 256)
+    mapper, codes_rm, codes_fm, nb = gpu_bin_features(torch.from_numpy(X).cuda(), 256)
+    want = host.transform(X)
+    assert np.array_equal(codes_fm.cpu().numpy().T[:, : X.shape[1]], want)
+    assert np.array_equal(codes_rm.cpu().numpy()[:, : X.shape[1]], want)
+
+
 @pytest.mark.parametrize("labels", ["int64", "int32-gaps", "negative", "float", "host"])
 def test_gpu_label_prepare_paths(labels):
     """Device label encoding (range count + LUT, gpu_prepare) == host np.unique,
