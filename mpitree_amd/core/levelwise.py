@@ -453,18 +453,8 @@ class LevelwiseBuilder:
         rpos = np.where(inner, tab.pos[np.maximum(tab.right[ids], 0)], -1)
         self.be.put_positions(tab.pos[ids], f, tab.tbin[ids], lpos, rpos, tab.depth[ids],
                               tab.nsamp[ids], tab.stats[ids])
-        a = self.be.assemble_positions(self._edges, int(self.p.criterion), self._y_exp)
-        st = a["stats"]
-        ta = TreeArrays(
-            feature=a["feature"], threshold=a["threshold"], threshold_bin=a["bin"],
-            left=a["left"], right=a["right"], depth=a["depth"], n_samples=a["nsamp"],
-            impurity=a["impurity"], count=None if reg else st,
-            value=a["value"] if reg else None,
-        )
-        if reg:
-            ta.meta["sum_fixed"] = st[:, 1]
-        ta.meta["final"] = True  # thresholds, impurity and values are filled in
-        return ta
+        # thresholds, impurity and values need no host pass (meta["final"])
+        return self.be.assemble_positions(self._edges, int(self.p.criterion), self._y_exp)
 
     def _to_arrays(self, tab: _Table) -> TreeArrays:
         reg = self.p.criterion == Criterion.SQUARED_ERROR

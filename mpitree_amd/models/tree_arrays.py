@@ -37,6 +37,90 @@ class TreeArrays:
     value: Optional[np.ndarray] = None  # float64 [N] (regression leaf mean)
     meta: dict = field(default_factory=dict)
 
+    # ------------------------------------------------------- deferred columns
+    def __getattr__(self, name):
+        # reached only when normal lookup fails: a column of a device-assembled
+        # tree that is derived from the transferred ones on first use
+        derive = self.__dict__.get("_derive")
+        if derive and name in derive:
+            v = derive.pop(name)(self)
+            self.__dict__[name] = v
+            return v
+        raise AttributeError(f"{type(self).__name__!s} has no attribute {name!r}")
+
+    def materialize(self) -> "TreeArrays":
+        """Compute every deferred column now."""
+        for name in list(self.__dict__.get("_derive") or ()):
+            getattr(self, name)
+        return self
+
+    def __getstate__(self):
+        self.materialize()
+        return {k: v for k, v in self.__dict__.items() if k != "_derive"}
+
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+
+    @classmethod
+    def deferred(cls, derive: dict, **cols) -> "TreeArrays":
+        """A tree whose columns in ``derive`` (name -> fn(tree)) are computed on
+        first access; ``cols`` are set now."""
+        ta = cls.__new__(cls)
+        ta.__dict__.update(cols)
+        ta.__dict__.setdefault("meta", {})
+        ta.__dict__["_derive"] = dict(derive)
+        return ta
+
+    @classmethod
+    def from_device_columns(cls, *, stats, threshold, feature, threshold_bin, right, depth,
+                            criterion: int, regression: bool, y_exp: int = 0) -> "TreeArrays":
+        """The device assembly's columns (``ops/csrc/assemble.hip``): class
+        counts (int32) or regression {count, fixed-point sum} (int64), split
+        thresholds, features, bins, right children and depths in pre-order.
+        Left children (pre-order: node + 1), node sizes, int64 counts,
+        impurities and regression leaf values follow from them and are computed
+        on first use with the same integer-form criterion as every builder
+        (``core/criterion.py``, bitwise equal to the device's)."""
+        from ..core import criterion as cr
+
+        N = int(feature.shape[0])
+
+        def left(t):
+            return np.where(t.feature >= 0, np.arange(1, N + 1, dtype=np.int32),
+                            np.int32(-1)).astype(np.int32)
+
+        if regression:
+            def n_samples(t):
+                return stats[:, 0].astype(np.int64)
+
+            def value(t):
+                s = stats[:, 1].astype(np.float64)
+                return np.ldexp(s / np.maximum(stats[:, 0], 1).astype(np.float64), -int(y_exp))
+
+            derive = {"left": left, "n_samples": n_samples, "value": value,
+                      "impurity": lambda t: np.full(N, np.nan)}
+            ta = cls.deferred(derive, feature=feature, threshold=threshold,
+                              threshold_bin=threshold_bin, right=right, depth=depth, count=None)
+            ta.meta["sum_fixed"] = stats[:, 1]
+        else:
+            def n_samples(t):
+                return stats.sum(axis=1, dtype=np.int64)
+
+            def impurity(t):
+                m = t.n_samples
+                c = cr.Criterion(int(criterion))
+                term = (cr.entropy_term(stats) if c == cr.Criterion.ENTROPY
+                        else cr.gini_term(stats))
+                with np.errstate(invalid="ignore", divide="ignore"):
+                    return np.where(m > 0, term / np.maximum(m, 1).astype(np.float64), 0.0)
+
+            derive = {"left": left, "n_samples": n_samples, "impurity": impurity,
+                      "count": lambda t: stats.astype(np.int64)}
+            ta = cls.deferred(derive, feature=feature, threshold=threshold,
+                              threshold_bin=threshold_bin, right=right, depth=depth, value=None)
+        ta.meta["final"] = True  # thresholds, impurity and values need no host pass
+        return ta
+
     # ------------------------------------------------------------------ basics
     @property
     def node_count(self) -> int:
@@ -392,3 +476,8 @@ class TreeArrays:
             count=None if d.get("count") is None else np.asarray(d["count"]),
             value=None if d.get("value") is None else np.asarray(d["value"]),
         )
+
+
+# the dataclass keeps these defaults in __init__; without the class attributes a
+# deferred count / value is found by __getattr__ rather than the class-level None
+del TreeArrays.count, TreeArrays.value

@@ -105,36 +105,32 @@ __global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __
 
 // Output columns, packed back to back for one D2H; the node count N is read
 // from the device (asm_offsets_kernel's total), so the emit launch needs no
-// host round trip. 8-byte columns first (alignment), then 4-byte columns:
-//   nsamp i64 [N] | stats i64 [N][C] | threshold f64 [N] | impurity f64 [N]
-//   | value f64 [N] (regression) | feature, bin, left, right, depth i32 [N]
+// host round trip. Only what the host cannot derive cheaply crosses the link:
+//   stats [N][C] (int32 class counts; regression int64 {count, fixed sum})
+//   | threshold f64 [N] | feature, bin, right, depth i32 [N]
+// Left children are implicit in pre-order (node j + 1), node sizes are the
+// stats' sums, impurities and leaf values follow from the stats with the same
+// integer-form criterion: the host derives those columns on first use
+// (TreeArrays.deferred). 32 B per node for a two-class tree instead of 60.
 struct AsmCols {
-  int64_t* nsamp;
-  int64_t* stats;
+  void* stats;
   double* threshold;
-  double* impurity;
-  double* value;
   int32_t* feature;
   int32_t* bin;
-  int32_t* left;
   int32_t* right;
   int32_t* depth;
 };
 
 __device__ inline AsmCols asm_cols(uint8_t* base, int64_t N, int C, bool reg) {
   AsmCols o;
-  int64_t* p8 = reinterpret_cast<int64_t*>(base);
-  o.nsamp = p8;
-  o.stats = p8 + N;
-  o.threshold = reinterpret_cast<double*>(p8 + N * (1 + C));
-  o.impurity = o.threshold + N;
-  o.value = reg ? o.impurity + N : nullptr;
-  int32_t* p4 = reinterpret_cast<int32_t*>(o.impurity + N * (reg ? 2 : 1));
+  o.stats = base;
+  const int64_t sbytes = reg ? N * 16 : ((N * C * 4 + 7) & ~(int64_t)7);
+  o.threshold = reinterpret_cast<double*>(base + sbytes);
+  int32_t* p4 = reinterpret_cast<int32_t*>(o.threshold + N);
   o.feature = p4;
   o.bin = p4 + N;
-  o.left = p4 + 2 * N;
-  o.right = p4 + 3 * N;
-  o.depth = p4 + 4 * N;
+  o.right = p4 + 2 * N;
+  o.depth = p4 + 3 * N;
   return o;
 }
 
@@ -143,53 +139,34 @@ template <typename StatT>
 __global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
     const int32_t* __restrict__ rec, const StatT* __restrict__ st, int64_t P, int C,
     const int32_t* __restrict__ rank, const double* __restrict__ edges, int EB,
-    const double* __restrict__ xtab, int xtab_n, int crit, int y_exp,
-    const int64_t* __restrict__ total, uint8_t* __restrict__ base) {
+    const int64_t* __restrict__ total, uint8_t* __restrict__ base, bool reg) {
   const int64_t p = (int64_t)blockIdx.x * kAsmThreads + threadIdx.x;
   if (p >= P) return;
   const int j = rank[p];
   if (j < 0) return;
-  const AsmCols o = asm_cols(base, *total, C, crit == kSquaredError);
+  const AsmCols o = asm_cols(base, *total, C, reg);
   const int32_t* R = rec + p * 6;
   const int f = R[0];
   const int b = R[1];
-  const int64_t n = R[5];
   o.feature[j] = f >= 0 ? f : -1;
   o.depth[j] = R[4];
-  o.nsamp[j] = n;
   if (f >= 0) {
     o.bin[j] = b;
-    o.left[j] = rank[R[2]];
     o.right[j] = rank[R[3]];
     o.threshold[j] = edges[(int64_t)f * EB + b];
   } else {
     o.bin[j] = -1;
-    o.left[j] = -1;
     o.right[j] = -1;
     o.threshold[j] = __builtin_nan("");
   }
-  auto T = [&](int64_t x) -> double {
-    return x < (int64_t)xtab_n ? xtab[x] : xlog2x((uint64_t)x);
-  };
   const StatT* s = st + p * C;
-  if (crit == kSquaredError) {
-    const int64_t cnt = (int64_t)s[0], sum = (int64_t)s[1];
-    o.stats[(int64_t)j * C + 0] = cnt;
-    o.stats[(int64_t)j * C + 1] = sum;
-    o.impurity[j] = __builtin_nan("");
-    o.value[j] = ldexp((double)sum / (double)(n > 1 ? n : 1), -y_exp);
+  if (reg) {
+    int64_t* so = reinterpret_cast<int64_t*>(o.stats) + (int64_t)j * 2;
+    so[0] = (int64_t)s[0];
+    so[1] = (int64_t)s[1];
   } else {
-    double acc = 0.0;
-    int64_t m = 0, sq = 0;
-    for (int c = 0; c < C; ++c) {
-      const int64_t v = (int64_t)s[c];
-      o.stats[(int64_t)j * C + c] = v;
-      acc = acc + T(v);
-      m += v;
-      sq += v * v;
-    }
-    const double term = crit == kEntropy ? T(m) - acc : gini_term(m, sq);
-    o.impurity[j] = n > 0 ? term / (double)n : 0.0;
+    int32_t* so = reinterpret_cast<int32_t*>(o.stats) + (int64_t)j * C;
+    for (int c = 0; c < C; ++c) so[c] = (int32_t)s[c];
   }
 }
 
@@ -207,22 +184,20 @@ void launch_asm_rank(hipStream_t stream, const int32_t* rec, int64_t P, int32_t*
 
 int asm_tiles(int64_t P) { return (int)((P + kAsmTile - 1) / kAsmTile); }
 
-int64_t asm_node_bytes(int C, bool reg) { return 8 * (1 + C + 2 + (reg ? 1 : 0)) + 4 * 5; }
+// upper bound per node (the stats block is padded to 8 bytes once, not per node)
+int64_t asm_node_bytes(int C, bool reg) { return (reg ? 16 : 4 * C) + 8 + 4 * 4 + 8; }
 
 void launch_asm_emit(hipStream_t stream, const int32_t* rec, const void* st, bool st64,
                      int64_t P, int C, const int32_t* rank, const double* edges, int EB,
-                     const double* xtab, int xtab_n, int crit, int y_exp, const int64_t* total,
-                     uint8_t* base) {
+                     const int64_t* total, uint8_t* base, bool reg) {
   const int64_t blocks = (P + kAsmThreads - 1) / kAsmThreads;
   if (blocks == 0) return;
   if (st64)
     hipLaunchKernelGGL(asm_emit_kernel<int64_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
-                       stream, rec, (const int64_t*)st, P, C, rank, edges, EB, xtab, xtab_n, crit,
-                       y_exp, total, base);
+                       stream, rec, (const int64_t*)st, P, C, rank, edges, EB, total, base, reg);
   else
     hipLaunchKernelGGL(asm_emit_kernel<int32_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
-                       stream, rec, (const int32_t*)st, P, C, rank, edges, EB, xtab, xtab_n, crit,
-                       y_exp, total, base);
+                       stream, rec, (const int32_t*)st, P, C, rank, edges, EB, total, base, reg);
   MT_HIP_CHECK(hipGetLastError());
 }
 

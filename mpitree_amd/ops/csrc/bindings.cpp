@@ -77,8 +77,7 @@ void launch_edges(hipStream_t, const void*, bool, int64_t, int, int, int, void*,
 void launch_asm_rank(hipStream_t, const int32_t*, int64_t, int32_t*, int64_t*, int32_t*);
 int64_t asm_node_bytes(int C, bool reg);
 void launch_asm_emit(hipStream_t, const int32_t*, const void*, bool, int64_t, int,
-                     const int32_t*, const double*, int, const double*, int, int, int,
-                     const int64_t*, uint8_t*);
+                     const int32_t*, const double*, int, const int64_t*, uint8_t*, bool);
 }  // namespace mt
 
 template <typename T>
@@ -321,11 +320,10 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("asm_node_bytes", &mt::asm_node_bytes);
   m.def("asm_emit", [](uintptr_t s, uintptr_t rec, uintptr_t st, bool st64, int64_t npos, int C,
-                       uintptr_t rank, uintptr_t edges, int EB, uintptr_t xtab, int xtab_n,
-                       int crit, int y_exp, uintptr_t total, uintptr_t base) {
+                       uintptr_t rank, uintptr_t edges, int EB, uintptr_t total, uintptr_t base,
+                       bool reg) {
     mt::launch_asm_emit(S(s), P<int32_t>(rec), P<void>(st), st64, npos, C, P<int32_t>(rank),
-                        P<double>(edges), EB, P<double>(xtab), xtab_n, crit, y_exp,
-                        P<int64_t>(total), P<uint8_t>(base));
+                        P<double>(edges), EB, P<int64_t>(total), P<uint8_t>(base), reg);
   });
   m.def("label_count", [](uintptr_t s, uintptr_t y, int64_t n, int64_t lo, int R,
                           uintptr_t counts, bool checked) {

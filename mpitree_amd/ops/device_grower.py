@@ -559,7 +559,7 @@ class DeviceGrower:
         t0 = time.perf_counter()
         if d_edges is None and not isinstance(edges, np.ndarray):
             edges = edges.padded_edges()
-        a = be.assemble_positions(edges, int(p.criterion), y_exp, d_edges=d_edges)
+        ta = be.assemble_positions(edges, int(p.criterion), y_exp, d_edges=d_edges)
         self.timings["assemble"] = time.perf_counter() - t0
         ev = getattr(self, "_sim_events", None)
         if ev is not None:
@@ -568,14 +568,4 @@ class DeviceGrower:
             self.stats["sim_rest_finisher_ms"] = ev[1].elapsed_time(ev[2])
             self._sim_events = None
         self._dp_keep = None
-        st = a["stats"]
-        ta = TreeArrays(
-            feature=a["feature"], threshold=a["threshold"], threshold_bin=a["bin"],
-            left=a["left"], right=a["right"], depth=a["depth"], n_samples=a["nsamp"],
-            impurity=a["impurity"], count=None if reg else st,
-            value=a["value"] if reg else None,
-        )
-        if reg:
-            ta.meta["sum_fixed"] = st[:, 1]
-        ta.meta["final"] = True
         return ta

@@ -16,6 +16,7 @@ import torch
 
 from ..core.binning import MAX_BINS_LIMIT, BinMapper, TableBinMapper
 from ..core.criterion import Criterion
+from ..models.tree_arrays import TreeArrays
 from . import native
 
 __all__ = ["HipBackend", "gpu_bin_features"]
@@ -508,13 +509,16 @@ class HipBackend:
         self.pos_rec.index_copy_(0, d_pos, d_rec.reshape(-1, 6).to(torch.int32))
         self.pos_st.index_copy_(0, d_pos, d_st.reshape(-1, self.C).to(self.pos_st.dtype))
 
-    def assemble_positions(self, edges, crit: int, y_exp: int = 0, d_edges=None) -> dict:
-        """Compact the position space into pre-ordered tree columns (numpy views
-        of one pinned host buffer). ``d_edges``: the device fp64 edge table
-        ``[F, W]`` (any row stride); otherwise ``edges`` (host ``[F, W]``) is
-        uploaded. Rank -> emit run back to back (the emit kernel lays the
-        columns out from the device node count), then two small host waits:
-        the node count, and the single D2H of the columns."""
+    def assemble_positions(self, edges, crit: int, y_exp: int = 0, d_edges=None) -> TreeArrays:
+        """Compact the position space into a pre-ordered :class:`TreeArrays`
+        (numpy views of one pinned host buffer). ``d_edges``: the device fp64
+        edge table ``[F, W]`` (any row stride); otherwise ``edges`` (host
+        ``[F, W]``) is uploaded. Rank -> emit run back to back (the emit kernel
+        lays the columns out from the device node count), then two small host
+        waits: the node count, and the single D2H of the columns. Only stats,
+        thresholds, feature, bin, right child and depth cross the link; left
+        children, node sizes, impurities, int64 counts and leaf values are
+        derived from them on first use (``TreeArrays.deferred``)."""
         P, C = self.P, self.C
         hip = self.hip
         s = _stream()
@@ -531,28 +535,30 @@ class HipBackend:
         total = ws[o_total : o_total + 8].view(torch.int64)
         hip.asm_rank(s, self.pos_rec.data_ptr(), P, base, base + o_total, base + o_rank)
         hip.asm_emit(s, self.pos_rec.data_ptr(), self.pos_st.data_ptr(), self.reg, P, C,
-                     base + o_rank, d_edges.data_ptr(), int(d_edges.stride(0)),
-                     self.xtab.data_ptr(), XTAB_N, int(crit), int(y_exp), base + o_total,
-                     base + o_out)
+                     base + o_rank, d_edges.data_ptr(), int(d_edges.stride(0)), base + o_total,
+                     base + o_out, bool(self.reg))
         h_total = _pinned_copy(total, "asm.total")
         torch.cuda.current_stream(self.device).synchronize()
         N = int(h_total[0])
-        host = torch.empty(max(N * bpn, 8), dtype=torch.uint8, pin_memory=True)
-        host[: N * bpn].copy_(ws[o_out : o_out + N * bpn], non_blocking=True)
+        sbytes = N * 16 if self.reg else (N * C * 4 + 7) // 8 * 8
+        nbytes = sbytes + N * 8 + N * 16
+        host = torch.empty(max(nbytes, 8), dtype=torch.uint8, pin_memory=True)
+        host[:nbytes].copy_(ws[o_out : o_out + nbytes], non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
-        cols8 = [("nsamp", torch.int64, 1), ("stats", torch.int64, C),
-                 ("threshold", torch.float64, 1), ("impurity", torch.float64, 1)]
+        h = host.numpy()
         if self.reg:
-            cols8.append(("value", torch.float64, 1))
-        cols4 = [(k, torch.int32, 1) for k in ("feature", "bin", "left", "right", "depth")]
-        out, o = {}, 0
-        for name, dt, w in cols8 + cols4:
-            nb = N * w * (8 if dt in (torch.int64, torch.float64) else 4)
-            t = host[o : o + nb].view(dt)
-            out[name] = (t.view(N, w) if (w > 1 or name == "stats") else t).numpy()
-            o += nb
+            stats = h[: N * 16].view(np.int64).reshape(N, 2)
+        else:
+            stats = h[: N * C * 4].view(np.int32).reshape(N, C)
+        o = sbytes
+        thr = h[o : o + N * 8].view(np.float64)
+        o += N * 8
+        i4 = h[o : o + N * 16].view(np.int32)
         self.pos_rec = self.pos_st = None
-        return out
+        return TreeArrays.from_device_columns(
+            stats=stats, threshold=thr, feature=i4[:N], threshold_bin=i4[N : 2 * N],
+            right=i4[2 * N : 3 * N], depth=i4[3 * N : 4 * N], criterion=int(crit),
+            regression=bool(self.reg), y_exp=int(y_exp))
 
     def launch_finisher(self, d_jobs, J: int, job_rows: int, params, rec, cnt, counter=None):
         """Launch the block + wave finisher kernels on ``J`` device jobs
