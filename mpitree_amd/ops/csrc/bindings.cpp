@@ -43,8 +43,8 @@ void launch_label_encode(hipStream_t, const int64_t*, int64_t, int64_t, const in
 void launch_finish(hipStream_t, const void*, int64_t, const void*, int, int64_t, uint32_t*,
                    uint32_t*, const int32_t*, int, const int64_t*, int, int32_t*, const int32_t*,
                    int, int, int, int, int, int64_t, int64_t, const double*, const float*, int,
-                   int32_t*,
-                   int32_t*, int32_t*, int, int, int64_t*, int, int64_t*);
+                   int32_t*, int32_t*, int64_t*, int32_t*, int32_t, int, int, int, int64_t*, int,
+                   int64_t*);
 int finish_lds_bytes(int F, int B, int C);
 int asm_tiles(int64_t P);
 void launch_grow_plan(hipStream_t, const PlanArgs&);
@@ -167,21 +167,23 @@ PYBIND11_MODULE(_hip, m) {
                      int lab_shift, uintptr_t jobs, int J, uintptr_t counter, uintptr_t nbins,
                      int F, int B, int C, int crit, int max_depth, int64_t mss, int64_t msl,
                      uintptr_t xtab, uintptr_t xtabf, int xtab_n, uintptr_t node_i32,
-                     uintptr_t node_cnt,
-                     uintptr_t job_nodes, int grid, int tiny_rows, uintptr_t tiny,
+                     uintptr_t node_cnt, uintptr_t tasks, uintptr_t task_flag, int epoch,
+                     int task_cap, int grid, int tiny_rows, uintptr_t tiny,
                      int tiny_grid, uintptr_t prof) {
     mt::launch_finish(S(s), P<void>(codes_rm), row_words, P<void>(codes_fm), cb, n_rows,
                       P<uint32_t>(idx), P<uint32_t>(tmp), P<int32_t>(y), lab_shift,
                       P<int64_t>(jobs), J, P<int32_t>(counter), P<int32_t>(nbins), F, B, C, crit,
                       max_depth, mss, msl, P<double>(xtab), P<float>(xtabf), xtab_n, P<int32_t>(node_i32),
-                      P<int32_t>(node_cnt), P<int32_t>(job_nodes), grid, tiny_rows,
+                      P<int32_t>(node_cnt), P<int64_t>(tasks), P<int32_t>(task_flag), epoch,
+                      task_cap, grid, tiny_rows,
                       P<int64_t>(tiny), tiny_grid, P<int64_t>(prof));
   }, py::arg("s"), py::arg("codes_rm"), py::arg("row_words"), py::arg("codes_fm"), py::arg("cb"),
      py::arg("n_rows"), py::arg("idx"), py::arg("tmp"), py::arg("y"), py::arg("lab_shift"),
      py::arg("jobs"), py::arg("J"), py::arg("counter"), py::arg("nbins"), py::arg("F"),
      py::arg("B"), py::arg("C"), py::arg("crit"), py::arg("max_depth"), py::arg("mss"),
      py::arg("msl"), py::arg("xtab"), py::arg("xtabf"), py::arg("xtab_n"), py::arg("node_i32"),
-     py::arg("node_cnt"), py::arg("job_nodes"), py::arg("grid"), py::arg("tiny_rows"),
+     py::arg("node_cnt"), py::arg("tasks"), py::arg("task_flag"), py::arg("epoch"),
+     py::arg("task_cap"), py::arg("grid"), py::arg("tiny_rows"),
      py::arg("tiny"), py::arg("tiny_grid"), py::arg("prof"));
   m.def("asm_tiles", &mt::asm_tiles);
   m.def("finish_reg_lds_bytes", &mt::finish_reg_lds_bytes);

@@ -30,12 +30,20 @@
 #include "common.h"
 #include "criterion.h"
 #include "tiny_sort.h"
+#include "grow.h"
 
 namespace mt {
 
 // threads per finisher workgroup: 512 (two per CU). A 1024-thread variant and an
 // in-kernel tiny-subtree queue were measured slower (profiles/kernel_experiments.md)
 constexpr int kFinThreadsSmall = 512;
+// job_counter words (int32 [kFinCounterWords], zeroed before each launch): the
+// claim cursor, the tiny-subtree count / cursor, the {completed, handed off}
+// queue word, the finished epoch and the watchdog each on their own 128-B line
+constexpr int kFinCtrTinyCount = 32;
+constexpr int kFinCtrQueue = 64;
+constexpr int kFinCtrFinished = 96;
+constexpr int kFinCtrWatch = 100;
 constexpr int kFinStack = 40;    // >= log2(max job rows) + 2
 constexpr int kFinMaxC = 16;     // classes supported by the finisher
 constexpr int kFinTab = 1024;    // LDS x*log2(x) entries
@@ -70,8 +78,9 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
     int32_t* __restrict__ job_counter, const int32_t* __restrict__ nbins, int F, int B, int C,
     int crit, int max_depth, int64_t mss, int64_t msl, const double* __restrict__ xtab,
     const float* __restrict__ xtabf, int xtab_n, int32_t* __restrict__ node_i32, int32_t* __restrict__ node_cnt,
-    int32_t* __restrict__ job_root, int tiny_rows,
-    int64_t* __restrict__ tiny, int32_t* __restrict__ tiny_count, int64_t* __restrict__ prof) {
+    int64_t* __restrict__ tasks, int32_t* __restrict__ task_flag, int32_t epoch, int task_cap,
+    int tiny_rows, int64_t* __restrict__ tiny, int32_t* __restrict__ tiny_count,
+    int64_t* __restrict__ prof) {
   // prof (optional): per workgroup {wall start, wall end, nodes, rows, cycles in
   // histogram, scan, partition, rest} -- the finisher's own phase profile
   constexpr int kFinWaves = kFinThreads / kWave;
@@ -265,19 +274,62 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
     wave_argmin_dpp(best_cost, best_bin);
   };
 
+  // Work queue: the J sorted jobs, then subtrees that running workgroups hand
+  // off while others idle (records in `tasks`, each published by an
+  // epoch-tagged flag). A workgroup claims the next index; an index past the
+  // published ones waits for its record or for the end of all work. One 64-bit
+  // word counts {completed tasks : 32, handed off : 32}; the work is over when
+  // completed == J + handed off (hand-offs only come from running tasks, so
+  // that cannot hold early), which the last completion sees in its own atomic
+  // and announces through q_finished. Waiters poll only their own flag and
+  // q_finished: lines nobody else keeps writing.
+  unsigned long long* const q_word =
+      reinterpret_cast<unsigned long long*>(job_counter + kFinCtrQueue);
+  int32_t* const q_finished = job_counter + kFinCtrFinished;
   for (;;) {
-    if (tid == 0) s_job = atomicAdd(job_counter, 1);
+    if (tid == 0) {
+      const int h = atomicAdd(job_counter, 1);
+      int got = h;
+      if (!kC2 || task_cap < 0) {  // the queue drives the two-class kernel only
+        if (h >= J) got = -1;
+      } else if (h >= J) {
+        // Waiting is cheap and bounded: relaxed loads that bypass L1 (no cache
+        // invalidation while co-resident workgroups work), one acquire fence
+        // once the record is there, and a wall-clock watchdog that reports
+        // through job_counter[6..7] instead of ever hanging the GPU.
+        const uint64_t t_start = wall_clock64();
+        for (uint32_t spins = 0;; ++spins) {
+          if (h - J < task_cap &&
+              __hip_atomic_load(task_flag + (h - J), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                  epoch) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            break;
+          }
+          if (__hip_atomic_load(q_finished, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) {
+            got = -1;
+            break;
+          }
+          if ((spins & 15u) == 15u && wall_clock64() - t_start > 500000000ull) {  // 5 s
+            atomicExch(job_counter + kFinCtrWatch, 1);
+            got = -1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(32);
+        }
+      }
+      s_job = got;
+    }
     __syncthreads();
     const int job = s_job;
-    if (job >= J) break;
+    if (job < 0) break;
     if (prof && tid == 0) s_pr[8] = (int64_t)clock64();
-    const int64_t* jb = jobs + (int64_t)job * JW;
+    const int64_t* jb =
+        (!kC2 || job < J) ? jobs + (int64_t)job * JW : tasks + (int64_t)(job - J) * JW;
     int32_t* ni = node_i32;  // indexed by pre-order position (see launch_finish)
     int32_t* nc = node_cnt;
     if (tid == 0) {
       const int r = (int)jb[3];
       s_root = r;
-      job_root[job] = r;
       s_sp = 1;
       s_st_start[0] = jb[0];
       s_st_count[0] = (int32_t)jb[1];
@@ -653,12 +705,42 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         int32_t* Rr = ni + (int64_t)rid * 6;
         L[0] = -1; L[1] = -1; L[2] = -1; L[3] = -1; L[4] = cd; L[5] = nl;
         Rr[0] = -1; Rr[1] = -1; Rr[2] = -1; Rr[3] = -1; Rr[4] = cd; Rr[5] = nr;
-        // push the larger child first so the smaller one is processed next
+        // push the larger child first so the smaller one is processed next --
+        // or hand the larger one to an idle workgroup (claims past the
+        // published work) when it is worth a workgroup
         const bool left_small = nl <= nr;
         for (int pass = 0; pass < 2; ++pass) {
           const bool is_left = (pass == 0) ? !left_small : left_small;
           if (is_left ? tlf : trf) continue;
           const int cm_rows = is_left ? nl : nr;
+          if (kC2 && pass == 0 && cm_rows > 2 * tiny_rows) {
+            const int head = __hip_atomic_load(job_counter, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+            const int pushed = (int)(__hip_atomic_load(q_word, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT) >> 32);
+            if (head > J + pushed && pushed < task_cap) {
+              const int k = (int)(__hip_atomic_fetch_add(q_word, 1ull << 32, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) >> 32);
+              if (k < task_cap) {
+                int64_t* T = tasks + (int64_t)k * JW;
+                T[0] = is_left ? start : start + nl;
+                T[1] = cm_rows;
+                T[2] = cd;
+                T[3] = is_left ? lid : rid;
+                T[4] = s_buf ^ 1;
+                for (int c = 0; c < C; ++c) T[5 + c] = is_left ? s_left[c] : s_cnt[c] - s_left[c];
+                // the child's rows (this workgroup's partition) and record are
+                // visible chip-wide before the flag (agent-scope release)
+                __threadfence();
+                __hip_atomic_store(task_flag + k, epoch, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                continue;
+              }
+              // (over capacity: the counter overshoot is undone below)
+              __hip_atomic_fetch_add(q_word, ~0ull << 32, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
           if (cm_rows <= tiny_rows) {  // hand the tiny subtree to a wavefront
             const int64_t t = atomicAdd(tiny_count, 1);
             int64_t* tr = tiny + t * 8;
@@ -682,6 +764,15 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
       __syncthreads();
     }
     mark(3);
+    if (kC2 && tid == 0) {
+      // the completion that brings {completed, handed off} to completed == J +
+      // handed off is the last one (no task runs, so none can be handed off):
+      // it releases the waiting workgroups
+      const unsigned long long q =
+          __hip_atomic_fetch_add(q_word, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((int)(uint32_t)q + 1 == J + (int)(q >> 32))
+        __hip_atomic_store(q_finished, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   if (prof && tid == 0) {
     int64_t* P = prof + (int64_t)blockIdx.x * 10;
@@ -1336,8 +1427,9 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                    int32_t* counter, const int32_t* nbins, int F, int B, int C, int crit,
                    int max_depth, int64_t mss, int64_t msl, const double* xtab,
                    const float* xtabf, int xtab_n,
-                   int32_t* node_i32, int32_t* node_cnt, int32_t* job_root, int grid,
-                   int tiny_rows, int64_t* tiny, int tiny_grid, int64_t* prof) {
+                   int32_t* node_i32, int32_t* node_cnt, int64_t* tasks, int32_t* task_flag,
+                   int32_t epoch, int task_cap, int grid, int tiny_rows, int64_t* tiny,
+                   int tiny_grid, int64_t* prof) {
   // counter: int32 [8] = {job cursor, tiny count, tiny cursor, -...}, zeroed by the
   // host. node_i32 / node_cnt are indexed by pre-order position (jobs[j][3] is
   // job j's root position); rows a fit never writes keep n = 0 (host memset).
@@ -1354,8 +1446,9 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   hipLaunchKernelGGL((finish_cls_kernel<CT, C2, NT>), dim3(grid), dim3(NT), lds, stream,      \
                      (const uint32_t*)codes_rm, row_words, (const CT*)codes_fm, n_rows, buf0, \
                      buf1, y, rl, jobs, J, counter, nbins, F, B, C, crit, max_depth, mss,     \
-                     msl, xtab, xtabf, xtab_n, node_i32, node_cnt, job_root, tiny_rows,       \
-                     tiny, counter + 1, prof);
+                     msl, xtab, xtabf, xtab_n, node_i32, node_cnt, tasks, task_flag, epoch,   \
+                     task_cap, tiny_rows,                                                     \
+                     tiny, counter + kFinCtrTinyCount, prof);
 #define MT_FIN(CT, C2) MT_FIN_NT(CT, C2, kFinThreadsSmall)
   if (code_bytes == 1) {
     if (C <= 2) {
@@ -1381,12 +1474,14 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       hipLaunchKernelGGL(finish_tiny_sorted_kernel, dim3(tiny_grid), dim3(kTinyWaves * kWave),
                          lds, stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl,
-                         tiny, counter + 1, counter + 2, F, C, crit, max_depth, mss, msl, xtab,
+                         tiny, counter + kFinCtrTinyCount, counter + kFinCtrTinyCount + 1, F, C,
+                         crit, max_depth, mss, msl, xtab,
                          node_i32, node_cnt);
     } else {
       hipLaunchKernelGGL(finish_tiny_kernel, dim3(tiny_grid), dim3(kTinyWaves * kWave), 0,
                          stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,
-                         counter + 1, counter + 2, F, C, crit, max_depth, mss, msl, xtab,
+                         counter + kFinCtrTinyCount, counter + kFinCtrTinyCount + 1, F, C, crit,
+                         max_depth, mss, msl, xtab,
                          node_i32, node_cnt);
     }
     MT_HIP_CHECK(hipGetLastError());

@@ -5,6 +5,11 @@
 
 namespace mt {
 
+// The finisher's int32 work counters; words that different workgroups update
+// concurrently sit on separate 128-byte lines (see finish.hip).
+constexpr int kFinCounterWords = 128;
+
+
 // Level work lists (one set per level parity). ctl: int32
 // {0: K frontier nodes, 1: built nodes, 2: hist items, 3: slab reductions,
 //  4: derive triples, 5: split nodes, 6: partition items, 7: reduction tasks,

@@ -635,7 +635,7 @@ __global__ __launch_bounds__(1024) void job_sort_kernel(const int64_t* __restric
     }
     key[i] = k;
   }
-  if (threadIdx.x < 8) counters[threadIdx.x] = 0;
+  if (threadIdx.x < kFinCounterWords) counters[threadIdx.x] = 0;
   __syncthreads();
   for (int size = 2; size <= N2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {

@@ -392,7 +392,7 @@ class DeviceGrower:
                     jobs=torch.empty((JMAX, W), **i64),
                     jobs_sorted=torch.empty((min(JMAX, hip.job_sort_max()), W), **i64),
                     job_count=torch.zeros(1, dtype=torch.int32, device=dev),
-                    fin_counter=torch.zeros(8, dtype=torch.int32, device=dev),
+                    fin_counter=torch.zeros(128, dtype=torch.int32, device=dev),
                     root=torch.empty(4 if reg else C, **i64),
                     root_host=torch.empty(4 if reg else C, dtype=torch.int64, pin_memory=True),
                 )

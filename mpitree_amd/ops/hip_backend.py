@@ -283,6 +283,22 @@ def xlog2x_table(device) -> torch.Tensor:
 _pinned: dict = {}
 
 
+_TASK_FLAGS: dict = {}  # device -> [int32 flag tensor, epoch]
+_FIN_WATCH: list = []  # pinned views of finisher watchdog words, checked at assembly
+
+
+def _task_flags(device, n: int):
+    """Epoch-tagged publish flags of the finisher's hand-off queue: a flag is
+    set when it equals this launch's epoch, so the buffer is never cleared
+    between launches (zeroed once when it grows)."""
+    key = str(device)
+    ent = _TASK_FLAGS.get(key)
+    if ent is None or ent[0].numel() < n:
+        ent = _TASK_FLAGS[key] = [torch.zeros(max(n, 4096), dtype=torch.int32, device=device), 0]
+    ent[1] = ent[1] % 0x7FFFFFFE + 1
+    return ent[0], ent[1]
+
+
 def _pinned_copy(t: torch.Tensor, key: str) -> np.ndarray:
     """Start an async D2H copy of ``t`` into a reusable pinned buffer; returns
     the numpy view (valid after the stream is synchronised). Buffers grow
@@ -539,6 +555,7 @@ class HipBackend:
                      base + o_out, bool(self.reg))
         h_total = _pinned_copy(total, "asm.total")
         torch.cuda.current_stream(self.device).synchronize()
+        self._check_finisher_watch()
         N = int(h_total[0])
         sbytes = N * 16 if self.reg else (N * C * 4 + 7) // 8 * 8
         nbytes = sbytes + N * 8 + N * 16
@@ -560,6 +577,15 @@ class HipBackend:
             right=i4[2 * N : 3 * N], depth=i4[3 * N : 4 * N], criterion=int(crit),
             regression=bool(self.reg), y_exp=int(y_exp))
 
+    def _check_finisher_watch(self):
+        watch = list(_FIN_WATCH)
+        _FIN_WATCH.clear()
+        for w in watch:
+            if int(w[0]) != 0:
+                raise RuntimeError(
+                    "subtree finisher: a workgroup's wait for handed-off work timed out "
+                    "; the tree is incomplete")
+
     def launch_finisher(self, d_jobs, J: int, job_rows: int, params, rec, cnt, counter=None):
         """Launch the block + wave finisher kernels on ``J`` device jobs
         (int64 [J][5 + C] = {start, count, depth, root position, buffer, counts},
@@ -568,17 +594,27 @@ class HipBackend:
             return
         C = self.C
         if counter is None:  # eight int32 work cursors, zero at launch
-            counter = torch.zeros(8, dtype=torch.int32, device=self.device)
+            counter = torch.zeros(128, dtype=torch.int32, device=self.device)
         if self.reg:
             self._launch_finisher_reg(d_jobs, J, job_rows, params, rec, cnt, counter)
             return
-        job_root = torch.empty(J, dtype=torch.int32, device=self.device)
         tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
         # every tiny subtree has >= 2 rows and they partition the job rows
         tiny = torch.empty((int(job_rows // 2 + J + 1), 8), dtype=torch.int64,
                            device=self.device)
         md = -1 if params.max_depth is None else int(params.max_depth)
-        grid = int(min(J, int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU))))
+        grid = int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU))
+        if C > 2:  # (the hand-off queue is on the two-class kernel only)
+            grid = min(grid, J)
+        # subtrees handed to idle workgroups (each > 2 tiny_rows rows, disjoint)
+        task_cap = int(job_rows // (2 * max(tiny_rows, 1) + 1) + 16)
+        steal = os.environ.get("MPITREE_FIN_STEAL", "1" if C <= 2 else "-1")
+        if steal == "0":
+            task_cap = 0  # no hand-offs: spare workgroups only wait for the end
+        elif steal == "-1":
+            task_cap = -1  # no queue at all (claims past the jobs exit at once)
+        tasks = torch.empty((max(task_cap, 1), 5 + C), dtype=torch.int64, device=self.device)
+        flags, epoch = _task_flags(self.device, max(task_cap, 0) + grid)
         prof = None
         if os.environ.get("MPITREE_FIN_PROF"):
             prof = torch.zeros((grid, 10), dtype=torch.int64, device=self.device)
@@ -589,10 +625,14 @@ class HipBackend:
                         int(self.crit), md, int(params.min_samples_split),
                         int(max(1, params.min_samples_leaf)), self.xtab.data_ptr(),
                         self.xtabf.data_ptr(), XTAB_N,
-                        rec.data_ptr(), cnt.data_ptr(), job_root.data_ptr(), grid,
-                        tiny_rows, tiny.data_ptr(), 4 * N_CU,
+                        rec.data_ptr(), cnt.data_ptr(), tasks.data_ptr(), flags.data_ptr(),
+                        epoch, task_cap, grid, tiny_rows, tiny.data_ptr(), 4 * N_CU,
                         0 if prof is None else prof.data_ptr())
-        self._fin_keep = (counter, job_root, tiny, d_jobs)
+        self._fin_keep = (counter, tasks, tiny, d_jobs)
+        # the hand-off queue's watchdog word (+ completed tasks), read
+        # with the assembly's node-count sync: a finisher that gave up waiting
+        # must fail the fit, never leave holes in the tree
+        _FIN_WATCH.append(_pinned_copy(counter[100:101], f"fin.watch{len(_FIN_WATCH)}"))
         if prof is not None:
             self.last_finisher_prof = prof.cpu().numpy()
 
