@@ -346,7 +346,14 @@ def fit_tree(
         from ..ops.device_grower import DeviceGrower, device_loop_supported
 
         ckpt = _level_checkpoint(checkpoint, codes_rm, yd, params, C)
-        if ckpt is None and device_loop_supported(be, params, comm):
+        if ckpt is None and (lo, hi) == (0, n) and be.small_fit_supported(comm):
+            # <= 1024 rows: the whole tree in one workgroup, any class count
+            edges_h = None if prep.d_edges64 is not None else mapper.padded_edges()
+            with roctx_range("mpitree.grow"):
+                ta = be.fit_small(params, edges_h, d_edges=prep.d_edges64)
+            eng = "hip-small"
+            stats = {}
+        elif ckpt is None and device_loop_supported(be, params, comm):
             if comm.world_size > 1:  # the redundant top levels use the 1-GPU split point
                 params.finisher_rows = min(default_fr, be.max_finisher_rows)
             builder = DeviceGrower(be, params, comm)
@@ -359,8 +366,9 @@ def fit_tree(
             with roctx_range("mpitree.grow"):
                 ta = builder.fit(hi - lo, C, F, edges=mapper.padded_edges(), y_exp=y_exp)
             eng = "hip-levelwise"
-        timings.update(builder.timings)
-        stats = dict(builder.stats)
+        if eng != "hip-small":
+            timings.update(builder.timings)
+            stats = dict(builder.stats)
     else:
         Xh = X.cpu().numpy() if _is_tensor(X) else X
         if _is_tensor(X) and X.is_cuda and not np.isfinite(Xh).all():

@@ -76,6 +76,10 @@ void launch_edges(hipStream_t, const void*, bool, int64_t, int, int, int, void*,
                   uint8_t*, double*);
 void launch_asm_rank(hipStream_t, const int32_t*, int64_t, int32_t*, int64_t*, int32_t*);
 int64_t asm_node_bytes(int C, bool reg);
+int small_fit_max_rows();
+void launch_small_fit(hipStream_t, const void*, int, int64_t, int, int, const int32_t*, int, int,
+                      int, int64_t, int64_t, const double*, int, uint16_t*, int32_t*, int32_t*,
+                      int64_t);
 void launch_asm_emit(hipStream_t, const int32_t*, const void*, bool, int64_t, int,
                      const int32_t*, const double*, int, const int64_t*, uint8_t*, bool);
 }  // namespace mt
@@ -186,6 +190,15 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("task_cap"), py::arg("grid"), py::arg("tiny_rows"),
      py::arg("tiny"), py::arg("tiny_grid"), py::arg("prof"));
   m.def("asm_tiles", &mt::asm_tiles);
+  m.def("small_fit_max_rows", &mt::small_fit_max_rows);
+  m.def("small_fit", [](uintptr_t s, uintptr_t codes_fm, int cb, int64_t n_stride, int n, int F,
+                        uintptr_t y, int C, int crit, int max_depth, int64_t mss, int64_t msl,
+                        uintptr_t xtab, int xtab_n, uintptr_t ord, uintptr_t node_i32,
+                        uintptr_t node_cnt, int64_t npos) {
+    mt::launch_small_fit(S(s), P<void>(codes_fm), cb, n_stride, n, F, P<int32_t>(y), C, crit,
+                         max_depth, mss, msl, P<double>(xtab), xtab_n, P<uint16_t>(ord),
+                         P<int32_t>(node_i32), P<int32_t>(node_cnt), npos);
+  });
   m.def("finish_reg_lds_bytes", &mt::finish_reg_lds_bytes);
   m.def("finish_reg", [](uintptr_t s, uintptr_t codes_rm, int64_t row_words, uintptr_t codes_fm,
                          int cb, int64_t n_rows, uintptr_t buf0, uintptr_t buf1, uintptr_t y,

@@ -577,6 +577,28 @@ class HipBackend:
             right=i4[2 * N : 3 * N], depth=i4[3 * N : 4 * N], criterion=int(crit),
             regression=bool(self.reg), y_exp=int(y_exp))
 
+    def small_fit_supported(self, comm=None) -> bool:
+        """One-workgroup whole-tree fit (``small_fit.hip``): classification on
+        at most 1024 rows, any number of classes (the reference's published
+        n-class sweep), one process."""
+        return (not self.reg and self.n <= int(self.hip.small_fit_max_rows())
+                and self.C < 65536 and getattr(comm, "world_size", 1) == 1
+                and os.environ.get("MPITREE_SMALL_FIT", "1") != "0")
+
+    def fit_small(self, params, edges, d_edges=None) -> TreeArrays:
+        """Grow the whole tree in one launch and assemble it (one sync)."""
+        n, F, C = self.n, self.F, self.C
+        self.begin_positions(max(2 * n - 1, 1))
+        ord_buf = _workspace(self.device, "small.ord", 2 * 2 * (F + 1) * max(n, 1))
+        md = -1 if params.max_depth is None else int(params.max_depth)
+        self.hip.small_fit(_stream(), self.codes_fm.data_ptr(), self.cb,
+                           int(self.codes_fm.stride(0)), n, F, self.y.data_ptr(), C,
+                           int(self.crit), md,
+                           int(params.min_samples_split), int(max(1, params.min_samples_leaf)),
+                           self.xtab.data_ptr(), XTAB_N, ord_buf.data_ptr(),
+                           self.pos_rec.data_ptr(), self.pos_st.data_ptr(), self.P)
+        return self.assemble_positions(edges, int(self.crit), 0, d_edges=d_edges)
+
     def _check_finisher_watch(self):
         watch = list(_FIN_WATCH)
         _FIN_WATCH.clear()

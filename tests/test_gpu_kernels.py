@@ -118,6 +118,7 @@ def test_gpu_finisher_matches_oracle(monkeypatch, rows, crit):
 def test_gpu_finisher_deep_chain(monkeypatch):
     # a fully grown tree whose splits peel one row at a time (deep, skinny)
     monkeypatch.setenv("MPITREE_FINISHER_ROWS", "1000")
+    monkeypatch.setenv("MPITREE_SMALL_FIT", "0")  # (600 rows: the finisher, not small_fit)
     n = 600
     X = np.arange(n, dtype=np.float64).reshape(-1, 1)
     y = np.arange(n) % 7
@@ -409,3 +410,36 @@ def test_gpu_exact_engine_device_tensors_and_quantile_optin():
     assert acc > 0.9
     q = DecisionTreeClassifier(max_depth=10, max_bins=256, device="cuda").fit(X, y)
     assert q.fit_stats_["engine"].startswith("hip-") and q.fit_stats_["engine"] != "hip-exact"
+
+
+@pytest.mark.parametrize("shape", [(2, 1, 2), (7, 3, 3), (150, 4, 3), (241, 1, 241), (600, 5, 40),
+                                   (1024, 9, 2), (1000, 2, 300)])
+@pytest.mark.parametrize("crit", ["entropy", "gini"])
+@pytest.mark.parametrize("md_msl", [(None, 1), (3, 1), (None, 4)])
+def test_gpu_small_fit_matches_host(shape, crit, md_msl):
+    """<= 1024 rows: the one-workgroup whole-tree kernel (small_fit.hip) builds
+    the host builder's tree bit for bit, for any class count."""
+    n, F, C = shape
+    md, msl = md_msl
+    rng = np.random.default_rng(n * 31 + F * 7 + C)
+    X = rng.integers(0, max(3, min(n // 3, 250)), size=(n, F)).astype(np.float32)
+    y = (X[:, 0].astype(np.int64) * 7 + rng.integers(0, 3, size=n)) % C
+    kw = dict(criterion=crit, max_depth=md, min_samples_leaf=msl)
+    g = DecisionTreeClassifier(device="cuda", **kw).fit(X, y)
+    assert g.fit_stats_["engine"] == "hip-small"
+    h = DecisionTreeClassifier(device="cpu", **kw).fit(X, y)
+    assert g.tree_arrays_.equal(h.tree_arrays_)
+    assert g.export_text(precision=17) == h.export_text(precision=17)
+    np.testing.assert_array_equal(g.predict(X), h.predict(X))
+
+
+def test_gpu_published_sweep_workload():
+    """The reference's published benchmark (experiments.ipynb:198-209): one
+    feature, n rows, n classes -- on the GPU, equal to the CPU tree."""
+    for n in (1, 11, 121, 241):
+        X = np.arange(n, dtype=np.float64).reshape(-1, 1)
+        y = np.arange(n)
+        g = DecisionTreeClassifier(device="cuda").fit(X, y)
+        h = DecisionTreeClassifier(device="cpu").fit(X, y)
+        assert g.tree_arrays_.equal(h.tree_arrays_), n
+        assert g.tree_arrays_.n_leaves == n
