@@ -333,8 +333,12 @@ def fit_tree(
                  criterion=crit)
         be.timing = profiling()  # synchronised per-phase timers (host-driven loop)
         env = os.environ.get("MPITREE_FINISHER_ROWS")
-        # ~2 subtree jobs per workgroup slot of the finisher grid
-        default_fr = int(env) if env else max(2048, n // 512)
+        # subtree jobs of up to n / 128 rows: idle finisher workgroups split big
+        # jobs between them (hand-off queue), so fewer replicated levels win
+        # (profiles/kernel_experiments.md: 1M x 64 3.52 -> 3.33 ms at 2048 -> 8192)
+        # (the regression finisher has no hand-off queue: smaller jobs balance it)
+        default_fr = int(env) if env else (max(2048, n // 512) if regression
+                                           else max(2048, min(n // 128, 32768)))
         if finisher_rows is None or (comm.world_size > 1 and comm.kind == "data"):
             # data-parallel GPU ranks finish subtrees on their owners (rows sent
             # there first), so the finisher applies as on one GPU
