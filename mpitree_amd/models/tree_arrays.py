@@ -119,6 +119,7 @@ class TreeArrays:
             ta = cls.deferred(derive, feature=feature, threshold=threshold,
                               threshold_bin=threshold_bin, right=right, depth=depth, value=None)
         ta.meta["final"] = True  # thresholds, impurity and values need no host pass
+        ta.meta["stats_raw"] = stats  # (the cross-rank digest hashes what was transferred)
         return ta
 
     # ------------------------------------------------------------------ basics

@@ -70,7 +70,11 @@ def tree_digest(ta) -> int:
     disagree on bin edges (e.g. row shards binned apart) cannot match.
     xxh3 over the arrays in place: ~0.3 ms for 200k nodes."""
     thr = np.nan_to_num(np.asarray(ta.threshold, dtype=np.float64), nan=0.0)
-    parts = (ta.feature, ta.threshold_bin, ta.left, ta.right, ta.n_samples, thr)
+    raw = ta.meta.get("stats_raw") if isinstance(getattr(ta, "meta", None), dict) else None
+    if raw is not None:  # device-assembled tree: its transferred columns determine the rest
+        parts = (ta.feature, ta.threshold_bin, ta.right, raw, thr)
+    else:
+        parts = (ta.feature, ta.threshold_bin, ta.left, ta.right, ta.n_samples, thr)
     try:
         import xxhash
 
