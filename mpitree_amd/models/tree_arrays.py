@@ -73,17 +73,26 @@ class TreeArrays:
 
     @classmethod
     def from_device_columns(cls, *, stats, threshold, feature, threshold_bin, right, depth,
-                            criterion: int, regression: bool, y_exp: int = 0) -> "TreeArrays":
+                            criterion: int, regression: bool, y_exp: int = 0,
+                            edges_table=None) -> "TreeArrays":
         """The device assembly's columns (``ops/csrc/assemble.hip``): class
         counts (int32) or regression {count, fixed-point sum} (int64), split
         thresholds, features, bins, right children and depths in pre-order.
         Left children (pre-order: node + 1), node sizes, int64 counts,
         impurities and regression leaf values follow from them and are computed
         on first use with the same integer-form criterion as every builder
-        (``core/criterion.py``, bitwise equal to the device's)."""
+        (``core/criterion.py``, bitwise equal to the device's). ``threshold``
+        None: split values come from ``edges_table[feature, bin]`` (the host's
+        padded edge table, the values the device table holds) on first use."""
         from ..core import criterion as cr
 
         N = int(feature.shape[0])
+
+        def threshold_from_edges(t):
+            out = np.full(N, np.nan)
+            inner = t.feature >= 0
+            out[inner] = edges_table[t.feature[inner], t.threshold_bin[inner]]
+            return out
 
         def left(t):
             return np.where(t.feature >= 0, np.arange(1, N + 1, dtype=np.int32),
@@ -99,8 +108,8 @@ class TreeArrays:
 
             derive = {"left": left, "n_samples": n_samples, "value": value,
                       "impurity": lambda t: np.full(N, np.nan)}
-            ta = cls.deferred(derive, feature=feature, threshold=threshold,
-                              threshold_bin=threshold_bin, right=right, depth=depth, count=None)
+            ta = cls.deferred(derive, feature=feature, threshold_bin=threshold_bin, right=right,
+                              depth=depth, count=None)
             ta.meta["sum_fixed"] = stats[:, 1]
         else:
             def n_samples(t):
@@ -116,8 +125,13 @@ class TreeArrays:
 
             derive = {"left": left, "n_samples": n_samples, "impurity": impurity,
                       "count": lambda t: stats.astype(np.int64)}
-            ta = cls.deferred(derive, feature=feature, threshold=threshold,
-                              threshold_bin=threshold_bin, right=right, depth=depth, value=None)
+            ta = cls.deferred(derive, feature=feature, threshold_bin=threshold_bin, right=right,
+                              depth=depth, value=None)
+        if threshold is not None:
+            ta.__dict__["threshold"] = threshold
+        else:
+            ta.__dict__["_derive"]["threshold"] = threshold_from_edges
+            ta.meta["edges_table"] = edges_table
         ta.meta["final"] = True  # thresholds, impurity and values need no host pass
         ta.meta["stats_raw"] = stats  # (the cross-rank digest hashes what was transferred)
         return ta

@@ -107,11 +107,12 @@ __global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __
 // from the device (asm_offsets_kernel's total), so the emit launch needs no
 // host round trip. Only what the host cannot derive cheaply crosses the link:
 //   stats [N][C] (int32 class counts; regression int64 {count, fixed sum})
-//   | threshold f64 [N] | feature, bin, right, depth i32 [N]
+//   | threshold f64 [N] (only when the host has no edge table: the exact
+//   engine's unique values stay on the device) | feature, bin, right, depth i32 [N]
 // Left children are implicit in pre-order (node j + 1), node sizes are the
 // stats' sums, impurities and leaf values follow from the stats with the same
 // integer-form criterion: the host derives those columns on first use
-// (TreeArrays.deferred). 32 B per node for a two-class tree instead of 60.
+// (TreeArrays.deferred). 24 B per node for a two-class tree instead of 60.
 struct AsmCols {
   void* stats;
   double* threshold;
@@ -121,12 +122,12 @@ struct AsmCols {
   int32_t* depth;
 };
 
-__device__ inline AsmCols asm_cols(uint8_t* base, int64_t N, int C, bool reg) {
+__device__ inline AsmCols asm_cols(uint8_t* base, int64_t N, int C, bool reg, bool thr) {
   AsmCols o;
   o.stats = base;
   const int64_t sbytes = reg ? N * 16 : ((N * C * 4 + 7) & ~(int64_t)7);
-  o.threshold = reinterpret_cast<double*>(base + sbytes);
-  int32_t* p4 = reinterpret_cast<int32_t*>(o.threshold + N);
+  o.threshold = thr ? reinterpret_cast<double*>(base + sbytes) : nullptr;
+  int32_t* p4 = reinterpret_cast<int32_t*>(base + sbytes + (thr ? N * 8 : 0));
   o.feature = p4;
   o.bin = p4 + N;
   o.right = p4 + 2 * N;
@@ -139,12 +140,12 @@ template <typename StatT>
 __global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
     const int32_t* __restrict__ rec, const StatT* __restrict__ st, int64_t P, int C,
     const int32_t* __restrict__ rank, const double* __restrict__ edges, int EB,
-    const int64_t* __restrict__ total, uint8_t* __restrict__ base, bool reg) {
+    const int64_t* __restrict__ total, uint8_t* __restrict__ base, bool reg, bool thr) {
   const int64_t p = (int64_t)blockIdx.x * kAsmThreads + threadIdx.x;
   if (p >= P) return;
   const int j = rank[p];
   if (j < 0) return;
-  const AsmCols o = asm_cols(base, *total, C, reg);
+  const AsmCols o = asm_cols(base, *total, C, reg, thr);
   const int32_t* R = rec + p * 6;
   const int f = R[0];
   const int b = R[1];
@@ -153,11 +154,11 @@ __global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
   if (f >= 0) {
     o.bin[j] = b;
     o.right[j] = rank[R[3]];
-    o.threshold[j] = edges[(int64_t)f * EB + b];
+    if (thr) o.threshold[j] = edges[(int64_t)f * EB + b];
   } else {
     o.bin[j] = -1;
     o.right[j] = -1;
-    o.threshold[j] = __builtin_nan("");
+    if (thr) o.threshold[j] = __builtin_nan("");
   }
   const StatT* s = st + p * C;
   if (reg) {
@@ -189,15 +190,17 @@ int64_t asm_node_bytes(int C, bool reg) { return (reg ? 16 : 4 * C) + 8 + 4 * 4 
 
 void launch_asm_emit(hipStream_t stream, const int32_t* rec, const void* st, bool st64,
                      int64_t P, int C, const int32_t* rank, const double* edges, int EB,
-                     const int64_t* total, uint8_t* base, bool reg) {
+                     const int64_t* total, uint8_t* base, bool reg, bool thr) {
   const int64_t blocks = (P + kAsmThreads - 1) / kAsmThreads;
   if (blocks == 0) return;
   if (st64)
     hipLaunchKernelGGL(asm_emit_kernel<int64_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
-                       stream, rec, (const int64_t*)st, P, C, rank, edges, EB, total, base, reg);
+                       stream, rec, (const int64_t*)st, P, C, rank, edges, EB, total, base, reg,
+                       thr);
   else
     hipLaunchKernelGGL(asm_emit_kernel<int32_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
-                       stream, rec, (const int32_t*)st, P, C, rank, edges, EB, total, base, reg);
+                       stream, rec, (const int32_t*)st, P, C, rank, edges, EB, total, base, reg,
+                       thr);
   MT_HIP_CHECK(hipGetLastError());
 }
 

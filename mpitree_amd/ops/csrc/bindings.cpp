@@ -81,7 +81,7 @@ void launch_small_fit(hipStream_t, const void*, int, int64_t, int, int, const in
                       int, int64_t, int64_t, const double*, int, uint16_t*, int32_t*, int32_t*,
                       int64_t);
 void launch_asm_emit(hipStream_t, const int32_t*, const void*, bool, int64_t, int,
-                     const int32_t*, const double*, int, const int64_t*, uint8_t*, bool);
+                     const int32_t*, const double*, int, const int64_t*, uint8_t*, bool, bool);
 }  // namespace mt
 
 template <typename T>
@@ -336,9 +336,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("asm_node_bytes", &mt::asm_node_bytes);
   m.def("asm_emit", [](uintptr_t s, uintptr_t rec, uintptr_t st, bool st64, int64_t npos, int C,
                        uintptr_t rank, uintptr_t edges, int EB, uintptr_t total, uintptr_t base,
-                       bool reg) {
+                       bool reg, bool thr) {
     mt::launch_asm_emit(S(s), P<int32_t>(rec), P<void>(st), st64, npos, C, P<int32_t>(rank),
-                        P<double>(edges), EB, P<int64_t>(total), P<uint8_t>(base), reg);
+                        P<double>(edges), EB, P<int64_t>(total), P<uint8_t>(base), reg, thr);
   });
   m.def("label_count", [](uintptr_t s, uintptr_t y, int64_t n, int64_t lo, int R,
                           uintptr_t counts, bool checked) {

@@ -557,9 +557,11 @@ class DeviceGrower:
         self.stats["levels"] = levels
         self.stats["finisher_subtrees"] = J
         t0 = time.perf_counter()
-        if d_edges is None and not isinstance(edges, np.ndarray):
-            edges = edges.padded_edges()
-        ta = be.assemble_positions(edges, int(p.criterion), y_exp, d_edges=d_edges)
+        # the host edge table: thresholds are derived from it on first use
+        # instead of crossing the link (8 B per node)
+        table = edges if isinstance(edges, np.ndarray) else edges.padded_edges()
+        ta = be.assemble_positions(table, int(p.criterion), y_exp, d_edges=d_edges,
+                                   host_table=table)
         self.timings["assemble"] = time.perf_counter() - t0
         ev = getattr(self, "_sim_events", None)
         if ev is not None:

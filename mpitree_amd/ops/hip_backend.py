@@ -525,7 +525,8 @@ class HipBackend:
         self.pos_rec.index_copy_(0, d_pos, d_rec.reshape(-1, 6).to(torch.int32))
         self.pos_st.index_copy_(0, d_pos, d_st.reshape(-1, self.C).to(self.pos_st.dtype))
 
-    def assemble_positions(self, edges, crit: int, y_exp: int = 0, d_edges=None) -> TreeArrays:
+    def assemble_positions(self, edges, crit: int, y_exp: int = 0, d_edges=None,
+                           host_table=None) -> TreeArrays:
         """Compact the position space into a pre-ordered :class:`TreeArrays`
         (numpy views of one pinned host buffer). ``d_edges``: the device fp64
         edge table ``[F, W]`` (any row stride); otherwise ``edges`` (host
@@ -534,11 +535,13 @@ class HipBackend:
         waits: the node count, and the single D2H of the columns. Only stats,
         thresholds, feature, bin, right child and depth cross the link; left
         children, node sizes, impurities, int64 counts and leaf values are
-        derived from them on first use (``TreeArrays.deferred``)."""
+        derived from them on first use (``TreeArrays.deferred``); so are the
+        thresholds when ``host_table`` (the host's padded edge table) is given."""
         P, C = self.P, self.C
         hip = self.hip
         s = _stream()
-        if d_edges is None:
+        thr = host_table is None
+        if thr and d_edges is None:
             d_edges = torch.from_numpy(np.ascontiguousarray(edges, np.float64)).to(self.device)
         tiles = hip.asm_tiles(P)
         bpn = int(hip.asm_node_bytes(C, self.reg))
@@ -551,14 +554,15 @@ class HipBackend:
         total = ws[o_total : o_total + 8].view(torch.int64)
         hip.asm_rank(s, self.pos_rec.data_ptr(), P, base, base + o_total, base + o_rank)
         hip.asm_emit(s, self.pos_rec.data_ptr(), self.pos_st.data_ptr(), self.reg, P, C,
-                     base + o_rank, d_edges.data_ptr(), int(d_edges.stride(0)), base + o_total,
-                     base + o_out, bool(self.reg))
+                     base + o_rank, d_edges.data_ptr() if thr else 0,
+                     int(d_edges.stride(0)) if thr else 0, base + o_total, base + o_out,
+                     bool(self.reg), thr)
         h_total = _pinned_copy(total, "asm.total")
         torch.cuda.current_stream(self.device).synchronize()
         self._check_finisher_watch()
         N = int(h_total[0])
         sbytes = N * 16 if self.reg else (N * C * 4 + 7) // 8 * 8
-        nbytes = sbytes + N * 8 + N * 16
+        nbytes = sbytes + (N * 8 if thr else 0) + N * 16
         host = torch.empty(max(nbytes, 8), dtype=torch.uint8, pin_memory=True)
         host[:nbytes].copy_(ws[o_out : o_out + nbytes], non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
@@ -568,14 +572,16 @@ class HipBackend:
         else:
             stats = h[: N * C * 4].view(np.int32).reshape(N, C)
         o = sbytes
-        thr = h[o : o + N * 8].view(np.float64)
-        o += N * 8
+        threshold = None
+        if thr:
+            threshold = h[o : o + N * 8].view(np.float64)
+            o += N * 8
         i4 = h[o : o + N * 16].view(np.int32)
         self.pos_rec = self.pos_st = None
         return TreeArrays.from_device_columns(
-            stats=stats, threshold=thr, feature=i4[:N], threshold_bin=i4[N : 2 * N],
+            stats=stats, threshold=threshold, feature=i4[:N], threshold_bin=i4[N : 2 * N],
             right=i4[2 * N : 3 * N], depth=i4[3 * N : 4 * N], criterion=int(crit),
-            regression=bool(self.reg), y_exp=int(y_exp))
+            regression=bool(self.reg), y_exp=int(y_exp), edges_table=host_table)
 
     def small_fit_supported(self, comm=None) -> bool:
         """One-workgroup whole-tree fit (``small_fit.hip``): classification on

@@ -50,3 +50,23 @@ def test_deferred_missing_attribute_raises():
     ta = TreeArrays.deferred({}, feature=np.zeros(1, np.int32))
     with pytest.raises(AttributeError):
         _ = ta.nonexistent
+
+
+def test_device_columns_thresholds_from_edge_table():
+    from mpitree_amd.core.binning import fit_bin_mapper
+
+    rng = np.random.default_rng(9)
+    X = rng.integers(0, 40, size=(2000, 4)).astype(np.float64)
+    y = (X[:, 0] + rng.integers(0, 5, 2000)) % 2
+    r = fit_tree(X, y, regression=False, criterion=0, max_depth=None, min_samples_split=2,
+                 device="cpu")
+    table = fit_bin_mapper(X, 256).padded_edges()
+    cols = _compact(r.arrays, False)
+    cols["threshold"] = None
+    dev = TreeArrays.from_device_columns(**cols, criterion=0, regression=False,
+                                         edges_table=table)
+    assert "threshold" not in dev.__dict__
+    assert dev.equal(r.arrays)
+    from mpitree_amd.utils.observability import tree_digest
+
+    assert tree_digest(dev) == tree_digest(dev)  # stable; hashes the edge table, not thresholds
