@@ -336,7 +336,7 @@ def fit_tree(
         # subtree jobs of up to n / 128 rows: idle finisher workgroups split big
         # jobs between them (hand-off queue), so fewer replicated levels win
         # (profiles/kernel_experiments.md: 1M x 64 3.52 -> 3.33 ms at 2048 -> 8192)
-        # (the regression finisher has no hand-off queue: smaller jobs balance it)
+        # (regression: the hand-off queue gains 0.35 ms at any of n/512 .. n/128)
         default_fr = int(env) if env else (max(2048, n // 512) if regression
                                            else max(2048, min(n // 128, 32768)))
         if finisher_rows is None or (comm.world_size > 1 and comm.kind == "data"):

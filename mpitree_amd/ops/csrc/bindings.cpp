@@ -66,7 +66,7 @@ void launch_job_sort(hipStream_t, const int64_t*, int, int, int64_t*, int32_t*);
 void launch_finish_reg(hipStream_t, const void*, int64_t, const void*, int, int64_t, uint32_t*,
                        uint32_t*, const int64_t*, const int64_t*, int, int32_t*, const int32_t*,
                        int, int, int, int64_t, int64_t, int32_t*, int64_t*, int, int, int64_t*,
-                       int);
+                       int, int64_t*, int32_t*, int32_t, int);
 void launch_seg_minmax(hipStream_t, const uint32_t*, const int64_t*, const int64_t*, int, int64_t*,
                        const int32_t*);
 void launch_hist_reduce_tasks(hipStream_t, const int64_t*, int, const int64_t*, int, const void*,
@@ -205,12 +205,14 @@ PYBIND11_MODULE(_hip, m) {
                          uintptr_t jobs, int J, uintptr_t counter, uintptr_t nbins, int F, int B,
                          int max_depth, int64_t mss, int64_t msl, uintptr_t node_i32,
                          uintptr_t node_st, int grid, int tiny_rows, uintptr_t tiny,
-                         int tiny_grid) {
+                         int tiny_grid, uintptr_t tasks, uintptr_t task_flag, int epoch,
+                         int task_cap) {
     mt::launch_finish_reg(S(s), P<void>(codes_rm), row_words, P<void>(codes_fm), cb, n_rows,
                           P<uint32_t>(buf0), P<uint32_t>(buf1), P<int64_t>(y), P<int64_t>(jobs),
                           J, P<int32_t>(counter), P<int32_t>(nbins), F, B, max_depth, mss, msl,
                           P<int32_t>(node_i32), P<int64_t>(node_st), grid, tiny_rows,
-                          P<int64_t>(tiny), tiny_grid);
+                          P<int64_t>(tiny), tiny_grid, P<int64_t>(tasks), P<int32_t>(task_flag),
+                          epoch, task_cap);
   });
   m.def("seg_minmax", [](uintptr_t s, uintptr_t idx, uintptr_t y, uintptr_t items, int n_items,
                          uintptr_t out, uintptr_t dcount) {

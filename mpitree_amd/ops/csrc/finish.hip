@@ -37,13 +37,8 @@ namespace mt {
 // threads per finisher workgroup: 512 (two per CU). A 1024-thread variant and an
 // in-kernel tiny-subtree queue were measured slower (profiles/kernel_experiments.md)
 constexpr int kFinThreadsSmall = 512;
-// job_counter words (int32 [kFinCounterWords], zeroed before each launch): the
-// claim cursor, the tiny-subtree count / cursor, the {completed, handed off}
-// queue word, the finished epoch and the watchdog each on their own 128-B line
-constexpr int kFinCtrTinyCount = 32;
-constexpr int kFinCtrQueue = 64;
-constexpr int kFinCtrFinished = 96;
-constexpr int kFinCtrWatch = 100;
+// job_counter word layout: kFinCtr* in grow.h (int32 [kFinCounterWords], zeroed
+// before each launch)
 constexpr int kFinStack = 40;    // >= log2(max job rows) + 2
 constexpr int kFinMaxC = 16;     // classes supported by the finisher
 constexpr int kFinTab = 1024;    // LDS x*log2(x) entries

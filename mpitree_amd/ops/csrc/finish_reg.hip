@@ -22,6 +22,7 @@
 
 #include "common.h"
 #include "criterion.h"
+#include "grow.h"
 #include "tiny_sort.h"
 
 namespace mt {
@@ -54,7 +55,8 @@ __global__ __launch_bounds__(kRegThreads, 2) void finish_reg_kernel(
     int32_t* __restrict__ job_counter, const int32_t* __restrict__ nbins, int F, int B,
     int max_depth, int64_t mss, int64_t msl, int32_t* __restrict__ node_i32,
     int64_t* __restrict__ node_st, int tiny_rows, int64_t* __restrict__ tiny,
-    int32_t* __restrict__ tiny_count) {
+    int32_t* __restrict__ tiny_count, int64_t* __restrict__ tasks,
+    int32_t* __restrict__ task_flag, int32_t epoch, int task_cap) {
   extern __shared__ __align__(16) uint8_t smem[];
   unsigned long long* t_sum = reinterpret_cast<unsigned long long*>(smem);  // [FT][B]
   uint32_t* t_cnt = reinterpret_cast<uint32_t*>(smem + (size_t)kRegFT * B * 8);  // [FT][B]
@@ -80,12 +82,46 @@ __global__ __launch_bounds__(kRegThreads, 2) void finish_reg_kernel(
   for (int f = tid; f < F; f += kRegThreads) s_nb[f] = min(B, nbins[f]);
   __syncthreads();
 
+  // Hand-off queue (as in finish_cls_kernel): a workgroup that splits a node
+  // while others idle gives them the larger child; waiters poll their own
+  // publish flag and the finished word; the last completion releases them.
+  unsigned long long* const q_word =
+      reinterpret_cast<unsigned long long*>(job_counter + kFinCtrQueue);
+  int32_t* const q_finished = job_counter + kFinCtrFinished;
   for (;;) {
-    if (tid == 0) s_job = atomicAdd(job_counter, 1);
+    if (tid == 0) {
+      const int h = atomicAdd(job_counter, 1);
+      int got = h;
+      if (task_cap < 0) {
+        if (h >= J) got = -1;
+      } else if (h >= J) {
+        const uint64_t t_start = wall_clock64();
+        for (uint32_t spins = 0;; ++spins) {
+          if (h - J < task_cap &&
+              __hip_atomic_load(task_flag + (h - J), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                  epoch) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            break;
+          }
+          if (__hip_atomic_load(q_finished, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch) {
+            got = -1;
+            break;
+          }
+          if ((spins & 15u) == 15u && wall_clock64() - t_start > 500000000ull) {  // 5 s
+            atomicExch(job_counter + kFinCtrWatch, 1);
+            got = -1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(32);
+        }
+      }
+      s_job = got;
+    }
     __syncthreads();
     const int job = s_job;
-    if (job >= J) break;
-    const int64_t* jb = jobs + (int64_t)job * 7;
+    if (job < 0) break;
+    const int64_t* jb =
+        job < J ? jobs + (int64_t)job * 7 : tasks + (int64_t)(job - J) * 7;
     if (tid == 0) {
       const int r = (int)jb[3];
       int32_t* R = node_i32 + (int64_t)r * 6;
@@ -332,6 +368,32 @@ __global__ __launch_bounds__(kRegThreads, 2) void finish_reg_kernel(
           if (is_left ? tlf : trf) continue;
           const int cm = is_left ? nl : nr;
           const int64_t cstart = is_left ? start : start + nl;
+          if (pass == 0 && cm > 2 * tiny_rows && task_cap > 0) {
+            const int head =
+                __hip_atomic_load(job_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int pushed = (int)(__hip_atomic_load(q_word, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT) >> 32);
+            if (head > J + pushed && pushed < task_cap) {
+              const int k = (int)(__hip_atomic_fetch_add(q_word, 1ull << 32, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) >> 32);
+              if (k < task_cap) {
+                int64_t* T = tasks + (int64_t)k * 7;
+                T[0] = cstart;
+                T[1] = cm;
+                T[2] = cd;
+                T[3] = is_left ? lid : rid;
+                T[4] = s_buf ^ 1;
+                T[5] = cm;
+                T[6] = is_left ? sl : sr;
+                __threadfence();  // the child's rows and record, chip-wide, before the flag
+                __hip_atomic_store(task_flag + k, epoch, __ATOMIC_RELEASE,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                continue;
+              }
+              __hip_atomic_fetch_add(q_word, ~0ull << 32, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
           if (cm <= tiny_rows) {
             const int t = atomicAdd(tiny_count, 1);
             int64_t* tr = tiny + (int64_t)t * 8;
@@ -352,6 +414,12 @@ __global__ __launch_bounds__(kRegThreads, 2) void finish_reg_kernel(
         }
       }
       __syncthreads();
+    }
+    if (tid == 0 && task_cap >= 0) {
+      const unsigned long long q =
+          __hip_atomic_fetch_add(q_word, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((int)(uint32_t)q + 1 == J + (int)(q >> 32))
+        __hip_atomic_store(q_finished, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -762,7 +830,8 @@ void launch_finish_reg(hipStream_t stream, const void* codes_rm, int64_t row_wor
                        uint32_t* buf1, const int64_t* y, const int64_t* jobs, int J,
                        int32_t* counter, const int32_t* nbins, int F, int B, int max_depth,
                        int64_t mss, int64_t msl, int32_t* node_i32, int64_t* node_st, int grid,
-                       int tiny_rows, int64_t* tiny, int tiny_grid) {
+                       int tiny_rows, int64_t* tiny, int tiny_grid, int64_t* tasks,
+                       int32_t* task_flag, int32_t epoch, int task_cap) {
   if (J <= 0) return;
   if (F > kRegMaxF) throw std::runtime_error("regression finisher supports at most 256 features");
   if (code_bytes != 1) tiny_rows = 0;
@@ -774,7 +843,7 @@ void launch_finish_reg(hipStream_t stream, const void* codes_rm, int64_t row_wor
   hipLaunchKernelGGL(finish_reg_kernel<CT>, dim3(grid), dim3(kRegThreads), lds, stream,     \
                      (const uint32_t*)codes_rm, row_words, (const CT*)codes_fm, n_rows, buf0, \
                      buf1, y, jobs, J, counter, nbins, F, B, max_depth, mss, msl, node_i32,  \
-                     node_st, tiny_rows, tiny, counter + 1);
+                     node_st, tiny_rows, tiny, counter + 1, tasks, task_flag, epoch, task_cap);
   if (code_bytes == 1) {
     MT_FR(uint8_t)
   } else {

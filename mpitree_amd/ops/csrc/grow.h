@@ -8,6 +8,13 @@ namespace mt {
 // The finisher's int32 work counters; words that different workgroups update
 // concurrently sit on separate 128-byte lines (see finish.hip).
 constexpr int kFinCounterWords = 128;
+// job_counter words: the claim cursor (0), the tiny-subtree count / cursor, the
+// {completed, handed off} queue word, the finished epoch and the watchdog, each
+// on its own 128-B line (the regression finisher keeps its tiny words at 1, 2)
+constexpr int kFinCtrTinyCount = 32;
+constexpr int kFinCtrQueue = 64;
+constexpr int kFinCtrFinished = 96;
+constexpr int kFinCtrWatch = 100;
 
 
 // Level work lists (one set per level parity). ctl: int32

@@ -668,15 +668,24 @@ class HipBackend:
         tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
         tiny = torch.empty((int(job_rows // 2 + J + 1), 8), dtype=torch.int64, device=self.device)
         md = -1 if params.max_depth is None else int(params.max_depth)
-        grid = int(min(J, int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU))))
+        grid = int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU))
+        task_cap = int(job_rows // (2 * max(tiny_rows, 1) + 1) + 16)
+        steal = os.environ.get("MPITREE_FIN_STEAL", "1")
+        if steal == "0":
+            task_cap = 0
+        elif steal == "-1":
+            task_cap, grid = -1, min(grid, J)
+        tasks = torch.empty((max(task_cap, 1), 7), dtype=torch.int64, device=self.device)
+        flags, epoch = _task_flags(self.device, max(task_cap, 0) + grid)
         self.hip.finish_reg(_stream(), self.codes_rm.data_ptr(), self.row_elems * self.cb // 4,
                             self.codes_fm.data_ptr(), self.cb, self.n, self.idx.data_ptr(),
                             self.tmp.data_ptr(), self.y.data_ptr(), d_jobs.data_ptr(), J,
                             counter.data_ptr(), self.nbins.data_ptr(), self.F, self.B, md,
                             int(params.min_samples_split), int(max(1, params.min_samples_leaf)),
                             rec.data_ptr(), st64.data_ptr(), grid, tiny_rows, tiny.data_ptr(),
-                            4 * N_CU)
-        self._fin_keep = (counter, tiny, d_jobs)
+                            4 * N_CU, tasks.data_ptr(), flags.data_ptr(), epoch, task_cap)
+        self._fin_keep = (counter, tasks, tiny, d_jobs)
+        _FIN_WATCH.append(_pinned_copy(counter[100:101], f"fin.watch{len(_FIN_WATCH)}"))
 
     def finish_subtrees(self, starts, counts, depths, params, stats=None, positions=None):
         """See :meth:`_finish_subtrees`."""
