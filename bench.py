@@ -46,7 +46,8 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--n", "--samples", dest="n", type=int, default=1_000_000,
+                    help="rows (--samples under torchrun, whose parser takes --n)")
     ap.add_argument("--features", type=int, default=64)
     ap.add_argument("--classes", type=int, default=2)
     ap.add_argument("--max-depth", type=int, default=-1, help="-1 = unlimited (reference default)")
@@ -157,6 +158,8 @@ def main(argv=None):
                 + int(stats.get("comm_bytes_exchange", 0)),
                 "tree_nodes": stats.get("node_count"),
                 "tree_depth": stats.get("max_depth"),
+                "comm_bytes_per_level": stats.get("comm_bytes_per_level"),
+                "peak_device_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 3),
             },
             "reference_note": "reference is infeasible at this size (BASELINE.md: >=775 CPU-h "
                               "for the root node alone); vs_baseline is null",
