@@ -443,3 +443,28 @@ def test_gpu_published_sweep_workload():
         h = DecisionTreeClassifier(device="cpu").fit(X, y)
         assert g.tree_arrays_.equal(h.tree_arrays_), n
         assert g.tree_arrays_.n_leaves == n
+
+
+@pytest.mark.parametrize("regression", [False, True])
+def test_gpu_finisher_handoff_queue_single_job(monkeypatch, regression):
+    """The whole tree is ONE finisher job: every other workgroup only works on
+    children handed off through the queue (and the watchdog never fires)."""
+    from mpitree_amd.core.fit import fit_tree
+
+    monkeypatch.setenv("MPITREE_FINISHER_ROWS", "60000")
+    rng = np.random.default_rng(21 + regression)
+    n, F = 50000, 12
+    X = rng.integers(0, 64, size=(n, F)).astype(np.float32)
+    if regression:
+        y = X[:, 0] * 0.1 + rng.normal(size=n)
+    else:
+        y = ((X[:, 0] + X[:, 1] + rng.integers(0, 30, size=n)) // 40) % 2
+    kw = dict(regression=regression, criterion=2 if regression else 0, max_depth=None,
+              min_samples_split=2)
+    g = fit_tree(X, y, device="cuda", **kw)
+    assert g.engine == "hip-device-loop" and g.stats.get("finisher_subtrees") == 1
+    h = fit_tree(X, y, device="cpu", **kw)
+    assert g.arrays.equal(h.arrays, check_impurity=not regression)
+    monkeypatch.setenv("MPITREE_FIN_STEAL", "-1")  # same tree without the queue
+    g2 = fit_tree(X, y, device="cuda", **kw)
+    assert g2.arrays.equal(h.arrays, check_impurity=not regression)
