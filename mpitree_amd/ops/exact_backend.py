@@ -70,9 +70,25 @@ class ExactHipBackend(HipBackend):
         self.crit = criterion
         self.reg = False
         self.chunk = int(self.hip.ex_chunk())
-        # per feature: values sorted (stable), dense ranks, unique-value table
+        # per feature: values sorted (stable), dense ranks, unique-value table.
+        # One 1-D radix sort of 64-bit keys {feature : 32, order-preserving value
+        # bits : 32} (radix sorts are stable) instead of a segmented merge sort
+        # of the [F, n] matrix (12.5 -> ~3 ms for 1M x 64).
         xt = X.t().contiguous()
-        vals, order = torch.sort(xt, dim=1, stable=True)
+        if xt.dtype == torch.float32:
+            xt = xt + 0.0  # -0.0 -> +0.0: equal values share one key (stable by row)
+            bits = xt.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+            neg = (bits >> 31) == 1
+            # IEEE order: negatives flip every bit, positives flip the sign bit
+            key = torch.where(neg, bits ^ 0xFFFFFFFF, bits | 0x80000000)
+            key = key | (torch.arange(F, device=dev, dtype=torch.int64)[:, None] << 32)
+            _, perm = torch.sort(key.view(-1), stable=True)
+            del bits, neg, key
+            order = (perm.view(F, n) - torch.arange(F, device=dev, dtype=torch.int64)[:, None] * n)
+            vals = torch.gather(xt, 1, order)
+            del perm
+        else:
+            vals, order = torch.sort(xt, dim=1, stable=True)
         del xt
         new = torch.ones_like(vals, dtype=torch.bool)
         new[:, 1:] = vals[:, 1:] != vals[:, :-1]
