@@ -16,8 +16,9 @@ F = int(os.environ.get("PMC_F", 64))
 if os.environ.get("PMC_REG"):  # the regression config (MSE criterion)
     X, y = make_regression(n, F, seed=0, device=torch.device("cuda", 0))
     est = DecisionTreeRegressor(device="cuda")
-else:
-    X, y = make_classification(n, F, seed=0, device=torch.device("cuda", 0))
+else:  # PMC_EXACT=1: continuous features (the exact-threshold engine)
+    lv = None if os.environ.get("PMC_EXACT") else 256
+    X, y = make_classification(n, F, seed=0, device=torch.device("cuda", 0), levels=lv)
     est = DecisionTreeClassifier(device="cuda")
 est.fit(X, y)
 torch.cuda.synchronize()

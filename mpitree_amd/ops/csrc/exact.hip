@@ -73,6 +73,21 @@ __global__ __launch_bounds__(kExThreads) void ex_tot_kernel(const uint64_t* __re
   const int64_t it = blockIdx.x;
   const int f = blockIdx.y;
   const int64_t c0 = items[it * 4 + 2], cn = items[it * 4 + 3];
+  if (C <= 2) {  // class-1 count by wave sums (LDS atomics on two words serialise)
+    const uint64_t* L = E + (int64_t)f * n + c0;
+    uint32_t ones = 0;
+    for (int64_t i = threadIdx.x; i < cn; i += kExThreads) ones += ex_lab(L[i]) == 1 ? 1u : 0u;
+    ones = wave_sum_u32(ones);
+    if (lane_id() == 0) cnt[threadIdx.x >> 6] = ones;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (int w = 0; w < kExThreads / kWave; ++w) t += cnt[w];
+      tot[(it * F + f) * C + 0] = (int32_t)(cn - t);
+      if (C == 2) tot[(it * F + f) * C + 1] = (int32_t)t;
+    }
+    return;
+  }
   for (int c = threadIdx.x; c < C; c += kExThreads) cnt[c] = 0;
   __syncthreads();
   const uint64_t* L = E + (int64_t)f * n + c0;
@@ -228,7 +243,7 @@ __global__ __launch_bounds__(kExThreads) void ex_scan_c2_kernel(
     const uint64_t* __restrict__ E, int64_t n, const int64_t* __restrict__ items,
     const int64_t* __restrict__ seg, const int32_t* __restrict__ carry,
     const int32_t* __restrict__ slot_tot, int F, int64_t msl,
-    unsigned long long* __restrict__ best) {
+    unsigned long long* __restrict__ best, const double* __restrict__ xtab, int xtab_n) {
   __shared__ uint32_t s_w[kExThreads / kWave];
   __shared__ uint32_t s_first[kExThreads];
   __shared__ unsigned long long s_min[kExThreads / kWave];
@@ -273,7 +288,12 @@ __global__ __launch_bounds__(kExThreads) void ex_scan_c2_kernel(
     valid[k] = (p0 + k - c0) < cn && mr > 0 && nr != ex_rank(e[k]) && ml >= msl && mr >= msl;
     l1[k] = (int64_t)(base1 + pre[k]);
   }
-  const double tm = xlog2x((uint64_t)m);
+  // x*log2(x) from the shared table (built by the same xlog2x: identical bits)
+  // below xtab_n, the atanh series above it
+  auto tl = [&](int64_t x) -> double {
+    return x < (int64_t)xtab_n ? __ldg(xtab + x) : xlog2x((uint64_t)x);
+  };
+  const double tm = tl(m);
   const double tu = tie_unit(tm, m);
   const double tinv = 1.0 / tu;
   auto exact_key = [&](int k) -> unsigned long long {
@@ -282,9 +302,9 @@ __global__ __launch_bounds__(kExThreads) void ex_scan_c2_kernel(
     const int64_t L1 = l1[k], L0 = ml - L1, R1 = t1 - L1, R0 = t0 - L0;
     double cost;
     if (CRIT == kEntropy) {
-      const double sl = xlog2x((uint64_t)L0) + xlog2x((uint64_t)L1);
-      const double sr = xlog2x((uint64_t)R0) + xlog2x((uint64_t)R1);
-      cost = (xlog2x((uint64_t)ml) - sl) + (xlog2x((uint64_t)mr) - sr);
+      const double sl = tl(L0) + tl(L1);
+      const double sr = tl(R0) + tl(R1);
+      cost = (tl(ml) - sl) + (tl(mr) - sr);
     } else {
       cost = gini_term(ml, L0 * L0 + L1 * L1) + gini_term(mr, R0 * R0 + R1 * R1);
     }
@@ -545,10 +565,10 @@ void ex_scan_level(hipStream_t stream, const uint64_t* E, int64_t n, const int64
   MT_HIP_CHECK(hipMemsetAsync(best, 0xFF, (size_t)K * F * sizeof(unsigned long long), stream));
   if (C == 2 && crit == kEntropy)
     hipLaunchKernelGGL(ex_scan_c2_kernel<kEntropy>, dim3(NI, F), dim3(kExThreads), 0, stream, E,
-                       n, items, seg, carry, slot_tot, F, msl, best);
+                       n, items, seg, carry, slot_tot, F, msl, best, xtab, xtab_n);
   else if (C == 2)
     hipLaunchKernelGGL(ex_scan_c2_kernel<kGini>, dim3(NI, F), dim3(kExThreads), 0, stream, E, n,
-                       items, seg, carry, slot_tot, F, msl, best);
+                       items, seg, carry, slot_tot, F, msl, best, xtab, xtab_n);
   else
     hipLaunchKernelGGL(ex_scan_kernel, dim3(NI, F), dim3(kExThreads), 0, stream, E, n, items,
                        seg, carry, slot_tot, F, C, crit, msl, xtab, xtab_n, best);
