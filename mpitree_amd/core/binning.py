@@ -104,6 +104,10 @@ class TableBinMapper(BinMapper):
     def n_bins(self) -> np.ndarray:
         return self._nb.astype(np.int32)
 
+    @property
+    def max_n_bins(self) -> int:  # (without slicing the per-feature edge lists)
+        return int(self._nb.max()) if self._nb.size else 1
+
     def padded_edges(self, dtype=np.float64) -> np.ndarray:
         bmax = self.max_n_bins
         out = np.array(self._table[:, :bmax], dtype=dtype)
