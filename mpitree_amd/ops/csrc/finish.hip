@@ -1380,7 +1380,11 @@ __device__ __forceinline__ void tiny_sorted_subtree(
   }
 }
 
-__global__ __launch_bounds__(256) void finish_tiny_sorted_kernel(
+// kW waves per workgroup share one H table; the launcher picks kW so the most
+// waves fit a CU's LDS (F = 64: 16 waves in one 1024-thread workgroup instead of
+// 3 x 4; F = 128: 8 instead of 4), see tiny_sorted_waves.
+template <int kW>
+__global__ __launch_bounds__(kW * kWave) void finish_tiny_sorted_kernel(
     const uint32_t* __restrict__ codes_rm, int64_t row_words, const uint32_t* __restrict__ buf0,
     const uint32_t* __restrict__ buf1, const int32_t* __restrict__ y, FinRowLab rl,
     const int64_t* __restrict__ tiny, const int32_t* __restrict__ tiny_count,
@@ -1390,8 +1394,8 @@ __global__ __launch_bounds__(256) void finish_tiny_sorted_kernel(
   extern __shared__ __align__(16) uint32_t dyn[];
   __shared__ double s_h[kTinyH];
   __shared__ uint32_t s_hrow[kTinyRows + 1];
-  __shared__ unsigned long long s_mask[kTinyWaves][16];
-  __shared__ int32_t s_dep[kTinyWaves][16], s_slot[kTinyWaves][16];
+  __shared__ unsigned long long s_mask[kW][16];
+  __shared__ int32_t s_dep[kW][16], s_slot[kW][16];
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
   uint8_t* wbase = reinterpret_cast<uint8_t*>(dyn) + (size_t)wave * tiny_wave_bytes(F);
@@ -1411,6 +1415,20 @@ __global__ __launch_bounds__(256) void finish_tiny_sorted_kernel(
                         (int)rec[2], rec[4], F, C, crit, max_depth, mss, msl, s_h, s_hrow, srt, flag,
                         s_mask[wave], s_dep[wave], s_slot[wave], TinyOut{node_i32, node_cnt});
   }
+}
+
+// Waves per workgroup of the sorted tiny kernel: the most resident waves per CU
+// under the LDS budget and the VGPR cap (<= 128 VGPRs: 4 waves per SIMD), fewer
+// waves per workgroup on ties.
+static int tiny_sorted_waves(int F) {
+  constexpr int kLdsPerCu = 160 * 1024, kWavesPerCu = 16;
+  int best_w = 4, best = 0;
+  for (int w : {4, 8, 16}) {
+    const int bytes = kTinyH * 8 + (kTinyRows + 1) * 4 + w * 16 * 16 + w * tiny_wave_bytes(F);
+    const int waves = std::min(kLdsPerCu / bytes, kWavesPerCu / w) * w;
+    if (waves > best) best = waves, best_w = w;
+  }
+  return best_w;
 }
 
 int finish_lds_bytes(int F, int B, int C) { return F * fin_fstride(B, (C + 1) / 2) * 4; }
@@ -1464,14 +1482,26 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   if (tiny_rows > 0) {
     const bool sorted = C <= 2 && getenv_int("MPITREE_TINY_SORTED", 1) != 0;
     if (sorted) {
-      const size_t lds = (size_t)kTinyWaves * tiny_wave_bytes(F);
-      MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_tiny_sorted_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL(finish_tiny_sorted_kernel, dim3(tiny_grid), dim3(kTinyWaves * kWave),
-                         lds, stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl,
-                         tiny, counter + kFinCtrTinyCount, counter + kFinCtrTinyCount + 1, F, C,
-                         crit, max_depth, mss, msl, xtab,
-                         node_i32, node_cnt);
+      int w = getenv_int("MPITREE_TINY_WAVES", tiny_sorted_waves(F));
+      w = w >= 16 && 16 * tiny_wave_bytes(F) <= 128 * 1024 ? 16 : (w >= 8 ? 8 : 4);
+      // tiny_grid counts 4-wave workgroups: keep the total wave count
+      const int g = std::max(1, tiny_grid * kTinyWaves / w);
+      const size_t lds = (size_t)w * tiny_wave_bytes(F);
+#define MT_TS(W)                                                                             \
+  MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_tiny_sorted_kernel<W>,                \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));   \
+  hipLaunchKernelGGL(finish_tiny_sorted_kernel<W>, dim3(g), dim3(W * kWave), lds, stream,    \
+                     (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,          \
+                     counter + kFinCtrTinyCount, counter + kFinCtrTinyCount + 1, F, C, crit, \
+                     max_depth, mss, msl, xtab, node_i32, node_cnt);
+      if (w == 16) {
+        MT_TS(16)
+      } else if (w == 8) {
+        MT_TS(8)
+      } else {
+        MT_TS(4)
+      }
+#undef MT_TS
     } else {
       hipLaunchKernelGGL(finish_tiny_kernel, dim3(tiny_grid), dim3(kTinyWaves * kWave), 0,
                          stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,
