@@ -34,9 +34,11 @@
 
 namespace mt {
 
-// threads per finisher workgroup: 512 (two per CU). A 1024-thread variant and an
-// in-kernel tiny-subtree queue were measured slower (profiles/kernel_experiments.md)
+// threads per finisher workgroup: 512 (two per CU). A 1024-thread variant where two
+// 512-thread workgroups fit a CU and an in-kernel tiny-subtree queue were measured
+// slower (profiles/kernel_experiments.md); 1024 threads run where only one fits.
 constexpr int kFinThreadsSmall = 512;
+constexpr int kFinThreadsWide = 1024;  // one workgroup per CU (F = 128 histograms)
 // job_counter word layout: kFinCtr* in grow.h (int32 [kFinCounterWords], zeroed
 // before each launch)
 constexpr int kFinStack = 40;    // >= log2(max job rows) + 2
@@ -1462,7 +1464,33 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                      msl, xtab, xtabf, xtab_n, node_i32, node_cnt, tasks, task_flag, epoch,   \
                      task_cap, tiny_rows,                                                     \
                      tiny, counter + kFinCtrTinyCount, prof);
-#define MT_FIN(CT, C2) MT_FIN_NT(CT, C2, kFinThreadsSmall)
+  // When the histogram leaves room for only one 512-thread workgroup per CU
+  // (F = 128: 133 KB), run 1024 threads per workgroup instead: same LDS, twice
+  // the waves to hide the gather and LDS latency. The persistent grid shrinks
+  // to match (one workgroup per CU where there were two).
+  bool wide = false;
+  if (getenv_int("MPITREE_FIN_WIDE", 1) != 0) {
+    int per_cu = 0;
+    const void* k512 = code_bytes == 1 ? (C <= 2 ? (const void*)finish_cls_kernel<uint8_t, true, kFinThreadsSmall>
+                                                 : (const void*)finish_cls_kernel<uint8_t, false, kFinThreadsSmall>)
+                                       : (C <= 2 ? (const void*)finish_cls_kernel<uint16_t, true, kFinThreadsSmall>
+                                                 : (const void*)finish_cls_kernel<uint16_t, false, kFinThreadsSmall>);
+    MT_HIP_CHECK(hipFuncSetAttribute(k512, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    MT_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k512, kFinThreadsSmall, lds));
+    wide = per_cu == 1;
+  }
+  if (wide) {
+    int dev = 0, n_cu = 0;
+    MT_HIP_CHECK(hipGetDevice(&dev));
+    MT_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+    grid = std::max(1, std::min(grid, n_cu));
+  }
+#define MT_FIN(CT, C2)                       \
+  if (wide) {                                \
+    MT_FIN_NT(CT, C2, kFinThreadsWide)       \
+  } else {                                   \
+    MT_FIN_NT(CT, C2, kFinThreadsSmall)      \
+  }
   if (code_bytes == 1) {
     if (C <= 2) {
       MT_FIN(uint8_t, true)
