@@ -202,7 +202,10 @@ def _fit_exact_gpu(Xd, yd, classes, C, crit, params, comm, timings, t_bin, t_sta
     be = ExactHipBackend()
     be.setup_exact(Xd, yd.to(torch.int32), C, crit)
     timings["bin"] = time.perf_counter() - t_bin
-    params.finisher_rows = 0
+    # subtrees of <= 256 rows continue in the histogram finisher on local codes
+    env = os.environ.get("MPITREE_EXACT_FINISHER_ROWS")
+    fr = int(env) if env else be.max_finisher_rows
+    params.finisher_rows = min(fr, be.max_finisher_rows) if be.finisher_supported() else 0
     builder = LevelwiseBuilder(be, params, LocalComm())
     dummy_edges = np.zeros((F, 1))  # thresholds come from the device unique-value table
     with roctx_range("mpitree.grow"):

@@ -267,6 +267,8 @@ class LevelwiseBuilder:
                 if small.any():
                     for key in deferred:
                         deferred[key].append(fr[key][small])
+                    if hasattr(be, "defer_segments"):
+                        be.defer_segments(fr["start"][small], fr["count"][small])
                     keep = ~small
                     # derived nodes whose built sibling was deferred: build from rows
                     sib = fr["sib"]

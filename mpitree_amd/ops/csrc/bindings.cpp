@@ -55,6 +55,11 @@ void ex_partition_level(hipStream_t, const uint64_t*, uint64_t*, int64_t, const 
                         const int64_t*, const int64_t*, int, int, uint8_t*, int32_t*, int32_t*,
                         int32_t*);
 int ex_chunk();
+void ex_local_codes(hipStream_t, const uint64_t*, const uint64_t*, int64_t, const int64_t*, int,
+                    int, int, uint8_t*, uint8_t*, uint32_t*, uint32_t*);
+void ex_local_fix(hipStream_t, const uint64_t*, const uint64_t*, int64_t, const int64_t*, int,
+                  int32_t*);
+int ex_local_max();
 void launch_fp_combine(hipStream_t, const int64_t*, int, int, int, const int32_t*, int64_t*);
 void launch_grow_dp_fixup(hipStream_t, const PlanArgs&);
 void launch_grow_init(hipStream_t, const LevelLists&, int64_t, int64_t, int64_t, int, int,
@@ -283,6 +288,19 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("msl"), py::arg("fr"), py::arg("host_ctl"), py::arg("host_tag"), py::arg("dp") = 0,
      py::arg("fixup") = false);
   m.def("ex_chunk", &mt::ex_chunk);
+  m.def("ex_local_max", &mt::ex_local_max);
+  m.def("ex_local_codes", [](uintptr_t s, uintptr_t E0, uintptr_t E1, int64_t n, uintptr_t seg,
+                             int J, int F, int row_bytes, uintptr_t codes_rm, uintptr_t codes_fm,
+                             uintptr_t ent, uintptr_t inv) {
+    mt::ex_local_codes(S(s), P<uint64_t>(E0), P<uint64_t>(E1), n, P<int64_t>(seg), J, F,
+                       row_bytes, P<uint8_t>(codes_rm), P<uint8_t>(codes_fm), P<uint32_t>(ent),
+                       P<uint32_t>(inv));
+  });
+  m.def("ex_local_fix", [](uintptr_t s, uintptr_t E0, uintptr_t E1, int64_t n, uintptr_t jobs,
+                           int J, uintptr_t node_i32) {
+    mt::ex_local_fix(S(s), P<uint64_t>(E0), P<uint64_t>(E1), n, P<int64_t>(jobs), J,
+                     P<int32_t>(node_i32));
+  });
   m.def("ex_scan_level", [](uintptr_t s, uintptr_t E, int64_t n, uintptr_t items, int NI,
                             uintptr_t ifirst, uintptr_t seg, int K, int F, int C, int crit,
                             int64_t msl, uintptr_t xtab, int xtab_n, uintptr_t tot,

@@ -548,6 +548,86 @@ __global__ __launch_bounds__(kExThreads) void ex_pscatter_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Small subtrees leave the list engine for the histogram finisher (finish.hip)
+// on subtree-local 8-bit codes. For a deferred segment [s, s + m) (m <= 256)
+// a row's code in feature f is the offset of the first entry of its value in
+// the segment of f's sorted list: codes ascend with the value, equal values
+// share a code, and the finisher's split "code <= b" is the split "x <= value
+// at s + b", so its candidates, costs and ties are the list engine's. Virtual
+// rows are positions of feature 0's list (v = s + offset there), giving the
+// finisher row-major codes codes_rm[v][.], feature-major codes_fm[f][v] and
+// packed entries ent[v] = label << 24 | v. ex_local_fix_kernel turns the
+// finished nodes' codes back into value ranks.
+// seg: int64 [J][3] = {start, count, list buffer}
+constexpr int kExLocalMax = 256;
+
+__global__ __launch_bounds__(kExLocalMax) void ex_local_codes_kernel(
+    const uint64_t* __restrict__ E0, const uint64_t* __restrict__ E1, int64_t n,
+    const int64_t* __restrict__ seg, int F, int row_bytes, uint8_t* __restrict__ codes_rm,
+    uint8_t* __restrict__ codes_fm, uint32_t* __restrict__ ent, uint32_t* __restrict__ inv) {
+  extern __shared__ __align__(16) uint8_t s_code[];  // [m][row_bytes]
+  __shared__ uint32_t s_rank[kExLocalMax];
+  __shared__ uint32_t s_w[kExLocalMax / kWave];
+  const int64_t s = seg[blockIdx.x * 3 + 0];
+  const int m = (int)seg[blockIdx.x * 3 + 1];
+  const uint64_t* __restrict__ E = seg[blockIdx.x * 3 + 2] ? E1 : E0;
+  const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
+  const int words = m * row_bytes / 4;
+  for (int i = t; i < words; i += kExLocalMax) reinterpret_cast<uint32_t*>(s_code)[i] = 0u;
+  if (t < m) {
+    const uint64_t e = E[s + t];
+    inv[ex_row(e)] = (uint32_t)t;
+    ent[s + t] = ((uint32_t)ex_lab(e) << 24) | (uint32_t)(s + t);
+  }
+  __threadfence_block();
+  __syncthreads();
+  for (int f = 0; f < F; ++f) {
+    uint32_t rank = 0xFFFFFFFFu, v = 0;
+    if (t < m) {
+      const uint64_t e = E[(int64_t)f * n + s + t];
+      rank = ex_rank(e);
+      v = inv[ex_row(e)];
+    }
+    s_rank[t] = rank;
+    __syncthreads();
+    // offset of the first entry of this value: inclusive max-scan of run starts
+    uint32_t b = (t < m && (t == 0 || s_rank[t - 1] != rank)) ? (uint32_t)t : 0u;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t o = __shfl_up(b, d, kWave);
+      if (lane >= d) b = max(b, o);
+    }
+    if (lane == kWave - 1) s_w[w] = b;
+    __syncthreads();
+    for (int k = 0; k < w; ++k) b = max(b, s_w[k]);
+    if (t < m) {
+      s_code[v * row_bytes + f] = (uint8_t)b;
+      codes_fm[(int64_t)f * n + s + v] = (uint8_t)b;
+    }
+    __syncthreads();  // s_rank / s_w reuse
+  }
+  uint32_t* out = reinterpret_cast<uint32_t*>(codes_rm + s * row_bytes);
+  for (int i = t; i < words; i += kExLocalMax) out[i] = reinterpret_cast<const uint32_t*>(s_code)[i];
+}
+
+// Finished subtree j owns positions [pos, pos + 2m - 1) of node_i32 ({feature,
+// bin, left, right, depth, n}; n = 0 marks an unused position): split codes ->
+// value ranks of the list the segment lives in.
+// jobs: int64 [J][4] = {root position, m, segment start, list buffer}
+__global__ __launch_bounds__(256) void ex_local_fix_kernel(const uint64_t* __restrict__ E0,
+                                                          const uint64_t* __restrict__ E1,
+                                                          int64_t n, const int64_t* __restrict__ jobs,
+                                                          int32_t* __restrict__ node_i32) {
+  const int64_t pos = jobs[blockIdx.x * 4 + 0], m = jobs[blockIdx.x * 4 + 1];
+  const int64_t s = jobs[blockIdx.x * 4 + 2];
+  const uint64_t* __restrict__ E = jobs[blockIdx.x * 4 + 3] ? E1 : E0;
+  for (int64_t p = pos + threadIdx.x; p < pos + 2 * m - 1; p += blockDim.x) {
+    int32_t* R = node_i32 + p * 6;
+    if (R[5] > 0 && R[0] >= 0) R[1] = (int32_t)ex_rank(E[(int64_t)R[0] * n + s + R[1]]);
+  }
+}
+
 // --------------------------------------------------------------- launchers
 void ex_scan_level(hipStream_t stream, const uint64_t* E, int64_t n, const int64_t* items, int NI,
                    const int64_t* ifirst, const int64_t* seg, int K, int F, int C, int crit,
@@ -598,5 +678,29 @@ void ex_partition_level(hipStream_t stream, const uint64_t* E, uint64_t* D, int6
 }
 
 int ex_chunk() { return kExChunk; }
+
+void ex_local_codes(hipStream_t stream, const uint64_t* E0, const uint64_t* E1, int64_t n,
+                    const int64_t* seg, int J, int F, int row_bytes, uint8_t* codes_rm,
+                    uint8_t* codes_fm, uint32_t* ent, uint32_t* inv) {
+  if (J <= 0) return;
+  if (row_bytes % 4 != 0 || row_bytes < F) throw std::runtime_error("ex_local_codes: row_bytes");
+  const size_t lds = (size_t)kExLocalMax * row_bytes;
+  MT_HIP_CHECK(hipFuncSetAttribute((const void*)ex_local_codes_kernel,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(ex_local_codes_kernel, dim3(J), dim3(kExLocalMax), lds, stream, E0, E1, n,
+                     seg, F, row_bytes, codes_rm, codes_fm, ent, inv);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void ex_local_fix(hipStream_t stream, const uint64_t* E0, const uint64_t* E1, int64_t n,
+                  const int64_t* jobs, int J, int32_t* node_i32) {
+  if (J <= 0) return;
+  hipLaunchKernelGGL(ex_local_fix_kernel, dim3(J), dim3(256), 0, stream, E0, E1, n, jobs,
+                     node_i32);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+int ex_local_max() { return kExLocalMax; }
+
 
 }  // namespace mt

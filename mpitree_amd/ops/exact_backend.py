@@ -108,6 +108,8 @@ class ExactHipBackend(HipBackend):
         self.xtab = hb.xlog2x_table(dev)
         self.xtabf = hb.xlog2x_table_f32(dev)
         self.y = y_codes
+        self._deferred = []
+        self._loc = None
 
     # the level-wise grower's histogram hooks: only the segments matter here
     def alloc_hist(self, slots: int, F_h: int | None = None):
@@ -121,7 +123,75 @@ class ExactHipBackend(HipBackend):
         raise RuntimeError("exact backend builds every node from its segment")
 
     def finisher_supported(self) -> bool:
-        return False
+        """Subtrees of <= ``max_finisher_rows`` rows continue in the histogram
+        finisher on subtree-local codes (see :meth:`defer_segments`)."""
+        return (self.C <= 16 and self.F <= 256
+                and self.hip.finish_lds_bytes(self.F, 256, self.C) <= 150 * 1024)
+
+    @property
+    def max_finisher_rows(self) -> int:
+        return int(self.hip.ex_local_max())  # local codes are offsets < 256: one byte
+
+    def defer_segments(self, starts, counts):
+        """The level-wise grower defers these frontier segments to the finisher:
+        note the list buffer holding them now (later levels only write the
+        other buffer at split segments, never these positions)."""
+        starts = np.asarray(starts, np.int64)
+        self._deferred.append(np.stack([starts, np.asarray(counts, np.int64),
+                                        np.full(starts.size, self.cur, np.int64)], 1))
+
+    def finish_subtrees(self, starts, counts, depths, params, stats=None, positions=None):
+        """Grow the deferred subtrees with the histogram finisher: per segment,
+        8-bit local codes (offset of the first list entry of the row's value)
+        as the finisher's row-major / feature-major code matrices over virtual
+        rows (positions of feature 0's list), packed label entries as its row
+        buffer; afterwards the split codes become value ranks again."""
+        segs = np.concatenate(self._deferred) if self._deferred else np.zeros((0, 3), np.int64)
+        self._deferred = []
+        starts = np.asarray(starts, np.int64)
+        if segs.shape[0] != starts.size or not np.array_equal(segs[:, 0], starts):
+            raise RuntimeError("exact finisher: deferred segments out of sync with the grower")
+        J = starts.size
+        if J == 0:
+            return None
+        dev, n, F = self.device, self.n, self.F
+        rb = (F + 15) // 16 * 16
+        if getattr(self, "_loc", None) is None:
+            self._loc = dict(
+                rm=torch.empty((n, rb), dtype=torch.uint8, device=dev),
+                fm=torch.empty((F, n), dtype=torch.uint8, device=dev),
+                ent=torch.empty(n, dtype=torch.int32, device=dev),
+                tmp=torch.empty(n, dtype=torch.int32, device=dev),
+                inv=torch.empty(n, dtype=torch.int32, device=dev),
+                nbins=torch.full((F,), 256, dtype=torch.int32, device=dev),
+            )
+        L = self._loc
+        (d_seg,) = self.up(segs)
+        E0, E1 = self.E[0].data_ptr(), self.E[1].data_ptr()
+        self.hip.ex_local_codes(hb._stream(), E0, E1, n, d_seg.data_ptr(), J, F, rb,
+                                L["rm"].data_ptr(), L["fm"].data_ptr(), L["ent"].data_ptr(),
+                                L["inv"].data_ptr())
+        self._seg_buf = segs[:, 2]
+        # the finisher reads the binned engine's fields: point them at the local codes
+        saved = {k: getattr(self, k, None) for k in
+                 ("codes_rm", "codes_fm", "idx", "tmp", "lab_shift", "nbins", "B", "row_elems",
+                  "cb", "y")}
+        self.codes_rm, self.codes_fm = L["rm"], L["fm"]
+        self.idx, self.tmp = L["ent"], L["tmp"]
+        self.lab_shift, self.nbins, self.B, self.row_elems, self.cb = 24, L["nbins"], 256, rb, 1
+        try:
+            return self._finish_subtrees(starts, counts, depths, params, stats, positions)
+        finally:
+            for k, v in saved.items():
+                setattr(self, k, v)
+
+    def _after_finisher(self, rec, starts, counts, positions):
+        jobs = np.stack([np.asarray(positions, np.int64), np.asarray(counts, np.int64),
+                         np.asarray(starts, np.int64), self._seg_buf], 1)
+        (d_jobs,) = self.up(jobs)
+        self.hip.ex_local_fix(hb._stream(), self.E[0].data_ptr(), self.E[1].data_ptr(), self.n,
+                              d_jobs.data_ptr(), jobs.shape[0], rec.data_ptr())
+        self._keep_fix = d_jobs
 
     def _chunks(self, starts, counts):
         """Chunk items {id, segment start, chunk start, chunk count} + first item per id."""

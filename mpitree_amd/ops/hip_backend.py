@@ -724,6 +724,7 @@ class HipBackend:
                                st[order]], 1)
         (d_jobs,) = self.up(jobs)
         self.launch_finisher(d_jobs, J, int(counts.sum()), params, rec, cnt)
+        self._after_finisher(rec, starts, counts, positions)
         if not table_mode:
             return None
         # compact the private position space into the merge table
@@ -745,6 +746,9 @@ class HipBackend:
         roots = rank[torch.from_numpy(positions).to(self.device)].cpu().numpy().astype(np.int64)
         return dict(feature=ni[:, 0], bin=ni[:, 1], left=ni[:, 2], right=ni[:, 3],
                     depth=ni[:, 4], nsamp=ni[:, 5], stats=nc, roots=roots, i32=ni, cnt=nc)
+
+    def _after_finisher(self, rec, starts, counts, positions):
+        """Hook on the finished position records (the exact engine maps codes back)."""
 
     def sync(self):
         if self.timing:

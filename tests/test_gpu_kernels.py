@@ -381,23 +381,45 @@ def test_gpu_regression_tiny_prefilter_matches_host(kind):
 
 
 @pytest.mark.parametrize("crit", ["entropy", "gini"])
-@pytest.mark.parametrize("shape", [(3000, 3, 2, None), (20000, 6, 3, None), (5000, 4, 5, 6)])
+@pytest.mark.parametrize("shape", [(3000, 3, 2, None, 1), (20000, 6, 3, None, 1),
+                                   (5000, 4, 5, 6, 1), (12000, 70, 2, None, 1),
+                                   (8000, 5, 2, None, 3)])
 def test_gpu_exact_engine_matches_host(crit, shape):
     """Continuous features (> 256 unique values) with the exact default: the
-    presorted-list engine (exact.hip) builds the host builder's tree bit for bit."""
-    n, F, C, md = shape
+    presorted-list engine (exact.hip), whose <= 256-row subtrees continue in the
+    histogram finisher on local codes, builds the host builder's tree bit for bit."""
+    n, F, C, md, msl = shape
     rng = np.random.default_rng(n + F)
     X = np.round(rng.normal(size=(n, F)), 4).astype(np.float32)
     X[:, 0] = np.round(X[:, 0], 1)  # many ties on one feature
     s = X[:, 0] + 0.7 * X[:, 1] + rng.normal(scale=0.8, size=n)
     y = np.digitize(s, np.quantile(s, np.linspace(0, 1, C + 1)[1:-1]))
-    g = DecisionTreeClassifier(criterion=crit, max_depth=md, device="cuda").fit(X, y)
+    kw = dict(criterion=crit, max_depth=md, min_samples_leaf=msl, min_samples_split=2 * msl + 1)
+    g = DecisionTreeClassifier(device="cuda", **kw).fit(X, y)
     assert g.fit_stats_["engine"] == "hip-exact"
-    h = DecisionTreeClassifier(criterion=crit, max_depth=md, device="cpu").fit(X, y)
+    if md is None:
+        assert g.fit_stats_.get("finisher_subtrees", 0) > 0
+    h = DecisionTreeClassifier(device="cpu", **kw).fit(X, y)
     assert g.tree_arrays_.equal(h.tree_arrays_)
     np.testing.assert_array_equal(g.tree_arrays_.threshold, h.tree_arrays_.threshold)
     assert g.export_text(precision=17) == h.export_text(precision=17)
     np.testing.assert_array_equal(g.predict(X), h.predict(X))
+
+
+def test_gpu_exact_finisher_handoff_same_tree(monkeypatch):
+    """The exact engine's finisher hand-off changes no split: the same tree with
+    the list engine growing every level (MPITREE_EXACT_FINISHER_ROWS=0)."""
+    rng = np.random.default_rng(11)
+    X = rng.normal(size=(30000, 12)).astype(np.float32)
+    X[:, 3] = np.round(X[:, 3], 2)
+    y = ((X[:, 0] + X[:, 1] * X[:, 2] + rng.normal(scale=0.5, size=30000)) > 0).astype(np.int64)
+    a = DecisionTreeClassifier(device="cuda").fit(X, y)
+    assert a.fit_stats_.get("finisher_subtrees", 0) > 0
+    monkeypatch.setenv("MPITREE_EXACT_FINISHER_ROWS", "0")
+    b = DecisionTreeClassifier(device="cuda").fit(X, y)
+    assert b.fit_stats_.get("finisher_subtrees", 0) == 0
+    assert a.tree_arrays_.equal(b.tree_arrays_)
+    np.testing.assert_array_equal(a.tree_arrays_.threshold, b.tree_arrays_.threshold)
 
 
 def test_gpu_exact_engine_device_tensors_and_quantile_optin():
