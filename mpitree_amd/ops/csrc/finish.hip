@@ -1422,11 +1422,15 @@ __global__ __launch_bounds__(kW * kWave) void finish_tiny_sorted_kernel(
 // Waves per workgroup of the sorted tiny kernel: the most resident waves per CU
 // under the LDS budget and the VGPR cap (<= 128 VGPRs: 4 waves per SIMD), fewer
 // waves per workgroup on ties.
+static int tiny_sorted_lds(int F, int w) {  // static + dynamic LDS of one workgroup
+  return kTinyH * 8 + (kTinyRows + 1) * 4 + w * 16 * 16 + w * tiny_wave_bytes(F);
+}
+
 static int tiny_sorted_waves(int F) {
   constexpr int kLdsPerCu = 160 * 1024, kWavesPerCu = 16;
   int best_w = 4, best = 0;
   for (int w : {4, 8, 16}) {
-    const int bytes = kTinyH * 8 + (kTinyRows + 1) * 4 + w * 16 * 16 + w * tiny_wave_bytes(F);
+    const int bytes = tiny_sorted_lds(F, w);
     const int waves = std::min(kLdsPerCu / bytes, kWavesPerCu / w) * w;
     if (waves > best) best = waves, best_w = w;
   }
@@ -1511,7 +1515,8 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
     const bool sorted = C <= 2 && getenv_int("MPITREE_TINY_SORTED", 1) != 0;
     if (sorted) {
       int w = getenv_int("MPITREE_TINY_WAVES", tiny_sorted_waves(F));
-      w = w >= 16 && 16 * tiny_wave_bytes(F) <= 128 * 1024 ? 16 : (w >= 8 ? 8 : 4);
+      w = w >= 16 && tiny_sorted_lds(F, 16) <= 160 * 1024 ? 16
+          : (w >= 8 && tiny_sorted_lds(F, 8) <= 160 * 1024 ? 8 : 4);
       // tiny_grid counts 4-wave workgroups: keep the total wave count
       const int g = std::max(1, tiny_grid * kTinyWaves / w);
       const size_t lds = (size_t)w * tiny_wave_bytes(F);

@@ -7,6 +7,9 @@ namespace mt {
 
 // The finisher's int32 work counters; words that different workgroups update
 // concurrently sit on separate 128-byte lines (see finish.hip).
+// rows per partition work item (one workgroup): items of one node share its two
+// cursor atomics, so fewer, larger items contend less on that cache line
+constexpr int kPartChunk = 4096;
 constexpr int kFinCounterWords = 128;
 // job_counter words: the claim cursor (0), the tiny-subtree count / cursor, the
 // {completed, handed off} queue word, the finished epoch and the watchdog, each

@@ -424,7 +424,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
   __syncthreads();
   // ---- pass 3: histogram items of the next level's built slots (dp: after the partition)
   if (!a.dp) plan_hist_items(a, sh, NB);
-  // ---- pass 4: partition items of this level's split nodes (1024 rows each)
+  // ---- pass 4: partition items of this level's split nodes (kPartChunk rows each)
   __syncthreads();
   if (tid == 0) sh.carry[3] = 0;
   __syncthreads();
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     int64_t cnt = 0, kk = 0;
     if (j < NS) {
       cnt = a.split[(int64_t)j * 4 + 1];
-      kk = (cnt + 1023) / 1024;
+      kk = (cnt + kPartChunk - 1) / kPartChunk;
       if (kk < 1) kk = 1;
     }
     int tp;
@@ -443,11 +443,11 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     const int pbase = sh.carry[3];
     plan_expand(sh, op_l, tp, [&](int jj, int c) {
       int64_t* it = a.pitems + (int64_t)(pbase + sh.off[jj] + c) * 3;
-      const int64_t c0 = (int64_t)c * 1024;
+      const int64_t c0 = (int64_t)c * kPartChunk;
       const int64_t cn = sh.pb[jj] - c0;
       it[0] = b0 + jj;
       it[1] = sh.pa[jj] + c0;
-      it[2] = cn < 1024 ? cn : 1024;
+      it[2] = cn < kPartChunk ? cn : kPartChunk;
     });
     __syncthreads();
     if (tid == 0) sh.carry[3] += tp;

@@ -7,7 +7,7 @@
 // segment. The split feature is read from the feature-major code matrix, a
 // single 1-byte column per node that stays L2-resident.
 //
-// Each workgroup handles a 1024-row chunk of one split node's segment, counts
+// Each workgroup handles a <= kPartChunk-row chunk of one split node's segment, counts
 // its left rows with wave prefix sums, reserves space with one atomic per
 // cursor (left cursor grows from the segment start, right cursor shrinks from
 // the segment end) and scatters into a temporary buffer; a copy kernel writes
@@ -18,11 +18,12 @@
 #include <climits>
 
 #include "common.h"
+#include "grow.h"
 
 namespace mt {
 
 constexpr int kPartThreads = 256;
-constexpr int kPartRows = 4;  // rows per thread -> 1024 rows per workgroup
+constexpr int kPartRows = kPartChunk / kPartThreads;  // rows per thread (grow.h)
 
 // items: int64 [n][3] = {split j, chunk start, chunk count}
 // split: int64 [k][4] = {seg start, seg count, feature, bin}
