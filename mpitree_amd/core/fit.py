@@ -315,12 +315,15 @@ def fit_tree(
         from ..ops.exact_backend import exact_supported, needs_exact
 
         if max_bins is None and g_mapper is None and needs_exact(mapper):
-            if exact_supported(n, C, regression) and checkpoint is None:
+            if exact_supported(n, C, regression):
+                if checkpoint is not None:  # the same tree, just no mid-fit state
+                    logger.warning("the exact-threshold GPU engine keeps no level "
+                                   "checkpoint: fitting without one")
                 return _fit_exact_gpu(Xd, yd, classes, C, crit, params, comm, timings, t0,
                                       t_start, F)
             logger.warning("exact thresholds on > 256-value features are not available on "
-                           "the GPU for this fit (regression, >= 2^24 rows, > 256 classes or "
-                           "a level checkpoint): using 256 quantile bins per feature")
+                           "the GPU for this fit (regression, >= 2^24 rows or > 256 "
+                           "classes): using 256 quantile bins per feature")
         lo, hi = comm.local_rows(n)
         if (lo, hi) != (0, n):  # data-parallel shard of a replicated input
             codes_rm = codes_rm[lo:hi].contiguous()
@@ -352,6 +355,8 @@ def fit_tree(
         params.finisher_rows = int(finisher_rows)
         from ..ops.device_grower import DeviceGrower, device_loop_supported
 
+        if (lo, hi) == (0, n) and be.small_fit_supported(comm):
+            checkpoint = None  # one kernel launch: nothing to resume
         ckpt = _level_checkpoint(checkpoint, codes_rm, yd, params, C)
         if ckpt is None and (lo, hi) == (0, n) and be.small_fit_supported(comm):
             # <= 1024 rows: the whole tree in one workgroup, any class count
@@ -360,16 +365,17 @@ def fit_tree(
                 ta = be.fit_small(params, edges_h, d_edges=prep.d_edges64)
             eng = "hip-small"
             stats = {}
-        elif ckpt is None and device_loop_supported(be, params, comm):
+        elif device_loop_supported(be, params, comm):
             if comm.world_size > 1:  # the redundant top levels use the 1-GPU split point
                 params.finisher_rows = min(default_fr, be.max_finisher_rows)
-            builder = DeviceGrower(be, params, comm)
+            builder = DeviceGrower(be, params, comm, checkpoint=ckpt)
             with roctx_range("mpitree.grow"):
                 ta = builder.fit(hi - lo, C, F, mapper, y_exp, root=root,
                                  d_edges=prep.d_edges64)
             eng = "hip-device-loop"
-        else:
-            builder = LevelwiseBuilder(be, params, comm, checkpoint=ckpt)
+        else:  # (host-driven levels: per-process checkpoints only)
+            builder = LevelwiseBuilder(be, params, comm,
+                                       checkpoint=ckpt if comm.world_size == 1 else None)
             with roctx_range("mpitree.grow"):
                 ta = builder.fit(hi - lo, C, F, edges=mapper.padded_edges(), y_exp=y_exp)
             eng = "hip-levelwise"
@@ -404,6 +410,9 @@ def fit_tree(
             be = NumpyBackend()
             be.setup(codes, yh, n_bins=mapper.max_n_bins, n_classes=C, criterion=crit)
             params.finisher_rows = int(finisher_rows or 0)
+            if checkpoint is not None and comm.world_size > 1:
+                logger.warning("level checkpoints of multi-process CPU fits are not kept")
+                checkpoint = None
             builder = LevelwiseBuilder(be, params, comm,
                                        checkpoint=_level_checkpoint(checkpoint, codes, yh,
                                                                     params, C))

@@ -110,9 +110,10 @@ class _BaseTree(BaseEstimator):
     def fit(self, X, y, *, checkpoint=None):
         """Grow the tree on ``X`` (n, F) and targets ``y`` (n,).
 
-        ``checkpoint``: a file path; the level-wise builder saves its state
-        there after every level and a re-run of the same fit resumes from the
-        last saved level (``utils/level_checkpoint.py``; single process)."""
+        ``checkpoint``: a file path; the grower (the GPU's device level loop or
+        the level-wise builder) saves its state there after every level and a
+        re-run of the same fit resumes from the last saved level
+        (``utils/level_checkpoint.py``)."""
         if checkpoint is not None:
             return self._fit_impl(X, y, checkpoint=checkpoint)
         return self._fit_impl(X, y)
@@ -333,14 +334,16 @@ class _ParallelMixin:
     WORLD_RANK = _WorldAttr("rank")
     WORLD_SIZE = _WorldAttr("size")
 
-    def fit(self, X, y, *, data_sharded: bool = False):
+    def fit(self, X, y, *, data_sharded: bool = False, checkpoint=None):
         """Collective fit. Failure handling the reference lacks (an exception
         on one rank there deadlocks the others, ``decision_tree.py:446-477``):
         every rank reports its status in one all-reduce after the fit, so an
         error on any rank raises on all of them; a cross-rank digest check
         (``MPITREE_CHECK_CONSISTENCY``, default on) verifies every rank holds
         the same tree. Hangs are bounded by the process-group timeout
-        (``MPITREE_DIST_TIMEOUT`` seconds)."""
+        (``MPITREE_DIST_TIMEOUT`` seconds). ``checkpoint``: a path every rank
+        passes; GPU ranks save per-rank device-loop state there after every
+        level and resume from the newest level all of them hold."""
         from ..parallel.strategies import make_comm
         from ..utils.observability import maybe_inject_fault, tree_digest
 
@@ -352,8 +355,11 @@ class _ParallelMixin:
             data_sharded=data_sharded,
             regression=self._regression,
         )
+        kw = dict(comm.fit_kwargs())
+        if checkpoint is not None:
+            kw["checkpoint"] = checkpoint
         if getattr(comm, "world_size", 1) == 1:
-            return self._fit_impl(X, y, comm=comm, **comm.fit_kwargs())
+            return self._fit_impl(X, y, comm=comm, **kw)
         # pre-flight (fault injection / MPITREE_PREFLIGHT=1): a rank that cannot
         # start makes every rank raise instead of leaving the others blocked in a
         # collective. Off by default: every rank validates the same replicated
@@ -366,7 +372,7 @@ class _ParallelMixin:
                 error = e
             self._raise_if_any_failed(comm, error)
         try:
-            self._fit_impl(X, y, comm=comm, **comm.fit_kwargs())
+            self._fit_impl(X, y, comm=comm, **kw)
         except Exception as e:  # reported to every rank below
             error = e
         # one all-gather of {failed, tree digest}: failure propagation + consistency

@@ -110,12 +110,60 @@ def device_loop_supported(be, params, comm) -> bool:
 
 
 class DeviceGrower:
-    def __init__(self, be, params, comm=None):
+    def __init__(self, be, params, comm=None, checkpoint=None):
         self.be = be
         self.p = params
         self.comm = comm
+        self.ckpt = checkpoint  # utils/level_checkpoint.LevelCheckpoint (or None)
         self.timings: dict = {}
         self.stats: dict = {}
+
+    # ------------------------------------------------------- checkpoint
+    def _ckpt_save(self, lvl, ws, sets, hists, rank, P):
+        """After level ``lvl``'s kernels: one sync, then the loop's device state
+        (nothing is saved once the next frontier is empty: the fit is about to
+        finish)."""
+        be = self.be
+        torch.cuda.synchronize(be.device)
+        nxt = sets[(lvl + 1) % 2]
+        if int(nxt["ctl"][0]) == 0:
+            return
+        kc = int(sets[lvl % 2]["ctl"][0])  # this level's frontier (the next derives from it)
+        jc = int(ws["job_count"][0])
+        arrs = {"set_" + k: v.cpu().numpy() for k, v in nxt.items()}
+        arrs["hist"] = hists[lvl % 2][: max(kc, 1)].cpu().numpy()
+        arrs["hist_k"] = np.array([kc], np.int64)
+        arrs["pos_rec"] = be.pos_rec.cpu().numpy()
+        arrs["pos_st"] = be.pos_st.cpu().numpy()
+        arrs["jobs"] = ws["jobs"][: max(jc, 1)].cpu().numpy()
+        arrs["job_count"] = np.array([jc], np.int64)
+        arrs["idx"] = be.idx.cpu().numpy()
+        arrs["tmp"] = be.tmp.cpu().numpy()
+        self.ckpt.save_device(lvl, arrs, rank, P)
+
+    def _ckpt_restore(self, st, ws, sets, hists):
+        """Load a saved level's state into the workspace; returns that level."""
+        be = self.be
+        lvl = int(st["level"][0])
+        dev = be.device
+
+        def put(dst, a):
+            dst.copy_(torch.from_numpy(np.ascontiguousarray(a)).to(dev))
+
+        for k, v in sets[(lvl + 1) % 2].items():
+            put(v, st["set_" + k])
+        kc = int(st["hist_k"][0])
+        if kc:
+            put(hists[lvl % 2][:kc], st["hist"])
+        put(be.pos_rec, st["pos_rec"])
+        put(be.pos_st, st["pos_st"])
+        jc = int(st["job_count"][0])
+        if jc:
+            put(ws["jobs"][:jc], st["jobs"][:jc])
+        ws["job_count"].fill_(jc)
+        put(be.idx, st["idx"])
+        put(be.tmp, st["tmp"])
+        return lvl
 
     # ------------------------------------------------------------ buffers
     def _lists(self, KMAX, IMAX, TMAX, MMAX, C, reg, dev):
@@ -406,15 +454,27 @@ class DeviceGrower:
             _FIT_SEQ[0] = (_FIT_SEQ[0] + 1) % (1 << 18)
             tag0 = _FIT_SEQ[0] << 12
             ptrs = [self._ptrs(x) for x in sets]
-            # level 0: the root, built from rows (one init launch; root stats H2D)
-            chunk = int(min(hb.MAX_ITEM_ROWS, max(1024, -(-n_loc // (2 * hb.N_CU)))))
-            ws["root_host"].numpy()[: root_full.size] = root_full
-            ws["root"].copy_(ws["root_host"], non_blocking=True)
-            hip.grow_init(s(), ptrs[0], n_loc, n, chunk, C, int(reg), ws["root"].data_ptr(),
-                          job_count.data_ptr())
+            ck, rank = self.ckpt, int(getattr(comm, "rank", 0))
+            state = None
+            if ck is not None:
+                state = ck.load_device(rank, P, (lambda a: comm._all_gather(a)) if P > 1
+                                       else None)
+            first_lvl = 0  # levels before it ran in an earlier process (resume)
+            if state is not None:
+                first_lvl = self._ckpt_restore(state, ws, sets, hists) + 1
+                self.stats["resumed_from_level"] = first_lvl - 1
+                del state
+            else:
+                # level 0: the root, built from rows (one init launch; root stats H2D)
+                chunk = int(min(hb.MAX_ITEM_ROWS, max(1024, -(-n_loc // (2 * hb.N_CU)))))
+                ws["root_host"].numpy()[: root_full.size] = root_full
+                ws["root"].copy_(ws["root_host"], non_blocking=True)
+                hip.grow_init(s(), ptrs[0], n_loc, n, chunk, C, int(reg), ws["root"].data_ptr(),
+                              job_count.data_ptr())
+            ck_every = max(1, int(os.environ.get("MPITREE_CKPT_EVERY", "1")))
             cb, rs = be.cb, be.row_elems * be.cb
             bufs = (be.idx.data_ptr(), be.tmp.data_ptr())
-            lvl = 0
+            lvl = first_lvl
             done_at = None
             prof = profiling()
             marks = []  # per level: events at start and after hist, derive, scan, plan, partition
@@ -464,10 +524,11 @@ class DeviceGrower:
                                           H.data_ptr(), F_h, B, C, ctl + 4 * 3, ctl + 4 * 7,
                                           zero=False)
                 if dp:  # sum the built slots' histograms over the row shards
-                    if lvl >= 2:  # built slots <= splits of the previous level (lagged read)
+                    # built slots <= splits of the previous level (lagged read)
+                    if lvl - 2 >= first_lvl:
                         nbb = int(hctl[(lvl - 2) % 64, 0])
                     else:
-                        nbb = 1
+                        nbb = 1 if lvl < 2 else KMAX  # (resumed: no lagged value yet)
                     nbb = max(1, min(nbb, KMAX))
                     comm.all_reduce_device(H[:nbb])
                 mark()
@@ -503,10 +564,12 @@ class DeviceGrower:
                 mark()
                 if comm is not None and P > 1:
                     comm_bytes.append(int(getattr(comm, "bytes_communicated", 0) - b0))
+                if ck is not None and (lvl - first_lvl + 1) % ck_every == 0:
+                    self._ckpt_save(lvl, ws, sets, hists, rank, P)
                 # lagged completion check: the planner stored the next level's
                 # frontier size + job count into host slot lvl % 64
                 lvl += 1
-                if lvl >= 2:
+                if lvl - 2 >= first_lvl:
                     _wait_slot(hctl, (lvl - 2) % 64, tag0 + ((lvl - 2) % 4096) + 1)
                     if int(hctl[(lvl - 2) % 64, 0]) == 0:
                         done_at = lvl - 2
@@ -563,6 +626,9 @@ class DeviceGrower:
         ta = be.assemble_positions(table, int(p.criterion), y_exp, d_edges=d_edges,
                                    host_table=table)
         self.timings["assemble"] = time.perf_counter() - t0
+        if self.ckpt is not None:
+            self.stats["checkpoint_levels_saved"] = self.ckpt.saved_levels
+            self.ckpt.clear()
         ev = getattr(self, "_sim_events", None)
         if ev is not None:
             ev[2].synchronize()

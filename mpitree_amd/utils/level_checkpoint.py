@@ -19,7 +19,18 @@ A later ``fit`` with the same ``path`` and problem resumes after the last
 saved level; its tree is identical to an uninterrupted fit's (the sibling
 subtraction of the resumed level is replaced by histogram builds, which give
 the same integer histograms). The file is removed when the fit completes.
-Single-process fits only (the state is per rank).
+
+GPU fits keep the device-driven level loop (``ops/device_grower.py``): after a
+level's kernels the grower synchronises once and saves the loop's device state
+-- the next frontier's work lists, the level's histograms (the next level
+derives siblings from them), the pre-order position space, the finisher jobs
+and both row-permutation buffers -- and a resumed fit restores it and carries
+on from the next level (:meth:`LevelCheckpoint.save_device`,
+:meth:`LevelCheckpoint.load_device`). ``MPITREE_CKPT_EVERY=k`` saves every
+k-th level. Multi-GPU fits save one file per rank in two generations (levels
+alternate between them); on resume the ranks all-gather which levels they
+hold and restart from the newest level every rank has, so a crash between
+two ranks' writes never mixes levels.
 """
 
 from __future__ import annotations
@@ -124,8 +135,64 @@ class LevelCheckpoint:
             out[k] = [np.asarray(a, np.int64)] if a is not None and a.size else []
         return out
 
+    # ------------------------------------------------- device level loop
+    def _dev_files(self, rank: int, world: int) -> list:
+        self._dev_rw = (rank, world)
+        if world <= 1:
+            return [self.path]
+        return [f"{self.path}.r{rank}of{world}.g{g}.npz" for g in (0, 1)]
+
+    def save_device(self, level: int, arrs: dict, rank: int = 0, world: int = 1) -> None:
+        """Write the device loop's state after ``level`` (atomic per file)."""
+        files = self._dev_files(rank, world)
+        dst = files[level % len(files)]
+        out = dict(arrs)
+        out["sig"] = np.frombuffer(self.signature.encode(), np.uint8)
+        out["level"] = np.array([level], np.int64)
+        out["device_loop"] = np.array([1], np.int64)
+        tmp = dst + ".tmp.npz"
+        np.savez(tmp, **out)
+        os.replace(tmp, dst)
+        self.saved_levels += 1
+        if self.fail_after_level is not None and level >= self.fail_after_level:
+            raise CheckpointInterrupt(f"interrupted after level {level} (test hook)")
+
+    def load_device(self, rank: int = 0, world: int = 1, gather=None):
+        """The newest saved device-loop state every rank holds, or None.
+        ``gather(int64 array [2]) -> [world, 2]`` all-gathers each rank's saved
+        levels (multi-rank fits)."""
+        have = {}
+        for f in self._dev_files(rank, world):
+            if not os.path.exists(f):
+                continue
+            with np.load(f, allow_pickle=False) as z:
+                if "device_loop" in z.files and bytes(z["sig"]).decode() == self.signature:
+                    have[int(z["level"][0])] = f
+        if world > 1:
+            mine = np.full(2, -1, np.int64)
+            lv = sorted(have)[-2:]
+            mine[: len(lv)] = lv
+            allv = np.asarray(gather(mine)).reshape(world, 2)
+            common = set(int(v) for v in allv[0] if v >= 0)
+            for r in range(1, world):
+                common &= set(int(v) for v in allv[r] if v >= 0)
+            level = max(common) if common else -1
+        else:
+            level = max(have) if have else -1
+        if level < 0:
+            return None
+        with np.load(have[level], allow_pickle=False) as z:
+            st = {k: z[k] for k in z.files}
+        self.resumed_from = level
+        return st
+
     def clear(self) -> None:
-        for p in (self.path, self.path + ".tmp.npz"):
+        paths = [self.path, self.path + ".tmp.npz"]
+        rw = getattr(self, "_dev_rw", None)
+        if rw is not None and rw[1] > 1:
+            for f in self._dev_files(*rw):
+                paths += [f, f + ".tmp.npz"]
+        for p in paths:
             if os.path.exists(p):
                 os.remove(p)
 

@@ -63,19 +63,77 @@ def test_checkpoint_of_other_data_is_ignored(tmp_path):
 
 
 @pytest.mark.gpu
-def test_gpu_resume_equals_device_loop(tmp_path):
+@pytest.mark.parametrize("regression", [False, True])
+def test_gpu_resume_equals_device_loop(tmp_path, regression):
+    """A checkpointed GPU fit keeps the device-driven level loop; interrupted
+    after level 3 and resumed, it restores the loop's device state and builds
+    the uninterrupted tree."""
+    from mpitree_amd.utils.datasets import make_classification, make_regression
+
+    if regression:
+        X, y = make_regression(150_000, 12, levels=64, seed=3, device="cuda")
+        make = lambda: DecisionTreeRegressor(device="cuda")  # noqa: E731
+    else:
+        X, y = make_classification(200_000, 16, n_classes=3, seed=2, device="cuda")
+        make = lambda: DecisionTreeClassifier(device="cuda")  # noqa: E731
+    ref = make().fit(X, y)
+    assert ref.fit_stats_["engine"] == "hip-device-loop"
+    full = make().fit(X, y, checkpoint=str(tmp_path / "f.npz"))
+    assert full.fit_stats_["engine"] == "hip-device-loop"
+    assert full.fit_stats_["checkpoint_levels_saved"] >= 3
+    assert full._arrays.equal(ref._arrays, check_impurity=False)
+    res = _interrupted_then_resumed(make, X, y, tmp_path / "g.npz", 3)
+    assert res.fit_stats_["engine"] == "hip-device-loop"
+    assert res._arrays.equal(ref._arrays, check_impurity=False)
+    a, b = res.predict(X[:5000]), ref.predict(X[:5000])
+    np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
+
+
+def _ckpt_rank(rank, world, path, strategy, stop):
+    import torch
+
+    from mpitree_amd import ParallelDecisionTreeClassifier
+    from mpitree_amd.utils.datasets import make_classification
+
+    X, y = make_classification(200_000, 16, seed=9, device=torch.device("cuda", 0))
+    make = lambda: ParallelDecisionTreeClassifier(strategy=strategy, device="cuda")  # noqa: E731
+    ck = LevelCheckpoint(path)
+    ck.fail_after_level = stop
+    try:
+        make().fit(X, y, checkpoint=ck)
+        raised = 0
+    except CheckpointInterrupt:
+        raised = 1
+    est = make().fit(X, y, checkpoint=path)
+    ta = est.tree_arrays_
+    left = [f for f in os.listdir(os.path.dirname(path)) if f.startswith(os.path.basename(path))]
+    return dict(feature=ta.feature, threshold=ta.threshold, n=ta.n_samples,
+                raised=np.array([raised]), resumed=np.array([est.fit_stats_["resumed_from_level"]]),
+                engine=np.array([est.fit_stats_["engine"]]), left=np.array([len(left)]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy", ["data", "feature"])
+def test_gpu_ranks_resume(tmp_path, strategy):
+    """Two ranks (gloo, sharing one GPU): per-rank device-loop checkpoints, the
+    ranks agree on the level to resume from, and the resumed trees equal the
+    single-GPU tree."""
     import torch
 
     from mpitree_amd.utils.datasets import make_classification
+    from tests.dist_utils import run_ranks
 
-    X, y = make_classification(200_000, 16, n_classes=3, seed=2, device="cuda")
-    make = lambda: DecisionTreeClassifier(device="cuda")  # noqa: E731
-    ref = make().fit(X, y)
-    assert ref.fit_stats_["engine"] == "hip-device-loop"
-    res = _interrupted_then_resumed(make, X, y, tmp_path / "g.npz", 3)
-    assert res.fit_stats_["engine"] == "hip-levelwise"
-    assert res._arrays.equal(ref._arrays, check_impurity=False)
-    assert torch.cuda.is_available()
+    path = str(tmp_path / "d.npz")
+    outs = run_ranks(_ckpt_rank, 2, path, strategy, 2, start_method="spawn")
+    X, y = make_classification(200_000, 16, seed=9, device=torch.device("cuda", 0))
+    ref = DecisionTreeClassifier(device="cuda").fit(X, y).tree_arrays_
+    for o in outs:
+        assert int(o["raised"][0]) == 1 and int(o["resumed"][0]) == 2
+        assert str(o["engine"][0]) == "hip-device-loop"
+        assert int(o["left"][0]) == 0  # every rank's files removed after the fit
+        np.testing.assert_array_equal(o["feature"], ref.feature)
+        np.testing.assert_array_equal(o["threshold"], ref.threshold)
+        np.testing.assert_array_equal(o["n"], ref.n_samples)
 
 
 def test_signature_covers_every_row():
@@ -95,3 +153,25 @@ def test_signature_covers_every_row():
         y2 = y.copy()
         y2[r] ^= 1
         assert problem_signature(codes, y2, p, 2) != base
+
+
+def test_device_checkpoint_generations_agree(tmp_path):
+    """Multi-rank device checkpoints: two generations per rank, and the ranks
+    resume from the newest level all of them hold (a crash between two ranks'
+    writes leaves them one level apart)."""
+    path = str(tmp_path / "m.npz")
+    cks = [LevelCheckpoint(path, "sig") for _ in range(2)]
+    for lvl in (1, 2, 3):
+        cks[0].save_device(lvl, {"x": np.array([lvl])}, rank=0, world=2)
+    for lvl in (1, 2):  # rank 1 died before writing level 3
+        cks[1].save_device(lvl, {"x": np.array([lvl])}, rank=1, world=2)
+    have = [np.array([2, 3]), np.array([1, 2])]
+    gather = lambda a: np.stack(have)  # noqa: E731
+    for r in range(2):
+        st = LevelCheckpoint(path, "sig").load_device(rank=r, world=2, gather=gather)
+        assert int(st["level"][0]) == 2 and int(st["x"][0]) == 2
+    assert LevelCheckpoint(path, "other").load_device(0, 2, lambda a: np.stack(
+        [a, a])) is None  # different problem: nothing to resume
+    for r, ck in enumerate(cks):
+        ck.clear()
+    assert not [f for f in os.listdir(tmp_path) if f.startswith("m.npz")]
