@@ -27,7 +27,7 @@ void launch_hist_derive(hipStream_t, const int64_t*, int, const void*, void*, in
                         const int32_t*);
 void launch_scan(hipStream_t, const void*, const int64_t*, int, const int32_t*, int, int, int,
                  int, int, int, double*, int32_t*, int64_t*, const double*, int,
-                 const int32_t*);
+                 const int32_t*, const int64_t*, const void*, const int32_t*);
 void launch_partition(hipStream_t, const void*, int, int64_t, uint32_t*, uint32_t*, uint32_t,
                       const int64_t*, int, const int64_t*, int32_t*, const int32_t*, bool);
 void launch_seg_stats(hipStream_t, const uint32_t*, const void*, int, bool, const int64_t*, int,
@@ -127,14 +127,16 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("E"), py::arg("is64"), py::arg("dcount") = 0);
   m.def("scan", [](uintptr_t s, uintptr_t hist, uintptr_t nodes, int k, uintptr_t nbins, int F_h,
                    int f_lo, int B, int C, int crit, int msl, uintptr_t cost, uintptr_t bins,
-                   uintptr_t rec, uintptr_t xtab, int xtab_n, uintptr_t dcount) {
+                   uintptr_t rec, uintptr_t xtab, int xtab_n, uintptr_t dcount, uintptr_t der,
+                   uintptr_t prev, uintptr_t nbuilt) {
     mt::launch_scan(S(s), P<void>(hist), P<int64_t>(nodes), k, P<int32_t>(nbins), F_h, f_lo, B, C,
                     crit, msl, P<double>(cost), P<int32_t>(bins), P<int64_t>(rec),
-                    P<double>(xtab), xtab_n, P<int32_t>(dcount));
+                    P<double>(xtab), xtab_n, P<int32_t>(dcount), P<int64_t>(der), P<void>(prev),
+                    P<int32_t>(nbuilt));
   }, "", py::arg("s"), py::arg("hist"), py::arg("nodes"), py::arg("k"), py::arg("nbins"),
      py::arg("F_h"), py::arg("f_lo"), py::arg("B"), py::arg("C"), py::arg("crit"), py::arg("msl"),
      py::arg("cost"), py::arg("bins"), py::arg("rec"), py::arg("xtab"), py::arg("xtab_n"),
-     py::arg("dcount") = 0);
+     py::arg("dcount") = 0, py::arg("der") = 0, py::arg("prev") = 0, py::arg("nbuilt") = 0);
   m.def("partition", [](uintptr_t s, uintptr_t codes_fm, int cb, int64_t n_rows, uintptr_t idx,
                         uintptr_t tmp, uint32_t mask, uintptr_t items, int n_items,
                         uintptr_t split, uintptr_t cursors, uintptr_t dcount, bool copy_back) {

@@ -26,23 +26,49 @@ __device__ __forceinline__ double tlog(uint64_t x, const double* __restrict__ ta
 
 // hist: uint32 [slots][F_h][B][C]; nodes: int64 [k] slot ids
 // out_cost: f64 [k][F_h]; out_bin: i32 [k][F_h]
+// Fused sibling derivation (device level loop): with ``der``, slots >= *nbuilt
+// are derived, der[slot - nbuilt] = {slot, parent slot in ``prev``, built
+// sibling slot}; the wave writes its feature's parent - sibling histogram into
+// ``hist`` (the select kernel and the next level read it) and scans the copy it
+// keeps in LDS -- one launch per level less than a separate derive kernel.
 __global__ __launch_bounds__(256) void scan_cls_kernel(
-    const uint32_t* __restrict__ hist, const int64_t* __restrict__ nodes,
+    uint32_t* __restrict__ hist, const int64_t* __restrict__ nodes,
     const int32_t* __restrict__ nbins, int F_h, int f_lo, int B, int C, int crit, int msl,
     double* __restrict__ out_cost, int32_t* __restrict__ out_bin,
-    const double* __restrict__ xtab, int xtab_n, const int32_t* __restrict__ dcount) {
+    const double* __restrict__ xtab, int xtab_n, const int32_t* __restrict__ dcount,
+    const int64_t* __restrict__ der, const uint32_t* __restrict__ prev,
+    const int32_t* __restrict__ nbuilt) {
   if (dcount && (int)blockIdx.x >= *dcount) return;  // device-side node count
-  extern __shared__ uint32_t sm[];  // per wave: C class totals + C carries
+  extern __shared__ uint32_t sm[];  // per wave: C class totals + C carries [+ B*C derived]
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
   const int f = blockIdx.y * 4 + wave;
   if (f >= F_h) return;
   const int64_t node = blockIdx.x;
   const int64_t slot = nodes[node];
-  const uint32_t* h = hist + (slot * F_h + f) * (int64_t)B * C;
+  const int64_t E = (int64_t)B * C;
+  const uint32_t* h = hist + (slot * F_h + f) * E;
   uint32_t* tot = sm + wave * 2 * C;
   uint32_t* carry = tot + C;
   const int nb = min(B, nbins[f_lo + f]);
+  if (der != nullptr) {
+    const int NB = *nbuilt;
+    if (slot >= NB) {
+      const int64_t* d = der + (slot - NB) * 3;
+      const uint32_t* pp = prev + (d[1] * F_h + f) * E;
+      const uint32_t* sp = hist + (d[2] * F_h + f) * E;
+      uint32_t* out = hist + (slot * F_h + f) * E;
+      uint32_t* loc = sm + 4 * 2 * C + wave * E;
+      for (int64_t e = lane; e < E; e += kWave) {
+        const uint32_t v = pp[e] - sp[e];
+        loc[e] = v;
+        out[e] = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      h = loc;
+    }
+  }
 
   // pass 1: per-class totals
   uint32_t m = 0;
@@ -376,19 +402,23 @@ __global__ __launch_bounds__(256) void select_kernel(
 void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int k,
                  const int32_t* nbins, int F_h, int f_lo, int B, int C, int crit, int msl,
                  double* cost, int32_t* bins, int64_t* rec, const double* xtab, int xtab_n,
-                 const int32_t* dcount) {
+                 const int32_t* dcount, const int64_t* der, const void* prev,
+                 const int32_t* nbuilt) {
   if (k <= 0) return;
   dim3 grid(k, (F_h + 3) / 4);
   if (crit == kSquaredError) {
     hipLaunchKernelGGL(scan_reg_kernel, grid, dim3(256), 0, stream, (const int64_t*)hist, nodes,
                        nbins, F_h, f_lo, B, msl, cost, bins, dcount);
   } else {
-    size_t lds = (size_t)4 * 2 * C * sizeof(uint32_t);
+    if (der != nullptr && (int64_t)B * C > 4096)
+      throw std::runtime_error("fused derive: at most 4096 bins x classes per feature");
+    size_t lds = (size_t)4 * 2 * C * sizeof(uint32_t) +
+                 (der != nullptr ? (size_t)4 * B * C * sizeof(uint32_t) : 0);
     MT_HIP_CHECK(hipFuncSetAttribute((const void*)scan_cls_kernel,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(scan_cls_kernel, grid, dim3(256), lds, stream, (const uint32_t*)hist,
+    hipLaunchKernelGGL(scan_cls_kernel, grid, dim3(256), lds, stream, (uint32_t*)hist,
                        nodes, nbins, F_h, f_lo, B, C, crit, msl, cost, bins, xtab, xtab_n,
-                       dcount);
+                       dcount, der, (const uint32_t*)prev, nbuilt);
   }
   MT_HIP_CHECK(hipGetLastError());
   const size_t sel_lds = crit == kSquaredError ? 16 : (size_t)2 * C * sizeof(int64_t);

@@ -532,12 +532,17 @@ class DeviceGrower:
                     nbb = max(1, min(nbb, KMAX))
                     comm.all_reduce_device(H[:nbb])
                 mark()
-                if lvl > 0:
+                # classification: the scan derives the larger siblings itself
+                # (parent - built sibling, written back for select / next level)
+                fuse = lvl > 0 and not reg
+                if lvl > 0 and reg:
                     hip.hist_derive(s(), cur["der"], kb, Hp.data_ptr(), H.data_ptr(), E, reg,
                                     dcount=ctl + 4 * 4)
                 hip.scan(s(), H.data_ptr(), ident.data_ptr(), kb, be.nbins.data_ptr(), F_h, f_lo,
                          B, C, int(be.crit), msl, cost.data_ptr(), bins.data_ptr(),
-                         rec.data_ptr(), be.xtab.data_ptr(), hb.XTAB_N, dcount=ctl)
+                         rec.data_ptr(), be.xtab.data_ptr(), hb.XTAB_N, dcount=ctl,
+                         der=cur["der"] if fuse else 0, prev=Hp.data_ptr() if fuse else 0,
+                         nbuilt=ctl + 4 * 1 if fuse else 0)
                 if fp:  # every rank's best split of each node -> the global best
                     g = ws["grec"][: P * kb * R]
                     comm.all_gather_device(g, rec[:kb].reshape(-1))
