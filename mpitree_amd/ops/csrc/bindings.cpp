@@ -60,6 +60,12 @@ void ex_local_codes(hipStream_t, const uint64_t*, const uint64_t*, int64_t, cons
 void ex_local_fix(hipStream_t, const uint64_t*, const uint64_t*, int64_t, const int64_t*, int,
                   int32_t*);
 int ex_local_max();
+size_t exact_setup_temp_bytes(int64_t, int);
+void exact_setup_sort(hipStream_t, const float*, int64_t, int, uint64_t*, uint64_t*, uint32_t*,
+                      uint32_t*, void*, size_t, int32_t*, int32_t*);
+void exact_setup_emit(hipStream_t, const uint64_t*, const uint32_t*, int64_t, int,
+                      const int32_t*, const int32_t*, int, uint64_t*, double*);
+int exact_setup_chunk();
 void launch_fp_combine(hipStream_t, const int64_t*, int, int, int, const int32_t*, int64_t*);
 void launch_grow_dp_fixup(hipStream_t, const PlanArgs&);
 void launch_grow_init(hipStream_t, const LevelLists&, int64_t, int64_t, int64_t, int, int,
@@ -291,6 +297,20 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("fixup") = false);
   m.def("ex_chunk", &mt::ex_chunk);
   m.def("ex_local_max", &mt::ex_local_max);
+  m.def("exact_setup_temp_bytes", &mt::exact_setup_temp_bytes);
+  m.def("exact_setup_chunk", &mt::exact_setup_chunk);
+  m.def("exact_setup_sort", [](uintptr_t s, uintptr_t X, int64_t n, int F, uintptr_t k0,
+                               uintptr_t k1, uintptr_t r0, uintptr_t r1, uintptr_t temp,
+                               size_t temp_bytes, uintptr_t cnt, uintptr_t nuniq) {
+    mt::exact_setup_sort(S(s), P<float>(X), n, F, P<uint64_t>(k0), P<uint64_t>(k1),
+                         P<uint32_t>(r0), P<uint32_t>(r1), P<void>(temp), temp_bytes,
+                         P<int32_t>(cnt), P<int32_t>(nuniq));
+  });
+  m.def("exact_setup_emit", [](uintptr_t s, uintptr_t k1, uintptr_t r1, int64_t n, int F,
+                               uintptr_t cnt, uintptr_t y, int B, uintptr_t E, uintptr_t uniq) {
+    mt::exact_setup_emit(S(s), P<uint64_t>(k1), P<uint32_t>(r1), n, F, P<int32_t>(cnt),
+                         P<int32_t>(y), B, P<uint64_t>(E), P<double>(uniq));
+  });
   m.def("ex_local_codes", [](uintptr_t s, uintptr_t E0, uintptr_t E1, int64_t n, uintptr_t seg,
                              int J, int F, int row_bytes, uintptr_t codes_rm, uintptr_t codes_fm,
                              uintptr_t ent, uintptr_t inv) {

@@ -70,6 +70,9 @@ class ExactHipBackend(HipBackend):
         self.crit = criterion
         self.reg = False
         self.chunk = int(self.hip.ex_chunk())
+        if X.dtype == torch.float32:
+            self._setup_native(X.contiguous(), y_codes)
+            return
         # per feature: values sorted (stable), dense ranks, unique-value table.
         # One 1-D radix sort of 64-bit keys {feature : 32, order-preserving value
         # bits : 32} (radix sorts are stable) instead of a segmented merge sort
@@ -103,6 +106,43 @@ class ExactHipBackend(HipBackend):
         e = (rank << 32) | (lab << 24) | order.to(torch.int64)
         del vals, order, rank, new, lab
         self.E = [e.contiguous(), torch.empty_like(e)]
+        self.cur = 0
+        self.flag = torch.empty(n, dtype=torch.uint8, device=dev)
+        self.xtab = hb.xlog2x_table(dev)
+        self.xtabf = hb.xlog2x_table_f32(dev)
+        self.y = y_codes
+        self._deferred = []
+        self._loc = None
+
+    def _setup_native(self, X: torch.Tensor, y_codes: torch.Tensor):
+        """float32 input (``ops/csrc/exact_setup.hip``): feature-major keys from
+        an LDS-transposed pass over X, one stable radix sort of {feature, value
+        bits} keys with 32-bit row ids, then per-chunk value-change counts, a
+        per-feature scan, and one pass writing the list entries and the unique
+        values. The two key buffers become the two list buffers."""
+        n, F, dev = self.n, self.F, self.device
+        s = hb._stream()
+        keys = [torch.empty((F, n), dtype=torch.int64, device=dev) for _ in range(2)]
+        rows = [torch.empty((F, n), dtype=torch.int32, device=dev) for _ in range(2)]
+        tb = int(self.hip.exact_setup_temp_bytes(n, F))
+        temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
+        nc = -(-n // int(self.hip.exact_setup_chunk()))
+        cnt = torch.empty((F, nc), dtype=torch.int32, device=dev)
+        nuniq = torch.empty(F, dtype=torch.int32, device=dev)
+        self.hip.exact_setup_sort(s, X.data_ptr(), n, F, keys[0].data_ptr(), keys[1].data_ptr(),
+                                  rows[0].data_ptr(), rows[1].data_ptr(), temp.data_ptr(), tb,
+                                  cnt.data_ptr(), nuniq.data_ptr())
+        del temp
+        self.nbins = nuniq
+        self.B = int(nuniq.max())  # (one small sync: the table width)
+        self.uniq = torch.full((F, self.B), float("inf"), dtype=torch.float64, device=dev)
+        y32 = y_codes.to(torch.int32).contiguous()
+        # entries go to keys[0] (the keys the sort consumed); keys[1] is the second list
+        self.hip.exact_setup_emit(s, keys[1].data_ptr(), rows[1].data_ptr(), n, F,
+                                  cnt.data_ptr(), y32.data_ptr(), self.B, keys[0].data_ptr(),
+                                  self.uniq.data_ptr())
+        self.E = [keys[0], keys[1]]
+        del rows, cnt, y32  # (stream-ordered frees: the kernels above run first)
         self.cur = 0
         self.flag = torch.empty(n, dtype=torch.uint8, device=dev)
         self.xtab = hb.xlog2x_table(dev)

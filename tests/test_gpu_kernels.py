@@ -406,6 +406,35 @@ def test_gpu_exact_engine_matches_host(crit, shape):
     np.testing.assert_array_equal(g.predict(X), h.predict(X))
 
 
+def test_gpu_exact_setup_native_equals_torch_path():
+    """float32 inputs take the native setup (exact_setup.hip: transposed keys,
+    one radix sort, rank / entry passes); float64 inputs the torch sort path.
+    Negative zeros, negatives, many ties and > 256 values per feature: the
+    same lists, unique values and tree."""
+    from mpitree_amd.core.criterion import Criterion
+    from mpitree_amd.ops.exact_backend import ExactHipBackend
+
+    rng = np.random.default_rng(21)
+    n, F = 9000, 70
+    X = np.round(rng.normal(size=(n, F)), 3).astype(np.float32)
+    X[rng.random((n, F)) < 0.05] = -0.0
+    X[:, 5] = np.round(X[:, 5], 0)
+    y = rng.integers(0, 3, size=n)
+    yd = torch.from_numpy(y).cuda().to(torch.int32)
+    a, b = ExactHipBackend(), ExactHipBackend()
+    a.setup_exact(torch.from_numpy(X).cuda(), yd, 3, Criterion.ENTROPY)
+    b.setup_exact(torch.from_numpy(X.astype(np.float64)).cuda(), yd, 3, Criterion.ENTROPY)
+    assert a.B == b.B
+    assert torch.equal(a.nbins.cpu(), b.nbins.cpu())
+    # (the float64 sort orders -0.0 before +0.0 rows inside an equal-value run)
+    assert torch.equal(torch.sort(a.E[0], 1)[0].cpu(), torch.sort(b.E[0], 1)[0].cpu())
+    assert torch.equal(a.uniq.cpu(), b.uniq.cpu())
+    g32 = DecisionTreeClassifier(device="cuda").fit(X, y)
+    g64 = DecisionTreeClassifier(device="cuda").fit(X.astype(np.float64), y)
+    assert g32.fit_stats_["engine"] == g64.fit_stats_["engine"] == "hip-exact"
+    assert g32.tree_arrays_.equal(g64.tree_arrays_)
+
+
 def test_gpu_exact_finisher_handoff_same_tree(monkeypatch):
     """The exact engine's finisher hand-off changes no split: the same tree with
     the list engine growing every level (MPITREE_EXACT_FINISHER_ROWS=0)."""
