@@ -76,7 +76,14 @@ __global__ __launch_bounds__(kExThreads) void ex_tot_kernel(const uint64_t* __re
   if (C <= 2) {  // class-1 count by wave sums (LDS atomics on two words serialise)
     const uint64_t* L = E + (int64_t)f * n + c0;
     uint32_t ones = 0;
-    for (int64_t i = threadIdx.x; i < cn; i += kExThreads) ones += ex_lab(L[i]) == 1 ? 1u : 0u;
+    uint64_t e[kExPer];
+#pragma unroll
+    for (int k = 0; k < kExPer; ++k) {  // all loads in flight before the first use
+      const int64_t i = (int64_t)k * kExThreads + threadIdx.x;
+      e[k] = i < cn ? L[i] : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < kExPer; ++k) ones += ex_lab(e[k]) == 1 ? 1u : 0u;
     ones = wave_sum_u32(ones);
     if (lane_id() == 0) cnt[threadIdx.x >> 6] = ones;
     __syncthreads();
@@ -244,10 +251,11 @@ __global__ __launch_bounds__(kExThreads) void ex_scan_c2_kernel(
     const int64_t* __restrict__ seg, const int32_t* __restrict__ carry,
     const int32_t* __restrict__ slot_tot, int F, int64_t msl,
     unsigned long long* __restrict__ best, const double* __restrict__ xtab, int xtab_n) {
-  __shared__ uint32_t s_w[kExThreads / kWave];
-  __shared__ uint32_t s_first[kExThreads];
-  __shared__ unsigned long long s_min[kExThreads / kWave];
-  __shared__ float s_fmin[kExThreads / kWave];
+  constexpr int kWaves = kExThreads / kWave;
+  __shared__ uint32_t s_cnt[kExPer * kWaves];    // class-1 entries of each (step, wave)
+  __shared__ uint32_t s_first[kExPer * kWaves];  // rank of each (step, wave)'s lane 0
+  __shared__ unsigned long long s_min[kWaves];
+  __shared__ float s_fmin[kWaves];
   const int64_t it = blockIdx.x;
   const int f = blockIdx.y;
   const int64_t slot = items[it * 4 + 0], sstart = items[it * 4 + 1];
@@ -255,38 +263,52 @@ __global__ __launch_bounds__(kExThreads) void ex_scan_c2_kernel(
   const int64_t m = seg[slot * 2 + 1];
   const uint64_t* L = E + (int64_t)f * n;
   const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
-  const int64_t p0 = c0 + (int64_t)tid * kExPer;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  // entry i = k * 256 + tid of the chunk (coalesced loads)
   uint64_t e[kExPer];
-  uint32_t run = 0;
-  uint32_t pre[kExPer];
 #pragma unroll
   for (int k = 0; k < kExPer; ++k) {
-    const int64_t p = p0 + k;
-    e[k] = (p - c0) < cn ? L[p] : ~0ull;
-    run += (e[k] != ~0ull && ex_lab(e[k]) == 1) ? 1u : 0u;
-    pre[k] = run;
+    const int64_t i = (int64_t)k * kExThreads + tid;
+    e[k] = i < cn ? L[c0 + i] : ~0ull;
   }
-  s_first[tid] = ex_rank(e[0]);
-  uint32_t total;
-  const uint32_t excl = ex_block_excl(run, s_w, total);  // (its barriers order s_first too)
-  const int64_t pn = p0 + kExPer;
-  uint32_t next_rank = 0xFFFFFFFFu;
-  if (tid + 1 < kExThreads && (pn - c0) < cn)
-    next_rank = s_first[tid + 1];
-  else if ((pn - sstart) < m)
-    next_rank = ex_rank(L[pn]);
+  unsigned long long bal[kExPer];
+#pragma unroll
+  for (int k = 0; k < kExPer; ++k) {
+    bal[k] = __ballot(e[k] != ~0ull && ex_lab(e[k]) == 1);
+    if (lane == 0) {
+      s_cnt[k * kWaves + wave] = (uint32_t)__popcll(bal[k]);
+      s_first[k * kWaves + wave] = ex_rank(e[k]);
+    }
+  }
+  __syncthreads();
+  if (tid < kWave) {  // exclusive scan of the 32 step counts
+    const uint32_t v = tid < kExPer * kWaves ? s_cnt[tid] : 0u;
+    const uint32_t incl = wave_incl_scan_dpp(v);
+    if (tid < kExPer * kWaves) s_cnt[tid] = incl - v;
+  }
+  __syncthreads();
   const int32_t* car = carry + (it * F + f) * 2;
-  const uint32_t base1 = (uint32_t)car[1] + excl;
+  const uint32_t base1 = (uint32_t)car[1];
   const int64_t t0 = slot_tot[slot * 2 + 0], t1 = slot_tot[slot * 2 + 1];
   bool valid[kExPer];
   int64_t l1[kExPer];
 #pragma unroll
   for (int k = 0; k < kExPer; ++k) {
-    const int64_t pos = p0 + k - sstart;
+    const int64_t i = (int64_t)k * kExThreads + tid;
+    const uint32_t r = ex_rank(e[k]);
+    // rank of the next position: the next lane, the next (step, wave)'s lane 0,
+    // or past the chunk the list itself (none past the segment)
+    uint32_t nr = __shfl_down(r, 1, kWave);
+    if (lane == kWave - 1) {
+      const int q = k * kWaves + wave + 1;
+      nr = q < kExPer * kWaves ? s_first[q] : 0xFFFFFFFFu;
+    }
+    if (i + 1 >= cn) nr = (c0 + i + 1 - sstart) < m ? ex_rank(L[c0 + i + 1]) : 0xFFFFFFFFu;
+    const int64_t pos = c0 + i - sstart;
     const int64_t ml = pos + 1, mr = m - ml;
-    const uint32_t nr = k + 1 < kExPer ? ex_rank(e[k + 1]) : next_rank;
-    valid[k] = (p0 + k - c0) < cn && mr > 0 && nr != ex_rank(e[k]) && ml >= msl && mr >= msl;
-    l1[k] = (int64_t)(base1 + pre[k]);
+    valid[k] = i < cn && mr > 0 && nr != r && ml >= msl && mr >= msl;
+    l1[k] = (int64_t)(base1 + s_cnt[k * kWaves + wave] + (uint32_t)__popcll(bal[k] & lt) +
+                      (uint32_t)((bal[k] >> lane) & 1ull));
   }
   // x*log2(x) from the shared table (built by the same xlog2x: identical bits)
   // below xtab_n, the atanh series above it
@@ -297,7 +319,7 @@ __global__ __launch_bounds__(kExThreads) void ex_scan_c2_kernel(
   const double tu = tie_unit(tm, m);
   const double tinv = 1.0 / tu;
   auto exact_key = [&](int k) -> unsigned long long {
-    const int64_t pos = p0 + k - sstart;
+    const int64_t pos = c0 + (int64_t)k * kExThreads + tid - sstart;
     const int64_t ml = pos + 1, mr = m - ml;
     const int64_t L1 = l1[k], L0 = ml - L1, R1 = t1 - L1, R0 = t0 - L0;
     double cost;
@@ -318,7 +340,8 @@ __global__ __launch_bounds__(kExThreads) void ex_scan_c2_kernel(
     float lmin = __builtin_inff();
 #pragma unroll
     for (int k = 0; k < kExPer; ++k) {
-      const uint32_t ml = (uint32_t)(p0 + k - sstart + 1), mr = (uint32_t)(m - ml);
+      const uint32_t ml = (uint32_t)(c0 + (int64_t)k * kExThreads + tid - sstart + 1),
+                     mr = (uint32_t)(m - ml);
       const uint32_t L1 = (uint32_t)l1[k], L0 = ml - L1;
       const uint32_t R1 = (uint32_t)t1 - L1, R0 = (uint32_t)t0 - L0;
       const float c = (ex_t32(ml) - (ex_t32(L0) + ex_t32(L1))) +
@@ -483,11 +506,23 @@ __global__ __launch_bounds__(kExThreads) void ex_pcount_kernel(const uint64_t* _
   const int f = blockIdx.y;
   const int64_t c0 = pitems[it * 4 + 2], cn = pitems[it * 4 + 3];
   const uint64_t* L = E + (int64_t)f * n + c0;
+  uint64_t e[kExPer];
+#pragma unroll
+  for (int k = 0; k < kExPer; ++k) {  // all loads, then all flag gathers, in flight
+    const int64_t i = (int64_t)k * kExThreads + threadIdx.x;
+    e[k] = i < cn ? L[i] : ~0ull;
+  }
   uint32_t v = 0;
-  for (int64_t i = threadIdx.x; i < cn; i += kExThreads) v += flag[ex_row(L[i])];
-  uint32_t total;
-  ex_block_excl(v, s_w, total);
-  if (threadIdx.x == 0) lc[it * F + f] = (int32_t)total;
+#pragma unroll
+  for (int k = 0; k < kExPer; ++k) v += e[k] != ~0ull ? flag[ex_row(e[k])] : 0u;
+  v = wave_sum_u32(v);
+  if (lane_id() == 0) s_w[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t total = 0;
+    for (int w = 0; w < kExThreads / kWave; ++w) total += s_w[w];
+    lc[it * F + f] = (int32_t)total;
+  }
 }
 
 // One thread per (split, feature): exclusive prefix of the chunk left counts
@@ -507,44 +542,54 @@ __global__ __launch_bounds__(kExThreads) void ex_pcarry_kernel(
   if (f == 0) nl[j] = acc;
 }
 
+// Stable partition of one chunk: entry c0 + k * 256 + tid (coalesced loads);
+// its rank among the chunk's left entries is the earlier (k, wave) steps' left
+// counts (one LDS scan over 8 x 4 ballot popcounts) + the lower lanes' bits.
 __global__ __launch_bounds__(kExThreads) void ex_pscatter_kernel(
     const uint64_t* __restrict__ E, uint64_t* __restrict__ D, int64_t n,
     const int64_t* __restrict__ pitems, const int32_t* __restrict__ lcar,
     const int32_t* __restrict__ nl, const uint8_t* __restrict__ flag, int F) {
-  __shared__ uint32_t s_w[kExThreads / kWave];
+  constexpr int kWaves = kExThreads / kWave;
+  __shared__ uint32_t s_cnt[kExPer * kWaves];
   const int64_t it = blockIdx.x;
   const int f = blockIdx.y;
   const int64_t j = pitems[it * 4 + 0], s0 = pitems[it * 4 + 1];
   const int64_t c0 = pitems[it * 4 + 2], cn = pitems[it * 4 + 3];
   const uint64_t* L = E + (int64_t)f * n;
   uint64_t* O = D + (int64_t)f * n;
-  const int64_t p0 = c0 + (int64_t)threadIdx.x * kExPer;
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const unsigned long long lt = (1ull << lane) - 1ull;
   uint64_t e[kExPer];
-  uint32_t fl[kExPer];
-  uint32_t run = 0;
 #pragma unroll
   for (int k = 0; k < kExPer; ++k) {
-    const bool v = (p0 + k - c0) < cn;
-    e[k] = v ? L[p0 + k] : 0ull;
-    fl[k] = v ? flag[ex_row(e[k])] : 0u;
-    run += fl[k];
+    const int64_t i = (int64_t)k * kExThreads + threadIdx.x;
+    e[k] = i < cn ? L[c0 + i] : ~0ull;
   }
-  uint32_t total;
-  const uint32_t excl = ex_block_excl(run, s_w, total);
-  const int64_t lb = (int64_t)lcar[it * F + f] + excl;  // left entries before this thread
-  const int64_t nlj = nl[j];
-  int64_t l = lb;
-  int64_t r = (p0 - s0) - lb;  // right entries before this thread
+  unsigned long long bal[kExPer];
 #pragma unroll
   for (int k = 0; k < kExPer; ++k) {
-    if ((p0 + k - c0) >= cn) break;
-    if (fl[k]) {
+    const bool go = e[k] != ~0ull && flag[ex_row(e[k])] != 0;
+    bal[k] = __ballot(go);
+    if (lane == 0) s_cnt[k * kWaves + w] = (uint32_t)__popcll(bal[k]);
+  }
+  __syncthreads();
+  if (threadIdx.x < kWave) {  // exclusive scan of the 32 step counts
+    const uint32_t v = threadIdx.x < kExPer * kWaves ? s_cnt[threadIdx.x] : 0u;
+    const uint32_t incl = wave_incl_scan_dpp(v);
+    if (threadIdx.x < kExPer * kWaves) s_cnt[threadIdx.x] = incl - v;
+  }
+  __syncthreads();
+  const int64_t lb = (int64_t)lcar[it * F + f];  // left entries of the segment before c0
+  const int64_t nlj = nl[j];
+#pragma unroll
+  for (int k = 0; k < kExPer; ++k) {
+    const int64_t i = (int64_t)k * kExThreads + threadIdx.x;
+    if (i >= cn) break;
+    const int64_t l = lb + s_cnt[k * kWaves + w] + __popcll(bal[k] & lt);  // left before
+    if ((bal[k] >> lane) & 1ull)
       O[s0 + l] = e[k];
-      ++l;
-    } else {
-      O[s0 + nlj + r] = e[k];
-      ++r;
-    }
+    else
+      O[s0 + nlj + (c0 + i - s0) - l] = e[k];
   }
 }
 
