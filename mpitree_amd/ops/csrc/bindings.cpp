@@ -53,8 +53,9 @@ void ex_scan_level(hipStream_t, const uint64_t*, int64_t, const int64_t*, int, c
                    int32_t*, int32_t*, unsigned long long*, int64_t*);
 void ex_partition_level(hipStream_t, const uint64_t*, uint64_t*, int64_t, const int64_t*, int,
                         const int64_t*, const int64_t*, int, int, uint8_t*, int32_t*, int32_t*,
-                        int32_t*);
+                        int32_t*, unsigned long long*);
 int ex_chunk();
+int ex_part_bits_words();
 void ex_local_codes(hipStream_t, const uint64_t*, const uint64_t*, int64_t, const int64_t*, int,
                     int, int, uint8_t*, uint8_t*, uint32_t*, uint32_t*);
 void ex_local_fix(hipStream_t, const uint64_t*, const uint64_t*, int64_t, const int64_t*, int,
@@ -335,11 +336,13 @@ PYBIND11_MODULE(_hip, m) {
   m.def("ex_partition_level", [](uintptr_t s, uintptr_t E, uintptr_t D, int64_t n,
                                  uintptr_t pitems, int NP, uintptr_t pfirst, uintptr_t split,
                                  int Sn, int F, uintptr_t flag, uintptr_t lc, uintptr_t lcar,
-                                 uintptr_t nl) {
+                                 uintptr_t nl, uintptr_t bits) {
     mt::ex_partition_level(S(s), P<uint64_t>(E), P<uint64_t>(D), n, P<int64_t>(pitems), NP,
                            P<int64_t>(pfirst), P<int64_t>(split), Sn, F, P<uint8_t>(flag),
-                           P<int32_t>(lc), P<int32_t>(lcar), P<int32_t>(nl));
+                           P<int32_t>(lc), P<int32_t>(lcar), P<int32_t>(nl),
+                           P<unsigned long long>(bits));
   });
+  m.def("ex_part_bits_words", &mt::ex_part_bits_words);
   m.def("fp_combine", [](uintptr_t s, uintptr_t g, int nranks, int KB, int R, uintptr_t dcount,
                          uintptr_t rec) {
     mt::launch_fp_combine(S(s), P<int64_t>(g), nranks, KB, R, P<int32_t>(dcount),

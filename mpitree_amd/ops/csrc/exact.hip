@@ -497,15 +497,21 @@ __global__ __launch_bounds__(kExThreads) void ex_flag_kernel(const uint64_t* __r
   }
 }
 
+// Left entries of every (chunk, feature): the row flags are gathered once here
+// and kept as one 64-bit ballot per (step, wave) in ``bits`` [NP][F][kExPer][4],
+// so the scatter streams them instead of gathering every flag again.
 __global__ __launch_bounds__(kExThreads) void ex_pcount_kernel(const uint64_t* __restrict__ E,
                                                                int64_t n, const int64_t* __restrict__ pitems,
                                                                const uint8_t* __restrict__ flag, int F,
-                                                               int32_t* __restrict__ lc) {
-  __shared__ uint32_t s_w[kExThreads / kWave];
+                                                               int32_t* __restrict__ lc,
+                                                               unsigned long long* __restrict__ bits) {
+  constexpr int kWaves = kExThreads / kWave;
+  __shared__ uint32_t s_w[kWaves];
   const int64_t it = blockIdx.x;
   const int f = blockIdx.y;
   const int64_t c0 = pitems[it * 4 + 2], cn = pitems[it * 4 + 3];
   const uint64_t* L = E + (int64_t)f * n + c0;
+  const int lane = lane_id(), w = threadIdx.x >> 6;
   uint64_t e[kExPer];
 #pragma unroll
   for (int k = 0; k < kExPer; ++k) {  // all loads, then all flag gathers, in flight
@@ -513,14 +519,20 @@ __global__ __launch_bounds__(kExThreads) void ex_pcount_kernel(const uint64_t* _
     e[k] = i < cn ? L[i] : ~0ull;
   }
   uint32_t v = 0;
+  unsigned long long* B = bits + (it * F + f) * (int64_t)(kExPer * kWaves);
 #pragma unroll
-  for (int k = 0; k < kExPer; ++k) v += e[k] != ~0ull ? flag[ex_row(e[k])] : 0u;
-  v = wave_sum_u32(v);
-  if (lane_id() == 0) s_w[threadIdx.x >> 6] = v;
+  for (int k = 0; k < kExPer; ++k) {
+    const unsigned long long b = __ballot(e[k] != ~0ull && flag[ex_row(e[k])] != 0);
+    if (lane == 0) {
+      B[k * kWaves + w] = b;
+      v += (uint32_t)__popcll(b);
+    }
+  }
+  if (lane == 0) s_w[w] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t total = 0;
-    for (int w = 0; w < kExThreads / kWave; ++w) total += s_w[w];
+    for (int q = 0; q < kWaves; ++q) total += s_w[q];
     lc[it * F + f] = (int32_t)total;
   }
 }
@@ -548,7 +560,7 @@ __global__ __launch_bounds__(kExThreads) void ex_pcarry_kernel(
 __global__ __launch_bounds__(kExThreads) void ex_pscatter_kernel(
     const uint64_t* __restrict__ E, uint64_t* __restrict__ D, int64_t n,
     const int64_t* __restrict__ pitems, const int32_t* __restrict__ lcar,
-    const int32_t* __restrict__ nl, const uint8_t* __restrict__ flag, int F) {
+    const int32_t* __restrict__ nl, const unsigned long long* __restrict__ bits, int F) {
   constexpr int kWaves = kExThreads / kWave;
   __shared__ uint32_t s_cnt[kExPer * kWaves];
   const int64_t it = blockIdx.x;
@@ -565,11 +577,11 @@ __global__ __launch_bounds__(kExThreads) void ex_pscatter_kernel(
     const int64_t i = (int64_t)k * kExThreads + threadIdx.x;
     e[k] = i < cn ? L[c0 + i] : ~0ull;
   }
+  const unsigned long long* Bt = bits + (it * F + f) * (int64_t)(kExPer * kWaves);
   unsigned long long bal[kExPer];
 #pragma unroll
   for (int k = 0; k < kExPer; ++k) {
-    const bool go = e[k] != ~0ull && flag[ex_row(e[k])] != 0;
-    bal[k] = __ballot(go);
+    bal[k] = Bt[k * kWaves + w];  // (wave-uniform: one scalar load)
     if (lane == 0) s_cnt[k * kWaves + w] = (uint32_t)__popcll(bal[k]);
   }
   __syncthreads();
@@ -705,24 +717,26 @@ void ex_scan_level(hipStream_t stream, const uint64_t* E, int64_t n, const int64
 
 void ex_partition_level(hipStream_t stream, const uint64_t* E, uint64_t* D, int64_t n,
                         const int64_t* pitems, int NP, const int64_t* pfirst, const int64_t* split,
-                        int S, int F, uint8_t* flag, int32_t* lc, int32_t* lcar, int32_t* nl) {
+                        int S, int F, uint8_t* flag, int32_t* lc, int32_t* lcar, int32_t* nl,
+                        unsigned long long* bits) {
   if (S <= 0 || NP <= 0) return;
   hipLaunchKernelGGL(ex_flag_kernel, dim3(NP), dim3(kExThreads), 0, stream, E, n, pitems, split,
                      flag);
   MT_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(ex_pcount_kernel, dim3(NP, F), dim3(kExThreads), 0, stream, E, n, pitems,
-                     flag, F, lc);
+                     flag, F, lc, bits);
   MT_HIP_CHECK(hipGetLastError());
   const int64_t ns = (int64_t)S * F;
   hipLaunchKernelGGL(ex_pcarry_kernel, dim3((unsigned)((ns + kExThreads - 1) / kExThreads)),
                      dim3(kExThreads), 0, stream, lc, pfirst, S, F, lcar, nl);
   MT_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(ex_pscatter_kernel, dim3(NP, F), dim3(kExThreads), 0, stream, E, D, n,
-                     pitems, lcar, nl, flag, F);
+                     pitems, lcar, nl, bits, F);
   MT_HIP_CHECK(hipGetLastError());
 }
 
 int ex_chunk() { return kExChunk; }
+int ex_part_bits_words() { return kExPer * (kExThreads / kWave); }  // per (chunk, feature)
 
 void ex_local_codes(hipStream_t stream, const uint64_t* E0, const uint64_t* E1, int64_t n,
                     const int64_t* seg, int J, int F, int row_bytes, uint8_t* codes_rm,

@@ -281,13 +281,17 @@ class ExactHipBackend(HipBackend):
         lc = torch.empty((NP, self.F), dtype=torch.int32, device=dev)
         lcar = torch.empty_like(lc)
         nl = torch.empty(S, dtype=torch.int32, device=dev)
+        # the scatter's left flags, one ballot word per 64 entries (pcount -> pscatter)
+        bits = torch.empty((NP, self.F, int(self.hip.ex_part_bits_words())), dtype=torch.int64,
+                           device=dev)
         src, dst = self.E[self.cur], self.E[1 - self.cur]
         self.hip.ex_partition_level(hb._stream(), src.data_ptr(), dst.data_ptr(), self.n,
                                     d_items.data_ptr(), NP, d_first.data_ptr(),
                                     d_split.data_ptr(), S, self.F, self.flag.data_ptr(),
-                                    lc.data_ptr(), lcar.data_ptr(), nl.data_ptr())
+                                    lc.data_ptr(), lcar.data_ptr(), nl.data_ptr(),
+                                    bits.data_ptr())
         self.cur = 1 - self.cur  # every next-level node lives in the list just written
-        self._keep_p = (d_items, d_first, d_split, lc, lcar)
+        self._keep_p = (d_items, d_first, d_split, lc, lcar, bits)
         if not need_counts:
             self._keep_nl = nl
             return None
