@@ -239,6 +239,7 @@ def fit_tree(
     finisher_rows=None,
     engine: str | None = None,
     checkpoint=None,
+    _sync_prepare: bool = False,
 ) -> FitResult:
     t_start = time.perf_counter()
     X = _validate_X(X)
@@ -308,7 +309,16 @@ def fit_tree(
                 prep = prepare(Xd, y, regression=regression,
                                max_bins=256 if max_bins is None else max_bins,
                                encode_labels=_encode_labels, encode_targets=_encode_targets,
-                               exponent=fixed_point_exponent)
+                               exponent=fixed_point_exponent, sync=_sync_prepare)
+                if prep.verify is not None:
+                    # the bin kernel's flags are read after growth (see prepare): a
+                    # sampled exact-mode feature that missed a value redoes the fit
+                    # with the flags checked first
+                    redo = dict(regression=regression, criterion=criterion,
+                                max_depth=max_depth, min_samples_split=min_samples_split,
+                                min_samples_leaf=min_samples_leaf, max_bins=max_bins,
+                                device=device, comm=comm, finisher_rows=finisher_rows,
+                                engine=engine, checkpoint=checkpoint, _sync_prepare=True)
         mapper, codes_rm, codes_fm, nb = prep.mapper, prep.codes_rm, prep.codes_fm, prep.nbins
         yd, classes, y_exp, root = prep.y, prep.classes, prep.y_exp, prep.root
         C = 0 if regression else len(classes)
@@ -319,6 +329,8 @@ def fit_tree(
                 if checkpoint is not None:  # the same tree, just no mid-fit state
                     logger.warning("the exact-threshold GPU engine keeps no level "
                                    "checkpoint: fitting without one")
+                if prep.verify is not None and not prep.verify():
+                    return fit_tree(X, y, **redo)
                 return _fit_exact_gpu(Xd, yd, classes, C, crit, params, comm, timings, t0,
                                       t_start, F)
             logger.warning("exact thresholds on > 256-value features are not available on "
@@ -382,6 +394,8 @@ def fit_tree(
         if eng != "hip-small":
             timings.update(builder.timings)
             stats = dict(builder.stats)
+        if prep.verify is not None and not prep.verify():  # (the assembly has synced)
+            return fit_tree(X, y, **redo)
     else:
         Xh = X.cpu().numpy() if _is_tensor(X) else X
         if _is_tensor(X) and X.is_cuda and not np.isfinite(Xh).all():

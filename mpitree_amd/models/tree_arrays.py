@@ -72,13 +72,14 @@ class TreeArrays:
         return ta
 
     @classmethod
-    def from_device_columns(cls, *, stats, threshold, feature, threshold_bin, right, depth,
+    def from_device_columns(cls, *, stats, threshold, split, right, max_depth: int,
                             criterion: int, regression: bool, y_exp: int = 0,
                             edges_table=None) -> "TreeArrays":
         """The device assembly's columns (``ops/csrc/assemble.hip``): class
         counts (int32) or regression {count, fixed-point sum} (int64), split
-        thresholds, features, bins, right children and depths in pre-order.
-        Left children (pre-order: node + 1), node sizes, int64 counts,
+        thresholds, packed splits ``feature << 16 | bin`` (-1: leaf) and right
+        children in pre-order, plus the tree depth. Features, bins, left
+        children (pre-order: node + 1), depths, node sizes, int64 counts,
         impurities and regression leaf values follow from them and are computed
         on first use with the same integer-form criterion as every builder
         (``core/criterion.py``, bitwise equal to the device's). ``threshold``
@@ -86,7 +87,17 @@ class TreeArrays:
         padded edge table, the values the device table holds) on first use."""
         from ..core import criterion as cr
 
-        N = int(feature.shape[0])
+        N = int(right.shape[0])
+        leaf = split == -1
+
+        def feature(t):
+            return np.where(leaf, np.int32(-1), (split.view(np.uint32) >> 16).astype(np.int32))
+
+        def threshold_bin(t):
+            return np.where(leaf, np.int32(-1), (split & 0xFFFF).astype(np.int32))
+
+        def depth(t):
+            return _preorder_depth(right, leaf)
 
         def threshold_from_edges(t):
             out = np.full(N, np.nan)
@@ -107,9 +118,9 @@ class TreeArrays:
                 return np.ldexp(s / np.maximum(stats[:, 0], 1).astype(np.float64), -int(y_exp))
 
             derive = {"left": left, "n_samples": n_samples, "value": value,
-                      "impurity": lambda t: np.full(N, np.nan)}
-            ta = cls.deferred(derive, feature=feature, threshold_bin=threshold_bin, right=right,
-                              depth=depth, count=None)
+                      "impurity": lambda t: np.full(N, np.nan), "feature": feature,
+                      "threshold_bin": threshold_bin, "depth": depth}
+            ta = cls.deferred(derive, right=right, count=None)
             ta.meta["sum_fixed"] = stats[:, 1]
         else:
             def n_samples(t):
@@ -124,22 +135,23 @@ class TreeArrays:
                     return np.where(m > 0, term / np.maximum(m, 1).astype(np.float64), 0.0)
 
             derive = {"left": left, "n_samples": n_samples, "impurity": impurity,
-                      "count": lambda t: stats.astype(np.int64)}
-            ta = cls.deferred(derive, feature=feature, threshold_bin=threshold_bin, right=right,
-                              depth=depth, value=None)
+                      "count": lambda t: stats.astype(np.int64), "feature": feature,
+                      "threshold_bin": threshold_bin, "depth": depth}
+            ta = cls.deferred(derive, right=right, value=None)
         if threshold is not None:
             ta.__dict__["threshold"] = threshold
         else:
             ta.__dict__["_derive"]["threshold"] = threshold_from_edges
             ta.meta["edges_table"] = edges_table
         ta.meta["final"] = True  # thresholds, impurity and values need no host pass
+        ta.meta["max_depth"] = int(max_depth)
         ta.meta["stats_raw"] = stats  # (the cross-rank digest hashes what was transferred)
         return ta
 
     # ------------------------------------------------------------------ basics
     @property
     def node_count(self) -> int:
-        return int(self.feature.shape[0])
+        return int(self.right.shape[0])
 
     @property
     def is_classifier(self) -> bool:
@@ -147,6 +159,8 @@ class TreeArrays:
 
     @property
     def max_depth(self) -> int:
+        if "max_depth" in self.meta and "depth" not in self.__dict__:
+            return int(self.meta["max_depth"])  # device-assembled: reduced on the device
         return int(self.depth.max()) if self.node_count else 0
 
     @property
@@ -496,3 +510,24 @@ class TreeArrays:
 # the dataclass keeps these defaults in __init__; without the class attributes a
 # deferred count / value is found by __getattr__ rather than the class-level None
 del TreeArrays.count, TreeArrays.value
+
+
+def _preorder_depth(right: np.ndarray, leaf: np.ndarray) -> np.ndarray:
+    """Node depths of a pre-order tree from its right-child links: an internal
+    node i (left child i + 1) adds one to every node of its subtree after it,
+    positions (i, end_i) with end_i = 1 + the last node of the subtree, reached
+    by following right links to a leaf (pointer jumping, O(N log depth))."""
+    N = int(right.shape[0])
+    if N == 0:
+        return np.zeros(0, np.int32)
+    idx = np.arange(N, dtype=np.int64)
+    last = np.where(leaf, idx, right.astype(np.int64))
+    while True:
+        nxt = last[last]
+        if np.array_equal(nxt, last):
+            break
+        last = nxt
+    inner = ~leaf
+    delta = np.bincount(idx[inner] + 1, minlength=N + 1) - np.bincount(last[inner] + 1,
+                                                                         minlength=N + 1)
+    return np.cumsum(delta[:N]).astype(np.int32)

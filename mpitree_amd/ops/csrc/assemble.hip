@@ -71,23 +71,35 @@ __global__ __launch_bounds__(kAsmThreads) void asm_offsets_kernel(int32_t* __res
     if (threadIdx.x == kAsmThreads - 1) s_carry = off + incl;
     __syncthreads();
   }
-  if (threadIdx.x == 0) *total = s_carry;
+  if (threadIdx.x == 0) {
+    total[0] = s_carry;
+    total[1] = 0;  // max depth: asm_rank_kernel reduces into it
+  }
 }
 
-// Final node id of every written position (positions no node occupies get -1).
+// Final node id of every written position (positions no node occupies get -1),
+// and the tree's depth (max over written positions) into total[1].
 __global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __restrict__ rec,
                                                                int64_t P,
                                                                const int32_t* __restrict__ tile_off,
-                                                               int32_t* __restrict__ rank) {
+                                                               int32_t* __restrict__ rank,
+                                                               int64_t* __restrict__ total) {
   // thread t owns kAsmPer consecutive positions so the in-tile order is preserved
   const int64_t base = (int64_t)blockIdx.x * kAsmTile + (int64_t)threadIdx.x * kAsmPer;
   uint32_t flags = 0;
-  int c = 0;
+  int c = 0, dmax = 0;
   for (int k = 0; k < kAsmPer; ++k) {
     const int64_t p = base + k;
     const bool v = p < P && rec[p * 6 + 5] > 0;
     flags |= (uint32_t)v << k;
     c += v;
+    if (v) dmax = max(dmax, rec[p * 6 + 4]);
+  }
+  {
+    int m = dmax;
+    for (int d = kWave / 2; d > 0; d >>= 1) m = max(m, __shfl_xor(m, d, kWave));
+    if (lane_id() == 0 && m > 0)
+      atomicMax(reinterpret_cast<unsigned long long*>(total) + 1, (unsigned long long)m);
   }
   const int incl = (int)wave_incl_scan_u32((uint32_t)c);
   __shared__ int w[kAsmThreads / kWave];
@@ -108,18 +120,19 @@ __global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __
 // host round trip. Only what the host cannot derive cheaply crosses the link:
 //   stats [N][C] (int32 class counts; regression int64 {count, fixed sum})
 //   | threshold f64 [N] (only when the host has no edge table: the exact
-//   engine's unique values stay on the device) | feature, bin, right, depth i32 [N]
-// Left children are implicit in pre-order (node j + 1), node sizes are the
+//   engine's unique values stay on the device) | split i32 [N] = feature << 16 |
+//   bin (-1: leaf) | right i32 [N]
+// Left children are implicit in pre-order (node j + 1), depths follow from the
+// child links (the tree's depth travels with the node count), node sizes are the
 // stats' sums, impurities and leaf values follow from the stats with the same
 // integer-form criterion: the host derives those columns on first use
-// (TreeArrays.deferred). 24 B per node for a two-class tree instead of 60.
+// (TreeArrays.deferred). 16 B per node for a two-class tree instead of 60.
+// (feature < 2^15 -- the caller checks F -- and bin < 2^16: codes are <= 16 bits.)
 struct AsmCols {
   void* stats;
   double* threshold;
-  int32_t* feature;
-  int32_t* bin;
+  int32_t* split;
   int32_t* right;
-  int32_t* depth;
 };
 
 __device__ inline AsmCols asm_cols(uint8_t* base, int64_t N, int C, bool reg, bool thr) {
@@ -128,10 +141,8 @@ __device__ inline AsmCols asm_cols(uint8_t* base, int64_t N, int C, bool reg, bo
   const int64_t sbytes = reg ? N * 16 : ((N * C * 4 + 7) & ~(int64_t)7);
   o.threshold = thr ? reinterpret_cast<double*>(base + sbytes) : nullptr;
   int32_t* p4 = reinterpret_cast<int32_t*>(base + sbytes + (thr ? N * 8 : 0));
-  o.feature = p4;
-  o.bin = p4 + N;
-  o.right = p4 + 2 * N;
-  o.depth = p4 + 3 * N;
+  o.split = p4;
+  o.right = p4 + N;
   return o;
 }
 
@@ -149,14 +160,12 @@ __global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
   const int32_t* R = rec + p * 6;
   const int f = R[0];
   const int b = R[1];
-  o.feature[j] = f >= 0 ? f : -1;
-  o.depth[j] = R[4];
   if (f >= 0) {
-    o.bin[j] = b;
+    o.split[j] = (int32_t)(((uint32_t)f << 16) | ((uint32_t)b & 0xffffu));
     o.right[j] = rank[R[3]];
     if (thr) o.threshold[j] = edges[(int64_t)f * EB + b];
   } else {
-    o.bin[j] = -1;
+    o.split[j] = -1;
     o.right[j] = -1;
     if (thr) o.threshold[j] = __builtin_nan("");
   }
@@ -179,14 +188,14 @@ void launch_asm_rank(hipStream_t stream, const int32_t* rec, int64_t P, int32_t*
   hipLaunchKernelGGL(asm_offsets_kernel, dim3(1), dim3(kAsmThreads), 0, stream, tile, n_tiles,
                      total);
   hipLaunchKernelGGL(asm_rank_kernel, dim3(n_tiles), dim3(kAsmThreads), 0, stream, rec, P, tile,
-                     rank);
+                     rank, total);
   MT_HIP_CHECK(hipGetLastError());
 }
 
 int asm_tiles(int64_t P) { return (int)((P + kAsmTile - 1) / kAsmTile); }
 
 // upper bound per node (the stats block is padded to 8 bytes once, not per node)
-int64_t asm_node_bytes(int C, bool reg) { return (reg ? 16 : 4 * C) + 8 + 4 * 4 + 8; }
+int64_t asm_node_bytes(int C, bool reg) { return (reg ? 16 : 4 * C) + 8 + 2 * 4 + 8; }
 
 void launch_asm_emit(hipStream_t stream, const int32_t* rec, const void* st, bool st64,
                      int64_t P, int C, const int32_t* rank, const double* edges, int EB,

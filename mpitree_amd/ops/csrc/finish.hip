@@ -104,6 +104,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
   __shared__ double s_pterm;
   __shared__ double w_gain[kFinWaves];
   __shared__ int w_feat[kFinWaves], w_bin[kFinWaves];
+  __shared__ int w_nc[kFinWaves];  // candidate features per wave; -1: one separated bin
   __shared__ int s_bf, s_bb;
   __shared__ int s_lc, s_rc;
   __shared__ int s_cand_total;
@@ -178,8 +179,12 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
   // Processes kFinPair features per call with every table read issued before
   // the first wait: each feature is a dependent chain (LDS read -> DPP scan ->
   // lookups -> DPP min), so independent features are what hides the latency.
-  auto scan_c2_f = [&](auto big_tag, int f0, uint32_t t0, uint32_t t1, int m,
-                       float (&out)[kFinPair]) {
+  // info[q] (for the exact-pass skip): bits 0-1 the lane's first minimum bin,
+  // bit 2 set when every other bin of the lane costs more than
+  // (min + T(m) 2^-19) + 2^-20 -- the candidate threshold's form with min >= the
+  // node's best, so such a bin is never a candidate
+  auto scan_c2_f = [&](auto big_tag, int f0, uint32_t t0, uint32_t t1, int m, float tmf,
+                       float (&out)[kFinPair], uint32_t (&info)[kFinPair]) {
     constexpr bool kBig = decltype(big_tag)::value;
     auto lk = [&](uint32_t x) -> float {
       if constexpr (!kBig) {
@@ -222,14 +227,20 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
     }
 #pragma unroll
     for (int q = 0; q < kFinPair; ++q) {
+      float c[4];
       float best = __builtin_inff();
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const float* t = tv[q][k];
-        const float c = (t[0] - (t[1] + t[2])) + (t[3] - (t[4] + t[5]));
-        best = fminf(best, ok[q][k] ? c : __builtin_inff());
+        c[k] = ok[q][k] ? (t[0] - (t[1] + t[2])) + (t[3] - (t[4] + t[5])) : __builtin_inff();
+        best = fminf(best, c[k]);
       }
+      const int idx = c[0] == best ? 0 : (c[1] == best ? 1 : (c[2] == best ? 2 : 3));
+      float s2 = __builtin_inff();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s2 = k == idx ? s2 : fminf(s2, c[k]);
       out[q] = best;
+      info[q] = (uint32_t)idx | (s2 > (best + tmf * 0x1p-19f) + 0x1p-20f ? 4u : 0u);
     }
   };
   // Exact (fp64, global table) best split of one feature: (cost, lowest bin).
@@ -450,12 +461,15 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
       // ---- wave-per-feature scan (B <= 256: one 256-bin pass)
       double bg = -__builtin_inf();
       int bfeat = 0x7fffffff, bbin = -1;
+      int nc_report = 0x40000000;  // no exact-pass skip unless pass 1 proves one
       if constexpr (kC2) {
         const uint32_t t0 = (uint32_t)s_cnt[0], t1 = C > 1 ? (uint32_t)s_cnt[1] : 0u;
         bool cand_all = true, one_chunk = false;
         float thr = 0.0f;
         float lmin[kFinChunk];
+        uint32_t linfo = 0u;  // scan_c2_f info of chunk feature i at bits 3i..3i+2
         uint32_t cand_mask = 0u;
+        bool clean = false;
         if (crit == kEntropy) {
           // pass 1: per-lane fp32 minima over each feature's bins (no per-feature
           // wave reduction), one wave minimum, then the node-wide threshold.
@@ -464,21 +478,25 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           const bool big = m >= tn;  // wave-uniform: small nodes never leave LDS
           const int fpw = (F - wave + kFinWaves - 1) / kFinWaves;  // this wave's features
           one_chunk = F <= kFinWaves * kFinChunk;
+          const float tmf = m < tn ? s_tabf[m] : __ldg(xtabf + m);
           float wl = __builtin_inff();
           for (int c0 = 0; c0 < fpw; c0 += kFinChunk) {
 #pragma unroll
             for (int i = 0; i < kFinChunk; i += kFinPair) {
               float fm[kFinPair];
+              uint32_t fi[kFinPair];
               if (c0 + i < fpw) {
                 const int f = wave + (c0 + i) * kFinWaves;
                 if (big)
-                  scan_c2_f(std::true_type{}, f, t0, t1, m, fm);
+                  scan_c2_f(std::true_type{}, f, t0, t1, m, tmf, fm, fi);
                 else
-                  scan_c2_f(std::false_type{}, f, t0, t1, m, fm);
+                  scan_c2_f(std::false_type{}, f, t0, t1, m, tmf, fm, fi);
               }
 #pragma unroll
-              for (int q = 0; q < kFinPair; ++q)
+              for (int q = 0; q < kFinPair; ++q) {
                 lmin[i + q] = c0 + i + q < fpw ? fm[q] : __builtin_inff();
+                if (c0 + i + q < fpw) linfo |= fi[q] << (3 * (i + q));
+              }
             }
 #pragma unroll
             for (int i = 0; i < kFinChunk; ++i) wl = fminf(wl, lmin[i]);
@@ -502,10 +520,34 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
             for (int i = 0; i < kFinChunk; ++i)
               if (__ballot(lmin[i] <= thr)) cand_mask |= 1u << i;
+            // exact-pass skip: this wave's only candidate is one lane's one bin,
+            // every other bin of that lane above the threshold. If it is also
+            // the node's only candidate (checked after the barrier), its exact
+            // cost is the unique minimum: every other bin's fp32 cost exceeds
+            // best + T(m) 2^-19 + 2^-20 > best + 2 * 12 * 2^-24 T(m) (twice the
+            // fp32 error bound), far more than the tie-rounding grid.
+            nc_report = __popc(cand_mask);
+            if (nc_report == 1) {
+              const int i = __ffs((int)cand_mask) - 1;
+              float li = lmin[0];
+#pragma unroll
+              for (int k = 1; k < kFinChunk; ++k) li = k == i ? lmin[k] : li;
+              const unsigned long long lanes = __ballot(li <= thr);
+              if (__popcll(lanes) == 1) {
+                const int l = __ffsll((long long)lanes) - 1;
+                const uint32_t inf = (uint32_t)__builtin_amdgcn_readlane((int)linfo, l) >> (3 * i);
+                if (inf & 4u) {
+                  clean = true;
+                  nc_report = -1;
+                  bfeat = wave + i * kFinWaves;
+                  bbin = l * 4 + (int)(inf & 3u);
+                }
+              }
+            }
           }
         }
         // pass 2: exact scores for candidate features only
-        for (int i = 0, f = wave; f < F; ++i, f += kFinWaves) {
+        for (int i = 0, f = wave; f < F && !clean; ++i, f += kFinWaves) {
           if (!cand_all) {
             if (one_chunk ? !((cand_mask >> i) & 1u) : !(s_fmin[f] <= thr)) continue;
           }
@@ -604,11 +646,39 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         w_gain[wave] = bg;
         w_feat[wave] = bfeat;
         w_bin[wave] = bbin;
+        w_nc[wave] = nc_report;
       }
       __syncthreads();
       mark(1);
-      int bf, bb;
-      {
+      int bf = -1, bb = -1;
+      bool decided = false;
+      if constexpr (kC2) {
+        int tot = 0, cw = -1;
+        for (int w = 0; w < kFinWaves; ++w) {
+          const int c = w_nc[w];
+          tot += c < 0 ? 1 : min(c, 0x40000000 / kFinWaves);
+          if (c < 0) cw = w;
+        }
+        if (cw >= 0 && tot == 1) {  // the node's only candidate: no exact pass
+          bf = w_feat[cw];
+          bb = w_bin[cw];
+          decided = true;
+        } else if (cw >= 0) {  // other candidates too: the skipped waves score theirs now
+          if (w_nc[wave] < 0) {
+            const uint32_t t0 = (uint32_t)s_cnt[0], t1 = C > 1 ? (uint32_t)s_cnt[1] : 0u;
+            const int f = w_feat[wave];
+            double best_cost;
+            int best_bin;
+            scan_c2(hist + f * fstride, s_nb[f], t0, t1, m, best_cost, best_bin);
+            if (lane == 0) {
+              w_gain[wave] = best_cost < __builtin_inf() ? pterm - best_cost : -__builtin_inf();
+              w_bin[wave] = best_bin;
+            }
+          }
+          __syncthreads();
+        }
+      }
+      if (!decided) {
         double g = w_gain[0];
         bf = w_feat[0];
         bb = w_bin[0];

@@ -183,11 +183,17 @@ __device__ void plan_hist_items(const PlanArgs& a, PlanShared& sh, int NB) {
     }
     const int multi = kk > 1 ? 1 : 0;
     const int nt = multi ? (int)((kk + 15) / 16) : 0;
-    int ti, tsl, tr, tt;
-    const int oi_l = plan_scan_excl((int)kk, sh.w, ti);
-    const int osl = plan_scan_excl(multi ? (int)kk : 0, sh.w, tsl) + sh.carry[1];
-    const int orr = plan_scan_excl(multi, sh.w, tr) + sh.carry[2];
-    const int ot = plan_scan_excl(nt, sh.w, tt) + sh.carry[3];
+    // two packed scans: {items, slabs} and {reductions, tasks}. Per chunk the items
+    // total <= level rows / chunk + kPlanThreads <= 2 n_cu + 1024 and tasks <= items,
+    // so every 16-bit field holds its sum
+    int tis, trt;
+    const int ois = plan_scan_excl((int)kk | ((multi ? (int)kk : 0) << 16), sh.w, tis);
+    const int ort = plan_scan_excl(multi | (nt << 16), sh.w, trt);
+    const int ti = tis & 0xffff, tsl = tis >> 16, tr = trt & 0xffff, tt = trt >> 16;
+    const int oi_l = ois & 0xffff;
+    const int osl = (ois >> 16) + sh.carry[1];
+    const int orr = (ort & 0xffff) + sh.carry[2];
+    const int ot = (ort >> 16) + sh.carry[3];
     sh.pa[tid] = sl < NB ? a.nxt.start[sl] : 0;
     sh.pb[tid] = cnt;
     sh.pc[tid] = multi ? osl : -1;
@@ -272,20 +278,14 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
   const int JW = plan_job_width(a);
   const int K = a.cur.ctl[0];
   // ---- pass 1: totals (built / derived next-frontier children, split nodes)
-  int nb_tot = 0, nd_tot = 0;
+  int nb_tot = 0;
   for (int b0 = 0; b0 < K; b0 += kPlanThreads) {
     const int i = b0 + tid;
-    int nb = 0, nd = 0;
-    if (i < K) {
-      const Decision d = plan_decide(a, i);
-      nb = d.built >= 0 ? 1 : 0;
-      nd = (d.fate[0] == 2 && d.fate[1] == 2) ? 1 : 0;
-    }
+    int nb = 0;
+    if (i < K) nb = plan_decide(a, i).built >= 0 ? 1 : 0;
     int t;
     plan_scan_excl(nb, sh.w, t);
     nb_tot += t;
-    plan_scan_excl(nd, sh.w, t);
-    nd_tot += t;
   }
   const int NB = nb_tot;
   if (tid == 0) {
@@ -306,9 +306,12 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     const int nb = d.built >= 0 ? 1 : 0;
     const int nd = (d.fate[0] == 2 && d.fate[1] == 2) ? 1 : 0;
     const int ns = d.split ? 1 : 0;
-    int tb, td, ts;
-    const int ob = plan_scan_excl(nb, sh.w, tb) + sh.carry[0];
-    const int od = plan_scan_excl(nd, sh.w, td) + sh.carry[1];
+    // built / derived offsets share one scan (each field <= kPlanThreads < 2^16)
+    int tbd, ts;
+    const int obd = plan_scan_excl(nb | (nd << 16), sh.w, tbd);
+    const int tb = tbd & 0xffff, td = tbd >> 16;
+    const int ob = (obd & 0xffff) + sh.carry[0];
+    const int od = (obd >> 16) + sh.carry[1];
     const int os = plan_scan_excl(ns, sh.w, ts) + sh.carry[2];
     if (i < K) {
       const int64_t pos = a.cur.pos[i];

@@ -49,6 +49,9 @@ class Prepared:
     y_exp: int
     root: np.ndarray | None  # root statistics when known without another sync
     d_edges64: torch.Tensor | None  # device fp64 edge table [F, W] (None: use host edges)
+    # deferred bin verification (None: already checked): call once the stream has
+    # passed the bin kernel; False means the fit must be redone with sync=True
+    verify: object = None
 
 
 def _np_dtype(dt: torch.dtype):
@@ -166,11 +169,19 @@ class _Targets:
 
 
 def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
-            encode_targets, exponent) -> Prepared:
+            encode_targets, exponent, sync: bool = False) -> Prepared:
     """Bin ``Xd`` (device, fp32/fp64) and encode ``y`` with two host syncs.
 
     ``encode_labels`` / ``encode_targets`` are the host encoders of
     ``core/fit.py``, used for host arrays and unusual label dtypes.
+
+    With at most 256 bins the first sync waits only for the edge table and the
+    label counts: the bin kernel (~0.1 ms on 1M x 64) keeps running while the
+    host builds its tables and enqueues the level loop. Its codes are always
+    valid bins (clamped), so nothing downstream depends on its verification
+    flags until the tree is assembled; ``Prepared.verify`` checks them then
+    (non-finite input raises, an exact-mode sample that missed a value asks
+    for a redo with ``sync=True``, which checks before growing).
     """
     n = Xd.shape[0]
     dev = Xd.device
@@ -178,14 +189,24 @@ def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
     lab = (_Targets(y, n, dev, encode_targets, exponent) if regression
            else _Labels(y, n, dev, encode_labels))
     binning = DeviceBinning(Xd, max_bins)
-    if binning.early:  # <= 256 bins: codes, flags and edges all land by sync 1
+    early = binning.early
+    if early:  # <= 256 bins: the bin kernel reads the bin counts on the device
+        tables = torch.cuda.Event()
+        tables.record(stream)  # edge table + label count copies are enqueued before it
         binning.launch_bin_early()
-    stream.synchronize()  # sync 1: edge table (+ bin flags) + label counts / target scale
+        if sync:
+            stream.synchronize()  # sync 1 covers the bin flags too
+        else:
+            tables.synchronize()  # sync 1: edge table + label counts / target scale
+    else:
+        stream.synchronize()  # sync 1: edge table + label counts / target scale
     need2 = lab.after_first_sync()
     binning.launch_bin()  # host tables; enqueues the bin kernel unless already done
-    if need2 or not binning.early:
+    deferred = early and not sync
+    if need2 or not early:
         stream.synchronize()  # sync 2: bin flags / class counts / target root stats
-    mapper, codes_rm, codes_fm, nb = binning.finish()
+        deferred = False
+    mapper, codes_rm, codes_fm, nb = binning.finish(check=not deferred)
     if regression:
         yenc, y_exp, root = lab.finish()
         classes = None
@@ -193,7 +214,8 @@ def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
         classes, yenc, root = lab.finish()
         y_exp = 0
     return Prepared(mapper=mapper, codes_rm=codes_rm, codes_fm=codes_fm, nbins=nb, y=yenc,
-                    classes=classes, y_exp=y_exp, root=root, d_edges64=binning.d_edges64)
+                    classes=classes, y_exp=y_exp, root=root, d_edges64=binning.d_edges64,
+                    verify=binning.verify if deferred else None)
 
 
 def prepare_with_mapper(Xd: torch.Tensor, y_enc, mapper, classes, y_exp: int) -> Prepared:

@@ -178,6 +178,8 @@ class DeviceBinning:
         self.codes_rm, self.codes_fm, flags = self._run_bin(self.edges, self.nb, self.exact,
                                                             self.limit)
         self._host_flags = _pinned_copy(flags, "bin.flags")
+        self._flags_ready = torch.cuda.Event()
+        self._flags_ready.record(torch.cuda.current_stream(self.dev))
         self._launched = True
 
     def host_tables(self):
@@ -199,16 +201,30 @@ class DeviceBinning:
             self._host_flags = _pinned_copy(flags, "bin.flags")
             self._launched = True
 
-    def finish(self):
-        """(mapper, codes_rm, codes_fm, nbins_dev) after a sync covering the flags copy."""
+    def finish(self, check: bool = True):
+        """(mapper, codes_rm, codes_fm, nbins_dev) after a sync covering the flags copy
+        (``check=False``: before it; :meth:`verify` then checks the flags later)."""
+        missed = False
+        if check:
+            fl = np.array(self._host_flags)
+            if (fl & 2).any():
+                raise ValueError("Input X contains NaN or infinity.")
+            missed = bool((fl & 1).any())
+            if missed:
+                self._refit_missed(np.nonzero(fl & 1)[0])
+        self.d_edges64 = None if missed else self.pack[: self.F * self.limit].view(
+            self.F, self.limit)
+        return self.mapper, self.codes_rm, self.codes_fm, self.nb
+
+    def verify(self) -> bool:
+        """Deferred flag check of an early bin pass whose result is already in use:
+        raises on non-finite input; False when an exact-mode sample missed a value
+        (the codes were clamped to the sampled edges: the fit must be redone)."""
+        self._flags_ready.synchronize()
         fl = np.array(self._host_flags)
         if (fl & 2).any():
             raise ValueError("Input X contains NaN or infinity.")
-        if (fl & 1).any():
-            self._refit_missed(np.nonzero(fl & 1)[0])
-        self.d_edges64 = None if (fl & 1).any() else self.pack[: self.F * self.limit].view(
-            self.F, self.limit)
-        return self.mapper, self.codes_rm, self.codes_fm, self.nb
+        return not bool((fl & 1).any())
 
     def _refit_missed(self, feats):
         """The sample missed values of an "exact" feature: use the full column."""
@@ -281,6 +297,7 @@ def xlog2x_table(device) -> torch.Tensor:
 
 
 _pinned: dict = {}
+_ASM_HINT: dict = {}  # (device, positions, C, reg, thresholds) -> last assembled node count
 
 
 _TASK_FLAGS: dict = {}  # device -> [int32 flag tensor, epoch]
@@ -538,6 +555,8 @@ class HipBackend:
         derived from them on first use (``TreeArrays.deferred``); so are the
         thresholds when ``host_table`` (the host's padded edge table) is given."""
         P, C = self.P, self.C
+        if self.F > 65535:  # the link packs feature << 16 | bin into 32 bits
+            raise ValueError("GPU fits support at most 65535 features")
         hip = self.hip
         s = _stream()
         thr = host_table is None
@@ -551,21 +570,39 @@ class HipBackend:
         o_out = o_rank + al(P * 4)
         ws = _workspace(self.device, "asm", o_out + P * bpn)
         base = ws.data_ptr()
-        total = ws[o_total : o_total + 8].view(torch.int64)
+        total = ws[o_total : o_total + 16].view(torch.int64)  # {nodes, depth}
         hip.asm_rank(s, self.pos_rec.data_ptr(), P, base, base + o_total, base + o_rank)
         hip.asm_emit(s, self.pos_rec.data_ptr(), self.pos_st.data_ptr(), self.reg, P, C,
                      base + o_rank, d_edges.data_ptr() if thr else 0,
                      int(d_edges.stride(0)) if thr else 0, base + o_total, base + o_out,
                      bool(self.reg), thr)
         h_total = _pinned_copy(total, "asm.total")
+
+        def col_bytes(N):
+            sb = N * 16 if self.reg else (N * C * 4 + 7) // 8 * 8
+            return sb, sb + (N * 8 if thr else 0) + N * 8
+
+        # the columns are laid out from the device node count, so a copy sized for
+        # the previous fit's count on this position space (a refit of the same
+        # data: the same count) is a prefix-complete guess, enqueued before the
+        # wait -- one host wait instead of two, the pinned allocation overlapping
+        # the finisher; a larger tree copies the rest after the count arrives
+        key = (str(self.device), P, C, bool(self.reg), thr)
+        guess = _ASM_HINT.get(key, 0)
+        host, have = None, 0
+        if guess:
+            have = col_bytes(guess)[1]
+            host = torch.empty(max(have, 8), dtype=torch.uint8, pin_memory=True)
+            host[:have].copy_(ws[o_out : o_out + have], non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
         self._check_finisher_watch()
-        N = int(h_total[0])
-        sbytes = N * 16 if self.reg else (N * C * 4 + 7) // 8 * 8
-        nbytes = sbytes + (N * 8 if thr else 0) + N * 16
-        host = torch.empty(max(nbytes, 8), dtype=torch.uint8, pin_memory=True)
-        host[:nbytes].copy_(ws[o_out : o_out + nbytes], non_blocking=True)
-        torch.cuda.current_stream(self.device).synchronize()
+        N, max_depth = int(h_total[0]), int(h_total[1])
+        _ASM_HINT[key] = N
+        sbytes, nbytes = col_bytes(N)
+        if nbytes > have:
+            host = torch.empty(max(nbytes, 8), dtype=torch.uint8, pin_memory=True)
+            host[:nbytes].copy_(ws[o_out : o_out + nbytes], non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
         h = host.numpy()
         if self.reg:
             stats = h[: N * 16].view(np.int64).reshape(N, 2)
@@ -576,12 +613,12 @@ class HipBackend:
         if thr:
             threshold = h[o : o + N * 8].view(np.float64)
             o += N * 8
-        i4 = h[o : o + N * 16].view(np.int32)
+        i4 = h[o : o + N * 8].view(np.int32)
         self.pos_rec = self.pos_st = None
         return TreeArrays.from_device_columns(
-            stats=stats, threshold=threshold, feature=i4[:N], threshold_bin=i4[N : 2 * N],
-            right=i4[2 * N : 3 * N], depth=i4[3 * N : 4 * N], criterion=int(crit),
-            regression=bool(self.reg), y_exp=int(y_exp), edges_table=host_table)
+            stats=stats, threshold=threshold, split=i4[:N], right=i4[N : 2 * N],
+            max_depth=max_depth, criterion=int(crit), regression=bool(self.reg),
+            y_exp=int(y_exp), edges_table=host_table)
 
     def small_fit_supported(self, comm=None) -> bool:
         """One-workgroup whole-tree fit (``small_fit.hip``): classification on
@@ -731,7 +768,7 @@ class HipBackend:
         P = rec.shape[0]
         tiles = self.hip.asm_tiles(P)
         tile = torch.empty(max(tiles, 1), dtype=torch.int32, device=self.device)
-        total = torch.zeros(1, dtype=torch.int64, device=self.device)
+        total = torch.zeros(2, dtype=torch.int64, device=self.device)
         rank = torch.empty(P, dtype=torch.int32, device=self.device)
         self.hip.asm_rank(_stream(), rec.data_ptr(), P, tile.data_ptr(), total.data_ptr(),
                           rank.data_ptr())

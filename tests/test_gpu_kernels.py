@@ -276,6 +276,35 @@ def test_gpu_job_sort_kernel_matches_torch_order(monkeypatch):
     assert a.arrays.equal(b.arrays)
 
 
+def test_gpu_sample_missed_value_redoes_fit():
+    """The first sync no longer waits for the bin kernel's flags: a value the
+    strided edge sample skipped is found after growth and the fit is redone
+    with the flags checked first -- the tree equals the host fit."""
+    from mpitree_amd.core.fit import fit_tree
+    from mpitree_amd.ops.hip_backend import DeviceBinning
+
+    rng = np.random.default_rng(21)
+    n = 200_000
+    X = rng.integers(0, 8, size=(n, 3)).astype(np.float32)
+    y = ((X[:, 0] + X[:, 1]) > 7).astype(np.int64)
+    for r in range(1, 64):
+        X2, y2 = X.copy(), y.copy()
+        X2[r, 0], y2[r] = 3.5, 1 - y2[r]
+        job = DeviceBinning(torch.from_numpy(X2).cuda(), 256)
+        torch.cuda.synchronize()
+        job.launch_bin()
+        torch.cuda.synchronize()
+        if np.array(job._host_flags)[0] & 1:
+            break
+    else:
+        pytest.skip("the edge sample covers every probed row")
+    kw = dict(regression=False, criterion=1, max_depth=None, min_samples_split=2)
+    a = fit_tree(torch.from_numpy(X2).cuda(), torch.from_numpy(y2).cuda(), device="cuda", **kw)
+    b = fit_tree(X2, y2, device="cpu", **kw)
+    assert 3.5 in a.mapper.edges[0]
+    assert a.arrays.equal(b.arrays)
+
+
 def test_gpu_rejects_nonfinite_tensor():
     X = torch.zeros((1000, 3), device="cuda")
     X[17, 1] = float("nan")

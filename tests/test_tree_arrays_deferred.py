@@ -15,9 +15,10 @@ def _compact(ta, regression):
         stats = np.stack([ta.n_samples, ta.meta["sum_fixed"]], 1).astype(np.int64)
     else:
         stats = ta.count.astype(np.int32)
-    return dict(stats=stats, threshold=ta.threshold.copy(), feature=ta.feature.astype(np.int32),
-                threshold_bin=ta.threshold_bin.astype(np.int32),
-                right=ta.right.astype(np.int32), depth=ta.depth.astype(np.int32))
+    f, b = ta.feature.astype(np.int64), ta.threshold_bin.astype(np.int64)
+    split = np.where(f >= 0, (f << 16) | b, -1).astype(np.int32)  # assemble.hip's packing
+    return dict(stats=stats, threshold=ta.threshold.copy(), split=split,
+                right=ta.right.astype(np.int32), max_depth=int(ta.depth.max()))
 
 
 @pytest.mark.parametrize("crit", [0, 1, 2])
@@ -35,7 +36,9 @@ def test_device_columns_derive_host_columns(crit):
     dev = TreeArrays.from_device_columns(**_compact(host, reg), criterion=crit, regression=reg,
                                          y_exp=r.y_scale_exp)
     assert "left" not in dev.__dict__  # still deferred
+    assert dev.max_depth == host.max_depth and "depth" not in dev.__dict__
     assert dev.equal(host)
+    assert np.array_equal(dev.depth, host.depth)  # derived from the right links
     assert dev.left.dtype == np.int32 and dev.n_samples.dtype == np.int64
     if reg:
         assert np.array_equal(dev.value, host.value)
