@@ -44,9 +44,17 @@ constexpr int kFinThreadsWide = 1024;  // one workgroup per CU (F = 128 histogra
 constexpr int kFinStack = 40;    // >= log2(max job rows) + 2
 constexpr int kFinMaxC = 16;     // classes supported by the finisher
 constexpr int kFinTab = 1024;    // LDS x*log2(x) entries
-constexpr int kFinUnroll = 4;    // row gathers in flight per lane
+// MT_FIN_UNROLL / MT_FIN_PAIR / MT_TINY_SMALL: compile-time overrides for variant
+// builds (tools/build_variant.sh, measured in profiles/kernel_experiments.md)
+#ifndef MT_FIN_UNROLL
+#define MT_FIN_UNROLL 4
+#endif
+#ifndef MT_FIN_PAIR
+#define MT_FIN_PAIR 1
+#endif
+constexpr int kFinUnroll = MT_FIN_UNROLL;  // row gathers in flight per lane
 constexpr int kFinMaxF = 256;    // features (the LDS histogram bounds F far lower)
-constexpr int kFinPair = 1;      // features scanned together per wave (latency hiding)
+constexpr int kFinPair = MT_FIN_PAIR;  // features scanned together per wave (latency hiding)
 constexpr int kFinChunk = 8;     // features per wave whose per-lane minima stay in registers
 
 // Histogram row stride in words: >= B*W + 1 (the odd word staggers features over
@@ -1113,7 +1121,10 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
 //
 // LDS per wave: srt [F][64] halfwords + 64 flag bytes (tiny_wave_bytes); per
 // workgroup: the H table (tiny_h_entries doubles).
-constexpr int kTinySmallNode = 16;  // nodes of 3..16 rows: one lane per feature
+#ifndef MT_TINY_SMALL
+#define MT_TINY_SMALL 16
+#endif
+constexpr int kTinySmallNode = MT_TINY_SMALL;  // nodes of 3..16 rows: one lane per feature
 constexpr int kTinyH = (kTinyRows + 1) * (kTinyRows + 2) / 2;  // triangular a <= 64, b <= a
 __device__ __forceinline__ int tiny_h_idx(int a, int b) { return ((a * (a + 1)) >> 1) + b; }
 
