@@ -195,8 +195,8 @@ class DeviceGrower:
         serpentine share."""
         be, comm = self.be, self.comm
         sim = int(os.environ.get("MPITREE_SIM_RANKS", "0"))
-        if comm is not None and comm.world_size > 1:
-            sim = 0
+        if comm is not None and comm.world_size > 1 and not getattr(comm, "simulated", False):
+            sim = 0  # (bench/sim_fp_ranks.py: a one-process stand-in for rank 0 keeps it)
         if sim > 1:
             # diagnostic (MPITREE_SIM_RANKS=P, one process): time rank 0's
             # serpentine share alone on the GPU, then finish the rest so the
