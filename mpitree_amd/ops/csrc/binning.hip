@@ -74,14 +74,27 @@ __global__ __launch_bounds__(kEdgeThreads) void edges_kernel(const XT* __restric
     s_over = use_hash ? 0 : 1;
   }
   for (int i = tid; i < kEdgeHash; i += kEdgeThreads) hset[i] = kEmpty;
-  for (int i = tid; i < S; i += kEdgeThreads) {
-    XT v = __builtin_inf();
-    if (i < s) {
-      const int64_t row = (int64_t)i * n / s;  // deterministic strided sample
-      v = X[row * F + f];
-      if (v == (XT)0) v = (XT)0;  // -0 and +0 are one value (x <= t cannot tell them apart)
+  // kEdgeLoads independent gathers in flight per thread before the LDS stores:
+  // each is a lone 4-8 B read from a different row, so the sample phase is
+  // latency-bound (one-at-a-time issue measured 75 us of a 1M x 64 fit)
+  constexpr int kEdgeLoads = 8;
+  for (int i0 = tid; i0 < S; i0 += kEdgeThreads * kEdgeLoads) {
+    XT v[kEdgeLoads];
+#pragma unroll
+    for (int u = 0; u < kEdgeLoads; ++u) {
+      const int i = i0 + u * kEdgeThreads;
+      v[u] = __builtin_inf();
+      if (i < s) {
+        const int64_t row = (int64_t)i * n / s;  // deterministic strided sample
+        v[u] = X[row * F + f];
+      }
     }
-    key[i] = v;
+#pragma unroll
+    for (int u = 0; u < kEdgeLoads; ++u) {
+      const int i = i0 + u * kEdgeThreads;
+      // -0 and +0 are one value (x <= t cannot tell them apart)
+      if (i < S) key[i] = v[u] == (XT)0 ? (XT)0 : v[u];
+    }
   }
   __syncthreads();
   // ---- exact-mode probe: distinct values into the LDS hash set
