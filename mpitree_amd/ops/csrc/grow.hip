@@ -28,7 +28,10 @@
 
 namespace mt {
 
-constexpr int kPlanThreads = 1024;
+#ifndef MT_PLAN_THREADS
+#define MT_PLAN_THREADS 512
+#endif
+constexpr int kPlanThreads = MT_PLAN_THREADS;  // (variant builds: tools/build_variant.sh)
 constexpr int kPlanWaves = kPlanThreads / kWave;
 
 __device__ __forceinline__ int plan_scan_excl(int v, int* s_w, int& total) {
