@@ -78,40 +78,56 @@ __global__ __launch_bounds__(kAsmThreads) void asm_offsets_kernel(int32_t* __res
 }
 
 // Final node id of every written position (positions no node occupies get -1),
-// and the tree's depth (max over written positions) into total[1].
+// and the tree's depth (max over written positions) into total[1]. Position
+// p = tile + k * kAsmThreads + thread (coalesced, the count kernel's order);
+// the in-tile rank comes from per-(k, wave) ballot masks kept in LDS, and
+// each workgroup adds one atomic for the depth.
 __global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __restrict__ rec,
                                                                int64_t P,
                                                                const int32_t* __restrict__ tile_off,
                                                                int32_t* __restrict__ rank,
                                                                int64_t* __restrict__ total) {
-  // thread t owns kAsmPer consecutive positions so the in-tile order is preserved
-  const int64_t base = (int64_t)blockIdx.x * kAsmTile + (int64_t)threadIdx.x * kAsmPer;
+  constexpr int kW = kAsmThreads / kWave;
+  __shared__ unsigned long long s_mask[kAsmPer][kW];
+  __shared__ int s_ktot[kAsmPer];
+  __shared__ int s_dmax[kW];
+  const int64_t base = (int64_t)blockIdx.x * kAsmTile;
+  const int lane = lane_id(), wv = (int)(threadIdx.x >> 6);
   uint32_t flags = 0;
-  int c = 0, dmax = 0;
+  int dmax = 0;
+#pragma unroll
   for (int k = 0; k < kAsmPer; ++k) {
-    const int64_t p = base + k;
+    const int64_t p = base + (int64_t)k * kAsmThreads + threadIdx.x;
     const bool v = p < P && rec[p * 6 + 5] > 0;
     flags |= (uint32_t)v << k;
-    c += v;
     if (v) dmax = max(dmax, rec[p * 6 + 4]);
+    const unsigned long long b = __ballot(v);
+    if (lane == 0) s_mask[k][wv] = b;
   }
-  {
-    int m = dmax;
-    for (int d = kWave / 2; d > 0; d >>= 1) m = max(m, __shfl_xor(m, d, kWave));
-    if (lane_id() == 0 && m > 0)
-      atomicMax(reinterpret_cast<unsigned long long*>(total) + 1, (unsigned long long)m);
-  }
-  const int incl = (int)wave_incl_scan_u32((uint32_t)c);
-  __shared__ int w[kAsmThreads / kWave];
-  if (lane_id() == kWave - 1) w[threadIdx.x >> 6] = incl;
+  for (int d = kWave / 2; d > 0; d >>= 1) dmax = max(dmax, __shfl_xor(dmax, d, kWave));
+  if (lane == 0) s_dmax[wv] = dmax;
   __syncthreads();
+  if (threadIdx.x < kAsmPer) {
+    int t = 0;
+    for (int w = 0; w < kW; ++w) t += __popcll(s_mask[threadIdx.x][w]);
+    s_ktot[threadIdx.x] = t;
+  }
+  if (threadIdx.x == 0) {
+    int m = 0;
+    for (int w = 0; w < kW; ++w) m = max(m, s_dmax[w]);
+    if (m > 0) atomicMax(reinterpret_cast<unsigned long long*>(total) + 1, (unsigned long long)m);
+  }
+  __syncthreads();
+  const unsigned long long below = (1ull << lane) - 1ull;
   int off = tile_off[blockIdx.x];
-  for (int k = 0; k < (int)(threadIdx.x >> 6); ++k) off += w[k];
-  int r = off + incl - c;
   for (int k = 0; k < kAsmPer; ++k) {
-    const int64_t p = base + k;
-    if (p >= P) break;
-    rank[p] = ((flags >> k) & 1u) ? r++ : -1;
+    const int64_t p = base + (int64_t)k * kAsmThreads + threadIdx.x;
+    if (p < P) {
+      int r = off + __popcll(s_mask[k][wv] & below);
+      for (int w = 0; w < wv; ++w) r += __popcll(s_mask[k][w]);
+      rank[p] = ((flags >> k) & 1u) ? r : -1;
+    }
+    off += s_ktot[k];
   }
 }
 
