@@ -73,6 +73,7 @@ void launch_grow_init(hipStream_t, const LevelLists&, int64_t, int64_t, int64_t,
                       const int64_t*,
                       int32_t*);
 int finish_reg_lds_bytes(int B);
+int finish_reg_blocks_per_cu(int B, int code_bytes);
 int job_sort_max();
 void launch_job_sort(hipStream_t, const int64_t*, int, int, int64_t*, int32_t*);
 void launch_finish_reg(hipStream_t, const void*, int64_t, const void*, int, int64_t, uint32_t*,
@@ -214,6 +215,7 @@ PYBIND11_MODULE(_hip, m) {
                          P<int32_t>(node_i32), P<int32_t>(node_cnt), npos);
   });
   m.def("finish_reg_lds_bytes", &mt::finish_reg_lds_bytes);
+  m.def("finish_reg_blocks_per_cu", &mt::finish_reg_blocks_per_cu);
   m.def("finish_reg", [](uintptr_t s, uintptr_t codes_rm, int64_t row_words, uintptr_t codes_fm,
                          int cb, int64_t n_rows, uintptr_t buf0, uintptr_t buf1, uintptr_t y,
                          uintptr_t jobs, int J, uintptr_t counter, uintptr_t nbins, int F, int B,

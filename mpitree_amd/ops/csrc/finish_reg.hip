@@ -824,6 +824,19 @@ __global__ __launch_bounds__(256) void finish_tiny_reg_kernel(
 
 int finish_reg_lds_bytes(int B) { return kRegFT * B * 12; }
 
+// Resident block-finisher workgroups per CU for B bins (LDS tile and VGPRs): the
+// persistent grid is this many per CU (1M x 64, B = 256: 3 per CU, 9.35 -> 8.83
+// ms per fit against the former fixed 2).
+int finish_reg_blocks_per_cu(int B, int code_bytes) {
+  const void* k = code_bytes == 1 ? (const void*)finish_reg_kernel<uint8_t>
+                                  : (const void*)finish_reg_kernel<uint16_t>;
+  const int lds = finish_reg_lds_bytes(B);
+  MT_HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  int per_cu = 0;
+  MT_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kRegThreads, lds));
+  return per_cu < 1 ? 1 : per_cu;
+}
+
 // counter: int32 [4] = {job cursor, tiny count, tiny cursor, -}, zeroed by the host.
 void launch_finish_reg(hipStream_t stream, const void* codes_rm, int64_t row_words,
                        const void* codes_fm, int code_bytes, int64_t n_rows, uint32_t* buf0,

@@ -301,6 +301,7 @@ _ASM_HINT: dict = {}  # (device, positions, C, reg, thresholds) -> last assemble
 
 
 _TASK_FLAGS: dict = {}  # device -> [int32 flag tensor, epoch]
+_REG_PER_CU: dict = {}  # (bins, code bytes) -> regression finisher workgroups per CU
 _FIN_WATCH: list = []  # pinned views of finisher watchdog words, checked at assembly
 
 
@@ -705,7 +706,13 @@ class HipBackend:
         tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
         tiny = torch.empty((int(job_rows // 2 + J + 1), 8), dtype=torch.int64, device=self.device)
         md = -1 if params.max_depth is None else int(params.max_depth)
-        grid = int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU))
+        grid = os.environ.get("MPITREE_FIN_GRID")
+        if grid is None:  # as many persistent workgroups as fit a CU (LDS tile, VGPRs)
+            key = (self.B, self.cb)
+            if key not in _REG_PER_CU:
+                _REG_PER_CU[key] = int(self.hip.finish_reg_blocks_per_cu(self.B, self.cb))
+            grid = _REG_PER_CU[key] * N_CU
+        grid = int(grid)
         task_cap = int(job_rows // (2 * max(tiny_rows, 1) + 1) + 16)
         steal = os.environ.get("MPITREE_FIN_STEAL", "1")
         if steal == "0":
