@@ -46,6 +46,9 @@ constexpr int kFinMaxC = 16;     // classes supported by the finisher
 constexpr int kFinTab = 1024;    // LDS x*log2(x) entries
 // MT_FIN_UNROLL / MT_FIN_PAIR / MT_TINY_SMALL: compile-time overrides for variant
 // builds (tools/build_variant.sh, measured in profiles/kernel_experiments.md)
+#ifndef MT_FIN_HANDOFF  // hand off only children above this many tiny subtrees' rows
+#define MT_FIN_HANDOFF 2
+#endif
 #ifndef MT_FIN_UNROLL
 #define MT_FIN_UNROLL 4
 #endif
@@ -788,7 +791,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           const bool is_left = (pass == 0) ? !left_small : left_small;
           if (is_left ? tlf : trf) continue;
           const int cm_rows = is_left ? nl : nr;
-          if (kC2 && pass == 0 && cm_rows > 2 * tiny_rows) {
+          if (kC2 && pass == 0 && cm_rows > MT_FIN_HANDOFF * tiny_rows) {
             const int head = __hip_atomic_load(job_counter, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
             const int pushed = (int)(__hip_atomic_load(q_word, __ATOMIC_RELAXED,
