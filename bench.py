@@ -6,7 +6,15 @@ synthetic at 1/2/4/8 GPUs". One *step* is one complete ``fit`` of a
 ``DecisionTreeClassifier`` (entropy, the reference's criterion and default
 hyperparameters unless overridden) from raw device features to the finished
 tree: input validation, label encoding, feature binning, level-wise growth,
-subtree finishing and the host copy of the tree arrays.
+subtree finishing, device assembly of every tree column (features, bins,
+thresholds, child links, depths, node sizes, class counts, impurities) and
+the host copy of those columns. ``fit`` returns a finished ``TreeArrays``:
+no column is derived on the host after the timer stops (``"materialized":
+true``).
+
+``--continuous`` fits N(0, 1) features (every value distinct): the
+reference's threshold semantics (every unique value a candidate) then run on
+the presorted-list exact engine instead of the <= 256-value histogram engines.
 
 Single GPU: ``python bench.py``. Multi-GPU (one process per GPU, RCCL):
 ``torchrun --nproc-per-node N bench.py --gpus N``; every rank holds the full
@@ -31,6 +39,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 
@@ -54,6 +63,8 @@ def main(argv=None):
     ap.add_argument("--criterion", default="entropy")
     ap.add_argument("--strategy", default="auto")
     ap.add_argument("--regression", action="store_true")
+    ap.add_argument("--continuous", action="store_true",
+                    help="N(0,1) features: exact thresholds over every unique value")
     ap.add_argument("--profile-levels", action="store_true")
     a = ap.parse_args(argv)
 
@@ -72,11 +83,13 @@ def main(argv=None):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     md = None if a.max_depth < 0 else a.max_depth
+    levels = None if a.continuous else 256
     if a.regression:
-        X, y = make_regression(a.n, a.features, seed=0, device=dev)
+        X, y = make_regression(a.n, a.features, levels=levels, seed=0, device=dev)
         crit = "squared_error"
     else:
-        X, y = make_classification(a.n, a.features, n_classes=a.classes, seed=0, device=dev)
+        X, y = make_classification(a.n, a.features, n_classes=a.classes, levels=levels, seed=0,
+                                   device=dev)
         crit = a.criterion
     if world > 1:
         import torch.distributed as dist
@@ -109,6 +122,12 @@ def main(argv=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     stats = est.fit_stats_
+    ta = est.tree_arrays_
+    # the fit returned finished columns (numpy arrays over host memory, no
+    # lazily derived attributes): check it, outside the timed region
+    cols = ("feature", "threshold", "threshold_bin", "left", "right", "depth", "n_samples",
+            "impurity", "value" if a.regression else "count")
+    materialized = all(isinstance(ta.__dict__.get(c), np.ndarray) for c in cols)
     mode = stats.get("mode", "single-gpu")
     if world > 1:
         parallelism = {"feature": f"fp{world}", "data": f"dp{world}",
@@ -138,8 +157,11 @@ def main(argv=None):
             "dtype": "fp32",
             "dtype_detail": "fp32 features (exact data-value thresholds), int32 histogram "
                             "counts, fp64 split criterion",
-            "data": "synthetic (generated on device: 256-level quantized features, labels from "
-                    "a random linear + interaction score with Gaussian noise)",
+            "data": "synthetic (generated on device: "
+                    + ("continuous N(0,1) features, every value a candidate threshold"
+                       if a.continuous else "256-level quantized features")
+                    + ", labels from a random linear + interaction score with Gaussian noise)",
+            "materialized": materialized,
             "config": {
                 "name": cfg_name,
                 "model": f"DecisionTree{'Regressor' if a.regression else 'Classifier'}"
@@ -158,6 +180,7 @@ def main(argv=None):
                 + int(stats.get("comm_bytes_exchange", 0)),
                 "tree_nodes": stats.get("node_count"),
                 "tree_depth": stats.get("max_depth"),
+                "thresholds": stats.get("thresholds", "exact (<= 256 values per feature)"),
                 "comm_bytes_per_level": stats.get("comm_bytes_per_level"),
                 "peak_device_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 3),
             },

@@ -37,115 +37,43 @@ class TreeArrays:
     value: Optional[np.ndarray] = None  # float64 [N] (regression leaf mean)
     meta: dict = field(default_factory=dict)
 
-    # ------------------------------------------------------- deferred columns
-    def __getattr__(self, name):
-        # reached only when normal lookup fails: a column of a device-assembled
-        # tree that is derived from the transferred ones on first use
-        derive = self.__dict__.get("_derive")
-        if derive and name in derive:
-            v = derive.pop(name)(self)
-            self.__dict__[name] = v
-            return v
-        raise AttributeError(f"{type(self).__name__!s} has no attribute {name!r}")
-
-    def materialize(self) -> "TreeArrays":
-        """Compute every deferred column now."""
-        for name in list(self.__dict__.get("_derive") or ()):
-            getattr(self, name)
-        return self
-
-    def __getstate__(self):
-        self.materialize()
-        return {k: v for k, v in self.__dict__.items() if k != "_derive"}
-
-    def __setstate__(self, state):
-        self.__dict__.update(state)
-
     @classmethod
-    def deferred(cls, derive: dict, **cols) -> "TreeArrays":
-        """A tree whose columns in ``derive`` (name -> fn(tree)) are computed on
-        first access; ``cols`` are set now."""
-        ta = cls.__new__(cls)
-        ta.__dict__.update(cols)
-        ta.__dict__.setdefault("meta", {})
-        ta.__dict__["_derive"] = dict(derive)
-        return ta
+    def from_packed(cls, buf: np.ndarray, N: int, C: int, regression: bool,
+                    max_depth: int | None = None) -> "TreeArrays":
+        """Views of the device assembly's packed columns (``ops/csrc/assemble.hip``
+        ``asm_cols``): n_samples i64 | threshold f64 | impurity f64 | counts i64
+        [N, C] (or leaf value f64 + fixed-point sum i64) | feature, threshold_bin,
+        left, right, depth i32. Every column is final: no host pass follows."""
+        o = 0
 
-    @classmethod
-    def from_device_columns(cls, *, stats, threshold, split, right, max_depth: int,
-                            criterion: int, regression: bool, y_exp: int = 0,
-                            edges_table=None) -> "TreeArrays":
-        """The device assembly's columns (``ops/csrc/assemble.hip``): class
-        counts (int32) or regression {count, fixed-point sum} (int64), split
-        thresholds, packed splits ``feature << 16 | bin`` (-1: leaf) and right
-        children in pre-order, plus the tree depth. Features, bins, left
-        children (pre-order: node + 1), depths, node sizes, int64 counts,
-        impurities and regression leaf values follow from them and are computed
-        on first use with the same integer-form criterion as every builder
-        (``core/criterion.py``, bitwise equal to the device's). ``threshold``
-        None: split values come from ``edges_table[feature, bin]`` (the host's
-        padded edge table, the values the device table holds) on first use."""
-        from ..core import criterion as cr
+        def take(dtype, count):
+            nonlocal o
+            a = buf[o : o + count * np.dtype(dtype).itemsize].view(dtype)
+            o += count * np.dtype(dtype).itemsize
+            return a
 
-        N = int(right.shape[0])
-        leaf = split == -1
-
-        def feature(t):
-            return np.where(leaf, np.int32(-1), (split.view(np.uint32) >> 16).astype(np.int32))
-
-        def threshold_bin(t):
-            return np.where(leaf, np.int32(-1), (split & 0xFFFF).astype(np.int32))
-
-        def depth(t):
-            return _preorder_depth(right, leaf)
-
-        def threshold_from_edges(t):
-            out = np.full(N, np.nan)
-            inner = t.feature >= 0
-            out[inner] = edges_table[t.feature[inner], t.threshold_bin[inner]]
-            return out
-
-        def left(t):
-            return np.where(t.feature >= 0, np.arange(1, N + 1, dtype=np.int32),
-                            np.int32(-1)).astype(np.int32)
-
+        n_samples = take(np.int64, N)
+        threshold = take(np.float64, N)
+        impurity = take(np.float64, N)
+        count = value = s_fixed = None
         if regression:
-            def n_samples(t):
-                return stats[:, 0].astype(np.int64)
-
-            def value(t):
-                s = stats[:, 1].astype(np.float64)
-                return np.ldexp(s / np.maximum(stats[:, 0], 1).astype(np.float64), -int(y_exp))
-
-            derive = {"left": left, "n_samples": n_samples, "value": value,
-                      "impurity": lambda t: np.full(N, np.nan), "feature": feature,
-                      "threshold_bin": threshold_bin, "depth": depth}
-            ta = cls.deferred(derive, right=right, count=None)
-            ta.meta["sum_fixed"] = stats[:, 1]
+            value = take(np.float64, N)
+            s_fixed = take(np.int64, N)
         else:
-            def n_samples(t):
-                return stats.sum(axis=1, dtype=np.int64)
-
-            def impurity(t):
-                m = t.n_samples
-                c = cr.Criterion(int(criterion))
-                term = (cr.entropy_term(stats) if c == cr.Criterion.ENTROPY
-                        else cr.gini_term(stats))
-                with np.errstate(invalid="ignore", divide="ignore"):
-                    return np.where(m > 0, term / np.maximum(m, 1).astype(np.float64), 0.0)
-
-            derive = {"left": left, "n_samples": n_samples, "impurity": impurity,
-                      "count": lambda t: stats.astype(np.int64), "feature": feature,
-                      "threshold_bin": threshold_bin, "depth": depth}
-            ta = cls.deferred(derive, right=right, value=None)
-        if threshold is not None:
-            ta.__dict__["threshold"] = threshold
-        else:
-            ta.__dict__["_derive"]["threshold"] = threshold_from_edges
-            ta.meta["edges_table"] = edges_table
-        ta.meta["final"] = True  # thresholds, impurity and values need no host pass
-        ta.meta["max_depth"] = int(max_depth)
-        ta.meta["stats_raw"] = stats  # (the cross-rank digest hashes what was transferred)
+            count = take(np.int64, N * C).reshape(N, C)
+        feature = take(np.int32, N)
+        threshold_bin = take(np.int32, N)
+        left = take(np.int32, N)
+        right = take(np.int32, N)
+        depth = take(np.int32, N)
+        ta = cls(feature=feature, threshold=threshold, threshold_bin=threshold_bin, left=left,
+                 right=right, depth=depth, n_samples=n_samples, impurity=impurity, count=count,
+                 value=value)
+        if regression:
+            ta.meta["sum_fixed"] = s_fixed
+        ta.meta["final"] = True  # thresholds, impurities and values need no host pass
+        if max_depth is not None:
+            ta.meta["max_depth"] = int(max_depth)
         return ta
 
     # ------------------------------------------------------------------ basics
@@ -159,7 +87,7 @@ class TreeArrays:
 
     @property
     def max_depth(self) -> int:
-        if "max_depth" in self.meta and "depth" not in self.__dict__:
+        if "max_depth" in self.meta:
             return int(self.meta["max_depth"])  # device-assembled: reduced on the device
         return int(self.depth.max()) if self.node_count else 0
 
@@ -505,29 +433,3 @@ class TreeArrays:
             count=None if d.get("count") is None else np.asarray(d["count"]),
             value=None if d.get("value") is None else np.asarray(d["value"]),
         )
-
-
-# the dataclass keeps these defaults in __init__; without the class attributes a
-# deferred count / value is found by __getattr__ rather than the class-level None
-del TreeArrays.count, TreeArrays.value
-
-
-def _preorder_depth(right: np.ndarray, leaf: np.ndarray) -> np.ndarray:
-    """Node depths of a pre-order tree from its right-child links: an internal
-    node i (left child i + 1) adds one to every node of its subtree after it,
-    positions (i, end_i) with end_i = 1 + the last node of the subtree, reached
-    by following right links to a leaf (pointer jumping, O(N log depth))."""
-    N = int(right.shape[0])
-    if N == 0:
-        return np.zeros(0, np.int32)
-    idx = np.arange(N, dtype=np.int64)
-    last = np.where(leaf, idx, right.astype(np.int64))
-    while True:
-        nxt = last[last]
-        if np.array_equal(nxt, last):
-            break
-        last = nxt
-    inner = ~leaf
-    delta = np.bincount(idx[inner] + 1, minlength=N + 1) - np.bincount(last[inner] + 1,
-                                                                         minlength=N + 1)
-    return np.cumsum(delta[:N]).astype(np.int32)

@@ -14,10 +14,11 @@
 //   rank_kernel    per tile: each written position's final node id
 //   emit_kernel    per written position: the final row of every output column,
 //                  child links through the rank table, split thresholds from
-//                  the padded bin-edge table, node terms / impurity / leaf value
-//                  with the same integer-form criterion as every other builder
+//                  the padded bin-edge table, node sizes, impurities / leaf
+//                  values with the same integer-form criterion as every other
+//                  builder
 //
-// so the host receives finished, pre-ordered columns in one pinned copy.
+// so the host receives the finished, pre-ordered tree in one pinned copy.
 #include "common.h"
 #include "criterion.h"
 
@@ -133,32 +134,62 @@ __global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __
 
 // Output columns, packed back to back for one D2H; the node count N is read
 // from the device (asm_offsets_kernel's total), so the emit launch needs no
-// host round trip. Only what the host cannot derive cheaply crosses the link:
-//   stats [N][C] (int32 class counts; regression int64 {count, fixed sum})
-//   | threshold f64 [N] (only when the host has no edge table: the exact
-//   engine's unique values stay on the device) | split i32 [N] = feature << 16 |
-//   bin (-1: leaf) | right i32 [N]
-// Left children are implicit in pre-order (node j + 1), depths follow from the
-// child links (the tree's depth travels with the node count), node sizes are the
-// stats' sums, impurities and leaf values follow from the stats with the same
-// integer-form criterion: the host derives those columns on first use
-// (TreeArrays.deferred). 16 B per node for a two-class tree instead of 60.
-// (feature < 2^15 -- the caller checks F -- and bin < 2^16: codes are <= 16 bits.)
+// host round trip. Every column of the finished tree is emitted in its final
+// dtype -- the host receives numpy views, nothing is derived after the copy:
+//   n_samples i64 [N] | threshold f64 [N] | impurity f64 [N]
+//   | counts i64 [N][C] (classification) or leaf value f64 [N] + fixed-point
+//     target sum i64 [N] (regression)
+//   | feature i32 [N] | threshold_bin i32 [N] | left i32 [N] | right i32 [N]
+//   | depth i32 [N]
+// Impurities use the integer-form criterion of every builder (criterion.h:
+// (T(m) - sum_c T(c)) / m, gini (m^2 - sum c^2) / m / m), regression leaf values
+// ldexp(S / m, -y_exp): the same IEEE op sequence as the host builders, so the
+// columns equal theirs bit for bit. Bins are a column of their own (exact-engine
+// value ranks exceed 16 bits).
 struct AsmCols {
-  void* stats;
+  int64_t* nsamp;
   double* threshold;
-  int32_t* split;
+  double* impurity;
+  int64_t* count;  // classification
+  double* value;   // regression
+  int64_t* sum;    // regression
+  int32_t* feature;
+  int32_t* bin;
+  int32_t* left;
   int32_t* right;
+  int32_t* depth;
 };
 
-__device__ inline AsmCols asm_cols(uint8_t* base, int64_t N, int C, bool reg, bool thr) {
+__host__ __device__ inline int64_t asm_bytes(int64_t N, int C, bool reg) {
+  return N * (24 + (reg ? 16 : 8 * (int64_t)C) + 20);
+}
+
+__device__ inline AsmCols asm_cols(uint8_t* base, int64_t N, int C, bool reg) {
   AsmCols o;
-  o.stats = base;
-  const int64_t sbytes = reg ? N * 16 : ((N * C * 4 + 7) & ~(int64_t)7);
-  o.threshold = thr ? reinterpret_cast<double*>(base + sbytes) : nullptr;
-  int32_t* p4 = reinterpret_cast<int32_t*>(base + sbytes + (thr ? N * 8 : 0));
-  o.split = p4;
-  o.right = p4 + N;
+  uint8_t* p = base;
+  o.nsamp = reinterpret_cast<int64_t*>(p);
+  p += N * 8;
+  o.threshold = reinterpret_cast<double*>(p);
+  p += N * 8;
+  o.impurity = reinterpret_cast<double*>(p);
+  p += N * 8;
+  o.count = nullptr;
+  o.value = nullptr;
+  o.sum = nullptr;
+  if (reg) {
+    o.value = reinterpret_cast<double*>(p);
+    p += N * 8;
+    o.sum = reinterpret_cast<int64_t*>(p);
+    p += N * 8;
+  } else {
+    o.count = reinterpret_cast<int64_t*>(p);
+    p += N * 8 * (int64_t)C;
+  }
+  o.feature = reinterpret_cast<int32_t*>(p);
+  o.bin = o.feature + N;
+  o.left = o.bin + N;
+  o.right = o.left + N;
+  o.depth = o.right + N;
   return o;
 }
 
@@ -167,32 +198,57 @@ template <typename StatT>
 __global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
     const int32_t* __restrict__ rec, const StatT* __restrict__ st, int64_t P, int C,
     const int32_t* __restrict__ rank, const double* __restrict__ edges, int EB,
-    const int64_t* __restrict__ total, uint8_t* __restrict__ base, bool reg, bool thr) {
+    const int64_t* __restrict__ total, uint8_t* __restrict__ base, bool reg, int crit, int y_exp,
+    const double* __restrict__ xtab, int xtab_n) {
   const int64_t p = (int64_t)blockIdx.x * kAsmThreads + threadIdx.x;
   if (p >= P) return;
   const int j = rank[p];
   if (j < 0) return;
-  const AsmCols o = asm_cols(base, *total, C, reg, thr);
+  const AsmCols o = asm_cols(base, *total, C, reg);
   const int32_t* R = rec + p * 6;
   const int f = R[0];
   const int b = R[1];
   if (f >= 0) {
-    o.split[j] = (int32_t)(((uint32_t)f << 16) | ((uint32_t)b & 0xffffu));
+    o.feature[j] = f;
+    o.bin[j] = b;
+    o.left[j] = rank[R[2]];
     o.right[j] = rank[R[3]];
-    if (thr) o.threshold[j] = edges[(int64_t)f * EB + b];
+    o.threshold[j] = edges[(int64_t)f * EB + b];
   } else {
-    o.split[j] = -1;
+    o.feature[j] = -1;
+    o.bin[j] = -1;
+    o.left[j] = -1;
     o.right[j] = -1;
-    if (thr) o.threshold[j] = __builtin_nan("");
+    o.threshold[j] = __builtin_nan("");
   }
+  o.depth[j] = R[4];
   const StatT* s = st + p * C;
+  auto T = [&](int64_t x) -> double {
+    return x < (int64_t)xtab_n ? xtab[x] : xlog2x((uint64_t)x);
+  };
   if (reg) {
-    int64_t* so = reinterpret_cast<int64_t*>(o.stats) + (int64_t)j * 2;
-    so[0] = (int64_t)s[0];
-    so[1] = (int64_t)s[1];
+    const int64_t m = (int64_t)s[0], sf = (int64_t)s[1];
+    o.nsamp[j] = m;
+    o.sum[j] = sf;
+    o.value[j] = ldexp((double)sf / (double)(m > 1 ? m : 1), -y_exp);
+    o.impurity[j] = __builtin_nan("");
   } else {
-    int32_t* so = reinterpret_cast<int32_t*>(o.stats) + (int64_t)j * C;
-    for (int c = 0; c < C; ++c) so[c] = (int32_t)s[c];
+    int64_t m = 0, sq = 0;
+    double acc = 0.0;
+    for (int c = 0; c < C; ++c) {
+      const int64_t v = (int64_t)s[c];
+      o.count[(int64_t)j * C + c] = v;
+      m += v;
+      sq += v * v;
+      acc = acc + T(v);
+    }
+    o.nsamp[j] = m;
+    double imp = 0.0;
+    if (m > 0) {
+      const double term = crit == kEntropy ? T(m) - acc : gini_term(m, sq);
+      imp = term / (double)m;
+    }
+    o.impurity[j] = imp;
   }
 }
 
@@ -210,22 +266,22 @@ void launch_asm_rank(hipStream_t stream, const int32_t* rec, int64_t P, int32_t*
 
 int asm_tiles(int64_t P) { return (int)((P + kAsmTile - 1) / kAsmTile); }
 
-// upper bound per node (the stats block is padded to 8 bytes once, not per node)
-int64_t asm_node_bytes(int C, bool reg) { return (reg ? 16 : 4 * C) + 8 + 2 * 4 + 8; }
+int64_t asm_node_bytes(int C, bool reg) { return asm_bytes(1, C, reg); }
 
 void launch_asm_emit(hipStream_t stream, const int32_t* rec, const void* st, bool st64,
                      int64_t P, int C, const int32_t* rank, const double* edges, int EB,
-                     const int64_t* total, uint8_t* base, bool reg, bool thr) {
+                     const int64_t* total, uint8_t* base, bool reg, int crit, int y_exp,
+                     const double* xtab, int xtab_n) {
   const int64_t blocks = (P + kAsmThreads - 1) / kAsmThreads;
   if (blocks == 0) return;
   if (st64)
     hipLaunchKernelGGL(asm_emit_kernel<int64_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
                        stream, rec, (const int64_t*)st, P, C, rank, edges, EB, total, base, reg,
-                       thr);
+                       crit, y_exp, xtab, xtab_n);
   else
     hipLaunchKernelGGL(asm_emit_kernel<int32_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
                        stream, rec, (const int32_t*)st, P, C, rank, edges, EB, total, base, reg,
-                       thr);
+                       crit, y_exp, xtab, xtab_n);
   MT_HIP_CHECK(hipGetLastError());
 }
 

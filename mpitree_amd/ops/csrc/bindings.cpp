@@ -94,7 +94,8 @@ void launch_small_fit(hipStream_t, const void*, int, int64_t, int, int, const in
                       int, int64_t, int64_t, const double*, int, uint16_t*, int32_t*, int32_t*,
                       int64_t);
 void launch_asm_emit(hipStream_t, const int32_t*, const void*, bool, int64_t, int,
-                     const int32_t*, const double*, int, const int64_t*, uint8_t*, bool, bool);
+                     const int32_t*, const double*, int, const int64_t*, uint8_t*, bool, int, int,
+                     const double*, int);
 }  // namespace mt
 
 template <typename T>
@@ -383,9 +384,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("asm_node_bytes", &mt::asm_node_bytes);
   m.def("asm_emit", [](uintptr_t s, uintptr_t rec, uintptr_t st, bool st64, int64_t npos, int C,
                        uintptr_t rank, uintptr_t edges, int EB, uintptr_t total, uintptr_t base,
-                       bool reg, bool thr) {
+                       bool reg, int crit, int y_exp, uintptr_t xtab, int xtab_n) {
     mt::launch_asm_emit(S(s), P<int32_t>(rec), P<void>(st), st64, npos, C, P<int32_t>(rank),
-                        P<double>(edges), EB, P<int64_t>(total), P<uint8_t>(base), reg, thr);
+                        P<double>(edges), EB, P<int64_t>(total), P<uint8_t>(base), reg, crit,
+                        y_exp, P<double>(xtab), xtab_n);
   });
   m.def("label_count", [](uintptr_t s, uintptr_t y, int64_t n, int64_t lo, int R,
                           uintptr_t counts, bool checked) {

@@ -625,11 +625,11 @@ class DeviceGrower:
         self.stats["levels"] = levels
         self.stats["finisher_subtrees"] = J
         t0 = time.perf_counter()
-        # the host edge table: thresholds are derived from it on first use
-        # instead of crossing the link (8 B per node)
-        table = edges if isinstance(edges, np.ndarray) else edges.padded_edges()
-        ta = be.assemble_positions(table, int(p.criterion), y_exp, d_edges=d_edges,
-                                   host_table=table)
+        # thresholds come from the device edge table (uploaded when absent)
+        table = None
+        if d_edges is None:
+            table = edges if isinstance(edges, np.ndarray) else edges.padded_edges()
+        ta = be.assemble_positions(table, int(p.criterion), y_exp, d_edges=d_edges)
         self.timings["assemble"] = time.perf_counter() - t0
         if self.ckpt is not None:
             self.stats["checkpoint_levels_saved"] = self.ckpt.saved_levels

@@ -543,25 +543,18 @@ class HipBackend:
         self.pos_rec.index_copy_(0, d_pos, d_rec.reshape(-1, 6).to(torch.int32))
         self.pos_st.index_copy_(0, d_pos, d_st.reshape(-1, self.C).to(self.pos_st.dtype))
 
-    def assemble_positions(self, edges, crit: int, y_exp: int = 0, d_edges=None,
-                           host_table=None) -> TreeArrays:
-        """Compact the position space into a pre-ordered :class:`TreeArrays`
-        (numpy views of one pinned host buffer). ``d_edges``: the device fp64
-        edge table ``[F, W]`` (any row stride); otherwise ``edges`` (host
-        ``[F, W]``) is uploaded. Rank -> emit run back to back (the emit kernel
-        lays the columns out from the device node count), then two small host
-        waits: the node count, and the single D2H of the columns. Only stats,
-        thresholds, feature, bin, right child and depth cross the link; left
-        children, node sizes, impurities, int64 counts and leaf values are
-        derived from them on first use (``TreeArrays.deferred``); so are the
-        thresholds when ``host_table`` (the host's padded edge table) is given."""
+    def assemble_positions(self, edges, crit: int, y_exp: int = 0, d_edges=None) -> TreeArrays:
+        """Compact the position space into the finished, pre-ordered
+        :class:`TreeArrays` (numpy views of one pinned host buffer; every column
+        is computed on the device, nothing is derived on the host afterwards).
+        ``d_edges``: the device fp64 threshold table ``[F, W]`` (any row stride);
+        otherwise ``edges`` (host ``[F, W]``) is uploaded. Rank -> emit run back
+        to back (the emit kernel lays the columns out from the device node
+        count), then the host waits for the node count and the single D2H."""
         P, C = self.P, self.C
-        if self.F > 65535:  # the link packs feature << 16 | bin into 32 bits
-            raise ValueError("GPU fits support at most 65535 features")
         hip = self.hip
         s = _stream()
-        thr = host_table is None
-        if thr and d_edges is None:
+        if d_edges is None:
             d_edges = torch.from_numpy(np.ascontiguousarray(edges, np.float64)).to(self.device)
         tiles = hip.asm_tiles(P)
         bpn = int(hip.asm_node_bytes(C, self.reg))
@@ -574,52 +567,34 @@ class HipBackend:
         total = ws[o_total : o_total + 16].view(torch.int64)  # {nodes, depth}
         hip.asm_rank(s, self.pos_rec.data_ptr(), P, base, base + o_total, base + o_rank)
         hip.asm_emit(s, self.pos_rec.data_ptr(), self.pos_st.data_ptr(), self.reg, P, C,
-                     base + o_rank, d_edges.data_ptr() if thr else 0,
-                     int(d_edges.stride(0)) if thr else 0, base + o_total, base + o_out,
-                     bool(self.reg), thr)
+                     base + o_rank, d_edges.data_ptr(), int(d_edges.stride(0)),
+                     base + o_total, base + o_out, bool(self.reg), int(crit), int(y_exp),
+                     self.xtab.data_ptr(), XTAB_N)
         h_total = _pinned_copy(total, "asm.total")
-
-        def col_bytes(N):
-            sb = N * 16 if self.reg else (N * C * 4 + 7) // 8 * 8
-            return sb, sb + (N * 8 if thr else 0) + N * 8
-
         # the columns are laid out from the device node count, so a copy sized for
         # the previous fit's count on this position space (a refit of the same
         # data: the same count) is a prefix-complete guess, enqueued before the
-        # wait -- one host wait instead of two, the pinned allocation overlapping
-        # the finisher; a larger tree copies the rest after the count arrives
-        key = (str(self.device), P, C, bool(self.reg), thr)
+        # wait -- one host wait instead of two; a larger tree copies the rest
+        # after the count arrives
+        key = (str(self.device), P, C, bool(self.reg))
         guess = _ASM_HINT.get(key, 0)
         host, have = None, 0
         if guess:
-            have = col_bytes(guess)[1]
+            have = guess * bpn
             host = torch.empty(max(have, 8), dtype=torch.uint8, pin_memory=True)
             host[:have].copy_(ws[o_out : o_out + have], non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
         self._check_finisher_watch()
         N, max_depth = int(h_total[0]), int(h_total[1])
         _ASM_HINT[key] = N
-        sbytes, nbytes = col_bytes(N)
+        nbytes = N * bpn
         if nbytes > have:
             host = torch.empty(max(nbytes, 8), dtype=torch.uint8, pin_memory=True)
             host[:nbytes].copy_(ws[o_out : o_out + nbytes], non_blocking=True)
             torch.cuda.current_stream(self.device).synchronize()
-        h = host.numpy()
-        if self.reg:
-            stats = h[: N * 16].view(np.int64).reshape(N, 2)
-        else:
-            stats = h[: N * C * 4].view(np.int32).reshape(N, C)
-        o = sbytes
-        threshold = None
-        if thr:
-            threshold = h[o : o + N * 8].view(np.float64)
-            o += N * 8
-        i4 = h[o : o + N * 8].view(np.int32)
         self.pos_rec = self.pos_st = None
-        return TreeArrays.from_device_columns(
-            stats=stats, threshold=threshold, split=i4[:N], right=i4[N : 2 * N],
-            max_depth=max_depth, criterion=int(crit), regression=bool(self.reg),
-            y_exp=int(y_exp), edges_table=host_table)
+        return TreeArrays.from_packed(host.numpy()[:nbytes], N, C, bool(self.reg),
+                                      max_depth=max_depth)
 
     def small_fit_supported(self, comm=None) -> bool:
         """One-workgroup whole-tree fit (``small_fit.hip``): classification on

@@ -69,18 +69,8 @@ def tree_digest(ta) -> int:
     child links and node sizes. Thresholds are hashed too, so ranks that
     disagree on bin edges (e.g. row shards binned apart) cannot match.
     xxh3 over the arrays in place: ~0.3 ms for 200k nodes."""
-    meta = ta.meta if isinstance(getattr(ta, "meta", None), dict) else {}
-    raw = meta.get("stats_raw")
-    if raw is not None:  # device-assembled tree: its transferred columns determine the rest
-        table = meta.get("edges_table")
-        if table is not None and "threshold" not in ta.__dict__:
-            thr = np.ascontiguousarray(table, dtype=np.float64)  # thresholds = table[f, bin]
-        else:
-            thr = np.nan_to_num(np.asarray(ta.threshold, dtype=np.float64), nan=0.0)
-        parts = (ta.feature, ta.threshold_bin, ta.right, raw, thr)
-    else:
-        thr = np.nan_to_num(np.asarray(ta.threshold, dtype=np.float64), nan=0.0)
-        parts = (ta.feature, ta.threshold_bin, ta.left, ta.right, ta.n_samples, thr)
+    thr = np.nan_to_num(np.asarray(ta.threshold, dtype=np.float64), nan=0.0)
+    parts = (ta.feature, ta.threshold_bin, ta.left, ta.right, ta.n_samples, thr)
     try:
         import xxhash
 
