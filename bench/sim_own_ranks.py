@@ -1,0 +1,127 @@
+"""Per-rank critical path of a P-GPU subtree-ownership fit, measured on ONE GPU.
+
+The multi-GPU ``auto`` / ``subtree`` fit (rows replicated on every rank, the
+reference's ParallelDecisionTreeClassifier contract) runs the device level loop
+replicated until the first level with at least ``k * P`` units (split nodes
+whose children keep growing + finisher jobs so far); that level's planner
+assigns the units to ranks by greedy LPT on row counts and from then on a rank
+grows only its own units -- level loop and finisher -- with no collective until
+one all-gather of the finished nodes (``ops/device_grower.py``,
+``grow.hip own_switch``). Rank r's kernel sequence therefore does not depend on
+the other ranks at all, so it can be run alone: this script fits with a
+stand-in communicator (``world_size = P``, ``rank = r``) whose node all-gather
+returns the other ranks' nodes from a single-GPU reference fit (the trees are
+bit-identical, so the result is the complete tree, and the script checks it
+against the reference). Per P it reports, over ranks, the median fit time of
+each rank's exact sequence (binning, replicated levels, own levels, own
+finisher share, exchange stand-in, assembly + the full tree's D2H):
+
+* ``max_rank_ms`` -- the critical path (what a P-GPU fit waits for, plus the
+  real all-gather's latency: ``exchange_mb`` over xGMI);
+* ``rows_owned`` / ``units`` -- the LPT's per-rank rows and the unit count.
+
+    python bench/sim_own_ranks.py [--n 1000000] [--features 64] [--ranks 1,2,4,8]
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from mpitree_amd.core.levelwise import LocalComm  # noqa: E402
+
+
+class SimOwnComm(LocalComm):
+    """Rank ``rank`` of a P-rank subtree-ownership group, without other ranks:
+    the node exchange returns this rank's rows plus every node of a reference fit."""
+
+    kind = "subtree"
+    simulated = True
+
+    def __init__(self, P: int, rank: int, device, ref_rows: torch.Tensor):
+        self.world_size = P
+        self.rank = rank
+        self.device = device
+        self.bytes_communicated = 0
+        self.ref_rows = ref_rows
+
+    def all_gather_rows(self, t):
+        # bytes of a real exchange: every rank's rows, padded to the largest share
+        self.bytes_communicated += self.ref_rows.numel() * self.ref_rows.element_size()
+        return torch.cat([t, self.ref_rows.to(t.dtype)], 0)
+
+
+def reference_rows(fit, dev):
+    """The position-space rows {pos, record[6], counts[C]} of a finished 1-GPU fit."""
+    from mpitree_amd.ops import hip_backend as hb
+
+    r = fit()
+    n_pos = 2 * r.arrays.n_samples[0] - 1
+    rec = hb._workspace(dev, "pos_rec", 0)[: n_pos * 24].view(torch.int32).view(-1, 6)
+    C = r.arrays.count.shape[1]
+    st = hb._workspace(dev, "pos_st", 0)[: n_pos * C * 4].view(torch.int32).view(-1, C)
+    live = torch.nonzero(rec[:, 5] > 0).squeeze(1)
+    rows = torch.cat([live.to(torch.int32)[:, None], rec[live], st[live]], 1).clone()
+    return r, rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--features", type=int, default=64)
+    ap.add_argument("--ranks", default="1,2,4,8")
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--units-per-rank", type=int, default=None)
+    a = ap.parse_args()
+    if a.units_per_rank is not None:
+        os.environ["MPITREE_OWN_UNITS_PER_RANK"] = str(a.units_per_rank)
+    from mpitree_amd.core.fit import fit_tree
+    from mpitree_amd.utils.datasets import make_classification
+
+    dev = torch.device("cuda", 0)
+    X, y = make_classification(a.n, a.features, n_classes=2, seed=0, device=dev)
+
+    def fit(comm=None):
+        return fit_tree(X, y, regression=False, criterion=0, max_depth=None,
+                        min_samples_split=2, device="cuda", comm=comm)
+
+    for _ in range(2):
+        fit()
+    ref, ref_rows = reference_rows(fit, dev)
+    for P in [int(v) for v in a.ranks.split(",")]:
+        per_rank = []
+        for r in range(P):
+            times, st = [], {}
+            for i in range(a.reps + 2):
+                comm = SimOwnComm(P, r, dev, ref_rows) if P > 1 else None
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                res = fit(comm)
+                torch.cuda.synchronize()
+                if i >= 2:
+                    times.append((time.perf_counter() - t0) * 1e3)
+                st = res.stats
+                assert res.arrays.equal(ref.arrays), f"P={P} rank {r}: tree differs"
+            per_rank.append(dict(ms=float(np.median(times)), rows=st.get("own_rows", a.n),
+                                 units=st.get("own_units", 0), levels=st.get("levels"),
+                                 mode=st.get("mode", "single-gpu"),
+                                 exchange_mb=st.get("comm_bytes_exchange", 0) / 1e6))
+        ms = [p["ms"] for p in per_rank]
+        out = dict(P=P, max_rank_ms=round(max(ms), 3), mean_rank_ms=round(float(np.mean(ms)), 3),
+                   rank_ms=[round(v, 3) for v in ms], rows_owned=[p["rows"] for p in per_rank],
+                   units=per_rank[0]["units"], levels=[p["levels"] for p in per_rank],
+                   mode=per_rank[0]["mode"], exchange_mb=round(per_rank[0]["exchange_mb"], 2),
+                   nodes=ref.arrays.node_count, tree_equal=True)
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

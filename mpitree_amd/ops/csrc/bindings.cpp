@@ -271,13 +271,21 @@ PYBIND11_MODULE(_hip, m) {
                            uintptr_t pos_st, uintptr_t pos_st64, int reg, int out_buf,
                            uintptr_t jobs, uintptr_t job_count, int C, int max_depth, int n_cu,
                            int64_t mss, int64_t msl, int64_t fr, uintptr_t host_ctl, int host_tag,
-                           int dp) {
+                           int dp, py::dict own) {
+    mt::OwnArgs o{0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr};
+    if (own.size()) {
+      auto g = [&](const char* k) { return own[k].cast<int64_t>(); };
+      o = mt::OwnArgs{(int)g("P"), (int)g("rank"), (int)g("min_units"), (int)g("cap"),
+                      P<int32_t>((uintptr_t)g("state")), P<int64_t>((uintptr_t)g("ranges")),
+                      P<int32_t>((uintptr_t)g("node_owner")),
+                      P<int32_t>((uintptr_t)g("job_owner"))};
+    }
     return mt::PlanArgs{lists(cur),          lists(nxt),         P<int64_t>(rec),
                         P<int64_t>(split),   P<int64_t>(pitems), P<int32_t>(cursors),
                         P<int32_t>(pctl),    P<int32_t>(pos_rec), P<int32_t>(pos_st),
                         P<int64_t>(pos_st64), reg, out_buf, P<int64_t>(jobs),
                         P<int32_t>(job_count), C, max_depth, n_cu, mss, msl, fr,
-                        P<int32_t>(host_ctl), host_tag, dp};
+                        P<int32_t>(host_ctl), host_tag, dp, o};
   };
   m.def("grow_plan", [plan_args](uintptr_t s, py::dict cur, py::dict nxt, uintptr_t rec,
                                  uintptr_t split, uintptr_t pitems, uintptr_t cursors,
@@ -285,10 +293,10 @@ PYBIND11_MODULE(_hip, m) {
                                  uintptr_t pos_st64, int reg, int out_buf, uintptr_t jobs,
                                  uintptr_t job_count, int C, int max_depth, int n_cu, int64_t mss,
                                  int64_t msl, int64_t fr, uintptr_t host_ctl, int host_tag,
-                                 int dp, bool fixup) {
+                                 int dp, bool fixup, py::dict own) {
     const mt::PlanArgs a = plan_args(cur, nxt, rec, split, pitems, cursors, pctl, pos_rec, pos_st,
                                      pos_st64, reg, out_buf, jobs, job_count, C, max_depth, n_cu,
-                                     mss, msl, fr, host_ctl, host_tag, dp);
+                                     mss, msl, fr, host_ctl, host_tag, dp, own);
     if (fixup)
       mt::launch_grow_dp_fixup(S(s), a);
     else
@@ -298,7 +306,7 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("pos_st"), py::arg("pos_st64"), py::arg("reg"), py::arg("out_buf"), py::arg("jobs"),
      py::arg("job_count"), py::arg("C"), py::arg("max_depth"), py::arg("n_cu"), py::arg("mss"),
      py::arg("msl"), py::arg("fr"), py::arg("host_ctl"), py::arg("host_tag"), py::arg("dp") = 0,
-     py::arg("fixup") = false);
+     py::arg("fixup") = false, py::arg("own") = py::dict());
   m.def("ex_chunk", &mt::ex_chunk);
   m.def("ex_local_max", &mt::ex_local_max);
   m.def("exact_setup_temp_bytes", &mt::exact_setup_temp_bytes);

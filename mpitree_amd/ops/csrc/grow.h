@@ -45,6 +45,26 @@ struct LevelLists {
   int32_t* src;     // [KMAX] 2 * (parent's split index) + side (data-parallel only)
 };
 
+// Subtree ownership (multi-GPU "subtree" / "auto" fits with replicated rows):
+// the level loop runs replicated until the first level whose *units* -- split
+// nodes with children that keep growing, plus finisher jobs created so far --
+// number at least min_units (or the frontier ends); that level's planner
+// assigns the units to ranks by greedy longest-processing-time on row counts
+// (every rank computes the same assignment from the same replicated state) and
+// from then on each rank grows only its own units. A unit's nodes occupy one
+// contiguous pre-order position range, so the ranks' outputs are disjoint
+// ranges of the position space.
+struct OwnArgs {
+  int P;             // ranks (>= 2: ownership on)
+  int rank;
+  int min_units;     // switch at the first level with at least this many units
+  int cap;           // capacity of ranges / of the LPT (units beyond it: no switch)
+  int32_t* state;    // [4] {switched (0/1), owned ranges, units at the switch, rows owned}
+  int64_t* ranges;   // [cap][2] this rank's position ranges [lo, hi); unused rows {0, 0}
+  int32_t* node_owner;  // [KMAX] scratch: owner of frontier node i at the switch
+  int32_t* job_owner;   // [JMAX] scratch: owner of job j at the switch
+};
+
 struct PlanArgs {
   LevelLists cur, nxt;
   const int64_t* rec;  // [KMAX][5 + 2C] split records of the current level
@@ -61,9 +81,10 @@ struct PlanArgs {
   int32_t* job_count;
   int C, max_depth, n_cu;
   int64_t mss, msl, fr;
-  int32_t* host_ctl;   // [3] host-mapped {next frontier size, jobs so far, tag} or null
+  int32_t* host_ctl;   // [4] host-mapped {next frontier size, jobs so far, tag, switched}
   int32_t host_tag;    // written last: the host polls it to know the slot is complete
   int dp;              // rows sharded across ranks: local segments fixed up after partition
+  OwnArgs own;         // subtree ownership (own.P < 2: off)
 };
 
 }  // namespace mt

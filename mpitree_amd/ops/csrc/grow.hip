@@ -274,18 +274,194 @@ __device__ void plan_minmax_items(const PlanArgs& a, PlanShared& sh, int K2) {
   __syncthreads();
 }
 
+
+// ---- subtree ownership (see OwnArgs in grow.h) -------------------------------
+constexpr int kOwnMax = 2048;                // units the switch level can sort in LDS
+constexpr int32_t kOwnJob = 0x40000000;      // unit id flag: a finisher job (else a node)
+
+struct OwnShared {
+  uint64_t key[kOwnMax];  // {0x7FFFFFFF - rows : 32, root position : 32}: unique, total order
+  int32_t unit[kOwnMax];  // frontier slot i, or kOwnJob | job index
+  int n, any_next, jobs0, nr;
+};
+
+// Pass 0 of the switch level: collect the units (split nodes whose children keep
+// growing, with their rows; finisher jobs so far), decide whether this level
+// switches, and if so assign the units by greedy LPT (largest first, ties by
+// position; each to the least-loaded rank, ties to the lowest), record this
+// rank's position ranges and compact the job list to this rank's jobs.
+// Returns true (block-uniform) when the level switched.
+__device__ bool own_switch(const PlanArgs& a, OwnShared& os, PlanShared& sh, int K, int JW) {
+  const int tid = threadIdx.x;
+  const int P = a.own.P, me = a.own.rank;
+  if (tid == 0) {
+    os.n = 0;
+    os.any_next = 0;
+    os.jobs0 = atomicAdd(a.job_count, 0);
+    os.nr = 0;
+  }
+  __syncthreads();
+  const int J0 = os.jobs0;
+  for (int i = tid; i < K; i += kPlanThreads) {
+    a.own.node_owner[i] = -1;
+    const Decision d = plan_decide(a, i);
+    if (!d.split) continue;
+    int64_t load = 0;
+    for (int c = 0; c < 2; ++c) {
+      if (d.fate[c] >= 1) load += c == 0 ? d.nl : d.nr;
+      if (d.fate[c] == 2) os.any_next = 1;
+    }
+    if (load > 0) {
+      const int u = atomicAdd(&os.n, 1);
+      if (u < kOwnMax) {
+        os.key[u] = ((uint64_t)(0x7FFFFFFFll - load) << 32) | (uint64_t)(a.cur.pos[i] & 0x7FFFFFFF);
+        os.unit[u] = i;
+      }
+    }
+  }
+  for (int j = tid; j < J0; j += kPlanThreads) {
+    const int64_t* J = a.jobs + (int64_t)j * JW;
+    const int u = atomicAdd(&os.n, 1);
+    if (u < kOwnMax) {
+      os.key[u] = ((uint64_t)(0x7FFFFFFFll - J[1]) << 32) | (uint64_t)(J[3] & 0x7FFFFFFF);
+      os.unit[u] = kOwnJob | j;
+    }
+  }
+  __syncthreads();
+  const int U = os.n;
+  const bool sw = U > 0 && U <= kOwnMax && (U >= a.own.min_units || !os.any_next);
+  if (!sw) return false;
+  // bitonic sort of the unit keys (ascending: largest rows first)
+  int N2 = 1;
+  while (N2 < U) N2 <<= 1;
+  for (int i = U + tid; i < N2; i += kPlanThreads) {
+    os.key[i] = ~0ull;
+    os.unit[i] = -1;
+  }
+  __syncthreads();
+  for (int size = 2; size <= N2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < N2; i += kPlanThreads) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const uint64_t ka = os.key[i], kb = os.key[j];
+          const bool up = (i & size) == 0;
+          if ((ka > kb) == up) {
+            os.key[i] = kb;
+            os.key[j] = ka;
+            const int32_t t = os.unit[i];
+            os.unit[i] = os.unit[j];
+            os.unit[j] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // greedy LPT on one wave: lane r holds rank r's load
+  if (tid < kWave) {
+    const int lane = tid;
+    uint64_t load = lane < P ? 0ull : ~0ull >> 9;
+    for (int u = 0; u < U; ++u) {
+      const uint64_t rows = 0x7FFFFFFFull - (os.key[u] >> 32);
+      uint64_t v = (load << 8) | (uint64_t)lane;
+      for (int d = kWave / 2; d > 0; d >>= 1) {
+        const uint64_t o = (uint64_t)__shfl_xor((long long)v, d, kWave);
+        v = o < v ? o : v;
+      }
+      const int r = (int)(v & 0xffu);
+      if (lane == r) load += rows;
+      if (lane == 0) {
+        const int32_t id = os.unit[u];
+        if (id & kOwnJob)
+          a.own.job_owner[id & ~kOwnJob] = r;
+        else
+          a.own.node_owner[id] = r;
+      }
+    }
+    if (lane == me) a.own.state[3] = (int32_t)load;
+  }
+  __threadfence_block();
+  __syncthreads();
+  // this rank's position ranges: a node's children subtrees [pos + 1, pos + 2m - 1),
+  // a job's subtree [root, root + 2 rows - 1)
+  for (int u = tid; u < U; u += kPlanThreads) {
+    const int32_t id = os.unit[u];
+    int64_t lo, hi;
+    bool mine;
+    if (id & kOwnJob) {
+      const int64_t* J = a.jobs + (int64_t)(id & ~kOwnJob) * JW;
+      mine = a.own.job_owner[id & ~kOwnJob] == me;
+      lo = J[3];
+      hi = J[3] + 2 * J[1] - 1;
+    } else {
+      mine = a.own.node_owner[id] == me;
+      lo = a.cur.pos[id] + 1;
+      hi = a.cur.pos[id] + 2 * (int64_t)a.cur.gcnt[id] - 1;
+    }
+    if (mine) {
+      const int k = atomicAdd(&os.nr, 1);
+      a.own.ranges[(int64_t)k * 2 + 0] = lo;
+      a.own.ranges[(int64_t)k * 2 + 1] = hi;
+    }
+  }
+  __syncthreads();
+  const int NR = os.nr;
+  for (int k = NR + tid; k < a.own.cap; k += kPlanThreads) {
+    a.own.ranges[(int64_t)k * 2 + 0] = 0;
+    a.own.ranges[(int64_t)k * 2 + 1] = 0;
+  }
+  // keep this rank's jobs (stable, in place: each column is read by every row
+  // before any row of it is rewritten)
+  if (tid == 0) sh.carry[0] = 0;
+  __syncthreads();
+  for (int b0 = 0; b0 < J0; b0 += kPlanThreads) {
+    const int j = b0 + tid;
+    const bool keep = j < J0 && a.own.job_owner[j] == me;
+    int tot;
+    const int o = plan_scan_excl(keep ? 1 : 0, sh.w, tot) + sh.carry[0];
+    for (int k = 0; k < JW; ++k) {
+      const int64_t v = keep ? a.jobs[(int64_t)j * JW + k] : 0;
+      __syncthreads();
+      if (keep) a.jobs[(int64_t)o * JW + k] = v;
+      __syncthreads();
+    }
+    if (tid == 0) sh.carry[0] += tot;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    *a.job_count = sh.carry[0];
+    a.own.state[0] = 1;
+    a.own.state[1] = NR;
+    a.own.state[2] = U;
+  }
+  __threadfence_block();
+  __syncthreads();
+  return true;
+}
+
 __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
   __shared__ PlanShared sh;
   const int tid = threadIdx.x;
   const int C = a.C;
   const int JW = plan_job_width(a);
   const int K = a.cur.ctl[0];
+  // ---- pass 0 (subtree ownership, before the switch): maybe switch this level
+  __shared__ OwnShared own_sh;
+  bool own_sw = false;
+  if (a.own.P > 1 && !a.dp && a.own.state[0] == 0) own_sw = own_switch(a, own_sh, sh, K, JW);
+  // a node this rank grows: every node, except at the switch level the units
+  // other ranks own (nodes that are no unit -- leaves, splits into two leaves --
+  // stay replicated)
+  auto active = [&](int i) {
+    return !own_sw || a.own.node_owner[i] < 0 || a.own.node_owner[i] == a.own.rank;
+  };
   // ---- pass 1: totals (built / derived next-frontier children, split nodes)
   int nb_tot = 0;
   for (int b0 = 0; b0 < K; b0 += kPlanThreads) {
     const int i = b0 + tid;
     int nb = 0;
-    if (i < K) nb = plan_decide(a, i).built >= 0 ? 1 : 0;
+    if (i < K && active(i)) nb = plan_decide(a, i).built >= 0 ? 1 : 0;
     int t;
     plan_scan_excl(nb, sh.w, t);
     nb_tot += t;
@@ -306,9 +482,10 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     d.built = -1;
     d.fate[0] = d.fate[1] = 0;
     if (i < K) d = plan_decide(a, i);
-    const int nb = d.built >= 0 ? 1 : 0;
-    const int nd = (d.fate[0] == 2 && d.fate[1] == 2) ? 1 : 0;
-    const int ns = d.split ? 1 : 0;
+    const bool act = i < K && active(i);
+    const int nb = act && d.built >= 0 ? 1 : 0;
+    const int nd = act && (d.fate[0] == 2 && d.fate[1] == 2) ? 1 : 0;
+    const int ns = act && d.split ? 1 : 0;
     // built / derived offsets share one scan (each field <= kPlanThreads < 2^16)
     int tbd, ts;
     const int obd = plan_scan_excl(nb | (nd << 16), sh.w, tbd);
@@ -343,6 +520,9 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
         P[1] = d.bin;
         P[2] = (int32_t)cpos[0];
         P[3] = (int32_t)cpos[1];
+      }
+      if (d.split && act) {
+        const int64_t cpos[2] = {pos + 1, pos + 2 * d.nl};
         // partition list (this rank's rows of the node)
         int64_t* S = a.split + (int64_t)os * 4;
         S[0] = start;
@@ -474,6 +654,8 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     a.pctl[0] = NS;
     a.pctl[1] = n_pitems;
     if (a.host_ctl) {  // the host's lagged termination read, stored straight to host memory
+      __hip_atomic_store(a.host_ctl + 3, a.own.P > 1 ? a.own.state[0] : 0, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(a.host_ctl + 1, jobs_so_far, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(a.host_ctl, K2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __threadfence_system();

@@ -63,6 +63,15 @@ __all__ = ["DeviceGrower", "device_loop_supported"]
 _WORKSPACES: dict = {}  # (device, n, F, B, C, reg, fr) -> level-loop buffers
 _HOST_CTL: dict = {}  # device index -> (device pointer, numpy view [64, 16] int32)
 _FIT_SEQ = [0]  # per-process fit counter: tags host slots so stale values never match
+OWN_CAP = 2048  # ownership units sorted at the switch level (grow.hip kOwnMax)
+
+
+def own_min_units(P: int) -> int:
+    """Units (split nodes that keep growing + finisher jobs) the switch level
+    needs before the ranks take ownership: more units balance the LPT better,
+    each replicated level before the switch costs every rank a full level."""
+    k = int(os.environ.get("MPITREE_OWN_UNITS_PER_RANK", "4"))
+    return max(2, k * P)
 POLL_TIMEOUT_S = float(os.environ.get("MPITREE_POLL_TIMEOUT", "120"))
 
 
@@ -139,6 +148,8 @@ class DeviceGrower:
         arrs["job_count"] = np.array([jc], np.int64)
         arrs["idx"] = be.idx.cpu().numpy()
         arrs["tmp"] = be.tmp.cpu().numpy()
+        arrs["own_state"] = ws["own_state"].cpu().numpy()  # subtree ownership (per rank)
+        arrs["own_ranges"] = ws["own_ranges"].cpu().numpy()
         self.ckpt.save_device(lvl, arrs, rank, P)
 
     def _ckpt_restore(self, st, ws, sets, hists):
@@ -163,6 +174,9 @@ class DeviceGrower:
         ws["job_count"].fill_(jc)
         put(be.idx, st["idx"])
         put(be.tmp, st["tmp"])
+        if "own_state" in st:
+            put(ws["own_state"], st["own_state"])
+            put(ws["own_ranges"], st["own_ranges"])
         return lvl
 
     # ------------------------------------------------------------ buffers
@@ -190,33 +204,12 @@ class DeviceGrower:
         lap, off = k // P, k % P
         return torch.where(lap % 2 == 0, off, P - 1 - off)
 
-    def _run_jobs(self, d_jobs, n: int, counter=None):
-        """Finish the (largest-first) job list; with several ranks each takes its
-        serpentine share."""
+    def _run_jobs(self, d_jobs, n: int, counter=None, split: bool = True):
+        """Finish the (largest-first) job list; with several ranks and ``split``
+        each takes its serpentine share (subtree ownership: the list is this
+        rank's already)."""
         be, comm = self.be, self.comm
-        sim = int(os.environ.get("MPITREE_SIM_RANKS", "0"))
-        if comm is not None and comm.world_size > 1 and not getattr(comm, "simulated", False):
-            sim = 0  # (bench/sim_fp_ranks.py: a one-process stand-in for rank 0 keeps it)
-        if sim > 1:
-            # diagnostic (MPITREE_SIM_RANKS=P, one process): time rank 0's
-            # serpentine share alone on the GPU, then finish the rest so the
-            # tree stays complete -- the per-rank finisher critical path of a
-            # P-GPU fit, measured on one GPU
-            owner = self._owners(d_jobs.shape[0], sim, d_jobs.device)
-            mine, rest = d_jobs[owner == 0].contiguous(), d_jobs[owner != 0].contiguous()
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-            ev[0].record()
-            be.launch_finisher(mine, int(mine.shape[0]), n, self.p, be.pos_rec, be.pos_st)
-            ev[1].record()
-            keep = be._fin_keep
-            if rest.shape[0]:
-                be.launch_finisher(rest, int(rest.shape[0]), n, self.p, be.pos_rec, be.pos_st)
-            ev[2].record()
-            be._fin_keep = (keep, be._fin_keep)
-            self._sim_events = ev  # read after the assembly's sync
-            self.stats["sim_rank0_jobs"] = int(mine.shape[0])
-            return
-        if comm is not None and comm.world_size > 1:
+        if comm is not None and comm.world_size > 1 and split:
             owner = self._owners(d_jobs.shape[0], comm.world_size, d_jobs.device)
             d_jobs = d_jobs[owner == comm.rank]
             counter = None
@@ -318,6 +311,29 @@ class DeviceGrower:
         be.pos_rec.index_copy_(0, pos, allr[:, 1:7].to(torch.int32).contiguous())
         be.pos_st.index_copy_(0, pos, allr[:, 7:].to(be.pos_st.dtype).contiguous())
 
+    def _exchange_owned(self, ws):
+        """Subtree ownership: this rank wrote every position inside its owned
+        ranges (the switch level's LPT units) and nothing else differs between
+        ranks. Compact the live positions of those ranges ({pos, record[6],
+        counts[C]} rows), all-gather them and scatter into the local position
+        space; every position then has its one writer's record on every rank."""
+        be, comm = self.be, self.comm
+        rg = ws["own_ranges"]  # [cap, 2], unused rows {0, 0}
+        Pp = be.pos_rec.shape[0]
+        diff = torch.zeros(Pp + 1, dtype=torch.int32, device=rg.device)
+        ones = torch.ones(rg.shape[0], dtype=torch.int32, device=rg.device)
+        diff.index_add_(0, rg[:, 0], ones)
+        diff.index_add_(0, rg[:, 1].clamp(max=Pp), -ones)
+        inside = torch.cumsum(diff[:Pp], 0, dtype=torch.int32) > 0
+        live = torch.nonzero((be.pos_rec[:, 5] > 0) & inside).squeeze(1)
+        dt = torch.int64 if be.reg else torch.int32
+        rows = torch.cat([live.to(dt)[:, None], be.pos_rec[live].to(dt),
+                          be.pos_st[live].to(dt)], 1)
+        allr = comm.all_gather_rows(rows)
+        pos = allr[:, 0].long()
+        be.pos_rec.index_copy_(0, pos, allr[:, 1:7].to(torch.int32).contiguous())
+        be.pos_st.index_copy_(0, pos, allr[:, 7:].to(be.pos_st.dtype).contiguous())
+
     def _level_profile(self, marks):
         """Per-level device times (ms) from the HIP events (MPITREE_PROFILE=1)."""
         names = ("hist", "derive", "scan", "plan", "partition")
@@ -347,18 +363,21 @@ class DeviceGrower:
         return ws
 
     def _mode(self, F: int):
-        """(feature-parallel?, data-parallel?, f_lo, f_hi) of this rank."""
+        """(feature-parallel?, data-parallel?, subtree ownership?, f_lo, f_hi) of
+        this rank."""
         comm = self.comm
         P = getattr(comm, "world_size", 1)
         kind = getattr(comm, "kind", "local")
         if P <= 1:
-            return False, False, 0, F
+            return False, False, False, 0, F
         if kind == "data":
-            return False, True, 0, F
-        if kind in ("feature", "auto") and F >= P:
+            return False, True, False, 0, F
+        if kind == "feature" and F >= P:
             lo, hi = comm.feature_range(F)
-            return True, False, int(lo), int(hi)
-        return False, False, 0, F  # subtree: replicated levels, split finisher
+            return True, False, False, int(lo), int(hi)
+        # "subtree" / "auto": replicated levels, then each rank grows the units
+        # the switch level's LPT gives it
+        return False, False, True, 0, F
 
     def fit(self, n: int, n_classes: int, n_features: int, edges, y_exp: int = 0,
             root=None, d_edges=None) -> TreeArrays:
@@ -375,7 +394,7 @@ class DeviceGrower:
         fr = int(p.finisher_rows)
         md = -1 if p.max_depth is None else int(p.max_depth)
         mss, msl = int(p.min_samples_split), int(max(1, p.min_samples_leaf))
-        fp, dp, f_lo, f_hi = self._mode(F)
+        fp, dp, own, f_lo, f_hi = self._mode(F)
         F_h = f_hi - f_lo
         P = getattr(comm, "world_size", 1)
         s = hb._stream
@@ -443,9 +462,13 @@ class DeviceGrower:
                     fin_counter=torch.zeros(128, dtype=torch.int32, device=dev),
                     root=torch.empty(4 if reg else C, **i64),
                     root_host=torch.empty(4 if reg else C, dtype=torch.int64, pin_memory=True),
+                    own_state=torch.zeros(4, dtype=torch.int32, device=dev),
+                    own_ranges=torch.zeros((OWN_CAP if own else 1, 2), **i64),
+                    own_node=torch.empty(KMAX if own else 1, dtype=torch.int32, device=dev),
+                    own_job=torch.empty(JMAX if own else 1, dtype=torch.int32, device=dev),
                 )
 
-            ws = self._workspace((str(dev), n, n_loc, F, f_lo, F_h, B, C, reg, fr, dp), make)
+            ws = self._workspace((str(dev), n, n_loc, F, f_lo, F_h, B, C, reg, fr, dp, own), make)
             sets, hists, slab, rec = ws["sets"], ws["hists"], ws["slab"], ws["rec"]
             cost, bins, ident, split = ws["cost"], ws["bins"], ws["ident"], ws["split"]
             pitems, cursors, jobs, job_count = (ws["pitems"], ws["cursors"], ws["jobs"],
@@ -460,6 +483,7 @@ class DeviceGrower:
                 state = ck.load_device(rank, P, (lambda a: comm._all_gather(a)) if P > 1
                                        else None)
             first_lvl = 0  # levels before it ran in an earlier process (resume)
+            ws["own_state"].zero_()  # (subtree ownership: not switched yet)
             if state is not None:
                 first_lvl = self._ckpt_restore(state, ws, sets, hists) + 1
                 self.stats["resumed_from_level"] = first_lvl - 1
@@ -485,6 +509,14 @@ class DeviceGrower:
                     e.record()
                     marks[-1].append(e)
 
+            own_args = {}
+            if own:
+                own_args = dict(P=P, rank=rank, min_units=own_min_units(P), cap=OWN_CAP,
+                                state=ws["own_state"].data_ptr(),
+                                ranges=ws["own_ranges"].data_ptr(),
+                                node_owner=ws["own_node"].data_ptr(),
+                                job_owner=ws["own_job"].data_ptr())
+
             def plan(cur, nxt, lvl, fixup=False):
                 hip.grow_plan(s(), cur, nxt, rec.data_ptr(), split.data_ptr(), pitems.data_ptr(),
                               cursors.data_ptr(), cur["ctl"] + 4 * 5, be.pos_rec.data_ptr(),
@@ -492,7 +524,7 @@ class DeviceGrower:
                               be.pos_st.data_ptr() if reg else 0, int(reg), (lvl + 1) % 2,
                               jobs.data_ptr(), job_count.data_ptr(), C, md, hb.N_CU, mss, msl,
                               fr, 0 if fixup else hctl_dev + (lvl % 64) * 64,
-                              tag0 + (lvl % 4096) + 1, dp=int(dp), fixup=fixup)
+                              tag0 + (lvl % 4096) + 1, dp=int(dp), fixup=fixup, own=own_args)
 
             while True:
                 b0 = getattr(comm, "bytes_communicated", 0)
@@ -582,10 +614,15 @@ class DeviceGrower:
                 if lvl > 4096:
                     raise RuntimeError("device level loop did not terminate")
             levels = done_at + 1
-            J = int(hctl[done_at % 64, 1])  # finisher jobs appended
+            J = int(hctl[done_at % 64, 1])  # finisher jobs appended (own: this rank's)
+            switched = bool(own and hctl[done_at % 64, 3])
             if prof:
                 self._level_profile(marks[:levels])
-            if P > 1:  # positions the (replicated) level loop decided: on every rank already
+            if switched:  # this rank's units: every job is its own, ranges to exchange
+                self._owned = ws
+                self.stats["own_units"] = int(ws["own_state"][2])
+                self.stats["own_rows"] = int(ws["own_state"][3])
+            elif P > 1:  # positions the (replicated) level loop decided: on every rank already
                 self._pre_live = be.pos_rec[:, 5] > 0
             if J:
                 counter = None
@@ -602,24 +639,29 @@ class DeviceGrower:
                 if dp:
                     self._dp_finish(d_jobs, W)
                 else:
-                    self._run_jobs(d_jobs, n, counter)
+                    self._run_jobs(d_jobs, n, counter, split=not switched)
         elif jobs_host is not None:
             J = 1
             (d_jobs,) = be.up(jobs_host)
-            if P > 1:
+            if P > 1 and not own:
                 self._pre_live = be.pos_rec[:, 5] > 0
             if dp:
                 self._dp_finish(d_jobs.view(1, -1), W)
-            else:
-                self._run_jobs(d_jobs.view(1, -1), n)
+            else:  # (ownership: one job -- every rank grows it, nothing to exchange)
+                self._run_jobs(d_jobs.view(1, -1), n, split=not own)
         if comm is not None and P > 1:
             t1 = time.perf_counter()
             b0 = comm.bytes_communicated
-            self._exchange_nodes()
+            if getattr(self, "_owned", None) is not None:
+                self._exchange_owned(self._owned)
+            elif not (own and getattr(self, "_pre_live", None) is None):
+                self._exchange_nodes()
+            self._owned = None
             self.timings["exchange"] = time.perf_counter() - t1
             self.stats["comm_bytes_per_level"] = comm_bytes
             self.stats["comm_bytes_exchange"] = int(comm.bytes_communicated - b0)
-            self.stats["mode"] = "data" if dp else ("feature" if fp else "replicated")
+            self.stats["mode"] = ("data" if dp else "feature" if fp
+                                  else "subtree-owned" if own else "replicated")
             self.stats["feature_block"] = [f_lo, f_hi]
         self.timings["levels"] = time.perf_counter() - t0
         self.stats["levels"] = levels
@@ -634,11 +676,5 @@ class DeviceGrower:
         if self.ckpt is not None:
             self.stats["checkpoint_levels_saved"] = self.ckpt.saved_levels
             self.ckpt.clear()
-        ev = getattr(self, "_sim_events", None)
-        if ev is not None:
-            ev[2].synchronize()
-            self.stats["sim_rank0_finisher_ms"] = ev[0].elapsed_time(ev[1])
-            self.stats["sim_rest_finisher_ms"] = ev[1].elapsed_time(ev[2])
-            self._sim_events = None
         self._dp_keep = None
         return ta

@@ -140,24 +140,29 @@ def _fit_rank_gpu_large(rank, world, regression, strategy="auto"):
             outs[f"{k}{it}"] = getattr(ta, k)
         outs[f"engine{it}"] = np.array([est.fit_stats_["engine"]])
         outs[f"mode{it}"] = np.array([est.fit_stats_.get("mode", "")])
-        outs[f"bytes{it}"] = np.array(est.fit_stats_.get("comm_bytes_per_level", [0]))
+        outs[f"bytes{it}"] = np.array(est.fit_stats_.get("comm_bytes_per_level", [0]) or [0])
+        outs[f"xbytes{it}"] = np.array([est.fit_stats_.get("comm_bytes_exchange", 0)])
+        outs[f"own_rows{it}"] = np.array([est.fit_stats_.get("own_rows", -1)])
     return outs
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("regression", [False, True])
-@pytest.mark.parametrize("strategy", ["auto", "data", "subtree"])
-def test_gpu_ranks_equal_single_gpu_at_scale(regression, strategy):
-    """Thousands of finisher jobs (many with equal row counts) split over two
-    ranks; feature-parallel (auto), data-parallel and replicated levels: every
-    rank, every repeat, equals the single-GPU device-loop tree."""
+@pytest.mark.parametrize("strategy,world", [("auto", 2), ("auto", 4), ("feature", 2),
+                                            ("data", 2), ("subtree", 3)])
+def test_gpu_ranks_equal_single_gpu_at_scale(regression, strategy, world):
+    """Thousands of finisher jobs (many with equal row counts) over 2-4 ranks:
+    subtree ownership (auto / subtree: replicated levels until the LPT switch,
+    then each rank grows its own units), feature-parallel and data-parallel
+    levels -- every rank, every repeat, equals the single-GPU device-loop tree."""
     import torch
 
     from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
     from mpitree_amd.utils.datasets import make_classification, make_regression
 
-    outs = run_ranks(_fit_rank_gpu_large, 2, regression, strategy, start_method="spawn")
-    want = {"auto": "feature", "data": "data", "subtree": "replicated"}[strategy]
+    outs = run_ranks(_fit_rank_gpu_large, world, regression, strategy, start_method="spawn")
+    want = {"auto": "subtree-owned", "data": "data", "subtree": "subtree-owned",
+            "feature": "feature"}[strategy]
     dev = torch.device("cuda", 0)
     if regression:
         X, y = make_regression(200_000, 16, levels=64, seed=5, device=dev)
@@ -169,7 +174,10 @@ def test_gpu_ranks_equal_single_gpu_at_scale(regression, strategy):
         for it in range(2):
             assert str(o[f"engine{it}"][0]) == "hip-device-loop"
             assert str(o[f"mode{it}"][0]) == want
-            if want != "replicated":
+            if want == "subtree-owned":  # no per-level collective, one node exchange
+                assert o[f"bytes{it}"].sum() == 0 and o[f"xbytes{it}"][0] > 0
+                assert o[f"own_rows{it}"][0] > 0  # every rank owns units
+            else:
                 assert o[f"bytes{it}"].sum() > 0  # per-level collectives ran
             for k in FIELDS:
                 np.testing.assert_array_equal(o[f"{k}{it}"], getattr(ref, k), err_msg=k)
@@ -228,7 +236,7 @@ def test_rccl_ranks_equal_single_gpu(strategy, regression):
         X, y = make_classification(300_000, 16, seed=5, device=dev)
         ref = DecisionTreeClassifier(device="cuda").fit(X, y).tree_arrays_
     for o in outs:
-        assert str(o["mode"][0]) == ("data" if strategy == "data" else "feature")
+        assert str(o["mode"][0]) == ("data" if strategy == "data" else "subtree-owned")
         for k in FIELDS:
             np.testing.assert_array_equal(o[k], getattr(ref, k), err_msg=k)
 
