@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--units-per-rank", type=int, default=None)
+    ap.add_argument("--only-rank", type=int, default=None,
+                    help="simulate this rank only (profiling one rank's kernel sequence)")
     a = ap.parse_args()
     if a.units_per_rank is not None:
         os.environ["MPITREE_OWN_UNITS_PER_RANK"] = str(a.units_per_rank)
@@ -98,7 +100,7 @@ def main():
     ref, ref_rows = reference_rows(fit, dev)
     for P in [int(v) for v in a.ranks.split(",")]:
         per_rank = []
-        for r in range(P):
+        for r in range(P) if a.only_rank is None else [a.only_rank]:
             times, st = [], {}
             for i in range(a.reps + 2):
                 comm = SimOwnComm(P, r, dev, ref_rows) if P > 1 else None

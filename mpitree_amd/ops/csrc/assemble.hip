@@ -30,14 +30,21 @@ constexpr int kAsmTile = kAsmThreads * kAsmPer;    // positions per tile
 
 // rec: int32 [P][6] = {feature (-1 leaf), bin, left pos, right pos, depth, n}; n == 0
 // marks a position no node was written to.
+// mask (optional): only positions with mask[p] != 0 count (a rank's own ranges).
+__device__ __forceinline__ bool asm_live(const int32_t* __restrict__ rec,
+                                         const uint8_t* __restrict__ mask, int64_t p, int64_t P) {
+  return p < P && rec[p * 6 + 5] > 0 && (mask == nullptr || mask[p] != 0);
+}
+
 __global__ __launch_bounds__(kAsmThreads) void asm_count_kernel(const int32_t* __restrict__ rec,
                                                                 int64_t P,
-                                                                int32_t* __restrict__ tile_cnt) {
+                                                                int32_t* __restrict__ tile_cnt,
+                                                                const uint8_t* __restrict__ mask) {
   const int64_t base = (int64_t)blockIdx.x * kAsmTile;
   int c = 0;
   for (int k = 0; k < kAsmPer; ++k) {
     const int64_t p = base + (int64_t)k * kAsmThreads + threadIdx.x;  // coalesced
-    c += (p < P && rec[p * 6 + 5] > 0) ? 1 : 0;
+    c += asm_live(rec, mask, p, P) ? 1 : 0;
   }
   c = (int)wave_sum_u32((uint32_t)c);
   __shared__ int w[kAsmThreads / kWave];
@@ -87,7 +94,8 @@ __global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __
                                                                int64_t P,
                                                                const int32_t* __restrict__ tile_off,
                                                                int32_t* __restrict__ rank,
-                                                               int64_t* __restrict__ total) {
+                                                               int64_t* __restrict__ total,
+                                                               const uint8_t* __restrict__ mask) {
   constexpr int kW = kAsmThreads / kWave;
   __shared__ unsigned long long s_mask[kAsmPer][kW];
   __shared__ int s_ktot[kAsmPer];
@@ -99,7 +107,7 @@ __global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __
 #pragma unroll
   for (int k = 0; k < kAsmPer; ++k) {
     const int64_t p = base + (int64_t)k * kAsmThreads + threadIdx.x;
-    const bool v = p < P && rec[p * 6 + 5] > 0;
+    const bool v = asm_live(rec, mask, p, P);
     flags |= (uint32_t)v << k;
     if (v) dmax = max(dmax, rec[p * 6 + 4]);
     const unsigned long long b = __ballot(v);
@@ -253,14 +261,85 @@ __global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
 }
 
 void launch_asm_rank(hipStream_t stream, const int32_t* rec, int64_t P, int32_t* tile,
-                     int64_t* total, int32_t* rank) {
+                     int64_t* total, int32_t* rank, const uint8_t* mask) {
   const int n_tiles = (int)((P + kAsmTile - 1) / kAsmTile);
   if (n_tiles == 0) return;
-  hipLaunchKernelGGL(asm_count_kernel, dim3(n_tiles), dim3(kAsmThreads), 0, stream, rec, P, tile);
+  hipLaunchKernelGGL(asm_count_kernel, dim3(n_tiles), dim3(kAsmThreads), 0, stream, rec, P, tile,
+                     mask);
   hipLaunchKernelGGL(asm_offsets_kernel, dim3(1), dim3(kAsmThreads), 0, stream, tile, n_tiles,
                      total);
   hipLaunchKernelGGL(asm_rank_kernel, dim3(n_tiles), dim3(kAsmThreads), 0, stream, rec, P, tile,
-                     rank, total);
+                     rank, total, mask);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// Node exchange of a multi-GPU subtree-ownership fit (ops/device_grower.py):
+// rank r wrote exactly the positions inside its owned ranges; these kernels
+// mark those ranges, pack the live positions in them as rows {pos, record[6],
+// stats[C]} (final order from asm_rank with the mask) for one all-gather, and
+// scatter every rank's rows back into the position space.
+// ranges: int64 [cap][2] {lo, hi}, unused rows {0, 0}; mask: uint8 [P], zeroed.
+__global__ __launch_bounds__(256) void own_mark_kernel(const int64_t* __restrict__ ranges,
+                                                       uint8_t* __restrict__ mask) {
+  const int64_t lo = ranges[blockIdx.x * 2 + 0], hi = ranges[blockIdx.x * 2 + 1];
+  for (int64_t p = lo + threadIdx.x; p < hi; p += 256) mask[p] = 1;
+}
+
+template <typename StatT>
+__global__ __launch_bounds__(kAsmThreads) void own_pack_kernel(
+    const int32_t* __restrict__ rec, const StatT* __restrict__ st, int64_t P, int C,
+    const int32_t* __restrict__ rank, StatT* __restrict__ rows) {
+  const int64_t p = (int64_t)blockIdx.x * kAsmThreads + threadIdx.x;
+  if (p >= P) return;
+  const int j = rank[p];
+  if (j < 0) return;
+  StatT* o = rows + (int64_t)j * (7 + C);
+  o[0] = (StatT)p;
+  for (int k = 0; k < 6; ++k) o[1 + k] = (StatT)rec[p * 6 + k];
+  for (int c = 0; c < C; ++c) o[7 + c] = st[p * C + c];
+}
+
+template <typename StatT>
+__global__ __launch_bounds__(256) void own_scatter_kernel(const StatT* __restrict__ rows,
+                                                          int64_t k, int C,
+                                                          int32_t* __restrict__ rec,
+                                                          StatT* __restrict__ st) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= k) return;
+  const StatT* r = rows + i * (7 + C);
+  const int64_t p = (int64_t)r[0];
+  for (int q = 0; q < 6; ++q) rec[p * 6 + q] = (int32_t)r[1 + q];
+  for (int c = 0; c < C; ++c) st[p * C + c] = r[7 + c];
+}
+
+void launch_own_pack(hipStream_t stream, const int64_t* ranges, int cap, uint8_t* mask,
+                     const int32_t* rec, const void* st, bool st64, int64_t P, int C,
+                     int32_t* tile, int64_t* total, int32_t* rank, void* rows) {
+  if (cap > 0)
+    hipLaunchKernelGGL(own_mark_kernel, dim3(cap), dim3(256), 0, stream, ranges, mask);
+  launch_asm_rank(stream, rec, P, tile, total, rank, mask);
+  const int64_t blocks = (P + kAsmThreads - 1) / kAsmThreads;
+  if (blocks == 0) return;
+  if (st64)
+    hipLaunchKernelGGL(own_pack_kernel<int64_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
+                       stream, rec, (const int64_t*)st, P, C, rank, (int64_t*)rows);
+  else
+    hipLaunchKernelGGL(own_pack_kernel<int32_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
+                       stream, rec, (const int32_t*)st, P, C, rank, (int32_t*)rows);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_own_scatter(hipStream_t stream, const void* rows, int64_t k, int C, int32_t* rec,
+                        void* st, bool st64) {
+  if (k <= 0) return;
+  const unsigned blocks = (unsigned)((k + 255) / 256);
+  if (st64)
+    hipLaunchKernelGGL(own_scatter_kernel<int64_t>, dim3(blocks), dim3(256), 0, stream,
+                       (const int64_t*)rows, k, C, rec, (int64_t*)st);
+  else
+    hipLaunchKernelGGL(own_scatter_kernel<int32_t>, dim3(blocks), dim3(256), 0, stream,
+                       (const int32_t*)rows, k, C, rec, (int32_t*)st);
   MT_HIP_CHECK(hipGetLastError());
 }
 

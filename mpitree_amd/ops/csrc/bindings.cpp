@@ -87,7 +87,11 @@ void launch_hist_reduce_tasks(hipStream_t, const int64_t*, int, const int64_t*, 
 int edges_sample_rows(bool x64);
 void launch_edges(hipStream_t, const void*, bool, int64_t, int, int, int, void*, int32_t*,
                   uint8_t*, double*);
-void launch_asm_rank(hipStream_t, const int32_t*, int64_t, int32_t*, int64_t*, int32_t*);
+void launch_asm_rank(hipStream_t, const int32_t*, int64_t, int32_t*, int64_t*, int32_t*,
+                     const uint8_t*);
+void launch_own_pack(hipStream_t, const int64_t*, int, uint8_t*, const int32_t*, const void*,
+                     bool, int64_t, int, int32_t*, int64_t*, int32_t*, void*);
+void launch_own_scatter(hipStream_t, const void*, int64_t, int, int32_t*, void*, bool);
 int64_t asm_node_bytes(int C, bool reg);
 int small_fit_max_rows();
 void launch_small_fit(hipStream_t, const void*, int, int64_t, int, int, const int32_t*, int, int,
@@ -385,9 +389,21 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("limit"), py::arg("edges"), py::arg("nbins"), py::arg("exact"),
       py::arg("pack") = 0);
   m.def("asm_rank", [](uintptr_t s, uintptr_t rec, int64_t npos, uintptr_t tile, uintptr_t total,
-                       uintptr_t rank) {
+                       uintptr_t rank, uintptr_t mask) {
     mt::launch_asm_rank(S(s), P<int32_t>(rec), npos, P<int32_t>(tile), P<int64_t>(total),
-                        P<int32_t>(rank));
+                        P<int32_t>(rank), P<uint8_t>(mask));
+  }, py::arg("s"), py::arg("rec"), py::arg("npos"), py::arg("tile"), py::arg("total"),
+     py::arg("rank"), py::arg("mask") = 0);
+  m.def("own_pack", [](uintptr_t s, uintptr_t ranges, int cap, uintptr_t mask, uintptr_t rec,
+                       uintptr_t st, bool st64, int64_t npos, int C, uintptr_t tile,
+                       uintptr_t total, uintptr_t rank, uintptr_t rows) {
+    mt::launch_own_pack(S(s), P<int64_t>(ranges), cap, P<uint8_t>(mask), P<int32_t>(rec),
+                        P<void>(st), st64, npos, C, P<int32_t>(tile), P<int64_t>(total),
+                        P<int32_t>(rank), P<void>(rows));
+  });
+  m.def("own_scatter", [](uintptr_t s, uintptr_t rows, int64_t k, int C, uintptr_t rec,
+                          uintptr_t st, bool st64) {
+    mt::launch_own_scatter(S(s), P<void>(rows), k, C, P<int32_t>(rec), P<void>(st), st64);
   });
   m.def("asm_node_bytes", &mt::asm_node_bytes);
   m.def("asm_emit", [](uintptr_t s, uintptr_t rec, uintptr_t st, bool st64, int64_t npos, int C,

@@ -81,7 +81,8 @@ struct PlanArgs {
   int32_t* job_count;
   int C, max_depth, n_cu;
   int64_t mss, msl, fr;
-  int32_t* host_ctl;   // [4] host-mapped {next frontier size, jobs so far, tag, switched}
+  int32_t* host_ctl;   // [6] host-mapped {next frontier size, jobs so far, tag, switched,
+                       //  units at the switch, rows owned}
   int32_t host_tag;    // written last: the host polls it to know the slot is complete
   int dp;              // rows sharded across ranks: local segments fixed up after partition
   OwnArgs own;         // subtree ownership (own.P < 2: off)

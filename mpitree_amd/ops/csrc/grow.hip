@@ -654,8 +654,16 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     a.pctl[0] = NS;
     a.pctl[1] = n_pitems;
     if (a.host_ctl) {  // the host's lagged termination read, stored straight to host memory
-      __hip_atomic_store(a.host_ctl + 3, a.own.P > 1 ? a.own.state[0] : 0, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
+      if (a.own.P > 1) {  // {switched, units at the switch, rows owned}
+        __hip_atomic_store(a.host_ctl + 3, a.own.state[0], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.host_ctl + 4, a.own.state[2], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.host_ctl + 5, a.own.state[3], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        __hip_atomic_store(a.host_ctl + 3, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       __hip_atomic_store(a.host_ctl + 1, jobs_so_far, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(a.host_ctl, K2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __threadfence_system();

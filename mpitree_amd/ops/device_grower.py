@@ -314,25 +314,41 @@ class DeviceGrower:
     def _exchange_owned(self, ws):
         """Subtree ownership: this rank wrote every position inside its owned
         ranges (the switch level's LPT units) and nothing else differs between
-        ranks. Compact the live positions of those ranges ({pos, record[6],
-        counts[C]} rows), all-gather them and scatter into the local position
-        space; every position then has its one writer's record on every rank."""
-        be, comm = self.be, self.comm
-        rg = ws["own_ranges"]  # [cap, 2], unused rows {0, 0}
-        Pp = be.pos_rec.shape[0]
-        diff = torch.zeros(Pp + 1, dtype=torch.int32, device=rg.device)
-        ones = torch.ones(rg.shape[0], dtype=torch.int32, device=rg.device)
-        diff.index_add_(0, rg[:, 0], ones)
-        diff.index_add_(0, rg[:, 1].clamp(max=Pp), -ones)
-        inside = torch.cumsum(diff[:Pp], 0, dtype=torch.int32) > 0
-        live = torch.nonzero((be.pos_rec[:, 5] > 0) & inside).squeeze(1)
-        dt = torch.int64 if be.reg else torch.int32
-        rows = torch.cat([live.to(dt)[:, None], be.pos_rec[live].to(dt),
-                          be.pos_st[live].to(dt)], 1)
+        ranks. ``own_pack`` (assemble.hip) marks those ranges and packs their live
+        positions as {pos, record[6], stats[C]} rows; one all-gather; every
+        rank's rows are scattered back, so each position then holds its one
+        writer's record on every rank. Two small host waits: the packed row
+        count, and the all-gather's size exchange."""
+        be, comm, hip = self.be, self.comm, self.be.hip
+        s = hb._stream()
+        Pp = int(be.pos_rec.shape[0])
+        C, reg = be.C, bool(be.reg)
+        dt = torch.int64 if reg else torch.int32
+        esz = 8 if reg else 4
+        tiles = int(hip.asm_tiles(Pp))
+        bound = min(Pp, 2 * int(self.stats.get("own_rows", Pp)) + 16)  # nodes <= 2 rows
+        al = lambda x: (x + 255) // 256 * 256  # noqa: E731
+        o_tile, o_total = 0, al(max(tiles, 1) * 4)
+        o_rank = o_total + 256
+        o_mask = o_rank + al(Pp * 4)
+        o_rows = o_mask + al(Pp)
+        buf = hb._workspace(be.device, "own_exchange", o_rows + bound * (7 + C) * esz)
+        buf[o_mask : o_mask + Pp].zero_()
+        base = buf.data_ptr()
+        rg = ws["own_ranges"]
+        hip.own_pack(s, rg.data_ptr(), int(rg.shape[0]), base + o_mask, be.pos_rec.data_ptr(),
+                     be.pos_st.data_ptr(), reg, Pp, C, base + o_tile, base + o_total,
+                     base + o_rank, base + o_rows)
+        h_k = hb._pinned_copy(buf[o_total : o_total + 8].view(torch.int64), "own.k")
+        torch.cuda.current_stream(be.device).synchronize()
+        k = int(h_k[0])
+        if k > bound:
+            raise RuntimeError(f"subtree exchange: {k} nodes exceed the bound {bound}")
+        rows = buf[o_rows : o_rows + k * (7 + C) * esz].view(dt).view(k, 7 + C)
         allr = comm.all_gather_rows(rows)
-        pos = allr[:, 0].long()
-        be.pos_rec.index_copy_(0, pos, allr[:, 1:7].to(torch.int32).contiguous())
-        be.pos_st.index_copy_(0, pos, allr[:, 7:].to(be.pos_st.dtype).contiguous())
+        hip.own_scatter(s, allr.data_ptr(), int(allr.shape[0]), C, be.pos_rec.data_ptr(),
+                        be.pos_st.data_ptr(), reg)
+        self._keep_x = allr
 
     def _level_profile(self, marks):
         """Per-level device times (ms) from the HIP events (MPITREE_PROFILE=1)."""
@@ -620,8 +636,8 @@ class DeviceGrower:
                 self._level_profile(marks[:levels])
             if switched:  # this rank's units: every job is its own, ranges to exchange
                 self._owned = ws
-                self.stats["own_units"] = int(ws["own_state"][2])
-                self.stats["own_rows"] = int(ws["own_state"][3])
+                self.stats["own_units"] = int(hctl[done_at % 64, 4])
+                self.stats["own_rows"] = int(hctl[done_at % 64, 5])
             elif P > 1:  # positions the (replicated) level loop decided: on every rank already
                 self._pre_live = be.pos_rec[:, 5] > 0
             if J:
