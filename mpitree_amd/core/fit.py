@@ -194,9 +194,9 @@ def _finalize(ta: TreeArrays, mapper: BinMapper, regression: bool, y_exp: int) -
 
 def _fit_exact_gpu(Xd, yd, classes, C, crit, params, comm, timings, t_bin, t_start, F):
     """Classification with every unique value a threshold on continuous
-    features: level-wise growth over presorted per-feature lists
-    (``ops/exact_backend.py``). Multi-rank fits run it replicated on each rank
-    (every rank holds all rows and builds the same tree)."""
+    features beyond the device engine's reach (more than 16 classes with a
+    wide histogram): level-wise growth over presorted per-feature lists
+    (``ops/exact_backend.py``), run by every rank."""
     from ..ops.exact_backend import ExactHipBackend
 
     be = ExactHipBackend()
@@ -212,7 +212,7 @@ def _fit_exact_gpu(Xd, yd, classes, C, crit, params, comm, timings, t_bin, t_sta
         ta = builder.fit(Xd.shape[0], C, F, edges=dummy_edges)
     timings.update(builder.timings)
     stats = dict(builder.stats)
-    stats["thresholds"] = "exact (presorted lists)"
+    stats["thresholds"] = "exact (presorted lists, host-driven levels)"
     if comm.world_size > 1:
         stats["strategy"] = comm.kind
         stats["mode"] = "replicated-exact"
@@ -222,6 +222,50 @@ def _fit_exact_gpu(Xd, yd, classes, C, crit, params, comm, timings, t_bin, t_sta
     mapper = BinMapper(edges=[], exact=np.ones(F, bool), max_bins=None)
     return FitResult(arrays=ta, classes=classes, n_features=F, mapper=mapper, y_scale_exp=0,
                      engine="hip-exact", timings=timings, stats=stats)
+
+
+def _exact_device_ok(n, F, C, regression) -> bool:
+    """The device-driven exact engine (``ops/exact_grower.py``) runs when its
+    finisher takes the <= 256-row jobs on local codes."""
+    from ..ops import native
+    from ..ops.exact_grower import exact_supported
+
+    if os.environ.get("MPITREE_EXACT_V1") == "1" or not exact_supported(n, C, regression):
+        return False
+    if F > 256:
+        return False
+    if regression:
+        return True
+    return C <= 16 and native.hip().finish_lds_bytes(F, 256, C) <= 150 * 1024
+
+
+def _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t_bin, t_start, F, regression):
+    """Every unique value a threshold on continuous features, classification or
+    regression: the device-driven presorted-list engine; feature-parallel over
+    the ranks of a multi-GPU fit (``ops/exact_grower.py``)."""
+    from ..ops.exact_grower import ExactGrower
+
+    timings["bin"] = time.perf_counter() - t_bin
+    root = prep.root
+    yd = prep.y
+    if root is None:  # (host-encoded labels / targets): one small device reduction
+        if regression:
+            mn, mx = torch.aminmax(yd)
+            root = torch.stack([torch.tensor(yd.numel(), device=yd.device), yd.sum(), mn,
+                                mx]).cpu().numpy()
+        else:
+            root = torch.bincount(yd.long(), minlength=C).cpu().numpy()
+    g = ExactGrower(params, comm if comm.world_size > 1 else None)
+    with roctx_range("mpitree.grow"):
+        ta = g.fit(Xd, yd, root, C, crit, prep.y_exp, timings=timings)
+    stats = dict(g.stats)
+    stats["thresholds"] = "exact (presorted lists)"
+    if comm.world_size > 1:
+        stats["strategy"] = comm.kind
+    timings["total"] = time.perf_counter() - t_start
+    mapper = BinMapper(edges=[], exact=np.ones(F, bool), max_bins=None)
+    return FitResult(arrays=ta, classes=prep.classes, n_features=F, mapper=mapper,
+                     y_scale_exp=prep.y_exp, engine="hip-exact", timings=timings, stats=stats)
 
 
 def fit_tree(
@@ -287,6 +331,7 @@ def fit_tree(
         min_samples_leaf=int(min_samples_leaf),
     )
     timings = {}
+    quantile_fallback = False
     if dev == "cuda":
         from ..ops.gpu_prepare import prepare
         from ..ops.hip_backend import HipBackend
@@ -325,17 +370,23 @@ def fit_tree(
         from ..ops.exact_backend import exact_supported, needs_exact
 
         if max_bins is None and g_mapper is None and needs_exact(mapper):
-            if exact_supported(n, C, regression):
+            dev_ok = _exact_device_ok(n, F, C, regression)
+            if dev_ok or exact_supported(n, C, regression):
                 if checkpoint is not None:  # the same tree, just no mid-fit state
                     logger.warning("the exact-threshold GPU engine keeps no level "
                                    "checkpoint: fitting without one")
                 if prep.verify is not None and not prep.verify():
                     return fit_tree(X, y, **redo)
+                if dev_ok:
+                    return _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t0,
+                                             t_start, F, regression)
                 return _fit_exact_gpu(Xd, yd, classes, C, crit, params, comm, timings, t0,
                                       t_start, F)
             logger.warning("exact thresholds on > 256-value features are not available on "
-                           "the GPU for this fit (regression, >= 2^24 rows or > 256 "
-                           "classes): using 256 quantile bins per feature")
+                           "the GPU for this fit (>= 2^24 rows, > 256 features with a "
+                           "regression target, or > 256 classes): using 256 quantile bins "
+                           "per feature")
+            quantile_fallback = True
         lo, hi = comm.local_rows(n)
         if (lo, hi) != (0, n):  # data-parallel shard of a replicated input
             codes_rm = codes_rm[lo:hi].contiguous()
@@ -437,6 +488,8 @@ def fit_tree(
     if comm.world_size > 1:
         stats["strategy"] = comm.kind
         stats["bytes_communicated"] = getattr(comm, "bytes_communicated", 0)
+    if quantile_fallback:
+        stats["thresholds"] = "quantile-256 fallback (exact thresholds unavailable for this fit)"
     t0 = time.perf_counter()
     ta = _finalize(ta, mapper, regression, y_exp)
     timings["finalize"] = time.perf_counter() - t0

@@ -148,6 +148,8 @@ __global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __
 //   | counts i64 [N][C] (classification) or leaf value f64 [N] + fixed-point
 //     target sum i64 [N] (regression)
 //   | feature i32 [N] | threshold_bin i32 [N] | left i32 [N] | right i32 [N]
+// (thresholds: edges[feature][bin], or per position from thr_pos -- the exact
+// engine's split values)
 //   | depth i32 [N]
 // Impurities use the integer-form criterion of every builder (criterion.h:
 // (T(m) - sum_c T(c)) / m, gini (m^2 - sum c^2) / m / m), regression leaf values
@@ -207,7 +209,7 @@ __global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
     const int32_t* __restrict__ rec, const StatT* __restrict__ st, int64_t P, int C,
     const int32_t* __restrict__ rank, const double* __restrict__ edges, int EB,
     const int64_t* __restrict__ total, uint8_t* __restrict__ base, bool reg, int crit, int y_exp,
-    const double* __restrict__ xtab, int xtab_n) {
+    const double* __restrict__ xtab, int xtab_n, const double* __restrict__ thr_pos) {
   const int64_t p = (int64_t)blockIdx.x * kAsmThreads + threadIdx.x;
   if (p >= P) return;
   const int j = rank[p];
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
     o.bin[j] = b;
     o.left[j] = rank[R[2]];
     o.right[j] = rank[R[3]];
-    o.threshold[j] = edges[(int64_t)f * EB + b];
+    o.threshold[j] = thr_pos ? thr_pos[p] : edges[(int64_t)f * EB + b];
   } else {
     o.feature[j] = -1;
     o.bin[j] = -1;
@@ -350,17 +352,17 @@ int64_t asm_node_bytes(int C, bool reg) { return asm_bytes(1, C, reg); }
 void launch_asm_emit(hipStream_t stream, const int32_t* rec, const void* st, bool st64,
                      int64_t P, int C, const int32_t* rank, const double* edges, int EB,
                      const int64_t* total, uint8_t* base, bool reg, int crit, int y_exp,
-                     const double* xtab, int xtab_n) {
+                     const double* xtab, int xtab_n, const double* thr_pos) {
   const int64_t blocks = (P + kAsmThreads - 1) / kAsmThreads;
   if (blocks == 0) return;
   if (st64)
     hipLaunchKernelGGL(asm_emit_kernel<int64_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
                        stream, rec, (const int64_t*)st, P, C, rank, edges, EB, total, base, reg,
-                       crit, y_exp, xtab, xtab_n);
+                       crit, y_exp, xtab, xtab_n, thr_pos);
   else
     hipLaunchKernelGGL(asm_emit_kernel<int32_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
                        stream, rec, (const int32_t*)st, P, C, rank, edges, EB, total, base, reg,
-                       crit, y_exp, xtab, xtab_n);
+                       crit, y_exp, xtab, xtab_n, thr_pos);
   MT_HIP_CHECK(hipGetLastError());
 }
 

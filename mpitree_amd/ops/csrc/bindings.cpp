@@ -63,7 +63,8 @@ void ex_local_fix(hipStream_t, const uint64_t*, const uint64_t*, int64_t, const 
 int ex_local_max();
 size_t exact_setup_temp_bytes(int64_t, int);
 void exact_setup_sort(hipStream_t, const float*, int64_t, int, uint64_t*, uint64_t*, uint32_t*,
-                      uint32_t*, void*, size_t, int32_t*, int32_t*);
+                      uint32_t*, void*, size_t, int32_t*, int32_t*, int, int);
+void bind_exact2(pybind11::module_& m);
 void exact_setup_emit(hipStream_t, const uint64_t*, const uint32_t*, int64_t, int,
                       const int32_t*, const int32_t*, int, uint64_t*, double*);
 int exact_setup_chunk();
@@ -99,7 +100,7 @@ void launch_small_fit(hipStream_t, const void*, int, int64_t, int, int, const in
                       int64_t);
 void launch_asm_emit(hipStream_t, const int32_t*, const void*, bool, int64_t, int,
                      const int32_t*, const double*, int, const int64_t*, uint8_t*, bool, int, int,
-                     const double*, int);
+                     const double*, int, const double*);
 }  // namespace mt
 
 template <typename T>
@@ -317,11 +318,14 @@ PYBIND11_MODULE(_hip, m) {
   m.def("exact_setup_chunk", &mt::exact_setup_chunk);
   m.def("exact_setup_sort", [](uintptr_t s, uintptr_t X, int64_t n, int F, uintptr_t k0,
                                uintptr_t k1, uintptr_t r0, uintptr_t r1, uintptr_t temp,
-                               size_t temp_bytes, uintptr_t cnt, uintptr_t nuniq) {
+                               size_t temp_bytes, uintptr_t cnt, uintptr_t nuniq, int xs,
+                               int f_lo) {
     mt::exact_setup_sort(S(s), P<float>(X), n, F, P<uint64_t>(k0), P<uint64_t>(k1),
                          P<uint32_t>(r0), P<uint32_t>(r1), P<void>(temp), temp_bytes,
-                         P<int32_t>(cnt), P<int32_t>(nuniq));
-  });
+                         P<int32_t>(cnt), P<int32_t>(nuniq), xs, f_lo);
+  }, py::arg("s"), py::arg("X"), py::arg("n"), py::arg("F"), py::arg("k0"), py::arg("k1"),
+     py::arg("r0"), py::arg("r1"), py::arg("temp"), py::arg("temp_bytes"), py::arg("cnt"),
+     py::arg("nuniq"), py::arg("xs") = 0, py::arg("f_lo") = 0);
   m.def("exact_setup_emit", [](uintptr_t s, uintptr_t k1, uintptr_t r1, int64_t n, int F,
                                uintptr_t cnt, uintptr_t y, int B, uintptr_t E, uintptr_t uniq) {
     mt::exact_setup_emit(S(s), P<uint64_t>(k1), P<uint32_t>(r1), n, F, P<int32_t>(cnt),
@@ -408,11 +412,15 @@ PYBIND11_MODULE(_hip, m) {
   m.def("asm_node_bytes", &mt::asm_node_bytes);
   m.def("asm_emit", [](uintptr_t s, uintptr_t rec, uintptr_t st, bool st64, int64_t npos, int C,
                        uintptr_t rank, uintptr_t edges, int EB, uintptr_t total, uintptr_t base,
-                       bool reg, int crit, int y_exp, uintptr_t xtab, int xtab_n) {
+                       bool reg, int crit, int y_exp, uintptr_t xtab, int xtab_n,
+                       uintptr_t thr_pos) {
     mt::launch_asm_emit(S(s), P<int32_t>(rec), P<void>(st), st64, npos, C, P<int32_t>(rank),
                         P<double>(edges), EB, P<int64_t>(total), P<uint8_t>(base), reg, crit,
-                        y_exp, P<double>(xtab), xtab_n);
-  });
+                        y_exp, P<double>(xtab), xtab_n, P<double>(thr_pos));
+  }, py::arg("s"), py::arg("rec"), py::arg("st"), py::arg("st64"), py::arg("npos"), py::arg("C"),
+     py::arg("rank"), py::arg("edges"), py::arg("EB"), py::arg("total"), py::arg("base"),
+     py::arg("reg"), py::arg("crit"), py::arg("y_exp"), py::arg("xtab"), py::arg("xtab_n"),
+     py::arg("thr_pos") = 0);
   m.def("label_count", [](uintptr_t s, uintptr_t y, int64_t n, int64_t lo, int R,
                           uintptr_t counts, bool checked) {
     mt::launch_label_count(S(s), P<int64_t>(y), n, lo, R, P<uint32_t>(counts), checked);
@@ -422,6 +430,7 @@ PYBIND11_MODULE(_hip, m) {
                            uintptr_t out) {
     mt::launch_label_encode(S(s), P<int64_t>(y), n, lo, P<int64_t>(lut), P<int32_t>(out));
   });
+  mt::bind_exact2(m);
   m.def("xlog2x_device", [](uintptr_t s, uintptr_t out, int64_t n) {
     mt::launch_xlog2x(S(s), P<double>(out), n);
   });

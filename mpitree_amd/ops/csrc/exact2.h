@@ -1,0 +1,115 @@
+// Exact-threshold engine v2 (exact2.hip): device structures shared with the
+// host bindings (exact2_bind.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace mt {
+
+// Per-level lists (one set per level parity).
+// ctl: int32 {0: K frontier slots, 1: chunk items, 2: split nodes, 3: partition items,
+//             4: jobs so far (copy), 5-15: -}
+struct XeLists {
+  int64_t* pos;     // [KMAX] pre-order position
+  int64_t* start;   // [KMAX] segment start (every list)
+  int32_t* cnt;     // [KMAX] rows
+  int32_t* depth;   // [KMAX]
+  int64_t* stats;   // [KMAX][Cs] class counts, or {count, target sum}
+  int64_t* minmax;  // [KMAX][2] regression: target min / max (xe_carry)
+  int64_t* items;   // [IMAX][4] {slot, segment start, chunk start, chunk count}
+  int32_t* ifirst;  // [KMAX + 1] first item of each slot
+  int32_t* ctl;     // [16]
+};
+
+// Everything a level needs besides the two list sets.
+struct XeArgs {
+  const uint32_t* E;   // current list buffer [F_loc][n]
+  uint32_t* D;         // other list buffer
+  const int64_t* Y;    // regression payload [F_loc][n] (current), or null
+  int64_t* DY;         // regression payload (other), or null
+  const uint32_t* rank_of;  // [F_loc][n] value rank of each row
+  const void* X;       // features [n][F] (fp32 or fp64): threshold values
+  int x64;
+  int64_t n;
+  int F, f_lo, F_loc;
+  int C;               // classes (classification); 0 for regression
+  int crit;
+  int64_t msl;
+  const double* xtab;
+  int xtab_n;
+  // level scratch
+  int64_t* tot;        // [IMAX][F_loc][Cc] chunk totals (Cc = C, or 1 target sum)
+  int64_t* carry;      // [IMAX][F_loc][Cc]
+  int64_t* cmm;        // [IMAX][2] chunk target min / max (regression, local feature 0)
+  uint64_t* cbest;     // [IMAX][F_loc][2] chunk best {cost key, position}
+  int64_t* rec;        // [KMAX][R] split records, R = 6 + (C or 1) + 1
+  // partition
+  int64_t* split;      // [SMAX][4] {start, count, feature (global), n_left}
+  int64_t* pitems;     // [PMAX][4] {split j, segment start, chunk start, chunk count}
+  int32_t* pfirst;     // [SMAX + 1]
+  uint8_t* flag;       // [n]
+  int32_t* lc;         // [PMAX][F_loc]
+  int32_t* lcar;       // [PMAX][F_loc]
+  unsigned long long* bits;  // [PMAX][F_loc][kXePer * kXeWaves]
+};
+
+__host__ __device__ inline int xe_cc(int C) { return C > 0 ? C : 1; }
+// record: {gain bits, feature, position, n_left, m, threshold rank, threshold row, left[Cc]}
+__host__ __device__ inline int xe_rec_width(int C) { return 7 + xe_cc(C); }
+
+// Planner (one workgroup): the split records of the level -> position space,
+// finisher jobs, split list + partition items, the next frontier and its items.
+// job row: {segment start, rows, depth, root position, list buffer, stats[Cs]}
+struct XePlanArgs {
+  XeLists cur, nxt;
+  const int64_t* rec;
+  int64_t* split;      // [SMAX][4]
+  int64_t* pitems;     // [PMAX][4]
+  int32_t* pfirst;     // [SMAX + 1]
+  int32_t* pos_rec;    // [P][6]
+  void* pos_st;        // [P][Cs] int32 class counts / int64 {count, sum}
+  double* pos_thr;     // [P] threshold values
+  const void* X;
+  int x64;
+  int F;
+  int C;
+  int out_buf;         // list buffer this level's partition writes
+  int64_t* jobs;       // [JMAX][5 + Cs]
+  int32_t* job_count;
+  int max_depth;
+  int64_t mss, msl, fr;
+  int32_t* host_ctl;   // host-mapped {next frontier size, jobs so far, tag}
+  int32_t host_tag;
+};
+
+
+// launchers (exact2.hip)
+int xe_chunk();
+int xe_bits_words();
+int xe_local_max();
+int xe_max_classes();
+void xe_init(hipStream_t s, const XeLists& L, int64_t n, int Cs, const int64_t* root, int32_t* jc);
+void xe_level_scan(hipStream_t s, const XeArgs& a, const XeLists& cur, int items_bound,
+                   int slots_bound);
+void xe_plan(hipStream_t s, const XePlanArgs& p);
+void xe_flag(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_bound, int write_right);
+void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_bound,
+                  int splits_bound);
+void xe_local_codes(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const int64_t* Y0,
+                    const int64_t* Y1, const uint32_t* rank_of, int64_t n, int F_loc, int f_lo,
+                    const int64_t* jobs, int J, int JW, uint8_t* codes_fm, uint32_t* ent,
+                    int64_t* yv);
+void xe_codes_rm(hipStream_t s, const uint8_t* codes_fm, int64_t n, int F, int row_bytes,
+                 const int64_t* jobs, int J, int JW, uint8_t* codes_rm);
+void xe_fix(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const uint32_t* rank_of,
+            const void* X, int x64, int F, int64_t n, int f_lo, int F_loc, const int64_t* jobs,
+            int J, int JW, int32_t* pos_rec, double* pos_thr, uint8_t* resolved);
+void xe_resolved_pack(hipStream_t s, const int32_t* pos_rec, const double* pos_thr, int64_t P,
+                      const int32_t* rank, int64_t* rows);
+void xe_resolved_scatter(hipStream_t s, const int64_t* rows, int64_t k, int32_t* pos_rec,
+                         double* pos_thr);
+void xe_emit(hipStream_t s, const uint64_t* keys, const uint32_t* rows, int64_t n, int F_loc,
+             int nc, int chunk, const int32_t* cbase, const int32_t* ylab, const int64_t* yfix,
+             uint32_t* E, int64_t* Y, uint32_t* rank_of);
+
+}  // namespace mt

@@ -1,0 +1,1244 @@
+// Exact split search on presorted per-feature lists, driven from the device.
+//
+// The reference takes every unique value of a feature as a candidate
+// threshold (mpitree/tree/decision_tree.py:73-90). Histogram engines are exact
+// only while a feature has at most 256 values; with continuous data a feature
+// has up to n. This engine keeps, for each of this rank's features (a
+// contiguous block [f_lo, f_hi) -- the whole range on one GPU, F/P features
+// per rank when feature-parallel), the rows sorted by value and grouped by
+// frontier node, in 4-byte entries
+//
+//   E[f][p] = row | dup << 24 | label << 25          (rows < 2^24, labels < 128)
+//
+// (dup: the value occurs more than once in the column; the value rank then
+// comes from rank_of[f][row]) plus, for regression, the fixed-point target
+// Y[f][p] moved alongside. Node i owns positions [start_i, start_i + m_i) of
+// every list. A level is a fixed chain of launches whose work counts are read
+// from device memory, with a one-workgroup planner -- the host never waits:
+//
+//   xe_tot       per (chunk, feature): class-1 count / class counts / target sum
+//                (+ min / max of the targets for feature 0: regression purity)
+//   xe_carry     per (node, feature): exclusive prefix of the chunk totals
+//   xe_scan      per (chunk, feature): class prefix (or target prefix sum) at
+//                every position, the shared integer-form cost (criterion.h) at
+//                every value boundary, the chunk's best (cost, position)
+//   xe_select    per node: best feature (max gain, ties to the lowest feature),
+//                the split's left statistics, threshold row and value rank
+//   [feature-parallel: all-gather of the records + fp_combine_kernel]
+//   xe_plan      one workgroup: decisions -> position space, finisher jobs, split
+//                list, next frontier, the next level's chunk items
+//   xe_flag      rows of split nodes: left iff their position in the split
+//                feature's segment is < n_left (the feature's owner writes them;
+//                feature-parallel ranks sum the flags with one all-reduce)
+//   xe_pcount / xe_pcarry / xe_pscatter
+//                stable partition of every feature's split segments into the
+//                other list buffer (left rows first, both halves stay sorted)
+//
+// Every quantity is an integer or the shared fp64 criterion, so trees equal the
+// host builders' bit for bit. Segments of at most 256 rows leave as finisher
+// jobs (the histogram finishers on subtree-local 8-bit codes, xe_local_codes).
+#include <climits>
+
+#include "common.h"
+#include "criterion.h"
+#include "grow.h"
+#include "exact2.h"
+
+namespace mt {
+
+constexpr int kXeThreads = 256;
+constexpr int kXePer = 8;                       // entries per thread
+constexpr int kXeChunk = kXeThreads * kXePer;   // entries per chunk item
+constexpr int kXeWaves = kXeThreads / kWave;
+constexpr int kXeMaxC = 128;                    // labels live in 7 bits of an entry
+constexpr int kXePlanThreads = 512;
+constexpr int kXePlanWaves = kXePlanThreads / kWave;
+constexpr int kXeLocalMax = 256;                // finisher jobs: local codes fit a byte
+
+__device__ __forceinline__ uint32_t xe_row(uint32_t e) { return e & 0xFFFFFFu; }
+__device__ __forceinline__ bool xe_dup(uint32_t e) { return (e >> 24) & 1u; }
+__device__ __forceinline__ int xe_lab(uint32_t e) { return (int)(e >> 25); }
+
+__device__ __forceinline__ double xe_tl(int64_t x, const double* __restrict__ tab, int tn) {
+  return x < (int64_t)tn ? tab[x] : xlog2x((uint64_t)x);
+}
+
+// Monotone uint64 image of a double (total order of non-NaN values).
+__device__ __forceinline__ uint64_t xe_dkey(double d) {
+  const uint64_t b = (uint64_t)__double_as_longlong(d);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double xe_dval(uint64_t k) {
+  return __longlong_as_double((long long)((k >> 63) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k));
+}
+
+// ---------------------------------------------------------------------------
+// xe_tot: grid (items bound, F_loc); block (it, f) exits past the device count.
+__global__ __launch_bounds__(kXeThreads) void xe_tot_kernel(XeArgs a, XeLists L) {
+  __shared__ uint32_t s_c[kXeMaxC];
+  __shared__ int64_t s_w[kXeWaves][3];
+  const int64_t it = blockIdx.x;
+  if (it >= L.ctl[1]) return;
+  const int f = blockIdx.y;
+  const int64_t c0 = L.items[it * 4 + 2], cn = L.items[it * 4 + 3];
+  const uint32_t* E = a.E + (int64_t)f * a.n + c0;
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const int Cc = xe_cc(a.C);
+  int64_t* out = a.tot + (it * a.F_loc + f) * Cc;
+  if (a.C == 0) {  // regression: target sum (+ min / max on the first local feature)
+    const int64_t* Yp = a.Y + (int64_t)f * a.n + c0;
+    int64_t s = 0, mn = LLONG_MAX, mx = LLONG_MIN;
+    for (int64_t i = tid; i < cn; i += kXeThreads) {
+      const int64_t v = Yp[i];
+      s += v;
+      mn = v < mn ? v : mn;
+      mx = v > mx ? v : mx;
+    }
+    for (int d = kWave / 2; d > 0; d >>= 1) {
+      s += __shfl_xor(s, d, kWave);
+      const int64_t o1 = __shfl_xor(mn, d, kWave), o2 = __shfl_xor(mx, d, kWave);
+      mn = o1 < mn ? o1 : mn;
+      mx = o2 > mx ? o2 : mx;
+    }
+    if (lane == 0) {
+      s_w[w][0] = s;
+      s_w[w][1] = mn;
+      s_w[w][2] = mx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int64_t t = 0, a1 = LLONG_MAX, a2 = LLONG_MIN;
+      for (int q = 0; q < kXeWaves; ++q) {
+        t += s_w[q][0];
+        a1 = s_w[q][1] < a1 ? s_w[q][1] : a1;
+        a2 = s_w[q][2] > a2 ? s_w[q][2] : a2;
+      }
+      out[0] = t;
+      if (f == 0) {
+        a.cmm[it * 2 + 0] = a1;
+        a.cmm[it * 2 + 1] = a2;
+      }
+    }
+    return;
+  }
+  if (a.C <= 2) {  // class-1 entries by wave sums
+    uint32_t e[kXePer];
+#pragma unroll
+    for (int k = 0; k < kXePer; ++k) {
+      const int64_t i = (int64_t)k * kXeThreads + tid;
+      e[k] = i < cn ? E[i] : 0u;
+    }
+    uint32_t ones = 0;
+#pragma unroll
+    for (int k = 0; k < kXePer; ++k)
+      ones += ((int64_t)k * kXeThreads + tid < cn && xe_lab(e[k]) == 1) ? 1u : 0u;
+    ones = wave_sum_u32(ones);
+    if (lane == 0) s_w[w][0] = ones;
+    __syncthreads();
+    if (tid == 0) {
+      int64_t t = 0;
+      for (int q = 0; q < kXeWaves; ++q) t += s_w[q][0];
+      out[0] = cn - t;
+      if (a.C == 2) out[1] = t;
+    }
+    return;
+  }
+  for (int c = tid; c < a.C; c += kXeThreads) s_c[c] = 0;
+  __syncthreads();
+  for (int64_t i = tid; i < cn; i += kXeThreads) atomicAdd(&s_c[xe_lab(E[i])], 1u);
+  __syncthreads();
+  for (int c = tid; c < a.C; c += kXeThreads) out[c] = s_c[c];
+}
+
+// xe_carry: one thread per (slot, local feature, stat): exclusive prefix of the
+// chunk totals over the slot's items; regression slot min / max (f = 0, k = 0).
+__global__ __launch_bounds__(kXeThreads) void xe_carry_kernel(XeArgs a, XeLists L) {
+  const int K = L.ctl[0];
+  const int Cc = xe_cc(a.C);
+  const int64_t g = (int64_t)blockIdx.x * kXeThreads + threadIdx.x;
+  if (g >= (int64_t)K * a.F_loc * Cc) return;
+  const int k = (int)(g % Cc);
+  const int f = (int)((g / Cc) % a.F_loc);
+  const int64_t slot = g / ((int64_t)Cc * a.F_loc);
+  const int i0 = L.ifirst[slot], i1 = L.ifirst[slot + 1];
+  int64_t acc = 0;
+  for (int it = i0; it < i1; ++it) {
+    const int64_t o = ((int64_t)it * a.F_loc + f) * Cc + k;
+    a.carry[o] = acc;
+    acc += a.tot[o];
+  }
+  if (a.C == 0 && f == 0 && k == 0) {
+    int64_t mn = LLONG_MAX, mx = LLONG_MIN;
+    for (int it = i0; it < i1; ++it) {
+      mn = a.cmm[it * 2 + 0] < mn ? a.cmm[it * 2 + 0] : mn;
+      mx = a.cmm[it * 2 + 1] > mx ? a.cmm[it * 2 + 1] : mx;
+    }
+    L.minmax[slot * 2 + 0] = mn;
+    L.minmax[slot * 2 + 1] = mx;
+  }
+}
+
+// Value boundary between consecutive entries of a segment: equal values need
+// both entries flagged dup and equal ranks.
+__device__ __forceinline__ bool xe_boundary(uint32_t e, uint32_t nx, const uint32_t* __restrict__ rk) {
+  if (!xe_dup(e) || !xe_dup(nx)) return true;
+  return rk[xe_row(e)] != rk[xe_row(nx)];
+}
+
+// xe_scan: per (chunk, feature): the chunk's best {cost key, position}.
+// Classification keys are tie-rounded costs (criterion.h tie_round units) so
+// ties compare equal and the lowest position (smallest threshold) wins;
+// regression keys are the exact fp64 costs (the host builder's strict <).
+__global__ __launch_bounds__(kXeThreads) void xe_scan_kernel(XeArgs a, XeLists L) {
+  __shared__ uint32_t s_cnt[kXePer * kXeWaves];
+  __shared__ uint32_t s_first[kXePer * kXeWaves];
+  __shared__ int64_t s_sum[kXePer * kXeWaves];
+  __shared__ uint64_t s_min[kXeWaves][2];
+  __shared__ float s_fmin[kXeWaves];
+  __shared__ uint32_t s_e[kXeThreads * kXePer + 1];
+  const int64_t it = blockIdx.x;
+  if (it >= L.ctl[1]) return;
+  const int f = blockIdx.y;
+  const int64_t slot = L.items[it * 4 + 0], sstart = L.items[it * 4 + 1];
+  const int64_t c0 = L.items[it * 4 + 2], cn = L.items[it * 4 + 3];
+  const int64_t m = L.cnt[slot];
+  const uint32_t* Ef = a.E + (int64_t)f * a.n;
+  const uint32_t* rk = a.rank_of + (int64_t)f * a.n;
+  const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const int Cc = xe_cc(a.C);
+  // entry i = k * 256 + tid of the chunk (coalesced), staged in LDS so every
+  // thread sees its successor; the entry after the chunk (if the segment goes on)
+  uint32_t e[kXePer];
+#pragma unroll
+  for (int k = 0; k < kXePer; ++k) {
+    const int64_t i = (int64_t)k * kXeThreads + tid;
+    e[k] = i < cn ? Ef[c0 + i] : 0xFFFFFFFFu;
+    s_e[i] = e[k];
+  }
+  if (tid == 0) s_e[kXeChunk] = (c0 + cn - sstart) < m ? Ef[c0 + cn] : 0xFFFFFFFFu;
+  __syncthreads();
+  bool valid[kXePer];
+#pragma unroll
+  for (int k = 0; k < kXePer; ++k) {
+    const int64_t i = (int64_t)k * kXeThreads + tid;
+    const int64_t pos = c0 + i - sstart;
+    const int64_t ml = pos + 1, mr = m - ml;
+    bool v = i < cn && mr > 0 && ml >= a.msl && mr >= a.msl;
+    if (v) v = xe_boundary(e[k], s_e[i + 1], rk);
+    valid[k] = v;
+  }
+  unsigned long long mine = ~0ull;
+  uint64_t mine_pos = ~0ull;
+  if (a.C == 0) {
+    // ---- regression: prefix sums of the targets, exact fp64 costs
+    const int64_t* Yp = a.Y + (int64_t)f * a.n;
+    int64_t y[kXePer];
+#pragma unroll
+    for (int k = 0; k < kXePer; ++k) {
+      const int64_t i = (int64_t)k * kXeThreads + tid;
+      y[k] = i < cn ? Yp[c0 + i] : 0;
+    }
+    // (step, wave) sums -> exclusive scan over the 32 steps; lanes within a wave
+#pragma unroll
+    for (int k = 0; k < kXePer; ++k) {
+      const int64_t incl = wave_incl_scan_i64(y[k]);
+      if (lane == kWave - 1) s_sum[k * kXeWaves + wave] = incl;
+      y[k] = incl;  // inclusive within the wave
+    }
+    __syncthreads();
+    if (tid < kWave) {
+      const int64_t v = tid < kXePer * kXeWaves ? s_sum[tid] : 0;
+      const int64_t incl = wave_incl_scan_i64(v);
+      if (tid < kXePer * kXeWaves) s_sum[tid] = incl - v;
+    }
+    __syncthreads();
+    const int64_t base = a.carry[(it * a.F_loc + f) * Cc];
+    const int64_t S = L.stats[slot * 2 + 1];
+#pragma unroll
+    for (int k = 0; k < kXePer; ++k) {
+      if (!valid[k]) continue;
+      const int64_t i = (int64_t)k * kXeThreads + tid;
+      const int64_t pos = c0 + i - sstart;
+      const int64_t ml = pos + 1, mr = m - ml;
+      const int64_t sl = base + s_sum[k * kXeWaves + wave] + y[k];
+      const double cost = mse_term(ml, sl) + mse_term(mr, S - sl);
+      const uint64_t key = xe_dkey(cost);
+      if (key < mine || (key == mine && (uint64_t)pos < mine_pos)) {
+        mine = key;
+        mine_pos = (uint64_t)pos;
+      }
+    }
+  } else if (a.C <= 2) {
+    // ---- two classes: one ballot scan of class 1 gives every side count
+    unsigned long long bal[kXePer];
+#pragma unroll
+    for (int k = 0; k < kXePer; ++k) {
+      const int64_t i = (int64_t)k * kXeThreads + tid;
+      bal[k] = __ballot(i < cn && xe_lab(e[k]) == 1);
+      if (lane == 0) s_cnt[k * kXeWaves + wave] = (uint32_t)__popcll(bal[k]);
+    }
+    __syncthreads();
+    if (tid < kWave) {
+      const uint32_t v = tid < kXePer * kXeWaves ? s_cnt[tid] : 0u;
+      const uint32_t incl = wave_incl_scan_dpp(v);
+      if (tid < kXePer * kXeWaves) s_cnt[tid] = incl - v;
+    }
+    __syncthreads();
+    const int64_t base1 = a.C == 2 ? a.carry[(it * a.F_loc + f) * Cc + 1] : 0;
+    const int64_t t0 = L.stats[slot * Cc + 0], t1 = a.C == 2 ? L.stats[slot * Cc + 1] : 0;
+    int64_t l1[kXePer];
+#pragma unroll
+    for (int k = 0; k < kXePer; ++k)
+      l1[k] = base1 + s_cnt[k * kXeWaves + wave] + __popcll(bal[k] & lt) + ((bal[k] >> lane) & 1ull);
+    const double tm = xe_tl(m, a.xtab, a.xtab_n);
+    const double tu = tie_unit(tm, m);
+    const double tinv = 1.0 / tu;
+    auto exact_key = [&](int k) -> unsigned long long {
+      const int64_t pos = c0 + (int64_t)k * kXeThreads + tid - sstart;
+      const int64_t ml = pos + 1, mr = m - ml;
+      const int64_t L1 = l1[k], L0 = ml - L1, R1 = t1 - L1, R0 = t0 - L0;
+      double cost;
+      if (a.crit == kEntropy) {
+        const double sl = xe_tl(L0, a.xtab, a.xtab_n) + xe_tl(L1, a.xtab, a.xtab_n);
+        const double sr = xe_tl(R0, a.xtab, a.xtab_n) + xe_tl(R1, a.xtab, a.xtab_n);
+        cost = (xe_tl(ml, a.xtab, a.xtab_n) - sl) + (xe_tl(mr, a.xtab, a.xtab_n) - sr);
+      } else {
+        cost = gini_term(ml, L0 * L0 + L1 * L1) + gini_term(mr, R0 * R0 + R1 * R1);
+      }
+      double q = __builtin_rint(cost * tinv);
+      return (unsigned long long)(q < 0.0 ? 0.0 : q);
+    };
+    auto take = [&](int k) {
+      const unsigned long long key = exact_key(k);
+      const uint64_t pos = (uint64_t)(c0 + (int64_t)k * kXeThreads + tid - sstart);
+      if (key < mine || (key == mine && pos < mine_pos)) {
+        mine = key;
+        mine_pos = pos;
+      }
+    };
+    if (a.crit == kEntropy) {
+      // fp32 prefilter (hardware log2): |fp32 - exact| <= 2^-17.5 T(m) over the
+      // six terms and their sums; only positions within 2^-16 (T(m) + m) of the
+      // chunk's fp32 minimum are rescored exactly
+      float c32[kXePer];
+      float lmin = __builtin_inff();
+#pragma unroll
+      for (int k = 0; k < kXePer; ++k) {
+        const uint32_t ml = (uint32_t)(c0 + (int64_t)k * kXeThreads + tid - sstart + 1);
+        const uint32_t mr = (uint32_t)(m - ml);
+        const uint32_t L1 = (uint32_t)l1[k], L0 = ml - L1;
+        const uint32_t R1 = (uint32_t)t1 - L1, R0 = (uint32_t)t0 - L0;
+        auto t32 = [](uint32_t x) -> float {
+          const float xf = (float)x;
+          return x <= 1u ? 0.0f : xf * __log2f(xf);
+        };
+        const float c = (t32(ml) - (t32(L0) + t32(L1))) + (t32(mr) - (t32(R0) + t32(R1)));
+        c32[k] = valid[k] ? c : __builtin_inff();
+        lmin = fminf(lmin, c32[k]);
+      }
+      lmin = wave_min_f32_dpp(lmin);
+      if (lane == 0) s_fmin[wave] = lmin;
+      __syncthreads();
+      float bmin = s_fmin[0];
+#pragma unroll
+      for (int w = 1; w < kXeWaves; ++w) bmin = fminf(bmin, s_fmin[w]);
+      const float thr = bmin + (float)((tm + (double)m) * 0x1p-16);
+#pragma unroll
+      for (int k = 0; k < kXePer; ++k)
+        if (valid[k] && c32[k] <= thr) take(k);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kXePer; ++k)
+        if (valid[k]) take(k);
+    }
+  } else {
+    // ---- C > 2: per class, one block scan of the class indicator
+    const double tm = xe_tl(m, a.xtab, a.xtab_n);
+    const double tu = tie_unit(tm, m);
+    const double tinv = 1.0 / tu;
+    double sL[kXePer], sR[kXePer];
+    int64_t qL[kXePer], qR[kXePer];
+#pragma unroll
+    for (int k = 0; k < kXePer; ++k) {
+      sL[k] = sR[k] = 0.0;
+      qL[k] = qR[k] = 0;
+    }
+    for (int c = 0; c < a.C; ++c) {
+      unsigned long long bal[kXePer];
+#pragma unroll
+      for (int k = 0; k < kXePer; ++k) {
+        const int64_t i = (int64_t)k * kXeThreads + tid;
+        bal[k] = __ballot(i < cn && xe_lab(e[k]) == c);
+        if (lane == 0) s_cnt[k * kXeWaves + wave] = (uint32_t)__popcll(bal[k]);
+      }
+      __syncthreads();
+      if (tid < kWave) {
+        const uint32_t v = tid < kXePer * kXeWaves ? s_cnt[tid] : 0u;
+        const uint32_t incl = wave_incl_scan_dpp(v);
+        if (tid < kXePer * kXeWaves) s_cnt[tid] = incl - v;
+      }
+      __syncthreads();
+      const int64_t basec = a.carry[(it * a.F_loc + f) * Cc + c];
+      const int64_t tc = L.stats[slot * Cc + c];
+#pragma unroll
+      for (int k = 0; k < kXePer; ++k) {
+        const int64_t Lc = basec + s_cnt[k * kXeWaves + wave] + __popcll(bal[k] & lt) +
+                           ((bal[k] >> lane) & 1ull);
+        const int64_t Rc = tc - Lc;
+        if (a.crit == kEntropy) {
+          sL[k] = sL[k] + xe_tl(Lc, a.xtab, a.xtab_n);
+          sR[k] = sR[k] + xe_tl(Rc, a.xtab, a.xtab_n);
+        } else {
+          qL[k] += Lc * Lc;
+          qR[k] += Rc * Rc;
+        }
+      }
+      __syncthreads();  // s_cnt reuse
+    }
+#pragma unroll
+    for (int k = 0; k < kXePer; ++k) {
+      if (!valid[k]) continue;
+      const int64_t pos = c0 + (int64_t)k * kXeThreads + tid - sstart;
+      const int64_t ml = pos + 1, mr = m - ml;
+      double cost;
+      if (a.crit == kEntropy)
+        cost = (xe_tl(ml, a.xtab, a.xtab_n) - sL[k]) + (xe_tl(mr, a.xtab, a.xtab_n) - sR[k]);
+      else
+        cost = gini_term(ml, qL[k]) + gini_term(mr, qR[k]);
+      double q = __builtin_rint(cost * tinv);
+      const unsigned long long key = (unsigned long long)(q < 0.0 ? 0.0 : q);
+      if (key < mine || (key == mine && (uint64_t)pos < mine_pos)) {
+        mine = key;
+        mine_pos = (uint64_t)pos;
+      }
+    }
+  }
+  // block lexicographic min of {key, position}
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    const unsigned long long ok = __shfl_xor(mine, d, kWave);
+    const unsigned long long op = __shfl_xor(mine_pos, d, kWave);
+    if (ok < mine || (ok == mine && op < mine_pos)) {
+      mine = ok;
+      mine_pos = op;
+    }
+  }
+  if (lane == 0) {
+    s_min[wave][0] = mine;
+    s_min[wave][1] = mine_pos;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t bk = s_min[0][0], bp = s_min[0][1];
+    for (int w = 1; w < kXeWaves; ++w)
+      if (s_min[w][0] < bk || (s_min[w][0] == bk && s_min[w][1] < bp)) {
+        bk = s_min[w][0];
+        bp = s_min[w][1];
+      }
+    uint64_t* o = a.cbest + (it * a.F_loc + f) * 2;
+    o[0] = bk;
+    o[1] = bp;
+  }
+}
+
+// xe_select: per slot, the best split over this rank's features.
+// rec [K][R] = {gain bits, feature (global, -1 none), position, n_left, m,
+//               threshold value rank, threshold row, left[Cc]}
+__global__ __launch_bounds__(kXeThreads) void xe_select_kernel(XeArgs a, XeLists L) {
+  __shared__ double s_gain[kXeWaves];
+  __shared__ int s_feat[kXeWaves];
+  __shared__ int64_t s_pos[kXeWaves];
+  __shared__ double s_pterm;
+  __shared__ uint32_t s_c[kXeMaxC];
+  __shared__ int64_t s_sum[kXeWaves];
+  const int64_t slot = blockIdx.x;
+  if (slot >= L.ctl[0]) return;
+  const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
+  const int Cc = xe_cc(a.C);
+  const int R = xe_rec_width(a.C);
+  const int64_t start = L.start[slot], m = L.cnt[slot];
+  const int64_t* st = L.stats + slot * Cc;
+  int64_t* out = a.rec + slot * R;
+  if (tid == 0) {  // sequential over classes, matching every other engine
+    if (a.C == 0) {
+      s_pterm = mse_term(m, L.stats[slot * 2 + 1]);
+    } else {
+      double acc = 0.0;
+      int64_t sq = 0;
+      for (int c = 0; c < a.C; ++c) {
+        acc = acc + xlog2x((uint64_t)st[c]);
+        sq += st[c] * st[c];
+      }
+      s_pterm = a.crit == kEntropy ? xlog2x((uint64_t)m) - acc : gini_term(m, sq);
+    }
+  }
+  for (int c = tid; c < a.C; c += kXeThreads) s_c[c] = 0;
+  __syncthreads();
+  const double pterm = s_pterm;
+  const double tu = a.C ? tie_unit(xe_tl(m, a.xtab, a.xtab_n), m) : 0.0;
+  const int i0 = L.ifirst[slot], i1 = L.ifirst[slot + 1];
+  double g = -__builtin_inf();
+  int bf = 0x7fffffff;
+  int64_t bp = -1;
+  for (int f = tid; f < a.F_loc; f += kXeThreads) {
+    uint64_t bk = ~0ull, bpos = ~0ull;
+    for (int it = i0; it < i1; ++it) {  // chunks in order: positions ascend
+      const uint64_t* c = a.cbest + ((int64_t)it * a.F_loc + f) * 2;
+      if (c[0] < bk) {
+        bk = c[0];
+        bpos = c[1];
+      }
+    }
+    if (bk == ~0ull) continue;
+    const double cost = a.C ? (double)bk * tu : xe_dval(bk);
+    const double gf = pterm - cost;
+    if (gf > g) {  // features ascend per thread: strict > keeps the lowest
+      g = gf;
+      bf = a.f_lo + f;
+      bp = (int64_t)bpos;
+    }
+  }
+  // (gain desc, feature asc) over the block
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    const double og = __shfl_xor(g, d, kWave);
+    const int of = __shfl_xor(bf, d, kWave);
+    const int64_t op = __shfl_xor(bp, d, kWave);
+    if (og > g || (og == g && of < bf)) {
+      g = og;
+      bf = of;
+      bp = op;
+    }
+  }
+  if (lane == 0) {
+    s_gain[wave] = g;
+    s_feat[wave] = bf;
+    s_pos[wave] = bp;
+  }
+  __syncthreads();
+  g = s_gain[0];
+  bf = s_feat[0];
+  bp = s_pos[0];
+  for (int w = 1; w < kXeWaves; ++w)
+    if (s_gain[w] > g || (s_gain[w] == g && s_feat[w] < bf)) {
+      g = s_gain[w];
+      bf = s_feat[w];
+      bp = s_pos[w];
+    }
+  if (!(g > -__builtin_inf())) {
+    if (tid == 0) {
+      out[0] = (int64_t)double_to_bits(-__builtin_inf());
+      out[1] = -1;
+      out[2] = -1;
+      out[3] = 0;
+      out[4] = m;
+      out[5] = -1;
+      out[6] = -1;
+    }
+    for (int c = tid; c < Cc; c += kXeThreads) out[7 + c] = 0;
+    return;
+  }
+  // left statistics: the carry of the chunk holding bp + the chunk's entries up to it
+  const int fl = bf - a.f_lo;
+  const uint32_t* Ef = a.E + (int64_t)fl * a.n;
+  const int64_t ci = i0 + bp / kXeChunk;
+  const int64_t cfirst = start + (bp / kXeChunk) * kXeChunk;
+  const int64_t* car = a.carry + (ci * a.F_loc + fl) * Cc;
+  if (a.C == 0) {
+    const int64_t* Yp = a.Y + (int64_t)fl * a.n;
+    int64_t s = 0;
+    for (int64_t p = cfirst + tid; p <= start + bp; p += kXeThreads) s += Yp[p];
+    s = wave_sum_i64(s);
+    if (lane == 0) s_sum[wave] = s;
+    __syncthreads();
+    if (tid == 0) {
+      int64_t t = car[0];
+      for (int w = 0; w < kXeWaves; ++w) t += s_sum[w];
+      out[7] = t;
+    }
+  } else {
+    for (int64_t p = cfirst + tid; p <= start + bp; p += kXeThreads)
+      atomicAdd(&s_c[xe_lab(Ef[p])], 1u);
+    __syncthreads();
+    for (int c = tid; c < a.C; c += kXeThreads) out[7 + c] = car[c] + (int64_t)s_c[c];
+  }
+  if (tid == 0) {
+    const uint32_t row = xe_row(Ef[start + bp]);
+    out[0] = (int64_t)double_to_bits(g);
+    out[1] = bf;
+    out[2] = bp;
+    out[3] = bp + 1;
+    out[4] = m;
+    out[5] = (int64_t)a.rank_of[(int64_t)fl * a.n + row];
+    out[6] = (int64_t)row;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Planner (one workgroup): see XePlanArgs in exact2.h.
+struct XePlanShared {
+  int w[kXePlanWaves];
+  int carry[4];
+};
+
+__device__ __forceinline__ int xe_scan_excl(int v, int* s_w, int& total) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int incl = (int)wave_incl_scan_u32((uint32_t)v);
+  if (lane == kWave - 1) s_w[w] = incl;
+  __syncthreads();
+  int off = 0, tot = 0;
+  for (int k = 0; k < kXePlanWaves; ++k) {
+    const int x = s_w[k];
+    off += k < w ? x : 0;
+    tot += x;
+  }
+  __syncthreads();
+  total = tot;
+  return off + incl - v;
+}
+
+__global__ __launch_bounds__(kXePlanThreads) void xe_plan_kernel(XePlanArgs a) {
+  __shared__ XePlanShared sh;
+  const int tid = threadIdx.x;
+  const int K = a.cur.ctl[0];
+  const int C = a.C, Cs = C > 0 ? C : 2;
+  const bool reg = C == 0;
+  const int R = xe_rec_width(C);
+  const int JW = 5 + Cs;
+  if (tid == 0) {
+    sh.carry[0] = 0;  // next frontier slots
+    sh.carry[1] = 0;  // split nodes
+    sh.carry[2] = 0;  // next chunk items
+    sh.carry[3] = 0;  // partition items
+  }
+  __syncthreads();
+  for (int b0 = 0; b0 < K; b0 += kXePlanThreads) {
+    const int i = b0 + tid;
+    bool split = false;
+    int fate[2] = {0, 0};
+    int64_t nl = 0, m = 0, cs[2][2] = {{0, 0}, {0, 0}};  // regression child {count, sum}
+    const int64_t* r = a.rec + (int64_t)(i < K ? i : 0) * R;
+    int depth = 0;
+    if (i < K) {
+      m = a.cur.cnt[i];
+      depth = a.cur.depth[i];
+      const double gain = __longlong_as_double((long long)r[0]);
+      split = gain > -__builtin_inf() && r[1] >= 0;
+      if (reg && a.cur.minmax[(int64_t)i * 2] == a.cur.minmax[(int64_t)i * 2 + 1]) split = false;
+      if (split) {
+        nl = r[3];
+        const int cd = depth + 1;
+        const bool depth_stop = a.max_depth >= 0 && cd >= a.max_depth;
+        for (int c = 0; c < 2; ++c) {
+          const int64_t cm = c == 0 ? nl : m - nl;
+          int nz = 2;
+          if (!reg) {
+            nz = 0;
+            for (int k = 0; k < C; ++k) {
+              const int64_t lc = r[7 + k];
+              const int64_t v = c == 0 ? lc : a.cur.stats[(int64_t)i * C + k] - lc;
+              nz += v > 0;
+            }
+          } else {
+            cs[c][0] = cm;
+            cs[c][1] = c == 0 ? r[7] : a.cur.stats[(int64_t)i * 2 + 1] - r[7];
+          }
+          const bool term = depth_stop || cm < a.mss || cm < 2 * a.msl || nz <= 1;
+          fate[c] = term ? 0 : ((a.fr > 0 && cm <= a.fr) ? 1 : 2);
+        }
+      }
+    }
+    const int nn = (fate[0] == 2) + (fate[1] == 2);
+    const int ns = split ? 1 : 0;
+    // next-level chunk items of this node's frontier children
+    int ni = 0;
+    for (int c = 0; c < 2; ++c)
+      if (fate[c] == 2) {
+        const int64_t cm = c == 0 ? nl : m - nl;
+        ni += (int)((cm + kXeChunk - 1) / kXeChunk);
+      }
+    const int np = split ? (int)((m + kXeChunk - 1) / kXeChunk) : 0;
+    int t_nn, t_ns, t_ni, t_np;
+    const int o_nn = xe_scan_excl(nn, sh.w, t_nn) + sh.carry[0];
+    const int o_ns = xe_scan_excl(ns, sh.w, t_ns) + sh.carry[1];
+    const int o_ni = xe_scan_excl(ni, sh.w, t_ni) + sh.carry[2];
+    const int o_np = xe_scan_excl(np, sh.w, t_np) + sh.carry[3];
+    if (i < K) {
+      const int64_t pos = a.cur.pos[i];
+      const int64_t start = a.cur.start[i];
+      int32_t* P = a.pos_rec + pos * 6;
+      if (reg) {
+        int64_t* ps = reinterpret_cast<int64_t*>(a.pos_st) + pos * 2;
+        ps[0] = a.cur.stats[(int64_t)i * 2 + 0];
+        ps[1] = a.cur.stats[(int64_t)i * 2 + 1];
+      } else {
+        int32_t* ps = reinterpret_cast<int32_t*>(a.pos_st) + pos * C;
+        for (int k = 0; k < C; ++k) ps[k] = (int32_t)a.cur.stats[(int64_t)i * C + k];
+      }
+      P[4] = depth;
+      P[5] = (int32_t)m;
+      if (!split) {
+        P[0] = P[1] = P[2] = P[3] = -1;
+      } else {
+        const int feat = (int)r[1];
+        const int64_t row = r[6];
+        const int64_t cpos[2] = {pos + 1, pos + 2 * nl};
+        P[0] = feat;
+        P[1] = (int32_t)r[5];  // threshold value rank
+        P[2] = (int32_t)cpos[0];
+        P[3] = (int32_t)cpos[1];
+        a.pos_thr[pos] = a.x64 ? reinterpret_cast<const double*>(a.X)[row * a.F + feat]
+                               : (double)reinterpret_cast<const float*>(a.X)[row * a.F + feat];
+        int64_t* S = a.split + (int64_t)o_ns * 4;
+        S[0] = start;
+        S[1] = m;
+        S[2] = feat;
+        S[3] = nl;
+        // partition items of this split node
+        for (int q = 0; q < np; ++q) {
+          int64_t* it = a.pitems + (int64_t)(o_np + q) * 4;
+          it[0] = o_ns;
+          it[1] = start;
+          it[2] = start + (int64_t)q * kXeChunk;
+          const int64_t rem = m - (int64_t)q * kXeChunk;
+          it[3] = rem < kXeChunk ? rem : kXeChunk;
+        }
+        a.pfirst[o_ns] = o_np;
+        const int cd = depth + 1;
+        int sl = o_nn, io = o_ni;
+        for (int c = 0; c < 2; ++c) {
+          const int64_t cm = c == 0 ? nl : m - nl;
+          const int64_t cst = c == 0 ? start : start + nl;
+          auto child_stat = [&](int k) -> int64_t {
+            if (reg) return cs[c][k];
+            const int64_t lc = r[7 + k];
+            return c == 0 ? lc : a.cur.stats[(int64_t)i * C + k] - lc;
+          };
+          if (fate[c] == 0) {
+            int32_t* Q = a.pos_rec + cpos[c] * 6;
+            Q[0] = Q[1] = Q[2] = Q[3] = -1;
+            Q[4] = cd;
+            Q[5] = (int32_t)cm;
+            if (reg) {
+              int64_t* ps = reinterpret_cast<int64_t*>(a.pos_st) + cpos[c] * 2;
+              ps[0] = child_stat(0);
+              ps[1] = child_stat(1);
+            } else {
+              int32_t* ps = reinterpret_cast<int32_t*>(a.pos_st) + cpos[c] * C;
+              for (int k = 0; k < C; ++k) ps[k] = (int32_t)child_stat(k);
+            }
+          } else if (fate[c] == 1) {
+            const int j = atomicAdd(a.job_count, 1);
+            int64_t* J = a.jobs + (int64_t)j * JW;
+            J[0] = cst;
+            J[1] = cm;
+            J[2] = cd;
+            J[3] = cpos[c];
+            J[4] = a.out_buf;
+            for (int k = 0; k < Cs; ++k) J[5 + k] = child_stat(k);
+          } else {
+            a.nxt.pos[sl] = cpos[c];
+            a.nxt.start[sl] = cst;
+            a.nxt.cnt[sl] = (int32_t)cm;
+            a.nxt.depth[sl] = cd;
+            for (int k = 0; k < Cs; ++k) a.nxt.stats[(int64_t)sl * Cs + k] = child_stat(k);
+            a.nxt.ifirst[sl] = io;
+            const int64_t nck = (cm + kXeChunk - 1) / kXeChunk;
+            for (int q = 0; q < nck; ++q) {
+              int64_t* it = a.nxt.items + (int64_t)(io + q) * 4;
+              it[0] = sl;
+              it[1] = cst;
+              it[2] = cst + (int64_t)q * kXeChunk;
+              const int64_t rem = cm - (int64_t)q * kXeChunk;
+              it[3] = rem < kXeChunk ? rem : kXeChunk;
+            }
+            io += (int)nck;
+            ++sl;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      sh.carry[0] += t_nn;
+      sh.carry[1] += t_ns;
+      sh.carry[2] += t_ni;
+      sh.carry[3] += t_np;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const int K2 = sh.carry[0], NS = sh.carry[1], NI = sh.carry[2], NP = sh.carry[3];
+    a.nxt.ifirst[K2] = NI;
+    a.pfirst[NS] = NP;
+    for (int q = 0; q < 16; ++q) a.nxt.ctl[q] = 0;
+    a.nxt.ctl[0] = K2;
+    a.nxt.ctl[1] = NI;
+    a.cur.ctl[2] = NS;
+    a.cur.ctl[3] = NP;
+    const int jobs_so_far = atomicAdd(a.job_count, 0);
+    a.nxt.ctl[4] = jobs_so_far;
+    if (a.host_ctl) {
+      __hip_atomic_store(a.host_ctl + 1, jobs_so_far, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(a.host_ctl, K2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+      __hip_atomic_store(a.host_ctl + 2, a.host_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Partition of the level's split segments.
+// xe_flag: grid (partition items bound); rows of split j in the split feature's
+// list: flag 1 for the first n_left positions. Only the feature's owner (f in
+// [f_lo, f_lo + F_loc)) writes; with zero_rest every entry of a split segment
+// gets a flag (one GPU: no clearing needed), else only the left rows get 1
+// (the flags were cleared and are summed over the ranks afterwards).
+__global__ __launch_bounds__(kXeThreads) void xe_flag_kernel(XeArgs a, XeLists cur, int write_right) {
+  const int64_t it = blockIdx.x;
+  if (it >= cur.ctl[3]) return;
+  const int64_t j = a.pitems[it * 4 + 0], s0 = a.pitems[it * 4 + 1];
+  const int64_t c0 = a.pitems[it * 4 + 2], cn = a.pitems[it * 4 + 3];
+  const int f = (int)a.split[j * 4 + 2] - a.f_lo;
+  if (f < 0 || f >= a.F_loc) return;
+  const int64_t nl = a.split[j * 4 + 3];
+  const uint32_t* Ef = a.E + (int64_t)f * a.n;
+  for (int64_t i = threadIdx.x; i < cn; i += kXeThreads) {
+    const int64_t p = c0 + i;
+    const bool left = (p - s0) < nl;
+    if (left || write_right) a.flag[xe_row(Ef[p])] = left ? 1 : 0;
+  }
+}
+
+// Left entries of every (chunk, feature): flags gathered once, kept as one
+// 64-bit ballot per (step, wave) for the scatter.
+__global__ __launch_bounds__(kXeThreads) void xe_pcount_kernel(XeArgs a, XeLists cur) {
+  __shared__ uint32_t s_w[kXeWaves];
+  const int64_t it = blockIdx.x;
+  if (it >= cur.ctl[3]) return;
+  const int f = blockIdx.y;
+  const int64_t c0 = a.pitems[it * 4 + 2], cn = a.pitems[it * 4 + 3];
+  const uint32_t* Ef = a.E + (int64_t)f * a.n + c0;
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  uint32_t e[kXePer];
+#pragma unroll
+  for (int k = 0; k < kXePer; ++k) {
+    const int64_t i = (int64_t)k * kXeThreads + threadIdx.x;
+    e[k] = i < cn ? Ef[i] : 0xFFFFFFFFu;
+  }
+  uint32_t v = 0;
+  unsigned long long* B = a.bits + (it * a.F_loc + f) * (int64_t)(kXePer * kXeWaves);
+#pragma unroll
+  for (int k = 0; k < kXePer; ++k) {
+    const int64_t i = (int64_t)k * kXeThreads + threadIdx.x;
+    const unsigned long long b = __ballot(i < cn && a.flag[xe_row(e[k])] != 0);
+    if (lane == 0) {
+      B[k * kXeWaves + w] = b;
+      v += (uint32_t)__popcll(b);
+    }
+  }
+  if (lane == 0) s_w[w] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t total = 0;
+    for (int q = 0; q < kXeWaves; ++q) total += s_w[q];
+    a.lc[it * a.F_loc + f] = (int32_t)total;
+  }
+}
+
+// One thread per (split, feature): exclusive prefix of the chunk left counts.
+__global__ __launch_bounds__(kXeThreads) void xe_pcarry_kernel(XeArgs a, XeLists cur) {
+  const int S = cur.ctl[2];
+  const int64_t g = (int64_t)blockIdx.x * kXeThreads + threadIdx.x;
+  if (g >= (int64_t)S * a.F_loc) return;
+  const int f = (int)(g % a.F_loc);
+  const int64_t j = g / a.F_loc;
+  const int p0 = a.pfirst[j], p1 = a.pfirst[j + 1];
+  int32_t acc = 0;
+  for (int it = p0; it < p1; ++it) {
+    a.lcar[(int64_t)it * a.F_loc + f] = acc;
+    acc += a.lc[(int64_t)it * a.F_loc + f];
+  }
+}
+
+__global__ __launch_bounds__(kXeThreads) void xe_pscatter_kernel(XeArgs a, XeLists cur) {
+  __shared__ uint32_t s_cnt[kXePer * kXeWaves];
+  const int64_t it = blockIdx.x;
+  if (it >= cur.ctl[3]) return;
+  const int f = blockIdx.y;
+  const int64_t j = a.pitems[it * 4 + 0], s0 = a.pitems[it * 4 + 1];
+  const int64_t c0 = a.pitems[it * 4 + 2], cn = a.pitems[it * 4 + 3];
+  const uint32_t* Ef = a.E + (int64_t)f * a.n;
+  uint32_t* O = a.D + (int64_t)f * a.n;
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  uint32_t e[kXePer];
+  int64_t y[kXePer];
+  const bool reg = a.C == 0;
+#pragma unroll
+  for (int k = 0; k < kXePer; ++k) {
+    const int64_t i = (int64_t)k * kXeThreads + threadIdx.x;
+    e[k] = i < cn ? Ef[c0 + i] : 0xFFFFFFFFu;
+    y[k] = (reg && i < cn) ? a.Y[(int64_t)f * a.n + c0 + i] : 0;
+  }
+  const unsigned long long* Bt = a.bits + (it * a.F_loc + f) * (int64_t)(kXePer * kXeWaves);
+  unsigned long long bal[kXePer];
+#pragma unroll
+  for (int k = 0; k < kXePer; ++k) {
+    bal[k] = Bt[k * kXeWaves + w];
+    if (lane == 0) s_cnt[k * kXeWaves + w] = (uint32_t)__popcll(bal[k]);
+  }
+  __syncthreads();
+  if (threadIdx.x < kWave) {
+    const uint32_t v = threadIdx.x < kXePer * kXeWaves ? s_cnt[threadIdx.x] : 0u;
+    const uint32_t incl = wave_incl_scan_dpp(v);
+    if (threadIdx.x < kXePer * kXeWaves) s_cnt[threadIdx.x] = incl - v;
+  }
+  __syncthreads();
+  const int64_t lb = (int64_t)a.lcar[it * a.F_loc + f];
+  const int64_t nlj = a.split[j * 4 + 3];
+#pragma unroll
+  for (int k = 0; k < kXePer; ++k) {
+    const int64_t i = (int64_t)k * kXeThreads + threadIdx.x;
+    if (i >= cn) break;
+    const int64_t l = lb + s_cnt[k * kXeWaves + w] + __popcll(bal[k] & lt);
+    const int64_t dst = ((bal[k] >> lane) & 1ull) ? s0 + l : s0 + nlj + (c0 + i - s0) - l;
+    O[dst] = e[k];
+    if (reg) a.DY[(int64_t)f * a.n + dst] = y[k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Root lists (level 0): one slot over all n rows.
+__global__ void xe_init_kernel(XeLists L, int64_t n, int Cs, const int64_t* __restrict__ root,
+                               int32_t* __restrict__ job_count) {
+  const int64_t k = (n + kXeChunk - 1) / kXeChunk;
+  for (int64_t q = threadIdx.x; q < k; q += blockDim.x) {
+    int64_t* it = L.items + q * 4;
+    it[0] = 0;
+    it[1] = 0;
+    it[2] = q * kXeChunk;
+    const int64_t rem = n - q * kXeChunk;
+    it[3] = rem < kXeChunk ? rem : kXeChunk;
+  }
+  if (threadIdx.x == 0) {
+    *job_count = 0;
+    L.pos[0] = 0;
+    L.start[0] = 0;
+    L.cnt[0] = (int32_t)n;
+    L.depth[0] = 0;
+    for (int c = 0; c < Cs; ++c) L.stats[c] = root[c];
+    L.ifirst[0] = 0;
+    L.ifirst[1] = (int32_t)k;
+    for (int q = 0; q < 16; ++q) L.ctl[q] = 0;
+    L.ctl[0] = 1;
+    L.ctl[1] = (int32_t)k;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Finisher jobs (segments of <= 256 rows) on subtree-local 8-bit codes: a row's
+// code in feature f is the offset of the first entry of its value in the
+// segment of f's list, so the finisher's "code <= b" is the split "x <= value
+// at offset b" with the list engine's candidates, costs and ties. Virtual rows
+// of segment [s, s + m): s + (the row's order among the segment's row ids) --
+// the same on every rank whatever its feature block. Outputs for this rank's
+// features: codes_fm[f_lo + f][v]; the label-packed entries ent[v] (classes)
+// (classification) or the row ids ent[v] = v and targets yv[v] (regression).
+// jobs: int64 [J][W] = {start, rows, depth, position, list buffer, ...}
+__global__ __launch_bounds__(kXeLocalMax) void xe_local_codes_kernel(
+    const uint32_t* __restrict__ E0, const uint32_t* __restrict__ E1,
+    const int64_t* __restrict__ Y0, const int64_t* __restrict__ Y1,
+    const uint32_t* __restrict__ rank_of, int64_t n, int F_loc, int f_lo,
+    const int64_t* __restrict__ jobs, int JW, uint8_t* __restrict__ codes_fm,
+    uint32_t* __restrict__ ent, int64_t* __restrict__ yv) {
+  __shared__ uint32_t s_row[kXeLocalMax];
+  __shared__ uint32_t s_w[kXeLocalMax / kWave];
+  __shared__ uint32_t s_e[kXeLocalMax + 1];
+  const int64_t* J = jobs + (int64_t)blockIdx.x * JW;
+  const int64_t s = J[0];
+  const int m = (int)J[1];
+  const bool b1 = J[4] != 0;
+  const uint32_t* E = b1 ? E1 : E0;
+  const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
+  // virtual row order: rank of the row id among the segment's rows (bitonic sort)
+  const uint32_t e0 = t < m ? E[s + t] : 0xFFFFFFFFu;
+  s_row[t] = t < m ? xe_row(e0) : 0xFFFFFFFFu;
+  __syncthreads();
+  for (int size = 2; size <= kXeLocalMax; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const int j = t ^ stride;
+      if (j > t) {
+        const uint32_t x = s_row[t], y = s_row[j];
+        const bool up = (t & size) == 0;
+        if ((x > y) == up) {
+          s_row[t] = y;
+          s_row[j] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // virtual index of a row: binary search in s_row[0, m)
+  auto vidx = [&](uint32_t row) -> int {
+    int lo = 0, hi = m;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (s_row[mid] <= row) lo = mid; else hi = mid;
+    }
+    return lo;
+  };
+  if (t < m) {  // labels / targets by virtual row (from the first local list)
+    const int v = vidx(xe_row(e0));
+    if (yv) {  // regression: plain virtual row ids + the targets
+      ent[s + v] = (uint32_t)(s + v);
+      yv[s + v] = (b1 ? Y1 : Y0)[s + t];
+    } else {
+      ent[s + v] = ((uint32_t)xe_lab(e0) << 24) | (uint32_t)(s + v);
+    }
+  }
+  for (int f = 0; f < F_loc; ++f) {
+    const uint32_t e = t < m ? E[(int64_t)f * n + s + t] : 0xFFFFFFFFu;
+    s_e[t] = e;
+    __syncthreads();
+    // offset of the first entry of this value: inclusive max-scan of run starts
+    bool start = t == 0;
+    if (t > 0 && t < m) {
+      const uint32_t pe = s_e[t - 1];
+      start = !(xe_dup(e) && xe_dup(pe)) ||
+              rank_of[(int64_t)f * n + xe_row(e)] != rank_of[(int64_t)f * n + xe_row(pe)];
+    }
+    uint32_t b = (t < m && start) ? (uint32_t)t : 0u;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint32_t o = __shfl_up(b, d, kWave);
+      if (lane >= d) b = max(b, o);
+    }
+    if (lane == kWave - 1) s_w[w] = b;
+    __syncthreads();
+    for (int k = 0; k < w; ++k) b = max(b, s_w[k]);
+    if (t < m) codes_fm[(int64_t)(f_lo + f) * n + s + vidx(xe_row(e))] = (uint8_t)b;
+    __syncthreads();
+  }
+}
+
+// Row-major copy of the finisher codes: codes_rm[v][f] for every virtual row of
+// every job (the finisher reads both layouts).
+__global__ __launch_bounds__(256) void xe_codes_rm_kernel(const uint8_t* __restrict__ codes_fm,
+                                                          int64_t n, int F, int row_bytes,
+                                                          const int64_t* __restrict__ jobs,
+                                                          int JW, uint8_t* __restrict__ codes_rm) {
+  const int64_t* J = jobs + (int64_t)blockIdx.x * JW;
+  const int64_t s = J[0];
+  const int m = (int)J[1];
+  for (int e = threadIdx.x; e < m * row_bytes; e += 256) {
+    const int v = e / row_bytes, f = e - v * row_bytes;
+    codes_rm[(s + v) * row_bytes + f] = f < F ? codes_fm[(int64_t)f * n + s + v] : (uint8_t)0;
+  }
+}
+
+// Finished job j owns positions [pos, pos + 2m - 1) of the position space; its
+// split nodes hold {feature, local code}. For this rank's features: code ->
+// the threshold row (the first entry of the value at that offset of the
+// feature's segment) -> value rank and threshold value. The feature-parallel
+// exchange packs what this rank resolved (resolved[p] = 1).
+__global__ __launch_bounds__(256) void xe_fix_kernel(
+    const uint32_t* __restrict__ E0, const uint32_t* __restrict__ E1,
+    const uint32_t* __restrict__ rank_of, const void* __restrict__ X, int x64, int F, int64_t n,
+    int f_lo, int F_loc, const int64_t* __restrict__ jobs, int JW, int32_t* __restrict__ pos_rec,
+    double* __restrict__ pos_thr, uint8_t* __restrict__ resolved) {
+  const int64_t* J = jobs + (int64_t)blockIdx.x * JW;
+  const int64_t s = J[0], m = J[1], pos = J[3];
+  const uint32_t* E = J[4] ? E1 : E0;
+  for (int64_t p = pos + threadIdx.x; p < pos + 2 * m - 1; p += blockDim.x) {
+    int32_t* R = pos_rec + p * 6;
+    if (R[5] <= 0 || R[0] < 0) continue;
+    const int f = R[0] - f_lo;
+    if (f < 0 || f >= F_loc) continue;
+    const uint32_t row = xe_row(E[(int64_t)f * n + s + R[1]]);
+    R[1] = (int32_t)rank_of[(int64_t)f * n + row];
+    pos_thr[p] = x64 ? reinterpret_cast<const double*>(X)[(int64_t)row * F + R[0]]
+                     : (double)reinterpret_cast<const float*>(X)[(int64_t)row * F + R[0]];
+    if (resolved) resolved[p] = 1;
+  }
+}
+
+// Pack / scatter {position, bin, threshold bits} of the positions a rank resolved
+// (feature-parallel finisher nodes), in position order via asm_rank (mask).
+__global__ __launch_bounds__(256) void xe_resolved_pack_kernel(const int32_t* __restrict__ pos_rec,
+                                                               const double* __restrict__ pos_thr,
+                                                               int64_t P, const int32_t* __restrict__ rank,
+                                                               int64_t* __restrict__ rows) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  const int j = rank[p];
+  if (j < 0) return;
+  rows[(int64_t)j * 3 + 0] = p;
+  rows[(int64_t)j * 3 + 1] = pos_rec[p * 6 + 1];
+  rows[(int64_t)j * 3 + 2] = (int64_t)__double_as_longlong(pos_thr[p]);
+}
+
+__global__ __launch_bounds__(256) void xe_resolved_scatter_kernel(const int64_t* __restrict__ rows,
+                                                                  int64_t k, int32_t* __restrict__ pos_rec,
+                                                                  double* __restrict__ pos_thr) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= k) return;
+  const int64_t p = rows[i * 3 + 0];
+  pos_rec[p * 6 + 1] = (int32_t)rows[i * 3 + 1];
+  pos_thr[p] = __longlong_as_double((long long)rows[i * 3 + 2]);
+}
+
+// ---------------------------------------------------------------------------
+// Setup: sorted keys {feature : 32 | value bits : 32} with row ids (exact_setup.hip
+// sort) -> entries, value ranks per row, duplicate flags. cbase: per-(feature,
+// chunk) first rank (exact_setup's count / scan of value changes).
+__global__ __launch_bounds__(256) void xe_emit_kernel(const uint64_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ rows, int64_t n,
+                                                      int nc, int chunk,
+                                                      const int32_t* __restrict__ cbase,
+                                                      const int32_t* __restrict__ ylab,
+                                                      const int64_t* __restrict__ yfix,
+                                                      uint32_t* __restrict__ E,
+                                                      int64_t* __restrict__ Y,
+                                                      uint32_t* __restrict__ rank_of) {
+  const int f = blockIdx.y, c = blockIdx.x;
+  const int64_t base = (int64_t)f * n;
+  const int64_t p0 = (int64_t)c * chunk;
+  const int64_t p1 = min<int64_t>(p0 + chunk, n);
+  __shared__ int32_t s_w[256 / kWave];
+  __shared__ int32_t s_carry;
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_carry = cbase[(int64_t)f * nc + c];
+  __syncthreads();
+  for (int64_t b = p0; b < p1; b += 256) {
+    const int64_t p = b + threadIdx.x;
+    const bool in = p < p1;
+    const uint64_t key = in ? keys[base + p] : 0ull;
+    const bool nw = in && (p == 0 || keys[base + p - 1] != key);
+    const bool dn = in && p + 1 < n && keys[base + p + 1] == key;
+    const bool dup = in && (!nw || dn);
+    const uint32_t incl = wave_incl_scan_dpp(nw ? 1u : 0u);
+    if (lane == kWave - 1) s_w[w] = (int32_t)incl;
+    __syncthreads();
+    int32_t off = s_carry;
+    for (int k = 0; k < w; ++k) off += s_w[k];
+    const int32_t rank = off + (int32_t)incl - 1;
+    if (in) {
+      const uint32_t row = rows[base + p];
+      const uint32_t lab = ylab ? (uint32_t)ylab[row] : 0u;
+      E[base + p] = row | ((uint32_t)dup << 24) | (lab << 25);
+      if (Y) Y[base + p] = yfix[row];
+      rank_of[base + row] = (uint32_t)rank;
+    }
+    __syncthreads();
+    if (threadIdx.x == 255) s_carry = off + (int32_t)incl;
+    __syncthreads();
+  }
+}
+
+// --------------------------------------------------------------- launchers
+int xe_chunk() { return kXeChunk; }
+int xe_bits_words() { return kXePer * kXeWaves; }
+int xe_local_max() { return kXeLocalMax; }
+int xe_max_classes() { return kXeMaxC; }
+
+void xe_init(hipStream_t s, const XeLists& L, int64_t n, int Cs, const int64_t* root, int32_t* jc) {
+  hipLaunchKernelGGL(xe_init_kernel, dim3(1), dim3(256), 0, s, L, n, Cs, root, jc);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+// the scan / select half of a level (grids are host bounds; blocks past the
+// device counts exit)
+void xe_level_scan(hipStream_t s, const XeArgs& a, const XeLists& cur, int items_bound,
+                   int slots_bound) {
+  if (items_bound <= 0 || slots_bound <= 0) return;
+  const int Cc = xe_cc(a.C);
+  hipLaunchKernelGGL(xe_tot_kernel, dim3(items_bound, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
+  const int64_t nc = (int64_t)slots_bound * a.F_loc * Cc;
+  hipLaunchKernelGGL(xe_carry_kernel, dim3((unsigned)((nc + kXeThreads - 1) / kXeThreads)),
+                     dim3(kXeThreads), 0, s, a, cur);
+  hipLaunchKernelGGL(xe_scan_kernel, dim3(items_bound, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
+  hipLaunchKernelGGL(xe_select_kernel, dim3(slots_bound), dim3(kXeThreads), 0, s, a, cur);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void xe_plan(hipStream_t s, const XePlanArgs& p) {
+  hipLaunchKernelGGL(xe_plan_kernel, dim3(1), dim3(kXePlanThreads), 0, s, p);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void xe_flag(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_bound, int write_right) {
+  if (pitems_bound <= 0) return;
+  hipLaunchKernelGGL(xe_flag_kernel, dim3(pitems_bound), dim3(kXeThreads), 0, s, a, cur,
+                     write_right);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_bound,
+                  int splits_bound) {
+  if (pitems_bound <= 0 || splits_bound <= 0) return;
+  hipLaunchKernelGGL(xe_pcount_kernel, dim3(pitems_bound, a.F_loc), dim3(kXeThreads), 0, s, a,
+                     cur);
+  const int64_t ns = (int64_t)splits_bound * a.F_loc;
+  hipLaunchKernelGGL(xe_pcarry_kernel, dim3((unsigned)((ns + kXeThreads - 1) / kXeThreads)),
+                     dim3(kXeThreads), 0, s, a, cur);
+  hipLaunchKernelGGL(xe_pscatter_kernel, dim3(pitems_bound, a.F_loc), dim3(kXeThreads), 0, s, a,
+                     cur);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void xe_local_codes(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const int64_t* Y0,
+                    const int64_t* Y1, const uint32_t* rank_of, int64_t n, int F_loc, int f_lo,
+                    const int64_t* jobs, int J, int JW, uint8_t* codes_fm, uint32_t* ent,
+                    int64_t* yv) {
+  if (J <= 0) return;
+  hipLaunchKernelGGL(xe_local_codes_kernel, dim3(J), dim3(kXeLocalMax), 0, s, E0, E1, Y0, Y1,
+                     rank_of, n, F_loc, f_lo, jobs, JW, codes_fm, ent, yv);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void xe_codes_rm(hipStream_t s, const uint8_t* codes_fm, int64_t n, int F, int row_bytes,
+                 const int64_t* jobs, int J, int JW, uint8_t* codes_rm) {
+  if (J <= 0) return;
+  hipLaunchKernelGGL(xe_codes_rm_kernel, dim3(J), dim3(256), 0, s, codes_fm, n, F, row_bytes,
+                     jobs, JW, codes_rm);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void xe_fix(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const uint32_t* rank_of,
+            const void* X, int x64, int F, int64_t n, int f_lo, int F_loc, const int64_t* jobs,
+            int J, int JW, int32_t* pos_rec, double* pos_thr, uint8_t* resolved) {
+  if (J <= 0) return;
+  hipLaunchKernelGGL(xe_fix_kernel, dim3(J), dim3(256), 0, s, E0, E1, rank_of, X, x64, F, n, f_lo,
+                     F_loc, jobs, JW, pos_rec, pos_thr, resolved);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void xe_resolved_pack(hipStream_t s, const int32_t* pos_rec, const double* pos_thr, int64_t P,
+                      const int32_t* rank, int64_t* rows) {
+  const int64_t b = (P + 255) / 256;
+  if (b == 0) return;
+  hipLaunchKernelGGL(xe_resolved_pack_kernel, dim3((unsigned)b), dim3(256), 0, s, pos_rec, pos_thr,
+                     P, rank, rows);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void xe_resolved_scatter(hipStream_t s, const int64_t* rows, int64_t k, int32_t* pos_rec,
+                         double* pos_thr) {
+  if (k <= 0) return;
+  hipLaunchKernelGGL(xe_resolved_scatter_kernel, dim3((unsigned)((k + 255) / 256)), dim3(256), 0,
+                     s, rows, k, pos_rec, pos_thr);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void xe_emit(hipStream_t s, const uint64_t* keys, const uint32_t* rows, int64_t n, int F_loc,
+             int nc, int chunk, const int32_t* cbase, const int32_t* ylab, const int64_t* yfix,
+             uint32_t* E, int64_t* Y, uint32_t* rank_of) {
+  if (n <= 0 || F_loc <= 0) return;
+  hipLaunchKernelGGL(xe_emit_kernel, dim3(nc, F_loc), dim3(256), 0, s, keys, rows, n, nc, chunk,
+                     cbase, ylab, yfix, E, Y, rank_of);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace mt

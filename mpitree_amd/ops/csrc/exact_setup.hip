@@ -29,9 +29,10 @@ __device__ __forceinline__ float xs_key_value(uint32_t k) {
   return __uint_as_float((k >> 31) ? (k & 0x7fffffffu) : ~k);
 }
 
-// keys[f * n + i] = f << 32 | bits(X[i][f]); rows[f * n + i] = i
+// keys[f * n + i] = f << 32 | bits(X[i][f_lo + f]); rows[f * n + i] = i for the
+// F features of the block starting at column f_lo of a row-major X of stride xs
 __global__ __launch_bounds__(kXsThreads) void xs_keys_kernel(const float* __restrict__ X,
-                                                             int64_t n, int F,
+                                                             int64_t n, int F, int xs, int f_lo,
                                                              uint64_t* __restrict__ keys,
                                                              uint32_t* __restrict__ rows) {
   __shared__ uint32_t tile[kXsTile][kXsTile + 1];
@@ -41,7 +42,7 @@ __global__ __launch_bounds__(kXsThreads) void xs_keys_kernel(const float* __rest
   for (int r = ty; r < kXsTile; r += kXsThreads / kXsTile) {
     const int64_t i = i0 + r;
     const int f = f0 + tx;
-    tile[r][tx] = (i < n && f < F) ? xs_key_bits(X[i * F + f]) : 0u;
+    tile[r][tx] = (i < n && f < F) ? xs_key_bits(X[i * xs + f_lo + f]) : 0u;
   }
   __syncthreads();
   for (int c = ty; c < kXsTile; c += kXsThreads / kXsTile) {
@@ -150,11 +151,13 @@ size_t exact_setup_temp_bytes(int64_t n, int F) {
 // cnt: int32 [F][nc]; nuniq: int32 [F].
 void exact_setup_sort(hipStream_t stream, const float* X, int64_t n, int F, uint64_t* keys0,
                       uint64_t* keys1, uint32_t* rows0, uint32_t* rows1, void* temp,
-                      size_t temp_bytes, int32_t* cnt, int32_t* nuniq) {
+                      size_t temp_bytes, int32_t* cnt, int32_t* nuniq, int xs, int f_lo) {
+  if (xs <= 0) xs = F;
   if (n <= 0 || F <= 0) return;
   if (n >= (int64_t)1 << 24) throw std::runtime_error("exact setup: rows < 2^24");
   dim3 tg((unsigned)((n + kXsTile - 1) / kXsTile), (unsigned)((F + kXsTile - 1) / kXsTile));
-  hipLaunchKernelGGL(xs_keys_kernel, tg, dim3(kXsThreads), 0, stream, X, n, F, keys0, rows0);
+  hipLaunchKernelGGL(xs_keys_kernel, tg, dim3(kXsThreads), 0, stream, X, n, F, xs, f_lo, keys0,
+                     rows0);
   MT_HIP_CHECK(hipGetLastError());
   int fbits = 0;
   while ((1 << fbits) < F) ++fbits;

@@ -118,6 +118,47 @@ def device_loop_supported(be, params, comm) -> bool:
     return be.hip.hist_feature_tile(be.F, be.B, be.C, bool(be.reg), hb.LDS_BUDGET) > 0
 
 
+def exchange_ranges(be, comm, ranges: torch.Tensor, bound: int):
+    """Every rank wrote the positions inside its own ``ranges`` (int64 [cap, 2]
+    {lo, hi}, unused rows {0, 0}) of the position space and nothing else differs
+    between ranks: ``own_pack`` (assemble.hip) marks those ranges and packs their
+    live positions as {pos, record[6], stats[C]} rows; one all-gather; every
+    rank's rows are scattered back, so each position then holds its one writer's
+    record everywhere. ``bound``: at most this many rows (a subtree of r rows has
+    <= 2r - 1 nodes). Two small host waits: the packed row count, and the
+    all-gather's size exchange. Returns the gathered rows (keep until the
+    stream has passed the scatter)."""
+    hip = be.hip
+    s = hb._stream()
+    Pp = int(be.pos_rec.shape[0])
+    C, reg = be.C, bool(be.reg)
+    dt = torch.int64 if reg else torch.int32
+    esz = 8 if reg else 4
+    tiles = int(hip.asm_tiles(Pp))
+    bound = int(min(Pp, bound))
+    al = lambda x: (x + 255) // 256 * 256  # noqa: E731
+    o_tile, o_total = 0, al(max(tiles, 1) * 4)
+    o_rank = o_total + 256
+    o_mask = o_rank + al(Pp * 4)
+    o_rows = o_mask + al(Pp)
+    buf = hb._workspace(be.device, "own_exchange", o_rows + bound * (7 + C) * esz)
+    buf[o_mask : o_mask + Pp].zero_()
+    base = buf.data_ptr()
+    hip.own_pack(s, ranges.data_ptr(), int(ranges.shape[0]), base + o_mask, be.pos_rec.data_ptr(),
+                 be.pos_st.data_ptr(), reg, Pp, C, base + o_tile, base + o_total, base + o_rank,
+                 base + o_rows)
+    h_k = hb._pinned_copy(buf[o_total : o_total + 8].view(torch.int64), "own.k")
+    torch.cuda.current_stream(be.device).synchronize()
+    k = int(h_k[0])
+    if k > bound:
+        raise RuntimeError(f"node exchange: {k} nodes exceed the bound {bound}")
+    rows = buf[o_rows : o_rows + k * (7 + C) * esz].view(dt).view(k, 7 + C)
+    allr = comm.all_gather_rows(rows)
+    hip.own_scatter(s, allr.data_ptr(), int(allr.shape[0]), C, be.pos_rec.data_ptr(),
+                    be.pos_st.data_ptr(), reg)
+    return allr
+
+
 class DeviceGrower:
     def __init__(self, be, params, comm=None, checkpoint=None):
         self.be = be
@@ -314,41 +355,9 @@ class DeviceGrower:
     def _exchange_owned(self, ws):
         """Subtree ownership: this rank wrote every position inside its owned
         ranges (the switch level's LPT units) and nothing else differs between
-        ranks. ``own_pack`` (assemble.hip) marks those ranges and packs their live
-        positions as {pos, record[6], stats[C]} rows; one all-gather; every
-        rank's rows are scattered back, so each position then holds its one
-        writer's record on every rank. Two small host waits: the packed row
-        count, and the all-gather's size exchange."""
-        be, comm, hip = self.be, self.comm, self.be.hip
-        s = hb._stream()
-        Pp = int(be.pos_rec.shape[0])
-        C, reg = be.C, bool(be.reg)
-        dt = torch.int64 if reg else torch.int32
-        esz = 8 if reg else 4
-        tiles = int(hip.asm_tiles(Pp))
-        bound = min(Pp, 2 * int(self.stats.get("own_rows", Pp)) + 16)  # nodes <= 2 rows
-        al = lambda x: (x + 255) // 256 * 256  # noqa: E731
-        o_tile, o_total = 0, al(max(tiles, 1) * 4)
-        o_rank = o_total + 256
-        o_mask = o_rank + al(Pp * 4)
-        o_rows = o_mask + al(Pp)
-        buf = hb._workspace(be.device, "own_exchange", o_rows + bound * (7 + C) * esz)
-        buf[o_mask : o_mask + Pp].zero_()
-        base = buf.data_ptr()
-        rg = ws["own_ranges"]
-        hip.own_pack(s, rg.data_ptr(), int(rg.shape[0]), base + o_mask, be.pos_rec.data_ptr(),
-                     be.pos_st.data_ptr(), reg, Pp, C, base + o_tile, base + o_total,
-                     base + o_rank, base + o_rows)
-        h_k = hb._pinned_copy(buf[o_total : o_total + 8].view(torch.int64), "own.k")
-        torch.cuda.current_stream(be.device).synchronize()
-        k = int(h_k[0])
-        if k > bound:
-            raise RuntimeError(f"subtree exchange: {k} nodes exceed the bound {bound}")
-        rows = buf[o_rows : o_rows + k * (7 + C) * esz].view(dt).view(k, 7 + C)
-        allr = comm.all_gather_rows(rows)
-        hip.own_scatter(s, allr.data_ptr(), int(allr.shape[0]), C, be.pos_rec.data_ptr(),
-                        be.pos_st.data_ptr(), reg)
-        self._keep_x = allr
+        ranks (:func:`exchange_ranges`)."""
+        self._keep_x = exchange_ranges(self.be, self.comm, ws["own_ranges"],
+                                       2 * int(self.stats.get("own_rows", self.be.P)) + 16)
 
     def _level_profile(self, marks):
         """Per-level device times (ms) from the HIP events (MPITREE_PROFILE=1)."""

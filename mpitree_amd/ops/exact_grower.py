@@ -1,0 +1,395 @@
+"""Exact thresholds on continuous features: the device-driven presorted-list engine.
+
+The reference scores every unique value of a feature as a threshold
+(``mpitree/tree/decision_tree.py:73-90``) and splits its work by handing
+subtrees to MPI sub-communicators (``:446-477``). The histogram engines are
+exact only while a feature has at most 256 values; beyond that a GPU fit runs
+this engine (``ops/csrc/exact2.hip``, classification and regression):
+
+* setup: every feature column of this rank's block sorted once (one stable
+  radix sort of {feature, value} keys, ``exact_setup.hip``) into 4-byte list
+  entries {row, duplicate flag, label} (+ the fixed-point targets for
+  regression) and a per-row value-rank table;
+* a fixed chain of launches per level (chunk totals, carries, scan, select,
+  planner, flags, stable partition) whose work counts live in device memory:
+  the host enqueues levels back to back and reads one lagged host-mapped slot
+  per level to learn that the frontier is empty -- no per-level ``.cpu()``;
+* segments of at most 256 rows leave as finisher jobs: subtree-local 8-bit
+  codes (the offset of each value's first entry in the segment) feed the same
+  histogram finishers as the binned engines.
+
+Multi-GPU (one process per GPU, RCCL over xGMI; every rank holds all rows, the
+reference's contract): **feature-parallel**. Rank r sorts, scans and partitions
+only its contiguous feature block -- setup, scans and partitions all shrink
+with 1/P -- and per level one ``all_gather`` of the per-node split records
+(``fp_combine_kernel``: max gain, ties to the lowest feature) plus one
+``all_reduce`` of the n-byte row-direction flags (the split feature's owner
+sets them) keep the ranks in lock step. The finisher codes of every block are
+all-gathered once, the jobs are split across ranks (serpentine over the
+largest-first order) and one exchange of the finished position ranges plus
+one of the thresholds each rank resolved leave every rank with the same tree,
+equal to the single-GPU tree bit for bit.
+"""
+
+from __future__ import annotations
+
+import os
+import time
+
+import numpy as np
+import torch
+
+from . import hip_backend as hb
+from .device_grower import _host_ctl, _wait_slot, _FIT_SEQ, exchange_ranges
+from ..core.criterion import Criterion
+
+__all__ = ["ExactGrower", "exact_supported"]
+
+MAX_ROWS = 1 << 24
+_WS: dict = {}
+
+
+def exact_supported(n: int, C: int, regression: bool) -> bool:
+    """Rows index 24 bits of a list entry; labels live in 7 bits."""
+    from . import native
+
+    if n >= MAX_ROWS:
+        return False
+    return regression or 1 <= C <= int(native.hip().xe_max_classes())
+
+
+def _owners(J: int, P: int, device) -> torch.Tensor:
+    k = torch.arange(J, device=device)
+    lap, off = k // P, k % P
+    return torch.where(lap % 2 == 0, off, P - 1 - off)
+
+
+class ExactGrower:
+    """One exact-threshold fit on the current GPU (optionally feature-parallel)."""
+
+    def __init__(self, params, comm=None):
+        self.p = params
+        self.comm = comm
+        self.timings: dict = {}
+        self.stats: dict = {}
+
+    # ------------------------------------------------------------- setup
+    def _setup(self, Xd, F, f_lo, F_loc, y32, yfix, reg):
+        """Sorted lists of this rank's features: E0 (+ Y0), rank_of."""
+        dev = Xd.device
+        n = Xd.shape[0]
+        hip = self.hip
+        s = hb._stream()
+        E = [torch.empty((F_loc, n), dtype=torch.int32, device=dev) for _ in range(2)]
+        Y = [torch.empty((F_loc, n), dtype=torch.int64, device=dev) for _ in range(2)] if reg \
+            else [None, None]
+        rank_of = torch.empty((F_loc, n), dtype=torch.int32, device=dev)
+        ylab = 0 if reg else y32.data_ptr()
+        yf = yfix.data_ptr() if reg else 0
+        if Xd.dtype == torch.float32:
+            keys = [torch.empty((F_loc, n), dtype=torch.int64, device=dev) for _ in range(2)]
+            rows = [torch.empty((F_loc, n), dtype=torch.int32, device=dev) for _ in range(2)]
+            tb = int(hip.exact_setup_temp_bytes(n, F_loc))
+            temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
+            chunk = int(hip.exact_setup_chunk())
+            nc = -(-n // chunk)
+            cnt = torch.empty((F_loc, nc), dtype=torch.int32, device=dev)
+            nuniq = torch.empty(F_loc, dtype=torch.int32, device=dev)
+            hip.exact_setup_sort(s, Xd.data_ptr(), n, F_loc, keys[0].data_ptr(),
+                                 keys[1].data_ptr(), rows[0].data_ptr(), rows[1].data_ptr(),
+                                 temp.data_ptr(), tb, cnt.data_ptr(), nuniq.data_ptr(),
+                                 xs=F, f_lo=f_lo)
+            hip.xe_emit(s, keys[1].data_ptr(), rows[1].data_ptr(), n, F_loc, nc, chunk,
+                        cnt.data_ptr(), ylab, yf, E[0].data_ptr(),
+                        Y[0].data_ptr() if reg else 0, rank_of.data_ptr())
+            del keys, rows, temp, cnt, nuniq  # (stream-ordered frees)
+        else:  # fp64: per-feature stable sorts (ties by row id, -0.0 == 0.0)
+            xt = Xd[:, f_lo:f_lo + F_loc].t().contiguous()
+            vals, order = torch.sort(xt, dim=1, stable=True)
+            del xt
+            new = torch.ones_like(vals, dtype=torch.bool)
+            new[:, 1:] = vals[:, 1:] != vals[:, :-1]
+            nxt_same = torch.zeros_like(new)
+            nxt_same[:, :-1] = ~new[:, 1:]
+            dup = (~new) | nxt_same
+            rank = torch.cumsum(new, 1, dtype=torch.int32) - 1
+            o32 = order.to(torch.int32)
+            ent = o32 | (dup.to(torch.int32) << 24)
+            if not reg:
+                ent = ent | (y32[order].to(torch.int32) << 25)
+            E[0].copy_(ent)
+            rank_of.scatter_(1, order, rank)
+            if reg:
+                Y[0].copy_(yfix[order])
+            del vals, order, new, nxt_same, dup, rank, o32, ent
+        return E, Y, rank_of
+
+    # --------------------------------------------------------------- fit
+    def fit(self, Xd: torch.Tensor, y_codes: torch.Tensor, root, C: int, crit: Criterion,
+            y_exp: int = 0, timings=None):
+        """Grow the tree of ``Xd`` (device [n, F] fp32/fp64, every rank the same
+        rows) with int32 labels ``y_codes`` (``C`` classes) or int64 fixed-point
+        targets (regression, ``C = 0``); ``root``: the root statistics (class
+        counts, or {count, sum, min, max})."""
+        from . import native
+
+        t0 = time.perf_counter()
+        hip = self.hip = native.hip()
+        p, comm = self.p, self.comm
+        reg = crit == Criterion.SQUARED_ERROR
+        Cs = 2 if reg else int(C)
+        Cc = 1 if reg else int(C)
+        Cx = 0 if reg else int(C)
+        n, F = Xd.shape
+        dev = Xd.device
+        P = int(getattr(comm, "world_size", 1) or 1)
+        rank = int(getattr(comm, "rank", 0) or 0)
+        if P > 1:
+            if F < P:
+                raise ValueError(f"exact feature-parallel fit needs n_features >= world size "
+                                 f"({F} < {P})")
+            from ..parallel.strategies import feature_blocks
+
+            blocks = feature_blocks(F, P)
+            f_lo, f_hi = blocks[rank]
+        else:
+            blocks = [(0, F)]
+            f_lo, f_hi = 0, F
+        F_loc = f_hi - f_lo
+        s = hb._stream
+        y32 = None if reg else y_codes.to(torch.int32).contiguous()
+        yfix = y_codes.to(torch.int64).contiguous() if reg else None
+        E, Y, rank_of = self._setup(Xd, F, f_lo, F_loc, y32, yfix, reg)
+        if timings is not None:
+            timings["exact_setup"] = time.perf_counter() - t0
+
+        # ---- position space and finisher backend (local codes)
+        be = hb.HipBackend(dev)
+        be.n, be.F, be.C = n, F, (2 if reg else int(C))
+        be.reg = reg
+        be.crit = crit
+        be.xtab = hb.xlog2x_table(dev)
+        be.xtabf = hb.xlog2x_table_f32(dev)
+        be.begin_positions(2 * n - 1)
+        pos_thr = hb._workspace(dev, "xe.thr", (2 * n - 1) * 8)[: (2 * n - 1) * 8].view(
+            torch.float64)
+        md = -1 if p.max_depth is None else int(p.max_depth)
+        mss, msl = int(p.min_samples_split), int(max(1, p.min_samples_leaf))
+        root = np.asarray(root, dtype=np.int64)
+        if reg:
+            root_stats = root[:2]
+            pure = n == 0 or root[2] == root[3]
+        else:
+            root_stats = root
+            pure = int((root > 0).sum()) <= 1
+        if md == 0 or n < mss or n < 2 * msl or pure:
+            be.put_positions([0], [-1], [-1], [-1], [-1], [0], [n], root_stats[None, :])
+            self.stats.update(levels=0, finisher_subtrees=0)
+            return be.assemble_positions(None, int(crit), y_exp, thr_pos=pos_thr)
+
+        fr = int(hip.xe_local_max())
+        env = os.environ.get("MPITREE_EXACT_FINISHER_ROWS")  # (tests: 0 = no finisher)
+        if env is not None:
+            fr = max(0, min(fr, int(env)))
+        chunk = int(hip.xe_chunk())
+        KMAX = n // (fr + 1) + 2
+        IMAX = KMAX + n // chunk + 2
+        JMAX = n // 2 + 2
+        R = int(hip.xe_rec_width(Cx))
+        JW = 5 + Cs
+        i64 = dict(dtype=torch.int64, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        key = (str(dev), n, F_loc, Cx, P)
+        ws = _WS.get(key)
+        if ws is None:
+            _WS.clear()
+
+            def lists():
+                return dict(pos=torch.empty(KMAX, **i64), start=torch.empty(KMAX, **i64),
+                            cnt=torch.empty(KMAX, **i32), depth=torch.empty(KMAX, **i32),
+                            stats=torch.empty((KMAX, Cs), **i64),
+                            minmax=torch.empty((KMAX, 2), **i64),
+                            items=torch.empty((IMAX, 4), **i64),
+                            ifirst=torch.empty(KMAX + 1, **i32), ctl=torch.zeros(16, **i32))
+
+            nbw = int(hip.xe_bits_words())
+            ws = _WS[key] = dict(
+                L=[lists(), lists()],
+                tot=torch.empty((IMAX, F_loc, Cc), **i64),
+                carry=torch.empty((IMAX, F_loc, Cc), **i64),
+                cmm=torch.empty((IMAX, 2), **i64),
+                cbest=torch.empty((IMAX, F_loc, 2), **i64),
+                rec=torch.empty((KMAX, R), **i64),
+                grec=torch.empty((P * KMAX * R) if P > 1 else 1, **i64),
+                split=torch.empty((KMAX, 4), **i64),
+                pitems=torch.empty((IMAX, 4), **i64),
+                pfirst=torch.empty(KMAX + 1, **i32),
+                flag=torch.empty(n, dtype=torch.uint8, device=dev),
+                lc=torch.empty((IMAX, F_loc), **i32),
+                lcar=torch.empty((IMAX, F_loc), **i32),
+                bits=torch.empty((IMAX, F_loc, nbw), **i64),
+                jobs=torch.empty((JMAX, JW), **i64),
+                job_count=torch.zeros(1, **i32),
+                root=torch.empty(Cs, **i64),
+            )
+        L = ws["L"]
+        ptr = {k: (v.data_ptr() if isinstance(v, torch.Tensor) else 0) for k, v in ws.items()}
+        lp = [{k: v.data_ptr() for k, v in x.items()} for x in L]
+        ctx = hip.XeCtx(dict(
+            E0=E[0].data_ptr(), E1=E[1].data_ptr(),
+            Y0=Y[0].data_ptr() if reg else 0, Y1=Y[1].data_ptr() if reg else 0,
+            rank_of=rank_of.data_ptr(), X=Xd.data_ptr(), x64=int(Xd.dtype == torch.float64),
+            n=n, F=F, f_lo=f_lo, F_loc=F_loc, C=Cx, crit=int(crit), msl=msl,
+            xtab=be.xtab.data_ptr(), xtab_n=hb.XTAB_N, tot=ptr["tot"], carry=ptr["carry"],
+            cmm=ptr["cmm"], cbest=ptr["cbest"], rec=ptr["rec"], split=ptr["split"],
+            pitems=ptr["pitems"], pfirst=ptr["pfirst"], flag=ptr["flag"], lc=ptr["lc"],
+            lcar=ptr["lcar"], bits=ptr["bits"], pos_rec=be.pos_rec.data_ptr(),
+            pos_st=be.pos_st.data_ptr(), pos_thr=pos_thr.data_ptr(), jobs=ptr["jobs"],
+            job_count=ptr["job_count"], max_depth=md, mss=mss, fr=fr), lp[0], lp[1])
+        ws["root"].copy_(torch.from_numpy(np.ascontiguousarray(root_stats, np.int64)))
+        ctx.init(s(), ws["root"].data_ptr())
+        self._keep = (ctx, E, Y, rank_of)
+
+        # ---- level loop: enqueue only; a lagged host-mapped slot tells the end
+        hctl_dev, hctl = _host_ctl(hip, dev)
+        _FIT_SEQ[0] = (_FIT_SEQ[0] + 1) % (1 << 18)
+        tag0 = _FIT_SEQ[0] << 12
+        t1 = time.perf_counter()
+        lvl, done_at = 0, None
+        comm_bytes = []
+        while True:
+            b0 = getattr(comm, "bytes_communicated", 0)
+            kb = int(min(2 ** min(lvl, 40), KMAX))
+            ib = int(min(IMAX, kb + n // chunk + 1))
+            ctx.level_scan(s(), lvl, ib, kb)
+            if P > 1:  # every rank's best split per node -> the global best
+                g = ws["grec"][: P * kb * R]
+                comm.all_gather_device(g, ws["rec"][:kb].reshape(-1))
+                hip.fp_combine(s(), g.data_ptr(), P, kb, R, lp[lvl % 2]["ctl"],
+                               ws["rec"].data_ptr())
+            ctx.plan(s(), lvl, hctl_dev + (lvl % 64) * 64, tag0 + (lvl % 4096) + 1)
+            if P > 1:  # the split feature's owner sets the left rows; summed over ranks
+                ws["flag"].zero_()
+                ctx.flag(s(), lvl, ib, 0)
+                comm.all_reduce_device(ws["flag"])
+                comm_bytes.append(int(getattr(comm, "bytes_communicated", 0) - b0))
+            else:
+                ctx.flag(s(), lvl, ib, 1)
+            ctx.partition(s(), lvl, ib, kb)
+            lvl += 1
+            if lvl >= 2:
+                _wait_slot(hctl, (lvl - 2) % 64, tag0 + ((lvl - 2) % 4096) + 1)
+                if int(hctl[(lvl - 2) % 64, 0]) == 0:
+                    done_at = lvl - 2
+                    break
+            if lvl > 4096:
+                raise RuntimeError("exact level loop did not terminate")
+        J = int(hctl[done_at % 64, 1])
+        self.stats["levels"] = done_at + 1
+        self.stats["finisher_subtrees"] = J
+        if timings is not None:
+            timings["levels"] = time.perf_counter() - t1
+        t2 = time.perf_counter()
+        if J:
+            self._finish(ws, be, E, Y, rank_of, Xd, J, JW, F, f_lo, F_loc, blocks, n, Cx, reg,
+                         crit, pos_thr, P, rank)
+        if P > 1:
+            self.stats["comm_bytes_per_level"] = comm_bytes
+            self.stats["mode"] = "feature"
+            self.stats["feature_block"] = [f_lo, f_hi]
+        if timings is not None:
+            timings["finisher"] = time.perf_counter() - t2
+        t3 = time.perf_counter()
+        ta = be.assemble_positions(None, int(crit), y_exp, thr_pos=pos_thr)
+        if timings is not None:
+            timings["assemble"] = time.perf_counter() - t3
+        self._keep = None
+        return ta
+
+    # --------------------------------------------------------- finisher
+    def _finish(self, ws, be, E, Y, rank_of, Xd, J, JW, F, f_lo, F_loc, blocks, n, Cx, reg,
+                crit, pos_thr, P, rank):
+        """Grow the <= 256-row job segments on subtree-local codes; turn the
+        finisher's codes back into value ranks and thresholds."""
+        hip, comm = self.hip, self.comm
+        s = hb._stream
+        dev = Xd.device
+        jobs = ws["jobs"][:J]
+        rb = (F + 15) // 16 * 16
+        key = (str(dev), n, F, P)
+        cache = _WS.setdefault("loc", {})
+        loc = cache.get(key)
+        if loc is None:
+            cache.clear()
+            Fb = max(hi - lo for lo, hi in blocks)
+            loc = cache[key] = dict(
+                rm=torch.empty((n, rb), dtype=torch.uint8, device=dev),
+                fm=torch.empty((F, n), dtype=torch.uint8, device=dev),
+                blk=torch.empty((Fb, n), dtype=torch.uint8, device=dev) if P > 1 else None,
+                ent=torch.empty(n, dtype=torch.int32, device=dev),
+                tmp=torch.empty(n, dtype=torch.int32, device=dev),
+                yv=torch.empty(n, dtype=torch.int64, device=dev) if reg else None,
+                nbins=torch.full((F,), 256, dtype=torch.int32, device=dev),
+                gather=(torch.empty((P, Fb, n), dtype=torch.uint8, device=dev) if P > 1
+                        else None),
+            )
+        fm_out = loc["blk"] if P > 1 else loc["fm"]
+        hip.xe_local_codes(s(), E[0].data_ptr(), E[1].data_ptr(),
+                           Y[0].data_ptr() if reg else 0, Y[1].data_ptr() if reg else 0,
+                           rank_of.data_ptr(), n, F_loc, 0, jobs.data_ptr(), J, JW,
+                           fm_out.data_ptr(), loc["ent"].data_ptr(),
+                           loc["yv"].data_ptr() if reg else 0)
+        if P > 1:  # every rank's feature block of the codes -> all features on every rank
+            g = loc["gather"]
+            comm.all_gather_device(g.view(-1), loc["blk"].view(-1))
+            for r, (lo, hi) in enumerate(blocks):
+                loc["fm"][lo:hi].copy_(g[r, : hi - lo])
+        hip.xe_codes_rm(s(), loc["fm"].data_ptr(), n, F, rb, jobs.data_ptr(), J, JW,
+                        loc["rm"].data_ptr())
+        # the finisher reads the binned engine's fields: point them at the local codes
+        be.codes_rm, be.codes_fm = loc["rm"], loc["fm"]
+        be.row_elems, be.cb, be.B, be.nbins = rb, 1, 256, loc["nbins"]
+        be.idx, be.tmp = loc["ent"], loc["tmp"]
+        if reg:
+            be.lab_shift, be.row_mask, be.y = 0, 0xFFFFFFFF, loc["yv"]
+        else:
+            be.lab_shift, be.row_mask, be.y = 24, (1 << 24) - 1, loc["ent"]
+        fj = jobs.clone()
+        fj[:, 4] = 0  # rows live in the virtual row buffer (idx)
+        order = torch.argsort(fj[:, 1] * (1 << 32) - fj[:, 3], descending=True)
+        fj = fj.index_select(0, order)
+        if P > 1:
+            own = _owners(J, P, dev) == rank
+            fj = fj[own].contiguous()
+        Jm = int(fj.shape[0])
+        if Jm:
+            be.launch_finisher(fj, Jm, n, self.p, be.pos_rec, be.pos_st)
+        if P > 1:  # finished job ranges -> every rank; then the thresholds each rank resolves
+            rg = torch.stack([fj[:, 3], fj[:, 3] + 2 * fj[:, 1] - 1], 1).contiguous()
+            if rg.shape[0] == 0:
+                rg = torch.zeros((1, 2), dtype=torch.int64, device=dev)
+            self._keep_x = exchange_ranges(be, comm, rg, int(2 * fj[:, 1].sum().item()) + 16)
+            Pp = int(be.pos_rec.shape[0])
+            resolved = torch.zeros(Pp, dtype=torch.uint8, device=dev)
+            hip.xe_fix(s(), E[0].data_ptr(), E[1].data_ptr(), rank_of.data_ptr(), Xd.data_ptr(),
+                       int(Xd.dtype == torch.float64), F, n, f_lo, F_loc, jobs.data_ptr(), J, JW,
+                       be.pos_rec.data_ptr(), pos_thr.data_ptr(), resolved.data_ptr())
+            tiles = int(hip.asm_tiles(Pp))
+            tile = torch.empty(max(tiles, 1), dtype=torch.int32, device=dev)
+            total = torch.zeros(2, dtype=torch.int64, device=dev)
+            rk = torch.empty(Pp, dtype=torch.int32, device=dev)
+            hip.asm_rank(s(), be.pos_rec.data_ptr(), Pp, tile.data_ptr(), total.data_ptr(),
+                         rk.data_ptr(), mask=resolved.data_ptr())
+            k = int(total[0].item())
+            rows = torch.empty((max(k, 1), 3), dtype=torch.int64, device=dev)
+            hip.xe_resolved_pack(s(), be.pos_rec.data_ptr(), pos_thr.data_ptr(), Pp,
+                                 rk.data_ptr(), rows.data_ptr())
+            allr = comm.all_gather_rows(rows[:k])
+            hip.xe_resolved_scatter(s(), allr.data_ptr(), int(allr.shape[0]),
+                                    be.pos_rec.data_ptr(), pos_thr.data_ptr())
+            self._keep_r = (allr, rows, resolved)
+        else:
+            hip.xe_fix(s(), E[0].data_ptr(), E[1].data_ptr(), rank_of.data_ptr(), Xd.data_ptr(),
+                       int(Xd.dtype == torch.float64), F, n, f_lo, F_loc, jobs.data_ptr(), J, JW,
+                       be.pos_rec.data_ptr(), pos_thr.data_ptr(), 0)
+        self._keep_f = (loc, fj)

@@ -578,7 +578,8 @@ class HipBackend:
         self.pos_rec.index_copy_(0, d_pos, d_rec.reshape(-1, 6).to(torch.int32))
         self.pos_st.index_copy_(0, d_pos, d_st.reshape(-1, self.C).to(self.pos_st.dtype))
 
-    def assemble_positions(self, edges, crit: int, y_exp: int = 0, d_edges=None) -> TreeArrays:
+    def assemble_positions(self, edges, crit: int, y_exp: int = 0, d_edges=None,
+                           thr_pos=None) -> TreeArrays:
         """Compact the position space into the finished, pre-ordered
         :class:`TreeArrays` (numpy views of one pinned host buffer; every column
         is computed on the device, nothing is derived on the host afterwards).
@@ -589,7 +590,7 @@ class HipBackend:
         P, C = self.P, self.C
         hip = self.hip
         s = _stream()
-        if d_edges is None:
+        if d_edges is None and thr_pos is None:
             d_edges = torch.from_numpy(np.ascontiguousarray(edges, np.float64)).to(self.device)
         tiles = hip.asm_tiles(P)
         bpn = int(hip.asm_node_bytes(C, self.reg))
@@ -602,9 +603,11 @@ class HipBackend:
         total = ws[o_total : o_total + 16].view(torch.int64)  # {nodes, depth}
         hip.asm_rank(s, self.pos_rec.data_ptr(), P, base, base + o_total, base + o_rank)
         hip.asm_emit(s, self.pos_rec.data_ptr(), self.pos_st.data_ptr(), self.reg, P, C,
-                     base + o_rank, d_edges.data_ptr(), int(d_edges.stride(0)),
+                     base + o_rank, 0 if d_edges is None else d_edges.data_ptr(),
+                     0 if d_edges is None else int(d_edges.stride(0)),
                      base + o_total, base + o_out, bool(self.reg), int(crit), int(y_exp),
-                     self.xtab.data_ptr(), XTAB_N)
+                     self.xtab.data_ptr(), XTAB_N,
+                     thr_pos=0 if thr_pos is None else thr_pos.data_ptr())
         h_total = _pinned_copy(total, "asm.total")
         # the columns are laid out from the device node count, so a copy sized for
         # the previous fit's count on this position space (a refit of the same

@@ -183,6 +183,60 @@ def test_gpu_ranks_equal_single_gpu_at_scale(regression, strategy, world):
                 np.testing.assert_array_equal(o[f"{k}{it}"], getattr(ref, k), err_msg=k)
 
 
+def _fit_rank_gpu_exact(rank, world, regression):
+    import torch
+
+    from mpitree_amd import ParallelDecisionTreeClassifier, ParallelDecisionTreeRegressor
+    from mpitree_amd.utils.datasets import make_classification, make_regression
+
+    dev = torch.device("cuda", 0)
+    if regression:
+        X, y = make_regression(60_000, 10, levels=None, seed=3, device=dev)
+        est = ParallelDecisionTreeRegressor(device="cuda").fit(X, y)
+    else:
+        X, y = make_classification(80_000, 10, levels=None, seed=3, device=dev)
+        est = ParallelDecisionTreeClassifier(device="cuda").fit(X, y)
+    ta = est.tree_arrays_
+    out = {k: getattr(ta, k) for k in FIELDS + ("threshold",)}
+    out["value" if regression else "count"] = ta.value if regression else ta.count
+    out["engine"] = np.array([est.fit_stats_["engine"]])
+    out["mode"] = np.array([est.fit_stats_.get("mode", "")])
+    out["block"] = np.array(est.fit_stats_.get("feature_block", [-1, -1]))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("regression", [False, True])
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_exact_feature_parallel_equals_single_gpu(regression, world):
+    """Continuous features (every value a threshold) over 2-3 ranks sharing one
+    MI355X: the exact engine runs feature-parallel (each rank sorts, scans and
+    partitions its feature block; per level one record all-gather and one flag
+    all-reduce) and every rank builds the single-GPU tree bit for bit."""
+    import torch
+
+    from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
+    from mpitree_amd.utils.datasets import make_classification, make_regression
+
+    outs = run_ranks(_fit_rank_gpu_exact, world, regression, start_method="spawn")
+    dev = torch.device("cuda", 0)
+    if regression:
+        X, y = make_regression(60_000, 10, levels=None, seed=3, device=dev)
+        ref = DecisionTreeRegressor(device="cuda").fit(X, y)
+    else:
+        X, y = make_classification(80_000, 10, levels=None, seed=3, device=dev)
+        ref = DecisionTreeClassifier(device="cuda").fit(X, y)
+    assert ref.fit_stats_["engine"] == "hip-exact"
+    blocks = sorted(tuple(o["block"]) for o in outs)
+    assert blocks[0][0] == 0 and blocks[-1][1] == 10  # the ranks cover every feature
+    for o in outs:
+        assert str(o["engine"][0]) == "hip-exact" and str(o["mode"][0]) == "feature"
+        for k in FIELDS + ("threshold",):
+            np.testing.assert_array_equal(o[k], getattr(ref.tree_arrays_, k), err_msg=k)
+        key = "value" if regression else "count"
+        np.testing.assert_array_equal(o[key], getattr(ref.tree_arrays_, key))
+
+
 def _fit_rank_rccl(rank, world, strategy, regression):
     import torch
     import torch.distributed as dist

@@ -480,6 +480,42 @@ def test_gpu_exact_finisher_handoff_same_tree(monkeypatch):
     np.testing.assert_array_equal(a.tree_arrays_.threshold, b.tree_arrays_.threshold)
 
 
+@pytest.mark.parametrize("shape", [(50000, 6, None, 1), (8000, 3, 5, 2)])
+def test_gpu_exact_regression_matches_host(shape):
+    """Regression on continuous features: exact thresholds on the GPU (the
+    presorted-list engine's target prefix sums), equal to the host builder."""
+    from mpitree_amd import DecisionTreeRegressor
+
+    n, F, md, msl = shape
+    rng = np.random.default_rng(n + F)
+    X = rng.normal(size=(n, F)).astype(np.float32)
+    X[:, 1] = np.round(X[:, 1], 2)  # ties on one feature
+    y = X[:, 0] * 2.0 + np.sin(3 * X[:, 1]) + rng.normal(scale=0.3, size=n)
+    kw = dict(max_depth=md, min_samples_leaf=msl)
+    g = DecisionTreeRegressor(device="cuda", **kw).fit(X, y)
+    assert g.fit_stats_["engine"] == "hip-exact", g.fit_stats_
+    assert g.fit_stats_["thresholds"] == "exact (presorted lists)"
+    h = DecisionTreeRegressor(device="cpu", **kw).fit(X, y)
+    assert g.tree_arrays_.equal(h.tree_arrays_, check_impurity=False)
+    np.testing.assert_array_equal(g.tree_arrays_.value, h.tree_arrays_.value)
+    np.testing.assert_array_equal(g.predict(X), h.predict(X))
+
+
+def test_gpu_exact_threshold_bins_beyond_16_bits():
+    """More than 65,536 unique values in a feature: split value ranks (the exact
+    engine's threshold bins) travel as full int32 columns and equal the host's."""
+    rng = np.random.default_rng(3)
+    n = 120_000
+    X = rng.normal(size=(n, 2)).astype(np.float32)
+    y = ((X[:, 0] + 0.5 * X[:, 1] + rng.normal(scale=0.7, size=n)) > 0).astype(np.int64)
+    g = DecisionTreeClassifier(max_depth=6, device="cuda").fit(X, y)
+    h = DecisionTreeClassifier(max_depth=6, device="cpu").fit(X, y)
+    assert g.fit_stats_["engine"] == "hip-exact"
+    assert int(g.tree_arrays_.threshold_bin.max()) > 65535
+    np.testing.assert_array_equal(g.tree_arrays_.threshold_bin, h.tree_arrays_.threshold_bin)
+    assert g.tree_arrays_.equal(h.tree_arrays_)
+
+
 def test_gpu_exact_engine_device_tensors_and_quantile_optin():
     rng = np.random.default_rng(7)
     X = torch.from_numpy(rng.normal(size=(50000, 8)).astype(np.float32)).cuda()
