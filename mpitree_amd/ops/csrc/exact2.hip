@@ -181,7 +181,7 @@ __global__ __launch_bounds__(kXeThreads) void xe_carry_kernel(XeArgs a, XeLists 
 // Value boundary between consecutive entries of a segment: equal values need
 // both entries flagged dup and equal ranks.
 __device__ __forceinline__ bool xe_boundary(uint32_t e, uint32_t nx, const uint32_t* __restrict__ rk) {
-  if (!xe_dup(e) || !xe_dup(nx)) return true;
+  if (nx == 0xFFFFFFFFu || !xe_dup(e) || !xe_dup(nx)) return true;
   return rk[xe_row(e)] != rk[xe_row(nx)];
 }
 
@@ -688,8 +688,10 @@ __global__ __launch_bounds__(kXePlanThreads) void xe_plan_kernel(XePlanArgs a) {
         P[1] = (int32_t)r[5];  // threshold value rank
         P[2] = (int32_t)cpos[0];
         P[3] = (int32_t)cpos[1];
-        a.pos_thr[pos] = a.x64 ? reinterpret_cast<const double*>(a.X)[row * a.F + feat]
-                               : (double)reinterpret_cast<const float*>(a.X)[row * a.F + feat];
+        // (+ 0.0: a -0.0 threshold prints as 0.0, as np.unique's representative)
+        a.pos_thr[pos] = (a.x64 ? reinterpret_cast<const double*>(a.X)[row * a.F + feat]
+                                : (double)reinterpret_cast<const float*>(a.X)[row * a.F + feat]) +
+                         0.0;
         int64_t* S = a.split + (int64_t)o_ns * 4;
         S[0] = start;
         S[1] = m;
@@ -1058,8 +1060,9 @@ __global__ __launch_bounds__(256) void xe_fix_kernel(
     if (f < 0 || f >= F_loc) continue;
     const uint32_t row = xe_row(E[(int64_t)f * n + s + R[1]]);
     R[1] = (int32_t)rank_of[(int64_t)f * n + row];
-    pos_thr[p] = x64 ? reinterpret_cast<const double*>(X)[(int64_t)row * F + R[0]]
-                     : (double)reinterpret_cast<const float*>(X)[(int64_t)row * F + R[0]];
+    pos_thr[p] = (x64 ? reinterpret_cast<const double*>(X)[(int64_t)row * F + R[0]]
+                      : (double)reinterpret_cast<const float*>(X)[(int64_t)row * F + R[0]]) +
+                 0.0;
     if (resolved) resolved[p] = 1;
   }
 }

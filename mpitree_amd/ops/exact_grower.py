@@ -47,6 +47,7 @@ __all__ = ["ExactGrower", "exact_supported"]
 
 MAX_ROWS = 1 << 24
 _WS: dict = {}
+_DEBUG_SYNC = os.environ.get("MPITREE_EXACT_SYNC") == "1"
 
 
 def exact_supported(n: int, C: int, regression: bool) -> bool:
@@ -199,7 +200,7 @@ class ExactGrower:
         JW = 5 + Cs
         i64 = dict(dtype=torch.int64, device=dev)
         i32 = dict(dtype=torch.int32, device=dev)
-        key = (str(dev), n, F_loc, Cx, P)
+        key = (str(dev), n, F_loc, Cx, P, KMAX, IMAX)
         ws = _WS.get(key)
         if ws is None:
             _WS.clear()
@@ -276,6 +277,10 @@ class ExactGrower:
             else:
                 ctx.flag(s(), lvl, ib, 1)
             ctx.partition(s(), lvl, ib, kb)
+            if _DEBUG_SYNC:  # (MPITREE_EXACT_SYNC=1: sync + report every level)
+                torch.cuda.synchronize(dev)
+                print(f"exact level {lvl}: next frontier {int(L[(lvl + 1) % 2]['ctl'][0])}, "
+                      f"jobs {int(ws['job_count'][0])}", flush=True)
             lvl += 1
             if lvl >= 2:
                 _wait_slot(hctl, (lvl - 2) % 64, tag0 + ((lvl - 2) % 4096) + 1)

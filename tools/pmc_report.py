@@ -12,8 +12,9 @@ identical fits), so per-level kernels report per-fit totals. Derived columns:
 * wait%, issue-stall%, active%: SQ_WAIT_ANY, SQ_WAIT_INST_ANY, SQ_ACTIVE_INST_ANY
   as shares of SQ_WAVE_CYCLES (disjoint buckets on gfx950)
 * LDS conflict%: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
-* MB: (FETCH_SIZE + WRITE_SIZE) KB / 1024 (FETCH_SIZE under-counts wide
-  streams by up to 2x on gfx950); GB/s over the traced kernel time
+* read / write MB: FETCH_SIZE / WRITE_SIZE KB / 1024 (FETCH_SIZE under-counts wide
+  streams by up to 2x on gfx950 -- MI355X_MICROARCH.md); GB/s: their sum over the
+  traced kernel time
 """
 
 from __future__ import annotations
@@ -54,8 +55,8 @@ def main():
     f = a.fits
     rows = sorted(ctr, key=lambda k: -dur.get(k, 0.0))[: a.top]
     print("| kernel | calls/fit | us/fit | VALU/wave | LDS/wave | wait% | issue-stall% | active% "
-          "| LDS conflict% | MB/fit | GB/s |")
-    print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
+          "| LDS conflict% | read MB/fit | write MB/fit | GB/s |")
+    print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
     for k in rows:
         c = ctr[k]
         waves = c.get("SQ_WAVES", 0.0)
@@ -67,13 +68,15 @@ def main():
         per = (lambda n: f"{c[n] / waves:.0f}" if waves and n in c else "")
         lds = (f"{100 * c['SQ_LDS_BANK_CONFLICT'] / c['SQ_LDS_IDX_ACTIVE']:.1f}"
                if c.get("SQ_LDS_IDX_ACTIVE") else "")
-        mb = (c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0)) / 1024 / f
+        rd = c.get("FETCH_SIZE", 0.0) / 1024 / f
+        wr = c.get("WRITE_SIZE", 0.0) / 1024 / f
+        mb = rd + wr
         us = dur.get(k, 0.0) / f
         gbs = f"{mb / 1e3 / (us / 1e6):.0f}" if us and mb else ""
         n = len({x for x in calls[k]}) / max(1, len(a.dirs)) / f
         print(f"| `{k}` | {n:.1f} | {us:.1f} | {per('SQ_INSTS_VALU')} | {per('SQ_INSTS_LDS')} | "
               f"{pct('SQ_WAIT_ANY')} | {pct('SQ_WAIT_INST_ANY')} | {pct('SQ_ACTIVE_INST_ANY')} | "
-              f"{lds} | {mb:.1f} | {gbs} |")
+              f"{lds} | {rd:.1f} | {wr:.1f} | {gbs} |")
 
 
 if __name__ == "__main__":
