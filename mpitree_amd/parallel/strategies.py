@@ -23,13 +23,20 @@ one fused collective per tree level instead of per node:
     every rank scans identically. Suited to n >> node count (10M x 128).
 ``SubtreeComm`` ("subtree")
     The reference's strategy made load-balanced: upper levels are computed
-    redundantly with no communication, then the finisher's subtree jobs are
-    assigned to ranks by greedy longest-processing-time on row counts (not by
-    rank parity) and the finished node tables are exchanged with one
-    ``all_gather``.
+    redundantly with no communication until the first level with at least
+    ``4 * P`` units (split nodes whose children keep growing + finisher jobs);
+    that level assigns the units to ranks by greedy longest-processing-time on
+    row counts (not by rank parity), each rank grows only its own units --
+    device level loop and finisher -- and one ``all_gather`` of the finished
+    position ranges completes the tree on every rank (GPU device loop,
+    ``ops/device_grower.py``). Host-driven fits hand out only the finisher's
+    subtree jobs that way.
 "auto"
-    Feature-parallel upper levels + load-balanced subtree finishing when
-    ``F >= world_size``, otherwise subtree.
+    Replicated rows: subtree ownership on the GPU device loop (feature-parallel
+    levels with load-balanced subtree finishing on host-driven fits when
+    ``F >= world_size``); row-sharded input: data-parallel. Exact thresholds on
+    continuous features run the presorted-list engine feature-parallel
+    (``ops/exact_grower.py``).
 
 Collectives run on the backend's device (RCCL over xGMI for GPU fits, gloo
 for CPU fits), so the same code is exercised by the multi-process CPU tests.
@@ -309,8 +316,11 @@ class DataParallelComm(DistComm):
         return np.concatenate([s, mn[:, None], mx[:, None]], 1)
 
     def fit_kwargs(self) -> dict:
-        # a subtree's rows live on every rank: the single-workgroup finisher
-        # does not apply (hybrid redistribution is the "auto" path's job)
+        # host-driven (CPU) data-parallel fits grow every level with per-level
+        # histogram all-reduces: a subtree's rows are spread over the ranks, so
+        # the single-process finisher does not apply. GPU fits ignore this: the
+        # device loop sends each subtree job's rows to its owner first
+        # (DeviceGrower._dp_finish) and uses the single-GPU finisher split point.
         return {"finisher_rows": 0}
 
 
@@ -328,10 +338,13 @@ class SubtreeComm(DistComm):
 
 
 class AutoComm(FeatureParallelComm):
-    """``strategy="auto"`` with replicated rows. Single-GPU-per-rank fits that
-    the device-driven loop supports use the replicated-top / split-finisher
-    scheme (:class:`~mpitree_amd.ops.device_grower.DeviceGrower`); everything
-    else runs feature-parallel levels with load-balanced subtree finishing."""
+    """``strategy="auto"`` with replicated rows. GPU fits on the device-driven
+    loop use subtree ownership (replicated levels until the LPT switch level,
+    then each rank grows its own units:
+    :class:`~mpitree_amd.ops.device_grower.DeviceGrower`); exact thresholds on
+    continuous features run feature-parallel (``ops/exact_grower.py``); the
+    host-driven level-wise builder (CPU fits) runs feature-parallel levels with
+    load-balanced subtree finishing."""
 
     kind = "auto"
 

@@ -145,7 +145,9 @@ class LevelCheckpoint:
     def save_device(self, level: int, arrs: dict, rank: int = 0, world: int = 1) -> None:
         """Write the device loop's state after ``level`` (atomic per file)."""
         files = self._dev_files(rank, world)
-        dst = files[level % len(files)]
+        # alternate generations by save count, not level parity: with
+        # MPITREE_CKPT_EVERY even every save would land on one file
+        dst = files[self.saved_levels % len(files)]
         out = dict(arrs)
         out["sig"] = np.frombuffer(self.signature.encode(), np.uint8)
         out["level"] = np.array([level], np.int64)

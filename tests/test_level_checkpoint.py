@@ -175,3 +175,18 @@ def test_device_checkpoint_generations_agree(tmp_path):
     for r, ck in enumerate(cks):
         ck.clear()
     assert not [f for f in os.listdir(tmp_path) if f.startswith("m.npz")]
+
+
+def test_device_checkpoint_every_other_level_keeps_two_generations(tmp_path):
+    """MPITREE_CKPT_EVERY=2 saves levels 1, 3, 5 (one parity): the generations
+    alternate by save count, so the two newest levels are both on disk."""
+    path = str(tmp_path / "e.npz")
+    ck = LevelCheckpoint(path, "sig")
+    for lvl in (1, 3, 5):
+        ck.save_device(lvl, {"x": np.array([lvl])}, rank=0, world=2)
+    levels = set()
+    for g in (0, 1):
+        with np.load(f"{path}.r0of2.g{g}.npz", allow_pickle=False) as z:
+            levels.add(int(z["level"][0]))
+    assert levels == {3, 5}
+    ck.clear()
