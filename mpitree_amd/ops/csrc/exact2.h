@@ -27,7 +27,7 @@ struct XeArgs {
   uint32_t* D;         // other list buffer
   const int64_t* Y;    // regression payload [F_loc][n] (current), or null
   int64_t* DY;         // regression payload (other), or null
-  const uint32_t* rank_of;  // [F_loc][n] value rank of each row
+  const uint32_t* rank_of;  // (unused by the level kernels)
   const void* X;       // features [n][F] (fp32 or fp64): threshold values
   int x64;
   int64_t n;
@@ -96,20 +96,23 @@ void xe_flag(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_boun
 void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_bound,
                   int splits_bound);
 void xe_local_codes(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const int64_t* Y0,
-                    const int64_t* Y1, const uint32_t* rank_of, int64_t n, int F_loc, int f_lo,
-                    const int64_t* jobs, int J, int JW, uint8_t* codes_fm, uint32_t* ent,
-                    int64_t* yv);
+                    const int64_t* Y1, const void* X, int x64, int F, int fg_lo, int64_t n,
+                    int F_loc, int f_lo, const int64_t* jobs, int J, int JW, uint8_t* codes_fm,
+                    uint32_t* ent, int64_t* yv);
 void xe_codes_rm(hipStream_t s, const uint8_t* codes_fm, int64_t n, int F, int row_bytes,
                  const int64_t* jobs, int J, int JW, uint8_t* codes_rm);
-void xe_fix(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const uint32_t* rank_of,
-            const void* X, int x64, int F, int64_t n, int f_lo, int F_loc, const int64_t* jobs,
-            int J, int JW, int32_t* pos_rec, double* pos_thr, uint8_t* resolved);
+void xe_fix(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const void* X, int x64, int F,
+            int64_t n, int f_lo, int F_loc, const int64_t* jobs, int J, int JW, int32_t* pos_rec,
+            double* pos_thr);
+void xe_rank(hipStream_t s, int32_t* pos_rec, const double* pos_thr, int64_t P,
+             const uint32_t* root_rows, const uint32_t* rank_at, const void* X, int x64, int F,
+             int64_t n, int f_lo, int F_loc, uint8_t* resolved);
 void xe_resolved_pack(hipStream_t s, const int32_t* pos_rec, const double* pos_thr, int64_t P,
                       const int32_t* rank, int64_t* rows);
 void xe_resolved_scatter(hipStream_t s, const int64_t* rows, int64_t k, int32_t* pos_rec,
                          double* pos_thr);
 void xe_emit(hipStream_t s, const uint64_t* keys, const uint32_t* rows, int64_t n, int F_loc,
              int nc, int chunk, const int32_t* cbase, const int32_t* ylab, const int64_t* yfix,
-             uint32_t* E, int64_t* Y, uint32_t* rank_of);
+             uint32_t* E, int64_t* Y, uint32_t* rank_at);
 
 }  // namespace mt

@@ -10,9 +10,11 @@
 //
 //   E[f][p] = row | dup << 24 | label << 25          (rows < 2^24, labels < 128)
 //
-// (dup: the value occurs more than once in the column; the value rank then
-// comes from rank_of[f][row]) plus, for regression, the fixed-point target
-// Y[f][p] moved alongside. Node i owns positions [start_i, start_i + m_i) of
+// (dup: the value occurs more than once in the column; only then do two
+// neighbours' values need comparing, from X itself) plus, for regression, the
+// fixed-point target Y[f][p] moved alongside. Split thresholds are data values
+// X[row][f]; their value ranks (the threshold bins) are resolved once at the
+// end by a binary search in the setup's sorted order (xe_rank_kernel). Node i owns positions [start_i, start_i + m_i) of
 // every list. A level is a fixed chain of launches whose work counts are read
 // from device memory, with a one-workgroup planner -- the host never waits:
 //
@@ -37,6 +39,7 @@
 // Every quantity is an integer or the shared fp64 criterion, so trees equal the
 // host builders' bit for bit. Segments of at most 256 rows leave as finisher
 // jobs (the histogram finishers on subtree-local 8-bit codes, xe_local_codes).
+#include <algorithm>
 #include <climits>
 
 #include "common.h"
@@ -74,12 +77,23 @@ __device__ __forceinline__ double xe_dval(uint64_t k) {
 
 // ---------------------------------------------------------------------------
 // xe_tot: grid (items bound, F_loc); block (it, f) exits past the device count.
+__device__ void xe_tot_item(const XeArgs& a, const XeLists& L, int64_t it, int f,
+                            uint32_t* s_c, int64_t (*s_w)[3]);
+
+// Items are visited grid-stride (the grid is a bounded slice of the host's
+// item bound): a level with few items costs few empty workgroups.
 __global__ __launch_bounds__(kXeThreads) void xe_tot_kernel(XeArgs a, XeLists L) {
   __shared__ uint32_t s_c[kXeMaxC];
   __shared__ int64_t s_w[kXeWaves][3];
-  const int64_t it = blockIdx.x;
-  if (it >= L.ctl[1]) return;
-  const int f = blockIdx.y;
+  const int NI = L.ctl[1];
+  for (int64_t it = blockIdx.x; it < NI; it += gridDim.x) {
+    xe_tot_item(a, L, it, blockIdx.y, s_c, s_w);
+    __syncthreads();
+  }
+}
+
+__device__ void xe_tot_item(const XeArgs& a, const XeLists& L, int64_t it, int f,
+                            uint32_t* s_c, int64_t (*s_w)[3]) {
   const int64_t c0 = L.items[it * 4 + 2], cn = L.items[it * 4 + 3];
   const uint32_t* E = a.E + (int64_t)f * a.n + c0;
   const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
@@ -178,32 +192,54 @@ __global__ __launch_bounds__(kXeThreads) void xe_carry_kernel(XeArgs a, XeLists 
   }
 }
 
+// Feature value of a row (the input matrix, fp32 or fp64, row-major [n][F]).
+__device__ __forceinline__ double xe_x(const void* X, int x64, int F, uint32_t row, int fg) {
+  const int64_t o = (int64_t)row * F + fg;
+  return x64 ? reinterpret_cast<const double*>(X)[o]
+             : (double)reinterpret_cast<const float*>(X)[o];
+}
+
 // Value boundary between consecutive entries of a segment: equal values need
-// both entries flagged dup and equal ranks.
-__device__ __forceinline__ bool xe_boundary(uint32_t e, uint32_t nx, const uint32_t* __restrict__ rk) {
+// both entries flagged dup (a value that occurs more than once in the column)
+// and equal values (-0.0 == 0.0, as np.unique).
+__device__ __forceinline__ bool xe_boundary(uint32_t e, uint32_t nx, const XeArgs& a, int fg) {
   if (nx == 0xFFFFFFFFu || !xe_dup(e) || !xe_dup(nx)) return true;
-  return rk[xe_row(e)] != rk[xe_row(nx)];
+  return xe_x(a.X, a.x64, a.F, xe_row(e), fg) != xe_x(a.X, a.x64, a.F, xe_row(nx), fg);
 }
 
 // xe_scan: per (chunk, feature): the chunk's best {cost key, position}.
 // Classification keys are tie-rounded costs (criterion.h tie_round units) so
 // ties compare equal and the lowest position (smallest threshold) wins;
 // regression keys are the exact fp64 costs (the host builder's strict <).
+struct XeScanShared {
+  uint32_t cnt[kXePer * kXeWaves];
+  int64_t sum[kXePer * kXeWaves];
+  uint64_t min[kXeWaves][2];
+  uint32_t e[kXeThreads * kXePer + 1];
+};
+
+__device__ void xe_scan_item(const XeArgs& a, const XeLists& L, int64_t it, int f,
+                             XeScanShared& sh);
+
 __global__ __launch_bounds__(kXeThreads) void xe_scan_kernel(XeArgs a, XeLists L) {
-  __shared__ uint32_t s_cnt[kXePer * kXeWaves];
-  __shared__ uint32_t s_first[kXePer * kXeWaves];
-  __shared__ int64_t s_sum[kXePer * kXeWaves];
-  __shared__ uint64_t s_min[kXeWaves][2];
-  __shared__ float s_fmin[kXeWaves];
-  __shared__ uint32_t s_e[kXeThreads * kXePer + 1];
-  const int64_t it = blockIdx.x;
-  if (it >= L.ctl[1]) return;
-  const int f = blockIdx.y;
+  __shared__ XeScanShared sh;
+  const int NI = L.ctl[1];
+  for (int64_t it = blockIdx.x; it < NI; it += gridDim.x) {
+    xe_scan_item(a, L, it, blockIdx.y, sh);
+    __syncthreads();
+  }
+}
+
+__device__ void xe_scan_item(const XeArgs& a, const XeLists& L, int64_t it, int f,
+                             XeScanShared& sh) {
+  uint32_t* s_cnt = sh.cnt;
+  int64_t* s_sum = sh.sum;
+  uint64_t (*s_min)[2] = sh.min;
+  uint32_t* s_e = sh.e;
   const int64_t slot = L.items[it * 4 + 0], sstart = L.items[it * 4 + 1];
   const int64_t c0 = L.items[it * 4 + 2], cn = L.items[it * 4 + 3];
   const int64_t m = L.cnt[slot];
   const uint32_t* Ef = a.E + (int64_t)f * a.n;
-  const uint32_t* rk = a.rank_of + (int64_t)f * a.n;
   const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
   const unsigned long long lt = (1ull << lane) - 1ull;
   const int Cc = xe_cc(a.C);
@@ -225,7 +261,7 @@ __global__ __launch_bounds__(kXeThreads) void xe_scan_kernel(XeArgs a, XeLists L
     const int64_t pos = c0 + i - sstart;
     const int64_t ml = pos + 1, mr = m - ml;
     bool v = i < cn && mr > 0 && ml >= a.msl && mr >= a.msl;
-    if (v) v = xe_boundary(e[k], s_e[i + 1], rk);
+    if (v) v = xe_boundary(e[k], s_e[i + 1], a, a.f_lo + f);
     valid[k] = v;
   }
   unsigned long long mine = ~0ull;
@@ -317,41 +353,11 @@ __global__ __launch_bounds__(kXeThreads) void xe_scan_kernel(XeArgs a, XeLists L
         mine_pos = pos;
       }
     };
-    if (a.crit == kEntropy) {
-      // fp32 prefilter (hardware log2): |fp32 - exact| <= 2^-17.5 T(m) over the
-      // six terms and their sums; only positions within 2^-16 (T(m) + m) of the
-      // chunk's fp32 minimum are rescored exactly
-      float c32[kXePer];
-      float lmin = __builtin_inff();
+    // every count of the node is below the table size (xtab holds T(x) for
+    // x <= n): six sequential-ish table reads per position, no prefilter
 #pragma unroll
-      for (int k = 0; k < kXePer; ++k) {
-        const uint32_t ml = (uint32_t)(c0 + (int64_t)k * kXeThreads + tid - sstart + 1);
-        const uint32_t mr = (uint32_t)(m - ml);
-        const uint32_t L1 = (uint32_t)l1[k], L0 = ml - L1;
-        const uint32_t R1 = (uint32_t)t1 - L1, R0 = (uint32_t)t0 - L0;
-        auto t32 = [](uint32_t x) -> float {
-          const float xf = (float)x;
-          return x <= 1u ? 0.0f : xf * __log2f(xf);
-        };
-        const float c = (t32(ml) - (t32(L0) + t32(L1))) + (t32(mr) - (t32(R0) + t32(R1)));
-        c32[k] = valid[k] ? c : __builtin_inff();
-        lmin = fminf(lmin, c32[k]);
-      }
-      lmin = wave_min_f32_dpp(lmin);
-      if (lane == 0) s_fmin[wave] = lmin;
-      __syncthreads();
-      float bmin = s_fmin[0];
-#pragma unroll
-      for (int w = 1; w < kXeWaves; ++w) bmin = fminf(bmin, s_fmin[w]);
-      const float thr = bmin + (float)((tm + (double)m) * 0x1p-16);
-#pragma unroll
-      for (int k = 0; k < kXePer; ++k)
-        if (valid[k] && c32[k] <= thr) take(k);
-    } else {
-#pragma unroll
-      for (int k = 0; k < kXePer; ++k)
-        if (valid[k]) take(k);
-    }
+    for (int k = 0; k < kXePer; ++k)
+      if (valid[k]) take(k);
   } else {
     // ---- C > 2: per class, one block scan of the class indicator
     const double tm = xe_tl(m, a.xtab, a.xtab_n);
@@ -570,7 +576,7 @@ __global__ __launch_bounds__(kXeThreads) void xe_select_kernel(XeArgs a, XeLists
     out[2] = bp;
     out[3] = bp + 1;
     out[4] = m;
-    out[5] = (int64_t)a.rank_of[(int64_t)fl * a.n + row];
+    out[5] = -1;  // value rank: resolved after growth (xe_rank_kernel)
     out[6] = (int64_t)row;
   }
 }
@@ -685,7 +691,7 @@ __global__ __launch_bounds__(kXePlanThreads) void xe_plan_kernel(XePlanArgs a) {
         const int64_t row = r[6];
         const int64_t cpos[2] = {pos + 1, pos + 2 * nl};
         P[0] = feat;
-        P[1] = (int32_t)r[5];  // threshold value rank
+        P[1] = -2;  // threshold value rank: resolved after growth (xe_rank_kernel)
         P[2] = (int32_t)cpos[0];
         P[3] = (int32_t)cpos[1];
         // (+ 0.0: a -0.0 threshold prints as 0.0, as np.unique's representative)
@@ -798,28 +804,36 @@ __global__ __launch_bounds__(kXePlanThreads) void xe_plan_kernel(XePlanArgs a) {
 // gets a flag (one GPU: no clearing needed), else only the left rows get 1
 // (the flags were cleared and are summed over the ranks afterwards).
 __global__ __launch_bounds__(kXeThreads) void xe_flag_kernel(XeArgs a, XeLists cur, int write_right) {
-  const int64_t it = blockIdx.x;
-  if (it >= cur.ctl[3]) return;
-  const int64_t j = a.pitems[it * 4 + 0], s0 = a.pitems[it * 4 + 1];
-  const int64_t c0 = a.pitems[it * 4 + 2], cn = a.pitems[it * 4 + 3];
-  const int f = (int)a.split[j * 4 + 2] - a.f_lo;
-  if (f < 0 || f >= a.F_loc) return;
-  const int64_t nl = a.split[j * 4 + 3];
-  const uint32_t* Ef = a.E + (int64_t)f * a.n;
-  for (int64_t i = threadIdx.x; i < cn; i += kXeThreads) {
-    const int64_t p = c0 + i;
-    const bool left = (p - s0) < nl;
-    if (left || write_right) a.flag[xe_row(Ef[p])] = left ? 1 : 0;
+  const int NP = cur.ctl[3];
+  for (int64_t it = blockIdx.x; it < NP; it += gridDim.x) {
+    const int64_t j = a.pitems[it * 4 + 0], s0 = a.pitems[it * 4 + 1];
+    const int64_t c0 = a.pitems[it * 4 + 2], cn = a.pitems[it * 4 + 3];
+    const int f = (int)a.split[j * 4 + 2] - a.f_lo;
+    if (f < 0 || f >= a.F_loc) continue;
+    const int64_t nl = a.split[j * 4 + 3];
+    const uint32_t* Ef = a.E + (int64_t)f * a.n;
+    for (int64_t i = threadIdx.x; i < cn; i += kXeThreads) {
+      const int64_t p = c0 + i;
+      const bool left = (p - s0) < nl;
+      if (left || write_right) a.flag[xe_row(Ef[p])] = left ? 1 : 0;
+    }
   }
 }
 
 // Left entries of every (chunk, feature): flags gathered once, kept as one
 // 64-bit ballot per (step, wave) for the scatter.
+__device__ void xe_pcount_item(const XeArgs& a, int64_t it, int f, uint32_t* s_w);
+
 __global__ __launch_bounds__(kXeThreads) void xe_pcount_kernel(XeArgs a, XeLists cur) {
   __shared__ uint32_t s_w[kXeWaves];
-  const int64_t it = blockIdx.x;
-  if (it >= cur.ctl[3]) return;
-  const int f = blockIdx.y;
+  const int NP = cur.ctl[3];
+  for (int64_t it = blockIdx.x; it < NP; it += gridDim.x) {
+    xe_pcount_item(a, it, blockIdx.y, s_w);
+    __syncthreads();
+  }
+}
+
+__device__ void xe_pcount_item(const XeArgs& a, int64_t it, int f, uint32_t* s_w) {
   const int64_t c0 = a.pitems[it * 4 + 2], cn = a.pitems[it * 4 + 3];
   const uint32_t* Ef = a.E + (int64_t)f * a.n + c0;
   const int lane = lane_id(), w = threadIdx.x >> 6;
@@ -864,11 +878,18 @@ __global__ __launch_bounds__(kXeThreads) void xe_pcarry_kernel(XeArgs a, XeLists
   }
 }
 
+__device__ void xe_pscatter_item(const XeArgs& a, int64_t it, int f, uint32_t* s_cnt);
+
 __global__ __launch_bounds__(kXeThreads) void xe_pscatter_kernel(XeArgs a, XeLists cur) {
   __shared__ uint32_t s_cnt[kXePer * kXeWaves];
-  const int64_t it = blockIdx.x;
-  if (it >= cur.ctl[3]) return;
-  const int f = blockIdx.y;
+  const int NP = cur.ctl[3];
+  for (int64_t it = blockIdx.x; it < NP; it += gridDim.x) {
+    xe_pscatter_item(a, it, blockIdx.y, s_cnt);
+    __syncthreads();
+  }
+}
+
+__device__ void xe_pscatter_item(const XeArgs& a, int64_t it, int f, uint32_t* s_cnt) {
   const int64_t j = a.pitems[it * 4 + 0], s0 = a.pitems[it * 4 + 1];
   const int64_t c0 = a.pitems[it * 4 + 2], cn = a.pitems[it * 4 + 3];
   const uint32_t* Ef = a.E + (int64_t)f * a.n;
@@ -951,8 +972,8 @@ __global__ void xe_init_kernel(XeLists L, int64_t n, int Cs, const int64_t* __re
 // jobs: int64 [J][W] = {start, rows, depth, position, list buffer, ...}
 __global__ __launch_bounds__(kXeLocalMax) void xe_local_codes_kernel(
     const uint32_t* __restrict__ E0, const uint32_t* __restrict__ E1,
-    const int64_t* __restrict__ Y0, const int64_t* __restrict__ Y1,
-    const uint32_t* __restrict__ rank_of, int64_t n, int F_loc, int f_lo,
+    const int64_t* __restrict__ Y0, const int64_t* __restrict__ Y1, const void* __restrict__ X,
+    int x64, int F, int fg_lo, int64_t n, int F_loc, int f_lo,
     const int64_t* __restrict__ jobs, int JW, uint8_t* __restrict__ codes_fm,
     uint32_t* __restrict__ ent, int64_t* __restrict__ yv) {
   __shared__ uint32_t s_row[kXeLocalMax];
@@ -1009,7 +1030,7 @@ __global__ __launch_bounds__(kXeLocalMax) void xe_local_codes_kernel(
     if (t > 0 && t < m) {
       const uint32_t pe = s_e[t - 1];
       start = !(xe_dup(e) && xe_dup(pe)) ||
-              rank_of[(int64_t)f * n + xe_row(e)] != rank_of[(int64_t)f * n + xe_row(pe)];
+              xe_x(X, x64, F, xe_row(e), fg_lo + f) != xe_x(X, x64, F, xe_row(pe), fg_lo + f);
     }
     uint32_t b = (t < m && start) ? (uint32_t)t : 0u;
 #pragma unroll
@@ -1047,9 +1068,9 @@ __global__ __launch_bounds__(256) void xe_codes_rm_kernel(const uint8_t* __restr
 // exchange packs what this rank resolved (resolved[p] = 1).
 __global__ __launch_bounds__(256) void xe_fix_kernel(
     const uint32_t* __restrict__ E0, const uint32_t* __restrict__ E1,
-    const uint32_t* __restrict__ rank_of, const void* __restrict__ X, int x64, int F, int64_t n,
+    const void* __restrict__ X, int x64, int F, int64_t n,
     int f_lo, int F_loc, const int64_t* __restrict__ jobs, int JW, int32_t* __restrict__ pos_rec,
-    double* __restrict__ pos_thr, uint8_t* __restrict__ resolved) {
+    double* __restrict__ pos_thr) {
   const int64_t* J = jobs + (int64_t)blockIdx.x * JW;
   const int64_t s = J[0], m = J[1], pos = J[3];
   const uint32_t* E = J[4] ? E1 : E0;
@@ -1059,12 +1080,36 @@ __global__ __launch_bounds__(256) void xe_fix_kernel(
     const int f = R[0] - f_lo;
     if (f < 0 || f >= F_loc) continue;
     const uint32_t row = xe_row(E[(int64_t)f * n + s + R[1]]);
-    R[1] = (int32_t)rank_of[(int64_t)f * n + row];
-    pos_thr[p] = (x64 ? reinterpret_cast<const double*>(X)[(int64_t)row * F + R[0]]
-                      : (double)reinterpret_cast<const float*>(X)[(int64_t)row * F + R[0]]) +
-                 0.0;
-    if (resolved) resolved[p] = 1;
+    R[1] = -2;  // value rank: xe_rank_kernel
+    pos_thr[p] = xe_x(X, x64, F, row, R[0]) + 0.0;
   }
+}
+
+// Threshold bins of every split node whose feature is this rank's: the value
+// rank of the threshold = the rank at the first position of the feature's
+// setup-sorted order whose value is >= the threshold (binary search; rows and
+// ranks by sorted position were kept from the setup). resolved[p] = 1 marks
+// what this rank resolved (the feature-parallel exchange packs those).
+__global__ __launch_bounds__(256) void xe_rank_kernel(
+    int32_t* __restrict__ pos_rec, const double* __restrict__ pos_thr, int64_t P,
+    const uint32_t* __restrict__ root_rows, const uint32_t* __restrict__ rank_at,
+    const void* __restrict__ X, int x64, int F, int64_t n, int f_lo, int F_loc,
+    uint8_t* __restrict__ resolved) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  int32_t* R = pos_rec + p * 6;
+  if (R[5] <= 0 || R[0] < 0) return;
+  const int f = R[0] - f_lo;
+  if (f < 0 || f >= F_loc) return;
+  const double thr = pos_thr[p];
+  const uint32_t* rows = root_rows + (int64_t)f * n;
+  int64_t lo = 0, hi = n;  // first sorted position with value >= thr
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (xe_x(X, x64, F, rows[mid], R[0]) < thr) lo = mid + 1; else hi = mid;
+  }
+  R[1] = (int32_t)rank_at[(int64_t)f * n + lo];
+  if (resolved) resolved[p] = 1;
 }
 
 // Pack / scatter {position, bin, threshold bits} of the positions a rank resolved
@@ -1094,7 +1139,7 @@ __global__ __launch_bounds__(256) void xe_resolved_scatter_kernel(const int64_t*
 
 // ---------------------------------------------------------------------------
 // Setup: sorted keys {feature : 32 | value bits : 32} with row ids (exact_setup.hip
-// sort) -> entries, value ranks per row, duplicate flags. cbase: per-(feature,
+// sort) -> entries, value ranks by sorted position, duplicate flags. cbase: per-(feature,
 // chunk) first rank (exact_setup's count / scan of value changes).
 __global__ __launch_bounds__(256) void xe_emit_kernel(const uint64_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ rows, int64_t n,
@@ -1104,7 +1149,7 @@ __global__ __launch_bounds__(256) void xe_emit_kernel(const uint64_t* __restrict
                                                       const int64_t* __restrict__ yfix,
                                                       uint32_t* __restrict__ E,
                                                       int64_t* __restrict__ Y,
-                                                      uint32_t* __restrict__ rank_of) {
+                                                      uint32_t* __restrict__ rank_at) {
   const int f = blockIdx.y, c = blockIdx.x;
   const int64_t base = (int64_t)f * n;
   const int64_t p0 = (int64_t)c * chunk;
@@ -1132,7 +1177,7 @@ __global__ __launch_bounds__(256) void xe_emit_kernel(const uint64_t* __restrict
       const uint32_t lab = ylab ? (uint32_t)ylab[row] : 0u;
       E[base + p] = row | ((uint32_t)dup << 24) | (lab << 25);
       if (Y) Y[base + p] = yfix[row];
-      rank_of[base + row] = (uint32_t)rank;
+      rank_at[base + p] = (uint32_t)rank;
     }
     __syncthreads();
     if (threadIdx.x == 255) s_carry = off + (int32_t)incl;
@@ -1153,15 +1198,23 @@ void xe_init(hipStream_t s, const XeLists& L, int64_t n, int Cs, const int64_t* 
 
 // the scan / select half of a level (grids are host bounds; blocks past the
 // device counts exit)
+// x extent of the (items, features) grids: items are visited grid-stride, so a
+// level's grid is a bounded slice (~16k workgroups) whatever its item bound
+static int xe_gx(int items_bound, int F_loc) {
+  const int cap = std::max(4, 16384 / std::max(1, F_loc));
+  return std::max(1, std::min(items_bound, cap));
+}
+
 void xe_level_scan(hipStream_t s, const XeArgs& a, const XeLists& cur, int items_bound,
                    int slots_bound) {
   if (items_bound <= 0 || slots_bound <= 0) return;
   const int Cc = xe_cc(a.C);
-  hipLaunchKernelGGL(xe_tot_kernel, dim3(items_bound, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
+  const int gx = xe_gx(items_bound, a.F_loc);
+  hipLaunchKernelGGL(xe_tot_kernel, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
   const int64_t nc = (int64_t)slots_bound * a.F_loc * Cc;
   hipLaunchKernelGGL(xe_carry_kernel, dim3((unsigned)((nc + kXeThreads - 1) / kXeThreads)),
                      dim3(kXeThreads), 0, s, a, cur);
-  hipLaunchKernelGGL(xe_scan_kernel, dim3(items_bound, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
+  hipLaunchKernelGGL(xe_scan_kernel, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
   hipLaunchKernelGGL(xe_select_kernel, dim3(slots_bound), dim3(kXeThreads), 0, s, a, cur);
   MT_HIP_CHECK(hipGetLastError());
 }
@@ -1173,31 +1226,30 @@ void xe_plan(hipStream_t s, const XePlanArgs& p) {
 
 void xe_flag(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_bound, int write_right) {
   if (pitems_bound <= 0) return;
-  hipLaunchKernelGGL(xe_flag_kernel, dim3(pitems_bound), dim3(kXeThreads), 0, s, a, cur,
-                     write_right);
+  hipLaunchKernelGGL(xe_flag_kernel, dim3(std::min(pitems_bound, 4096)), dim3(kXeThreads), 0, s, a,
+                     cur, write_right);
   MT_HIP_CHECK(hipGetLastError());
 }
 
 void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_bound,
                   int splits_bound) {
   if (pitems_bound <= 0 || splits_bound <= 0) return;
-  hipLaunchKernelGGL(xe_pcount_kernel, dim3(pitems_bound, a.F_loc), dim3(kXeThreads), 0, s, a,
-                     cur);
+  const int gx = xe_gx(pitems_bound, a.F_loc);
+  hipLaunchKernelGGL(xe_pcount_kernel, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
   const int64_t ns = (int64_t)splits_bound * a.F_loc;
   hipLaunchKernelGGL(xe_pcarry_kernel, dim3((unsigned)((ns + kXeThreads - 1) / kXeThreads)),
                      dim3(kXeThreads), 0, s, a, cur);
-  hipLaunchKernelGGL(xe_pscatter_kernel, dim3(pitems_bound, a.F_loc), dim3(kXeThreads), 0, s, a,
-                     cur);
+  hipLaunchKernelGGL(xe_pscatter_kernel, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
   MT_HIP_CHECK(hipGetLastError());
 }
 
 void xe_local_codes(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const int64_t* Y0,
-                    const int64_t* Y1, const uint32_t* rank_of, int64_t n, int F_loc, int f_lo,
-                    const int64_t* jobs, int J, int JW, uint8_t* codes_fm, uint32_t* ent,
-                    int64_t* yv) {
+                    const int64_t* Y1, const void* X, int x64, int F, int fg_lo, int64_t n,
+                    int F_loc, int f_lo, const int64_t* jobs, int J, int JW, uint8_t* codes_fm,
+                    uint32_t* ent, int64_t* yv) {
   if (J <= 0) return;
-  hipLaunchKernelGGL(xe_local_codes_kernel, dim3(J), dim3(kXeLocalMax), 0, s, E0, E1, Y0, Y1,
-                     rank_of, n, F_loc, f_lo, jobs, JW, codes_fm, ent, yv);
+  hipLaunchKernelGGL(xe_local_codes_kernel, dim3(J), dim3(kXeLocalMax), 0, s, E0, E1, Y0, Y1, X,
+                     x64, F, fg_lo, n, F_loc, f_lo, jobs, JW, codes_fm, ent, yv);
   MT_HIP_CHECK(hipGetLastError());
 }
 
@@ -1209,12 +1261,22 @@ void xe_codes_rm(hipStream_t s, const uint8_t* codes_fm, int64_t n, int F, int r
   MT_HIP_CHECK(hipGetLastError());
 }
 
-void xe_fix(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const uint32_t* rank_of,
-            const void* X, int x64, int F, int64_t n, int f_lo, int F_loc, const int64_t* jobs,
-            int J, int JW, int32_t* pos_rec, double* pos_thr, uint8_t* resolved) {
+void xe_fix(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const void* X, int x64, int F,
+            int64_t n, int f_lo, int F_loc, const int64_t* jobs, int J, int JW, int32_t* pos_rec,
+            double* pos_thr) {
   if (J <= 0) return;
-  hipLaunchKernelGGL(xe_fix_kernel, dim3(J), dim3(256), 0, s, E0, E1, rank_of, X, x64, F, n, f_lo,
-                     F_loc, jobs, JW, pos_rec, pos_thr, resolved);
+  hipLaunchKernelGGL(xe_fix_kernel, dim3(J), dim3(256), 0, s, E0, E1, X, x64, F, n, f_lo, F_loc,
+                     jobs, JW, pos_rec, pos_thr);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void xe_rank(hipStream_t s, int32_t* pos_rec, const double* pos_thr, int64_t P,
+             const uint32_t* root_rows, const uint32_t* rank_at, const void* X, int x64, int F,
+             int64_t n, int f_lo, int F_loc, uint8_t* resolved) {
+  const int64_t b = (P + 255) / 256;
+  if (b == 0) return;
+  hipLaunchKernelGGL(xe_rank_kernel, dim3((unsigned)b), dim3(256), 0, s, pos_rec, pos_thr, P,
+                     root_rows, rank_at, X, x64, F, n, f_lo, F_loc, resolved);
   MT_HIP_CHECK(hipGetLastError());
 }
 
@@ -1237,10 +1299,10 @@ void xe_resolved_scatter(hipStream_t s, const int64_t* rows, int64_t k, int32_t*
 
 void xe_emit(hipStream_t s, const uint64_t* keys, const uint32_t* rows, int64_t n, int F_loc,
              int nc, int chunk, const int32_t* cbase, const int32_t* ylab, const int64_t* yfix,
-             uint32_t* E, int64_t* Y, uint32_t* rank_of) {
+             uint32_t* E, int64_t* Y, uint32_t* rank_at) {
   if (n <= 0 || F_loc <= 0) return;
   hipLaunchKernelGGL(xe_emit_kernel, dim3(nc, F_loc), dim3(256), 0, s, keys, rows, n, nc, chunk,
-                     cbase, ylab, yfix, E, Y, rank_of);
+                     cbase, ylab, yfix, E, Y, rank_at);
   MT_HIP_CHECK(hipGetLastError());
 }
 

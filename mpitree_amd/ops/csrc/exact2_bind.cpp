@@ -75,7 +75,7 @@ void bind_exact2(py::module_& m) {
         c.Yb[0] = ptr<int64_t>(u("Y0"));
         c.Yb[1] = ptr<int64_t>(u("Y1"));
         XeArgs& a = c.a;
-        a.rank_of = ptr<uint32_t>(u("rank_of"));
+        a.rank_of = nullptr;
         a.X = ptr<void>(u("X"));
         a.x64 = (int)g("x64");
         a.n = g("n");
@@ -143,23 +143,30 @@ void bind_exact2(py::module_& m) {
       });
 
   m.def("xe_local_codes", [](uintptr_t s, uintptr_t E0, uintptr_t E1, uintptr_t Y0, uintptr_t Y1,
-                             uintptr_t rank_of, int64_t n, int F_loc, int f_lo, uintptr_t jobs,
-                             int J, int JW, uintptr_t codes_fm, uintptr_t ent, uintptr_t yv) {
+                             uintptr_t X, int x64, int F, int fg_lo, int64_t n, int F_loc,
+                             int f_lo, uintptr_t jobs, int J, int JW, uintptr_t codes_fm,
+                             uintptr_t ent, uintptr_t yv) {
     xe_local_codes(stream_of(s), ptr<uint32_t>(E0), ptr<uint32_t>(E1), ptr<int64_t>(Y0),
-                   ptr<int64_t>(Y1), ptr<uint32_t>(rank_of), n, F_loc, f_lo, ptr<int64_t>(jobs), J,
-                   JW, ptr<uint8_t>(codes_fm), ptr<uint32_t>(ent), ptr<int64_t>(yv));
+                   ptr<int64_t>(Y1), ptr<void>(X), x64, F, fg_lo, n, F_loc, f_lo,
+                   ptr<int64_t>(jobs), J, JW, ptr<uint8_t>(codes_fm), ptr<uint32_t>(ent),
+                   ptr<int64_t>(yv));
   });
   m.def("xe_codes_rm", [](uintptr_t s, uintptr_t codes_fm, int64_t n, int F, int row_bytes,
                           uintptr_t jobs, int J, int JW, uintptr_t codes_rm) {
     xe_codes_rm(stream_of(s), ptr<uint8_t>(codes_fm), n, F, row_bytes, ptr<int64_t>(jobs), J, JW,
                 ptr<uint8_t>(codes_rm));
   });
-  m.def("xe_fix", [](uintptr_t s, uintptr_t E0, uintptr_t E1, uintptr_t rank_of, uintptr_t X,
-                     int x64, int F, int64_t n, int f_lo, int F_loc, uintptr_t jobs, int J, int JW,
-                     uintptr_t pos_rec, uintptr_t pos_thr, uintptr_t resolved) {
-    xe_fix(stream_of(s), ptr<uint32_t>(E0), ptr<uint32_t>(E1), ptr<uint32_t>(rank_of),
-           ptr<void>(X), x64, F, n, f_lo, F_loc, ptr<int64_t>(jobs), J, JW, ptr<int32_t>(pos_rec),
-           ptr<double>(pos_thr), ptr<uint8_t>(resolved));
+  m.def("xe_fix", [](uintptr_t s, uintptr_t E0, uintptr_t E1, uintptr_t X, int x64, int F,
+                     int64_t n, int f_lo, int F_loc, uintptr_t jobs, int J, int JW,
+                     uintptr_t pos_rec, uintptr_t pos_thr) {
+    xe_fix(stream_of(s), ptr<uint32_t>(E0), ptr<uint32_t>(E1), ptr<void>(X), x64, F, n, f_lo,
+           F_loc, ptr<int64_t>(jobs), J, JW, ptr<int32_t>(pos_rec), ptr<double>(pos_thr));
+  });
+  m.def("xe_rank", [](uintptr_t s, uintptr_t pos_rec, uintptr_t pos_thr, int64_t P,
+                      uintptr_t root_rows, uintptr_t rank_at, uintptr_t X, int x64, int F,
+                      int64_t n, int f_lo, int F_loc, uintptr_t resolved) {
+    xe_rank(stream_of(s), ptr<int32_t>(pos_rec), ptr<double>(pos_thr), P, ptr<uint32_t>(root_rows),
+            ptr<uint32_t>(rank_at), ptr<void>(X), x64, F, n, f_lo, F_loc, ptr<uint8_t>(resolved));
   });
   m.def("xe_resolved_pack", [](uintptr_t s, uintptr_t pos_rec, uintptr_t pos_thr, int64_t P,
                                uintptr_t rank, uintptr_t rows) {
@@ -173,10 +180,10 @@ void bind_exact2(py::module_& m) {
   });
   m.def("xe_emit", [](uintptr_t s, uintptr_t keys, uintptr_t rows, int64_t n, int F_loc, int nc,
                       int chunk, uintptr_t cbase, uintptr_t ylab, uintptr_t yfix, uintptr_t E,
-                      uintptr_t Y, uintptr_t rank_of) {
+                      uintptr_t Y, uintptr_t rank_at) {
     xe_emit(stream_of(s), ptr<uint64_t>(keys), ptr<uint32_t>(rows), n, F_loc, nc, chunk,
             ptr<int32_t>(cbase), ptr<int32_t>(ylab), ptr<int64_t>(yfix), ptr<uint32_t>(E),
-            ptr<int64_t>(Y), ptr<uint32_t>(rank_of));
+            ptr<int64_t>(Y), ptr<uint32_t>(rank_at));
   });
 }
 

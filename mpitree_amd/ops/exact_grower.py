@@ -76,7 +76,9 @@ class ExactGrower:
 
     # ------------------------------------------------------------- setup
     def _setup(self, Xd, F, f_lo, F_loc, y32, yfix, reg):
-        """Sorted lists of this rank's features: E0 (+ Y0), rank_of."""
+        """Sorted lists of this rank's features: E0 (+ Y0); the setup's sorted
+        rows and value ranks by sorted position (threshold bins, resolved once
+        after growth)."""
         dev = Xd.device
         n = Xd.shape[0]
         hip = self.hip
@@ -84,7 +86,7 @@ class ExactGrower:
         E = [torch.empty((F_loc, n), dtype=torch.int32, device=dev) for _ in range(2)]
         Y = [torch.empty((F_loc, n), dtype=torch.int64, device=dev) for _ in range(2)] if reg \
             else [None, None]
-        rank_of = torch.empty((F_loc, n), dtype=torch.int32, device=dev)
+        rank_at = torch.empty((F_loc, n), dtype=torch.int32, device=dev)
         ylab = 0 if reg else y32.data_ptr()
         yf = yfix.data_ptr() if reg else 0
         if Xd.dtype == torch.float32:
@@ -102,7 +104,8 @@ class ExactGrower:
                                  xs=F, f_lo=f_lo)
             hip.xe_emit(s, keys[1].data_ptr(), rows[1].data_ptr(), n, F_loc, nc, chunk,
                         cnt.data_ptr(), ylab, yf, E[0].data_ptr(),
-                        Y[0].data_ptr() if reg else 0, rank_of.data_ptr())
+                        Y[0].data_ptr() if reg else 0, rank_at.data_ptr())
+            root_rows = rows[1]
             del keys, rows, temp, cnt, nuniq  # (stream-ordered frees)
         else:  # fp64: per-feature stable sorts (ties by row id, -0.0 == 0.0)
             xt = Xd[:, f_lo:f_lo + F_loc].t().contiguous()
@@ -119,11 +122,12 @@ class ExactGrower:
             if not reg:
                 ent = ent | (y32[order].to(torch.int32) << 25)
             E[0].copy_(ent)
-            rank_of.scatter_(1, order, rank)
+            rank_at.copy_(rank)
+            root_rows = o32
             if reg:
                 Y[0].copy_(yfix[order])
-            del vals, order, new, nxt_same, dup, rank, o32, ent
-        return E, Y, rank_of
+            del vals, order, new, nxt_same, dup, rank, ent
+        return E, Y, (root_rows, rank_at)
 
     # --------------------------------------------------------------- fit
     def fit(self, Xd: torch.Tensor, y_codes: torch.Tensor, root, C: int, crit: Criterion,
@@ -160,7 +164,7 @@ class ExactGrower:
         s = hb._stream
         y32 = None if reg else y_codes.to(torch.int32).contiguous()
         yfix = y_codes.to(torch.int64).contiguous() if reg else None
-        E, Y, rank_of = self._setup(Xd, F, f_lo, F_loc, y32, yfix, reg)
+        E, Y, ranks = self._setup(Xd, F, f_lo, F_loc, y32, yfix, reg)
         if timings is not None:
             timings["exact_setup"] = time.perf_counter() - t0
 
@@ -169,7 +173,7 @@ class ExactGrower:
         be.n, be.F, be.C = n, F, (2 if reg else int(C))
         be.reg = reg
         be.crit = crit
-        be.xtab = hb.xlog2x_table(dev)
+        be.xtab = hb.xlog2x_table(dev, n + 2)  # every count of a node is a table read
         be.xtabf = hb.xlog2x_table_f32(dev)
         be.begin_positions(2 * n - 1)
         pos_thr = hb._workspace(dev, "xe.thr", (2 * n - 1) * 8)[: (2 * n - 1) * 8].view(
@@ -239,9 +243,10 @@ class ExactGrower:
         ctx = hip.XeCtx(dict(
             E0=E[0].data_ptr(), E1=E[1].data_ptr(),
             Y0=Y[0].data_ptr() if reg else 0, Y1=Y[1].data_ptr() if reg else 0,
-            rank_of=rank_of.data_ptr(), X=Xd.data_ptr(), x64=int(Xd.dtype == torch.float64),
+            rank_of=0, X=Xd.data_ptr(), x64=int(Xd.dtype == torch.float64),
             n=n, F=F, f_lo=f_lo, F_loc=F_loc, C=Cx, crit=int(crit), msl=msl,
-            xtab=be.xtab.data_ptr(), xtab_n=hb.XTAB_N, tot=ptr["tot"], carry=ptr["carry"],
+            xtab=be.xtab.data_ptr(), xtab_n=int(be.xtab.numel()), tot=ptr["tot"],
+            carry=ptr["carry"],
             cmm=ptr["cmm"], cbest=ptr["cbest"], rec=ptr["rec"], split=ptr["split"],
             pitems=ptr["pitems"], pfirst=ptr["pfirst"], flag=ptr["flag"], lc=ptr["lc"],
             lcar=ptr["lcar"], bits=ptr["bits"], pos_rec=be.pos_rec.data_ptr(),
@@ -249,7 +254,7 @@ class ExactGrower:
             job_count=ptr["job_count"], max_depth=md, mss=mss, fr=fr), lp[0], lp[1])
         ws["root"].copy_(torch.from_numpy(np.ascontiguousarray(root_stats, np.int64)))
         ctx.init(s(), ws["root"].data_ptr())
-        self._keep = (ctx, E, Y, rank_of)
+        self._keep = (ctx, E, Y, ranks)
 
         # ---- level loop: enqueue only; a lagged host-mapped slot tells the end
         hctl_dev, hctl = _host_ctl(hip, dev)
@@ -296,8 +301,9 @@ class ExactGrower:
             timings["levels"] = time.perf_counter() - t1
         t2 = time.perf_counter()
         if J:
-            self._finish(ws, be, E, Y, rank_of, Xd, J, JW, F, f_lo, F_loc, blocks, n, Cx, reg,
-                         crit, pos_thr, P, rank)
+            self._finish(ws, be, E, Y, Xd, J, JW, F, f_lo, F_loc, blocks, n, reg, pos_thr, P,
+                         rank)
+        self._resolve_bins(be, ranks, Xd, F, f_lo, F_loc, n, pos_thr, P)
         if P > 1:
             self.stats["comm_bytes_per_level"] = comm_bytes
             self.stats["mode"] = "feature"
@@ -312,8 +318,40 @@ class ExactGrower:
         return ta
 
     # --------------------------------------------------------- finisher
-    def _finish(self, ws, be, E, Y, rank_of, Xd, J, JW, F, f_lo, F_loc, blocks, n, Cx, reg,
-                crit, pos_thr, P, rank):
+    def _resolve_bins(self, be, ranks, Xd, F, f_lo, F_loc, n, pos_thr, P):
+        """Threshold bins (value ranks) of every split node: each rank resolves
+        the nodes split on its own features (binary search in the setup's
+        sorted order); feature-parallel ranks then exchange {position, bin,
+        threshold} of what they resolved."""
+        hip, comm = self.hip, self.comm
+        s = hb._stream
+        dev = Xd.device
+        Pp = int(be.pos_rec.shape[0])
+        root_rows, rank_at = ranks
+        x64 = int(Xd.dtype == torch.float64)
+        resolved = torch.zeros(Pp, dtype=torch.uint8, device=dev) if P > 1 else None
+        hip.xe_rank(s(), be.pos_rec.data_ptr(), pos_thr.data_ptr(), Pp, root_rows.data_ptr(),
+                    rank_at.data_ptr(), Xd.data_ptr(), x64, F, n, f_lo, F_loc,
+                    0 if resolved is None else resolved.data_ptr())
+        if P == 1:
+            return
+        tiles = int(hip.asm_tiles(Pp))
+        tile = torch.empty(max(tiles, 1), dtype=torch.int32, device=dev)
+        total = torch.zeros(2, dtype=torch.int64, device=dev)
+        rk = torch.empty(Pp, dtype=torch.int32, device=dev)
+        hip.asm_rank(s(), be.pos_rec.data_ptr(), Pp, tile.data_ptr(), total.data_ptr(),
+                     rk.data_ptr(), mask=resolved.data_ptr())
+        k = int(total[0].item())
+        rows = torch.empty((max(k, 1), 3), dtype=torch.int64, device=dev)
+        hip.xe_resolved_pack(s(), be.pos_rec.data_ptr(), pos_thr.data_ptr(), Pp,
+                             rk.data_ptr(), rows.data_ptr())
+        allr = comm.all_gather_rows(rows[:k])
+        hip.xe_resolved_scatter(s(), allr.data_ptr(), int(allr.shape[0]),
+                                be.pos_rec.data_ptr(), pos_thr.data_ptr())
+        self._keep_r = (allr, rows, resolved, tile, total, rk)
+
+    def _finish(self, ws, be, E, Y, Xd, J, JW, F, f_lo, F_loc, blocks, n, reg, pos_thr, P,
+                rank):
         """Grow the <= 256-row job segments on subtree-local codes; turn the
         finisher's codes back into value ranks and thresholds."""
         hip, comm = self.hip, self.comm
@@ -339,9 +377,10 @@ class ExactGrower:
                         else None),
             )
         fm_out = loc["blk"] if P > 1 else loc["fm"]
+        x64 = int(Xd.dtype == torch.float64)
         hip.xe_local_codes(s(), E[0].data_ptr(), E[1].data_ptr(),
                            Y[0].data_ptr() if reg else 0, Y[1].data_ptr() if reg else 0,
-                           rank_of.data_ptr(), n, F_loc, 0, jobs.data_ptr(), J, JW,
+                           Xd.data_ptr(), x64, F, f_lo, n, F_loc, 0, jobs.data_ptr(), J, JW,
                            fm_out.data_ptr(), loc["ent"].data_ptr(),
                            loc["yv"].data_ptr() if reg else 0)
         if P > 1:  # every rank's feature block of the codes -> all features on every rank
@@ -369,32 +408,13 @@ class ExactGrower:
         Jm = int(fj.shape[0])
         if Jm:
             be.launch_finisher(fj, Jm, n, self.p, be.pos_rec, be.pos_st)
-        if P > 1:  # finished job ranges -> every rank; then the thresholds each rank resolves
+        if P > 1:  # finished job ranges -> every rank
             rg = torch.stack([fj[:, 3], fj[:, 3] + 2 * fj[:, 1] - 1], 1).contiguous()
             if rg.shape[0] == 0:
                 rg = torch.zeros((1, 2), dtype=torch.int64, device=dev)
             self._keep_x = exchange_ranges(be, comm, rg, int(2 * fj[:, 1].sum().item()) + 16)
-            Pp = int(be.pos_rec.shape[0])
-            resolved = torch.zeros(Pp, dtype=torch.uint8, device=dev)
-            hip.xe_fix(s(), E[0].data_ptr(), E[1].data_ptr(), rank_of.data_ptr(), Xd.data_ptr(),
-                       int(Xd.dtype == torch.float64), F, n, f_lo, F_loc, jobs.data_ptr(), J, JW,
-                       be.pos_rec.data_ptr(), pos_thr.data_ptr(), resolved.data_ptr())
-            tiles = int(hip.asm_tiles(Pp))
-            tile = torch.empty(max(tiles, 1), dtype=torch.int32, device=dev)
-            total = torch.zeros(2, dtype=torch.int64, device=dev)
-            rk = torch.empty(Pp, dtype=torch.int32, device=dev)
-            hip.asm_rank(s(), be.pos_rec.data_ptr(), Pp, tile.data_ptr(), total.data_ptr(),
-                         rk.data_ptr(), mask=resolved.data_ptr())
-            k = int(total[0].item())
-            rows = torch.empty((max(k, 1), 3), dtype=torch.int64, device=dev)
-            hip.xe_resolved_pack(s(), be.pos_rec.data_ptr(), pos_thr.data_ptr(), Pp,
-                                 rk.data_ptr(), rows.data_ptr())
-            allr = comm.all_gather_rows(rows[:k])
-            hip.xe_resolved_scatter(s(), allr.data_ptr(), int(allr.shape[0]),
-                                    be.pos_rec.data_ptr(), pos_thr.data_ptr())
-            self._keep_r = (allr, rows, resolved)
-        else:
-            hip.xe_fix(s(), E[0].data_ptr(), E[1].data_ptr(), rank_of.data_ptr(), Xd.data_ptr(),
-                       int(Xd.dtype == torch.float64), F, n, f_lo, F_loc, jobs.data_ptr(), J, JW,
-                       be.pos_rec.data_ptr(), pos_thr.data_ptr(), 0)
+        # finisher split codes -> threshold values (this rank's features; the bins
+        # follow in _resolve_bins)
+        hip.xe_fix(s(), E[0].data_ptr(), E[1].data_ptr(), Xd.data_ptr(), x64, F, n, f_lo, F_loc,
+                   jobs.data_ptr(), J, JW, be.pos_rec.data_ptr(), pos_thr.data_ptr())
         self._keep_f = (loc, fj)

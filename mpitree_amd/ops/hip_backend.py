@@ -285,15 +285,23 @@ XTAB_N = 1 << 16
 _xtab_cache: dict = {}
 
 
-def xlog2x_table(device) -> torch.Tensor:
-    """Device table of x*log2(x) for x < 2^16, built once per device by the same
-    device function the kernels would otherwise evaluate (identical bits)."""
+def xlog2x_table(device, min_n: int = XTAB_N) -> torch.Tensor:
+    """Device table of x*log2(x) for x < max(2^16, min_n), built by the same
+    device function the kernels would otherwise evaluate (identical bits) and
+    kept per device; a request for more entries rebuilds it larger (powers of
+    two). Kernels bound their lookups by the xtab_n they are given, so a larger
+    table serves every caller (the exact engine asks for n + 1 entries: every
+    count of a node is a table read)."""
     key = str(device)
     t = _xtab_cache.get(key)
-    if t is None:
-        t = torch.empty(XTAB_N, dtype=torch.float64, device=device)
-        native.hip().xlog2x_device(_stream(), t.data_ptr(), XTAB_N)
+    if t is None or t.numel() < min_n:
+        size = XTAB_N
+        while size < min_n:
+            size *= 2
+        t = torch.empty(size, dtype=torch.float64, device=device)
+        native.hip().xlog2x_device(_stream(), t.data_ptr(), size)
         _xtab_cache[key] = t
+        _xtab_cache.pop("f32:" + key, None)
     return t
 
 
@@ -372,7 +380,7 @@ def xlog2x_table_f32(device) -> torch.Tensor:
     key = "f32:" + str(device)
     t = _xtab_cache.get(key)
     if t is None:
-        t = xlog2x_table(device).float()
+        t = xlog2x_table(device)[:XTAB_N].float()
         _xtab_cache[key] = t
     return t
 
