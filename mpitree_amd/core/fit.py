@@ -232,11 +232,11 @@ def _exact_device_ok(n, F, C, regression) -> bool:
 
     if os.environ.get("MPITREE_EXACT_V1") == "1" or not exact_supported(n, C, regression):
         return False
-    if F > 256:
+    if F > 256:  # (the v2 engine's local-code finisher rows are at most 256 bytes)
         return False
     if regression:
         return True
-    return C <= 16 and native.hip().finish_lds_bytes(F, 256, C) <= 150 * 1024
+    return native.hip().finish_feature_tile(F, 256, C) > 0
 
 
 def _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t_bin, t_start, F, regression):

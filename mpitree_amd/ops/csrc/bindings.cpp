@@ -46,6 +46,7 @@ void launch_finish(hipStream_t, const void*, int64_t, const void*, int, int64_t,
                    int32_t*, int32_t*, int64_t*, int32_t*, int32_t, int, int, int, int64_t*, int,
                    int64_t*);
 int finish_lds_bytes(int F, int B, int C);
+int finish_feature_tile(int F, int B, int C);
 int asm_tiles(int64_t P);
 void launch_grow_plan(hipStream_t, const PlanArgs&);
 void ex_scan_level(hipStream_t, const uint64_t*, int64_t, const int64_t*, int, const int64_t*,
@@ -187,6 +188,7 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("row_elems"), py::arg("codes_fm"), py::arg("cb"), py::arg("bad"),
       py::arg("estride") = 0);
   m.def("finish_lds_bytes", &mt::finish_lds_bytes);
+  m.def("finish_feature_tile", &mt::finish_feature_tile);
   m.def("finish", [](uintptr_t s, uintptr_t codes_rm, int64_t row_words, uintptr_t codes_fm,
                      int cb, int64_t n_rows, uintptr_t idx, uintptr_t tmp, uintptr_t y,
                      int lab_shift, uintptr_t jobs, int J, uintptr_t counter, uintptr_t nbins,

@@ -47,10 +47,13 @@ struct XeArgs {
   int64_t* split;      // [SMAX][4] {start, count, feature (global), n_left}
   int64_t* pitems;     // [PMAX][4] {split j, segment start, chunk start, chunk count}
   int32_t* pfirst;     // [SMAX + 1]
-  uint8_t* flag;       // [n]
-  int32_t* lc;         // [PMAX][F_loc]
-  int32_t* lcar;       // [PMAX][F_loc]
-  unsigned long long* bits;  // [PMAX][F_loc][kXePer * kXeWaves]
+  uint32_t* flag;      // [(n + 31) / 32] row-direction bits (1: left)
+  // single-pass scans (decoupled look-back): per (item, feature) status words
+  // {tag : 30, state : 2 (1 aggregate, 2 inclusive prefix), value : 32}
+  uint64_t* sstat;     // [IMAX][F_loc] class-1 counts (two-class split scan)
+  uint64_t* pstat;     // [PMAX][F_loc] left counts (partition)
+  int32_t* tick;       // [4] {scan ticket, partition ticket, watchdog, -}
+  uint32_t tag;        // this level's status tag (30 bits, nonzero)
 };
 
 __host__ __device__ inline int xe_cc(int C) { return C > 0 ? C : 1; }
@@ -80,12 +83,12 @@ struct XePlanArgs {
   int64_t mss, msl, fr;
   int32_t* host_ctl;   // host-mapped {next frontier size, jobs so far, tag}
   int32_t host_tag;
+  int32_t* tick;       // XeArgs::tick: the planner rearms both tickets
 };
 
 
 // launchers (exact2.hip)
 int xe_chunk();
-int xe_bits_words();
 int xe_local_max();
 int xe_max_classes();
 void xe_init(hipStream_t s, const XeLists& L, int64_t n, int Cs, const int64_t* root, int32_t* jc);

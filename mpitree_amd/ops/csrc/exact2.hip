@@ -41,6 +41,7 @@
 // jobs (the histogram finishers on subtree-local 8-bit codes, xe_local_codes).
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "common.h"
 #include "criterion.h"
@@ -76,8 +77,58 @@ __device__ __forceinline__ double xe_dval(uint64_t k) {
 }
 
 // ---------------------------------------------------------------------------
+// Decoupled look-back: single-pass segmented prefix sums over chunk items.
+//
+// Work is claimed through an atomic ticket t -> (item t / F_loc, feature
+// t % F_loc), so an item's predecessors in its segment hold smaller tickets:
+// running (or finished) workgroups, which publish their chunk's aggregate
+// before they look back themselves. The smallest unfinished ticket never
+// waits, so the grid always drains. Status words are relaxed agent-scope
+// atomics -- the value travels inside the word, nothing else needs ordering --
+// tagged per level, so they are never cleared.
+constexpr uint64_t kXeAgg = 1, kXeIncl = 2;
+
+
+__device__ __forceinline__ void xe_publish(uint64_t* w, uint32_t tag, uint64_t state, uint32_t v) {
+  __hip_atomic_store(w, ((uint64_t)tag << 34) | (state << 32) | (uint64_t)v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Exclusive prefix of chunk q >= 1 of a segment whose status words are
+// st[-stride], ..., st[-q stride] (nearest first). Called by one whole wave:
+// lane 0 walks back, adding aggregates until the nearest inclusive prefix
+// (predecessors claimed just before this chunk, so the walk is short); every
+// lane returns the prefix. A wait beyond 2 s (a bug, never a schedule) sets
+// *watch and returns instead of hanging the GPU.
+__device__ __forceinline__ int64_t xe_lookback(const uint64_t* st, int64_t stride, int64_t q, uint32_t tag,
+                               int32_t* watch) {
+  int64_t acc = 0;
+  if (lane_id() == 0) {
+    const uint64_t t0 = wall_clock64();
+    bool dead = false;
+    for (int64_t d = 1; d <= q && !dead; ++d) {
+      uint64_t s;
+      for (uint32_t spins = 0;; ++spins) {
+        s = __hip_atomic_load(st - d * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(s >> 34) == tag) break;
+        if ((spins & 63u) == 63u && wall_clock64() - t0 > 200000000ull) {
+          atomicExch(watch, 1);
+          dead = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (dead) break;
+      acc += (int64_t)(uint32_t)s;
+      if (((s >> 32) & 3ull) == kXeIncl) break;
+    }
+  }
+  return (int64_t)__shfl((long long)acc, 0, kWave);
+}
+
+// ---------------------------------------------------------------------------
 // xe_tot: grid (items bound, F_loc); block (it, f) exits past the device count.
-__device__ void xe_tot_item(const XeArgs& a, const XeLists& L, int64_t it, int f,
+__device__ __forceinline__ void xe_tot_item(const XeArgs& a, const XeLists& L, int64_t it, int f,
                             uint32_t* s_c, int64_t (*s_w)[3]);
 
 // Items are visited grid-stride (the grid is a bounded slice of the host's
@@ -92,7 +143,7 @@ __global__ __launch_bounds__(kXeThreads) void xe_tot_kernel(XeArgs a, XeLists L)
   }
 }
 
-__device__ void xe_tot_item(const XeArgs& a, const XeLists& L, int64_t it, int f,
+__device__ __forceinline__ void xe_tot_item(const XeArgs& a, const XeLists& L, int64_t it, int f,
                             uint32_t* s_c, int64_t (*s_w)[3]) {
   const int64_t c0 = L.items[it * 4 + 2], cn = L.items[it * 4 + 3];
   const uint32_t* E = a.E + (int64_t)f * a.n + c0;
@@ -215,23 +266,51 @@ struct XeScanShared {
   uint32_t cnt[kXePer * kXeWaves];
   int64_t sum[kXePer * kXeWaves];
   uint64_t min[kXeWaves][2];
+  float fmin[kXeWaves];
+  uint32_t total;
+  int64_t prefix;
   uint32_t e[kXeThreads * kXePer + 1];
 };
 
-__device__ void xe_scan_item(const XeArgs& a, const XeLists& L, int64_t it, int f,
-                             XeScanShared& sh);
+// kKind: the problem kind compiled into the item (0 regression, 1 two classes,
+// 2 more classes) -- each kernel carries one path only, which keeps the
+// scan's register (and scalar-register) footprint to what that path needs.
+template <int kKind>
+__device__ __forceinline__ void xe_scan_item(const XeArgs& a, const XeLists& L, int64_t it, int f,
+                                             XeScanShared& sh, bool lb);
 
+template <int kKind>
 __global__ __launch_bounds__(kXeThreads) void xe_scan_kernel(XeArgs a, XeLists L) {
   __shared__ XeScanShared sh;
   const int NI = L.ctl[1];
   for (int64_t it = blockIdx.x; it < NI; it += gridDim.x) {
-    xe_scan_item(a, L, it, blockIdx.y, sh);
+    xe_scan_item<kKind>(a, L, it, blockIdx.y, sh, false);
     __syncthreads();
   }
 }
 
-__device__ void xe_scan_item(const XeArgs& a, const XeLists& L, int64_t it, int f,
-                             XeScanShared& sh) {
+// Two classes: the class-1 carry of every chunk comes from a decoupled
+// look-back inside the scan (no xe_tot / xe_carry pass over the lists); the
+// chunk's carries are stored for xe_select as the two-pass path would.
+__global__ __launch_bounds__(kXeThreads) void xe_scan_lb_kernel(XeArgs a, XeLists L) {
+  __shared__ XeScanShared sh;
+  __shared__ int s_t;
+  const int64_t total = (int64_t)L.ctl[1] * a.F_loc;
+  for (;;) {
+    if (threadIdx.x == 0) s_t = atomicAdd(a.tick, 1);
+    __syncthreads();
+    // the ticket is uniform: read it into scalar registers so every branch and
+    // loop derived from it compiles as wave-uniform (scalar) control flow
+    const int64_t t = (int64_t)__builtin_amdgcn_readfirstlane((int)s_t);
+    __syncthreads();  // (every thread has read the ticket before the next claim)
+    if (t >= total) break;
+    xe_scan_item<1>(a, L, t / a.F_loc, (int)(t % a.F_loc), sh, true);
+  }
+}
+
+template <int kKind>
+__device__ __forceinline__ void xe_scan_item(const XeArgs& a, const XeLists& L, int64_t it, int f,
+                                             XeScanShared& sh, bool lb) {
   uint32_t* s_cnt = sh.cnt;
   int64_t* s_sum = sh.sum;
   uint64_t (*s_min)[2] = sh.min;
@@ -266,7 +345,7 @@ __device__ void xe_scan_item(const XeArgs& a, const XeLists& L, int64_t it, int 
   }
   unsigned long long mine = ~0ull;
   uint64_t mine_pos = ~0ull;
-  if (a.C == 0) {
+  if constexpr (kKind == 0) {
     // ---- regression: prefix sums of the targets, exact fp64 costs
     const int64_t* Yp = a.Y + (int64_t)f * a.n;
     int64_t y[kXePer];
@@ -305,7 +384,7 @@ __device__ void xe_scan_item(const XeArgs& a, const XeLists& L, int64_t it, int 
         mine_pos = (uint64_t)pos;
       }
     }
-  } else if (a.C <= 2) {
+  } else if constexpr (kKind == 1) {
     // ---- two classes: one ballot scan of class 1 gives every side count
     unsigned long long bal[kXePer];
 #pragma unroll
@@ -319,9 +398,33 @@ __device__ void xe_scan_item(const XeArgs& a, const XeLists& L, int64_t it, int 
       const uint32_t v = tid < kXePer * kXeWaves ? s_cnt[tid] : 0u;
       const uint32_t incl = wave_incl_scan_dpp(v);
       if (tid < kXePer * kXeWaves) s_cnt[tid] = incl - v;
+      if (tid == kXePer * kXeWaves - 1) sh.total = incl;
     }
     __syncthreads();
-    const int64_t base1 = a.C == 2 ? a.carry[(it * a.F_loc + f) * Cc + 1] : 0;
+    int64_t base1;
+    if (lb) {
+      if (wave == 0) {
+        const int64_t q = (c0 - sstart) / kXeChunk;  // chunk index within the segment
+        uint64_t* st = a.sstat + it * a.F_loc + f;
+        const uint32_t T1 = sh.total;
+        if (lane == 0) xe_publish(st, a.tag, q == 0 ? kXeIncl : kXeAgg, T1);
+        int64_t pre = 0;
+        if (q > 0) {
+          pre = xe_lookback(st, a.F_loc, q, a.tag, a.tick + 2);
+          if (lane == 0) xe_publish(st, a.tag, kXeIncl, (uint32_t)(pre + T1));
+        }
+        if (lane == 0) {
+          sh.prefix = pre;
+          int64_t* car = a.carry + (it * a.F_loc + f) * Cc;  // xe_select's chunk carries
+          car[0] = (c0 - sstart) - pre;
+          if (a.C == 2) car[1] = pre;
+        }
+      }
+      __syncthreads();
+      base1 = a.C == 2 ? sh.prefix : 0;
+    } else {
+      base1 = a.C == 2 ? a.carry[(it * a.F_loc + f) * Cc + 1] : 0;
+    }
     const int64_t t0 = L.stats[slot * Cc + 0], t1 = a.C == 2 ? L.stats[slot * Cc + 1] : 0;
     int64_t l1[kXePer];
 #pragma unroll
@@ -353,11 +456,44 @@ __device__ void xe_scan_item(const XeArgs& a, const XeLists& L, int64_t it, int 
         mine_pos = pos;
       }
     };
-    // every count of the node is below the table size (xtab holds T(x) for
-    // x <= n): six sequential-ish table reads per position, no prefilter
+    if (a.crit == kEntropy) {
+      // Pass 1: fp32 costs from the hardware log2 (no table reads). Each term
+      // T(x) <= T(m) carries <= 1.25 * 2^-22 relative error (log2f <= 2 ulp,
+      // one rounded product) and the five sums <= 2^-24 T(m) each, so
+      // |fp32 - exact| <= 2^-18.8 T(m). The chunk's exact best (tie-rounded,
+      // then lowest position) has an fp32 cost <= the chunk's fp32 minimum +
+      // 2^-17.8 T(m) + the tie grid (2^-31 T(m)): pass 2 scores in fp64 (six
+      // table reads) only positions within 2^-15 T(m) of the fp32 minimum.
+      auto t32 = [](int64_t x) -> float {
+        const float f = (float)x;  // counts < 2^24: exact
+        return x > 1 ? f * log2f(f) : 0.0f;
+      };
+      float c32[kXePer];
+      float fm = __builtin_inff();
 #pragma unroll
-    for (int k = 0; k < kXePer; ++k)
-      if (valid[k]) take(k);
+      for (int k = 0; k < kXePer; ++k) {
+        c32[k] = __builtin_inff();
+        if (!valid[k]) continue;
+        const int64_t ml = c0 + (int64_t)k * kXeThreads + tid - sstart + 1, mr = m - ml;
+        const int64_t L1 = l1[k], L0 = ml - L1, R1 = t1 - L1, R0 = t0 - L0;
+        c32[k] = (t32(ml) - (t32(L0) + t32(L1))) + (t32(mr) - (t32(R0) + t32(R1)));
+        fm = fminf(fm, c32[k]);
+      }
+      fm = wave_min_f32_dpp(fm);
+      if (lane == 0) sh.fmin[wave] = fm;
+      __syncthreads();
+      fm = sh.fmin[0];
+#pragma unroll
+      for (int w = 1; w < kXeWaves; ++w) fm = fminf(fm, sh.fmin[w]);
+      const float thr = fm + (float)tm * 0x1p-15f;
+#pragma unroll
+      for (int k = 0; k < kXePer; ++k)
+        if (valid[k] && c32[k] <= thr) take(k);
+    } else {  // gini: exact integer-form costs are a few flops
+#pragma unroll
+      for (int k = 0; k < kXePer; ++k)
+        if (valid[k]) take(k);
+    }
   } else {
     // ---- C > 2: per class, one block scan of the class indicator
     const double tm = xe_tl(m, a.xtab, a.xtab_n);
@@ -787,6 +923,8 @@ __global__ __launch_bounds__(kXePlanThreads) void xe_plan_kernel(XePlanArgs a) {
     a.cur.ctl[3] = NP;
     const int jobs_so_far = atomicAdd(a.job_count, 0);
     a.nxt.ctl[4] = jobs_so_far;
+    a.tick[0] = 0;  // the next level's scan and this level's partition claim from 0
+    a.tick[1] = 0;
     if (a.host_ctl) {
       __hip_atomic_store(a.host_ctl + 1, jobs_so_far, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(a.host_ctl, K2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -799,10 +937,12 @@ __global__ __launch_bounds__(kXePlanThreads) void xe_plan_kernel(XePlanArgs a) {
 // ---------------------------------------------------------------------------
 // Partition of the level's split segments.
 // xe_flag: grid (partition items bound); rows of split j in the split feature's
-// list: flag 1 for the first n_left positions. Only the feature's owner (f in
-// [f_lo, f_lo + F_loc)) writes; with zero_rest every entry of a split segment
-// gets a flag (one GPU: no clearing needed), else only the left rows get 1
-// (the flags were cleared and are summed over the ranks afterwards).
+// list: bit 1 for the first n_left positions. Only the feature's owner (f in
+// [f_lo, f_lo + F_loc)) writes; with write_right every entry of a split segment
+// sets or clears its bit (one GPU: no clearing needed), else only the left rows
+// set theirs (the words were zeroed; the ranks' bits are disjoint -- one owner
+// per row -- so an integer-sum all-reduce ORs them). One bit per row keeps the
+// partition's random gathers in a 128 KB (n = 1M) array: L2-resident per XCD.
 __global__ __launch_bounds__(kXeThreads) void xe_flag_kernel(XeArgs a, XeLists cur, int write_right) {
   const int NP = cur.ctl[3];
   for (int64_t it = blockIdx.x; it < NP; it += gridDim.x) {
@@ -815,120 +955,96 @@ __global__ __launch_bounds__(kXeThreads) void xe_flag_kernel(XeArgs a, XeLists c
     for (int64_t i = threadIdx.x; i < cn; i += kXeThreads) {
       const int64_t p = c0 + i;
       const bool left = (p - s0) < nl;
-      if (left || write_right) a.flag[xe_row(Ef[p])] = left ? 1 : 0;
+      const uint32_t r = xe_row(Ef[p]);
+      if (left)
+        atomicOr(a.flag + (r >> 5), 1u << (r & 31));
+      else if (write_right)
+        atomicAnd(a.flag + (r >> 5), ~(1u << (r & 31)));
     }
   }
 }
 
-// Left entries of every (chunk, feature): flags gathered once, kept as one
-// 64-bit ballot per (step, wave) for the scatter.
-__device__ void xe_pcount_item(const XeArgs& a, int64_t it, int f, uint32_t* s_w);
+// xe_part: stable partition of every (split chunk, feature): the chunk's left
+// rows (flag bits gathered once), their exclusive prefix over the split's
+// earlier chunks by decoupled look-back, then the scatter -- left rows to the
+// segment's front, right rows after the split's n_left, both in list order.
+struct XePartShared {
+  uint32_t cnt[kXePer * kXeWaves];
+  uint32_t total;
+  int64_t prefix;
+};
 
-__global__ __launch_bounds__(kXeThreads) void xe_pcount_kernel(XeArgs a, XeLists cur) {
-  __shared__ uint32_t s_w[kXeWaves];
-  const int NP = cur.ctl[3];
-  for (int64_t it = blockIdx.x; it < NP; it += gridDim.x) {
-    xe_pcount_item(a, it, blockIdx.y, s_w);
-    __syncthreads();
-  }
-}
-
-__device__ void xe_pcount_item(const XeArgs& a, int64_t it, int f, uint32_t* s_w) {
-  const int64_t c0 = a.pitems[it * 4 + 2], cn = a.pitems[it * 4 + 3];
-  const uint32_t* Ef = a.E + (int64_t)f * a.n + c0;
-  const int lane = lane_id(), w = threadIdx.x >> 6;
-  uint32_t e[kXePer];
-#pragma unroll
-  for (int k = 0; k < kXePer; ++k) {
-    const int64_t i = (int64_t)k * kXeThreads + threadIdx.x;
-    e[k] = i < cn ? Ef[i] : 0xFFFFFFFFu;
-  }
-  uint32_t v = 0;
-  unsigned long long* B = a.bits + (it * a.F_loc + f) * (int64_t)(kXePer * kXeWaves);
-#pragma unroll
-  for (int k = 0; k < kXePer; ++k) {
-    const int64_t i = (int64_t)k * kXeThreads + threadIdx.x;
-    const unsigned long long b = __ballot(i < cn && a.flag[xe_row(e[k])] != 0);
-    if (lane == 0) {
-      B[k * kXeWaves + w] = b;
-      v += (uint32_t)__popcll(b);
-    }
-  }
-  if (lane == 0) s_w[w] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t total = 0;
-    for (int q = 0; q < kXeWaves; ++q) total += s_w[q];
-    a.lc[it * a.F_loc + f] = (int32_t)total;
-  }
-}
-
-// One thread per (split, feature): exclusive prefix of the chunk left counts.
-__global__ __launch_bounds__(kXeThreads) void xe_pcarry_kernel(XeArgs a, XeLists cur) {
-  const int S = cur.ctl[2];
-  const int64_t g = (int64_t)blockIdx.x * kXeThreads + threadIdx.x;
-  if (g >= (int64_t)S * a.F_loc) return;
-  const int f = (int)(g % a.F_loc);
-  const int64_t j = g / a.F_loc;
-  const int p0 = a.pfirst[j], p1 = a.pfirst[j + 1];
-  int32_t acc = 0;
-  for (int it = p0; it < p1; ++it) {
-    a.lcar[(int64_t)it * a.F_loc + f] = acc;
-    acc += a.lc[(int64_t)it * a.F_loc + f];
-  }
-}
-
-__device__ void xe_pscatter_item(const XeArgs& a, int64_t it, int f, uint32_t* s_cnt);
-
-__global__ __launch_bounds__(kXeThreads) void xe_pscatter_kernel(XeArgs a, XeLists cur) {
-  __shared__ uint32_t s_cnt[kXePer * kXeWaves];
-  const int NP = cur.ctl[3];
-  for (int64_t it = blockIdx.x; it < NP; it += gridDim.x) {
-    xe_pscatter_item(a, it, blockIdx.y, s_cnt);
-    __syncthreads();
-  }
-}
-
-__device__ void xe_pscatter_item(const XeArgs& a, int64_t it, int f, uint32_t* s_cnt) {
+__device__ __forceinline__ void xe_part_item(const XeArgs& a, int64_t it, int f, XePartShared& sh) {
   const int64_t j = a.pitems[it * 4 + 0], s0 = a.pitems[it * 4 + 1];
   const int64_t c0 = a.pitems[it * 4 + 2], cn = a.pitems[it * 4 + 3];
   const uint32_t* Ef = a.E + (int64_t)f * a.n;
   uint32_t* O = a.D + (int64_t)f * a.n;
-  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const unsigned long long lt = (1ull << lane) - 1ull;
+  const bool reg = a.C == 0;
   uint32_t e[kXePer];
   int64_t y[kXePer];
-  const bool reg = a.C == 0;
 #pragma unroll
   for (int k = 0; k < kXePer; ++k) {
-    const int64_t i = (int64_t)k * kXeThreads + threadIdx.x;
+    const int64_t i = (int64_t)k * kXeThreads + tid;
     e[k] = i < cn ? Ef[c0 + i] : 0xFFFFFFFFu;
     y[k] = (reg && i < cn) ? a.Y[(int64_t)f * a.n + c0 + i] : 0;
   }
-  const unsigned long long* Bt = a.bits + (it * a.F_loc + f) * (int64_t)(kXePer * kXeWaves);
   unsigned long long bal[kXePer];
 #pragma unroll
   for (int k = 0; k < kXePer; ++k) {
-    bal[k] = Bt[k * kXeWaves + w];
-    if (lane == 0) s_cnt[k * kXeWaves + w] = (uint32_t)__popcll(bal[k]);
+    const int64_t i = (int64_t)k * kXeThreads + tid;
+    const uint32_t r = xe_row(e[k]);
+    bal[k] = __ballot(i < cn && ((a.flag[r >> 5] >> (r & 31)) & 1u));
+    if (lane == 0) sh.cnt[k * kXeWaves + w] = (uint32_t)__popcll(bal[k]);
   }
   __syncthreads();
-  if (threadIdx.x < kWave) {
-    const uint32_t v = threadIdx.x < kXePer * kXeWaves ? s_cnt[threadIdx.x] : 0u;
+  if (tid < kWave) {
+    const uint32_t v = tid < kXePer * kXeWaves ? sh.cnt[tid] : 0u;
     const uint32_t incl = wave_incl_scan_dpp(v);
-    if (threadIdx.x < kXePer * kXeWaves) s_cnt[threadIdx.x] = incl - v;
+    if (tid < kXePer * kXeWaves) sh.cnt[tid] = incl - v;
+    if (tid == kXePer * kXeWaves - 1) sh.total = incl;
   }
   __syncthreads();
-  const int64_t lb = (int64_t)a.lcar[it * a.F_loc + f];
+  if (w == 0) {
+    const int64_t q = (c0 - s0) / kXeChunk;  // chunk index within the split's segment
+    uint64_t* st = a.pstat + it * a.F_loc + f;
+    const uint32_t T = sh.total;
+    if (lane == 0) xe_publish(st, a.tag, q == 0 ? kXeIncl : kXeAgg, T);
+    int64_t pre = 0;
+    if (q > 0) {
+      pre = xe_lookback(st, a.F_loc, q, a.tag, a.tick + 2);
+      if (lane == 0) xe_publish(st, a.tag, kXeIncl, (uint32_t)(pre + T));
+    }
+    if (lane == 0) sh.prefix = pre;
+  }
+  __syncthreads();
+  const int64_t lb = sh.prefix;
   const int64_t nlj = a.split[j * 4 + 3];
 #pragma unroll
   for (int k = 0; k < kXePer; ++k) {
-    const int64_t i = (int64_t)k * kXeThreads + threadIdx.x;
+    const int64_t i = (int64_t)k * kXeThreads + tid;
     if (i >= cn) break;
-    const int64_t l = lb + s_cnt[k * kXeWaves + w] + __popcll(bal[k] & lt);
+    const int64_t l = lb + sh.cnt[k * kXeWaves + w] + __popcll(bal[k] & lt);
     const int64_t dst = ((bal[k] >> lane) & 1ull) ? s0 + l : s0 + nlj + (c0 + i - s0) - l;
     O[dst] = e[k];
     if (reg) a.DY[(int64_t)f * a.n + dst] = y[k];
+  }
+}
+
+__global__ __launch_bounds__(kXeThreads) void xe_part_kernel(XeArgs a, XeLists cur) {
+  __shared__ XePartShared sh;
+  __shared__ int s_t;
+  const int64_t total = (int64_t)cur.ctl[3] * a.F_loc;
+  for (;;) {
+    if (threadIdx.x == 0) s_t = atomicAdd(a.tick + 1, 1);
+    __syncthreads();
+    // the ticket is uniform: read it into scalar registers so every branch and
+    // loop derived from it compiles as wave-uniform (scalar) control flow
+    const int64_t t = (int64_t)__builtin_amdgcn_readfirstlane((int)s_t);
+    __syncthreads();  // (every thread has read the ticket before the next claim)
+    if (t >= total) break;
+    xe_part_item(a, t / a.F_loc, (int)(t % a.F_loc), sh);
   }
 }
 
@@ -1187,7 +1303,6 @@ __global__ __launch_bounds__(256) void xe_emit_kernel(const uint64_t* __restrict
 
 // --------------------------------------------------------------- launchers
 int xe_chunk() { return kXeChunk; }
-int xe_bits_words() { return kXePer * kXeWaves; }
 int xe_local_max() { return kXeLocalMax; }
 int xe_max_classes() { return kXeMaxC; }
 
@@ -1205,16 +1320,39 @@ static int xe_gx(int items_bound, int F_loc) {
   return std::max(1, std::min(items_bound, cap));
 }
 
+// Workgroups of a ticketed kernel: enough to fill the chip (8 per CU), never
+// more than the (item, feature) pairs.
+static int xe_ticket_grid(int items_bound, int F_loc) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)items_bound * F_loc, 2048));
+}
+
 void xe_level_scan(hipStream_t s, const XeArgs& a, const XeLists& cur, int items_bound,
                    int slots_bound) {
   if (items_bound <= 0 || slots_bound <= 0) return;
   const int Cc = xe_cc(a.C);
-  const int gx = xe_gx(items_bound, a.F_loc);
-  hipLaunchKernelGGL(xe_tot_kernel, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
-  const int64_t nc = (int64_t)slots_bound * a.F_loc * Cc;
-  hipLaunchKernelGGL(xe_carry_kernel, dim3((unsigned)((nc + kXeThreads - 1) / kXeThreads)),
-                     dim3(kXeThreads), 0, s, a, cur);
-  hipLaunchKernelGGL(xe_scan_kernel, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
+  // MPITREE_EXACT_SCAN_LB=1: the single-pass two-class scan (ticketed chunks,
+  // look-back carries; experimental -- see profiles/kernel_experiments.md).
+  // Default: chunk totals, carries, then the scan.
+  static const bool lb = [] {
+    const char* v = std::getenv("MPITREE_EXACT_SCAN_LB");
+    return v && v[0] == '1';
+  }();
+  if ((a.C == 1 || a.C == 2) && lb) {
+    hipLaunchKernelGGL(xe_scan_lb_kernel, dim3(xe_ticket_grid(items_bound, a.F_loc)),
+                       dim3(kXeThreads), 0, s, a, cur);
+  } else {
+    const int gx = xe_gx(items_bound, a.F_loc);
+    hipLaunchKernelGGL(xe_tot_kernel, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
+    const int64_t nc = (int64_t)slots_bound * a.F_loc * Cc;
+    hipLaunchKernelGGL(xe_carry_kernel, dim3((unsigned)((nc + kXeThreads - 1) / kXeThreads)),
+                       dim3(kXeThreads), 0, s, a, cur);
+    if (a.C == 0)
+      hipLaunchKernelGGL(xe_scan_kernel<0>, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
+    else if (a.C <= 2)
+      hipLaunchKernelGGL(xe_scan_kernel<1>, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
+    else
+      hipLaunchKernelGGL(xe_scan_kernel<2>, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
+  }
   hipLaunchKernelGGL(xe_select_kernel, dim3(slots_bound), dim3(kXeThreads), 0, s, a, cur);
   MT_HIP_CHECK(hipGetLastError());
 }
@@ -1234,12 +1372,8 @@ void xe_flag(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_boun
 void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_bound,
                   int splits_bound) {
   if (pitems_bound <= 0 || splits_bound <= 0) return;
-  const int gx = xe_gx(pitems_bound, a.F_loc);
-  hipLaunchKernelGGL(xe_pcount_kernel, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
-  const int64_t ns = (int64_t)splits_bound * a.F_loc;
-  hipLaunchKernelGGL(xe_pcarry_kernel, dim3((unsigned)((ns + kXeThreads - 1) / kXeThreads)),
+  hipLaunchKernelGGL(xe_part_kernel, dim3(xe_ticket_grid(pitems_bound, a.F_loc)),
                      dim3(kXeThreads), 0, s, a, cur);
-  hipLaunchKernelGGL(xe_pscatter_kernel, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
   MT_HIP_CHECK(hipGetLastError());
 }
 

@@ -27,10 +27,12 @@ struct XeCtx {
   uint32_t* Eb[2]{};
   int64_t* Yb[2]{};
   XePlanArgs p{};
+  uint32_t seq = 1;  // fit sequence number: look-back status tags differ per (fit, level)
 
   XeArgs args(int lvl) const {
     XeArgs x = a;
     const int c = lvl & 1;
+    x.tag = (uint32_t)((((uint64_t)seq << 12) + (uint64_t)(lvl & 4095)) % 0x3FFFFFFFull) + 1u;
     x.E = Eb[c];
     x.D = Eb[c ^ 1];
     x.Y = Yb[c];
@@ -58,7 +60,6 @@ XeLists lists_of(const py::dict& d) {
 
 void bind_exact2(py::module_& m) {
   m.def("xe_chunk", &xe_chunk);
-  m.def("xe_bits_words", &xe_bits_words);
   m.def("xe_local_max", &xe_local_max);
   m.def("xe_max_classes", &xe_max_classes);
   m.def("xe_rec_width", [](int C) { return xe_rec_width(C); });
@@ -95,10 +96,11 @@ void bind_exact2(py::module_& m) {
         a.split = ptr<int64_t>(u("split"));
         a.pitems = ptr<int64_t>(u("pitems"));
         a.pfirst = ptr<int32_t>(u("pfirst"));
-        a.flag = ptr<uint8_t>(u("flag"));
-        a.lc = ptr<int32_t>(u("lc"));
-        a.lcar = ptr<int32_t>(u("lcar"));
-        a.bits = ptr<unsigned long long>(u("bits"));
+        a.flag = ptr<uint32_t>(u("flag"));
+        a.sstat = ptr<uint64_t>(u("sstat"));
+        a.pstat = ptr<uint64_t>(u("pstat"));
+        a.tick = ptr<int32_t>(u("tick"));
+        a.tag = 1;
         XePlanArgs& p = c.p;
         p.rec = a.rec;
         p.split = a.split;
@@ -117,8 +119,10 @@ void bind_exact2(py::module_& m) {
         p.mss = g("mss");
         p.msl = g("msl");
         p.fr = g("fr");
+        p.tick = a.tick;
         return c;
       }))
+      .def("begin", [](XeCtx& c, int64_t seq) { c.seq = (uint32_t)seq; })
       .def("init", [](XeCtx& c, uintptr_t s, uintptr_t root) {
         xe_init(stream_of(s), c.L[0], c.a.n, c.a.C > 0 ? c.a.C : 2, ptr<int64_t>(root),
                 c.p.job_count);

@@ -42,7 +42,9 @@ constexpr int kFinThreadsWide = 1024;  // one workgroup per CU (F = 128 histogra
 // job_counter word layout: kFinCtr* in grow.h (int32 [kFinCounterWords], zeroed
 // before each launch)
 constexpr int kFinStack = 40;    // >= log2(max job rows) + 2
-constexpr int kFinMaxC = 16;     // classes supported by the finisher
+constexpr int kFinMaxC = 256;    // classes supported by the block finisher
+constexpr int kFinStackC = 16;   // C <= this: DFS-stack class counts in LDS, else global scratch
+constexpr int kTinyMaxC = 16;    // classes supported by the generic tiny kernel
 constexpr int kFinTab = 1024;    // LDS x*log2(x) entries
 // MT_FIN_UNROLL / MT_FIN_PAIR / MT_TINY_SMALL: compile-time overrides for variant
 // builds (tools/build_variant.sh, measured in profiles/kernel_experiments.md)
@@ -56,7 +58,7 @@ constexpr int kFinTab = 1024;    // LDS x*log2(x) entries
 #define MT_FIN_PAIR 1
 #endif
 constexpr int kFinUnroll = MT_FIN_UNROLL;  // row gathers in flight per lane
-constexpr int kFinMaxF = 256;    // features (the LDS histogram bounds F far lower)
+constexpr int kFinMaxF = 256;    // features with LDS-cached bin counts (two-class path: all)
 constexpr int kFinPair = MT_FIN_PAIR;  // features scanned together per wave (latency hiding)
 constexpr int kFinChunk = 8;     // features per wave whose per-lane minima stay in registers
 
@@ -88,7 +90,13 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
     const float* __restrict__ xtabf, int xtab_n, int32_t* __restrict__ node_i32, int32_t* __restrict__ node_cnt,
     int64_t* __restrict__ tasks, int32_t* __restrict__ task_flag, int32_t epoch, int task_cap,
     int tiny_rows, int64_t* __restrict__ tiny, int32_t* __restrict__ tiny_count,
-    int64_t* __restrict__ prof) {
+    int64_t* __restrict__ prof, int Ft, int32_t* __restrict__ gstk) {
+  // Ft: features per LDS histogram tile. Ft == F is the single-pass layout; Ft < F
+  // (many classes or many features: generic path only) builds and scans the
+  // node's histogram one feature tile at a time, re-reading the node's rows per
+  // tile, and counts the winning split's left classes during the partition.
+  // gstk (C > kFinStackC): global scratch [grid][kFinStack][C] for the DFS
+  // stack's class counts (thread 0 writes and reads them; no LDS for many classes)
   // prof (optional): per workgroup {wall start, wall end, nodes, rows, cycles in
   // histogram, scan, partition, rest} -- the finisher's own phase profile
   constexpr int kFinWaves = kFinThreads / kWave;
@@ -107,7 +115,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
   __shared__ int64_t s_st_start[kFinStack];
   __shared__ int32_t s_st_count[kFinStack], s_st_depth[kFinStack], s_st_id[kFinStack];
   __shared__ int32_t s_st_buf[kFinStack];
-  __shared__ int32_t s_st_cnt[kFinStack][kFinMaxC];
+  __shared__ int32_t s_st_cnt[kFinStack * kFinStackC];
   __shared__ int s_sp, s_root;
   __shared__ int64_t s_start;
   __shared__ int32_t s_count, s_depth, s_id, s_buf;
@@ -122,19 +130,17 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
   if (threadIdx.x == 0) s_cand_total = 0;
 
   const int tid = threadIdx.x;
+  const bool tiled = Ft < F;
+  int32_t* const stc = gstk ? gstk + (int64_t)blockIdx.x * kFinStack * C : s_st_cnt;
+  const int stw = gstk ? C : kFinStackC;  // stack row stride
   const int wave = tid >> 6;
   const int lane = lane_id();
   const int W = (C + 1) >> 1;
   const int fstride = fin_fstride(B, W);
   constexpr int cpw = 4 / sizeof(CodeT);
-  const int words = (F + cpw - 1) / cpw;
   const int tn = min(kFinTab, xtab_n);
   const int tnd = min(kFinTab / 4, xtab_n);  // C <= 2: fp64 entries kept in LDS
   const int JW = 5 + C;
-  // 16-B row loads when the row stride allows it; lanes per row = pow2 >= words/vec
-  const int vec = (row_words % 4) == 0 ? 4 : 1;
-  int lane_shift = 0;
-  while ((1 << lane_shift) * vec < words && lane_shift < 6) ++lane_shift;
 
   // profile counters live in LDS (thread 0 only): no VGPRs on the hot path
   __shared__ int64_t s_pr[9];  // {wall0, nodes, rows, cycles[5], last clock}
@@ -155,8 +161,9 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
   } else {
     for (int i = tid; i < tn; i += kFinThreads) s_tab[i] = xtab[i];
   }
-  for (int f = tid; f < F; f += kFinThreads) s_nb[f] = min(B, nbins[f]);
-  const int hist_q = F * fstride / 4;  // uint4 words (fstride is a multiple of 4)
+  for (int f = tid; f < min(F, kFinMaxF); f += kFinThreads) s_nb[f] = min(B, nbins[f]);
+  auto nbf = [&](int f) { return f < kFinMaxF ? s_nb[f] : min(B, nbins[f]); };
+  const int hist_q = Ft * fstride / 4;  // uint4 words (fstride is a multiple of 4)
   uint4* hist4 = reinterpret_cast<uint4*>(hist);
   for (int e = tid; e < hist_q; e += kFinThreads) hist4[e] = make_uint4(0, 0, 0, 0);
 
@@ -373,9 +380,9 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         s_sp = 0;
       }
     }
-    if (tid < C) s_st_cnt[0][tid] = (int32_t)jb[5 + tid];
+    for (int c = tid; c < C; c += kFinThreads) stc[c] = (int32_t)jb[5 + c];
     __syncthreads();
-    if (tid < C) nc[(int64_t)s_root * C + tid] = (int32_t)jb[5 + tid];
+    for (int c = tid; c < C; c += kFinThreads) nc[(int64_t)s_root * C + c] = (int32_t)jb[5 + c];
     while (s_sp > 0) {
       __syncthreads();  // everyone has read s_sp before thread 0 pops
       // ---- pop + node term (thread 0); the histogram is already zero
@@ -389,8 +396,9 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         double acc = 0.0;
         int64_t mm = 0, sq = 0;
         for (int c = 0; c < C; ++c) {
-          const int64_t t = s_st_cnt[sp][c];
+          const int64_t t = stc[sp * stw + c];
           s_cnt[c] = (int32_t)t;
+          s_left[c] = 0;  // tiled: counted during the partition
           mm += t;
           acc = acc + tl((uint64_t)t);
           sq += t * t;
@@ -411,14 +419,32 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
       }
       uint32_t* __restrict__ src = s_buf ? buf1 : buf0;
       uint32_t* __restrict__ dst = s_buf ? buf0 : buf1;
-      // ---- histogram of this node's rows (all features): VEC words per lane,
-      // lanes_per_row lanes per row, kFinUnroll rows in flight per lane
+      const double pterm = s_pterm;
+      double bg = -__builtin_inf();
+      int bfeat = 0x7fffffff, bbin = -1;
+      int nc_report = 0x40000000;  // no exact-pass skip unless pass 1 proves one
+      for (int ft0 = 0; ft0 < F; ft0 += Ft) {
+      const int ft1 = min(F, ft0 + Ft);
+      if (ft0 > 0) {  // next feature tile: clear the previous tile's counts
+        __syncthreads();
+        for (int e = tid; e < hist_q; e += kFinThreads) hist4[e] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+      }
+      // ---- histogram of this node's rows (features [ft0, ft1)): VEC words per
+      // lane, lanes_per_row lanes per row, kFinUnroll rows in flight per lane
       {
+        const int w_lo = ft0 / cpw;
+        const int words = (ft1 + cpw - 1) / cpw - w_lo;
+        // 16-B row loads when the row stride and tile start allow it; lanes per
+        // row = pow2 >= words/vec
+        const int vec = (row_words % 4) == 0 && (w_lo % 4) == 0 ? 4 : 1;
+        int lane_shift = 0;
+        while ((1 << lane_shift) * vec < words && lane_shift < 6) ++lane_shift;
         const int L = 1 << lane_shift;
         const int sub = tid & (L - 1);
         const int rpp = kFinThreads >> lane_shift;
-        const int my_w = sub * vec;
-        const bool active = my_w < words;
+        const int my_w = w_lo + sub * vec;
+        const bool active = sub * vec < words;
         for (int base_r = tid >> lane_shift; base_r < m; base_r += rpp * kFinUnroll) {
           uint32_t ent[kFinUnroll];
 #pragma unroll
@@ -456,10 +482,10 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
               for (int j = 0; j < cpw; ++j) {
                 const int f = (my_w + v) * cpw + j;
-                if (f < F) {
+                if (f >= ft0 && f < ft1) {
                   const uint32_t code = (wv[u][v] >> (j * 8 * sizeof(CodeT))) &
                                         ((sizeof(CodeT) == 1) ? 0xffu : 0xffffu);
-                  atomicAdd(&hist[f * fstride + (int)code * W + off], inc);
+                  atomicAdd(&hist[(f - ft0) * fstride + (int)code * W + off], inc);
                 }
               }
             }
@@ -468,12 +494,8 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
       }
       __syncthreads();
       mark(0);
-      const double pterm = s_pterm;
       // ---- wave-per-feature scan (B <= 256: one 256-bin pass)
-      double bg = -__builtin_inf();
-      int bfeat = 0x7fffffff, bbin = -1;
-      int nc_report = 0x40000000;  // no exact-pass skip unless pass 1 proves one
-      if constexpr (kC2) {
+      if constexpr (kC2) {  // (single tile: Ft == F)
         const uint32_t t0 = (uint32_t)s_cnt[0], t1 = C > 1 ? (uint32_t)s_cnt[1] : 0u;
         bool cand_all = true, one_chunk = false;
         float thr = 0.0f;
@@ -576,9 +598,9 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           }
         }
       } else
-      for (int f = wave; f < F; f += kFinWaves) {
-        const int nb = s_nb[f];
-        const uint32_t* h = hist + f * fstride;
+      for (int f = ft0 + wave; f < ft1; f += kFinWaves) {
+        const int nb = nbf(f);
+        const uint32_t* h = hist + (f - ft0) * fstride;
         double best_cost = __builtin_inf();
         int best_bin = 0x7fffffff;
         const double tu = tie_unit(tl((uint64_t)m), (int64_t)m);
@@ -653,6 +675,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           }
         }
       }
+      }  // feature tiles
       if (lane == 0) {
         w_gain[wave] = bg;
         w_feat[wave] = bfeat;
@@ -703,8 +726,8 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         if (!(g > -__builtin_inf())) bf = -1;
       }
       if (bf >= 0) {
-        // ---- left class counts of the winning split
-        for (int c = wave; c < C; c += kFinWaves) {
+        // ---- left class counts of the winning split (tiled: counted below)
+        for (int c = wave; c < C && !tiled; c += kFinWaves) {
           uint32_t s = 0;
           const uint32_t* h = hist + bf * fstride;
           for (int b = lane; b <= bb; b += kWave) {
@@ -746,6 +769,10 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
             basel = __builtin_amdgcn_readfirstlane(basel);
             baser = __builtin_amdgcn_readfirstlane(baser);
             if (valid) {
+              if (tiled && go) {
+                const uint32_t e = ent[u];
+                atomicAdd(&s_left[rl.shift ? (int)(e >> rl.shift) : y[e & rl.mask]], 1);
+              }
               if (go)
                 dst[start + basel + __popcll(bl & lt)] = ent[u];
               else
@@ -836,7 +863,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           s_st_id[sp] = is_left ? lid : rid;
           s_st_buf[sp] = s_buf ^ 1;
           for (int c = 0; c < C; ++c)
-            s_st_cnt[sp][c] = is_left ? s_left[c] : s_cnt[c] - s_left[c];
+            stc[sp * stw + c] = is_left ? s_left[c] : s_cnt[c] - s_left[c];
         }
       }
       __syncthreads();
@@ -937,9 +964,9 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
       lab = rl.shift ? (int)(ent >> rl.shift) : y[row];
       for (int i = 0; i < nw; ++i) my_codes[i] = codes_rm[(int64_t)row * row_words + i];
     }
-    unsigned long long cm[kFinMaxC];
+    unsigned long long cm[kTinyMaxC];
 #pragma unroll
-    for (int c = 0; c < kFinMaxC; ++c) cm[c] = c < C ? __ballot(act && lab == c) : 0ull;
+    for (int c = 0; c < kTinyMaxC; ++c) cm[c] = c < C ? __ballot(act && lab == c) : 0ull;
     if (lane == 0) {
       s_mask[wave][0] = m == 64 ? ~0ull : ((1ull << m) - 1ull);
       s_dep[wave][0] = depth0;
@@ -956,11 +983,11 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       const int mm = __popcll(M);
-      int mc[kFinMaxC];
+      int mc[kTinyMaxC];
       double acc = 0.0;
       int64_t sq = 0;
 #pragma unroll
-      for (int c = 0; c < kFinMaxC; ++c) {
+      for (int c = 0; c < kTinyMaxC; ++c) {
         mc[c] = c < C ? __popcll(M & cm[c]) : 0;
         if (c < C) {
           acc = acc + s_tab[mc[c]];
@@ -996,7 +1023,7 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
           if (crit == kEntropy) {
             double sl = 0.0, sr = 0.0;
 #pragma unroll
-            for (int c = 0; c < kFinMaxC; ++c) {
+            for (int c = 0; c < kTinyMaxC; ++c) {
               if (c < C) {
                 const int lc = __popcll(le & cm[c]);
                 sl = sl + s_tab[lc];
@@ -1007,7 +1034,7 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
           } else {
             int64_t ql = 0, qr = 0;
 #pragma unroll
-            for (int c = 0; c < kFinMaxC; ++c) {
+            for (int c = 0; c < kTinyMaxC; ++c) {
               if (c < C) {
                 const int64_t lc = __popcll(le & cm[c]);
                 const int64_t rc = mc[c] - lc;
@@ -1059,7 +1086,7 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
       const int64_t ls = slot + 1, rs = slot + 2 * nl;  // pre-order position ranges
       int nzl = 0, nzr = 0;
 #pragma unroll
-      for (int c = 0; c < kFinMaxC; ++c) {
+      for (int c = 0; c < kTinyMaxC; ++c) {
         if (c < C) {
           const int lc = __popcll(LM & cm[c]);
           const int rc = mc[c] - lc;
@@ -1512,17 +1539,54 @@ static int tiny_sorted_lds(int F, int w) {  // static + dynamic LDS of one workg
 
 static int tiny_sorted_waves(int F) {
   constexpr int kLdsPerCu = 160 * 1024, kWavesPerCu = 16;
-  int best_w = 4, best = 0;
-  for (int w : {4, 8, 16}) {
+  int best_w = 1, best = 0;
+  for (int w : {1, 2, 4, 8, 16}) {
     const int bytes = tiny_sorted_lds(F, w);
+    if (bytes > kLdsPerCu) continue;
     const int waves = std::min(kLdsPerCu / bytes, kWavesPerCu / w) * w;
     if (waves > best) best = waves, best_w = w;
   }
   return best_w;
 }
 
-int finish_lds_bytes(int F, int B, int C) { return F * fin_fstride(B, (C + 1) / 2) * 4; }
+// Features per LDS histogram tile of the block finisher; 0: unsupported shape.
+// The whole node histogram in one pass when it fits (<= 150 KB, F <= 256);
+// else tiles sized for two 512-thread workgroups per CU (<= 62 KB), or -- when
+// that leaves fewer than 4 features per tile (many classes) -- for one
+// 1024-thread workgroup per CU (<= 140 KB).
+int finish_feature_tile(int F, int B, int C) {
+  if (F <= 0 || C > kFinMaxC || B > 256) return 0;
+  const int per_f = fin_fstride(B, (C + 1) / 2) * 4;
+  if (F <= kFinMaxF && F * per_f <= 150 * 1024) return F;
+  int ft = 62 * 1024 / per_f;
+  if (ft < 4) ft = 140 * 1024 / per_f;
+  if (ft <= 0) return 0;
+  // <= 256: a tile's row words (one byte per code) fit one wave's 64 lanes
+  ft = std::min(ft, kFinMaxF);
+  if (ft >= 16) ft &= ~15;  // 16-B row loads stay aligned at every tile start
+  return std::min(ft, F);
+}
+int finish_lds_bytes(int F, int B, int C) {
+  return finish_feature_tile(F, B, C) * fin_fstride(B, (C + 1) / 2) * 4;
+}
 int finish_max_classes() { return kFinMaxC; }
+
+// Global scratch for the DFS stack's class counts (C > kFinStackC): grow-only,
+// one buffer per device (finisher launches of a device share one stream).
+static int32_t* fin_stack_scratch(int grid, int C) {
+  static int32_t* buf[64] = {};
+  static size_t cap[64] = {};
+  int dev = 0;
+  MT_HIP_CHECK(hipGetDevice(&dev));
+  const size_t need = (size_t)grid * kFinStack * C * sizeof(int32_t);
+  if (dev < 0 || dev >= 64) throw std::runtime_error("finisher: device index out of range");
+  if (need > cap[dev]) {
+    if (buf[dev]) MT_HIP_CHECK(hipFree(buf[dev]));
+    MT_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&buf[dev]), need));
+    cap[dev] = need;
+  }
+  return buf[dev];
+}
 
 void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                    const void* codes_fm, int code_bytes, int64_t n_rows, uint32_t* buf0,
@@ -1537,12 +1601,19 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   // host. node_i32 / node_cnt are indexed by pre-order position (jobs[j][3] is
   // job j's root position); rows a fit never writes keep n = 0 (host memset).
   if (J <= 0) return;
-  if (C > kFinMaxC) throw std::runtime_error("finisher supports at most 16 classes");
-  if (F > kFinMaxF) throw std::runtime_error("finisher supports at most 256 features");
-  if (code_bytes != 1 || F > kTinyMaxF || tiny == nullptr) tiny_rows = 0;
+  const int Ft = finish_feature_tile(F, B, C);
+  if (Ft <= 0) throw std::runtime_error("finisher: unsupported shape (C > 256 or B > 256)");
+  // the two-class kernel (fp32 prefilter, hand-off queue) needs the single-pass
+  // layout (Ft == F <= kFinMaxF: per-feature LDS arrays)
+  const bool c2 = C <= 2 && Ft == F && F <= kFinMaxF;
+  const bool tiny_sorted = C <= 2 && getenv_int("MPITREE_TINY_SORTED", 1) != 0;
+  if (code_bytes != 1 || tiny == nullptr) tiny_rows = 0;
+  if (!tiny_sorted && (F > kTinyMaxF || C > kTinyMaxC)) tiny_rows = 0;
+  if (tiny_sorted && tiny_sorted_lds(F, 1) > 160 * 1024) tiny_rows = 0;  // > ~1100 features
   tiny_rows = std::min(tiny_rows, kTinyRows);
   FinRowLab rl{lab_shift ? ((1u << lab_shift) - 1u) : 0xffffffffu, lab_shift};
   const size_t lds = (size_t)finish_lds_bytes(F, B, C);
+  int32_t* gstk = nullptr;
 #define MT_FIN_NT(CT, C2, NT)                                                                 \
   MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_cls_kernel<CT, C2, NT>,                \
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));    \
@@ -1551,7 +1622,7 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                      buf1, y, rl, jobs, J, counter, nbins, F, B, C, crit, max_depth, mss,     \
                      msl, xtab, xtabf, xtab_n, node_i32, node_cnt, tasks, task_flag, epoch,   \
                      task_cap, tiny_rows,                                                     \
-                     tiny, counter + kFinCtrTinyCount, prof);
+                     tiny, counter + kFinCtrTinyCount, prof, Ft, gstk);
   // When the histogram leaves room for only one 512-thread workgroup per CU
   // (F = 128: 133 KB), run 1024 threads per workgroup instead: same LDS, twice
   // the waves to hide the gather and LDS latency. The persistent grid shrinks
@@ -1559,10 +1630,10 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   bool wide = false;
   if (getenv_int("MPITREE_FIN_WIDE", 1) != 0) {
     int per_cu = 0;
-    const void* k512 = code_bytes == 1 ? (C <= 2 ? (const void*)finish_cls_kernel<uint8_t, true, kFinThreadsSmall>
-                                                 : (const void*)finish_cls_kernel<uint8_t, false, kFinThreadsSmall>)
-                                       : (C <= 2 ? (const void*)finish_cls_kernel<uint16_t, true, kFinThreadsSmall>
-                                                 : (const void*)finish_cls_kernel<uint16_t, false, kFinThreadsSmall>);
+    const void* k512 = code_bytes == 1 ? (c2 ? (const void*)finish_cls_kernel<uint8_t, true, kFinThreadsSmall>
+                                             : (const void*)finish_cls_kernel<uint8_t, false, kFinThreadsSmall>)
+                                       : (c2 ? (const void*)finish_cls_kernel<uint16_t, true, kFinThreadsSmall>
+                                             : (const void*)finish_cls_kernel<uint16_t, false, kFinThreadsSmall>);
     MT_HIP_CHECK(hipFuncSetAttribute(k512, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     MT_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k512, kFinThreadsSmall, lds));
     wide = per_cu == 1;
@@ -1573,6 +1644,7 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
     MT_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
     grid = std::max(1, std::min(grid, n_cu));
   }
+  if (C > kFinStackC) gstk = fin_stack_scratch(grid, C);
 #define MT_FIN(CT, C2)                       \
   if (wide) {                                \
     MT_FIN_NT(CT, C2, kFinThreadsWide)       \
@@ -1580,13 +1652,13 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
     MT_FIN_NT(CT, C2, kFinThreadsSmall)      \
   }
   if (code_bytes == 1) {
-    if (C <= 2) {
+    if (c2) {
       MT_FIN(uint8_t, true)
     } else {
       MT_FIN(uint8_t, false)
     }
   } else {
-    if (C <= 2) {
+    if (c2) {
       MT_FIN(uint16_t, true)
     } else {
       MT_FIN(uint16_t, false)
@@ -1596,11 +1668,14 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
 #undef MT_FIN_NT
   MT_HIP_CHECK(hipGetLastError());
   if (tiny_rows > 0) {
-    const bool sorted = C <= 2 && getenv_int("MPITREE_TINY_SORTED", 1) != 0;
-    if (sorted) {
+    if (tiny_sorted) {
       int w = getenv_int("MPITREE_TINY_WAVES", tiny_sorted_waves(F));
-      w = w >= 16 && tiny_sorted_lds(F, 16) <= 160 * 1024 ? 16
-          : (w >= 8 && tiny_sorted_lds(F, 8) <= 160 * 1024 ? 8 : 4);
+      for (int cand : {16, 8, 4, 2, 1}) {  // the largest allowed width <= the request
+        if (cand <= w && tiny_sorted_lds(F, cand) <= 160 * 1024) {
+          w = cand;
+          break;
+        }
+      }
       // tiny_grid counts 4-wave workgroups: keep the total wave count
       const int g = std::max(1, tiny_grid * kTinyWaves / w);
       const size_t lds = (size_t)w * tiny_wave_bytes(F);
@@ -1615,8 +1690,12 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
         MT_TS(16)
       } else if (w == 8) {
         MT_TS(8)
-      } else {
+      } else if (w == 4) {
         MT_TS(4)
+      } else if (w == 2) {
+        MT_TS(2)
+      } else {
+        MT_TS(1)
       }
 #undef MT_TS
     } else {

@@ -391,9 +391,11 @@ static int ceil_pow2_shift(int v) {
 }
 
 // Features per LDS tile for the histogram kernel (0 -> global-atomic fallback).
+// At most 128: a row's tile is read by at most 64 lanes of one word each
+// (16-bit codes, unaligned rows), so wider tiles would drop features.
 int hist_feature_tile(int F_h, int B, int C, bool reg, int lds_budget) {
   int per_f = reg ? (B * 8 + (B + 1) * 4) : (B * ((C + 1) / 2) + 1) * 4;
-  int ft = lds_budget / per_f;
+  int ft = std::min(lds_budget / per_f, 128);
   if (ft <= 0) return 0;
   if (ft >= F_h) return F_h;
   if (ft >= 16) ft &= ~15;

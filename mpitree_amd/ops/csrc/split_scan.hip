@@ -37,7 +37,9 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
     double* __restrict__ out_cost, int32_t* __restrict__ out_bin,
     const double* __restrict__ xtab, int xtab_n, const int32_t* __restrict__ dcount,
     const int64_t* __restrict__ der, const uint32_t* __restrict__ prev,
-    const int32_t* __restrict__ nbuilt) {
+    const int32_t* __restrict__ nbuilt, int der_lds) {
+  // der_lds: the derived histogram (B*C words per wave) fits in LDS; else the
+  // scan reads parent - sibling from global memory on the fly (many classes)
   if (dcount && (int)blockIdx.x >= *dcount) return;  // device-side node count
   extern __shared__ uint32_t sm[];  // per wave: C class totals + C carries [+ B*C derived]
   const int wave = threadIdx.x >> 6;
@@ -51,6 +53,8 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
   uint32_t* tot = sm + wave * 2 * C;
   uint32_t* carry = tot + C;
   const int nb = min(B, nbins[f_lo + f]);
+  const uint32_t* gp = nullptr;  // on-the-fly derivation: parent and sibling
+  const uint32_t* gs = nullptr;
   if (der != nullptr) {
     const int NB = *nbuilt;
     if (slot >= NB) {
@@ -58,23 +62,29 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
       const uint32_t* pp = prev + (d[1] * F_h + f) * E;
       const uint32_t* sp = hist + (d[2] * F_h + f) * E;
       uint32_t* out = hist + (slot * F_h + f) * E;
-      uint32_t* loc = sm + 4 * 2 * C + wave * E;
+      uint32_t* loc = der_lds ? sm + 4 * 2 * C + wave * E : nullptr;
       for (int64_t e = lane; e < E; e += kWave) {
         const uint32_t v = pp[e] - sp[e];
-        loc[e] = v;
+        if (der_lds) loc[e] = v;
         out[e] = v;
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      h = loc;
+      if (der_lds) {
+        h = loc;
+      } else {
+        gp = pp;
+        gs = sp;
+      }
     }
   }
+  auto hv = [&](int64_t i) -> uint32_t { return gp ? gp[i] - gs[i] : h[i]; };
 
   // pass 1: per-class totals
   uint32_t m = 0;
   for (int c = 0; c < C; ++c) {
     uint32_t s = 0;
-    for (int b = lane; b < nb; b += kWave) s += h[(int64_t)b * C + c];
+    for (int b = lane; b < nb; b += kWave) s += hv((int64_t)b * C + c);
     s = wave_sum_u32(s);
     if (lane == 0) {
       tot[c] = s;
@@ -111,7 +121,7 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
 #pragma unroll
       for (int k = 0; k < kBinsPerLane; ++k) {
         const int b = b0 + k;
-        v[k] = (b < nb) ? h[(int64_t)b * C + c] : 0u;
+        v[k] = (b < nb) ? hv((int64_t)b * C + c) : 0u;
       }
       uint32_t p[kBinsPerLane];
       p[0] = v[0];
@@ -410,15 +420,16 @@ void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int
     hipLaunchKernelGGL(scan_reg_kernel, grid, dim3(256), 0, stream, (const int64_t*)hist, nodes,
                        nbins, F_h, f_lo, B, msl, cost, bins, dcount);
   } else {
-    if (der != nullptr && (int64_t)B * C > 4096)
-      throw std::runtime_error("fused derive: at most 4096 bins x classes per feature");
+    // derived histograms stay in LDS up to 4096 bins x classes (64 KB for the
+    // four waves); past that the scan derives each count from global memory
+    const int der_lds = der != nullptr && (int64_t)B * C <= 4096;
     size_t lds = (size_t)4 * 2 * C * sizeof(uint32_t) +
-                 (der != nullptr ? (size_t)4 * B * C * sizeof(uint32_t) : 0);
+                 (der_lds ? (size_t)4 * B * C * sizeof(uint32_t) : 0);
     MT_HIP_CHECK(hipFuncSetAttribute((const void*)scan_cls_kernel,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL(scan_cls_kernel, grid, dim3(256), lds, stream, (uint32_t*)hist,
                        nodes, nbins, F_h, f_lo, B, C, crit, msl, cost, bins, xtab, xtab_n,
-                       dcount, der, (const uint32_t*)prev, nbuilt);
+                       dcount, der, (const uint32_t*)prev, nbuilt, der_lds);
   }
   MT_HIP_CHECK(hipGetLastError());
   const size_t sel_lds = crit == kSquaredError ? 16 : (size_t)2 * C * sizeof(int64_t);

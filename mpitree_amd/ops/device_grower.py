@@ -28,11 +28,18 @@ the stream between the level kernels, never a host round trip):
   only; one ``all_gather_into_tensor`` of the per-node split records per level
   feeds ``fp_combine_kernel`` (max gain, ties to the lowest feature), after
   which the planner and partition run identically on every rank;
-* data-parallel (``strategy="data"``): rows sharded, the built (smaller-child)
-  histograms of each level are summed with one ``all_reduce`` (integer counts:
-  exact, order independent); local row segments are fixed up after the
-  partition (``grow_dp_fixup_kernel``); regression purity takes one min/max
-  all-reduce per level;
+* data-parallel (``strategy="data"``): rows sharded. Each level's built
+  (smaller-child) histograms are built one destination feature block at a
+  time, and each block is summed into its owner rank with a ``reduce``
+  enqueued (async) right behind its block's kernels, so block r's reduce runs
+  on the process group's stream while block r + 1 builds -- a reduce-scatter
+  by feature that overlaps the build (integer counts: exact, order
+  independent). Every rank then scans only its own block (deriving larger
+  siblings from its block of the parent) and the split records take the
+  feature-parallel all-gather + ``fp_combine_kernel``. Local row segments are
+  fixed up after the partition (``grow_dp_fixup_kernel``); regression purity
+  takes one min/max all-reduce per level. (Fewer features than ranks: one
+  all-reduce of the whole built histograms instead.)
 * subtree jobs (nodes of at most ``finisher_rows`` rows) are split across
   ranks (serpentine over the largest-first job order); data-parallel ranks
   first send each job's rows to its owner (one ``all_to_all``); one
@@ -57,6 +64,7 @@ import torch
 from ..models.tree_arrays import TreeArrays
 from ..utils.observability import profiling
 from . import hip_backend as hb
+from ..parallel.strategies import feature_blocks
 
 __all__ = ["DeviceGrower", "device_loop_supported"]
 
@@ -396,6 +404,9 @@ class DeviceGrower:
         if P <= 1:
             return False, False, False, 0, F
         if kind == "data":
+            if F >= P:  # the built histograms are reduced to their feature block's owner
+                lo, hi = feature_blocks(F, P)[int(comm.rank)]
+                return False, True, False, int(lo), int(hi)
             return False, True, False, 0, F
         if kind == "feature" and F >= P:
             lo, hi = comm.feature_range(F)
@@ -422,6 +433,10 @@ class DeviceGrower:
         fp, dp, own, f_lo, f_hi = self._mode(F)
         F_h = f_hi - f_lo
         P = getattr(comm, "world_size", 1)
+        # data-parallel with >= P features: built histograms reduced per feature
+        # block to the block's owner (reduce-scatter by feature), scans per block
+        dprs = dp and F_h < F
+        blocks = feature_blocks(F, P) if dprs else None
         s = hb._stream
         t0 = time.perf_counter()
         n_loc = int(n)
@@ -474,7 +489,11 @@ class DeviceGrower:
                     slab=torch.empty((IMAX, hip.hist_slab_words(F_h, B, C, reg)), dtype=hdt,
                                      device=dev),
                     rec=torch.empty((KMAX, R), **i64),
-                    grec=torch.empty((P * KMAX * R) if fp else 1, **i64),
+                    grec=torch.empty((P * KMAX * R) if (fp or dprs) else 1, **i64),
+                    # the other ranks' feature blocks of this rank's built histograms
+                    rs=[torch.empty((KMAX, hi - lo, B, C), dtype=hdt, device=dev)
+                        if r != int(comm.rank) else None
+                        for r, (lo, hi) in enumerate(blocks)] if dprs else None,
                     cost=torch.empty((KMAX, F_h), dtype=torch.float64, device=dev),
                     bins=torch.empty((KMAX, F_h), dtype=torch.int32, device=dev),
                     ident=torch.arange(KMAX, **i64),
@@ -565,29 +584,45 @@ class DeviceGrower:
                 # rows alternate between the two permutation buffers level by level
                 src, dst = bufs[lvl % 2], bufs[(lvl + 1) % 2]
                 rb = int(min(kb, RMAX))
-                # classification: the hist launch also zeroes the slots the slab
-                # reduction adds into (one launch less per level)
-                hip.hist(s(), be.codes_rm.data_ptr(), cb, rs, src, be.y.data_ptr(),
-                         be.lab_shift, cur["items"], ib, H.data_ptr(), slab.data_ptr(), F_h, f_lo,
-                         B, C, reg, hb.LDS_BUDGET, dcount=ctl + 4 * 2,
-                         zred=0 if reg else cur["red"], zred_bound=0 if reg else rb,
-                         zcount=0 if reg else ctl + 4 * 3)
-                if reg:  # slabs summed straight into the slot
-                    hip.hist_reduce(s(), cur["red"], rb, 1, slab.data_ptr(), H.data_ptr(), F_h, B,
-                                    C, True, dcount=ctl + 4 * 3)
-                else:
-                    hip.hist_reduce_tasks(s(), cur["red"], rb, cur["tasks"],
-                                          int(min(TMAX, rb + ib // 16 + 1)), slab.data_ptr(),
-                                          H.data_ptr(), F_h, B, C, ctl + 4 * 3, ctl + 4 * 7,
-                                          zero=False)
-                if dp:  # sum the built slots' histograms over the row shards
-                    # built slots <= splits of the previous level (lagged read)
+                if dp:  # built slots <= splits of the previous level (lagged read)
                     if lvl - 2 >= first_lvl:
                         nbb = int(hctl[(lvl - 2) % 64, 0])
                     else:
                         nbb = 1 if lvl < 2 else KMAX  # (resumed: no lagged value yet)
                     nbb = max(1, min(nbb, KMAX))
-                    comm.all_reduce_device(H[:nbb])
+
+                def build(Ht, lo, nf):
+                    # classification: the hist launch also zeroes the slots the slab
+                    # reduction adds into (one launch less per level)
+                    hip.hist(s(), be.codes_rm.data_ptr(), cb, rs, src, be.y.data_ptr(),
+                             be.lab_shift, cur["items"], ib, Ht.data_ptr(), slab.data_ptr(), nf,
+                             lo, B, C, reg, hb.LDS_BUDGET, dcount=ctl + 4 * 2,
+                             zred=0 if reg else cur["red"], zred_bound=0 if reg else rb,
+                             zcount=0 if reg else ctl + 4 * 3)
+                    if reg:  # slabs summed straight into the slot
+                        hip.hist_reduce(s(), cur["red"], rb, 1, slab.data_ptr(), Ht.data_ptr(),
+                                        nf, B, C, True, dcount=ctl + 4 * 3)
+                    else:
+                        hip.hist_reduce_tasks(s(), cur["red"], rb, cur["tasks"],
+                                              int(min(TMAX, rb + ib // 16 + 1)), slab.data_ptr(),
+                                              Ht.data_ptr(), nf, B, C, ctl + 4 * 3, ctl + 4 * 7,
+                                              zero=False)
+
+                if dprs:
+                    # block r of the built slots -> rank r, enqueued behind block r's
+                    # kernels: the reduce of block r overlaps the build of block r + 1
+                    works = []
+                    for r, (lo, hi) in enumerate(blocks):
+                        Hr = H if r == rank else ws["rs"][r]
+                        build(Hr, lo, hi - lo)
+                        works.append(comm.reduce_device(Hr[:nbb], r, async_op=True))
+                    for w in works:
+                        if w is not None:
+                            w.wait()
+                else:
+                    build(H, f_lo, F_h)
+                    if dp:  # sum the built slots' histograms over the row shards
+                        comm.all_reduce_device(H[:nbb])
                 mark()
                 # classification: the scan derives the larger siblings itself
                 # (parent - built sibling, written back for select / next level)
@@ -600,7 +635,7 @@ class DeviceGrower:
                          rec.data_ptr(), be.xtab.data_ptr(), hb.XTAB_N, dcount=ctl,
                          der=cur["der"] if fuse else 0, prev=Hp.data_ptr() if fuse else 0,
                          nbuilt=ctl + 4 * 1 if fuse else 0)
-                if fp:  # every rank's best split of each node -> the global best
+                if fp or dprs:  # every rank's best split of each node -> the global best
                     g = ws["grec"][: P * kb * R]
                     comm.all_gather_device(g, rec[:kb].reshape(-1))
                     hip.fp_combine(s(), g.data_ptr(), P, kb, R, ctl, rec.data_ptr())
@@ -688,6 +723,8 @@ class DeviceGrower:
             self.stats["mode"] = ("data" if dp else "feature" if fp
                                   else "subtree-owned" if own else "replicated")
             self.stats["feature_block"] = [f_lo, f_hi]
+            if dp:
+                self.stats["dp_reduce"] = "reduce-to-owner" if dprs else "all-reduce"
         self.timings["levels"] = time.perf_counter() - t0
         self.stats["levels"] = levels
         self.stats["finisher_subtrees"] = J

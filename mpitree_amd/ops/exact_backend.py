@@ -165,8 +165,7 @@ class ExactHipBackend(HipBackend):
     def finisher_supported(self) -> bool:
         """Subtrees of <= ``max_finisher_rows`` rows continue in the histogram
         finisher on subtree-local codes (see :meth:`defer_segments`)."""
-        return (self.C <= 16 and self.F <= 256
-                and self.hip.finish_lds_bytes(self.F, 256, self.C) <= 150 * 1024)
+        return self.F <= 256 and self.hip.finish_feature_tile(self.F, 256, self.C) > 0
 
     @property
     def max_finisher_rows(self) -> int:

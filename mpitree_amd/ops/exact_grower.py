@@ -23,7 +23,7 @@ reference's contract): **feature-parallel**. Rank r sorts, scans and partitions
 only its contiguous feature block -- setup, scans and partitions all shrink
 with 1/P -- and per level one ``all_gather`` of the per-node split records
 (``fp_combine_kernel``: max gain, ties to the lowest feature) plus one
-``all_reduce`` of the n-byte row-direction flags (the split feature's owner
+``all_reduce`` of the n-bit row-direction flags (the split feature's owner
 sets them) keep the ranks in lock step. The finisher codes of every block are
 all-gathered once, the jobs are split across ranks (serpentine over the
 largest-first order) and one exchange of the finished position ranges plus
@@ -47,7 +47,14 @@ __all__ = ["ExactGrower", "exact_supported"]
 
 MAX_ROWS = 1 << 24
 _WS: dict = {}
-_DEBUG_SYNC = os.environ.get("MPITREE_EXACT_SYNC") == "1"
+_DEBUG_SYNC = os.environ.get("MPITREE_EXACT_SYNC", "0") != "0"
+_DEBUG_STEP = os.environ.get("MPITREE_EXACT_SYNC") == "2"  # (+ a sync after every launch)
+
+
+def _step(dev, what):
+    if _DEBUG_STEP:
+        torch.cuda.synchronize(dev)
+        print(f"  exact: {what} done", flush=True)
 
 
 def exact_supported(n: int, C: int, regression: bool) -> bool:
@@ -217,7 +224,6 @@ class ExactGrower:
                             items=torch.empty((IMAX, 4), **i64),
                             ifirst=torch.empty(KMAX + 1, **i32), ctl=torch.zeros(16, **i32))
 
-            nbw = int(hip.xe_bits_words())
             ws = _WS[key] = dict(
                 L=[lists(), lists()],
                 tot=torch.empty((IMAX, F_loc, Cc), **i64),
@@ -229,10 +235,11 @@ class ExactGrower:
                 split=torch.empty((KMAX, 4), **i64),
                 pitems=torch.empty((IMAX, 4), **i64),
                 pfirst=torch.empty(KMAX + 1, **i32),
-                flag=torch.empty(n, dtype=torch.uint8, device=dev),
-                lc=torch.empty((IMAX, F_loc), **i32),
-                lcar=torch.empty((IMAX, F_loc), **i32),
-                bits=torch.empty((IMAX, F_loc, nbw), **i64),
+                flag=torch.empty((n + 31) // 32, dtype=torch.int32, device=dev),
+                # look-back status words (tagged per fit and level: zeroed once)
+                sstat=torch.zeros((IMAX, F_loc), **i64),
+                pstat=torch.zeros((IMAX, F_loc), **i64),
+                tick=torch.zeros(4, **i32),
                 jobs=torch.empty((JMAX, JW), **i64),
                 job_count=torch.zeros(1, **i32),
                 root=torch.empty(Cs, **i64),
@@ -248,17 +255,19 @@ class ExactGrower:
             xtab=be.xtab.data_ptr(), xtab_n=int(be.xtab.numel()), tot=ptr["tot"],
             carry=ptr["carry"],
             cmm=ptr["cmm"], cbest=ptr["cbest"], rec=ptr["rec"], split=ptr["split"],
-            pitems=ptr["pitems"], pfirst=ptr["pfirst"], flag=ptr["flag"], lc=ptr["lc"],
-            lcar=ptr["lcar"], bits=ptr["bits"], pos_rec=be.pos_rec.data_ptr(),
+            pitems=ptr["pitems"], pfirst=ptr["pfirst"], flag=ptr["flag"], sstat=ptr["sstat"],
+            pstat=ptr["pstat"], tick=ptr["tick"], pos_rec=be.pos_rec.data_ptr(),
             pos_st=be.pos_st.data_ptr(), pos_thr=pos_thr.data_ptr(), jobs=ptr["jobs"],
             job_count=ptr["job_count"], max_depth=md, mss=mss, fr=fr), lp[0], lp[1])
         ws["root"].copy_(torch.from_numpy(np.ascontiguousarray(root_stats, np.int64)))
+        ws["tick"].zero_()  # work tickets + the look-back watchdog
         ctx.init(s(), ws["root"].data_ptr())
         self._keep = (ctx, E, Y, ranks)
 
         # ---- level loop: enqueue only; a lagged host-mapped slot tells the end
         hctl_dev, hctl = _host_ctl(hip, dev)
         _FIT_SEQ[0] = (_FIT_SEQ[0] + 1) % (1 << 18)
+        ctx.begin(_FIT_SEQ[0] + 1)
         tag0 = _FIT_SEQ[0] << 12
         t1 = time.perf_counter()
         lvl, done_at = 0, None
@@ -267,13 +276,16 @@ class ExactGrower:
             b0 = getattr(comm, "bytes_communicated", 0)
             kb = int(min(2 ** min(lvl, 40), KMAX))
             ib = int(min(IMAX, kb + n // chunk + 1))
+            _step(dev, f"level {lvl} start")
             ctx.level_scan(s(), lvl, ib, kb)
+            _step(dev, "scan + select")
             if P > 1:  # every rank's best split per node -> the global best
                 g = ws["grec"][: P * kb * R]
                 comm.all_gather_device(g, ws["rec"][:kb].reshape(-1))
                 hip.fp_combine(s(), g.data_ptr(), P, kb, R, lp[lvl % 2]["ctl"],
                                ws["rec"].data_ptr())
             ctx.plan(s(), lvl, hctl_dev + (lvl % 64) * 64, tag0 + (lvl % 4096) + 1)
+            _step(dev, "plan")
             if P > 1:  # the split feature's owner sets the left rows; summed over ranks
                 ws["flag"].zero_()
                 ctx.flag(s(), lvl, ib, 0)
@@ -281,11 +293,17 @@ class ExactGrower:
                 comm_bytes.append(int(getattr(comm, "bytes_communicated", 0) - b0))
             else:
                 ctx.flag(s(), lvl, ib, 1)
+            _step(dev, "flag")
             ctx.partition(s(), lvl, ib, kb)
+            _step(dev, "partition")
             if _DEBUG_SYNC:  # (MPITREE_EXACT_SYNC=1: sync + report every level)
                 torch.cuda.synchronize(dev)
+                ni = int(L[lvl % 2]["ctl"][1])
+                st = ws["sstat"][: min(ni, 4)].cpu().numpy().astype(np.uint64)
                 print(f"exact level {lvl}: next frontier {int(L[(lvl + 1) % 2]['ctl'][0])}, "
-                      f"jobs {int(ws['job_count'][0])}", flush=True)
+                      f"jobs {int(ws['job_count'][0])}, tickets {ws['tick'].tolist()}, "
+                      f"items {ni}, status tags {(st >> np.uint64(34)).tolist()} "
+                      f"states {((st >> np.uint64(32)) & np.uint64(3)).tolist()}", flush=True)
             lvl += 1
             if lvl >= 2:
                 _wait_slot(hctl, (lvl - 2) % 64, tag0 + ((lvl - 2) % 4096) + 1)
@@ -311,7 +329,10 @@ class ExactGrower:
         if timings is not None:
             timings["finisher"] = time.perf_counter() - t2
         t3 = time.perf_counter()
-        ta = be.assemble_positions(None, int(crit), y_exp, thr_pos=pos_thr)
+        watch = hb._pinned_copy(ws["tick"][2:3], "exact.watch")
+        ta = be.assemble_positions(None, int(crit), y_exp, thr_pos=pos_thr)  # (synchronises)
+        if int(watch[0]) != 0:
+            raise RuntimeError("exact engine: a look-back wait timed out; the tree is invalid")
         if timings is not None:
             timings["assemble"] = time.perf_counter() - t3
         self._keep = None

@@ -549,13 +549,15 @@ class HipBackend:
 
     # -------------------------------------------------------------- finisher
     def finisher_supported(self) -> bool:
-        if self.B > 256 or self.F > 256:
+        if self.B > 256:
             return False
-        if self.reg:  # feature-tiled LDS histograms: any F
-            return True
-        if self.cb != 1 or self.C > 16:
+        if self.reg:
+            return self.F <= 256
+        if self.cb != 1:
             return False
-        return self.hip.finish_lds_bytes(self.F, self.B, self.C) <= 150 * 1024
+        # C <= 256, any F: the block finisher tiles features (and classes' words)
+        # through LDS when one node's histogram does not fit in one pass
+        return self.hip.finish_feature_tile(self.F, self.B, self.C) > 0
 
     # finisher jobs index the x*log2(x) table with row counts: keep them below it
     max_finisher_rows = XTAB_N - 1

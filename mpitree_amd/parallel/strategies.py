@@ -232,6 +232,24 @@ class DistComm(LocalComm):
             dist.all_reduce(t, op=op, group=self.group)
         self.bytes_communicated += t.numel() * t.element_size()
 
+    def reduce_device(self, t: torch.Tensor, dst: int, async_op: bool = False):
+        """Sum ``t`` over the ranks into rank ``dst``'s ``t`` (other ranks' ``t``
+        is left as it was or unspecified). With RCCL and ``async_op`` the reduce
+        is enqueued on the process group's stream behind the current stream's
+        kernels and the call returns at once -- the caller keeps launching work
+        (the next feature block's histogram) and ``wait()`` on the returned work
+        orders the current stream after the reduce. Returns None when done."""
+        self.bytes_communicated += t.numel() * t.element_size()
+        gdst = dst if self.group is None else dist.get_global_rank(self.group, dst)
+        if self._staged(t):
+            h = t.cpu()
+            dist.reduce(h, dst=gdst, op=dist.ReduceOp.SUM, group=self.group)
+            if self.rank == dst:
+                t.copy_(h)
+            return None
+        return dist.reduce(t, dst=gdst, op=dist.ReduceOp.SUM, group=self.group,
+                           async_op=async_op)
+
     def all_to_all_device(self, out: torch.Tensor, inp: torch.Tensor, out_splits: list,
                           in_splits: list) -> None:
         """Rows (dim 0) of ``inp`` go to ranks by ``in_splits``; ``out`` receives by

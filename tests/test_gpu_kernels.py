@@ -584,3 +584,23 @@ def test_gpu_finisher_handoff_queue_single_job(monkeypatch, regression):
     monkeypatch.setenv("MPITREE_FIN_STEAL", "-1")  # same tree without the queue
     g2 = fit_tree(X, y, device="cuda", **kw)
     assert g2.arrays.equal(h.arrays, check_impurity=not regression)
+
+
+@pytest.mark.parametrize("C,F,n", [(64, 16, 40000), (200, 8, 30000), (2, 300, 20000),
+                                   (5, 300, 8000)])
+def test_gpu_finisher_many_classes_and_features(C, F, n):
+    # the block finisher tiles features through LDS when one node's histogram does
+    # not fit (many classes: 16-bit class pairs per bin; many features), keeps the
+    # DFS stack's class counts in global scratch past 16 classes, and the sorted
+    # tiny kernel runs with fewer waves per workgroup for wide rows
+    rng = np.random.default_rng(C * 1000 + F)
+    X, y = random_problem(rng, n, F, C, levels=48)
+    cpu = DecisionTreeClassifier(device="cpu").fit(X, y)
+    gpu = DecisionTreeClassifier(device="cuda").fit(torch.from_numpy(X).cuda(),
+                                                    torch.from_numpy(y).cuda())
+    st = gpu.fit_stats_
+    assert st.get("finisher_subtrees", 0) > 0, st
+    if C <= 64:  # (C = 200: the level histograms exceed LDS -> host-driven levels)
+        assert st["engine"] == "hip-device-loop", st["engine"]
+    assert gpu.tree_arrays_.equal(cpu.tree_arrays_), (gpu.tree_arrays_.node_count,
+                                                      cpu.tree_arrays_.node_count)
