@@ -408,6 +408,10 @@ def fit_tree(
         # (regression: the hand-off queue gains 0.35 ms at any of n/512 .. n/128)
         default_fr = int(env) if env else (max(2048, n // 512) if regression
                                            else max(2048, min(n // 128, 32768)))
+        if not env and C > 2:
+            # (more classes: no hand-off queue, and a node's histogram scan grows
+            # with B * C -- smaller jobs keep every finisher workgroup busy)
+            default_fr = min(default_fr, 4096 if C <= 16 else 2048)
         if finisher_rows is None or (comm.world_size > 1 and comm.kind == "data"):
             # data-parallel GPU ranks finish subtrees on their owners (rows sent
             # there first), so the finisher applies as on one GPU

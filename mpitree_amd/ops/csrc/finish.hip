@@ -95,8 +95,9 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
   // (many classes or many features: generic path only) builds and scans the
   // node's histogram one feature tile at a time, re-reading the node's rows per
   // tile, and counts the winning split's left classes during the partition.
-  // gstk (C > kFinStackC): global scratch [grid][kFinStack][C] for the DFS
-  // stack's class counts (thread 0 writes and reads them; no LDS for many classes)
+  // gstk (C > kFinStackC): global scratch [grid][kFinStack + 2][C] for the DFS
+  // stack's class counts and the node's / left class counts (no LDS for many
+  // classes)
   // prof (optional): per workgroup {wall start, wall end, nodes, rows, cycles in
   // histogram, scan, partition, rest} -- the finisher's own phase profile
   constexpr int kFinWaves = kFinThreads / kWave;
@@ -119,7 +120,10 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
   __shared__ int s_sp, s_root;
   __shared__ int64_t s_start;
   __shared__ int32_t s_count, s_depth, s_id, s_buf;
-  __shared__ int32_t s_cnt[kFinMaxC], s_left[kFinMaxC];
+  // node / left class counts: LDS up to kFinStackC classes, else global scratch
+  // (keeps the two-class kernel's static LDS small: two 512-thread workgroups
+  // per CU with the 66 KB F = 64 histogram)
+  __shared__ int32_t s_cnt_l[kFinStackC], s_left_l[kFinStackC];
   __shared__ double s_pterm;
   __shared__ double w_gain[kFinWaves];
   __shared__ int w_feat[kFinWaves], w_bin[kFinWaves];
@@ -131,8 +135,10 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
 
   const int tid = threadIdx.x;
   const bool tiled = Ft < F;
-  int32_t* const stc = gstk ? gstk + (int64_t)blockIdx.x * kFinStack * C : s_st_cnt;
+  int32_t* const stc = gstk ? gstk + (int64_t)blockIdx.x * (kFinStack + 2) * C : s_st_cnt;
   const int stw = gstk ? C : kFinStackC;  // stack row stride
+  int32_t* const s_cnt = gstk ? stc + kFinStack * C : s_cnt_l;
+  int32_t* const s_left = gstk ? s_cnt + C : s_left_l;
   const int wave = tid >> 6;
   const int lane = lane_id();
   const int W = (C + 1) >> 1;
@@ -926,6 +932,12 @@ __device__ __forceinline__ uint32_t wave_min_u32_dpp(uint32_t v) {
 constexpr int kTinyMaxF = 128;
 constexpr int kTinyStride = kTinyMaxF / 4 + 1;  // words per staged row (+1: bank spread)
 
+// kMany (C > kTinyMaxC, up to 256 classes): the subtree's classes present in
+// its <= 64 rows -- at most 64 -- are compacted in ascending class order at the
+// subtree root (their lane masks and counts live in LDS), and every class sum
+// runs over them only. Absent classes add T(0) = 0 / 0 to the host builder's
+// sequential sums, so the fp64 results are bit-identical.
+template <bool kMany>
 __global__ __launch_bounds__(256) void finish_tiny_kernel(
     const uint32_t* __restrict__ codes_rm, int64_t row_words, const uint32_t* __restrict__ buf0,
     const uint32_t* __restrict__ buf1, const int32_t* __restrict__ y, FinRowLab rl,
@@ -933,10 +945,15 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
     int32_t* __restrict__ tiny_counter, int F, int C, int crit, int max_depth, int64_t mss,
     int64_t msl, const double* __restrict__ xtab, int32_t* __restrict__ node_i32,
     int32_t* __restrict__ node_cnt) {
+  constexpr int kMC = kMany ? kTinyRows : kTinyMaxC;  // class slots per wave
   __shared__ double s_tab[kTinyRows + 1];
   __shared__ uint32_t s_codes[kTinyWaves][kTinyRows * kTinyStride];
   __shared__ unsigned long long s_mask[kTinyWaves][16];
   __shared__ int32_t s_dep[kTinyWaves][16], s_slot[kTinyWaves][16];
+  // kMany: compacted classes {lane mask, class id} and the node's counts per wave
+  __shared__ unsigned long long s_cm[kMany ? kTinyWaves : 1][kMany ? kTinyRows : 1];
+  __shared__ int32_t s_cid[kMany ? kTinyWaves : 1][kMany ? kTinyRows : 1];
+  __shared__ int32_t s_mc[kMany ? kTinyWaves : 1][kMany ? kTinyRows : 1];
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
   for (int i = threadIdx.x; i <= kTinyRows; i += blockDim.x) s_tab[i] = xtab[i];
@@ -964,9 +981,32 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
       lab = rl.shift ? (int)(ent >> rl.shift) : y[row];
       for (int i = 0; i < nw; ++i) my_codes[i] = codes_rm[(int64_t)row * row_words + i];
     }
-    unsigned long long cm[kTinyMaxC];
+    unsigned long long cm[kMany ? 1 : kTinyMaxC];
+    int nc = C;  // class slots in use
+    if constexpr (kMany) {
+      // ascending distinct labels of the subtree: repeated wave minimum
+      unsigned long long left = __ballot(act);
+      nc = 0;
+      while (left) {
+        const uint32_t cur = wave_min_u32_dpp(((left >> lane) & 1ull) ? (uint32_t)lab : 0xffffffffu);
+        const unsigned long long mk = __ballot(((left >> lane) & 1ull) && (uint32_t)lab == cur);
+        if (lane == 0) {
+          s_cm[wave][nc] = mk;
+          s_cid[wave][nc] = (int)cur;
+        }
+        left &= ~mk;
+        ++nc;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    } else {
 #pragma unroll
-    for (int c = 0; c < kTinyMaxC; ++c) cm[c] = c < C ? __ballot(act && lab == c) : 0ull;
+      for (int c = 0; c < kTinyMaxC; ++c) cm[c] = c < C ? __ballot(act && lab == c) : 0ull;
+    }
+    auto cmask = [&](int c) -> unsigned long long {
+      if constexpr (kMany) return s_cm[wave][c];
+      else return cm[c];
+    };
     if (lane == 0) {
       s_mask[wave][0] = m == 64 ? ~0ull : ((1ull << m) - 1ull);
       s_dep[wave][0] = depth0;
@@ -983,17 +1023,32 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       const int mm = __popcll(M);
-      int mc[kTinyMaxC];
+      int mc[kMany ? 1 : kTinyMaxC];
       double acc = 0.0;
       int64_t sq = 0;
+      if constexpr (kMany) {
+        for (int c = 0; c < nc; ++c) {
+          const int v = __popcll(M & s_cm[wave][c]);
+          if (lane == 0) s_mc[wave][c] = v;
+          acc = acc + s_tab[v];
+          sq += (int64_t)v * v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      } else {
 #pragma unroll
-      for (int c = 0; c < kTinyMaxC; ++c) {
-        mc[c] = c < C ? __popcll(M & cm[c]) : 0;
-        if (c < C) {
-          acc = acc + s_tab[mc[c]];
-          sq += (int64_t)mc[c] * mc[c];
+        for (int c = 0; c < kTinyMaxC; ++c) {
+          mc[c] = c < C ? __popcll(M & cm[c]) : 0;
+          if (c < C) {
+            acc = acc + s_tab[mc[c]];
+            sq += (int64_t)mc[c] * mc[c];
+          }
         }
       }
+      auto ccount = [&](int c) -> int {
+        if constexpr (kMany) return s_mc[wave][c];
+        else return mc[c];
+      };
       const double pterm = crit == kEntropy ? s_tab[mm] - acc : gini_term(mm, sq);
       const double tu = tie_unit(s_tab[mm], (int64_t)mm);
       const double tinv = 1.0 / tu;
@@ -1023,21 +1078,21 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
           if (crit == kEntropy) {
             double sl = 0.0, sr = 0.0;
 #pragma unroll
-            for (int c = 0; c < kTinyMaxC; ++c) {
-              if (c < C) {
-                const int lc = __popcll(le & cm[c]);
+            for (int c = 0; c < kMC; ++c) {
+              if (c < nc) {
+                const int lc = __popcll(le & cmask(c));
                 sl = sl + s_tab[lc];
-                sr = sr + s_tab[mc[c] - lc];
+                sr = sr + s_tab[ccount(c) - lc];
               }
             }
             cost = (s_tab[ml] - sl) + (s_tab[mr] - sr);
           } else {
             int64_t ql = 0, qr = 0;
 #pragma unroll
-            for (int c = 0; c < kTinyMaxC; ++c) {
-              if (c < C) {
-                const int64_t lc = __popcll(le & cm[c]);
-                const int64_t rc = mc[c] - lc;
+            for (int c = 0; c < kMC; ++c) {
+              if (c < nc) {
+                const int64_t lc = __popcll(le & cmask(c));
+                const int64_t rc = ccount(c) - lc;
                 ql += lc * lc;
                 qr += rc * rc;
               }
@@ -1085,16 +1140,36 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
       if (nl == 0 || nr == 0) continue;
       const int64_t ls = slot + 1, rs = slot + 2 * nl;  // pre-order position ranges
       int nzl = 0, nzr = 0;
-#pragma unroll
-      for (int c = 0; c < kTinyMaxC; ++c) {
-        if (c < C) {
-          const int lc = __popcll(LM & cm[c]);
-          const int rc = mc[c] - lc;
+      if constexpr (kMany) {
+        // every class of both children: absent ones 0, the subtree's from its masks
+        for (int c = lane; c < C; c += kWave) {
+          node_cnt[ls * C + c] = 0;
+          node_cnt[rs * C + c] = 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (int c = 0; c < nc; ++c) {
+          const int lc = __popcll(LM & s_cm[wave][c]);
+          const int rc = s_mc[wave][c] - lc;
           nzl += lc > 0;
           nzr += rc > 0;
-          if (lane == c) {
-            node_cnt[ls * C + c] = lc;
-            node_cnt[rs * C + c] = rc;
+          if (lane == 0) {
+            node_cnt[ls * C + s_cid[wave][c]] = lc;
+            node_cnt[rs * C + s_cid[wave][c]] = rc;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < kTinyMaxC; ++c) {
+          if (c < C) {
+            const int lc = __popcll(LM & cm[c]);
+            const int rc = mc[c] - lc;
+            nzl += lc > 0;
+            nzr += rc > 0;
+            if (lane == c) {
+              node_cnt[ls * C + c] = lc;
+              node_cnt[rs * C + c] = rc;
+            }
           }
         }
       }
@@ -1571,14 +1646,15 @@ int finish_lds_bytes(int F, int B, int C) {
 }
 int finish_max_classes() { return kFinMaxC; }
 
-// Global scratch for the DFS stack's class counts (C > kFinStackC): grow-only,
-// one buffer per device (finisher launches of a device share one stream).
+// Global scratch for the DFS stack's class counts and the node's / left class
+// counts (C > kFinStackC): [grid][kFinStack + 2][C], grow-only, one buffer per
+// device (finisher launches of a device share one stream).
 static int32_t* fin_stack_scratch(int grid, int C) {
   static int32_t* buf[64] = {};
   static size_t cap[64] = {};
   int dev = 0;
   MT_HIP_CHECK(hipGetDevice(&dev));
-  const size_t need = (size_t)grid * kFinStack * C * sizeof(int32_t);
+  const size_t need = (size_t)grid * (kFinStack + 2) * C * sizeof(int32_t);
   if (dev < 0 || dev >= 64) throw std::runtime_error("finisher: device index out of range");
   if (need > cap[dev]) {
     if (buf[dev]) MT_HIP_CHECK(hipFree(buf[dev]));
@@ -1608,7 +1684,7 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   const bool c2 = C <= 2 && Ft == F && F <= kFinMaxF;
   const bool tiny_sorted = C <= 2 && getenv_int("MPITREE_TINY_SORTED", 1) != 0;
   if (code_bytes != 1 || tiny == nullptr) tiny_rows = 0;
-  if (!tiny_sorted && (F > kTinyMaxF || C > kTinyMaxC)) tiny_rows = 0;
+  if (!tiny_sorted && F > kTinyMaxF) tiny_rows = 0;
   if (tiny_sorted && tiny_sorted_lds(F, 1) > 160 * 1024) tiny_rows = 0;  // > ~1100 features
   tiny_rows = std::min(tiny_rows, kTinyRows);
   FinRowLab rl{lab_shift ? ((1u << lab_shift) - 1u) : 0xffffffffu, lab_shift};
@@ -1699,11 +1775,17 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
       }
 #undef MT_TS
     } else {
-      hipLaunchKernelGGL(finish_tiny_kernel, dim3(tiny_grid), dim3(kTinyWaves * kWave), 0,
-                         stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,
-                         counter + kFinCtrTinyCount, counter + kFinCtrTinyCount + 1, F, C, crit,
-                         max_depth, mss, msl, xtab,
-                         node_i32, node_cnt);
+#define MT_TG(MANY)                                                                          \
+  hipLaunchKernelGGL(finish_tiny_kernel<MANY>, dim3(tiny_grid), dim3(kTinyWaves * kWave), 0,  \
+                     stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,   \
+                     counter + kFinCtrTinyCount, counter + kFinCtrTinyCount + 1, F, C, crit, \
+                     max_depth, mss, msl, xtab, node_i32, node_cnt);
+      if (C > kTinyMaxC) {
+        MT_TG(true)
+      } else {
+        MT_TG(false)
+      }
+#undef MT_TG
     }
     MT_HIP_CHECK(hipGetLastError());
   }
