@@ -396,6 +396,46 @@ def test_data_sharded_agrees_with_concatenated_fit(regression):
             np.testing.assert_array_equal(o["value"], ta.count)
 
 
+def _fit_sharded_continuous(rank, world, max_bins):
+    from mpitree_amd import ParallelDecisionTreeClassifier
+    from mpitree_amd.utils.observability import tree_digest
+
+    rng = np.random.default_rng(40 + rank)  # every shard its own continuous rows
+    X = rng.normal(size=(3000, 5)) * (1 + rank)
+    y = (X[:, 0] + X[:, 1] ** 2 > 1).astype(np.int64)
+    est = ParallelDecisionTreeClassifier(strategy="data", device="cpu", max_bins=max_bins)
+    try:
+        est.fit(X, y, data_sharded=True)
+    except ValueError as e:
+        return {"error": np.array([str(e)])}
+    ta = est.tree_arrays_
+    return {"digest": np.array([tree_digest(ta)]), "nodes": np.array([ta.node_count]),
+            "acc": np.array([est.score(X, y)]), "thr": ta.threshold}
+
+
+def test_data_sharded_continuous_quantile_summary():
+    """Continuous row shards with max_bins: the per-rank summaries merge into one
+    agreed quantile table (no gather of every unique value); every rank grows
+    the same tree and its thresholds are data values of some shard."""
+    outs = run_ranks(_fit_sharded_continuous, 2, 64)
+    assert "error" not in outs[0], outs[0].get("error")
+    assert outs[0]["digest"][0] == outs[1]["digest"][0]
+    assert outs[0]["nodes"][0] > 10 and min(o["acc"][0] for o in outs) > 0.9
+    vals = np.concatenate([np.random.default_rng(40 + r).normal(size=(3000, 5)) * (1 + r)
+                           for r in range(2)]).ravel()
+    thr = outs[0]["thr"]
+    assert np.isin(thr[~np.isnan(thr)], vals).all()
+
+
+def test_data_sharded_exact_continuous_raises():
+    """max_bins=None (exact) with > 256 distinct values in a sharded feature:
+    an explicit error naming the limit and the options, on every rank."""
+    outs = run_ranks(_fit_sharded_continuous, 2, None)
+    for o in outs:
+        msg = str(o["error"][0])
+        assert "256 distinct values" in msg and "max_bins" in msg
+
+
 def test_tree_digest_covers_thresholds():
     from mpitree_amd import DecisionTreeClassifier
     from mpitree_amd.utils.observability import tree_digest
