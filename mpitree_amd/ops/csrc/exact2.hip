@@ -96,34 +96,45 @@ __device__ __forceinline__ void xe_publish(uint64_t* w, uint32_t tag, uint64_t s
 
 // Exclusive prefix of chunk q >= 1 of a segment whose status words are
 // st[-stride], ..., st[-q stride] (nearest first). Called by one whole wave:
-// lane 0 walks back, adding aggregates until the nearest inclusive prefix
-// (predecessors claimed just before this chunk, so the walk is short); every
-// lane returns the prefix. A wait beyond 2 s (a bug, never a schedule) sets
-// *watch and returns instead of hanging the GPU.
-__device__ __forceinline__ int64_t xe_lookback(const uint64_t* st, int64_t stride, int64_t q, uint32_t tag,
-                               int32_t* watch) {
+// each round reads 64 predecessors at once (lane l: st[-(d0 + l) stride]) and
+// ends at the nearest inclusive prefix once every status up to it has been
+// published, adding the aggregates before it; a window of 64 aggregates moves
+// the next one back. Every decision is a wave-uniform ballot and the loop is
+// bounded by q, so it always ends; a wait beyond 2 s (a bug, never a schedule)
+// sets *watch and returns instead of hanging the GPU. Every lane returns the
+// prefix.
+__device__ __forceinline__ int64_t xe_lookback(const uint64_t* st, int64_t stride, int q,
+                                               uint32_t tag, int32_t* watch) {
+  const int lane = lane_id();
+  q = __builtin_amdgcn_readfirstlane(q);
   int64_t acc = 0;
-  if (lane_id() == 0) {
-    const uint64_t t0 = wall_clock64();
-    bool dead = false;
-    for (int64_t d = 1; d <= q && !dead; ++d) {
-      uint64_t s;
-      for (uint32_t spins = 0;; ++spins) {
-        s = __hip_atomic_load(st - d * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)(s >> 34) == tag) break;
-        if ((spins & 63u) == 63u && wall_clock64() - t0 > 200000000ull) {
-          atomicExch(watch, 1);
-          dead = true;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (dead) break;
-      acc += (int64_t)(uint32_t)s;
-      if (((s >> 32) & 3ull) == kXeIncl) break;
+  const uint64_t t0 = wall_clock64();
+  int d0 = 1;
+  uint32_t spins = 0;
+  while (d0 <= q) {
+    const int d = d0 + lane;
+    const bool in = d <= q;
+    const uint64_t s =
+        in ? __hip_atomic_load(st - (int64_t)d * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+           : 0ull;
+    const bool ready = in && (uint32_t)(s >> 34) == tag;
+    const unsigned long long nr = __ballot(in && !ready);
+    const unsigned long long bi = __ballot(ready && ((s >> 32) & 3ull) == kXeIncl);
+    const int fi = bi ? __ffsll((long long)bi) - 1 : kWave;  // nearest inclusive prefix
+    const int fn = nr ? __ffsll((long long)nr) - 1 : kWave;  // nearest unpublished
+    if (fi < kWave ? fn > fi : nr == 0ull) {
+      acc += (int64_t)wave_sum_u32((in && lane <= fi) ? (uint32_t)s : 0u);
+      if (fi < kWave) break;
+      d0 += kWave;  // 64 aggregates (the segment's first chunk is inclusive)
+      continue;
     }
+    if ((++spins & 63u) == 0u && wall_clock64() - t0 > 200000000ull) {
+      if (lane == 0) atomicExch(watch, 1);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
   }
-  return (int64_t)__shfl((long long)acc, 0, kWave);
+  return acc;
 }
 
 // ---------------------------------------------------------------------------
@@ -410,7 +421,7 @@ __device__ __forceinline__ void xe_scan_item(const XeArgs& a, const XeLists& L, 
         if (lane == 0) xe_publish(st, a.tag, q == 0 ? kXeIncl : kXeAgg, T1);
         int64_t pre = 0;
         if (q > 0) {
-          pre = xe_lookback(st, a.F_loc, q, a.tag, a.tick + 2);
+          pre = xe_lookback(st, a.F_loc, (int)q, a.tag, a.tick + 2);
           if (lane == 0) xe_publish(st, a.tag, kXeIncl, (uint32_t)(pre + T1));
         }
         if (lane == 0) {
@@ -581,6 +592,143 @@ __device__ __forceinline__ void xe_scan_item(const XeArgs& a, const XeLists& L, 
     uint64_t* o = a.cbest + (it * a.F_loc + f) * 2;
     o[0] = bk;
     o[1] = bp;
+  }
+}
+
+// Two-class scan, one wave per (chunk item, feature) and no workgroup barriers:
+// the wave walks its 2048-entry chunk in four 512-entry rounds (8 entries per
+// lane, round-robin so loads coalesce), carrying the class-1 count from round to
+// round; a position's successor comes from the next lane (lane 63: the next row
+// of the round, or memory past it). Per round: one ballot per row gives every
+// left count, fp32 costs from the hardware log2 pick the candidates (the bound
+// of the block scan: within 2^-15 T(m) of the round's fp32 minimum -- the
+// round's exact best is among them, so the chunk's is among the rounds'), their
+// exact tie-rounded keys, and a running (key, position) minimum. Same outputs
+// (cbest per item) and carries as the block scan; waves of a workgroup take
+// different (item, feature) pairs.
+__device__ __forceinline__ void xe_scan_wave_c2(const XeArgs& a, const XeLists& L, int64_t it,
+                                                int f) {
+  const int lane = lane_id();
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const int64_t slot = L.items[it * 4 + 0], sstart = L.items[it * 4 + 1];
+  const int64_t c0 = L.items[it * 4 + 2], cn = L.items[it * 4 + 3];
+  const int64_t m = L.cnt[slot];
+  const int Cc = xe_cc(a.C);
+  const uint32_t* Ef = a.E + (int64_t)f * a.n;
+  const int64_t t0 = L.stats[slot * Cc + 0], t1 = a.C == 2 ? L.stats[slot * Cc + 1] : 0;
+  int64_t run1 = a.C == 2 ? a.carry[(it * a.F_loc + f) * Cc + 1] : 0;  // class-1 rows before
+  const double tm = xe_tl(m, a.xtab, a.xtab_n);
+  const double tu = tie_unit(tm, m);
+  const double tinv = 1.0 / tu;
+  const bool entropy = a.crit == kEntropy;
+  const float thr_pad = (float)tm * 0x1p-15f;
+  const int fg = a.f_lo + f;
+  auto t32 = [](int64_t x) -> float {
+    const float v = (float)x;  // counts < 2^24: exact
+    return x > 1 ? v * log2f(v) : 0.0f;
+  };
+  unsigned long long mine = ~0ull;
+  uint64_t mine_pos = ~0ull;
+  constexpr int kRound = kWave * kXePer;  // 512
+  for (int64_t r0 = 0; r0 < cn; r0 += kRound) {
+    uint32_t e[kXePer];
+#pragma unroll
+    for (int k = 0; k < kXePer; ++k) {
+      const int64_t i = r0 + (int64_t)k * kWave + lane;
+      e[k] = i < cn ? Ef[c0 + i] : 0xFFFFFFFFu;
+    }
+    // entries past the round: lane 63 of the last row reads its successor
+    const int64_t iend = r0 + kRound;  // first index of the next round
+    uint32_t after = 0xFFFFFFFFu;
+    if (lane == kWave - 1) {
+      if (iend < cn) after = Ef[c0 + iend];
+      else if (c0 + cn - sstart < m) after = Ef[c0 + cn];
+    }
+    unsigned long long bal[kXePer];
+    int64_t l1[kXePer];
+    bool valid[kXePer];
+#pragma unroll
+    for (int k = 0; k < kXePer; ++k) {
+      const int64_t i = r0 + (int64_t)k * kWave + lane;
+      bal[k] = __ballot(i < cn && xe_lab(e[k]) == 1);
+      l1[k] = run1 + __popcll(bal[k] & lt) + ((bal[k] >> lane) & 1ull);
+      run1 += __popcll(bal[k]);
+      // successor: next lane, or (lane 63) the next row's lane 0 / the entry after
+      uint32_t nx = (uint32_t)__shfl_down((int)e[k], 1, kWave);
+      const uint32_t row_next = k + 1 < kXePer
+                                    ? (uint32_t)__builtin_amdgcn_readlane((int)e[k + 1 < kXePer ? k + 1 : k], 0)
+                                    : after;
+      if (lane == kWave - 1) nx = (k + 1 < kXePer && i + 1 < cn) ? row_next : after;
+      const int64_t pos = c0 + i - sstart;
+      const int64_t ml = pos + 1, mr = m - ml;
+      bool v = i < cn && mr > 0 && ml >= a.msl && mr >= a.msl;
+      if (v) v = xe_boundary(e[k], nx, a, fg);
+      valid[k] = v;
+    }
+    auto exact_key = [&](int k) -> unsigned long long {
+      const int64_t pos = c0 + r0 + (int64_t)k * kWave + lane - sstart;
+      const int64_t ml = pos + 1, mr = m - ml;
+      const int64_t L1 = l1[k], L0 = ml - L1, R1 = t1 - L1, R0 = t0 - L0;
+      double cost;
+      if (entropy) {
+        const double sl = xe_tl(L0, a.xtab, a.xtab_n) + xe_tl(L1, a.xtab, a.xtab_n);
+        const double sr = xe_tl(R0, a.xtab, a.xtab_n) + xe_tl(R1, a.xtab, a.xtab_n);
+        cost = (xe_tl(ml, a.xtab, a.xtab_n) - sl) + (xe_tl(mr, a.xtab, a.xtab_n) - sr);
+      } else {
+        cost = gini_term(ml, L0 * L0 + L1 * L1) + gini_term(mr, R0 * R0 + R1 * R1);
+      }
+      const double q = __builtin_rint(cost * tinv);
+      return (unsigned long long)(q < 0.0 ? 0.0 : q);
+    };
+    float c32[kXePer];
+    float fm = __builtin_inff();
+    if (entropy) {
+#pragma unroll
+      for (int k = 0; k < kXePer; ++k) {
+        c32[k] = __builtin_inff();
+        if (!valid[k]) continue;
+        const int64_t ml = c0 + r0 + (int64_t)k * kWave + lane - sstart + 1, mr = m - ml;
+        const int64_t L1 = l1[k], L0 = ml - L1, R1 = t1 - L1, R0 = t0 - L0;
+        c32[k] = (t32(ml) - (t32(L0) + t32(L1))) + (t32(mr) - (t32(R0) + t32(R1)));
+        fm = fminf(fm, c32[k]);
+      }
+      fm = wave_min_f32_dpp(fm);
+    }
+    const float thr = fm + thr_pad;
+#pragma unroll
+    for (int k = 0; k < kXePer; ++k) {
+      if (!valid[k] || (entropy && !(c32[k] <= thr))) continue;
+      const unsigned long long key = exact_key(k);
+      const uint64_t pos = (uint64_t)(c0 + r0 + (int64_t)k * kWave + lane - sstart);
+      if (key < mine || (key == mine && pos < mine_pos)) {
+        mine = key;
+        mine_pos = pos;
+      }
+    }
+  }
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    const unsigned long long ok = __shfl_xor(mine, d, kWave);
+    const unsigned long long op = __shfl_xor(mine_pos, d, kWave);
+    if (ok < mine || (ok == mine && op < mine_pos)) {
+      mine = ok;
+      mine_pos = op;
+    }
+  }
+  if (lane == 0) {
+    uint64_t* o = a.cbest + (it * a.F_loc + f) * 2;
+    o[0] = mine;
+    o[1] = mine_pos;
+  }
+}
+
+// One wave per (chunk item, feature) pair, grid-stride over the level's pairs.
+__global__ __launch_bounds__(kXeThreads) void xe_scan_c2_kernel(XeArgs a, XeLists L) {
+  const int64_t total = (int64_t)L.ctl[1] * a.F_loc;
+  const int64_t waves = (int64_t)gridDim.x * kXeWaves;
+  for (int64_t w = (int64_t)blockIdx.x * kXeWaves + (threadIdx.x >> 6); w < total; w += waves) {
+    const int64_t wu = __builtin_amdgcn_readfirstlane((int)w);
+    xe_scan_wave_c2(a, L, wu / a.F_loc, (int)(wu % a.F_loc));
   }
 }
 
@@ -964,87 +1112,96 @@ __global__ __launch_bounds__(kXeThreads) void xe_flag_kernel(XeArgs a, XeLists c
   }
 }
 
-// xe_part: stable partition of every (split chunk, feature): the chunk's left
-// rows (flag bits gathered once), their exclusive prefix over the split's
-// earlier chunks by decoupled look-back, then the scatter -- left rows to the
-// segment's front, right rows after the split's n_left, both in list order.
-struct XePartShared {
-  uint32_t cnt[kXePer * kXeWaves];
-  uint32_t total;
-  int64_t prefix;
-};
+// xe_part: stable partition of every split segment of every feature list into
+// the other list buffer: left rows to the segment's front, right rows after
+// the split's n_left, both in list order.
+//
+// Work unit: one wave and 512 entries (a quarter of a planner chunk item), no
+// workgroup barriers. A wave claims a ticket t -> (feature t % F_loc, sub-chunk
+// t / F_loc), gathers its rows' direction bits -- from an LDS copy of the
+// n-bit flag array when it fits (n <= kXePartLdsRows: every workgroup copies it
+// once, then all gathers are LDS reads), else from global memory -- counts its
+// left rows, publishes that aggregate, takes the exclusive prefix over the
+// segment's earlier sub-chunks by look-back (xe_lookback) and scatters.
+constexpr int kXePartWaves = 16;                       // waves per workgroup
+constexpr int kXePartPer = 16;                         // entries per lane and unit
+constexpr int kXeSub = kWave * kXePartPer;             // entries per wave unit (1024)
+constexpr int kXeSubPerChunk = kXeChunk / kXeSub;      // 2
+constexpr int kXePartLdsWords = 36 * 1024;             // 144 KB of flag words in LDS
+constexpr int64_t kXePartLdsRows = (int64_t)kXePartLdsWords * 32;
+constexpr int kXePartBatch = 16;                       // tickets per claim
 
-__device__ __forceinline__ void xe_part_item(const XeArgs& a, int64_t it, int f, XePartShared& sh) {
-  const int64_t j = a.pitems[it * 4 + 0], s0 = a.pitems[it * 4 + 1];
-  const int64_t c0 = a.pitems[it * 4 + 2], cn = a.pitems[it * 4 + 3];
-  const uint32_t* Ef = a.E + (int64_t)f * a.n;
-  uint32_t* O = a.D + (int64_t)f * a.n;
-  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  const bool reg = a.C == 0;
-  uint32_t e[kXePer];
-  int64_t y[kXePer];
-#pragma unroll
-  for (int k = 0; k < kXePer; ++k) {
-    const int64_t i = (int64_t)k * kXeThreads + tid;
-    e[k] = i < cn ? Ef[c0 + i] : 0xFFFFFFFFu;
-    y[k] = (reg && i < cn) ? a.Y[(int64_t)f * a.n + c0 + i] : 0;
-  }
-  unsigned long long bal[kXePer];
-#pragma unroll
-  for (int k = 0; k < kXePer; ++k) {
-    const int64_t i = (int64_t)k * kXeThreads + tid;
-    const uint32_t r = xe_row(e[k]);
-    bal[k] = __ballot(i < cn && ((a.flag[r >> 5] >> (r & 31)) & 1u));
-    if (lane == 0) sh.cnt[k * kXeWaves + w] = (uint32_t)__popcll(bal[k]);
-  }
-  __syncthreads();
-  if (tid < kWave) {
-    const uint32_t v = tid < kXePer * kXeWaves ? sh.cnt[tid] : 0u;
-    const uint32_t incl = wave_incl_scan_dpp(v);
-    if (tid < kXePer * kXeWaves) sh.cnt[tid] = incl - v;
-    if (tid == kXePer * kXeWaves - 1) sh.total = incl;
-  }
-  __syncthreads();
-  if (w == 0) {
-    const int64_t q = (c0 - s0) / kXeChunk;  // chunk index within the split's segment
-    uint64_t* st = a.pstat + it * a.F_loc + f;
-    const uint32_t T = sh.total;
-    if (lane == 0) xe_publish(st, a.tag, q == 0 ? kXeIncl : kXeAgg, T);
-    int64_t pre = 0;
-    if (q > 0) {
-      pre = xe_lookback(st, a.F_loc, q, a.tag, a.tick + 2);
-      if (lane == 0) xe_publish(st, a.tag, kXeIncl, (uint32_t)(pre + T));
-    }
-    if (lane == 0) sh.prefix = pre;
-  }
-  __syncthreads();
-  const int64_t lb = sh.prefix;
-  const int64_t nlj = a.split[j * 4 + 3];
-#pragma unroll
-  for (int k = 0; k < kXePer; ++k) {
-    const int64_t i = (int64_t)k * kXeThreads + tid;
-    if (i >= cn) break;
-    const int64_t l = lb + sh.cnt[k * kXeWaves + w] + __popcll(bal[k] & lt);
-    const int64_t dst = ((bal[k] >> lane) & 1ull) ? s0 + l : s0 + nlj + (c0 + i - s0) - l;
-    O[dst] = e[k];
-    if (reg) a.DY[(int64_t)f * a.n + dst] = y[k];
-  }
-}
-
-__global__ __launch_bounds__(kXeThreads) void xe_part_kernel(XeArgs a, XeLists cur) {
-  __shared__ XePartShared sh;
-  __shared__ int s_t;
-  const int64_t total = (int64_t)cur.ctl[3] * a.F_loc;
-  for (;;) {
-    if (threadIdx.x == 0) s_t = atomicAdd(a.tick + 1, 1);
+template <bool kLdsFlags, bool kReg>
+__global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a, XeLists cur) {
+  extern __shared__ uint32_t s_flag[];
+  if constexpr (kLdsFlags) {
+    const int nw = (int)((a.n + 31) >> 5);
+    for (int i = threadIdx.x; i < nw; i += blockDim.x) s_flag[i] = a.flag[i];
     __syncthreads();
-    // the ticket is uniform: read it into scalar registers so every branch and
-    // loop derived from it compiles as wave-uniform (scalar) control flow
-    const int64_t t = (int64_t)__builtin_amdgcn_readfirstlane((int)s_t);
-    __syncthreads();  // (every thread has read the ticket before the next claim)
+  }
+  const uint32_t* fl = kLdsFlags ? s_flag : a.flag;
+  const int lane = lane_id();
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const int64_t total = (int64_t)cur.ctl[3] * kXeSubPerChunk * a.F_loc;
+  // tickets are claimed kXePartBatch at a time (one counter serialises its
+  // atomics: ~10 ns each) and run in order, so the wave holding the smallest
+  // unfinished ticket still never waits
+  for (int t = 0, tb = 0;; ++t) {
+    if (t == tb) {
+      int c = 0;
+      if (lane == 0) c = atomicAdd(a.tick + 1, kXePartBatch);
+      t = __builtin_amdgcn_readfirstlane(c);
+      tb = t + kXePartBatch;
+    }
     if (t >= total) break;
-    xe_part_item(a, t / a.F_loc, (int)(t % a.F_loc), sh);
+    const int f = t % a.F_loc;
+    const int u = t / a.F_loc;  // sub-chunk index over the level's partition items
+    const int it = u / kXeSubPerChunk, k = u % kXeSubPerChunk;
+    const int64_t j = a.pitems[(int64_t)it * 4 + 0], s0 = a.pitems[(int64_t)it * 4 + 1];
+    const int64_t c0 = a.pitems[(int64_t)it * 4 + 2] + (int64_t)k * kXeSub;
+    const int64_t cn = a.pitems[(int64_t)it * 4 + 3] - (int64_t)k * kXeSub;  // may be <= 0
+    if (cn <= 0) continue;  // past its segment's end: no successor reads its status
+    const uint32_t* Ef = a.E + (int64_t)f * a.n;
+    uint32_t* O = a.D + (int64_t)f * a.n;
+    uint32_t e[kXePartPer];
+    int64_t y[kReg ? kXePartPer : 1];
+#pragma unroll
+    for (int q = 0; q < kXePartPer; ++q) {
+      const int64_t i = (int64_t)q * kWave + lane;
+      e[q] = i < cn ? Ef[c0 + i] : 0xFFFFFFFFu;
+      if constexpr (kReg) y[q] = i < cn ? a.Y[(int64_t)f * a.n + c0 + i] : 0;
+    }
+    unsigned long long bal[kXePartPer];
+    uint32_t T = 0;
+#pragma unroll
+    for (int q = 0; q < kXePartPer; ++q) {
+      const int64_t i = (int64_t)q * kWave + lane;
+      const uint32_t r = xe_row(e[q]);
+      bal[q] = __ballot(i < cn && ((fl[r >> 5] >> (r & 31)) & 1u));
+      T += (uint32_t)__popcll(bal[q]);
+    }
+    // sub-chunk index within the split's segment; its status word, and the
+    // exclusive prefix of left rows over the segment's earlier sub-chunks
+    const int qs = (int)((c0 - s0) / kXeSub);
+    uint64_t* st = a.pstat + (int64_t)u * a.F_loc + f;
+    if (lane == 0) xe_publish(st, a.tag, qs == 0 ? kXeIncl : kXeAgg, T);
+    int64_t lb = 0;
+    if (qs > 0) {
+      lb = xe_lookback(st, a.F_loc, qs, a.tag, a.tick + 2);
+      if (lane == 0) xe_publish(st, a.tag, kXeIncl, (uint32_t)(lb + T));
+    }
+    const int64_t nlj = a.split[j * 4 + 3];
+#pragma unroll
+    for (int q = 0; q < kXePartPer; ++q) {
+      const int64_t i = (int64_t)q * kWave + lane;
+      const int64_t l = lb + __popcll(bal[q] & lt);
+      lb += __popcll(bal[q]);
+      if (i < cn) {
+        const int64_t dst = ((bal[q] >> lane) & 1ull) ? s0 + l : s0 + nlj + (c0 + i - s0) - l;
+        O[dst] = e[q];
+        if constexpr (kReg) a.DY[(int64_t)f * a.n + dst] = y[q];
+      }
+    }
   }
 }
 
@@ -1348,8 +1505,11 @@ void xe_level_scan(hipStream_t s, const XeArgs& a, const XeLists& cur, int items
                        dim3(kXeThreads), 0, s, a, cur);
     if (a.C == 0)
       hipLaunchKernelGGL(xe_scan_kernel<0>, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
-    else if (a.C <= 2)
-      hipLaunchKernelGGL(xe_scan_kernel<1>, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
+    else if (a.C <= 2)  // one wave per (item, feature): no workgroup barriers
+      hipLaunchKernelGGL(xe_scan_c2_kernel,
+                         dim3((unsigned)std::min<int64_t>(
+                             ((int64_t)items_bound * a.F_loc + kXeWaves - 1) / kXeWaves, 8192)),
+                         dim3(kXeThreads), 0, s, a, cur);
     else
       hipLaunchKernelGGL(xe_scan_kernel<2>, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
   }
@@ -1372,8 +1532,37 @@ void xe_flag(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_boun
 void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_bound,
                   int splits_bound) {
   if (pitems_bound <= 0 || splits_bound <= 0) return;
-  hipLaunchKernelGGL(xe_part_kernel, dim3(xe_ticket_grid(pitems_bound, a.F_loc)),
-                     dim3(kXeThreads), 0, s, a, cur);
+  int dev = 0, n_cu = 0;
+  MT_HIP_CHECK(hipGetDevice(&dev));
+  MT_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  // one workgroup of 16 wave workers per CU (the LDS flag copy is per workgroup)
+  const int64_t units = (int64_t)pitems_bound * kXeSubPerChunk * a.F_loc;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(n_cu, (units + kXePartWaves - 1) /
+                                                                          kXePartWaves));
+  static const bool lds_off = [] {  // (MPITREE_EXACT_PART_LDS=0: global flags, tests)
+    const char* v = std::getenv("MPITREE_EXACT_PART_LDS");
+    return v && v[0] == '0';
+  }();
+  if (a.n <= kXePartLdsRows && !lds_off) {
+    const size_t lds = (size_t)((a.n + 31) / 32) * 4;
+#define MT_XP(REG)                                                                            \
+  MT_HIP_CHECK(hipFuncSetAttribute((const void*)xe_part_kernel<true, REG>,                    \
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));    \
+  hipLaunchKernelGGL((xe_part_kernel<true, REG>), dim3(grid), dim3(kXePartWaves * kWave), lds, \
+                     s, a, cur);
+    if (a.C == 0) {
+      MT_XP(true)
+    } else {
+      MT_XP(false)
+    }
+#undef MT_XP
+  } else if (a.C == 0) {
+    hipLaunchKernelGGL((xe_part_kernel<false, true>), dim3(grid * 2), dim3(kXePartWaves * kWave),
+                       0, s, a, cur);
+  } else {
+    hipLaunchKernelGGL((xe_part_kernel<false, false>), dim3(grid * 2),
+                       dim3(kXePartWaves * kWave), 0, s, a, cur);
+  }
   MT_HIP_CHECK(hipGetLastError());
 }
 

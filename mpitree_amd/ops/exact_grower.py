@@ -238,7 +238,7 @@ class ExactGrower:
                 flag=torch.empty((n + 31) // 32, dtype=torch.int32, device=dev),
                 # look-back status words (tagged per fit and level: zeroed once)
                 sstat=torch.zeros((IMAX, F_loc), **i64),
-                pstat=torch.zeros((IMAX, F_loc), **i64),
+                pstat=torch.zeros((2 * IMAX, F_loc), **i64),  # (2 wave units per item)
                 tick=torch.zeros(4, **i32),
                 jobs=torch.empty((JMAX, JW), **i64),
                 job_count=torch.zeros(1, **i32),
