@@ -14,6 +14,9 @@ One JSON line per config (wall-clock per fit, samples/s, tree size):
               (the reference's search; the presorted-list exact engine), 1 GPU
   100k_exact  100k x 32 continuous, max_depth=12, exact engine, 1 GPU
   1m_reg      1M x 64 regression tree (squared error), 1 GPU
+  1m_exact_reg  1M x 64 continuous regression, exact thresholds (presorted lists), 1 GPU
+  1m_c64      1M x 64 classification with 64 classes, 1 GPU (feature-tiled finisher)
+  200k_f512   200k x 512 classification, 1 GPU (feature-tiled finisher)
   10m         10M x 128 synthetic classification, 1 GPU (the 8-GPU
               data-parallel run is bench.py under torchrun)
 
@@ -124,7 +127,7 @@ def _gpu_fit(n, F, reps, md=None, regression=False, classes=2, seed=0, levels=25
     from mpitree_amd.utils.datasets import make_classification, make_regression
 
     if regression:
-        X, y = make_regression(n, F, seed=seed)
+        X, y = make_regression(n, F, seed=seed, levels=levels)
         est = DecisionTreeRegressor(max_depth=md, device="cuda")
     else:
         X, y = make_classification(n, F, n_classes=classes, seed=seed, levels=levels)
@@ -139,7 +142,9 @@ def _gpu_fit(n, F, reps, md=None, regression=False, classes=2, seed=0, levels=25
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("names", nargs="*",
-                    default=["iris", "sweep", "sweep_gpu", "100k", "1m", "1m_reg", "10m"])
+                    default=["iris", "sweep", "sweep_gpu", "100k", "1m", "1m_exact",
+                             "100k_exact", "1m_reg", "1m_exact_reg", "1m_c64", "200k_f512",
+                             "10m"])
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args(argv)
     for name in a.names:
@@ -166,6 +171,17 @@ def main(argv=None):
         elif name == "1m_reg":
             rows = [{"config": "1M x 64 regression (squared_error), full depth, 1 GPU",
                      **_gpu_fit(1_000_000, 64, a.reps, regression=True)}]
+        elif name == "1m_exact_reg":
+            rows = [{"config": "1M x 64 continuous (randn) regression, exact thresholds, "
+                               "full depth, 1 GPU",
+                     **_gpu_fit(1_000_000, 64, max(2, a.reps // 2), regression=True,
+                                levels=None)}]
+        elif name == "1m_c64":
+            rows = [{"config": "1M x 64 classification, 64 classes, full depth, 1 GPU",
+                     **_gpu_fit(1_000_000, 64, max(2, a.reps // 2), classes=64)}]
+        elif name == "200k_f512":
+            rows = [{"config": "200k x 512 classification, full depth, 1 GPU",
+                     **_gpu_fit(200_000, 512, a.reps)}]
         elif name == "10m":
             rows = [{"config": "10M x 128 classification, full depth, 1 GPU",
                      **_gpu_fit(10_000_000, 128, max(2, a.reps // 2))}]
