@@ -224,7 +224,10 @@ class LevelwiseBuilder:
         # backend lays the tree out on the device and compacts it in one pass.
         self._device_asm = (
             hasattr(be, "begin_positions") and comm.world_size == 1 and edges is not None
-            and os.environ.get("MPITREE_DEVICE_ASSEMBLY", "1") != "0" and self.ckpt is None
+            and (os.environ.get("MPITREE_DEVICE_ASSEMBLY", "1") != "0"
+                 # (the exact engine's thresholds exist only on the device)
+                 or getattr(be, "thresholds_on_device", False))
+            and self.ckpt is None
         )
         if self._device_asm:
             be.begin_positions(2 * m_root - 1)

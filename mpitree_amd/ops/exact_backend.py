@@ -56,6 +56,8 @@ class _Frontier:
 class ExactHipBackend(HipBackend):
     """Level-wise backend over presorted feature lists (no histograms)."""
 
+    thresholds_on_device = True  # the unique values never leave the GPU: device assembly always
+
     name = "hip-exact"
     derives = False  # every frontier node is scanned from its own segment
 
