@@ -314,11 +314,13 @@ _REG_PER_CU: dict = {}  # (bins, code bytes) -> regression finisher workgroups p
 _FIN_WATCH: list = []  # pinned views of finisher watchdog words, checked at assembly
 
 
-def _task_flags(device, n: int):
+def _task_flags(device, n: int, slot: int = 0):
     """Epoch-tagged publish flags of the finisher's hand-off queue: a flag is
     set when it equals this launch's epoch, so the buffer is never cleared
-    between launches (zeroed once when it grows)."""
-    key = str(device)
+    between launches (zeroed once when it grows). Launches that can run at the
+    same time (``slot``: the early finisher batch on a side stream) own
+    separate buffers."""
+    key = f"{device}/{slot}"
     ent = _TASK_FLAGS.get(key)
     if ent is None or ent[0].numel() < n:
         ent = _TASK_FLAGS[key] = [torch.zeros(max(n, 4096), dtype=torch.int32, device=device), 0]
@@ -675,7 +677,8 @@ class HipBackend:
                     "subtree finisher: a workgroup's wait for handed-off work timed out "
                     "; the tree is incomplete")
 
-    def launch_finisher(self, d_jobs, J: int, job_rows: int, params, rec, cnt, counter=None):
+    def launch_finisher(self, d_jobs, J: int, job_rows: int, params, rec, cnt, counter=None,
+                        grid=None, slot: int = 0):
         """Launch the block + wave finisher kernels on ``J`` device jobs
         (int64 [J][5 + C] = {start, count, depth, root position, buffer, counts},
         largest first for load balance) writing into position space rec/cnt."""
@@ -685,14 +688,14 @@ class HipBackend:
         if counter is None:  # eight int32 work cursors, zero at launch
             counter = torch.zeros(128, dtype=torch.int32, device=self.device)
         if self.reg:
-            self._launch_finisher_reg(d_jobs, J, job_rows, params, rec, cnt, counter)
+            self._launch_finisher_reg(d_jobs, J, job_rows, params, rec, cnt, counter, grid, slot)
             return
         tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
         # every tiny subtree has >= 2 rows and they partition the job rows
         tiny = torch.empty((int(job_rows // 2 + J + 1), 8), dtype=torch.int64,
                            device=self.device)
         md = -1 if params.max_depth is None else int(params.max_depth)
-        grid = int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU))
+        grid = int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU)) if grid is None else int(grid)
         if C > 2:  # (the hand-off queue is on the two-class kernel only)
             grid = min(grid, J)
         # subtrees handed to idle workgroups (each > 2 tiny_rows rows, disjoint)
@@ -703,7 +706,7 @@ class HipBackend:
         elif steal == "-1":
             task_cap = -1  # no queue at all (claims past the jobs exit at once)
         tasks = torch.empty((max(task_cap, 1), 5 + C), dtype=torch.int64, device=self.device)
-        flags, epoch = _task_flags(self.device, max(task_cap, 0) + grid)
+        flags, epoch = _task_flags(self.device, max(task_cap, 0) + grid, slot)
         prof = None
         if os.environ.get("MPITREE_FIN_PROF"):
             prof = torch.zeros((grid, 10), dtype=torch.int64, device=self.device)
@@ -725,11 +728,12 @@ class HipBackend:
         if prof is not None:
             self.last_finisher_prof = prof.cpu().numpy()
 
-    def _launch_finisher_reg(self, d_jobs, J, job_rows, params, rec, st64, counter):
+    def _launch_finisher_reg(self, d_jobs, J, job_rows, params, rec, st64, counter, grid_o=None,
+                             slot=0):
         tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
         tiny = torch.empty((int(job_rows // 2 + J + 1), 8), dtype=torch.int64, device=self.device)
         md = -1 if params.max_depth is None else int(params.max_depth)
-        grid = os.environ.get("MPITREE_FIN_GRID")
+        grid = os.environ.get("MPITREE_FIN_GRID") if grid_o is None else grid_o
         if grid is None:  # as many persistent workgroups as fit a CU (LDS tile, VGPRs)
             key = (self.B, self.cb)
             if key not in _REG_PER_CU:
@@ -743,7 +747,7 @@ class HipBackend:
         elif steal == "-1":
             task_cap, grid = -1, min(grid, J)
         tasks = torch.empty((max(task_cap, 1), 7), dtype=torch.int64, device=self.device)
-        flags, epoch = _task_flags(self.device, max(task_cap, 0) + grid)
+        flags, epoch = _task_flags(self.device, max(task_cap, 0) + grid, slot)
         self.hip.finish_reg(_stream(), self.codes_rm.data_ptr(), self.row_elems * self.cb // 4,
                             self.codes_fm.data_ptr(), self.cb, self.n, self.idx.data_ptr(),
                             self.tmp.data_ptr(), self.y.data_ptr(), d_jobs.data_ptr(), J,
