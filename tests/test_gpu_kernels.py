@@ -604,3 +604,28 @@ def test_gpu_finisher_many_classes_and_features(C, F, n):
         assert st["engine"] == "hip-device-loop", st["engine"]
     assert gpu.tree_arrays_.equal(cpu.tree_arrays_), (gpu.tree_arrays_.node_count,
                                                       cpu.tree_arrays_.node_count)
+
+
+@pytest.mark.parametrize("v1", [False, True])
+def test_gpu_exact_engine_matches_reference_source(monkeypatch, v1):
+    """The GPU exact-threshold engines against the reference implementation's own
+    outputs: continuous problems (every value unique) fitted by the reference
+    source on a CPU (tools/make_reference_exact_fixtures.py; the GPU box has no
+    reference checkout). ``export_text(precision=17)`` and ``predict`` agree."""
+    import json
+    import pathlib
+    import re
+
+    monkeypatch.setenv("MPITREE_SMALL_FIT", "0")  # (<= 1024 rows: the exact list engine)
+    if v1:
+        monkeypatch.setenv("MPITREE_EXACT_V1", "1")
+    path = pathlib.Path(__file__).parent / "fixtures" / "reference_exact.json"
+    canon = lambda t: re.sub(r"-(0\.0+)\]", r"\1]", t)  # noqa: E731
+    for p in json.loads(path.read_text()):
+        X = np.asarray(p["X"])
+        y = np.asarray(p["y"])
+        g = DecisionTreeClassifier(max_depth=p["max_depth"], device="cuda").fit(
+            torch.from_numpy(X).cuda(), torch.from_numpy(y).cuda())
+        assert g.fit_stats_["engine"] == "hip-exact", g.fit_stats_["engine"]
+        assert canon(g.export_text(precision=17)) == canon(p["text"])
+        np.testing.assert_array_equal(np.asarray(g.predict(X)), np.asarray(p["predict"]))
