@@ -50,7 +50,6 @@ struct XeArgs {
   uint32_t* flag;      // [(n + 31) / 32] row-direction bits (1: left)
   // single-pass scans (decoupled look-back): per (item, feature) status words
   // {tag : 30, state : 2 (1 aggregate, 2 inclusive prefix), value : 32}
-  uint64_t* sstat;     // [IMAX][F_loc] class-1 counts (two-class split scan)
   uint64_t* pstat;     // [PMAX][F_loc] left counts (partition)
   int32_t* tick;       // [4] {scan ticket, partition ticket, watchdog, -}
   uint32_t tag;        // this level's status tag (30 bits, nonzero)

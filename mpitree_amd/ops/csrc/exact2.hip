@@ -278,50 +278,29 @@ struct XeScanShared {
   int64_t sum[kXePer * kXeWaves];
   uint64_t min[kXeWaves][2];
   float fmin[kXeWaves];
-  uint32_t total;
-  int64_t prefix;
   uint32_t e[kXeThreads * kXePer + 1];
 };
 
-// kKind: the problem kind compiled into the item (0 regression, 1 two classes,
-// 2 more classes) -- each kernel carries one path only, which keeps the
+// kKind: the problem kind compiled into the item (0 regression, 2 more than
+// two classes; two classes run xe_scan_c2_kernel) -- each kernel carries one path only, which keeps the
 // scan's register (and scalar-register) footprint to what that path needs.
 template <int kKind>
 __device__ __forceinline__ void xe_scan_item(const XeArgs& a, const XeLists& L, int64_t it, int f,
-                                             XeScanShared& sh, bool lb);
+                                             XeScanShared& sh);
 
 template <int kKind>
 __global__ __launch_bounds__(kXeThreads) void xe_scan_kernel(XeArgs a, XeLists L) {
   __shared__ XeScanShared sh;
   const int NI = L.ctl[1];
   for (int64_t it = blockIdx.x; it < NI; it += gridDim.x) {
-    xe_scan_item<kKind>(a, L, it, blockIdx.y, sh, false);
+    xe_scan_item<kKind>(a, L, it, blockIdx.y, sh);
     __syncthreads();
-  }
-}
-
-// Two classes: the class-1 carry of every chunk comes from a decoupled
-// look-back inside the scan (no xe_tot / xe_carry pass over the lists); the
-// chunk's carries are stored for xe_select as the two-pass path would.
-__global__ __launch_bounds__(kXeThreads) void xe_scan_lb_kernel(XeArgs a, XeLists L) {
-  __shared__ XeScanShared sh;
-  __shared__ int s_t;
-  const int64_t total = (int64_t)L.ctl[1] * a.F_loc;
-  for (;;) {
-    if (threadIdx.x == 0) s_t = atomicAdd(a.tick, 1);
-    __syncthreads();
-    // the ticket is uniform: read it into scalar registers so every branch and
-    // loop derived from it compiles as wave-uniform (scalar) control flow
-    const int64_t t = (int64_t)__builtin_amdgcn_readfirstlane((int)s_t);
-    __syncthreads();  // (every thread has read the ticket before the next claim)
-    if (t >= total) break;
-    xe_scan_item<1>(a, L, t / a.F_loc, (int)(t % a.F_loc), sh, true);
   }
 }
 
 template <int kKind>
 __device__ __forceinline__ void xe_scan_item(const XeArgs& a, const XeLists& L, int64_t it, int f,
-                                             XeScanShared& sh, bool lb) {
+                                             XeScanShared& sh) {
   uint32_t* s_cnt = sh.cnt;
   int64_t* s_sum = sh.sum;
   uint64_t (*s_min)[2] = sh.min;
@@ -394,116 +373,6 @@ __device__ __forceinline__ void xe_scan_item(const XeArgs& a, const XeLists& L, 
         mine = key;
         mine_pos = (uint64_t)pos;
       }
-    }
-  } else if constexpr (kKind == 1) {
-    // ---- two classes: one ballot scan of class 1 gives every side count
-    unsigned long long bal[kXePer];
-#pragma unroll
-    for (int k = 0; k < kXePer; ++k) {
-      const int64_t i = (int64_t)k * kXeThreads + tid;
-      bal[k] = __ballot(i < cn && xe_lab(e[k]) == 1);
-      if (lane == 0) s_cnt[k * kXeWaves + wave] = (uint32_t)__popcll(bal[k]);
-    }
-    __syncthreads();
-    if (tid < kWave) {
-      const uint32_t v = tid < kXePer * kXeWaves ? s_cnt[tid] : 0u;
-      const uint32_t incl = wave_incl_scan_dpp(v);
-      if (tid < kXePer * kXeWaves) s_cnt[tid] = incl - v;
-      if (tid == kXePer * kXeWaves - 1) sh.total = incl;
-    }
-    __syncthreads();
-    int64_t base1;
-    if (lb) {
-      if (wave == 0) {
-        const int64_t q = (c0 - sstart) / kXeChunk;  // chunk index within the segment
-        uint64_t* st = a.sstat + it * a.F_loc + f;
-        const uint32_t T1 = sh.total;
-        if (lane == 0) xe_publish(st, a.tag, q == 0 ? kXeIncl : kXeAgg, T1);
-        int64_t pre = 0;
-        if (q > 0) {
-          pre = xe_lookback(st, a.F_loc, (int)q, a.tag, a.tick + 2);
-          if (lane == 0) xe_publish(st, a.tag, kXeIncl, (uint32_t)(pre + T1));
-        }
-        if (lane == 0) {
-          sh.prefix = pre;
-          int64_t* car = a.carry + (it * a.F_loc + f) * Cc;  // xe_select's chunk carries
-          car[0] = (c0 - sstart) - pre;
-          if (a.C == 2) car[1] = pre;
-        }
-      }
-      __syncthreads();
-      base1 = a.C == 2 ? sh.prefix : 0;
-    } else {
-      base1 = a.C == 2 ? a.carry[(it * a.F_loc + f) * Cc + 1] : 0;
-    }
-    const int64_t t0 = L.stats[slot * Cc + 0], t1 = a.C == 2 ? L.stats[slot * Cc + 1] : 0;
-    int64_t l1[kXePer];
-#pragma unroll
-    for (int k = 0; k < kXePer; ++k)
-      l1[k] = base1 + s_cnt[k * kXeWaves + wave] + __popcll(bal[k] & lt) + ((bal[k] >> lane) & 1ull);
-    const double tm = xe_tl(m, a.xtab, a.xtab_n);
-    const double tu = tie_unit(tm, m);
-    const double tinv = 1.0 / tu;
-    auto exact_key = [&](int k) -> unsigned long long {
-      const int64_t pos = c0 + (int64_t)k * kXeThreads + tid - sstart;
-      const int64_t ml = pos + 1, mr = m - ml;
-      const int64_t L1 = l1[k], L0 = ml - L1, R1 = t1 - L1, R0 = t0 - L0;
-      double cost;
-      if (a.crit == kEntropy) {
-        const double sl = xe_tl(L0, a.xtab, a.xtab_n) + xe_tl(L1, a.xtab, a.xtab_n);
-        const double sr = xe_tl(R0, a.xtab, a.xtab_n) + xe_tl(R1, a.xtab, a.xtab_n);
-        cost = (xe_tl(ml, a.xtab, a.xtab_n) - sl) + (xe_tl(mr, a.xtab, a.xtab_n) - sr);
-      } else {
-        cost = gini_term(ml, L0 * L0 + L1 * L1) + gini_term(mr, R0 * R0 + R1 * R1);
-      }
-      double q = __builtin_rint(cost * tinv);
-      return (unsigned long long)(q < 0.0 ? 0.0 : q);
-    };
-    auto take = [&](int k) {
-      const unsigned long long key = exact_key(k);
-      const uint64_t pos = (uint64_t)(c0 + (int64_t)k * kXeThreads + tid - sstart);
-      if (key < mine || (key == mine && pos < mine_pos)) {
-        mine = key;
-        mine_pos = pos;
-      }
-    };
-    if (a.crit == kEntropy) {
-      // Pass 1: fp32 costs from the hardware log2 (no table reads). Each term
-      // T(x) <= T(m) carries <= 1.25 * 2^-22 relative error (log2f <= 2 ulp,
-      // one rounded product) and the five sums <= 2^-24 T(m) each, so
-      // |fp32 - exact| <= 2^-18.8 T(m). The chunk's exact best (tie-rounded,
-      // then lowest position) has an fp32 cost <= the chunk's fp32 minimum +
-      // 2^-17.8 T(m) + the tie grid (2^-31 T(m)): pass 2 scores in fp64 (six
-      // table reads) only positions within 2^-15 T(m) of the fp32 minimum.
-      auto t32 = [](int64_t x) -> float {
-        const float f = (float)x;  // counts < 2^24: exact
-        return x > 1 ? f * log2f(f) : 0.0f;
-      };
-      float c32[kXePer];
-      float fm = __builtin_inff();
-#pragma unroll
-      for (int k = 0; k < kXePer; ++k) {
-        c32[k] = __builtin_inff();
-        if (!valid[k]) continue;
-        const int64_t ml = c0 + (int64_t)k * kXeThreads + tid - sstart + 1, mr = m - ml;
-        const int64_t L1 = l1[k], L0 = ml - L1, R1 = t1 - L1, R0 = t0 - L0;
-        c32[k] = (t32(ml) - (t32(L0) + t32(L1))) + (t32(mr) - (t32(R0) + t32(R1)));
-        fm = fminf(fm, c32[k]);
-      }
-      fm = wave_min_f32_dpp(fm);
-      if (lane == 0) sh.fmin[wave] = fm;
-      __syncthreads();
-      fm = sh.fmin[0];
-#pragma unroll
-      for (int w = 1; w < kXeWaves; ++w) fm = fminf(fm, sh.fmin[w]);
-      const float thr = fm + (float)tm * 0x1p-15f;
-#pragma unroll
-      for (int k = 0; k < kXePer; ++k)
-        if (valid[k] && c32[k] <= thr) take(k);
-    } else {  // gini: exact integer-form costs are a few flops
-#pragma unroll
-      for (int k = 0; k < kXePer; ++k)
-        if (valid[k]) take(k);
     }
   } else {
     // ---- C > 2: per class, one block scan of the class indicator
@@ -1477,42 +1346,25 @@ static int xe_gx(int items_bound, int F_loc) {
   return std::max(1, std::min(items_bound, cap));
 }
 
-// Workgroups of a ticketed kernel: enough to fill the chip (8 per CU), never
-// more than the (item, feature) pairs.
-static int xe_ticket_grid(int items_bound, int F_loc) {
-  return (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)items_bound * F_loc, 2048));
-}
-
 void xe_level_scan(hipStream_t s, const XeArgs& a, const XeLists& cur, int items_bound,
                    int slots_bound) {
   if (items_bound <= 0 || slots_bound <= 0) return;
   const int Cc = xe_cc(a.C);
-  // MPITREE_EXACT_SCAN_LB=1: the single-pass two-class scan (ticketed chunks,
-  // look-back carries; experimental -- see profiles/kernel_experiments.md).
-  // Default: chunk totals, carries, then the scan.
-  static const bool lb = [] {
-    const char* v = std::getenv("MPITREE_EXACT_SCAN_LB");
-    return v && v[0] == '1';
-  }();
-  if ((a.C == 1 || a.C == 2) && lb) {
-    hipLaunchKernelGGL(xe_scan_lb_kernel, dim3(xe_ticket_grid(items_bound, a.F_loc)),
+  // chunk totals, carries, then the scan
+  const int gx = xe_gx(items_bound, a.F_loc);
+  hipLaunchKernelGGL(xe_tot_kernel, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
+  const int64_t nc = (int64_t)slots_bound * a.F_loc * Cc;
+  hipLaunchKernelGGL(xe_carry_kernel, dim3((unsigned)((nc + kXeThreads - 1) / kXeThreads)),
+                     dim3(kXeThreads), 0, s, a, cur);
+  if (a.C == 0)
+    hipLaunchKernelGGL(xe_scan_kernel<0>, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
+  else if (a.C <= 2)  // one wave per (item, feature): no workgroup barriers
+    hipLaunchKernelGGL(xe_scan_c2_kernel,
+                       dim3((unsigned)std::min<int64_t>(
+                           ((int64_t)items_bound * a.F_loc + kXeWaves - 1) / kXeWaves, 8192)),
                        dim3(kXeThreads), 0, s, a, cur);
-  } else {
-    const int gx = xe_gx(items_bound, a.F_loc);
-    hipLaunchKernelGGL(xe_tot_kernel, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
-    const int64_t nc = (int64_t)slots_bound * a.F_loc * Cc;
-    hipLaunchKernelGGL(xe_carry_kernel, dim3((unsigned)((nc + kXeThreads - 1) / kXeThreads)),
-                       dim3(kXeThreads), 0, s, a, cur);
-    if (a.C == 0)
-      hipLaunchKernelGGL(xe_scan_kernel<0>, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
-    else if (a.C <= 2)  // one wave per (item, feature): no workgroup barriers
-      hipLaunchKernelGGL(xe_scan_c2_kernel,
-                         dim3((unsigned)std::min<int64_t>(
-                             ((int64_t)items_bound * a.F_loc + kXeWaves - 1) / kXeWaves, 8192)),
-                         dim3(kXeThreads), 0, s, a, cur);
-    else
-      hipLaunchKernelGGL(xe_scan_kernel<2>, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
-  }
+  else
+    hipLaunchKernelGGL(xe_scan_kernel<2>, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
   hipLaunchKernelGGL(xe_select_kernel, dim3(slots_bound), dim3(kXeThreads), 0, s, a, cur);
   MT_HIP_CHECK(hipGetLastError());
 }

@@ -97,7 +97,6 @@ void bind_exact2(py::module_& m) {
         a.pitems = ptr<int64_t>(u("pitems"));
         a.pfirst = ptr<int32_t>(u("pfirst"));
         a.flag = ptr<uint32_t>(u("flag"));
-        a.sstat = ptr<uint64_t>(u("sstat"));
         a.pstat = ptr<uint64_t>(u("pstat"));
         a.tick = ptr<int32_t>(u("tick"));
         a.tag = 1;

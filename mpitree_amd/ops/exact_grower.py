@@ -237,7 +237,6 @@ class ExactGrower:
                 pfirst=torch.empty(KMAX + 1, **i32),
                 flag=torch.empty((n + 31) // 32, dtype=torch.int32, device=dev),
                 # look-back status words (tagged per fit and level: zeroed once)
-                sstat=torch.zeros((IMAX, F_loc), **i64),
                 pstat=torch.zeros((2 * IMAX, F_loc), **i64),  # (2 wave units per item)
                 tick=torch.zeros(4, **i32),
                 jobs=torch.empty((JMAX, JW), **i64),
@@ -255,7 +254,7 @@ class ExactGrower:
             xtab=be.xtab.data_ptr(), xtab_n=int(be.xtab.numel()), tot=ptr["tot"],
             carry=ptr["carry"],
             cmm=ptr["cmm"], cbest=ptr["cbest"], rec=ptr["rec"], split=ptr["split"],
-            pitems=ptr["pitems"], pfirst=ptr["pfirst"], flag=ptr["flag"], sstat=ptr["sstat"],
+            pitems=ptr["pitems"], pfirst=ptr["pfirst"], flag=ptr["flag"],
             pstat=ptr["pstat"], tick=ptr["tick"], pos_rec=be.pos_rec.data_ptr(),
             pos_st=be.pos_st.data_ptr(), pos_thr=pos_thr.data_ptr(), jobs=ptr["jobs"],
             job_count=ptr["job_count"], max_depth=md, mss=mss, fr=fr), lp[0], lp[1])
@@ -299,10 +298,10 @@ class ExactGrower:
             if _DEBUG_SYNC:  # (MPITREE_EXACT_SYNC=1: sync + report every level)
                 torch.cuda.synchronize(dev)
                 ni = int(L[lvl % 2]["ctl"][1])
-                st = ws["sstat"][: min(ni, 4)].cpu().numpy().astype(np.uint64)
+                st = ws["pstat"][: min(ni, 4)].cpu().numpy().astype(np.uint64)
                 print(f"exact level {lvl}: next frontier {int(L[(lvl + 1) % 2]['ctl'][0])}, "
                       f"jobs {int(ws['job_count'][0])}, tickets {ws['tick'].tolist()}, "
-                      f"items {ni}, status tags {(st >> np.uint64(34)).tolist()} "
+                      f"items {ni}, partition status tags {(st >> np.uint64(34)).tolist()} "
                       f"states {((st >> np.uint64(32)) & np.uint64(3)).tolist()}", flush=True)
             lvl += 1
             if lvl >= 2:
