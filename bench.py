@@ -65,6 +65,8 @@ def main(argv=None):
     ap.add_argument("--regression", action="store_true")
     ap.add_argument("--continuous", action="store_true",
                     help="N(0,1) features: exact thresholds over every unique value")
+    ap.add_argument("--max-bins", type=int, default=0,
+                    help="> 0: quantile bins (e.g. 1024 with --continuous: 16-bit codes)")
     ap.add_argument("--profile-levels", action="store_true")
     a = ap.parse_args(argv)
 
@@ -91,6 +93,7 @@ def main(argv=None):
         X, y = make_classification(a.n, a.features, n_classes=a.classes, levels=levels, seed=0,
                                    device=dev)
         crit = a.criterion
+    mb = {"max_bins": a.max_bins} if a.max_bins > 0 else {}
     if world > 1:
         import torch.distributed as dist
 
@@ -98,11 +101,11 @@ def main(argv=None):
 
         init_distributed(backend=backend)
         cls = ParallelDecisionTreeRegressor if a.regression else ParallelDecisionTreeClassifier
-        est = cls(max_depth=md, criterion=crit, device="cuda", strategy=a.strategy)
+        est = cls(max_depth=md, criterion=crit, device="cuda", strategy=a.strategy, **mb)
     else:
         dist = None
         cls = DecisionTreeRegressor if a.regression else DecisionTreeClassifier
-        est = cls(max_depth=md, criterion=crit, device="cuda")
+        est = cls(max_depth=md, criterion=crit, device="cuda", **mb)
 
     def barrier():
         if dist is not None:
@@ -180,7 +183,8 @@ def main(argv=None):
                 + int(stats.get("comm_bytes_exchange", 0)),
                 "tree_nodes": stats.get("node_count"),
                 "tree_depth": stats.get("max_depth"),
-                "thresholds": stats.get("thresholds", "exact (<= 256 values per feature)"),
+                "thresholds": (f"quantile ({a.max_bins} bins)" if a.max_bins > 0 else
+                               stats.get("thresholds", "exact (<= 256 values per feature)")),
                 "comm_bytes_per_level": stats.get("comm_bytes_per_level"),
                 "peak_device_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 3),
             },

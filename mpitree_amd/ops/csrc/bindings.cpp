@@ -46,6 +46,7 @@ void launch_finish(hipStream_t, const void*, int64_t, const void*, int, int64_t,
                    int32_t*, int32_t*, int64_t*, int32_t*, int32_t, int, int, int, int64_t*, int,
                    int64_t*);
 int finish_lds_bytes(int F, int B, int C);
+void launch_hw_xlog2x(hipStream_t, float*, int);
 int finish_feature_tile(int F, int B, int C);
 int asm_tiles(int64_t P);
 void launch_grow_plan(hipStream_t, const PlanArgs&);
@@ -435,6 +436,9 @@ PYBIND11_MODULE(_hip, m) {
   mt::bind_exact2(m);
   m.def("xlog2x_device", [](uintptr_t s, uintptr_t out, int64_t n) {
     mt::launch_xlog2x(S(s), P<double>(out), n);
+  });
+  m.def("hw_xlog2x_device", [](uintptr_t s, uintptr_t out, int n) {
+    mt::launch_hw_xlog2x(S(s), P<float>(out), n);
   });
   m.def("xlog2x_host", [](py::array_t<int64_t> x) {
     auto in = x.unchecked<1>();

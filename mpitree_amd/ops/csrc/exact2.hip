@@ -464,6 +464,12 @@ __device__ __forceinline__ void xe_scan_item(const XeArgs& a, const XeLists& L, 
   }
 }
 
+#ifndef MT_XE_HWLOG
+#define MT_XE_HWLOG 1
+#endif
+#ifndef MT_XE_PAD
+#define MT_XE_PAD -15
+#endif
 // Two-class scan, one wave per (chunk item, feature) and no workgroup barriers:
 // the wave walks its 2048-entry chunk in four 512-entry rounds (8 entries per
 // lane, round-robin so loads coalesce), carrying the class-1 count from round to
@@ -490,11 +496,21 @@ __device__ __forceinline__ void xe_scan_wave_c2(const XeArgs& a, const XeLists& 
   const double tu = tie_unit(tm, m);
   const double tinv = 1.0 / tu;
   const bool entropy = a.crit == kEntropy;
-  const float thr_pad = (float)tm * 0x1p-15f;
+  // candidates: within 2^MT_XE_PAD T(m) of the round's fp32 minimum (the terms'
+  // error is <= 35 * 2^-24 T(m), so any pad >= 2^-17 is safe; -15 .. -18 measured
+  // the same: profiles/kernel_experiments.md)
+  const float thr_pad = (float)tm * __builtin_ldexpf(1.0f, MT_XE_PAD);
   const int fg = a.f_lo + f;
   auto t32 = [](int64_t x) -> float {
     const float v = (float)x;  // counts < 2^24: exact
+#if MT_XE_HWLOG
+    // hardware log2 (v_log_f32, |error| <= 4 * 2^-24 * x log2 x, checked for
+    // x < 2^22 by tests/test_gpu_kernels.py::test_hw_log_terms_error_bound):
+    // six terms err by far less than the 2^-15 T(m) pad
+    return x > 1 ? v * __builtin_amdgcn_logf(v) : 0.0f;
+#else
     return x > 1 ? v * log2f(v) : 0.0f;
+#endif
   };
   unsigned long long mine = ~0ull;
   uint64_t mine_pos = ~0ull;

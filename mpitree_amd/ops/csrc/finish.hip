@@ -44,6 +44,7 @@ constexpr int kFinThreadsWide = 1024;  // one workgroup per CU (F = 128 histogra
 constexpr int kFinStack = 40;    // >= log2(max job rows) + 2
 constexpr int kFinMaxC = 256;    // classes supported by the block finisher
 constexpr int kFinStackC = 16;   // C <= this: DFS-stack class counts in LDS, else global scratch
+constexpr int kFinMaxB = 4096;   // bins (16-bit codes past 256: multi-pass scans, feature tiles)
 constexpr int kTinyMaxC = 16;    // classes supported by the generic tiny kernel
 constexpr int kFinTab = 1024;    // LDS x*log2(x) entries
 // MT_FIN_UNROLL / MT_FIN_PAIR / MT_TINY_SMALL: compile-time overrides for variant
@@ -611,7 +612,14 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         int best_bin = 0x7fffffff;
         const double tu = tie_unit(tl((uint64_t)m), (int64_t)m);
         const double tinv = 1.0 / tu;
-        const int b0 = lane * 4;
+        // B > 256 (16-bit codes): 256-bin passes, each class's left count carried
+        // from pass to pass in this wave's LDS words (wave-uniform values)
+        int32_t* const carry = reinterpret_cast<int32_t*>(hist + Ft * fstride) + wave * C;
+        const bool multi = nb > kWave * 4;
+        if (multi)
+          for (int c = lane; c < C; c += kWave) carry[c] = 0;
+        for (int bc = 0; bc < nb; bc += kWave * 4) {
+        const int b0 = bc + lane * 4;
         uint32_t mL[4] = {0, 0, 0, 0}, ne[4] = {0, 0, 0, 0};
         double sL[4] = {0.0, 0.0, 0.0, 0.0}, sR[4] = {0.0, 0.0, 0.0, 0.0};
         int64_t qL[4] = {0, 0, 0, 0}, qR[4] = {0, 0, 0, 0};
@@ -635,7 +643,13 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
             p[2] = p[1] + vv[2];
             p[3] = p[2] + vv[3];
             const uint32_t incl = wave_incl_scan_dpp(p[3]);
-            const uint32_t excl = incl - p[3];
+            uint32_t excl = incl - p[3];
+            if (multi) {  // + the class's rows in the earlier passes
+              const uint32_t cin = (uint32_t)carry[c];
+              excl += cin;
+              const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+              if (lane == 0) carry[c] = (int32_t)(cin + tot);
+            }
             const uint32_t tc = (uint32_t)s_cnt[c];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -671,7 +685,11 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
             }
           }
         }
-        wave_argmin_dpp(best_cost, best_bin);  // single 256-bin pass: lanes own ascending bins
+        }  // 256-bin passes
+        if (multi)
+          wave_argmin(best_cost, best_bin);  // (cost, bin): lanes' bins interleave across passes
+        else
+          wave_argmin_dpp(best_cost, best_bin);  // single 256-bin pass: lanes own ascending bins
         if (best_cost < __builtin_inf()) {
           const double g = pterm - best_cost;
           if (g > bg) {  // features visited in increasing order: strict > keeps the lowest
@@ -1630,7 +1648,7 @@ static int tiny_sorted_waves(int F) {
 // that leaves fewer than 4 features per tile (many classes) -- for one
 // 1024-thread workgroup per CU (<= 140 KB).
 int finish_feature_tile(int F, int B, int C) {
-  if (F <= 0 || C > kFinMaxC || B > 256) return 0;
+  if (F <= 0 || C > kFinMaxC || B <= 0 || B > kFinMaxB) return 0;
   const int per_f = fin_fstride(B, (C + 1) / 2) * 4;
   if (F <= kFinMaxF && F * per_f <= 150 * 1024) return F;
   int ft = 62 * 1024 / per_f;
@@ -1642,7 +1660,9 @@ int finish_feature_tile(int F, int B, int C) {
   return std::min(ft, F);
 }
 int finish_lds_bytes(int F, int B, int C) {
-  return finish_feature_tile(F, B, C) * fin_fstride(B, (C + 1) / 2) * 4;
+  // + per-wave class carries of the multi-pass (B > 256) scan
+  return finish_feature_tile(F, B, C) * fin_fstride(B, (C + 1) / 2) * 4 +
+         (B > 256 ? (kFinThreadsWide / kWave) * C * 4 : 0);
 }
 int finish_max_classes() { return kFinMaxC; }
 
@@ -1681,7 +1701,7 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   if (Ft <= 0) throw std::runtime_error("finisher: unsupported shape (C > 256 or B > 256)");
   // the two-class kernel (fp32 prefilter, hand-off queue) needs the single-pass
   // layout (Ft == F <= kFinMaxF: per-feature LDS arrays)
-  const bool c2 = C <= 2 && Ft == F && F <= kFinMaxF;
+  const bool c2 = C <= 2 && Ft == F && F <= kFinMaxF && B <= 256;
   const bool tiny_sorted = C <= 2 && getenv_int("MPITREE_TINY_SORTED", 1) != 0;
   if (code_bytes != 1 || tiny == nullptr) tiny_rows = 0;
   if (!tiny_sorted && F > kTinyMaxF) tiny_rows = 0;

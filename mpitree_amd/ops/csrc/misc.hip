@@ -19,6 +19,23 @@ void launch_xlog2x(hipStream_t stream, double* out, int64_t n) {
   MT_HIP_CHECK(hipGetLastError());
 }
 
+// x * log2(x) in fp32 from the hardware log2 (v_log_f32), as the exact
+// engine's two-class prefilter computes its terms (exact2.hip): the error bound
+// its margin assumes is checked against the fp64 table for every x < n.
+__global__ void hw_xlog2x_kernel(float* __restrict__ out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const float f = (float)i;
+    out[i] = i > 1 ? f * __builtin_amdgcn_logf(f) : 0.0f;
+  }
+}
+
+void launch_hw_xlog2x(hipStream_t stream, float* out, int n) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(hw_xlog2x_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, out, n);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
 // ---- device-resident class labels (core/fit.py prepare path) --------------
 // The reference encodes labels with np.unique on every rank
 // (mpitree/tree/decision_tree.py:418-421); here an int64 label column on the

@@ -551,14 +551,11 @@ class HipBackend:
 
     # -------------------------------------------------------------- finisher
     def finisher_supported(self) -> bool:
-        if self.B > 256:
-            return False
         if self.reg:
-            return self.F <= 256
-        if self.cb != 1:
-            return False
-        # C <= 256, any F: the block finisher tiles features (and classes' words)
-        # through LDS when one node's histogram does not fit in one pass
+            return self.B <= 256 and self.F <= 256
+        # C <= 256, any F, B <= 4096 (16-bit codes past 256 bins: multi-pass
+        # scans): the block finisher tiles features (and classes' words) through
+        # LDS when one node's histogram does not fit in one pass
         return self.hip.finish_feature_tile(self.F, self.B, self.C) > 0
 
     # finisher jobs index the x*log2(x) table with row counts: keep them below it

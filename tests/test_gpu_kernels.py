@@ -31,6 +31,22 @@ def test_xlog2x_device_matches_host_bitwise():
     assert np.array_equal(dev.view(np.int64), host.view(np.int64))
 
 
+def test_hw_log_terms_error_bound():
+    # the exact engine's two-class fp32 prefilter (exact2.hip) computes its terms
+    # as x * v_log_f32(x); its 2^-15 T(m) margin assumes |error| <= 4 * 2^-24 *
+    # x log2 x for every count (checked here up to 2^22) and exact zeros at 0, 1
+    from mpitree_amd.ops import native
+
+    n = 1 << 22
+    out = torch.empty(n, dtype=torch.float32, device="cuda")
+    native.hip().hw_xlog2x_device(torch.cuda.current_stream().cuda_stream, out.data_ptr(), n)
+    dev = out.cpu().numpy().astype(np.float64)
+    exact = xlog2x(np.arange(n, dtype=np.int64))
+    assert dev[0] == 0.0 and dev[1] == 0.0
+    rel = np.abs(dev[2:] - exact[2:]) / exact[2:]
+    assert rel.max() <= 4 * 2.0 ** -24, rel.max()
+
+
 @pytest.mark.parametrize("crit", ["entropy", "gini"])
 @pytest.mark.parametrize("seed", range(4))
 def test_gpu_classifier_matches_oracle(crit, seed):
@@ -327,6 +343,29 @@ def test_gpu_device_loop_matches_host_loop(monkeypatch, seed, max_depth):
     monkeypatch.setenv("MPITREE_DEVICE_LOOP", "1")
     r1 = fit_tree(X, y, **kw)
     assert r1.engine == "hip-device-loop"
+    monkeypatch.setenv("MPITREE_DEVICE_LOOP", "0")
+    r2 = fit_tree(X, y, **kw)
+    assert r2.engine == "hip-levelwise"
+    assert r1.arrays.equal(r2.arrays)
+    assert np.array_equal(r1.arrays.impurity, r2.arrays.impurity)
+
+
+@pytest.mark.parametrize("C,crit,levels", [(2, 0, 1000), (3, 1, 600), (2, 1, 4000), (5, 0, 300)])
+def test_gpu_device_loop_wide_bins(monkeypatch, C, crit, levels):
+    """More than 256 bins (16-bit codes): the device level loop and the block
+    finisher's multi-pass scans (finish.hip) == the host-driven builder."""
+    from mpitree_amd.core.fit import fit_tree
+
+    rng = np.random.default_rng(levels + C)
+    n, F = 60000, 7
+    X = rng.integers(0, levels, size=(n, F)).astype(np.float32)
+    y = (X[:, 0] * 3 // levels + X[:, 1] * 2 // levels + rng.integers(0, 2, size=n)) % C
+    kw = dict(regression=False, criterion=crit, max_depth=None, min_samples_split=2,
+              device="cuda", max_bins=4096)
+    monkeypatch.setenv("MPITREE_DEVICE_LOOP", "1")
+    r1 = fit_tree(X, y, **kw)
+    assert r1.engine == "hip-device-loop"
+    assert r1.stats["finisher_subtrees"] > 0
     monkeypatch.setenv("MPITREE_DEVICE_LOOP", "0")
     r2 = fit_tree(X, y, **kw)
     assert r2.engine == "hip-levelwise"
