@@ -42,6 +42,8 @@ struct XeArgs {
   int64_t* carry;      // [IMAX][F_loc][Cc]
   int64_t* cmm;        // [IMAX][2] chunk target min / max (regression, local feature 0)
   uint64_t* cbest;     // [IMAX][F_loc][2] chunk best {cost key, position}
+  uint32_t* cmin;      // [IMAX][F_loc] two-pass scan: chunk fp32 minimum (ordered bits)
+  uint32_t* nmin;      // [KMAX][F_loc] two-pass scan: node fp32 minimum per feature
   int64_t* rec;        // [KMAX][R] split records, R = 6 + (C or 1) + 1
   // partition
   int64_t* split;      // [SMAX][4] {start, count, feature (global), n_left}

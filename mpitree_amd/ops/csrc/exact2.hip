@@ -237,6 +237,7 @@ __global__ __launch_bounds__(kXeThreads) void xe_carry_kernel(XeArgs a, XeLists 
   const int f = (int)((g / Cc) % a.F_loc);
   const int64_t slot = g / ((int64_t)Cc * a.F_loc);
   const int i0 = L.ifirst[slot], i1 = L.ifirst[slot + 1];
+  if (k == 0 && a.nmin) a.nmin[slot * a.F_loc + f] = 0xffffffffu;  // (two-pass scan)
   int64_t acc = 0;
   for (int it = i0; it < i1; ++it) {
     const int64_t o = ((int64_t)it * a.F_loc + f) * Cc + k;
@@ -464,49 +465,73 @@ __device__ __forceinline__ void xe_scan_item(const XeArgs& a, const XeLists& L, 
   }
 }
 
+// Two-class scan, one wave per (chunk item, feature) and no workgroup barriers:
+// the wave walks its 2048-entry chunk in four 512-entry rounds (8 entries per
+// lane, round-robin so loads coalesce), carrying the class-1 count from round to
+// round; a position's successor comes from the next lane (lane 63: the next row
+// of the round, or memory past it). Per round: one ballot per row gives every
+// left count, fp32 costs from the hardware log2 pick the candidates, their exact
+// tie-rounded keys, and a running (key, position) minimum. Same outputs (cbest
+// per item) and carries as the block scan; waves of a workgroup take different
+// (item, feature) pairs. Per-position arithmetic is 32-bit (rows < 2^24).
+//
+// kPass 0 (gini; or entropy with MT_XE_TWO_PASS=0): candidates within the pad of
+//   the ROUND's fp32 minimum -- near a flat optimum a round's costs all lie
+//   within the pad, so nearly every position pays an exact key.
+// kPass 1 (entropy): fp32 costs only; the chunk's minimum over valid positions
+//   -> cmin[item][f], and an atomic minimum per (node, feature) -> nmin.
+// kPass 2 (entropy): G = the node's fp32 minimum over this rank's features.
+//   The node's exact best b satisfies c32(b) <= exact(b) + err <= exact(p) + err
+//   <= c32(p) + 2 err for the valid position p attaining G, so only chunks with
+//   cmin <= G + pad (pad >= 2 err) can hold it: every other chunk writes an
+//   empty record without reading its entries, and a candidate chunk keys only
+//   positions with c32 <= G + pad.
 #ifndef MT_XE_HWLOG
 #define MT_XE_HWLOG 1
 #endif
 #ifndef MT_XE_PAD
 #define MT_XE_PAD -15
 #endif
-// Two-class scan, one wave per (chunk item, feature) and no workgroup barriers:
-// the wave walks its 2048-entry chunk in four 512-entry rounds (8 entries per
-// lane, round-robin so loads coalesce), carrying the class-1 count from round to
-// round; a position's successor comes from the next lane (lane 63: the next row
-// of the round, or memory past it). Per round: one ballot per row gives every
-// left count, fp32 costs from the hardware log2 pick the candidates (the bound
-// of the block scan: within 2^-15 T(m) of the round's fp32 minimum -- the
-// round's exact best is among them, so the chunk's is among the rounds'), their
-// exact tie-rounded keys, and a running (key, position) minimum. Same outputs
-// (cbest per item) and carries as the block scan; waves of a workgroup take
-// different (item, feature) pairs.
+#ifndef MT_XE_TWO_PASS
+#define MT_XE_TWO_PASS 1
+#endif
+// IEEE order as unsigned order (-0.0 folded into +0.0), and back
+__device__ __forceinline__ uint32_t xe_fkey(float v) {
+  const uint32_t b = __float_as_uint(v + 0.0f);
+  return (b >> 31) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float xe_fval(uint32_t k) {
+  return __uint_as_float((k >> 31) ? (k & 0x7fffffffu) : ~k);
+}
+
+template <int kPass>
 __device__ __forceinline__ void xe_scan_wave_c2(const XeArgs& a, const XeLists& L, int64_t it,
                                                 int f) {
   const int lane = lane_id();
   const unsigned long long lt = (1ull << lane) - 1ull;
   const int64_t slot = L.items[it * 4 + 0], sstart = L.items[it * 4 + 1];
-  const int64_t c0 = L.items[it * 4 + 2], cn = L.items[it * 4 + 3];
-  const int64_t m = L.cnt[slot];
+  const int64_t c0 = L.items[it * 4 + 2];
+  const int cn = (int)L.items[it * 4 + 3];
+  const int m = L.cnt[slot];
   const int Cc = xe_cc(a.C);
   const uint32_t* Ef = a.E + (int64_t)f * a.n;
-  const int64_t t0 = L.stats[slot * Cc + 0], t1 = a.C == 2 ? L.stats[slot * Cc + 1] : 0;
-  int64_t run1 = a.C == 2 ? a.carry[(it * a.F_loc + f) * Cc + 1] : 0;  // class-1 rows before
+  const int t0 = (int)L.stats[slot * Cc + 0], t1 = a.C == 2 ? (int)L.stats[slot * Cc + 1] : 0;
+  int run1 = a.C == 2 ? (int)a.carry[(it * a.F_loc + f) * Cc + 1] : 0;  // class-1 rows before
+  const int msl = (int)(a.msl < (int64_t)m ? a.msl : (int64_t)m);
+  const int p0 = (int)(c0 - sstart);  // the chunk's first position in its segment
   const double tm = xe_tl(m, a.xtab, a.xtab_n);
   const double tu = tie_unit(tm, m);
   const double tinv = 1.0 / tu;
   const bool entropy = a.crit == kEntropy;
-  // candidates: within 2^MT_XE_PAD T(m) of the round's fp32 minimum (the terms'
-  // error is <= 35 * 2^-24 T(m), so any pad >= 2^-17 is safe; -15 .. -18 measured
-  // the same: profiles/kernel_experiments.md)
+  // candidates: within 2^MT_XE_PAD T(m) of the reference fp32 minimum (the
+  // terms' error is <= 35 * 2^-24 T(m), so any pad >= 2^-17 is safe)
   const float thr_pad = (float)tm * __builtin_ldexpf(1.0f, MT_XE_PAD);
   const int fg = a.f_lo + f;
-  auto t32 = [](int64_t x) -> float {
+  auto t32 = [](int x) -> float {
     const float v = (float)x;  // counts < 2^24: exact
 #if MT_XE_HWLOG
     // hardware log2 (v_log_f32, |error| <= 4 * 2^-24 * x log2 x, checked for
-    // x < 2^22 by tests/test_gpu_kernels.py::test_hw_log_terms_error_bound):
-    // six terms err by far less than the 2^-15 T(m) pad
+    // x < 2^22 by tests/test_gpu_kernels.py::test_hw_log_terms_error_bound)
     return x > 1 ? v * __builtin_amdgcn_logf(v) : 0.0f;
 #else
     return x > 1 ? v * log2f(v) : 0.0f;
@@ -514,29 +539,53 @@ __device__ __forceinline__ void xe_scan_wave_c2(const XeArgs& a, const XeLists& 
   };
   unsigned long long mine = ~0ull;
   uint64_t mine_pos = ~0ull;
+  float gthr = 0.0f;  // kPass 2: the node-wide candidate threshold
+  if constexpr (kPass == 2) {
+    uint32_t nk = 0xffffffffu;
+    for (int q = lane; q < a.F_loc; q += kWave) {
+      const uint32_t v = a.nmin[slot * a.F_loc + q];
+      nk = v < nk ? v : nk;
+    }
+#pragma unroll
+    for (int d = kWave / 2; d > 0; d >>= 1) {
+      const uint32_t o = (uint32_t)__shfl_xor((int)nk, d, kWave);
+      nk = o < nk ? o : nk;
+    }
+    const uint32_t ck = a.cmin[it * a.F_loc + f];
+    gthr = xe_fval(nk) + thr_pad;
+    if (ck == 0xffffffffu || nk == 0xffffffffu || !(xe_fval(ck) <= gthr)) {
+      if (lane == 0) {  // no candidate here: an empty record (never the minimum)
+        uint64_t* o = a.cbest + (it * a.F_loc + f) * 2;
+        o[0] = ~0ull;
+        o[1] = ~0ull;
+      }
+      return;
+    }
+  }
+  float wmin = __builtin_inff();  // kPass 1: the chunk's fp32 minimum
   constexpr int kRound = kWave * kXePer;  // 512
-  for (int64_t r0 = 0; r0 < cn; r0 += kRound) {
+  for (int r0 = 0; r0 < cn; r0 += kRound) {
     uint32_t e[kXePer];
 #pragma unroll
     for (int k = 0; k < kXePer; ++k) {
-      const int64_t i = r0 + (int64_t)k * kWave + lane;
+      const int i = r0 + k * kWave + lane;
       e[k] = i < cn ? Ef[c0 + i] : 0xFFFFFFFFu;
     }
     // entries past the round: lane 63 of the last row reads its successor
-    const int64_t iend = r0 + kRound;  // first index of the next round
+    const int iend = r0 + kRound;  // first index of the next round
     uint32_t after = 0xFFFFFFFFu;
     if (lane == kWave - 1) {
       if (iend < cn) after = Ef[c0 + iend];
-      else if (c0 + cn - sstart < m) after = Ef[c0 + cn];
+      else if (p0 + cn < m) after = Ef[c0 + cn];
     }
     unsigned long long bal[kXePer];
-    int64_t l1[kXePer];
+    int l1[kXePer];
     bool valid[kXePer];
 #pragma unroll
     for (int k = 0; k < kXePer; ++k) {
-      const int64_t i = r0 + (int64_t)k * kWave + lane;
+      const int i = r0 + k * kWave + lane;
       bal[k] = __ballot(i < cn && xe_lab(e[k]) == 1);
-      l1[k] = run1 + __popcll(bal[k] & lt) + ((bal[k] >> lane) & 1ull);
+      l1[k] = run1 + __popcll(bal[k] & lt) + (int)((bal[k] >> lane) & 1ull);
       run1 += __popcll(bal[k]);
       // successor: next lane, or (lane 63) the next row's lane 0 / the entry after
       uint32_t nx = (uint32_t)__shfl_down((int)e[k], 1, kWave);
@@ -544,15 +593,13 @@ __device__ __forceinline__ void xe_scan_wave_c2(const XeArgs& a, const XeLists& 
                                     ? (uint32_t)__builtin_amdgcn_readlane((int)e[k + 1 < kXePer ? k + 1 : k], 0)
                                     : after;
       if (lane == kWave - 1) nx = (k + 1 < kXePer && i + 1 < cn) ? row_next : after;
-      const int64_t pos = c0 + i - sstart;
-      const int64_t ml = pos + 1, mr = m - ml;
-      bool v = i < cn && mr > 0 && ml >= a.msl && mr >= a.msl;
+      const int ml = p0 + i + 1, mr = m - ml;
+      bool v = i < cn && mr > 0 && ml >= msl && mr >= msl;
       if (v) v = xe_boundary(e[k], nx, a, fg);
       valid[k] = v;
     }
     auto exact_key = [&](int k) -> unsigned long long {
-      const int64_t pos = c0 + r0 + (int64_t)k * kWave + lane - sstart;
-      const int64_t ml = pos + 1, mr = m - ml;
+      const int64_t ml = p0 + r0 + k * kWave + lane + 1, mr = m - ml;
       const int64_t L1 = l1[k], L0 = ml - L1, R1 = t1 - L1, R0 = t0 - L0;
       double cost;
       if (entropy) {
@@ -572,24 +619,37 @@ __device__ __forceinline__ void xe_scan_wave_c2(const XeArgs& a, const XeLists& 
       for (int k = 0; k < kXePer; ++k) {
         c32[k] = __builtin_inff();
         if (!valid[k]) continue;
-        const int64_t ml = c0 + r0 + (int64_t)k * kWave + lane - sstart + 1, mr = m - ml;
-        const int64_t L1 = l1[k], L0 = ml - L1, R1 = t1 - L1, R0 = t0 - L0;
+        const int ml = p0 + r0 + k * kWave + lane + 1, mr = m - ml;
+        const int L1 = l1[k], L0 = ml - L1, R1 = t1 - L1, R0 = t0 - L0;
         c32[k] = (t32(ml) - (t32(L0) + t32(L1))) + (t32(mr) - (t32(R0) + t32(R1)));
         fm = fminf(fm, c32[k]);
       }
-      fm = wave_min_f32_dpp(fm);
+      if constexpr (kPass == 0) fm = wave_min_f32_dpp(fm);
     }
-    const float thr = fm + thr_pad;
+    if constexpr (kPass == 1) {
+      wmin = fminf(wmin, fm);
+      continue;
+    }
+    const float thr = kPass == 2 ? gthr : fm + thr_pad;
 #pragma unroll
     for (int k = 0; k < kXePer; ++k) {
       if (!valid[k] || (entropy && !(c32[k] <= thr))) continue;
       const unsigned long long key = exact_key(k);
-      const uint64_t pos = (uint64_t)(c0 + r0 + (int64_t)k * kWave + lane - sstart);
+      const uint64_t pos = (uint64_t)(p0 + r0 + k * kWave + lane);
       if (key < mine || (key == mine && pos < mine_pos)) {
         mine = key;
         mine_pos = pos;
       }
     }
+  }
+  if constexpr (kPass == 1) {
+    wmin = wave_min_f32_dpp(wmin);
+    if (lane == 0) {
+      const uint32_t k = wmin < __builtin_inff() ? xe_fkey(wmin) : 0xffffffffu;
+      a.cmin[it * a.F_loc + f] = k;
+      if (k != 0xffffffffu) atomicMin(a.nmin + slot * a.F_loc + f, k);
+    }
+    return;
   }
 #pragma unroll
   for (int d = kWave / 2; d > 0; d >>= 1) {
@@ -608,12 +668,13 @@ __device__ __forceinline__ void xe_scan_wave_c2(const XeArgs& a, const XeLists& 
 }
 
 // One wave per (chunk item, feature) pair, grid-stride over the level's pairs.
+template <int kPass>
 __global__ __launch_bounds__(kXeThreads) void xe_scan_c2_kernel(XeArgs a, XeLists L) {
   const int64_t total = (int64_t)L.ctl[1] * a.F_loc;
   const int64_t waves = (int64_t)gridDim.x * kXeWaves;
   for (int64_t w = (int64_t)blockIdx.x * kXeWaves + (threadIdx.x >> 6); w < total; w += waves) {
     const int64_t wu = __builtin_amdgcn_readfirstlane((int)w);
-    xe_scan_wave_c2(a, L, wu / a.F_loc, (int)(wu % a.F_loc));
+    xe_scan_wave_c2<kPass>(a, L, wu / a.F_loc, (int)(wu % a.F_loc));
   }
 }
 
@@ -1374,11 +1435,16 @@ void xe_level_scan(hipStream_t s, const XeArgs& a, const XeLists& cur, int items
                      dim3(kXeThreads), 0, s, a, cur);
   if (a.C == 0)
     hipLaunchKernelGGL(xe_scan_kernel<0>, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
-  else if (a.C <= 2)  // one wave per (item, feature): no workgroup barriers
-    hipLaunchKernelGGL(xe_scan_c2_kernel,
-                       dim3((unsigned)std::min<int64_t>(
-                           ((int64_t)items_bound * a.F_loc + kXeWaves - 1) / kXeWaves, 8192)),
-                       dim3(kXeThreads), 0, s, a, cur);
+  else if (a.C <= 2) {  // one wave per (item, feature): no workgroup barriers
+    const dim3 g((unsigned)std::min<int64_t>(
+        ((int64_t)items_bound * a.F_loc + kXeWaves - 1) / kXeWaves, 8192));
+    if (MT_XE_TWO_PASS && a.crit == kEntropy && a.nmin && a.cmin) {
+      hipLaunchKernelGGL(xe_scan_c2_kernel<1>, g, dim3(kXeThreads), 0, s, a, cur);
+      hipLaunchKernelGGL(xe_scan_c2_kernel<2>, g, dim3(kXeThreads), 0, s, a, cur);
+    } else {
+      hipLaunchKernelGGL(xe_scan_c2_kernel<0>, g, dim3(kXeThreads), 0, s, a, cur);
+    }
+  }
   else
     hipLaunchKernelGGL(xe_scan_kernel<2>, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
   hipLaunchKernelGGL(xe_select_kernel, dim3(slots_bound), dim3(kXeThreads), 0, s, a, cur);

@@ -92,6 +92,8 @@ void bind_exact2(py::module_& m) {
         a.carry = ptr<int64_t>(u("carry"));
         a.cmm = ptr<int64_t>(u("cmm"));
         a.cbest = ptr<uint64_t>(u("cbest"));
+        a.cmin = d.contains("cmin") ? ptr<uint32_t>(u("cmin")) : nullptr;
+        a.nmin = d.contains("nmin") ? ptr<uint32_t>(u("nmin")) : nullptr;
         a.rec = ptr<int64_t>(u("rec"));
         a.split = ptr<int64_t>(u("split"));
         a.pitems = ptr<int64_t>(u("pitems"));

@@ -1263,18 +1263,24 @@ __device__ __forceinline__ void tiny_fill_h(double* __restrict__ H, const double
   }
 }
 
-__host__ __device__ inline int tiny_wave_bytes(int F) { return F * kWave * 2 + kWave; }
+// code_bytes 1: 16-bit sorted entries {code : 8, run end : 1, -, lane : 6};
+// 2 (more than 256 bins): 32-bit entries {code : 16, run end : 1, -, lane : 6}
+__host__ __device__ inline int tiny_wave_bytes(int F, int code_bytes = 1) {
+  return F * kWave * 2 * code_bytes + kWave;
+}
 
 struct TinyOut {
   int32_t* node_i32;
   int32_t* node_cnt;
 };
 
+template <typename CodeT>
 __device__ __forceinline__ void tiny_sorted_subtree(
     const uint32_t* __restrict__ codes_rm, int64_t row_words, const uint32_t* __restrict__ src,
     const int32_t* __restrict__ y, FinRowLab rl, int64_t start, int m, int depth0,
     int64_t root_slot, int F, int C, int crit, int max_depth, int64_t mss, int64_t msl,
-    const double* __restrict__ H, const uint32_t* __restrict__ Hrow, uint16_t* __restrict__ srt,
+    const double* __restrict__ H, const uint32_t* __restrict__ Hrow,
+    std::conditional_t<sizeof(CodeT) == 1, uint16_t, uint32_t>* __restrict__ srt,
     uint8_t* __restrict__ flag,
     unsigned long long* __restrict__ st_mask, int32_t* __restrict__ st_dep,
     int32_t* __restrict__ st_slot, TinyOut out, bool coherent = false) {
@@ -1297,12 +1303,32 @@ __device__ __forceinline__ void tiny_sorted_subtree(
   const int mslw = (int)(msl < 65 ? msl : 65);
   // ---- presort: srt[f][position] = {code, run end, lane}. Keys {code : 8,
   // lane : 8} are unique, so a bitonic network over the wave sorts them stably;
-  // two features share a 32-bit register (packed 16-bit min / max).
+  // two features share a 32-bit register (packed 16-bit min / max). 16-bit
+  // codes: keys {code : 16, lane : 8}, one feature per register.
+  constexpr int kCpw = 4 / (int)sizeof(CodeT);         // codes per 32-bit word
+  constexpr uint32_t kCodeMask = sizeof(CodeT) == 1 ? 0xffu : 0xffffu;
   const uint32_t* rowp = codes_rm + (int64_t)row * row_words;
-  const int nwords = (F + 3) >> 2;
+  const int nwords = (F + kCpw - 1) / kCpw;
   // subtrees of at most kTinySmallNode rows never scan (every node takes the
   // lane-per-feature path below), so they skip the presort
-  if (m > kTinySmallNode) {
+  if (m > kTinySmallNode && sizeof(CodeT) == 2) {
+    int lg = 1;  // sort network size 2^lg >= m (m >= 2)
+    while ((1 << lg) < m) ++lg;
+    for (int w = 0; w < nwords; ++w) {
+      const uint32_t word = act ? rowp[w] : 0u;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int f = w * 2 + h;
+        if (f >= F) break;
+        uint32_t v = act ? ((word >> (16 * h)) & 0xffffu) << 8 | (uint32_t)lane : 0xffffffffu;
+        v = bitonic64_u32(v, lane, lg);
+        const uint32_t nv = (uint32_t)__shfl_down((int)v, 1, kWave);
+        const bool endl = lane == m - 1;
+        const uint32_t ea = (endl || (nv >> 8) != (v >> 8)) ? 0x80u : 0u;
+        srt[f * kWave + lane] = act ? (v | ea) : 0xffffff3fu;
+      }
+    }
+  } else if (m > kTinySmallNode) {
     int lg = 1;  // sort network size 2^lg >= m (m >= 2)
     while ((1 << lg) < m) ++lg;
     for (int w = 0; w < nwords; ++w) {
@@ -1376,11 +1402,12 @@ __device__ __forceinline__ void tiny_sorted_subtree(
             const int wl = __ffsll((long long)nz) - 1;
             const uint32_t xw = (uint32_t)__builtin_amdgcn_readlane((int)x, wl);
             const uint32_t aw = (uint32_t)__builtin_amdgcn_readlane((int)wa, wl);
-            const int byte = (__ffs((int)xw) - 1) >> 3;
-            const int f = (w0 + wl) * 4 + byte;
-            if (f < F) {  // (bytes past F are row padding)
-              const uint32_t ca = (aw >> (8 * byte)) & 0xffu;
-              const uint32_t cb = ca ^ ((xw >> (8 * byte)) & 0xffu);
+            constexpr int kBits = 8 * (int)sizeof(CodeT);
+            const int byte = (__ffs((int)xw) - 1) / kBits;  // (the code's index in the word)
+            const int f = (w0 + wl) * kCpw + byte;
+            if (f < F) {  // (codes past F are row padding)
+              const uint32_t ca = (aw >> (kBits * byte)) & kCodeMask;
+              const uint32_t cb = ca ^ ((xw >> (kBits * byte)) & kCodeMask);
               bf = f;
               bb = ca < cb ? ca : cb;
               LM = ca < cb ? (1ull << a) : (1ull << b);
@@ -1408,8 +1435,8 @@ __device__ __forceinline__ void tiny_sorted_subtree(
       }
       double bg = -__builtin_inf(), bc = __builtin_inf();
       bf = 0x7fffffff;
-      const uint8_t* cb8 = reinterpret_cast<const uint8_t*>(codes_rm);
-      const int64_t rbytes = row_words * 4;
+      const CodeT* cb8 = reinterpret_cast<const CodeT*>(codes_rm);
+      const int64_t rbytes = row_words * kCpw;  // (codes per row)
       uint32_t code[kTinySmallNode];
       for (int f0 = 0; f0 < F; f0 += kWave) {
         const int f = f0 + lane;
@@ -1589,7 +1616,7 @@ __device__ __forceinline__ void tiny_sorted_subtree(
 // kW waves per workgroup share one H table; the launcher picks kW so the most
 // waves fit a CU's LDS (F = 64: 16 waves in one 1024-thread workgroup instead of
 // 3 x 4; F = 128: 8 instead of 4), see tiny_sorted_waves.
-template <int kW>
+template <int kW, typename CodeT>
 __global__ __launch_bounds__(kW * kWave) void finish_tiny_sorted_kernel(
     const uint32_t* __restrict__ codes_rm, int64_t row_words, const uint32_t* __restrict__ buf0,
     const uint32_t* __restrict__ buf1, const int32_t* __restrict__ y, FinRowLab rl,
@@ -1604,9 +1631,10 @@ __global__ __launch_bounds__(kW * kWave) void finish_tiny_sorted_kernel(
   __shared__ int32_t s_dep[kW][16], s_slot[kW][16];
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
-  uint8_t* wbase = reinterpret_cast<uint8_t*>(dyn) + (size_t)wave * tiny_wave_bytes(F);
-  uint16_t* srt = reinterpret_cast<uint16_t*>(wbase);
-  uint8_t* flag = wbase + F * kWave * 2;
+  using SrtT = std::conditional_t<sizeof(CodeT) == 1, uint16_t, uint32_t>;
+  uint8_t* wbase = reinterpret_cast<uint8_t*>(dyn) + (size_t)wave * tiny_wave_bytes(F, sizeof(CodeT));
+  SrtT* srt = reinterpret_cast<SrtT*>(wbase);
+  uint8_t* flag = wbase + F * kWave * sizeof(SrtT);
   tiny_fill_h(s_h, xtab, crit);
   for (int a = threadIdx.x; a <= kTinyRows; a += blockDim.x) s_hrow[a] = 8u * (uint32_t)tiny_h_idx(a, 0);
   __syncthreads();
@@ -1617,7 +1645,7 @@ __global__ __launch_bounds__(kW * kWave) void finish_tiny_sorted_kernel(
     k = __builtin_amdgcn_readfirstlane(k);
     if (k >= K) break;
     const int64_t* rec = tiny + (int64_t)k * 8;
-    tiny_sorted_subtree(codes_rm, row_words, rec[3] ? buf1 : buf0, y, rl, rec[0], (int)rec[1],
+    tiny_sorted_subtree<CodeT>(codes_rm, row_words, rec[3] ? buf1 : buf0, y, rl, rec[0], (int)rec[1],
                         (int)rec[2], rec[4], F, C, crit, max_depth, mss, msl, s_h, s_hrow, srt, flag,
                         s_mask[wave], s_dep[wave], s_slot[wave], TinyOut{node_i32, node_cnt});
   }
@@ -1626,15 +1654,15 @@ __global__ __launch_bounds__(kW * kWave) void finish_tiny_sorted_kernel(
 // Waves per workgroup of the sorted tiny kernel: the most resident waves per CU
 // under the LDS budget and the VGPR cap (<= 128 VGPRs: 4 waves per SIMD), fewer
 // waves per workgroup on ties.
-static int tiny_sorted_lds(int F, int w) {  // static + dynamic LDS of one workgroup
-  return kTinyH * 8 + (kTinyRows + 1) * 4 + w * 16 * 16 + w * tiny_wave_bytes(F);
+static int tiny_sorted_lds(int F, int w, int cb = 1) {  // static + dynamic LDS of one workgroup
+  return kTinyH * 8 + (kTinyRows + 1) * 4 + w * 16 * 16 + w * tiny_wave_bytes(F, cb);
 }
 
-static int tiny_sorted_waves(int F) {
+static int tiny_sorted_waves(int F, int cb = 1) {
   constexpr int kLdsPerCu = 160 * 1024, kWavesPerCu = 16;
   int best_w = 1, best = 0;
   for (int w : {1, 2, 4, 8, 16}) {
-    const int bytes = tiny_sorted_lds(F, w);
+    const int bytes = tiny_sorted_lds(F, w, cb);
     if (bytes > kLdsPerCu) continue;
     const int waves = std::min(kLdsPerCu / bytes, kWavesPerCu / w) * w;
     if (waves > best) best = waves, best_w = w;
@@ -1703,9 +1731,10 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   // layout (Ft == F <= kFinMaxF: per-feature LDS arrays)
   const bool c2 = C <= 2 && Ft == F && F <= kFinMaxF && B <= 256;
   const bool tiny_sorted = C <= 2 && getenv_int("MPITREE_TINY_SORTED", 1) != 0;
-  if (code_bytes != 1 || tiny == nullptr) tiny_rows = 0;
+  // (16-bit codes: the sorted tiny kernel only, 32-bit sorted entries)
+  if (tiny == nullptr || (code_bytes != 1 && !tiny_sorted)) tiny_rows = 0;
   if (!tiny_sorted && F > kTinyMaxF) tiny_rows = 0;
-  if (tiny_sorted && tiny_sorted_lds(F, 1) > 160 * 1024) tiny_rows = 0;  // > ~1100 features
+  if (tiny_sorted && tiny_sorted_lds(F, 1, code_bytes) > 160 * 1024) tiny_rows = 0;  // > ~1100 features
   tiny_rows = std::min(tiny_rows, kTinyRows);
   FinRowLab rl{lab_shift ? ((1u << lab_shift) - 1u) : 0xffffffffu, lab_shift};
   const size_t lds = (size_t)finish_lds_bytes(F, B, C);
@@ -1765,34 +1794,42 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   MT_HIP_CHECK(hipGetLastError());
   if (tiny_rows > 0) {
     if (tiny_sorted) {
-      int w = getenv_int("MPITREE_TINY_WAVES", tiny_sorted_waves(F));
+      const int cb = code_bytes;
+      int w = getenv_int("MPITREE_TINY_WAVES", tiny_sorted_waves(F, cb));
       for (int cand : {16, 8, 4, 2, 1}) {  // the largest allowed width <= the request
-        if (cand <= w && tiny_sorted_lds(F, cand) <= 160 * 1024) {
+        if (cand <= w && tiny_sorted_lds(F, cand, cb) <= 160 * 1024) {
           w = cand;
           break;
         }
       }
       // tiny_grid counts 4-wave workgroups: keep the total wave count
       const int g = std::max(1, tiny_grid * kTinyWaves / w);
-      const size_t lds = (size_t)w * tiny_wave_bytes(F);
-#define MT_TS(W)                                                                             \
-  MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_tiny_sorted_kernel<W>,                \
+      const size_t lds = (size_t)w * tiny_wave_bytes(F, cb);
+#define MT_TS(W, CT)                                                                         \
+  MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_tiny_sorted_kernel<W, CT>,            \
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));   \
-  hipLaunchKernelGGL(finish_tiny_sorted_kernel<W>, dim3(g), dim3(W * kWave), lds, stream,    \
-                     (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,          \
+  hipLaunchKernelGGL((finish_tiny_sorted_kernel<W, CT>), dim3(g), dim3(W * kWave), lds,      \
+                     stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,  \
                      counter + kFinCtrTinyCount, counter + kFinCtrTinyCount + 1, F, C, crit, \
                      max_depth, mss, msl, xtab, node_i32, node_cnt);
-      if (w == 16) {
-        MT_TS(16)
-      } else if (w == 8) {
-        MT_TS(8)
-      } else if (w == 4) {
-        MT_TS(4)
-      } else if (w == 2) {
-        MT_TS(2)
+#define MT_TSW(CT)   \
+  if (w == 16) {     \
+    MT_TS(16, CT)    \
+  } else if (w == 8) { \
+    MT_TS(8, CT)     \
+  } else if (w == 4) { \
+    MT_TS(4, CT)     \
+  } else if (w == 2) { \
+    MT_TS(2, CT)     \
+  } else {           \
+    MT_TS(1, CT)     \
+  }
+      if (cb == 1) {
+        MT_TSW(uint8_t)
       } else {
-        MT_TS(1)
+        MT_TSW(uint16_t)
       }
+#undef MT_TSW
 #undef MT_TS
     } else {
 #define MT_TG(MANY)                                                                          \

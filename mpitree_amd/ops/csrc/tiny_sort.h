@@ -70,4 +70,43 @@ __device__ __forceinline__ uint32_t bitonic64_pk_u16(uint32_t v, int lane, int l
   return v;
 }
 
+template <int K, int J>
+__device__ __forceinline__ uint32_t bitonic_step_u32(uint32_t v, int lane) {
+  const uint32_t p = lane_xor_u32<J>(v);
+  const bool keep_min = ((lane & K) == 0) == ((lane & J) == 0);
+  return keep_min ? (v < p ? v : p) : (v < p ? p : v);
+}
+
+// Ascending bitonic sort of 64 lanes, one 32-bit key per lane (16-bit codes);
+// lg as for bitonic64_pk_u16.
+__device__ __forceinline__ uint32_t bitonic64_u32(uint32_t v, int lane, int lg) {
+  v = bitonic_step_u32<2, 1>(v, lane);
+  if (lg < 2) return v;
+  v = bitonic_step_u32<4, 2>(v, lane);
+  v = bitonic_step_u32<4, 1>(v, lane);
+  if (lg < 3) return v;
+  v = bitonic_step_u32<8, 4>(v, lane);
+  v = bitonic_step_u32<8, 2>(v, lane);
+  v = bitonic_step_u32<8, 1>(v, lane);
+  if (lg < 4) return v;
+  v = bitonic_step_u32<16, 8>(v, lane);
+  v = bitonic_step_u32<16, 4>(v, lane);
+  v = bitonic_step_u32<16, 2>(v, lane);
+  v = bitonic_step_u32<16, 1>(v, lane);
+  if (lg < 5) return v;
+  v = bitonic_step_u32<32, 16>(v, lane);
+  v = bitonic_step_u32<32, 8>(v, lane);
+  v = bitonic_step_u32<32, 4>(v, lane);
+  v = bitonic_step_u32<32, 2>(v, lane);
+  v = bitonic_step_u32<32, 1>(v, lane);
+  if (lg < 6) return v;
+  v = bitonic_step_u32<64, 32>(v, lane);
+  v = bitonic_step_u32<64, 16>(v, lane);
+  v = bitonic_step_u32<64, 8>(v, lane);
+  v = bitonic_step_u32<64, 4>(v, lane);
+  v = bitonic_step_u32<64, 2>(v, lane);
+  v = bitonic_step_u32<64, 1>(v, lane);
+  return v;
+}
+
 }  // namespace mt
