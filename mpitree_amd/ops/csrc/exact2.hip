@@ -239,10 +239,16 @@ __global__ __launch_bounds__(kXeThreads) void xe_carry_kernel(XeArgs a, XeLists 
   const int i0 = L.ifirst[slot], i1 = L.ifirst[slot + 1];
   if (k == 0 && a.nmin) a.nmin[slot * a.F_loc + f] = 0xffffffffu;  // (two-pass scan)
   int64_t acc = 0;
-  for (int it = i0; it < i1; ++it) {
-    const int64_t o = ((int64_t)it * a.F_loc + f) * Cc + k;
-    a.carry[o] = acc;
-    acc += a.tot[o];
+  for (int it = i0; it < i1; it += 8) {  // 8 totals in flight per round trip
+    int64_t v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      v[q] = it + q < i1 ? a.tot[((int64_t)(it + q) * a.F_loc + f) * Cc + k] : 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      if (it + q < i1) a.carry[((int64_t)(it + q) * a.F_loc + f) * Cc + k] = acc;
+      acc += v[q];
+    }
   }
   if (a.C == 0 && f == 0 && k == 0) {
     int64_t mn = LLONG_MAX, mx = LLONG_MIN;
@@ -717,19 +723,31 @@ __global__ __launch_bounds__(kXeThreads) void xe_select_kernel(XeArgs a, XeLists
   double g = -__builtin_inf();
   int bf = 0x7fffffff;
   int64_t bp = -1;
-  for (int f = tid; f < a.F_loc; f += kXeThreads) {
+  // one wave per feature, lanes over the slot's chunks: (key, position) minimum
+  // (a level-0 slot holds n / 2048 chunks per feature)
+  for (int f = wave; f < a.F_loc; f += kXeWaves) {
     uint64_t bk = ~0ull, bpos = ~0ull;
-    for (int it = i0; it < i1; ++it) {  // chunks in order: positions ascend
+    for (int it = i0 + lane; it < i1; it += kWave) {
       const uint64_t* c = a.cbest + ((int64_t)it * a.F_loc + f) * 2;
-      if (c[0] < bk) {
-        bk = c[0];
-        bpos = c[1];
+      const uint64_t k = c[0], q = c[1];
+      if (k < bk || (k == bk && q < bpos)) {
+        bk = k;
+        bpos = q;
       }
     }
-    if (bk == ~0ull) continue;
+#pragma unroll
+    for (int d = kWave / 2; d > 0; d >>= 1) {
+      const uint64_t ok = (uint64_t)__shfl_xor((unsigned long long)bk, d, kWave);
+      const uint64_t oq = (uint64_t)__shfl_xor((unsigned long long)bpos, d, kWave);
+      if (ok < bk || (ok == bk && oq < bpos)) {
+        bk = ok;
+        bpos = oq;
+      }
+    }
+    if (bk == ~0ull) continue;  // (wave-uniform after the reduction)
     const double cost = a.C ? (double)bk * tu : xe_dval(bk);
     const double gf = pterm - cost;
-    if (gf > g) {  // features ascend per thread: strict > keeps the lowest
+    if (gf > g) {  // features ascend per wave: strict > keeps the lowest
       g = gf;
       bf = a.f_lo + f;
       bp = (int64_t)bpos;
@@ -792,6 +810,20 @@ __global__ __launch_bounds__(kXeThreads) void xe_select_kernel(XeArgs a, XeLists
       int64_t t = car[0];
       for (int w = 0; w < kXeWaves; ++w) t += s_sum[w];
       out[7] = t;
+    }
+  } else if (a.C <= 2) {  // class-1 entries counted, class 0 the rest
+    uint32_t ones = 0;
+    for (int64_t p = cfirst + tid; p <= start + bp; p += kXeThreads)
+      ones += xe_lab(Ef[p]) == 1 ? 1u : 0u;
+    ones = wave_sum_u32(ones);
+    if (lane == 0) s_sum[wave] = ones;
+    __syncthreads();
+    if (tid == 0) {
+      int64_t t = 0;
+      for (int w = 0; w < kXeWaves; ++w) t += s_sum[w];
+      const int64_t nrows = bp - (cfirst - start) + 1;
+      out[7] = car[0] + (nrows - t);
+      if (a.C == 2) out[8] = car[1] + t;
     }
   } else {
     for (int64_t p = cfirst + tid; p <= start + bp; p += kXeThreads)
