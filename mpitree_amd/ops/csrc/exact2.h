@@ -44,6 +44,7 @@ struct XeArgs {
   uint64_t* cbest;     // [IMAX][F_loc][2] chunk best {cost key, position}
   uint32_t* cmin;      // [IMAX][F_loc] two-pass scan: chunk fp32 minimum (ordered bits)
   uint32_t* nmin;      // [KMAX][F_loc] two-pass scan: node fp32 minimum per feature
+  float* gthr;         // [KMAX] two-pass scan: node candidate threshold
   int64_t* rec;        // [KMAX][R] split records, R = 6 + (C or 1) + 1
   // partition
   int64_t* split;      // [SMAX][4] {start, count, feature (global), n_left}

@@ -495,11 +495,14 @@ __device__ __forceinline__ void xe_scan_item(const XeArgs& a, const XeLists& L, 
 #ifndef MT_XE_HWLOG
 #define MT_XE_HWLOG 1
 #endif
-#ifndef MT_XE_PAD
-#define MT_XE_PAD -15
+#ifndef MT_XE_PAD  // candidate pad exponent: >= 2 x the fp32 error bound (35 * 2^-24)
+#define MT_XE_PAD -17
 #endif
 #ifndef MT_XE_TWO_PASS
 #define MT_XE_TWO_PASS 1
+#endif
+#ifndef MT_XE_P2_GRID  // workgroups of the second pass
+#define MT_XE_P2_GRID 1024
 #endif
 // IEEE order as unsigned order (-0.0 folded into +0.0), and back
 __device__ __forceinline__ uint32_t xe_fkey(float v) {
@@ -512,7 +515,7 @@ __device__ __forceinline__ float xe_fval(uint32_t k) {
 
 template <int kPass>
 __device__ __forceinline__ void xe_scan_wave_c2(const XeArgs& a, const XeLists& L, int64_t it,
-                                                int f) {
+                                                int f, float gthr = 0.0f) {
   const int lane = lane_id();
   const unsigned long long lt = (1ull << lane) - 1ull;
   const int64_t slot = L.items[it * 4 + 0], sstart = L.items[it * 4 + 1];
@@ -530,7 +533,7 @@ __device__ __forceinline__ void xe_scan_wave_c2(const XeArgs& a, const XeLists& 
   const double tinv = 1.0 / tu;
   const bool entropy = a.crit == kEntropy;
   // candidates: within 2^MT_XE_PAD T(m) of the reference fp32 minimum (the
-  // terms' error is <= 35 * 2^-24 T(m), so any pad >= 2^-17 is safe)
+  // terms' error is <= 35 * 2^-24 T(m), so any pad >= 2^-17 = 128 * 2^-24 is safe)
   const float thr_pad = (float)tm * __builtin_ldexpf(1.0f, MT_XE_PAD);
   const int fg = a.f_lo + f;
   auto t32 = [](int x) -> float {
@@ -545,29 +548,8 @@ __device__ __forceinline__ void xe_scan_wave_c2(const XeArgs& a, const XeLists& 
   };
   unsigned long long mine = ~0ull;
   uint64_t mine_pos = ~0ull;
-  float gthr = 0.0f;  // kPass 2: the node-wide candidate threshold
-  if constexpr (kPass == 2) {
-    uint32_t nk = 0xffffffffu;
-    for (int q = lane; q < a.F_loc; q += kWave) {
-      const uint32_t v = a.nmin[slot * a.F_loc + q];
-      nk = v < nk ? v : nk;
-    }
-#pragma unroll
-    for (int d = kWave / 2; d > 0; d >>= 1) {
-      const uint32_t o = (uint32_t)__shfl_xor((int)nk, d, kWave);
-      nk = o < nk ? o : nk;
-    }
-    const uint32_t ck = a.cmin[it * a.F_loc + f];
-    gthr = xe_fval(nk) + thr_pad;
-    if (ck == 0xffffffffu || nk == 0xffffffffu || !(xe_fval(ck) <= gthr)) {
-      if (lane == 0) {  // no candidate here: an empty record (never the minimum)
-        uint64_t* o = a.cbest + (it * a.F_loc + f) * 2;
-        o[0] = ~0ull;
-        o[1] = ~0ull;
-      }
-      return;
-    }
-  }
+  // kPass 2: gthr = the node-wide candidate threshold (xe_gthr_kernel); the
+  // caller only runs chunks whose fp32 minimum is within it
   float wmin = __builtin_inff();  // kPass 1: the chunk's fp32 minimum
   constexpr int kRound = kWave * kXePer;  // 512
   for (int r0 = 0; r0 < cn; r0 += kRound) {
@@ -678,9 +660,64 @@ template <int kPass>
 __global__ __launch_bounds__(kXeThreads) void xe_scan_c2_kernel(XeArgs a, XeLists L) {
   const int64_t total = (int64_t)L.ctl[1] * a.F_loc;
   const int64_t waves = (int64_t)gridDim.x * kXeWaves;
+  if constexpr (kPass == 2) {
+    // 64 pairs per wave step: each lane checks one chunk's fp32 minimum against
+    // its node's threshold (lane-parallel empty records for the rest), then the
+    // wave scans the few candidate chunks one by one
+    const int lane = lane_id();
+    for (int64_t b = ((int64_t)blockIdx.x * kXeWaves + (threadIdx.x >> 6)) * kWave; b < total;
+         b += waves * kWave) {
+      const int64_t w = b + lane;
+      bool cand = false;
+      float th = 0.0f;
+      if (w < total) {
+        const int64_t it = w / a.F_loc;
+        th = a.gthr[L.items[it * 4 + 0]];
+        cand = xe_fval(a.cmin[w]) <= th;  // (an empty chunk's key decodes to NaN)
+        if (!cand) {
+          uint64_t* o = a.cbest + w * 2;
+          o[0] = ~0ull;
+          o[1] = ~0ull;
+        }
+      }
+      unsigned long long cm = __ballot(cand);
+      while (cm) {
+        const int l = __ffsll((long long)cm) - 1;
+        cm &= cm - 1ull;
+        const int64_t wu = b + l;
+        const float t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(th), l));
+        xe_scan_wave_c2<2>(a, L, wu / a.F_loc, (int)(wu % a.F_loc), t);
+      }
+    }
+    return;
+  }
   for (int64_t w = (int64_t)blockIdx.x * kXeWaves + (threadIdx.x >> 6); w < total; w += waves) {
     const int64_t wu = __builtin_amdgcn_readfirstlane((int)w);
     xe_scan_wave_c2<kPass>(a, L, wu / a.F_loc, (int)(wu % a.F_loc));
+  }
+}
+
+// Per slot: the node's fp32 minimum over this rank's features (pass 1's atomic
+// minima) -> the pass-2 candidate threshold min + 2^MT_XE_PAD T(m) (-inf: no
+// valid position, every chunk writes an empty record). One wave per slot.
+__global__ __launch_bounds__(kXeThreads) void xe_gthr_kernel(XeArgs a, XeLists L) {
+  const int64_t slot = (int64_t)blockIdx.x * kXeWaves + (threadIdx.x >> 6);
+  if (slot >= L.ctl[0]) return;
+  const int lane = lane_id();
+  uint32_t nk = 0xffffffffu;
+  for (int q = lane; q < a.F_loc; q += kWave) {
+    const uint32_t v = a.nmin[slot * a.F_loc + q];
+    nk = v < nk ? v : nk;
+  }
+#pragma unroll
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)nk, d, kWave);
+    nk = o < nk ? o : nk;
+  }
+  if (lane == 0) {
+    const int m = L.cnt[slot];
+    const float pad = (float)xe_tl(m, a.xtab, a.xtab_n) * __builtin_ldexpf(1.0f, MT_XE_PAD);
+    a.gthr[slot] = nk == 0xffffffffu ? -__builtin_inff() : xe_fval(nk) + pad;
   }
 }
 
@@ -1470,9 +1507,16 @@ void xe_level_scan(hipStream_t s, const XeArgs& a, const XeLists& cur, int items
   else if (a.C <= 2) {  // one wave per (item, feature): no workgroup barriers
     const dim3 g((unsigned)std::min<int64_t>(
         ((int64_t)items_bound * a.F_loc + kXeWaves - 1) / kXeWaves, 8192));
-    if (MT_XE_TWO_PASS && a.crit == kEntropy && a.nmin && a.cmin) {
+    if (MT_XE_TWO_PASS && a.crit == kEntropy && a.nmin && a.cmin && a.gthr) {
       hipLaunchKernelGGL(xe_scan_c2_kernel<1>, g, dim3(kXeThreads), 0, s, a, cur);
-      hipLaunchKernelGGL(xe_scan_c2_kernel<2>, g, dim3(kXeThreads), 0, s, a, cur);
+      hipLaunchKernelGGL(xe_gthr_kernel, dim3((unsigned)((slots_bound + kXeWaves - 1) / kXeWaves)),
+                         dim3(kXeThreads), 0, s, a, cur);
+      // pass 2: 64 chunk checks per wave step, entries read only near the minimum
+      hipLaunchKernelGGL(xe_scan_c2_kernel<2>,
+                         dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(
+                             ((int64_t)items_bound * a.F_loc + kXeThreads - 1) / kXeThreads,
+                             MT_XE_P2_GRID))),
+                         dim3(kXeThreads), 0, s, a, cur);
     } else {
       hipLaunchKernelGGL(xe_scan_c2_kernel<0>, g, dim3(kXeThreads), 0, s, a, cur);
     }

@@ -94,6 +94,7 @@ void bind_exact2(py::module_& m) {
         a.cbest = ptr<uint64_t>(u("cbest"));
         a.cmin = d.contains("cmin") ? ptr<uint32_t>(u("cmin")) : nullptr;
         a.nmin = d.contains("nmin") ? ptr<uint32_t>(u("nmin")) : nullptr;
+        a.gthr = d.contains("gthr") ? ptr<float>(u("gthr")) : nullptr;
         a.rec = ptr<int64_t>(u("rec"));
         a.split = ptr<int64_t>(u("split"));
         a.pitems = ptr<int64_t>(u("pitems"));

@@ -232,6 +232,7 @@ class ExactGrower:
                 cbest=torch.empty((IMAX, F_loc, 2), **i64),
                 cmin=torch.empty((IMAX, F_loc), **i32),  # two-pass scan references
                 nmin=torch.empty((KMAX, F_loc), **i32),
+                gthr=torch.empty(KMAX, dtype=torch.float32, device=dev),
                 rec=torch.empty((KMAX, R), **i64),
                 grec=torch.empty((P * KMAX * R) if P > 1 else 1, **i64),
                 split=torch.empty((KMAX, 4), **i64),
@@ -255,7 +256,7 @@ class ExactGrower:
             n=n, F=F, f_lo=f_lo, F_loc=F_loc, C=Cx, crit=int(crit), msl=msl,
             xtab=be.xtab.data_ptr(), xtab_n=int(be.xtab.numel()), tot=ptr["tot"],
             carry=ptr["carry"],
-            cmm=ptr["cmm"], cbest=ptr["cbest"], cmin=ptr["cmin"], nmin=ptr["nmin"],
+            cmm=ptr["cmm"], cbest=ptr["cbest"], cmin=ptr["cmin"], nmin=ptr["nmin"], gthr=ptr["gthr"],
             rec=ptr["rec"], split=ptr["split"],
             pitems=ptr["pitems"], pfirst=ptr["pfirst"], flag=ptr["flag"],
             pstat=ptr["pstat"], tick=ptr["tick"], pos_rec=be.pos_rec.data_ptr(),

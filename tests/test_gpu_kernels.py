@@ -33,7 +33,7 @@ def test_xlog2x_device_matches_host_bitwise():
 
 def test_hw_log_terms_error_bound():
     # the exact engine's two-class fp32 prefilter (exact2.hip) computes its terms
-    # as x * v_log_f32(x); its 2^-15 T(m) margin assumes |error| <= 4 * 2^-24 *
+    # as x * v_log_f32(x); its 2^-17 T(m) candidate pad assumes |error| <= 4 * 2^-24 *
     # x log2 x for every count (checked here up to 2^22) and exact zeros at 0, 1
     from mpitree_amd.ops import native
 
