@@ -15,6 +15,7 @@ One JSON line per config (wall-clock per fit, samples/s, tree size):
   100k_exact  100k x 32 continuous, max_depth=12, exact engine, 1 GPU
   1m_reg      1M x 64 regression tree (squared error), 1 GPU
   1m_exact_reg  1M x 64 continuous regression, exact thresholds (presorted lists), 1 GPU
+  1m_q1024    1M x 64 continuous features, 1024 quantile bins (16-bit codes), 1 GPU
   1m_c64      1M x 64 classification with 64 classes, 1 GPU (feature-tiled finisher)
   200k_f512   200k x 512 classification, 1 GPU (feature-tiled finisher)
   10m         10M x 128 synthetic classification, 1 GPU (the 8-GPU
@@ -120,7 +121,8 @@ def run_sweep_gpu(reps):
     return out
 
 
-def _gpu_fit(n, F, reps, md=None, regression=False, classes=2, seed=0, levels=256):
+def _gpu_fit(n, F, reps, md=None, regression=False, classes=2, seed=0, levels=256,
+             max_bins=None):
     import torch
 
     from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
@@ -128,10 +130,10 @@ def _gpu_fit(n, F, reps, md=None, regression=False, classes=2, seed=0, levels=25
 
     if regression:
         X, y = make_regression(n, F, seed=seed, levels=levels)
-        est = DecisionTreeRegressor(max_depth=md, device="cuda")
+        est = DecisionTreeRegressor(max_depth=md, device="cuda", max_bins=max_bins)
     else:
         X, y = make_classification(n, F, n_classes=classes, seed=seed, levels=levels)
-        est = DecisionTreeClassifier(max_depth=md, device="cuda")
+        est = DecisionTreeClassifier(max_depth=md, device="cuda", max_bins=max_bins)
     med, best = _time(lambda: est.fit(X, y), reps, sync=torch.cuda.synchronize)
     st = est.fit_stats_
     return {"ms_median": med * 1e3, "ms_best": best * 1e3, "samples_per_sec": n / med,
@@ -143,8 +145,8 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("names", nargs="*",
                     default=["iris", "sweep", "sweep_gpu", "100k", "1m", "1m_exact",
-                             "100k_exact", "1m_reg", "1m_exact_reg", "1m_c64", "200k_f512",
-                             "10m"])
+                             "100k_exact", "1m_reg", "1m_exact_reg", "1m_q1024", "1m_c64",
+                             "200k_f512", "10m"])
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args(argv)
     for name in a.names:
@@ -176,6 +178,10 @@ def main(argv=None):
                                "full depth, 1 GPU",
                      **_gpu_fit(1_000_000, 64, max(2, a.reps // 2), regression=True,
                                 levels=None)}]
+        elif name == "1m_q1024":
+            rows = [{"config": "1M x 64 continuous (randn) classification, 1024 quantile bins "
+                               "(16-bit codes), full depth, 1 GPU",
+                     **_gpu_fit(1_000_000, 64, max(2, a.reps // 2), levels=None, max_bins=1024)}]
         elif name == "1m_c64":
             rows = [{"config": "1M x 64 classification, 64 classes, full depth, 1 GPU",
                      **_gpu_fit(1_000_000, 64, max(2, a.reps // 2), classes=64)}]
