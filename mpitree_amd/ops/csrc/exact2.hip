@@ -1144,7 +1144,10 @@ constexpr int kXeSub = kWave * kXePartPer;             // entries per wave unit 
 constexpr int kXeSubPerChunk = kXeChunk / kXeSub;      // 2
 constexpr int kXePartLdsWords = 36 * 1024;             // 144 KB of flag words in LDS
 constexpr int64_t kXePartLdsRows = (int64_t)kXePartLdsWords * 32;
-constexpr int kXePartBatch = 16;                       // tickets per claim
+#ifndef MT_XE_PART_BATCH  // (4 / 8 / 32 / 64 measured slower: profiles/kernel_experiments.md)
+#define MT_XE_PART_BATCH 16
+#endif
+constexpr int kXePartBatch = MT_XE_PART_BATCH;         // tickets per claim
 
 template <bool kLdsFlags, bool kReg>
 __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a, XeLists cur) {
