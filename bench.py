@@ -19,12 +19,15 @@ the presorted-list exact engine instead of the <= 256-value histogram engines.
 Single GPU: ``python bench.py``. Multi-GPU (one process per GPU, RCCL):
 ``torchrun --nproc-per-node N bench.py --gpus N``; every rank holds the full
 data (the reference's ParallelDecisionTreeClassifier contract) and the total
-work is fixed, so scaling is "strong". ``--strategy auto`` (default) runs the
-feature-parallel device level loop (each rank builds and scans F/N features,
-one RCCL all-gather of split records per level) and splits the subtree
-finisher jobs across ranks; ``--strategy data`` runs row-sharded histograms
-with one RCCL all-reduce per level (BASELINE config 4:
-``--n 10000000 --features 128 --strategy data``). The JSON line reports the
+work is fixed, so scaling is "strong". ``--strategy auto`` (default) runs
+subtree ownership: the device level loop replicated until a level holds >= 4N
+units, then each rank grows only the subtrees the device planner assigned it
+(LPT on rows; level loop and finisher, no per-level collective) and one RCCL
+all-gather of finished position ranges completes the tree on every rank;
+``--strategy feature`` runs the feature-parallel level loop (F/N features per
+rank, one all-gather of split records per level); ``--strategy data`` runs
+row-sharded histograms reduced per feature block to their owner ranks (BASELINE
+config 4: ``--n 10000000 --features 128 --strategy data``). The JSON line reports the
 level loop that actually ran (``config.level_loop``) and the bytes moved.
 
 ``MPITREE_BENCH_BACKEND=gloo`` rehearses the multi-rank path with ranks
@@ -134,7 +137,8 @@ def main(argv=None):
     mode = stats.get("mode", "single-gpu")
     if world > 1:
         parallelism = {"feature": f"fp{world}", "data": f"dp{world}",
-                       "replicated": f"subtree{world}"}.get(mode, f"{a.strategy}{world}")
+                       "replicated": f"subtree{world}",
+                       "subtree-owned": f"subtree{world}"}.get(mode, f"{a.strategy}{world}")
     else:
         parallelism = "single"
     if a.regression:
