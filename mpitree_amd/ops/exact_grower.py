@@ -256,7 +256,8 @@ class ExactGrower:
             n=n, F=F, f_lo=f_lo, F_loc=F_loc, C=Cx, crit=int(crit), msl=msl,
             xtab=be.xtab.data_ptr(), xtab_n=int(be.xtab.numel()), tot=ptr["tot"],
             carry=ptr["carry"],
-            cmm=ptr["cmm"], cbest=ptr["cbest"], cmin=ptr["cmin"], nmin=ptr["nmin"], gthr=ptr["gthr"],
+            cmm=ptr["cmm"], cbest=ptr["cbest"], cmin=ptr["cmin"], nmin=ptr["nmin"],
+            gthr=ptr["gthr"],
             rec=ptr["rec"], split=ptr["split"],
             pitems=ptr["pitems"], pfirst=ptr["pfirst"], flag=ptr["flag"],
             pstat=ptr["pstat"], tick=ptr["tick"], pos_rec=be.pos_rec.data_ptr(),
