@@ -219,7 +219,7 @@ def main():
             if P > 1:
                 data_r = dict(data, others=data["others"])
                 data_r["others"] = {r: data["others"][(P, r)]}
-            times, st = [], {}
+            times, st, ph = [], {}, []
             for i in range(a.reps + 1):
                 comm = SimFeatureComm(P, r, data_r, a.n, a.features, 2) if P > 1 else None
                 torch.cuda.synchronize()
@@ -228,9 +228,13 @@ def main():
                 torch.cuda.synchronize()
                 if i >= 1:
                     times.append((time.perf_counter() - t0) * 1e3)
+                    ph.append({k: v * 1e3 for k, v in res.timings.items()
+                               if k in ("exact_setup", "levels", "finisher", "assemble")})
                 st = res.stats
                 assert res.arrays.equal(ref.arrays), f"P={P} rank {r}: tree differs"
             per_rank.append(dict(ms=float(np.median(times)),
+                                 phases={k: round(float(np.median([q[k] for q in ph])), 2)
+                                         for k in ph[0]},
                                  F_loc=(st.get("feature_block", [0, a.features])[1]
                                         - st.get("feature_block", [0, a.features])[0]),
                                  comm_mb=(comm.bytes_communicated / 1e6 if comm else 0.0)))
@@ -238,6 +242,7 @@ def main():
         print(json.dumps(dict(P=P, max_rank_ms=round(max(ms), 3),
                               rank_ms=[round(v, 3) for v in ms],
                               F_loc=[p["F_loc"] for p in per_rank],
+                              phases_rank0=per_rank[0]["phases"],
                               comm_mb=round(max(p["comm_mb"] for p in per_rank), 2),
                               levels=ref.stats.get("levels"), nodes=ref.arrays.node_count,
                               tree_equal=True)), flush=True)
