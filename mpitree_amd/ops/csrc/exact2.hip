@@ -1147,7 +1147,20 @@ constexpr int64_t kXePartLdsRows = (int64_t)kXePartLdsWords * 32;
 #ifndef MT_XE_PART_BATCH  // (4 / 8 / 32 / 64 measured slower: profiles/kernel_experiments.md)
 #define MT_XE_PART_BATCH 16
 #endif
-constexpr int kXePartBatch = MT_XE_PART_BATCH;         // tickets per claim
+constexpr int kXePartBatch = MT_XE_PART_BATCH;         // tickets per claim (at most)
+
+// Tickets per claim for F_loc lists: a ticket depends on the one F_loc earlier
+// (same feature, previous sub-chunk), so a batch must not be longer than F_loc
+// and should divide it -- then batch b's tickets wait only on batch b - F_loc /
+// batch in the same order and consecutive waves lag by one ticket. A longer
+// batch serialises the waves (feature-parallel ranks with F_loc = 8 spent
+// 1.7 ms per partition with 16-ticket claims: profiles/r3/session3/).
+__device__ __forceinline__ int xe_part_batch(int F_loc) {
+  if (F_loc <= kXePartBatch) return F_loc;
+  for (int d = kXePartBatch; d >= 4; --d)
+    if (F_loc % d == 0) return d;
+  return F_loc <= 64 ? F_loc : 1;
+}
 
 template <bool kLdsFlags, bool kReg>
 __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a, XeLists cur) {
@@ -1164,12 +1177,13 @@ __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a,
   // tickets are claimed kXePartBatch at a time (one counter serialises its
   // atomics: ~10 ns each) and run in order, so the wave holding the smallest
   // unfinished ticket still never waits
+  const int batch = xe_part_batch(a.F_loc);
   for (int t = 0, tb = 0;; ++t) {
     if (t == tb) {
       int c = 0;
-      if (lane == 0) c = atomicAdd(a.tick + 1, kXePartBatch);
+      if (lane == 0) c = atomicAdd(a.tick + 1, batch);
       t = __builtin_amdgcn_readfirstlane(c);
-      tb = t + kXePartBatch;
+      tb = t + batch;
     }
     if (t >= total) break;
     const int f = t % a.F_loc;
