@@ -17,7 +17,11 @@ reference's threshold semantics (every unique value a candidate) then run on
 the presorted-list exact engine instead of the <= 256-value histogram engines.
 
 Single GPU: ``python bench.py``. Multi-GPU (one process per GPU, RCCL):
-``torchrun --nproc-per-node N bench.py --gpus N``; every rank holds the full
+``torchrun --nproc-per-node N bench.py --gpus N``, or ``python bench.py --gpus N``,
+which starts the N rank processes itself (``torch.distributed.run`` as a child
+process, before this process touches the GPU); ``--gpus`` must equal the
+launcher's ``WORLD_SIZE`` and fewer visible GPUs than ``--gpus`` is an error
+(never a silent one-rank run). Every rank holds the full
 data (the reference's ParallelDecisionTreeClassifier contract) and the total
 work is fixed, so scaling is "strong". ``--strategy auto`` (default) runs
 subtree ownership: the device level loop replicated until a level holds >= 4N
@@ -46,11 +50,46 @@ import numpy as np
 import torch
 
 
-# BASELINE.json's headline metric and the configuration this script runs
+# BASELINE.json's headline metric and the configurations it names
 METRIC = "tree fit wall-clock (s) + samples/sec, 1M\u00d764 synthetic at 1/2/4/8 GPUs"
 CONFIG = "1M\u00d764 synthetic, feature-parallel split search, RCCL all-reduce on 8\u00d7MI355X"
 CONFIG_REG = "1M\u00d764 regression tree (MSE split criterion) on 8\u00d7MI355X"
 CONFIG_10M = "10M\u00d7128 synthetic, data-parallel histogram all-reduce, 288 GB HBM sizing, 8 GPUs"
+
+# what actually ran, by the level loop's reported mode (config.name)
+MODE_TEXT = {
+    "single-gpu": "one MI355X, no collectives",
+    "subtree-owned": "subtree ownership: replicated levels until >= 4 units per rank, LPT "
+                     "assignment, one RCCL all-gather of finished subtrees",
+    "replicated": "replicated levels (too few units to switch), one RCCL all-gather of "
+                  "finisher subtrees",
+    "feature": "feature-parallel split search, one RCCL all-gather of split records per level",
+    "data": "data-parallel row shards, histograms reduced per feature block to owner ranks "
+            "over RCCL per level",
+    "replicated-exact": "exact thresholds, replicated on every rank (fewer features than ranks)",
+}
+
+
+def _spawn_ranks(a, argv) -> int:
+    """``--gpus N`` outside a launcher: run N rank processes under
+    ``torch.distributed.run`` as children (this process never touches the GPU:
+    counting devices does not initialise it) and return their exit code."""
+    import socket
+    import subprocess
+
+    import torch
+
+    have = torch.cuda.device_count()
+    if os.environ.get("MPITREE_BENCH_BACKEND", "nccl") == "nccl" and have < a.gpus:
+        sys.stderr.write(f"bench.py: --gpus {a.gpus} needs {a.gpus} visible GPUs, found {have}\n")
+        return 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
 
 
 def main(argv=None):
@@ -71,7 +110,15 @@ def main(argv=None):
     ap.add_argument("--max-bins", type=int, default=0,
                     help="> 0: quantile bins (e.g. 1024 with --continuous: 16-bit codes)")
     ap.add_argument("--profile-levels", action="store_true")
+    argv = sys.argv[1:] if argv is None else list(argv)
     a = ap.parse_args(argv)
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(_spawn_ranks(a, argv))
+    if int(os.environ.get("WORLD_SIZE", "1")) != a.gpus:
+        ap.error(f"--gpus {a.gpus} but the launcher started WORLD_SIZE="
+                 f"{os.environ.get('WORLD_SIZE')} ranks")
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
@@ -142,11 +189,13 @@ def main(argv=None):
     else:
         parallelism = "single"
     if a.regression:
-        cfg_name = CONFIG_REG
+        baseline_cfg = CONFIG_REG
     elif a.n >= 10_000_000 and a.features >= 128:
-        cfg_name = CONFIG_10M
+        baseline_cfg = CONFIG_10M
     else:
-        cfg_name = CONFIG
+        baseline_cfg = CONFIG
+    shape = f"{a.n:,}\u00d7{a.features} synthetic" + (" regression" if a.regression else "")
+    cfg_name = f"{shape}, {MODE_TEXT.get(mode, mode)}, {world}\u00d7MI355X"
     if rank == 0:
         value = a.n / dt
         out = {
@@ -171,6 +220,7 @@ def main(argv=None):
             "materialized": materialized,
             "config": {
                 "name": cfg_name,
+                "baseline_config": baseline_cfg,
                 "model": f"DecisionTree{'Regressor' if a.regression else 'Classifier'}"
                          f"(criterion={crit}, max_depth={md})",
                 "n_samples": a.n,

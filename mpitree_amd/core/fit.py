@@ -255,13 +255,19 @@ def _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t_bin, t_start, 
                                 mx]).cpu().numpy()
         else:
             root = torch.bincount(yd.long(), minlength=C).cpu().numpy()
-    g = ExactGrower(params, comm if comm.world_size > 1 else None)
+    # feature-parallel needs a feature block per rank; with fewer features than
+    # ranks every rank grows the same tree on all features (replicated, as the
+    # reference's ranks do above their split level)
+    fp = comm.world_size > 1 and F >= comm.world_size
+    g = ExactGrower(params, comm if fp else None)
     with roctx_range("mpitree.grow"):
         ta = g.fit(Xd, yd, root, C, crit, prep.y_exp, timings=timings)
     stats = dict(g.stats)
     stats["thresholds"] = "exact (presorted lists)"
     if comm.world_size > 1:
         stats["strategy"] = comm.kind
+        if not fp:
+            stats["mode"] = "replicated-exact"
     timings["total"] = time.perf_counter() - t_start
     mapper = BinMapper(edges=[], exact=np.ones(F, bool), max_bins=None)
     return FitResult(arrays=ta, classes=prep.classes, n_features=F, mapper=mapper,

@@ -261,7 +261,13 @@ class LevelwiseBuilder:
     def _grow(self, tab, fr, deferred, levels, C, F_h, f_lo, f_hi, reg) -> TreeArrays:
         p, be, comm = self.p, self.be, self.comm
         prev_hist = None
+        multi = comm.world_size > 1
         while fr["id"].size:
+            if multi:  # failure containment: a failed peer / injected fault
+                from ..parallel.failure import check_abort, fault_point
+
+                check_abort()
+                fault_point(comm, f"level:{levels}")
             levels += 1
             K = fr["id"].size
             # small subtrees go to the finisher (global row count decides)

@@ -321,10 +321,16 @@ class _ParallelMixin:
 
     * ``"feature"`` -- feature-parallel split search, one small all-gather of
       per-node candidates per level (rows replicated, as in the reference);
-    * ``"data"`` -- row-sharded histograms, one all-reduce per level;
+    * ``"data"`` -- row-sharded histograms; per level each feature block's
+      histograms are reduced to the block's owner rank (a reduce-scatter by
+      feature) and one all-gather of split records picks the splits;
     * ``"subtree"`` -- load-balanced subtree task parallelism (the reference's
-      strategy, without its parity-split load imbalance);
-    * ``"auto"`` -- feature-parallel top levels + subtree finishing.
+      strategy, without its parity-split load imbalance): replicated levels
+      until a level holds >= 4 units per rank, an LPT assignment of those
+      units, no per-level collective, one all-gather of finished subtrees;
+    * ``"auto"`` -- replicated rows: ``"subtree"`` on the GPU device loop,
+      feature-parallel exact thresholds on continuous features; row-sharded
+      input (``data_sharded=True``): ``"data"``.
 
     The process group is created lazily on first use (``nccl``/RCCL for GPU
     fits, ``gloo`` otherwise); importing the module has no side effects.
@@ -346,6 +352,8 @@ class _ParallelMixin:
         level and resume from the newest level all of them hold."""
         from ..parallel.strategies import make_comm
         from ..utils.observability import maybe_inject_fault, tree_digest
+
+        from ..parallel.failure import ABORT, CollectiveFitAborted, FitGuard
 
         comm, X, y = make_comm(
             getattr(self, "strategy", "auto"),
@@ -371,14 +379,29 @@ class _ParallelMixin:
             except Exception as e:
                 error = e
             self._raise_if_any_failed(comm, error)
-        try:
-            self._fit_impl(X, y, comm=comm, **kw)
-        except Exception as e:  # reported to every rank below
-            error = e
-        # one all-gather of {failed, tree digest}: failure propagation + consistency
-        check = os.environ.get("MPITREE_CHECK_CONSISTENCY", "1") != "0"
-        digest = tree_digest(self._arrays) if (error is None and check) else 0
-        st = comm._all_gather(np.array([1 if error is not None else 0, digest], np.int64))
+        # failure containment (parallel/failure.py): a rank that fails mid-fit
+        # publishes it through the c10d store; peers' host loops notice and fail
+        # too, or, when a peer is stuck inside a collective, the group is aborted
+        # -- no rank waits for the process-group timeout
+        with FitGuard(comm) as guard:
+            try:
+                self._fit_impl(X, y, comm=comm, **kw)
+            except Exception as e:  # reported to every rank below
+                error = e
+                if isinstance(e, CollectiveFitAborted) or ABORT.is_set():
+                    # (a peer failed first: its error, not this rank's broken collective)
+                    error = CollectiveFitAborted(f"collective fit aborted ({guard.describe()})")
+                torn = guard.fail(error)
+                if torn is not None:
+                    raise torn
+            # one all-gather of {failed, tree digest}: failure propagation + consistency
+            check = os.environ.get("MPITREE_CHECK_CONSISTENCY", "1") != "0"
+            digest = tree_digest(self._arrays) if (error is None and check) else 0
+            try:
+                st = comm._all_gather(np.array([1 if error is not None else 0, digest],
+                                               np.int64))
+            except Exception as e:  # a failed peer tore the group down meanwhile
+                raise CollectiveFitAborted(f"collective fit aborted ({guard.describe()})") from e
         if st[:, 0].any():
             self._raise_if_any_failed(comm, error, known_failed=True)
         if check and not (st[:, 1] == st[0, 1]).all():

@@ -1159,7 +1159,10 @@ __device__ __forceinline__ int xe_part_batch(int F_loc) {
   if (F_loc <= kXePartBatch) return F_loc;
   for (int d = kXePartBatch; d >= 4; --d)
     if (F_loc % d == 0) return d;
-  return F_loc <= 64 ? F_loc : 1;
+  // no divisor: a claim of kXePartBatch < F_loc tickets still never holds a
+  // ticket and the one it depends on (F_loc earlier); it only straddles two
+  // sub-chunks, which costs nothing like 16x the counter atomics
+  return kXePartBatch;
 }
 
 template <bool kLdsFlags, bool kReg>

@@ -64,6 +64,7 @@ import torch
 from ..models.tree_arrays import TreeArrays
 from ..utils.observability import profiling
 from . import hip_backend as hb
+from ..parallel.failure import ABORT, check_abort, fault_point
 from ..parallel.strategies import feature_blocks
 
 __all__ = ["DeviceGrower", "device_loop_supported"]
@@ -94,6 +95,8 @@ def _wait_slot(hctl, slot: int, tag: int):
     while row[2] != tag:
         k += 1
         if (k & 0xFFFF) == 0:
+            if ABORT.is_set():  # a peer rank failed the collective fit
+                check_abort()
             if time.perf_counter() > t_end:
                 raise RuntimeError("device level loop: planner result never arrived "
                                    f"(slot {slot}, tag {tag}); the GPU stream is stuck")
@@ -571,6 +574,9 @@ class DeviceGrower:
                               tag0 + (lvl % 4096) + 1, dp=int(dp), fixup=fixup, own=own_args)
 
             while True:
+                if P > 1:  # failure containment: a failed peer / injected fault
+                    check_abort()
+                    fault_point(comm, f"level:{lvl}")
                 b0 = getattr(comm, "bytes_communicated", 0)
                 if prof:
                     marks.append([])

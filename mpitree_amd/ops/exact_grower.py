@@ -42,6 +42,7 @@ import torch
 from . import hip_backend as hb
 from .device_grower import _host_ctl, _wait_slot, _FIT_SEQ, exchange_ranges
 from ..core.criterion import Criterion
+from ..parallel.failure import check_abort, fault_point
 
 __all__ = ["ExactGrower", "exact_supported"]
 
@@ -277,6 +278,9 @@ class ExactGrower:
         lvl, done_at = 0, None
         comm_bytes = []
         while True:
+            if P > 1:  # failure containment: a failed peer / injected fault
+                check_abort()
+                fault_point(comm, f"level:{lvl}")
             b0 = getattr(comm, "bytes_communicated", 0)
             kb = int(min(2 ** min(lvl, 40), KMAX))
             ib = int(min(IMAX, kb + n // chunk + 1))
@@ -333,6 +337,9 @@ class ExactGrower:
         if timings is not None:
             timings["finisher"] = time.perf_counter() - t2
         t3 = time.perf_counter()
+        if P > 1:  # a rank whose look-back timed out shared corrupt records / flags:
+            # every rank must raise, not only that one (MAX of the watchdog words)
+            comm.all_reduce_device(ws["tick"][2:3], op=torch.distributed.ReduceOp.MAX)
         watch = hb._pinned_copy(ws["tick"][2:3], "exact.watch")
         ta = be.assemble_positions(None, int(crit), y_exp, thr_pos=pos_thr)  # (synchronises)
         if int(watch[0]) != 0:

@@ -30,7 +30,8 @@ def _entry(rank, world, port, fn, args, outdir, backend="gloo"):
         out = fn(rank, world, *args)
         np.savez(os.path.join(outdir, f"r{rank}.npz"), **out)
     finally:
-        dist.destroy_process_group()
+        if dist.is_initialized():  # (a failed collective fit may have torn it down)
+            dist.destroy_process_group()
 
 
 def run_ranks(fn, world, *args, start_method="fork", backend="gloo"):

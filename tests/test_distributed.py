@@ -325,6 +325,39 @@ def test_fault_on_one_rank_raises_everywhere(fault_rank):
     assert outs[0]["nodes"][0] == outs[1]["nodes"][0] > 1
 
 
+def _fault_mid_loop(rank, world, strategy):
+    import os
+    import time
+
+    from mpitree_amd import ParallelDecisionTreeClassifier
+    from mpitree_amd.parallel.failure import CollectiveFitAborted
+    from mpitree_amd.utils.observability import InjectedFault
+
+    os.environ.update(MPITREE_FAULT_RANK="1", MPITREE_FAULT_AT="level:2", MPITREE_FAIL_WAIT="2")
+    X, y = _data(3, n=3000)
+    kind, t0 = "ok", time.monotonic()
+    try:
+        ParallelDecisionTreeClassifier(strategy=strategy, device="cpu").fit(X, y)
+    except InjectedFault:
+        kind = "injected"
+    except CollectiveFitAborted as e:
+        kind = "peer" if "rank 1" in str(e) and "InjectedFault" in str(e) else f"other:{e}"
+    except Exception as e:  # noqa: BLE001
+        kind = f"other:{type(e).__name__}:{e}"
+    return {"kind": np.array([kind]), "s": np.array([time.monotonic() - t0])}
+
+
+@pytest.mark.parametrize("strategy", ["feature", "data", "subtree"])
+def test_fault_inside_level_loop_raises_everywhere(strategy):
+    """A rank that fails inside the level loop (peers blocked in that level's
+    collective, or still growing) makes every rank raise within seconds -- not
+    after the process-group timeout (parallel/failure.py)."""
+    outs = run_ranks(_fault_mid_loop, 2, strategy)
+    kinds = [str(o["kind"][0]) for o in outs]
+    assert kinds == ["peer", "injected"], kinds
+    assert max(float(o["s"][0]) for o in outs) < 30
+
+
 def _digest_rank(rank, world):
     from mpitree_amd.parallel.strategies import FeatureParallelComm
 
