@@ -192,51 +192,14 @@ def _finalize(ta: TreeArrays, mapper: BinMapper, regression: bool, y_exp: int) -
     return ta
 
 
-def _fit_exact_gpu(Xd, yd, classes, C, crit, params, comm, timings, t_bin, t_start, F):
-    """Classification with every unique value a threshold on continuous
-    features beyond the device engine's reach (more than 16 classes with a
-    wide histogram): level-wise growth over presorted per-feature lists
-    (``ops/exact_backend.py``), run by every rank."""
-    from ..ops.exact_backend import ExactHipBackend
-
-    be = ExactHipBackend()
-    be.setup_exact(Xd, yd.to(torch.int32), C, crit)
-    timings["bin"] = time.perf_counter() - t_bin
-    # subtrees of <= 256 rows continue in the histogram finisher on local codes
-    env = os.environ.get("MPITREE_EXACT_FINISHER_ROWS")
-    fr = int(env) if env else be.max_finisher_rows
-    params.finisher_rows = min(fr, be.max_finisher_rows) if be.finisher_supported() else 0
-    builder = LevelwiseBuilder(be, params, LocalComm())
-    dummy_edges = np.zeros((F, 1))  # thresholds come from the device unique-value table
-    with roctx_range("mpitree.grow"):
-        ta = builder.fit(Xd.shape[0], C, F, edges=dummy_edges)
-    timings.update(builder.timings)
-    stats = dict(builder.stats)
-    stats["thresholds"] = "exact (presorted lists, host-driven levels)"
-    if comm.world_size > 1:
-        stats["strategy"] = comm.kind
-        stats["mode"] = "replicated-exact"
-    ta = _finalize(ta, None, False, 0)
-    timings["total"] = time.perf_counter() - t_start
-    # the exact engine's "bins" are value ranks; the unique values stay on the device
-    mapper = BinMapper(edges=[], exact=np.ones(F, bool), max_bins=None)
-    return FitResult(arrays=ta, classes=classes, n_features=F, mapper=mapper, y_scale_exp=0,
-                     engine="hip-exact", timings=timings, stats=stats)
-
-
 def _exact_device_ok(n, F, C, regression) -> bool:
-    """The device-driven exact engine (``ops/exact_grower.py``) runs when its
-    finisher takes the <= 256-row jobs on local codes."""
-    from ..ops import native
+    """The device-driven exact engine (``ops/exact_grower.py``) takes any
+    feature count and any class count below 2^20 on fewer than 2^24 rows (its
+    <= 256-row finisher jobs run where the local-code finishers fit: at most 256
+    classes; otherwise its level loop grows to the leaves)."""
     from ..ops.exact_grower import exact_supported
 
-    if os.environ.get("MPITREE_EXACT_V1") == "1" or not exact_supported(n, C, regression):
-        return False
-    if F > 256:  # (the v2 engine's local-code finisher rows are at most 256 bytes)
-        return False
-    if regression:
-        return True
-    return native.hip().finish_feature_tile(F, 256, C) > 0
+    return exact_supported(n, C, regression)
 
 
 def _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t_bin, t_start, F, regression):
@@ -373,25 +336,20 @@ def fit_tree(
         mapper, codes_rm, codes_fm, nb = prep.mapper, prep.codes_rm, prep.codes_fm, prep.nbins
         yd, classes, y_exp, root = prep.y, prep.classes, prep.y_exp, prep.root
         C = 0 if regression else len(classes)
-        from ..ops.exact_backend import exact_supported, needs_exact
+        from ..ops.exact_grower import needs_exact
 
         if max_bins is None and g_mapper is None and needs_exact(mapper):
-            dev_ok = _exact_device_ok(n, F, C, regression)
-            if dev_ok or exact_supported(n, C, regression):
+            if _exact_device_ok(n, F, C, regression):
                 if checkpoint is not None:  # the same tree, just no mid-fit state
                     logger.warning("the exact-threshold GPU engine keeps no level "
                                    "checkpoint: fitting without one")
                 if prep.verify is not None and not prep.verify():
                     return fit_tree(X, y, **redo)
-                if dev_ok:
-                    return _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t0,
-                                             t_start, F, regression)
-                return _fit_exact_gpu(Xd, yd, classes, C, crit, params, comm, timings, t0,
-                                      t_start, F)
+                return _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t0,
+                                         t_start, F, regression)
             logger.warning("exact thresholds on > 256-value features are not available on "
-                           "the GPU for this fit (>= 2^24 rows, > 256 features with a "
-                           "regression target, or > 256 classes): using 256 quantile bins "
-                           "per feature")
+                           "the GPU for this fit (>= 2^24 rows or >= 2^20 classes): using "
+                           "256 quantile bins per feature")
             quantile_fallback = True
         lo, hi = comm.local_rows(n)
         if (lo, hi) != (0, n):  # data-parallel shard of a replicated input

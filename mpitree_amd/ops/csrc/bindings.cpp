@@ -50,25 +50,10 @@ void launch_hw_xlog2x(hipStream_t, float*, int);
 int finish_feature_tile(int F, int B, int C);
 int asm_tiles(int64_t P);
 void launch_grow_plan(hipStream_t, const PlanArgs&);
-void ex_scan_level(hipStream_t, const uint64_t*, int64_t, const int64_t*, int, const int64_t*,
-                   const int64_t*, int, int, int, int, int64_t, const double*, int, int32_t*,
-                   int32_t*, int32_t*, unsigned long long*, int64_t*);
-void ex_partition_level(hipStream_t, const uint64_t*, uint64_t*, int64_t, const int64_t*, int,
-                        const int64_t*, const int64_t*, int, int, uint8_t*, int32_t*, int32_t*,
-                        int32_t*, unsigned long long*);
-int ex_chunk();
-int ex_part_bits_words();
-void ex_local_codes(hipStream_t, const uint64_t*, const uint64_t*, int64_t, const int64_t*, int,
-                    int, int, uint8_t*, uint8_t*, uint32_t*, uint32_t*);
-void ex_local_fix(hipStream_t, const uint64_t*, const uint64_t*, int64_t, const int64_t*, int,
-                  int32_t*);
-int ex_local_max();
 size_t exact_setup_temp_bytes(int64_t, int);
 void exact_setup_sort(hipStream_t, const float*, int64_t, int, uint64_t*, uint64_t*, uint32_t*,
                       uint32_t*, void*, size_t, int32_t*, int32_t*, int, int);
 void bind_exact2(pybind11::module_& m);
-void exact_setup_emit(hipStream_t, const uint64_t*, const uint32_t*, int64_t, int,
-                      const int32_t*, const int32_t*, int, uint64_t*, double*);
 int exact_setup_chunk();
 void launch_fp_combine(hipStream_t, const int64_t*, int, int, int, const int32_t*, int64_t*);
 void launch_grow_dp_fixup(hipStream_t, const PlanArgs&);
@@ -315,8 +300,6 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("job_count"), py::arg("C"), py::arg("max_depth"), py::arg("n_cu"), py::arg("mss"),
      py::arg("msl"), py::arg("fr"), py::arg("host_ctl"), py::arg("host_tag"), py::arg("dp") = 0,
      py::arg("fixup") = false, py::arg("own") = py::dict());
-  m.def("ex_chunk", &mt::ex_chunk);
-  m.def("ex_local_max", &mt::ex_local_max);
   m.def("exact_setup_temp_bytes", &mt::exact_setup_temp_bytes);
   m.def("exact_setup_chunk", &mt::exact_setup_chunk);
   m.def("exact_setup_sort", [](uintptr_t s, uintptr_t X, int64_t n, int F, uintptr_t k0,
@@ -329,42 +312,6 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("s"), py::arg("X"), py::arg("n"), py::arg("F"), py::arg("k0"), py::arg("k1"),
      py::arg("r0"), py::arg("r1"), py::arg("temp"), py::arg("temp_bytes"), py::arg("cnt"),
      py::arg("nuniq"), py::arg("xs") = 0, py::arg("f_lo") = 0);
-  m.def("exact_setup_emit", [](uintptr_t s, uintptr_t k1, uintptr_t r1, int64_t n, int F,
-                               uintptr_t cnt, uintptr_t y, int B, uintptr_t E, uintptr_t uniq) {
-    mt::exact_setup_emit(S(s), P<uint64_t>(k1), P<uint32_t>(r1), n, F, P<int32_t>(cnt),
-                         P<int32_t>(y), B, P<uint64_t>(E), P<double>(uniq));
-  });
-  m.def("ex_local_codes", [](uintptr_t s, uintptr_t E0, uintptr_t E1, int64_t n, uintptr_t seg,
-                             int J, int F, int row_bytes, uintptr_t codes_rm, uintptr_t codes_fm,
-                             uintptr_t ent, uintptr_t inv) {
-    mt::ex_local_codes(S(s), P<uint64_t>(E0), P<uint64_t>(E1), n, P<int64_t>(seg), J, F,
-                       row_bytes, P<uint8_t>(codes_rm), P<uint8_t>(codes_fm), P<uint32_t>(ent),
-                       P<uint32_t>(inv));
-  });
-  m.def("ex_local_fix", [](uintptr_t s, uintptr_t E0, uintptr_t E1, int64_t n, uintptr_t jobs,
-                           int J, uintptr_t node_i32) {
-    mt::ex_local_fix(S(s), P<uint64_t>(E0), P<uint64_t>(E1), n, P<int64_t>(jobs), J,
-                     P<int32_t>(node_i32));
-  });
-  m.def("ex_scan_level", [](uintptr_t s, uintptr_t E, int64_t n, uintptr_t items, int NI,
-                            uintptr_t ifirst, uintptr_t seg, int K, int F, int C, int crit,
-                            int64_t msl, uintptr_t xtab, int xtab_n, uintptr_t tot,
-                            uintptr_t carry, uintptr_t slot_tot, uintptr_t best, uintptr_t rec) {
-    mt::ex_scan_level(S(s), P<uint64_t>(E), n, P<int64_t>(items), NI, P<int64_t>(ifirst),
-                      P<int64_t>(seg), K, F, C, crit, msl, P<double>(xtab), xtab_n,
-                      P<int32_t>(tot), P<int32_t>(carry), P<int32_t>(slot_tot),
-                      P<unsigned long long>(best), P<int64_t>(rec));
-  });
-  m.def("ex_partition_level", [](uintptr_t s, uintptr_t E, uintptr_t D, int64_t n,
-                                 uintptr_t pitems, int NP, uintptr_t pfirst, uintptr_t split,
-                                 int Sn, int F, uintptr_t flag, uintptr_t lc, uintptr_t lcar,
-                                 uintptr_t nl, uintptr_t bits) {
-    mt::ex_partition_level(S(s), P<uint64_t>(E), P<uint64_t>(D), n, P<int64_t>(pitems), NP,
-                           P<int64_t>(pfirst), P<int64_t>(split), Sn, F, P<uint8_t>(flag),
-                           P<int32_t>(lc), P<int32_t>(lcar), P<int32_t>(nl),
-                           P<unsigned long long>(bits));
-  });
-  m.def("ex_part_bits_words", &mt::ex_part_bits_words);
   m.def("fp_combine", [](uintptr_t s, uintptr_t g, int nranks, int KB, int R, uintptr_t dcount,
                          uintptr_t rec) {
     mt::launch_fp_combine(S(s), P<int64_t>(g), nranks, KB, R, P<int32_t>(dcount),

@@ -33,6 +33,9 @@ struct XeArgs {
   int64_t n;
   int F, f_lo, F_loc;
   int C;               // classes (classification); 0 for regression
+  // labels by row when C > 128 (xe_packed_classes): the list entries then carry
+  // none and every label read gathers ylab[row]; null when the entries carry them
+  const int32_t* ylab;
   int crit;
   int64_t msl;
   const double* xtab;
@@ -93,6 +96,7 @@ struct XePlanArgs {
 int xe_chunk();
 int xe_local_max();
 int xe_max_classes();
+int xe_packed_classes();
 void xe_init(hipStream_t s, const XeLists& L, int64_t n, int Cs, const int64_t* root, int32_t* jc);
 void xe_level_scan(hipStream_t s, const XeArgs& a, const XeLists& cur, int items_bound,
                    int slots_bound);
@@ -103,7 +107,7 @@ void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems
 void xe_local_codes(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const int64_t* Y0,
                     const int64_t* Y1, const void* X, int x64, int F, int fg_lo, int64_t n,
                     int F_loc, int f_lo, const int64_t* jobs, int J, int JW, uint8_t* codes_fm,
-                    uint32_t* ent, int64_t* yv);
+                    uint32_t* ent, int64_t* yv, const int32_t* ylab);
 void xe_codes_rm(hipStream_t s, const uint8_t* codes_fm, int64_t n, int F, int row_bytes,
                  const int64_t* jobs, int J, int JW, uint8_t* codes_rm);
 void xe_fix(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const void* X, int x64, int F,

@@ -10,6 +10,9 @@
 //
 //   E[f][p] = row | dup << 24 | label << 25          (rows < 2^24, labels < 128)
 //
+// (more than 128 classes: E[f][p] = row | dup << 24 and labels are gathered from
+// the row-indexed label array -- any class count, one gather per label read)
+//
 // (dup: the value occurs more than once in the column; only then do two
 // neighbours' values need comparing, from X itself) plus, for regression, the
 // fixed-point target Y[f][p] moved alongside. Split thresholds are data values
@@ -55,6 +58,7 @@ constexpr int kXePer = 8;                       // entries per thread
 constexpr int kXeChunk = kXeThreads * kXePer;   // entries per chunk item
 constexpr int kXeWaves = kXeThreads / kWave;
 constexpr int kXeMaxC = 128;                    // labels live in 7 bits of an entry
+constexpr int kXeMaxClasses = 1 << 20;          // labels by row (XeArgs::ylab) past kXeMaxC
 constexpr int kXePlanThreads = 512;
 constexpr int kXePlanWaves = kXePlanThreads / kWave;
 constexpr int kXeLocalMax = 256;                // finisher jobs: local codes fit a byte
@@ -62,6 +66,10 @@ constexpr int kXeLocalMax = 256;                // finisher jobs: local codes fi
 __device__ __forceinline__ uint32_t xe_row(uint32_t e) { return e & 0xFFFFFFu; }
 __device__ __forceinline__ bool xe_dup(uint32_t e) { return (e >> 24) & 1u; }
 __device__ __forceinline__ int xe_lab(uint32_t e) { return (int)(e >> 25); }
+// the label of an entry: packed in the entry, or (C > kXeMaxC) gathered by row
+__device__ __forceinline__ int xe_label(const XeArgs& a, uint32_t e) {
+  return a.ylab ? a.ylab[xe_row(e)] : xe_lab(e);
+}
 
 __device__ __forceinline__ double xe_tl(int64_t x, const double* __restrict__ tab, int tn) {
   return x < (int64_t)tn ? tab[x] : xlog2x((uint64_t)x);
@@ -219,9 +227,17 @@ __device__ __forceinline__ void xe_tot_item(const XeArgs& a, const XeLists& L, i
     }
     return;
   }
+  if (a.C > kXeMaxC) {  // many classes: count straight into the chunk's totals
+    for (int c = tid; c < a.C; c += kXeThreads) out[c] = 0;
+    __threadfence_block();
+    __syncthreads();
+    for (int64_t i = tid; i < cn; i += kXeThreads)
+      atomicAdd(reinterpret_cast<unsigned long long*>(out + xe_label(a, E[i])), 1ull);
+    return;
+  }
   for (int c = tid; c < a.C; c += kXeThreads) s_c[c] = 0;
   __syncthreads();
-  for (int64_t i = tid; i < cn; i += kXeThreads) atomicAdd(&s_c[xe_lab(E[i])], 1u);
+  for (int64_t i = tid; i < cn; i += kXeThreads) atomicAdd(&s_c[xe_label(a, E[i])], 1u);
   __syncthreads();
   for (int c = tid; c < a.C; c += kXeThreads) out[c] = s_c[c];
 }
@@ -393,12 +409,18 @@ __device__ __forceinline__ void xe_scan_item(const XeArgs& a, const XeLists& L, 
       sL[k] = sR[k] = 0.0;
       qL[k] = qR[k] = 0;
     }
+    int lab[kXePer];
+#pragma unroll
+    for (int k = 0; k < kXePer; ++k)
+      lab[k] = (int64_t)k * kXeThreads + tid < cn ? xe_label(a, e[k]) : -1;
     for (int c = 0; c < a.C; ++c) {
+      // a class absent from the node adds T(0) = 0 (or 0 squared) on both sides:
+      // skipping it leaves every sum bit-identical (block-uniform: one slot per item)
+      if (L.stats[slot * Cc + c] == 0) continue;
       unsigned long long bal[kXePer];
 #pragma unroll
       for (int k = 0; k < kXePer; ++k) {
-        const int64_t i = (int64_t)k * kXeThreads + tid;
-        bal[k] = __ballot(i < cn && xe_lab(e[k]) == c);
+        bal[k] = __ballot(lab[k] == c);
         if (lane == 0) s_cnt[k * kXeWaves + wave] = (uint32_t)__popcll(bal[k]);
       }
       __syncthreads();
@@ -752,7 +774,7 @@ __global__ __launch_bounds__(kXeThreads) void xe_select_kernel(XeArgs a, XeLists
       s_pterm = a.crit == kEntropy ? xlog2x((uint64_t)m) - acc : gini_term(m, sq);
     }
   }
-  for (int c = tid; c < a.C; c += kXeThreads) s_c[c] = 0;
+  for (int c = tid; c < a.C && c < kXeMaxC; c += kXeThreads) s_c[c] = 0;
   __syncthreads();
   const double pterm = s_pterm;
   const double tu = a.C ? tie_unit(xe_tl(m, a.xtab, a.xtab_n), m) : 0.0;
@@ -862,9 +884,15 @@ __global__ __launch_bounds__(kXeThreads) void xe_select_kernel(XeArgs a, XeLists
       out[7] = car[0] + (nrows - t);
       if (a.C == 2) out[8] = car[1] + t;
     }
+  } else if (a.C > kXeMaxC) {  // many classes: the chunk carry, then count into the record
+    for (int c = tid; c < a.C; c += kXeThreads) out[7 + c] = car[c];
+    __threadfence_block();
+    __syncthreads();
+    for (int64_t p = cfirst + tid; p <= start + bp; p += kXeThreads)
+      atomicAdd(reinterpret_cast<unsigned long long*>(out + 7 + xe_label(a, Ef[p])), 1ull);
   } else {
     for (int64_t p = cfirst + tid; p <= start + bp; p += kXeThreads)
-      atomicAdd(&s_c[xe_lab(Ef[p])], 1u);
+      atomicAdd(&s_c[xe_label(a, Ef[p])], 1u);
     __syncthreads();
     for (int c = tid; c < a.C; c += kXeThreads) out[7 + c] = car[c] + (int64_t)s_c[c];
   }
@@ -1283,7 +1311,7 @@ __global__ __launch_bounds__(kXeLocalMax) void xe_local_codes_kernel(
     const int64_t* __restrict__ Y0, const int64_t* __restrict__ Y1, const void* __restrict__ X,
     int x64, int F, int fg_lo, int64_t n, int F_loc, int f_lo,
     const int64_t* __restrict__ jobs, int JW, uint8_t* __restrict__ codes_fm,
-    uint32_t* __restrict__ ent, int64_t* __restrict__ yv) {
+    uint32_t* __restrict__ ent, int64_t* __restrict__ yv, const int32_t* __restrict__ ylab) {
   __shared__ uint32_t s_row[kXeLocalMax];
   __shared__ uint32_t s_w[kXeLocalMax / kWave];
   __shared__ uint32_t s_e[kXeLocalMax + 1];
@@ -1326,7 +1354,8 @@ __global__ __launch_bounds__(kXeLocalMax) void xe_local_codes_kernel(
       ent[s + v] = (uint32_t)(s + v);
       yv[s + v] = (b1 ? Y1 : Y0)[s + t];
     } else {
-      ent[s + v] = ((uint32_t)xe_lab(e0) << 24) | (uint32_t)(s + v);
+      const uint32_t lab = ylab ? (uint32_t)ylab[xe_row(e0)] : (uint32_t)xe_lab(e0);
+      ent[s + v] = (lab << 24) | (uint32_t)(s + v);  // (finisher jobs: <= 256 classes)
     }
   }
   for (int f = 0; f < F_loc; ++f) {
@@ -1496,7 +1525,8 @@ __global__ __launch_bounds__(256) void xe_emit_kernel(const uint64_t* __restrict
 // --------------------------------------------------------------- launchers
 int xe_chunk() { return kXeChunk; }
 int xe_local_max() { return kXeLocalMax; }
-int xe_max_classes() { return kXeMaxC; }
+int xe_max_classes() { return kXeMaxClasses; }
+int xe_packed_classes() { return kXeMaxC; }
 
 void xe_init(hipStream_t s, const XeLists& L, int64_t n, int Cs, const int64_t* root, int32_t* jc) {
   hipLaunchKernelGGL(xe_init_kernel, dim3(1), dim3(256), 0, s, L, n, Cs, root, jc);
@@ -1599,10 +1629,10 @@ void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems
 void xe_local_codes(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const int64_t* Y0,
                     const int64_t* Y1, const void* X, int x64, int F, int fg_lo, int64_t n,
                     int F_loc, int f_lo, const int64_t* jobs, int J, int JW, uint8_t* codes_fm,
-                    uint32_t* ent, int64_t* yv) {
+                    uint32_t* ent, int64_t* yv, const int32_t* ylab) {
   if (J <= 0) return;
   hipLaunchKernelGGL(xe_local_codes_kernel, dim3(J), dim3(kXeLocalMax), 0, s, E0, E1, Y0, Y1, X,
-                     x64, F, fg_lo, n, F_loc, f_lo, jobs, JW, codes_fm, ent, yv);
+                     x64, F, fg_lo, n, F_loc, f_lo, jobs, JW, codes_fm, ent, yv, ylab);
   MT_HIP_CHECK(hipGetLastError());
 }
 

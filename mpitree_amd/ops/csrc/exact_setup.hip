@@ -1,5 +1,5 @@
-// Setup of the exact-threshold engine (exact.hip): per feature, the rows sorted
-// by value, their dense value ranks and the sorted unique values.
+// Setup of the exact-threshold engine (exact2.hip): per feature, the rows sorted
+// by value and a per-chunk count of value changes (the dense value ranks).
 //
 // The reference sorts implicitly through np.unique per feature and node
 // (mpitree/tree/decision_tree.py:73). Here one pass over X builds 64-bit keys
@@ -8,8 +8,7 @@
 // features at once over only the key bits that vary (32 + ceil(log2 F)) with
 // 32-bit row ids as values, and two passes over the sorted keys derive the
 // ranks (a per-chunk count of value changes, a per-feature scan of the chunk
-// counts) and write the list entries E = rank << 32 | label << 24 | row and
-// the unique-value table.
+// counts); xe_emit_kernel (exact2.hip) then writes the list entries.
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
@@ -92,51 +91,6 @@ __global__ void xs_scan_kernel(int32_t* __restrict__ cnt, int nc, int F,
   nuniq[f] = acc;
 }
 
-// E[f][p] = rank << 32 | label << 24 | row; uniq[f][rank] = value at each change.
-// Entry p0 + k * 256 + tid (coalesced): a value change is a ballot bit, its
-// rank the chunk base + the changes of earlier (k, wave) steps (an LDS scan
-// over 16 x 4 counts) + the popcount of the lower lanes.
-__global__ __launch_bounds__(kXsThreads) void xs_emit_kernel(
-    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ rows, int64_t n, int nc,
-    const int32_t* __restrict__ cbase, const int32_t* __restrict__ y, int B,
-    uint64_t* __restrict__ E, double* __restrict__ uniq) {
-  constexpr int kSteps = kXsChunk / kXsThreads;
-  constexpr int kWaves = kXsThreads / kWave;
-  __shared__ int32_t s_cnt[kSteps * kWaves];
-  const int f = blockIdx.y, c = blockIdx.x;
-  const int lane = lane_id(), w = threadIdx.x >> 6;
-  const int64_t base = (int64_t)f * n;
-  const int64_t p0 = (int64_t)c * kXsChunk;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  unsigned long long bal[kSteps];
-#pragma unroll
-  for (int k = 0; k < kSteps; ++k) {
-    const int64_t p = p0 + k * kXsThreads + threadIdx.x;
-    const bool nw = p < n && (p == 0 || keys[base + p] != keys[base + p - 1]);
-    bal[k] = __ballot(nw);
-    if (lane == 0) s_cnt[k * kWaves + w] = __popcll(bal[k]);
-  }
-  __syncthreads();
-  if (threadIdx.x < kWave) {  // exclusive scan of the 64 step counts (one wave)
-    const uint32_t v = (uint32_t)s_cnt[threadIdx.x];
-    const uint32_t incl = wave_incl_scan_dpp(v);
-    s_cnt[threadIdx.x] = (int32_t)(incl - v);
-  }
-  __syncthreads();
-  const int32_t cb = cbase[(int64_t)f * nc + c];
-#pragma unroll
-  for (int k = 0; k < kSteps; ++k) {
-    const int64_t p = p0 + k * kXsThreads + threadIdx.x;
-    if (p >= n) break;
-    const bool nw = (bal[k] >> lane) & 1ull;
-    const int32_t rank = cb + s_cnt[k * kWaves + w] + __popcll(bal[k] & lt) + (nw ? 1 : 0) - 1;
-    const uint64_t key = keys[base + p];
-    if (nw) uniq[(int64_t)f * B + rank] = (double)xs_key_value((uint32_t)key);
-    const uint32_t row = rows[base + p];
-    E[base + p] = ((uint64_t)(uint32_t)rank << 32) | ((uint64_t)(y[row] & 0xff) << 24) | row;
-  }
-}
-
 size_t exact_setup_temp_bytes(int64_t n, int F) {
   size_t bytes = 0;
   const int64_t N = n * F;
@@ -170,17 +124,6 @@ void exact_setup_sort(hipStream_t stream, const float* X, int64_t n, int F, uint
   MT_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(xs_scan_kernel, dim3((F + 63) / 64), dim3(64), 0, stream, cnt, nc, F,
                      nuniq);
-  MT_HIP_CHECK(hipGetLastError());
-}
-
-// Phase 2: list entries and the [F][B] unique-value table (preset to +inf).
-void exact_setup_emit(hipStream_t stream, const uint64_t* keys1, const uint32_t* rows1,
-                      int64_t n, int F, const int32_t* cnt, const int32_t* y, int B, uint64_t* E,
-                      double* uniq) {
-  if (n <= 0 || F <= 0) return;
-  const int nc = (int)((n + kXsChunk - 1) / kXsChunk);
-  hipLaunchKernelGGL(xs_emit_kernel, dim3(nc, F), dim3(kXsThreads), 0, stream, keys1, rows1, n,
-                     nc, cnt, y, B, E, uniq);
   MT_HIP_CHECK(hipGetLastError());
 }
 

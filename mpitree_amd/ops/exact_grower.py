@@ -44,7 +44,7 @@ from .device_grower import _host_ctl, _wait_slot, _FIT_SEQ, exchange_ranges
 from ..core.criterion import Criterion
 from ..parallel.failure import check_abort, fault_point
 
-__all__ = ["ExactGrower", "exact_supported"]
+__all__ = ["ExactGrower", "exact_supported", "needs_exact"]
 
 MAX_ROWS = 1 << 24
 _WS: dict = {}
@@ -59,12 +59,25 @@ def _step(dev, what):
 
 
 def exact_supported(n: int, C: int, regression: bool) -> bool:
-    """Rows index 24 bits of a list entry; labels live in 7 bits."""
+    """Rows index 24 bits of a list entry. Labels of up to 128 classes ride in
+    the entries; more classes are gathered from a row-indexed label array."""
     from . import native
 
     if n >= MAX_ROWS:
         return False
     return regression or 1 <= C <= int(native.hip().xe_max_classes())
+
+
+def needs_exact(mapper) -> bool:
+    """A binned fit cannot be exact: some feature kept quantile edges."""
+    ex = np.asarray(getattr(mapper, "exact", []), dtype=bool)
+    return bool(ex.size) and not bool(ex.all())
+
+
+def _packed_labels(C: int) -> bool:
+    from . import native
+
+    return C <= int(native.hip().xe_packed_classes())
 
 
 def _owners(J: int, P: int, device) -> torch.Tensor:
@@ -95,7 +108,9 @@ class ExactGrower:
         Y = [torch.empty((F_loc, n), dtype=torch.int64, device=dev) for _ in range(2)] if reg \
             else [None, None]
         rank_at = torch.empty((F_loc, n), dtype=torch.int32, device=dev)
-        ylab = 0 if reg else y32.data_ptr()
+        # labels packed in the entries (<= 128 classes) or gathered by row (more)
+        packed = not reg and _packed_labels(int(self.C))
+        ylab = y32.data_ptr() if packed else 0
         yf = yfix.data_ptr() if reg else 0
         if Xd.dtype == torch.float32:
             keys = [torch.empty((F_loc, n), dtype=torch.int64, device=dev) for _ in range(2)]
@@ -127,7 +142,7 @@ class ExactGrower:
             rank = torch.cumsum(new, 1, dtype=torch.int32) - 1
             o32 = order.to(torch.int32)
             ent = o32 | (dup.to(torch.int32) << 24)
-            if not reg:
+            if packed:
                 ent = ent | (y32[order].to(torch.int32) << 25)
             E[0].copy_(ent)
             rank_at.copy_(rank)
@@ -155,6 +170,7 @@ class ExactGrower:
         Cx = 0 if reg else int(C)
         n, F = Xd.shape
         dev = Xd.device
+        self.C = Cx
         P = int(getattr(comm, "world_size", 1) or 1)
         rank = int(getattr(comm, "rank", 0) or 0)
         if P > 1:
@@ -172,6 +188,7 @@ class ExactGrower:
         s = hb._stream
         y32 = None if reg else y_codes.to(torch.int32).contiguous()
         yfix = y_codes.to(torch.int64).contiguous() if reg else None
+        self._y32 = y32
         E, Y, ranks = self._setup(Xd, F, f_lo, F_loc, y32, yfix, reg)
         if timings is not None:
             timings["exact_setup"] = time.perf_counter() - t0
@@ -201,6 +218,8 @@ class ExactGrower:
             return be.assemble_positions(None, int(crit), y_exp, thr_pos=pos_thr)
 
         fr = int(hip.xe_local_max())
+        if not reg and (C > 256 or int(hip.finish_feature_tile(F, 256, C)) <= 0):
+            fr = 0  # (the local-code finishers take <= 256 classes): levels to the leaves
         env = os.environ.get("MPITREE_EXACT_FINISHER_ROWS")  # (tests: 0 = no finisher)
         if env is not None:
             fr = max(0, min(fr, int(env)))
@@ -255,6 +274,7 @@ class ExactGrower:
             Y0=Y[0].data_ptr() if reg else 0, Y1=Y[1].data_ptr() if reg else 0,
             rank_of=0, X=Xd.data_ptr(), x64=int(Xd.dtype == torch.float64),
             n=n, F=F, f_lo=f_lo, F_loc=F_loc, C=Cx, crit=int(crit), msl=msl,
+            **({} if reg or _packed_labels(Cx) else {"ylab": y32.data_ptr()}),
             xtab=be.xtab.data_ptr(), xtab_n=int(be.xtab.numel()), tot=ptr["tot"],
             carry=ptr["carry"],
             cmm=ptr["cmm"], cbest=ptr["cbest"], cmin=ptr["cmin"], nmin=ptr["nmin"],
@@ -414,7 +434,8 @@ class ExactGrower:
                            Y[0].data_ptr() if reg else 0, Y[1].data_ptr() if reg else 0,
                            Xd.data_ptr(), x64, F, f_lo, n, F_loc, 0, jobs.data_ptr(), J, JW,
                            fm_out.data_ptr(), loc["ent"].data_ptr(),
-                           loc["yv"].data_ptr() if reg else 0)
+                           loc["yv"].data_ptr() if reg else 0,
+                           0 if reg or _packed_labels(self.C) else self._y32.data_ptr())
         if P > 1:  # every rank's feature block of the codes -> all features on every rank
             g = loc["gather"]
             comm.all_gather_device(g.view(-1), loc["blk"].view(-1))

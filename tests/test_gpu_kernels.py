@@ -454,7 +454,7 @@ def test_gpu_regression_tiny_prefilter_matches_host(kind):
                                    (8000, 5, 2, None, 3)])
 def test_gpu_exact_engine_matches_host(crit, shape):
     """Continuous features (> 256 unique values) with the exact default: the
-    presorted-list engine (exact.hip), whose <= 256-row subtrees continue in the
+    presorted-list engine (exact2.hip), whose <= 256-row subtrees continue in the
     histogram finisher on local codes, builds the host builder's tree bit for bit."""
     n, F, C, md, msl = shape
     rng = np.random.default_rng(n + F)
@@ -476,31 +476,74 @@ def test_gpu_exact_engine_matches_host(crit, shape):
 
 def test_gpu_exact_setup_native_equals_torch_path():
     """float32 inputs take the native setup (exact_setup.hip: transposed keys,
-    one radix sort, rank / entry passes); float64 inputs the torch sort path.
-    Negative zeros, negatives, many ties and > 256 values per feature: the
-    same lists, unique values and tree."""
-    from mpitree_amd.core.criterion import Criterion
-    from mpitree_amd.ops.exact_backend import ExactHipBackend
-
+    one radix sort, rank passes, xe_emit); float64 inputs the torch sort path.
+    Negative zeros, negatives, many ties and > 256 values per feature: the same
+    tree either way, equal to the host builder's."""
     rng = np.random.default_rng(21)
     n, F = 9000, 70
     X = np.round(rng.normal(size=(n, F)), 3).astype(np.float32)
     X[rng.random((n, F)) < 0.05] = -0.0
     X[:, 5] = np.round(X[:, 5], 0)
     y = rng.integers(0, 3, size=n)
-    yd = torch.from_numpy(y).cuda().to(torch.int32)
-    a, b = ExactHipBackend(), ExactHipBackend()
-    a.setup_exact(torch.from_numpy(X).cuda(), yd, 3, Criterion.ENTROPY)
-    b.setup_exact(torch.from_numpy(X.astype(np.float64)).cuda(), yd, 3, Criterion.ENTROPY)
-    assert a.B == b.B
-    assert torch.equal(a.nbins.cpu(), b.nbins.cpu())
-    # (the float64 sort orders -0.0 before +0.0 rows inside an equal-value run)
-    assert torch.equal(torch.sort(a.E[0], 1)[0].cpu(), torch.sort(b.E[0], 1)[0].cpu())
-    assert torch.equal(a.uniq.cpu(), b.uniq.cpu())
     g32 = DecisionTreeClassifier(device="cuda").fit(X, y)
     g64 = DecisionTreeClassifier(device="cuda").fit(X.astype(np.float64), y)
     assert g32.fit_stats_["engine"] == g64.fit_stats_["engine"] == "hip-exact"
     assert g32.tree_arrays_.equal(g64.tree_arrays_)
+    h = DecisionTreeClassifier(device="cpu").fit(X, y)
+    assert g32.tree_arrays_.equal(h.tree_arrays_)
+
+
+@pytest.mark.parametrize("C", [130, 300])
+def test_gpu_exact_many_classes_matches_host(C):
+    """More than 128 classes on continuous features: labels leave the list
+    entries (gathered by row); more than 256 classes also skip the local-code
+    finisher (the list engine grows every level). Same tree as the host."""
+    rng = np.random.default_rng(C)
+    n, F = 6000, 3
+    X = np.round(rng.normal(size=(n, F)), 3).astype(np.float32)
+    s = X[:, 0] + 0.5 * X[:, 1]
+    y = np.digitize(s, np.quantile(s, np.linspace(0, 1, C + 1)[1:-1]))
+    g = DecisionTreeClassifier(device="cuda").fit(torch.from_numpy(X).cuda(),
+                                                  torch.from_numpy(y).cuda())
+    assert g.fit_stats_["engine"] == "hip-exact"
+    assert "quantile" not in str(g.fit_stats_.get("thresholds", ""))
+    h = DecisionTreeClassifier(device="cpu").fit(X, y)
+    assert g.tree_arrays_.equal(h.tree_arrays_)
+    np.testing.assert_array_equal(g.tree_arrays_.threshold, h.tree_arrays_.threshold)
+
+
+def test_gpu_exact_n_classes_published_workload():
+    """The reference's published timing workload at n = 5000: X = arange(n)
+    (one feature), y = arange(n) (every row its own class). On the GPU the exact
+    list engine grows it to n leaves -- the CPU tree, node for node."""
+    n = 5000
+    X = np.arange(n, dtype=np.float64).reshape(-1, 1)
+    y = np.arange(n)
+    g = DecisionTreeClassifier(device="cuda").fit(torch.from_numpy(X).cuda(),
+                                                  torch.from_numpy(y).cuda())
+    assert g.fit_stats_["engine"] == "hip-exact"
+    h = DecisionTreeClassifier(device="cpu").fit(X, y)
+    assert g.tree_arrays_.equal(h.tree_arrays_)
+    assert int((g.tree_arrays_.feature < 0).sum()) == n
+    np.testing.assert_array_equal(np.asarray(g.predict(X)), y)
+
+
+@pytest.mark.parametrize("regression", [False, True])
+def test_gpu_exact_wide_features_device_engine(regression):
+    """More than 256 continuous features run the device-driven list engine
+    (feature-tiled local-code finisher), equal to the host builder."""
+    from mpitree_amd import DecisionTreeRegressor
+
+    rng = np.random.default_rng(300)
+    n, F = 4000, 300
+    X = np.round(rng.normal(size=(n, F)), 3).astype(np.float32)
+    s = X[:, 0] + X[:, 7] * X[:, 290] + rng.normal(scale=0.3, size=n)
+    cls = DecisionTreeRegressor if regression else DecisionTreeClassifier
+    yv = np.round(s, 2) if regression else (s > 0).astype(np.int64)
+    g = cls(device="cuda", max_depth=12).fit(X, yv)
+    assert g.fit_stats_["engine"] == "hip-exact"
+    h = cls(device="cpu", max_depth=12).fit(X, yv)
+    assert g.tree_arrays_.equal(h.tree_arrays_)
 
 
 def test_gpu_exact_finisher_handoff_same_tree(monkeypatch):
@@ -645,8 +688,7 @@ def test_gpu_finisher_many_classes_and_features(C, F, n):
                                                       cpu.tree_arrays_.node_count)
 
 
-@pytest.mark.parametrize("v1", [False, True])
-def test_gpu_exact_engine_matches_reference_source(monkeypatch, v1):
+def test_gpu_exact_engine_matches_reference_source(monkeypatch):
     """The GPU exact-threshold engines against the reference implementation's own
     outputs: continuous problems (every value unique) fitted by the reference
     source on a CPU (tools/make_reference_exact_fixtures.py; the GPU box has no
@@ -656,8 +698,6 @@ def test_gpu_exact_engine_matches_reference_source(monkeypatch, v1):
     import re
 
     monkeypatch.setenv("MPITREE_SMALL_FIT", "0")  # (<= 1024 rows: the exact list engine)
-    if v1:
-        monkeypatch.setenv("MPITREE_EXACT_V1", "1")
     path = pathlib.Path(__file__).parent / "fixtures" / "reference_exact.json"
     canon = lambda t: re.sub(r"-(0\.0+)\]", r"\1]", t)  # noqa: E731
     for p in json.loads(path.read_text()):
