@@ -21,6 +21,10 @@ finisher share, exchange stand-in, assembly + the full tree's D2H):
 * ``rows_owned`` / ``units`` -- the LPT's per-rank rows and the unit count.
 
     python bench/sim_own_ranks.py [--n 1000000] [--features 64] [--ranks 1,2,4,8]
+                                  [--regression] [--continuous]
+
+``--regression``: the 1M x 64 MSE regression tree (BASELINE config 5), whose
+exchange rows carry int64 {count, sum} statistics.
 """
 
 from __future__ import annotations
@@ -59,17 +63,22 @@ class SimOwnComm(LocalComm):
         return torch.cat([t, self.ref_rows.to(t.dtype)], 0)
 
 
-def reference_rows(fit, dev):
-    """The position-space rows {pos, record[6], counts[C]} of a finished 1-GPU fit."""
+def reference_rows(fit, dev, regression=False):
+    """The position-space rows {pos, record[6], stats} of a finished 1-GPU fit:
+    int32 class counts, or (regression) int64 {count, fixed-point sum}."""
     from mpitree_amd.ops import hip_backend as hb
 
     r = fit()
     n_pos = 2 * r.arrays.n_samples[0] - 1
     rec = hb._workspace(dev, "pos_rec", 0)[: n_pos * 24].view(torch.int32).view(-1, 6)
-    C = r.arrays.count.shape[1]
-    st = hb._workspace(dev, "pos_st", 0)[: n_pos * C * 4].view(torch.int32).view(-1, C)
     live = torch.nonzero(rec[:, 5] > 0).squeeze(1)
-    rows = torch.cat([live.to(torch.int32)[:, None], rec[live], st[live]], 1).clone()
+    if regression:
+        st = hb._workspace(dev, "pos_st", 0)[: n_pos * 16].view(torch.int64).view(-1, 2)
+        rows = torch.cat([live[:, None], rec[live].long(), st[live]], 1).clone()
+    else:
+        C = r.arrays.count.shape[1]
+        st = hb._workspace(dev, "pos_st", 0)[: n_pos * C * 4].view(torch.int32).view(-1, C)
+        rows = torch.cat([live.to(torch.int32)[:, None], rec[live], st[live]], 1).clone()
     return r, rows
 
 
@@ -82,22 +91,26 @@ def main():
     ap.add_argument("--units-per-rank", type=int, default=None)
     ap.add_argument("--only-rank", type=int, default=None,
                     help="simulate this rank only (profiling one rank's kernel sequence)")
+    ap.add_argument("--regression", action="store_true")
     a = ap.parse_args()
     if a.units_per_rank is not None:
         os.environ["MPITREE_OWN_UNITS_PER_RANK"] = str(a.units_per_rank)
     from mpitree_amd.core.fit import fit_tree
-    from mpitree_amd.utils.datasets import make_classification
+    from mpitree_amd.utils.datasets import make_classification, make_regression
 
     dev = torch.device("cuda", 0)
-    X, y = make_classification(a.n, a.features, n_classes=2, seed=0, device=dev)
+    if a.regression:  # (bench.py --regression: the same generator and seed)
+        X, y = make_regression(a.n, a.features, levels=256, seed=0, device=dev)
+    else:
+        X, y = make_classification(a.n, a.features, n_classes=2, seed=0, device=dev)
 
     def fit(comm=None):
-        return fit_tree(X, y, regression=False, criterion=0, max_depth=None,
-                        min_samples_split=2, device="cuda", comm=comm)
+        return fit_tree(X, y, regression=a.regression, criterion=2 if a.regression else 0,
+                        max_depth=None, min_samples_split=2, device="cuda", comm=comm)
 
     for _ in range(2):
         fit()
-    ref, ref_rows = reference_rows(fit, dev)
+    ref, ref_rows = reference_rows(fit, dev, a.regression)
     for P in [int(v) for v in a.ranks.split(",")]:
         per_rank = []
         for r in range(P) if a.only_rank is None else [a.only_rank]:

@@ -54,6 +54,7 @@ size_t exact_setup_temp_bytes(int64_t, int);
 void exact_setup_sort(hipStream_t, const float*, int64_t, int, uint64_t*, uint64_t*, uint32_t*,
                       uint32_t*, void*, size_t, int32_t*, int32_t*, int, int);
 void bind_exact2(pybind11::module_& m);
+void bind_grow(pybind11::module_& m);
 int exact_setup_chunk();
 void launch_fp_combine(hipStream_t, const int64_t*, int, int, int, const int32_t*, int64_t*);
 void launch_grow_dp_fixup(hipStream_t, const PlanArgs&);
@@ -381,6 +382,7 @@ PYBIND11_MODULE(_hip, m) {
     mt::launch_label_encode(S(s), P<int64_t>(y), n, lo, P<int64_t>(lut), P<int32_t>(out));
   });
   mt::bind_exact2(m);
+  mt::bind_grow(m);
   m.def("xlog2x_device", [](uintptr_t s, uintptr_t out, int64_t n) {
     mt::launch_xlog2x(S(s), P<double>(out), n);
   });

@@ -518,8 +518,8 @@ void launch_edges(hipStream_t stream, const void* X, bool x64, int64_t n, int F,
   const size_t lds = (size_t)S * xb + (size_t)kEdgeHash * xb;
   if (s > edges_sample_rows(x64)) throw std::runtime_error("edges sample exceeds LDS");
 #define MT_EDGES(XT)                                                                           \
-  MT_HIP_CHECK(hipFuncSetAttribute((const void*)edges_kernel<XT>,                              \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));     \
+  MT_HIP_CHECK(mt_set_max_lds((const void*)edges_kernel<XT>,                              \
+                                   (int)lds));     \
   hipLaunchKernelGGL(edges_kernel<XT>, dim3(F), dim3(kEdgeThreads), lds, stream, (const XT*)X, \
                      n, F, s, S, limit, (XT*)edges, nbins, exact);                             \
   if (pack) {                                                                                  \
@@ -559,8 +559,7 @@ void launch_bin(hipStream_t stream, const void* X, bool x64, int64_t n, int F, c
     const unsigned gx = (unsigned)((n + rpb - 1) / rpb);
     const size_t lds2 = (((size_t)nf * (Bmax | 1) * 4 + 15) & ~(size_t)15) + (size_t)batch * nf;
     const int fm_vec = ((n & 15) == 0 && ((uintptr_t)codes_fm & 15) == 0) ? 1 : 0;
-    MT_HIP_CHECK(hipFuncSetAttribute((const void*)bin_rows_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+    MT_HIP_CHECK(mt_set_max_lds((const void*)bin_rows_kernel, (int)lds2));
     hipLaunchKernelGGL(bin_rows_kernel, dim3(gx, (unsigned)tiles), dim3(kBrThreads), lds2, stream,
                        (const float*)X, n, F, (const float*)edges, Bmax, estride, steps0, nbins,
                        exact, (uint8_t*)codes_rm, row_elems, (uint8_t*)codes_fm, flags, rpb,
@@ -571,8 +570,8 @@ void launch_bin(hipStream_t stream, const void* X, bool x64, int64_t n, int F, c
   dim3 grid((unsigned)((n + kBinRows - 1) / kBinRows), (unsigned)((F + kBinFt - 1) / kBinFt));
 #define MT_BIN(XT, CT, L)                                                                      \
   {                                                                                            \
-    MT_HIP_CHECK(hipFuncSetAttribute((const void*)bin_kernel<XT, CT, L>,                       \
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));   \
+    MT_HIP_CHECK(mt_set_max_lds((const void*)bin_kernel<XT, CT, L>,                       \
+                                     (int)lds));   \
     hipLaunchKernelGGL((bin_kernel<XT, CT, L>), grid, dim3(256), lds, stream, (const XT*)X, n, \
                        F, (const XT*)edges, Bmax, estride, steps0, nbins, exact, (CT*)codes_rm, \
                        row_elems, (CT*)codes_fm, flags);                                       \

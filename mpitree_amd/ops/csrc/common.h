@@ -3,7 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdexcept>
+#include <map>
+#include <mutex>
 #include <string>
+#include <utility>
 
 #define MT_HIP_CHECK(expr)                                                        \
   do {                                                                            \
@@ -14,6 +17,23 @@
   } while (0)
 
 namespace mt {
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device,
+// size): the driver call costs microseconds of host time and the level loop
+// launches half a dozen LDS kernels per level. Sizes only grow (a larger
+// maximum serves every smaller launch).
+inline hipError_t mt_set_max_lds(const void* fn, int bytes) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = done.find({fn, dev});
+  if (it != done.end() && it->second >= bytes) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done[{fn, dev}] = bytes;
+  return e;
+}
 
 constexpr int kWave = 64;  // CDNA wavefront width
 

@@ -1606,8 +1606,8 @@ void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems
   if (a.n <= kXePartLdsRows && !lds_off) {
     const size_t lds = (size_t)((a.n + 31) / 32) * 4;
 #define MT_XP(REG)                                                                            \
-  MT_HIP_CHECK(hipFuncSetAttribute((const void*)xe_part_kernel<true, REG>,                    \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));    \
+  MT_HIP_CHECK(mt_set_max_lds((const void*)xe_part_kernel<true, REG>,                    \
+                                   (int)lds));    \
   hipLaunchKernelGGL((xe_part_kernel<true, REG>), dim3(grid), dim3(kXePartWaves * kWave), lds, \
                      s, a, cur);
     if (a.C == 0) {

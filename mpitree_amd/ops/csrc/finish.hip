@@ -62,10 +62,12 @@ constexpr int kFinUnroll = MT_FIN_UNROLL;  // row gathers in flight per lane
 constexpr int kFinMaxF = 256;    // features with LDS-cached bin counts (two-class path: all)
 constexpr int kFinPair = MT_FIN_PAIR;  // features scanned together per wave (latency hiding)
 constexpr int kFinChunk = 8;     // features per wave whose per-lane minima stay in registers
+constexpr int kFinCG = 4;        // generic scan: classes whose loads / DPP scans overlap
 
 // Histogram row stride in words: >= B*W + 1 (the odd word staggers features over
 // LDS banks for the atomics), rounded to 4 so each feature row is 16-B aligned.
 __host__ __device__ inline int fin_fstride(int B, int W) { return ((B * W + 1) + 3) & ~3; }
+__host__ __device__ inline int fstride_of(int B, int C) { return fin_fstride(B, (C + 1) >> 1); }
 
 inline int getenv_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -136,6 +138,11 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
 
   const int tid = threadIdx.x;
   const bool tiled = Ft < F;
+  // C > 2 (generic path): the node's present class ids + their count at [C]
+  int32_t* const cls_lds =
+      (!kC2 && C > 2) ? reinterpret_cast<int32_t*>(hist + Ft * fstride_of(B, C)) +
+                            (B > 256 ? (kFinThreadsWide / kWave) * C : 0)
+                      : nullptr;
   int32_t* const stc = gstk ? gstk + (int64_t)blockIdx.x * (kFinStack + 2) * C : s_st_cnt;
   const int stw = gstk ? C : kFinStackC;  // stack row stride
   int32_t* const s_cnt = gstk ? stc + kFinStack * C : s_cnt_l;
@@ -415,6 +422,29 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         s_rc = 0;
       }
       __syncthreads();
+      // ---- more than two classes: the node's present classes in ascending order
+      // (dynamic LDS after the histogram and the carries). An absent class adds
+      // T(0) = 0 (or 0 squared) to every left / right sum, so scanning the present
+      // ones only leaves each sum bit-identical -- deep nodes hold few classes.
+      int ncls = C;
+      if constexpr (!kC2) {
+        if (cls_lds) {
+          if (wave == 0) {
+            const unsigned long long lt = (1ull << lane) - 1ull;
+            int off = 0;
+            for (int c0 = 0; c0 < C; c0 += kWave) {
+              const int c = c0 + lane;
+              const bool pr = c < C && s_cnt[c] > 0;
+              const unsigned long long mk = __ballot(pr);
+              if (pr) cls_lds[off + __popcll(mk & lt)] = c;
+              off += __popcll(mk);
+            }
+            if (lane == 0) cls_lds[C] = off;
+          }
+          __syncthreads();
+          ncls = cls_lds[C];
+        }
+      }
       const int64_t start = s_start;
       const int m = s_count;
       const int depth = s_depth;
@@ -623,40 +653,50 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         uint32_t mL[4] = {0, 0, 0, 0}, ne[4] = {0, 0, 0, 0};
         double sL[4] = {0.0, 0.0, 0.0, 0.0}, sR[4] = {0.0, 0.0, 0.0, 0.0};
         int64_t qL[4] = {0, 0, 0, 0}, qR[4] = {0, 0, 0, 0};
-        for (int w = 0; w < W; ++w) {
-          uint32_t vlo[4], vhi[4];
+        // classes in groups of kFinCG: a group's bin loads and DPP prefix sums are
+        // independent chains issued together; the sums still add class by class in
+        // ascending order (bit-identical to the sequential host sums)
+        for (int j0 = 0; j0 < ncls; j0 += kFinCG) {
+          uint32_t vv[kFinCG][4], p[kFinCG][4], incl[kFinCG];
+          int cc[kFinCG];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int b = b0 + k;
-            const uint32_t v = b < nb ? h[b * W + w] : 0u;
-            vlo[k] = v & 0xffffu;
-            vhi[k] = v >> 16;
+          for (int g = 0; g < kFinCG; ++g) {
+            const int j = j0 + g;
+            const int c = j < ncls ? (cls_lds ? cls_lds[j] : j) : -1;
+            cc[g] = c;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const int b = b0 + k;
+              const uint32_t v = (c >= 0 && b < nb) ? h[b * W + (c >> 1)] : 0u;
+              vv[g][k] = (c & 1) ? (v >> 16) : (v & 0xffffu);
+            }
           }
 #pragma unroll
-          for (int half = 0; half < 2; ++half) {
-            const int c = 2 * w + half;
-            if (c >= C) break;
-            const uint32_t* vv = half ? vhi : vlo;
-            uint32_t p[4];
-            p[0] = vv[0];
-            p[1] = p[0] + vv[1];
-            p[2] = p[1] + vv[2];
-            p[3] = p[2] + vv[3];
-            const uint32_t incl = wave_incl_scan_dpp(p[3]);
-            uint32_t excl = incl - p[3];
+          for (int g = 0; g < kFinCG; ++g) {
+            p[g][0] = vv[g][0];
+            p[g][1] = p[g][0] + vv[g][1];
+            p[g][2] = p[g][1] + vv[g][2];
+            p[g][3] = p[g][2] + vv[g][3];
+            incl[g] = wave_incl_scan_dpp(p[g][3]);
+          }
+#pragma unroll
+          for (int g = 0; g < kFinCG; ++g) {
+            const int c = cc[g];
+            if (c < 0) break;  // (wave-uniform: the group's tail)
+            uint32_t excl = incl[g] - p[g][3];
             if (multi) {  // + the class's rows in the earlier passes
               const uint32_t cin = (uint32_t)carry[c];
               excl += cin;
-              const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+              const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl[g], kWave - 1);
               if (lane == 0) carry[c] = (int32_t)(cin + tot);
             }
             const uint32_t tc = (uint32_t)s_cnt[c];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-              const uint32_t L = excl + p[k];
+              const uint32_t L = excl + p[g][k];
               const uint32_t R = tc - L;
               mL[k] += L;
-              ne[k] |= vv[k];
+              ne[k] |= vv[g][k];
               if (crit == kEntropy) {
                 sL[k] = sL[k] + tl(L);
                 sR[k] = sR[k] + tl(R);
@@ -1688,9 +1728,10 @@ int finish_feature_tile(int F, int B, int C) {
   return std::min(ft, F);
 }
 int finish_lds_bytes(int F, int B, int C) {
-  // + per-wave class carries of the multi-pass (B > 256) scan
+  // + per-wave class carries of the multi-pass (B > 256) scan, + the node's
+  // present-class list (C > 2)
   return finish_feature_tile(F, B, C) * fin_fstride(B, (C + 1) / 2) * 4 +
-         (B > 256 ? (kFinThreadsWide / kWave) * C * 4 : 0);
+         (B > 256 ? (kFinThreadsWide / kWave) * C * 4 : 0) + (C > 2 ? (C + 1) * 4 : 0);
 }
 int finish_max_classes() { return kFinMaxC; }
 
@@ -1740,8 +1781,8 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   const size_t lds = (size_t)finish_lds_bytes(F, B, C);
   int32_t* gstk = nullptr;
 #define MT_FIN_NT(CT, C2, NT)                                                                 \
-  MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_cls_kernel<CT, C2, NT>,                \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));    \
+  MT_HIP_CHECK(mt_set_max_lds((const void*)finish_cls_kernel<CT, C2, NT>,                \
+                                   (int)lds));    \
   hipLaunchKernelGGL((finish_cls_kernel<CT, C2, NT>), dim3(grid), dim3(NT), lds, stream,      \
                      (const uint32_t*)codes_rm, row_words, (const CT*)codes_fm, n_rows, buf0, \
                      buf1, y, rl, jobs, J, counter, nbins, F, B, C, crit, max_depth, mss,     \
@@ -1759,7 +1800,7 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                                              : (const void*)finish_cls_kernel<uint8_t, false, kFinThreadsSmall>)
                                        : (c2 ? (const void*)finish_cls_kernel<uint16_t, true, kFinThreadsSmall>
                                              : (const void*)finish_cls_kernel<uint16_t, false, kFinThreadsSmall>);
-    MT_HIP_CHECK(hipFuncSetAttribute(k512, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    MT_HIP_CHECK(mt_set_max_lds(k512, (int)lds));
     MT_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k512, kFinThreadsSmall, lds));
     wide = per_cu == 1;
   }
@@ -1806,8 +1847,8 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
       const int g = std::max(1, tiny_grid * kTinyWaves / w);
       const size_t lds = (size_t)w * tiny_wave_bytes(F, cb);
 #define MT_TS(W, CT)                                                                         \
-  MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_tiny_sorted_kernel<W, CT>,            \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));   \
+  MT_HIP_CHECK(mt_set_max_lds((const void*)finish_tiny_sorted_kernel<W, CT>,            \
+                                   (int)lds));   \
   hipLaunchKernelGGL((finish_tiny_sorted_kernel<W, CT>), dim3(g), dim3(W * kWave), lds,      \
                      stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,  \
                      counter + kFinCtrTinyCount, counter + kFinCtrTinyCount + 1, F, C, crit, \

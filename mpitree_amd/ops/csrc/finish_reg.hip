@@ -831,7 +831,7 @@ int finish_reg_blocks_per_cu(int B, int code_bytes) {
   const void* k = code_bytes == 1 ? (const void*)finish_reg_kernel<uint8_t>
                                   : (const void*)finish_reg_kernel<uint16_t>;
   const int lds = finish_reg_lds_bytes(B);
-  MT_HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  MT_HIP_CHECK(mt_set_max_lds(k, lds));
   int per_cu = 0;
   MT_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, kRegThreads, lds));
   return per_cu < 1 ? 1 : per_cu;
@@ -851,8 +851,8 @@ void launch_finish_reg(hipStream_t stream, const void* codes_rm, int64_t row_wor
   tiny_rows = std::min(tiny_rows, kRegTinyRows);
   const size_t lds = (size_t)finish_reg_lds_bytes(B);
 #define MT_FR(CT)                                                                           \
-  MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_reg_kernel<CT>,                      \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));  \
+  MT_HIP_CHECK(mt_set_max_lds((const void*)finish_reg_kernel<CT>,                      \
+                                   (int)lds));  \
   hipLaunchKernelGGL(finish_reg_kernel<CT>, dim3(grid), dim3(kRegThreads), lds, stream,     \
                      (const uint32_t*)codes_rm, row_words, (const CT*)codes_fm, n_rows, buf0, \
                      buf1, y, jobs, J, counter, nbins, F, B, max_depth, mss, msl, node_i32,  \
@@ -866,8 +866,7 @@ void launch_finish_reg(hipStream_t stream, const void* codes_rm, int64_t row_wor
   MT_HIP_CHECK(hipGetLastError());
   if (tiny_rows > 0) {
     const size_t tl = (size_t)kRegTinyWaves * reg_tiny_wave_bytes(F);
-    MT_HIP_CHECK(hipFuncSetAttribute((const void*)finish_tiny_reg_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl));
+    MT_HIP_CHECK(mt_set_max_lds((const void*)finish_tiny_reg_kernel, (int)tl));
     hipLaunchKernelGGL(finish_tiny_reg_kernel, dim3(tiny_grid), dim3(kRegTinyWaves * kWave), tl,
                        stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, tiny,
                        counter + 1, counter + 2, F, max_depth, mss, msl, node_i32, node_st);

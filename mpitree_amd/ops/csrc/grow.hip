@@ -863,8 +863,7 @@ void launch_job_sort(hipStream_t stream, const int64_t* jobs, int J, int W, int6
   int N2 = 1;
   while (N2 < J) N2 <<= 1;
   const int lds = N2 * (int)sizeof(uint64_t);
-  MT_HIP_CHECK(hipFuncSetAttribute((const void*)job_sort_kernel,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, kSortMax * 8));
+  MT_HIP_CHECK(mt_set_max_lds((const void*)job_sort_kernel, kSortMax * 8));
   hipLaunchKernelGGL(job_sort_kernel, dim3(1), dim3(1024), lds, stream, jobs, J, W, out, counters);
   MT_HIP_CHECK(hipGetLastError());
 }

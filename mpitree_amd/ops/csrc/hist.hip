@@ -461,8 +461,8 @@ void launch_hist(hipStream_t stream, const void* codes, int code_bytes, int64_t 
     int shift = std::min(ceil_pow2_shift(words), 9);
     size_t lds = (size_t)ft * (B * 8 + (B + 1) * 4);
 #define MT_REG(CT)                                                                            \
-  MT_HIP_CHECK(hipFuncSetAttribute((const void*)hist_reg_lds_kernel<CT>,                      \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));    \
+  MT_HIP_CHECK(mt_set_max_lds((const void*)hist_reg_lds_kernel<CT>,                      \
+                                   (int)lds));    \
   hipLaunchKernelGGL(hist_reg_lds_kernel<CT>, grid, dim3(kHistThreads), lds, stream,          \
                      (const CT*)codes, row_words, idx, (const int64_t*)y, items,              \
                      (int64_t*)hist, (int64_t*)slab, F_h, f_lo, B, ft, shift, dcount);
@@ -488,8 +488,8 @@ void launch_hist(hipStream_t stream, const void* codes, int code_bytes, int64_t 
   const int shift = std::min(ceil_pow2_shift(lanes), 6);
   size_t lds = (size_t)ft * (B * ((C + 1) / 2) + 1) * 4;
 #define MT_CLS(CT, V)                                                                         \
-  MT_HIP_CHECK(hipFuncSetAttribute((const void*)hist_cls_lds_kernel<CT, V>,                   \
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));    \
+  MT_HIP_CHECK(mt_set_max_lds((const void*)hist_cls_lds_kernel<CT, V>,                   \
+                                   (int)lds));    \
   hipLaunchKernelGGL((hist_cls_lds_kernel<CT, V>), grid, dim3(kHistThreads), lds, stream,     \
                      (const uint32_t*)codes, row_words, idx, (const int32_t*)y, rl, items,    \
                      (uint32_t*)hist, (uint32_t*)slab, F_h, f_lo, B, C, ft, shift, dcount,   \

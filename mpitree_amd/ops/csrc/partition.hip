@@ -258,8 +258,7 @@ void launch_seg_stats(hipStream_t stream, const uint32_t* idx, const void* y, in
                        (const int64_t*)y, items, (int64_t*)out);
   } else {
     size_t lds = (size_t)C * 4;
-    MT_HIP_CHECK(hipFuncSetAttribute((const void*)seg_stats_cls_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    MT_HIP_CHECK(mt_set_max_lds((const void*)seg_stats_cls_kernel, (int)lds));
     hipLaunchKernelGGL(seg_stats_cls_kernel, dim3(n_items), dim3(256), lds, stream, idx,
                        (const int32_t*)y, lab_shift, items, (uint32_t*)out, C);
   }

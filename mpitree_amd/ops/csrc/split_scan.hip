@@ -16,6 +16,7 @@ namespace mt {
 
 constexpr int kBinsPerLane = 4;
 constexpr int kChunk = kWave * kBinsPerLane;  // 256 bins per wave pass
+constexpr int kScanCG = 4;                     // classes whose scans overlap (C > 2)
 
 // T(x) = x*log2(x) from a device table built by the same function (so the
 // values are identical) for small counts, evaluated otherwise. The scan is
@@ -80,17 +81,27 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
   }
   auto hv = [&](int64_t i) -> uint32_t { return gp ? gp[i] - gs[i] : h[i]; };
 
-  // pass 1: per-class totals
+  // pass 1: per-class totals, kScanCG classes at a time (independent reductions)
   uint32_t m = 0;
-  for (int c = 0; c < C; ++c) {
-    uint32_t s = 0;
-    for (int b = lane; b < nb; b += kWave) s += hv((int64_t)b * C + c);
-    s = wave_sum_u32(s);
-    if (lane == 0) {
-      tot[c] = s;
-      carry[c] = 0;
+  for (int c0 = 0; c0 < C; c0 += kScanCG) {
+    uint32_t s[kScanCG];
+#pragma unroll
+    for (int g = 0; g < kScanCG; ++g) s[g] = 0;
+    for (int b = lane; b < nb; b += kWave) {
+#pragma unroll
+      for (int g = 0; g < kScanCG; ++g)
+        if (c0 + g < C) s[g] += hv((int64_t)b * C + c0 + g);
     }
-    m += s;
+#pragma unroll
+    for (int g = 0; g < kScanCG; ++g) {
+      if (c0 + g >= C) break;
+      const uint32_t t = wave_sum_u32(s[g]);
+      if (lane == 0) {
+        tot[c0 + g] = t;
+        carry[c0 + g] = 0;
+      }
+      m += t;
+    }
   }
   // tot/carry are private to this wave: order lane 0's LDS writes before the
   // other lanes' reads without a workgroup barrier (waves may have exited).
@@ -116,36 +127,53 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
       qL[k] = 0;
       qR[k] = 0;
     }
-    for (int c = 0; c < C; ++c) {
-      uint32_t v[kBinsPerLane];
+    // classes in groups of kScanCG: a group's loads and DPP prefix sums are
+    // independent chains issued together; classes absent from the node (total 0)
+    // add exact zeros and are skipped; the sums still add class by class in
+    // ascending order (bit-identical to the sequential host sums)
+    for (int c0 = 0; c0 < C; c0 += kScanCG) {
+      uint32_t v[kScanCG][kBinsPerLane], p[kScanCG][kBinsPerLane], incl[kScanCG];
+      bool live[kScanCG];
 #pragma unroll
-      for (int k = 0; k < kBinsPerLane; ++k) {
-        const int b = b0 + k;
-        v[k] = (b < nb) ? hv((int64_t)b * C + c) : 0u;
-      }
-      uint32_t p[kBinsPerLane];
-      p[0] = v[0];
+      for (int g = 0; g < kScanCG; ++g) {
+        const int c = c0 + g;
+        live[g] = c < C && tot[c] != 0u;  // (wave-uniform)
 #pragma unroll
-      for (int k = 1; k < kBinsPerLane; ++k) p[k] = p[k - 1] + v[k];
-      const uint32_t incl = wave_incl_scan_dpp(p[kBinsPerLane - 1]);
-      const uint32_t excl = incl - p[kBinsPerLane - 1] + carry[c];
-      const uint32_t tc = tot[c];
-#pragma unroll
-      for (int k = 0; k < kBinsPerLane; ++k) {
-        const uint32_t L = excl + p[k];
-        const uint32_t R = tc - L;
-        mL[k] += L;
-        nonempty[k] |= v[k];
-        if (crit == kEntropy) {
-          sL[k] = sL[k] + tlog(L, xtab, xtab_n);
-          sR[k] = sR[k] + tlog(R, xtab, xtab_n);
-        } else {
-          qL[k] += (int64_t)L * L;
-          qR[k] += (int64_t)R * R;
+        for (int k = 0; k < kBinsPerLane; ++k) {
+          const int b = b0 + k;
+          v[g][k] = (live[g] && b < nb) ? hv((int64_t)b * C + c) : 0u;
         }
       }
-      const uint32_t chunk_total = __shfl(incl, kWave - 1, kWave);
-      if (lane == 0) carry[c] += chunk_total;
+#pragma unroll
+      for (int g = 0; g < kScanCG; ++g) {
+        p[g][0] = v[g][0];
+#pragma unroll
+        for (int k = 1; k < kBinsPerLane; ++k) p[g][k] = p[g][k - 1] + v[g][k];
+        incl[g] = live[g] ? wave_incl_scan_dpp(p[g][kBinsPerLane - 1]) : 0u;
+      }
+#pragma unroll
+      for (int g = 0; g < kScanCG; ++g) {
+        if (!live[g]) continue;
+        const int c = c0 + g;
+        const uint32_t excl = incl[g] - p[g][kBinsPerLane - 1] + carry[c];
+        const uint32_t tc = tot[c];
+#pragma unroll
+        for (int k = 0; k < kBinsPerLane; ++k) {
+          const uint32_t L = excl + p[g][k];
+          const uint32_t R = tc - L;
+          mL[k] += L;
+          nonempty[k] |= v[g][k];
+          if (crit == kEntropy) {
+            sL[k] = sL[k] + tlog(L, xtab, xtab_n);
+            sR[k] = sR[k] + tlog(R, xtab, xtab_n);
+          } else {
+            qL[k] += (int64_t)L * L;
+            qR[k] += (int64_t)R * R;
+          }
+        }
+        const uint32_t chunk_total = __shfl(incl[g], kWave - 1, kWave);
+        if (lane == 0) carry[c] += chunk_total;
+      }
     }
 #pragma unroll
     for (int k = 0; k < kBinsPerLane; ++k) {
@@ -425,16 +453,14 @@ void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int
     const int der_lds = der != nullptr && (int64_t)B * C <= 4096;
     size_t lds = (size_t)4 * 2 * C * sizeof(uint32_t) +
                  (der_lds ? (size_t)4 * B * C * sizeof(uint32_t) : 0);
-    MT_HIP_CHECK(hipFuncSetAttribute((const void*)scan_cls_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    MT_HIP_CHECK(mt_set_max_lds((const void*)scan_cls_kernel, (int)lds));
     hipLaunchKernelGGL(scan_cls_kernel, grid, dim3(256), lds, stream, (uint32_t*)hist,
                        nodes, nbins, F_h, f_lo, B, C, crit, msl, cost, bins, xtab, xtab_n,
                        dcount, der, (const uint32_t*)prev, nbuilt, der_lds);
   }
   MT_HIP_CHECK(hipGetLastError());
   const size_t sel_lds = crit == kSquaredError ? 16 : (size_t)2 * C * sizeof(int64_t);
-  MT_HIP_CHECK(hipFuncSetAttribute((const void*)select_kernel,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sel_lds));
+  MT_HIP_CHECK(mt_set_max_lds((const void*)select_kernel, (int)sel_lds));
   hipLaunchKernelGGL(select_kernel, dim3(k), dim3(256), sel_lds, stream, hist, nodes, cost, bins,
                      F_h, f_lo, B, C, crit, rec, dcount);
   MT_HIP_CHECK(hipGetLastError());

@@ -564,6 +564,26 @@ class DeviceGrower:
                                 node_owner=ws["own_node"].data_ptr(),
                                 job_owner=ws["own_job"].data_ptr())
 
+            # single-rank and subtree-ownership levels (no collective between the
+            # kernels, no per-phase profile events): one C++ call enqueues a level
+            ctx = None
+            if not (dp or fp or prof) and os.environ.get("MPITREE_LEVEL_CTX", "1") != "0":
+                ctx = hip.GrowCtx(dict(
+                    hist0=hists[0].data_ptr(), hist1=hists[1].data_ptr(), idx=bufs[0],
+                    tmp=bufs[1], codes_rm=be.codes_rm.data_ptr(),
+                    codes_fm=be.codes_fm.data_ptr(), y=be.y.data_ptr(), slab=slab.data_ptr(),
+                    rec=rec.data_ptr(), cost=cost.data_ptr(), bins=bins.data_ptr(),
+                    ident=ident.data_ptr(), split=split.data_ptr(), pitems=pitems.data_ptr(),
+                    cursors=cursors.data_ptr(), jobs=jobs.data_ptr(),
+                    job_count=job_count.data_ptr(), pos_rec=be.pos_rec.data_ptr(),
+                    pos_st=be.pos_st.data_ptr(), nbins=be.nbins.data_ptr(),
+                    xtab=be.xtab.data_ptr(), xtab_n=hb.XTAB_N, host_ctl=hctl_dev, cb=cb,
+                    row_bytes=rs, lab_shift=be.lab_shift, row_mask=be.row_mask, n_codes=be.n,
+                    n_loc=n_loc, F_h=F_h, f_lo=f_lo, B=B, C=C, reg=int(reg), crit=int(be.crit),
+                    E=E, max_depth=md, mss=mss, msl=msl, fr=fr, n_cu=hb.N_CU,
+                    lds_budget=hb.LDS_BUDGET, KMAX=KMAX, IMAX=IMAX, TMAX=TMAX, RMAX=RMAX,
+                    PMAX=PMAX, MMAX=MMAX, tag0=tag0), ptrs[0], ptrs[1], own_args)
+
             def plan(cur, nxt, lvl, fixup=False):
                 hip.grow_plan(s(), cur, nxt, rec.data_ptr(), split.data_ptr(), pitems.data_ptr(),
                               cursors.data_ptr(), cur["ctl"] + 4 * 5, be.pos_rec.data_ptr(),
@@ -578,6 +598,19 @@ class DeviceGrower:
                     check_abort()
                     fault_point(comm, f"level:{lvl}")
                 b0 = getattr(comm, "bytes_communicated", 0)
+                if ctx is not None:
+                    ctx.level(s(), lvl)
+                    if ck is not None and (lvl - first_lvl + 1) % ck_every == 0:
+                        self._ckpt_save(lvl, ws, sets, hists, rank, P)
+                    lvl += 1
+                    if lvl - 2 >= first_lvl:
+                        _wait_slot(hctl, (lvl - 2) % 64, tag0 + ((lvl - 2) % 4096) + 1)
+                        if int(hctl[(lvl - 2) % 64, 0]) == 0:
+                            done_at = lvl - 2
+                            break
+                    if lvl > 4096:
+                        raise RuntimeError("device level loop did not terminate")
+                    continue
                 if prof:
                     marks.append([])
                     mark()

@@ -218,6 +218,8 @@ class ExactGrower:
             return be.assemble_positions(None, int(crit), y_exp, thr_pos=pos_thr)
 
         fr = int(hip.xe_local_max())
+        if reg and F > 256:
+            fr = 0  # (the regression finisher keeps <= 256 features): levels to the leaves
         if not reg and (C > 256 or int(hip.finish_feature_tile(F, 256, C)) <= 0):
             fr = 0  # (the local-code finishers take <= 256 classes): levels to the leaves
         env = os.environ.get("MPITREE_EXACT_FINISHER_ROWS")  # (tests: 0 = no finisher)
