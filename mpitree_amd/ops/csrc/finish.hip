@@ -137,12 +137,13 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
   if (threadIdx.x == 0) s_cand_total = 0;
 
   const int tid = threadIdx.x;
-  const bool tiled = Ft < F;
-  // C > 2 (generic path): the node's present class ids + their count at [C]
+  // C > 2 (generic path): the node's present class ids + their count at [C],
+  // then the class -> compacted slot map [C]
   int32_t* const cls_lds =
       (!kC2 && C > 2) ? reinterpret_cast<int32_t*>(hist + Ft * fstride_of(B, C)) +
                             (B > 256 ? (kFinThreadsWide / kWave) * C : 0)
                       : nullptr;
+  int32_t* const cmap = cls_lds ? cls_lds + C + 1 : nullptr;
   int32_t* const stc = gstk ? gstk + (int64_t)blockIdx.x * (kFinStack + 2) * C : s_st_cnt;
   const int stw = gstk ? C : kFinStackC;  // stack row stride
   int32_t* const s_cnt = gstk ? stc + kFinStack * C : s_cnt_l;
@@ -437,6 +438,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
               const bool pr = c < C && s_cnt[c] > 0;
               const unsigned long long mk = __ballot(pr);
               if (pr) cls_lds[off + __popcll(mk & lt)] = c;
+              if (c < C) cmap[c] = pr ? off + __popcll(mk & lt) : 0;
               off += __popcll(mk);
             }
             if (lane == 0) cls_lds[C] = off;
@@ -445,6 +447,18 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           ncls = cls_lds[C];
         }
       }
+      // the node's histogram layout: its present classes only (two per word), so
+      // a node holding few of many classes packs more features per LDS tile --
+      // fewer tiles re-reading its rows, more waves scanning
+      int Wn = W, fstr = fstride, Ftn = Ft;
+      if (cls_lds) {
+        Wn = (ncls + 1) >> 1;
+        fstr = fin_fstride(B, Wn);
+        Ftn = min(min(F, kFinMaxF), (Ft * fstride) / fstr);
+        if (Ftn >= 16 && Ftn < F) Ftn &= ~15;  // (16-B row loads at every tile start)
+      }
+      const bool tiled_n = Ftn < F;
+      const int hq = Ftn * fstr / 4;  // uint4 words this node's tiles use
       const int64_t start = s_start;
       const int m = s_count;
       const int depth = s_depth;
@@ -460,11 +474,11 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
       double bg = -__builtin_inf();
       int bfeat = 0x7fffffff, bbin = -1;
       int nc_report = 0x40000000;  // no exact-pass skip unless pass 1 proves one
-      for (int ft0 = 0; ft0 < F; ft0 += Ft) {
-      const int ft1 = min(F, ft0 + Ft);
+      for (int ft0 = 0; ft0 < F; ft0 += Ftn) {
+      const int ft1 = min(F, ft0 + Ftn);
       if (ft0 > 0) {  // next feature tile: clear the previous tile's counts
         __syncthreads();
-        for (int e = tid; e < hist_q; e += kFinThreads) hist4[e] = make_uint4(0, 0, 0, 0);
+        for (int e = tid; e < hq; e += kFinThreads) hist4[e] = make_uint4(0, 0, 0, 0);
         __syncthreads();
       }
       // ---- histogram of this node's rows (features [ft0, ft1)): VEC words per
@@ -511,8 +525,9 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
           for (int u = 0; u < kFinUnroll; ++u) {
             if (ent[u] == 0xffffffffu) continue;
-            const uint32_t inc = 1u << ((lab[u] & 1) * 16);
-            const int off = lab[u] >> 1;
+            const int sl = cmap ? cmap[lab[u]] : lab[u];  // (compacted class slot)
+            const uint32_t inc = 1u << ((sl & 1) * 16);
+            const int off = sl >> 1;
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
               if (v >= vec) break;
@@ -522,7 +537,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
                 if (f >= ft0 && f < ft1) {
                   const uint32_t code = (wv[u][v] >> (j * 8 * sizeof(CodeT))) &
                                         ((sizeof(CodeT) == 1) ? 0xffu : 0xffffu);
-                  atomicAdd(&hist[(f - ft0) * fstride + (int)code * W + off], inc);
+                  atomicAdd(&hist[(f - ft0) * fstr + (int)code * Wn + off], inc);
                 }
               }
             }
@@ -637,7 +652,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
       } else
       for (int f = ft0 + wave; f < ft1; f += kFinWaves) {
         const int nb = nbf(f);
-        const uint32_t* h = hist + (f - ft0) * fstride;
+        const uint32_t* h = hist + (f - ft0) * fstr;
         double best_cost = __builtin_inf();
         int best_bin = 0x7fffffff;
         const double tu = tie_unit(tl((uint64_t)m), (int64_t)m);
@@ -661,14 +676,14 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           int cc[kFinCG];
 #pragma unroll
           for (int g = 0; g < kFinCG; ++g) {
-            const int j = j0 + g;
+            const int j = j0 + g;  // compacted slot j holds class cls_lds[j]
             const int c = j < ncls ? (cls_lds ? cls_lds[j] : j) : -1;
             cc[g] = c;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
               const int b = b0 + k;
-              const uint32_t v = (c >= 0 && b < nb) ? h[b * W + (c >> 1)] : 0u;
-              vv[g][k] = (c & 1) ? (v >> 16) : (v & 0xffffu);
+              const uint32_t v = (c >= 0 && b < nb) ? h[b * Wn + (j >> 1)] : 0u;
+              vv[g][k] = (j & 1) ? (v >> 16) : (v & 0xffffu);
             }
           }
 #pragma unroll
@@ -790,13 +805,15 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         if (!(g > -__builtin_inf())) bf = -1;
       }
       if (bf >= 0) {
-        // ---- left class counts of the winning split (tiled: counted below)
-        for (int c = wave; c < C && !tiled; c += kFinWaves) {
+        // ---- left class counts of the winning split (tiled: counted below);
+        // compacted slot j holds class cls_lds[j] (absent classes stay 0)
+        for (int j = wave; j < ncls && !tiled_n; j += kFinWaves) {
+          const int c = cls_lds ? cls_lds[j] : j;
           uint32_t s = 0;
-          const uint32_t* h = hist + bf * fstride;
+          const uint32_t* h = hist + bf * fstr;
           for (int b = lane; b <= bb; b += kWave) {
-            const uint32_t v = h[b * W + (c >> 1)];
-            s += (c & 1) ? (v >> 16) : (v & 0xffffu);
+            const uint32_t v = h[b * Wn + (j >> 1)];
+            s += (j & 1) ? (v >> 16) : (v & 0xffffu);
           }
           s = wave_sum_u32(s);
           if (lane == 0) s_left[c] = (int32_t)s;
@@ -833,7 +850,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
             basel = __builtin_amdgcn_readfirstlane(basel);
             baser = __builtin_amdgcn_readfirstlane(baser);
             if (valid) {
-              if (tiled && go) {
+              if (tiled_n && go) {
                 const uint32_t e = ent[u];
                 atomicAdd(&s_left[rl.shift ? (int)(e >> rl.shift) : y[e & rl.mask]], 1);
               }
@@ -848,7 +865,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
       __syncthreads();
       mark(2);
       // ---- clear the histogram for the next node (all scan reads are done)
-      for (int e = tid; e < hist_q; e += kFinThreads) hist4[e] = make_uint4(0, 0, 0, 0);
+      for (int e = tid; e < hq; e += kFinThreads) hist4[e] = make_uint4(0, 0, 0, 0);
       // ---- children
       if (tid == 0 && bf >= 0) {
         const int nl = s_lc;
@@ -1731,7 +1748,7 @@ int finish_lds_bytes(int F, int B, int C) {
   // + per-wave class carries of the multi-pass (B > 256) scan, + the node's
   // present-class list (C > 2)
   return finish_feature_tile(F, B, C) * fin_fstride(B, (C + 1) / 2) * 4 +
-         (B > 256 ? (kFinThreadsWide / kWave) * C * 4 : 0) + (C > 2 ? (C + 1) * 4 : 0);
+         (B > 256 ? (kFinThreadsWide / kWave) * C * 4 : 0) + (C > 2 ? (2 * C + 1) * 4 : 0);
 }
 int finish_max_classes() { return kFinMaxC; }
 

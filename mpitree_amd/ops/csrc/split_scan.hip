@@ -17,6 +17,7 @@ namespace mt {
 constexpr int kBinsPerLane = 4;
 constexpr int kChunk = kWave * kBinsPerLane;  // 256 bins per wave pass
 constexpr int kScanCG = 4;                     // classes whose scans overlap (C > 2)
+constexpr int kScanTab = 1024;                 // C > 2: x*log2(x) entries staged in LDS
 
 // T(x) = x*log2(x) from a device table built by the same function (so the
 // values are identical) for small counts, evaluated otherwise. The scan is
@@ -42,10 +43,24 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
   // der_lds: the derived histogram (B*C words per wave) fits in LDS; else the
   // scan reads parent - sibling from global memory on the fly (many classes)
   if (dcount && (int)blockIdx.x >= *dcount) return;  // device-side node count
-  extern __shared__ uint32_t sm[];  // per wave: C class totals + C carries [+ B*C derived]
+  // per wave: C class totals + C carries [+ B*C derived]; C > 2: then the first
+  // kScanTab x*log2(x) values (many classes: deep nodes' counts are small, and
+  // 2 C table reads per bin from global memory dominated the scan)
+  extern __shared__ __align__(16) uint32_t sm[];
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
   const int f = blockIdx.y * 4 + wave;
+  int tn = 0;
+  double* stab = nullptr;
+  if (C > 2) {
+    tn = min(kScanTab, xtab_n);
+    stab = reinterpret_cast<double*>(sm + ((4 * 2 * C + (der_lds ? 4 * B * C : 0) + 3) & ~3));
+    for (int i = threadIdx.x; i < tn; i += blockDim.x) stab[i] = xtab[i];
+    __syncthreads();
+  }
+  auto tl = [&](uint64_t x) -> double {
+    return x < (uint64_t)tn ? stab[x] : tlog(x, xtab, xtab_n);
+  };
   if (f >= F_h) return;
   const int64_t node = blockIdx.x;
   const int64_t slot = nodes[node];
@@ -164,8 +179,8 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
           mL[k] += L;
           nonempty[k] |= v[g][k];
           if (crit == kEntropy) {
-            sL[k] = sL[k] + tlog(L, xtab, xtab_n);
-            sR[k] = sR[k] + tlog(R, xtab, xtab_n);
+            sL[k] = sL[k] + tl(L);
+            sR[k] = sR[k] + tl(R);
           } else {
             qL[k] += (int64_t)L * L;
             qR[k] += (int64_t)R * R;
@@ -183,8 +198,7 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
       if (b < nb && nonempty[k] && ml >= msl && mr >= msl) {
         double cost;
         if (crit == kEntropy)
-          cost = (tlog((uint64_t)ml, xtab, xtab_n) - sL[k]) +
-                 (tlog((uint64_t)mr, xtab, xtab_n) - sR[k]);
+          cost = (tl((uint64_t)ml) - sL[k]) + (tl((uint64_t)mr) - sR[k]);
         else
           cost = gini_term(ml, qL[k]) + gini_term(mr, qR[k]);
         cost = tie_round(cost, tinv, tu);
@@ -453,6 +467,7 @@ void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int
     const int der_lds = der != nullptr && (int64_t)B * C <= 4096;
     size_t lds = (size_t)4 * 2 * C * sizeof(uint32_t) +
                  (der_lds ? (size_t)4 * B * C * sizeof(uint32_t) : 0);
+    if (C > 2) lds = ((lds + 15) & ~(size_t)15) + (size_t)kScanTab * sizeof(double);
     MT_HIP_CHECK(mt_set_max_lds((const void*)scan_cls_kernel, (int)lds));
     hipLaunchKernelGGL(scan_cls_kernel, grid, dim3(256), lds, stream, (uint32_t*)hist,
                        nodes, nbins, F_h, f_lo, B, C, crit, msl, cost, bins, xtab, xtab_n,

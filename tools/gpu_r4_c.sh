@@ -16,3 +16,6 @@ for rep in 1 2; do
 done
 bash tools/gpu_timeline_bench.sh ctx "--steps 3 --warmup 1" c64 "--steps 2 --warmup 1 --classes 64"
 timeout -k 10 300 python -u bench/sim_own_ranks.py --regression --reps 3 > gpurun_out/sim_own_reg.log 2>&1
+timeout -k 10 300 python -u bench/sim_own_ranks.py --reps 3 > gpurun_out/sim_own_cls.log 2>&1
+timeout -k 10 400 python -u bench/sim_own_ranks.py --n 10000000 --features 128 --reps 2 > gpurun_out/sim_own_10m.log 2>&1
+bash tools/gpu_r4_d2h.sh
