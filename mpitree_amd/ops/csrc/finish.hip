@@ -671,11 +671,13 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         // classes in groups of kFinCG: a group's bin loads and DPP prefix sums are
         // independent chains issued together; the sums still add class by class in
         // ascending order (bit-identical to the sequential host sums)
-        for (int j0 = 0; j0 < ncls; j0 += kFinCG) {
-          uint32_t vv[kFinCG][4], p[kFinCG][4], incl[kFinCG];
-          int cc[kFinCG];
+        auto class_pass = [&](auto group_tag) {
+        constexpr int kG = decltype(group_tag)::value;
+        for (int j0 = 0; j0 < ncls; j0 += kG) {
+          uint32_t vv[kG][4], p[kG][4], incl[kG];
+          int cc[kG];
 #pragma unroll
-          for (int g = 0; g < kFinCG; ++g) {
+          for (int g = 0; g < kG; ++g) {
             const int j = j0 + g;  // compacted slot j holds class cls_lds[j]
             const int c = j < ncls ? (cls_lds ? cls_lds[j] : j) : -1;
             cc[g] = c;
@@ -687,7 +689,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
             }
           }
 #pragma unroll
-          for (int g = 0; g < kFinCG; ++g) {
+          for (int g = 0; g < kG; ++g) {
             p[g][0] = vv[g][0];
             p[g][1] = p[g][0] + vv[g][1];
             p[g][2] = p[g][1] + vv[g][2];
@@ -695,7 +697,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
             incl[g] = wave_incl_scan_dpp(p[g][3]);
           }
 #pragma unroll
-          for (int g = 0; g < kFinCG; ++g) {
+          for (int g = 0; g < kG; ++g) {
             const int c = cc[g];
             if (c < 0) break;  // (wave-uniform: the group's tail)
             uint32_t excl = incl[g] - p[g][3];
@@ -721,6 +723,53 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
               }
             }
           }
+        }
+        };
+        if (ncls <= 2) {  // two classes share one word: one load, both halves
+          uint32_t vlo[4], vhi[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int b = b0 + k;
+            const uint32_t v = b < nb ? h[b * Wn] : 0u;
+            vlo[k] = v & 0xffffu;
+            vhi[k] = v >> 16;
+          }
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            if (half >= ncls) break;
+            const int c = cls_lds ? cls_lds[half] : half;  // (slot half's class)
+            const uint32_t* vv = half ? vhi : vlo;
+            uint32_t p[4];
+            p[0] = vv[0];
+            p[1] = p[0] + vv[1];
+            p[2] = p[1] + vv[2];
+            p[3] = p[2] + vv[3];
+            const uint32_t incl = wave_incl_scan_dpp(p[3]);
+            uint32_t excl = incl - p[3];
+            if (multi) {  // + the class's rows in the earlier passes
+              const uint32_t cin = (uint32_t)carry[c];
+              excl += cin;
+              const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
+              if (lane == 0) carry[c] = (int32_t)(cin + tot);
+            }
+            const uint32_t tc = (uint32_t)s_cnt[c];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const uint32_t L = excl + p[k];
+              const uint32_t R = tc - L;
+              mL[k] += L;
+              ne[k] |= vv[k];
+              if (crit == kEntropy) {
+                sL[k] = sL[k] + tl(L);
+                sR[k] = sR[k] + tl(R);
+              } else {
+                qL[k] += (int64_t)L * L;
+                qR[k] += (int64_t)R * R;
+              }
+            }
+          }
+        } else {
+          class_pass(std::integral_constant<int, kFinCG>{});
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {

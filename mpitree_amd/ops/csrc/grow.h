@@ -63,6 +63,10 @@ struct OwnArgs {
   int64_t* ranges;   // [cap][2] this rank's position ranges [lo, hi); unused rows {0, 0}
   int32_t* node_owner;  // [KMAX] scratch: owner of frontier node i at the switch
   int32_t* job_owner;   // [JMAX] scratch: owner of job j at the switch
+  // > 0: at the switch level every owned child that would keep growing in the
+  // level loop becomes a finisher job instead (when it has at most this many
+  // rows): the rank's own work is its finisher jobs, no own levels
+  int jobs_at_switch = 0;
 };
 
 struct PlanArgs {

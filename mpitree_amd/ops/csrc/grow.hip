@@ -456,12 +456,32 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
   auto active = [&](int i) {
     return !own_sw || a.own.node_owner[i] < 0 || a.own.node_owner[i] == a.own.rank;
   };
+  // decisions of this level; at the switch (jobs_at_switch) the children that
+  // would keep growing become finisher jobs: the rank's own work is its jobs
+  auto decide = [&](int i) {
+    Decision d = plan_decide(a, i);
+    if (own_sw && a.own.jobs_at_switch > 0 && d.split) {
+      for (int c = 0; c < 2; ++c) {
+        const int64_t cm = c == 0 ? d.nl : d.nr;
+        if (d.fate[c] == 2 && cm <= a.own.jobs_at_switch) d.fate[c] = 1;
+      }
+      if (d.fate[0] == 2 && d.fate[1] == 2)
+        d.built = d.nl <= d.nr ? 0 : 1;
+      else if (d.fate[0] == 2)
+        d.built = 0;
+      else if (d.fate[1] == 2)
+        d.built = 1;
+      else
+        d.built = -1;
+    }
+    return d;
+  };
   // ---- pass 1: totals (built / derived next-frontier children, split nodes)
   int nb_tot = 0;
   for (int b0 = 0; b0 < K; b0 += kPlanThreads) {
     const int i = b0 + tid;
     int nb = 0;
-    if (i < K && active(i)) nb = plan_decide(a, i).built >= 0 ? 1 : 0;
+    if (i < K && active(i)) nb = decide(i).built >= 0 ? 1 : 0;
     int t;
     plan_scan_excl(nb, sh.w, t);
     nb_tot += t;
@@ -481,7 +501,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     d.split = false;
     d.built = -1;
     d.fate[0] = d.fate[1] = 0;
-    if (i < K) d = plan_decide(a, i);
+    if (i < K) d = decide(i);
     const bool act = i < K && active(i);
     const int nb = act && d.built >= 0 ? 1 : 0;
     const int nd = act && (d.fate[0] == 2 && d.fate[1] == 2) ? 1 : 0;

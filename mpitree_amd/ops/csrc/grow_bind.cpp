@@ -90,7 +90,7 @@ struct GrowCtx {
   int64_t KMAX = 0, IMAX = 0, TMAX = 0, RMAX = 0, PMAX = 0, MMAX = 0;
   int64_t mss = 2, msl = 1, fr = 0;
   int32_t tag0 = 0;
-  OwnArgs own{0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr};
+  OwnArgs own{0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, 0};
 
   void level(hipStream_t s, int lvl) {
     const int par = lvl & 1;
@@ -201,7 +201,8 @@ void bind_grow(py::module_& m) {
           auto o = [&](const char* k) { return own[k].cast<int64_t>(); };
           c.own = OwnArgs{(int)o("P"), (int)o("rank"), (int)o("min_units"), (int)o("cap"),
                           ptr<int32_t>(o("state")), ptr<int64_t>(o("ranges")),
-                          ptr<int32_t>(o("node_owner")), ptr<int32_t>(o("job_owner"))};
+                          ptr<int32_t>(o("node_owner")), ptr<int32_t>(o("job_owner")),
+                          own.contains("jobs_at_switch") ? (int)o("jobs_at_switch") : 0};
         }
         return c;
       }), py::arg("args"), py::arg("l0"), py::arg("l1"), py::arg("own") = py::dict())

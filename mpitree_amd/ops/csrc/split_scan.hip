@@ -9,6 +9,8 @@
 // is bit-identical to the host builders. A wave argmin over (cost, bin) picks
 // the first minimum; ``select_kernel`` then reduces (gain, feature) per node
 // with ties to the lowest feature and gathers the winning split's left counts.
+#include <type_traits>
+
 #include "common.h"
 #include "criterion.h"
 
@@ -17,7 +19,6 @@ namespace mt {
 constexpr int kBinsPerLane = 4;
 constexpr int kChunk = kWave * kBinsPerLane;  // 256 bins per wave pass
 constexpr int kScanCG = 4;                     // classes whose scans overlap (C > 2)
-constexpr int kScanTab = 1024;                 // C > 2: x*log2(x) entries staged in LDS
 
 // T(x) = x*log2(x) from a device table built by the same function (so the
 // values are identical) for small counts, evaluated otherwise. The scan is
@@ -43,24 +44,14 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
   // der_lds: the derived histogram (B*C words per wave) fits in LDS; else the
   // scan reads parent - sibling from global memory on the fly (many classes)
   if (dcount && (int)blockIdx.x >= *dcount) return;  // device-side node count
-  // per wave: C class totals + C carries [+ B*C derived]; C > 2: then the first
-  // kScanTab x*log2(x) values (many classes: deep nodes' counts are small, and
-  // 2 C table reads per bin from global memory dominated the scan)
-  extern __shared__ __align__(16) uint32_t sm[];
+  // per wave: C class totals + C carries [+ B*C derived]. (Staging the first 1024
+  // x*log2(x) values in LDS for many classes was measured slower: 1.77 -> 2.02 ms
+  // per level at C = 64, profiles/kernel_experiments.md.)
+  extern __shared__ uint32_t sm[];
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
   const int f = blockIdx.y * 4 + wave;
-  int tn = 0;
-  double* stab = nullptr;
-  if (C > 2) {
-    tn = min(kScanTab, xtab_n);
-    stab = reinterpret_cast<double*>(sm + ((4 * 2 * C + (der_lds ? 4 * B * C : 0) + 3) & ~3));
-    for (int i = threadIdx.x; i < tn; i += blockDim.x) stab[i] = xtab[i];
-    __syncthreads();
-  }
-  auto tl = [&](uint64_t x) -> double {
-    return x < (uint64_t)tn ? stab[x] : tlog(x, xtab, xtab_n);
-  };
+  auto tl = [&](uint64_t x) -> double { return tlog(x, xtab, xtab_n); };
   if (f >= F_h) return;
   const int64_t node = blockIdx.x;
   const int64_t slot = nodes[node];
@@ -146,11 +137,14 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
     // independent chains issued together; classes absent from the node (total 0)
     // add exact zeros and are skipped; the sums still add class by class in
     // ascending order (bit-identical to the sequential host sums)
-    for (int c0 = 0; c0 < C; c0 += kScanCG) {
-      uint32_t v[kScanCG][kBinsPerLane], p[kScanCG][kBinsPerLane], incl[kScanCG];
-      bool live[kScanCG];
+    // (two classes: one class per group, the register footprint of the scalar loop)
+    auto class_pass = [&](auto group_tag) {
+    constexpr int kG = decltype(group_tag)::value;
+    for (int c0 = 0; c0 < C; c0 += kG) {
+      uint32_t v[kG][kBinsPerLane], p[kG][kBinsPerLane], incl[kG];
+      bool live[kG];
 #pragma unroll
-      for (int g = 0; g < kScanCG; ++g) {
+      for (int g = 0; g < kG; ++g) {
         const int c = c0 + g;
         live[g] = c < C && tot[c] != 0u;  // (wave-uniform)
 #pragma unroll
@@ -160,14 +154,14 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
         }
       }
 #pragma unroll
-      for (int g = 0; g < kScanCG; ++g) {
+      for (int g = 0; g < kG; ++g) {
         p[g][0] = v[g][0];
 #pragma unroll
         for (int k = 1; k < kBinsPerLane; ++k) p[g][k] = p[g][k - 1] + v[g][k];
         incl[g] = live[g] ? wave_incl_scan_dpp(p[g][kBinsPerLane - 1]) : 0u;
       }
 #pragma unroll
-      for (int g = 0; g < kScanCG; ++g) {
+      for (int g = 0; g < kG; ++g) {
         if (!live[g]) continue;
         const int c = c0 + g;
         const uint32_t excl = incl[g] - p[g][kBinsPerLane - 1] + carry[c];
@@ -190,6 +184,11 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
         if (lane == 0) carry[c] += chunk_total;
       }
     }
+    };
+    if (C <= 2)
+      class_pass(std::integral_constant<int, 1>{});
+    else
+      class_pass(std::integral_constant<int, kScanCG>{});
 #pragma unroll
     for (int k = 0; k < kBinsPerLane; ++k) {
       const int b = b0 + k;
@@ -467,7 +466,6 @@ void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int
     const int der_lds = der != nullptr && (int64_t)B * C <= 4096;
     size_t lds = (size_t)4 * 2 * C * sizeof(uint32_t) +
                  (der_lds ? (size_t)4 * B * C * sizeof(uint32_t) : 0);
-    if (C > 2) lds = ((lds + 15) & ~(size_t)15) + (size_t)kScanTab * sizeof(double);
     MT_HIP_CHECK(mt_set_max_lds((const void*)scan_cls_kernel, (int)lds));
     hipLaunchKernelGGL(scan_cls_kernel, grid, dim3(256), lds, stream, (uint32_t*)hist,
                        nodes, nbins, F_h, f_lo, B, C, crit, msl, cost, bins, xtab, xtab_n,

@@ -78,10 +78,24 @@ OWN_CAP = 2048  # ownership units sorted at the switch level (grow.hip kOwnMax)
 def own_min_units(P: int) -> int:
     """Units (split nodes that keep growing + finisher jobs) the switch level
     needs before the ranks take ownership: more units balance the LPT better,
-    each replicated level before the switch costs every rank a full level."""
-    k = int(os.environ.get("MPITREE_OWN_UNITS_PER_RANK", "4"))
+    each replicated level before the switch costs every rank a full level.
+    2 per rank from P = 4 on (1M x 64 at P = 8: 2.24 vs 2.32 ms max rank;
+    P = 4: equal, ``profiles/r4/sim_own_variants.log``), 4 below."""
+    k = int(os.environ.get("MPITREE_OWN_UNITS_PER_RANK", "2" if P >= 4 else "4"))
     return max(2, k * P)
 POLL_TIMEOUT_S = float(os.environ.get("MPITREE_POLL_TIMEOUT", "120"))
+# histogram work items per CU and level (1 or 2): fewer, larger items write fewer
+# LDS slabs for the reduction to read back
+HIST_ITEMS_PER_CU = max(1, min(2, int(os.environ.get("MPITREE_HIST_ITEMS", "2"))))
+
+
+def own_jobs_at_switch(be) -> int:
+    """``MPITREE_OWN_JOBS=1``: at the ownership switch the owned children that would
+    keep growing become finisher jobs (up to the finisher's row limit), so a rank
+    runs no level after the switch (0: own levels until the jobs are small)."""
+    if os.environ.get("MPITREE_OWN_JOBS", "0") == "0":
+        return 0
+    return int(be.max_finisher_rows)
 
 
 def _wait_slot(hctl, slot: int, tag: int):
@@ -537,7 +551,8 @@ class DeviceGrower:
                 del state
             else:
                 # level 0: the root, built from rows (one init launch; root stats H2D)
-                chunk = int(min(hb.MAX_ITEM_ROWS, max(1024, -(-n_loc // (2 * hb.N_CU)))))
+                chunk = int(min(hb.MAX_ITEM_ROWS,
+                                max(1024, -(-n_loc // (HIST_ITEMS_PER_CU * hb.N_CU)))))
                 ws["root_host"].numpy()[: root_full.size] = root_full
                 ws["root"].copy_(ws["root_host"], non_blocking=True)
                 hip.grow_init(s(), ptrs[0], n_loc, n, chunk, C, int(reg), ws["root"].data_ptr(),
@@ -562,8 +577,10 @@ class DeviceGrower:
                                 state=ws["own_state"].data_ptr(),
                                 ranges=ws["own_ranges"].data_ptr(),
                                 node_owner=ws["own_node"].data_ptr(),
-                                job_owner=ws["own_job"].data_ptr())
+                                job_owner=ws["own_job"].data_ptr(),
+                                jobs_at_switch=own_jobs_at_switch(be))
 
+            plan_cu = hb.N_CU * HIST_ITEMS_PER_CU // 2  # (the planner makes 2 items per "CU")
             # single-rank and subtree-ownership levels (no collective between the
             # kernels, no per-phase profile events): one C++ call enqueues a level
             ctx = None
@@ -580,7 +597,7 @@ class DeviceGrower:
                     xtab=be.xtab.data_ptr(), xtab_n=hb.XTAB_N, host_ctl=hctl_dev, cb=cb,
                     row_bytes=rs, lab_shift=be.lab_shift, row_mask=be.row_mask, n_codes=be.n,
                     n_loc=n_loc, F_h=F_h, f_lo=f_lo, B=B, C=C, reg=int(reg), crit=int(be.crit),
-                    E=E, max_depth=md, mss=mss, msl=msl, fr=fr, n_cu=hb.N_CU,
+                    E=E, max_depth=md, mss=mss, msl=msl, fr=fr, n_cu=plan_cu,
                     lds_budget=hb.LDS_BUDGET, KMAX=KMAX, IMAX=IMAX, TMAX=TMAX, RMAX=RMAX,
                     PMAX=PMAX, MMAX=MMAX, tag0=tag0), ptrs[0], ptrs[1], own_args)
 
@@ -589,7 +606,7 @@ class DeviceGrower:
                               cursors.data_ptr(), cur["ctl"] + 4 * 5, be.pos_rec.data_ptr(),
                               0 if reg else be.pos_st.data_ptr(),
                               be.pos_st.data_ptr() if reg else 0, int(reg), (lvl + 1) % 2,
-                              jobs.data_ptr(), job_count.data_ptr(), C, md, hb.N_CU, mss, msl,
+                              jobs.data_ptr(), job_count.data_ptr(), C, md, plan_cu, mss, msl,
                               fr, 0 if fixup else hctl_dev + (lvl % 64) * 64,
                               tag0 + (lvl % 4096) + 1, dp=int(dp), fixup=fixup, own=own_args)
 
