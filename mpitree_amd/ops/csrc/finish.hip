@@ -58,11 +58,28 @@ constexpr int kFinTab = 1024;    // LDS x*log2(x) entries
 #ifndef MT_FIN_PAIR
 #define MT_FIN_PAIR 1
 #endif
+#ifndef MT_FIN_VMASK  // fp32 first pass: terms {T(ml), T(l0), T(l1), T(mr), T(r0), T(r1)}
+#define MT_FIN_VMASK 0  // computed on the VALU (bit set) instead of looked up in LDS
+#endif
 constexpr int kFinUnroll = MT_FIN_UNROLL;  // row gathers in flight per lane
 constexpr int kFinMaxF = 256;    // features with LDS-cached bin counts (two-class path: all)
 constexpr int kFinPair = MT_FIN_PAIR;  // features scanned together per wave (latency hiding)
 constexpr int kFinChunk = 8;     // features per wave whose per-lane minima stay in registers
 constexpr int kFinCG = 4;        // generic scan: classes whose loads / DPP scans overlap
+// fp32 first pass: which of the six x*log2(x) terms per bin come from v_log_f32
+// instead of the LDS table. The table lookups are random-address LDS reads (bank
+// conflicts, shared by the CU's two workgroups); splitting the terms between the
+// LDS and the VALU runs both pipes at once. Per-term error: see tfv.
+constexpr int kFinVMask = MT_FIN_VMASK;
+
+// x*log2(x) of an integer count in fp32 on the VALU (v_log_f32). Exhaustively
+// measured over 0 <= x < 2^24 (tools/probes/vlog_probe.hip, profiles/r4/vlog_probe.log):
+// relative error <= kTfvRelErr, T(0) = T(1) = 0 exactly -- inside the first pass's
+// error budget (scan_c2_f).
+__device__ __forceinline__ float tfv(uint32_t x) {
+  const float f = (float)x;
+  return f * __builtin_amdgcn_logf(fmaxf(f, 1.0f));
+}
 
 // Histogram row stride in words: >= B*W + 1 (the odd word staggers features over
 // LDS banks for the atomics), rounded to 4 so each feature row is 16-B aligned.
@@ -250,12 +267,9 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         // every bin looks its terms up, empty ones included: redirecting empty
         // bins to one broadcast entry measured slower (the selects cost more VALU
         // than the bank conflicts they remove)
-        tv[q][k][0] = lk(ml);
-        tv[q][k][1] = lk(l0);
-        tv[q][k][2] = lk(l1);
-        tv[q][k][3] = lk(mr);
-        tv[q][k][4] = lk(t0 - l0);
-        tv[q][k][5] = lk(t1 - l1);
+        const uint32_t xs[6] = {ml, l0, l1, mr, t0 - l0, t1 - l1};
+#pragma unroll
+        for (int e = 0; e < 6; ++e) tv[q][k][e] = ((kFinVMask >> e) & 1) ? tfv(xs[e]) : lk(xs[e]);
       }
     }
 #pragma unroll
