@@ -74,8 +74,9 @@ constexpr int kFinVMask = MT_FIN_VMASK;
 
 // x*log2(x) of an integer count in fp32 on the VALU (v_log_f32). Exhaustively
 // measured over 0 <= x < 2^24 (tools/probes/vlog_probe.hip, profiles/r4/vlog_probe.log):
-// relative error <= kTfvRelErr, T(0) = T(1) = 0 exactly -- inside the first pass's
-// error budget (scan_c2_f).
+// relative error <= 2.90 * 2^-24, T(0) = T(1) = 0 exactly -- inside the first pass's
+// per-term budget of 5 * 2^-24 (scan_c2_f). Measured slower than the table on the
+// flagship (profiles/kernel_experiments.md), so the default mask is 0.
 __device__ __forceinline__ float tfv(uint32_t x) {
   const float f = (float)x;
   return f * __builtin_amdgcn_logf(fmaxf(f, 1.0f));
