@@ -1093,6 +1093,10 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
   __shared__ unsigned long long s_cm[kMany ? kTinyWaves : 1][kMany ? kTinyRows : 1];
   __shared__ int32_t s_cid[kMany ? kTinyWaves : 1][kMany ? kTinyRows : 1];
   __shared__ int32_t s_mc[kMany ? kTinyWaves : 1][kMany ? kTinyRows : 1];
+  // kMany: the node's present classes (ascending): their row masks in the node and
+  // counts -- the feature loop sums over these only (deep nodes hold few classes)
+  __shared__ unsigned long long s_nm[kMany ? kTinyWaves : 1][kMany ? kTinyRows : 1];
+  __shared__ int32_t s_nmc[kMany ? kTinyWaves : 1][kMany ? kTinyRows : 1];
   const int lane = lane_id();
   const int wave = threadIdx.x >> 6;
   for (int i = threadIdx.x; i <= kTinyRows; i += blockDim.x) s_tab[i] = xtab[i];
@@ -1165,10 +1169,19 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
       int mc[kMany ? 1 : kTinyMaxC];
       double acc = 0.0;
       int64_t sq = 0;
+      int ncn = 0;  // kMany: classes present in this node
       if constexpr (kMany) {
         for (int c = 0; c < nc; ++c) {
-          const int v = __popcll(M & s_cm[wave][c]);
-          if (lane == 0) s_mc[wave][c] = v;
+          const unsigned long long nm = M & s_cm[wave][c];
+          const int v = __popcll(nm);
+          if (lane == 0) {
+            s_mc[wave][c] = v;
+            if (v > 0) {
+              s_nm[wave][ncn] = nm;
+              s_nmc[wave][ncn] = v;
+            }
+          }
+          ncn += v > 0;
           acc = acc + s_tab[v];
           sq += (int64_t)v * v;
         }
@@ -1214,7 +1227,28 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
         const int mr = mm - ml;
         double cost = __builtin_inf();
         if (inm && ml >= msl && mr >= msl) {
-          if (crit == kEntropy) {
+          // absent classes add T(0) = 0 (or 0 squared) to both sums: the node's
+          // present classes in ascending order give bit-identical sums
+          if constexpr (kMany) {
+            if (crit == kEntropy) {
+              double sl = 0.0, sr = 0.0;
+              for (int i = 0; i < ncn; ++i) {
+                const int lc = __popcll(le & s_nm[wave][i]);
+                sl = sl + s_tab[lc];
+                sr = sr + s_tab[s_nmc[wave][i] - lc];
+              }
+              cost = (s_tab[ml] - sl) + (s_tab[mr] - sr);
+            } else {
+              int64_t ql = 0, qr = 0;
+              for (int i = 0; i < ncn; ++i) {
+                const int64_t lc = __popcll(le & s_nm[wave][i]);
+                const int64_t rc = s_nmc[wave][i] - lc;
+                ql += lc * lc;
+                qr += rc * rc;
+              }
+              cost = gini_term(ml, ql) + gini_term(mr, qr);
+            }
+          } else if (crit == kEntropy) {
             double sl = 0.0, sr = 0.0;
 #pragma unroll
             for (int c = 0; c < kMC; ++c) {

@@ -1,0 +1,9 @@
+#!/bin/bash
+# GPU call (round 4): many-class tiny kernel (per-node class lists): tests + C = 64 bench.
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -v --timeout 120 \
+  --timeout-method thread -p no:cacheprovider \
+  -k "finisher or device_loop or tiny or classifier or many" > gpurun_out/gputests_m.log 2>&1
+timeout -k 10 300 python -u bench.py --classes 64 --steps 3 --warmup 1 > gpurun_out/bench_c64.log 2>&1
