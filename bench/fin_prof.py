@@ -23,7 +23,8 @@ def spy(self, d_jobs, J, *a, **k):
 
 
 hb.HipBackend.launch_finisher = spy
-X, y = make_classification(1_000_000, 64, seed=0)
+C_ARG = int(os.environ.get("FIN_PROF_CLASSES", "2"))
+X, y = make_classification(1_000_000, 64, n_classes=C_ARG, seed=0)
 for _ in range(3):
     r = fitmod.fit_tree(X, y, regression=False, criterion=0, max_depth=None, min_samples_split=2,
                         device="cuda")

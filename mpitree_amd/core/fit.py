@@ -375,7 +375,9 @@ def fit_tree(
         if not env and C > 2:
             # (more classes: no hand-off queue, and a node's histogram scan grows
             # with B * C -- smaller jobs keep every finisher workgroup busy)
-            default_fr = min(default_fr, 4096 if C <= 16 else 2048)
+            # (C = 64: 4096 -> 116.7 ms, 2048 -> 119.0, 1024 -> 134.5, 512 -> 168.0;
+            # profiles/r4/ab_c64_finisher_rows.log)
+            default_fr = min(default_fr, 4096 if C <= 64 else 2048)
         if finisher_rows is None or (comm.world_size > 1 and comm.kind == "data"):
             # data-parallel GPU ranks finish subtrees on their owners (rows sent
             # there first), so the finisher applies as on one GPU

@@ -164,8 +164,11 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
   int32_t* const cmap = cls_lds ? cls_lds + C + 1 : nullptr;
   int32_t* const stc = gstk ? gstk + (int64_t)blockIdx.x * (kFinStack + 2) * C : s_st_cnt;
   const int stw = gstk ? C : kFinStackC;  // stack row stride
-  int32_t* const s_cnt = gstk ? stc + kFinStack * C : s_cnt_l;
-  int32_t* const s_left = gstk ? s_cnt + C : s_left_l;
+  // the node's / left class counts: static LDS up to kFinStackC classes, else
+  // dynamic LDS after the class map (read per class in the scan's inner loop:
+  // never from global scratch)
+  int32_t* const s_cnt = (!kC2 && gstk && cmap) ? cmap + C : s_cnt_l;
+  int32_t* const s_left = (!kC2 && gstk && cmap) ? cmap + 2 * C : s_left_l;
   const int wave = tid >> 6;
   const int lane = lane_id();
   const int W = (C + 1) >> 1;
@@ -1846,7 +1849,8 @@ int finish_lds_bytes(int F, int B, int C) {
   // + per-wave class carries of the multi-pass (B > 256) scan, + the node's
   // present-class list (C > 2)
   return finish_feature_tile(F, B, C) * fin_fstride(B, (C + 1) / 2) * 4 +
-         (B > 256 ? (kFinThreadsWide / kWave) * C * 4 : 0) + (C > 2 ? (2 * C + 1) * 4 : 0);
+         (B > 256 ? (kFinThreadsWide / kWave) * C * 4 : 0) + (C > 2 ? (2 * C + 1) * 4 : 0) +
+         (C > kFinStackC ? 2 * C * 4 : 0);
 }
 int finish_max_classes() { return kFinMaxC; }
 

@@ -150,9 +150,9 @@ def exchange_ranges(be, comm, ranges: torch.Tensor, bound: int):
     live positions as {pos, record[6], stats[C]} rows; one all-gather; every
     rank's rows are scattered back, so each position then holds its one writer's
     record everywhere. ``bound``: at most this many rows (a subtree of r rows has
-    <= 2r - 1 nodes). Two small host waits: the packed row count, and the
-    all-gather's size exchange. Returns the gathered rows (keep until the
-    stream has passed the scatter)."""
+    <= 2r - 1 nodes). One host wait: the packed row counts of every rank, exchanged
+    on the device (``all_gather_rows_counted``). Returns the gathered rows (keep
+    until the stream has passed the scatter)."""
     hip = be.hip
     s = hb._stream()
     Pp = int(be.pos_rec.shape[0])
@@ -172,13 +172,18 @@ def exchange_ranges(be, comm, ranges: torch.Tensor, bound: int):
     hip.own_pack(s, ranges.data_ptr(), int(ranges.shape[0]), base + o_mask, be.pos_rec.data_ptr(),
                  be.pos_st.data_ptr(), reg, Pp, C, base + o_tile, base + o_total, base + o_rank,
                  base + o_rows)
-    h_k = hb._pinned_copy(buf[o_total : o_total + 8].view(torch.int64), "own.k")
-    torch.cuda.current_stream(be.device).synchronize()
-    k = int(h_k[0])
-    if k > bound:
-        raise RuntimeError(f"node exchange: {k} nodes exceed the bound {bound}")
-    rows = buf[o_rows : o_rows + k * (7 + C) * esz].view(dt).view(k, 7 + C)
-    allr = comm.all_gather_rows(rows)
+    k_dev = buf[o_total : o_total + 8].view(torch.int64)
+    if hasattr(comm, "all_gather_rows_counted"):
+        allr = comm.all_gather_rows_counted(
+            buf[o_rows : o_rows + bound * (7 + C) * esz].view(dt).view(bound, 7 + C), k_dev)
+    else:  # (stand-in communicators: the local count first)
+        h_k = hb._pinned_copy(k_dev, "own.k")
+        torch.cuda.current_stream(be.device).synchronize()
+        k = int(h_k[0])
+        if k > bound:
+            raise RuntimeError(f"node exchange: {k} nodes exceed the bound {bound}")
+        rows = buf[o_rows : o_rows + k * (7 + C) * esz].view(dt).view(k, 7 + C)
+        allr = comm.all_gather_rows(rows)
     hip.own_scatter(s, allr.data_ptr(), int(allr.shape[0]), C, be.pos_rec.data_ptr(),
                     be.pos_st.data_ptr(), reg)
     return allr

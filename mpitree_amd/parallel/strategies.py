@@ -205,6 +205,33 @@ class DistComm(LocalComm):
         parts = [out[r * kmax : r * kmax + int(sizes[r])] for r in range(self.world_size)]
         return torch.cat(parts, 0).to(t.device)
 
+    def all_gather_rows_counted(self, buf, k_dev):
+        """All-gather the first ``k_dev`` rows of ``buf`` ([cap, w] on the device;
+        ``k_dev``: a one-element device int64 count a kernel wrote). The counts
+        are exchanged on the device and read with ONE host wait -- the kernel
+        that packed the rows and the count exchange finish together -- where
+        :meth:`all_gather_rows` needs the local count on the host first. Rows
+        past each rank's count are exchanged padded and dropped."""
+        import torch
+
+        P = self.world_size
+        kd = k_dev.reshape(1).to(torch.int64)
+        sizes_d = torch.empty(P, dtype=torch.int64, device=kd.device)
+        self.all_gather_device(sizes_d, kd)
+        sizes = sizes_d.cpu().numpy()  # the one host wait
+        kmax = int(max(1, sizes.max()))
+        k, cap, w = int(sizes[self.rank]), int(buf.shape[0]), int(buf.shape[1])
+        if k > cap:
+            raise RuntimeError(f"row exchange: {k} rows exceed the buffer ({cap})")
+        if kmax <= cap:
+            src = buf[:kmax].contiguous()
+        else:  # a peer has more rows than this buffer holds: pad a copy
+            src = torch.empty((kmax, w), dtype=buf.dtype, device=buf.device)
+            src[:k].copy_(buf[:k])
+        out = torch.empty((P * kmax, w), dtype=buf.dtype, device=buf.device)
+        self.all_gather_device(out.view(-1), src.view(-1))
+        return torch.cat([out[r * kmax : r * kmax + int(sizes[r])] for r in range(P)], 0)
+
     # ------------------------------------------- device-resident collectives
     # The device level loop enqueues these between its kernels: with RCCL the
     # collective runs on the process group's stream ordered after the current

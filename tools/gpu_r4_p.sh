@@ -1,0 +1,13 @@
+#!/bin/bash
+# GPU call (round 4): many-class finisher with LDS class counts (tests, C = 64 bench,
+# finisher profile, finisher_rows sweep) + distributed GPU tests (counted exchange).
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_distributed.py -m gpu -x -v \
+  --timeout 300 --timeout-method thread -p no:cacheprovider \
+  -k "finisher or device_loop or tiny or classifier or many or distributed or own or subtree or rank" \
+  > gpurun_out/gputests_p.log 2>&1
+timeout -k 10 300 python -u bench.py --classes 64 --steps 3 --warmup 1 > gpurun_out/bench_c64.log 2>&1
+FIN_PROF_CLASSES=64 MPITREE_FIN_PROF=1 timeout -k 10 300 python -u bench/fin_prof.py > gpurun_out/fin_prof_c64.log 2>&1
+BENCH_ARGS="--classes 64 --steps 2 --warmup 1" bash tools/gpu_ab_env.sh "MPITREE_FINISHER_ROWS=512" "MPITREE_FINISHER_ROWS=1024" "MPITREE_FINISHER_ROWS=4096"
