@@ -465,12 +465,17 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           ncls = cls_lds[C];
         }
       }
-      // the node's histogram layout: its present classes only (two per word), so
-      // a node holding few of many classes packs more features per LDS tile --
-      // fewer tiles re-reading its rows, more waves scanning
+      // the node's histogram layout: its present classes only, two 16-bit counts
+      // per word -- or four 8-bit ones when the node has at most 255 rows -- so a
+      // node holding few of many classes, or few rows, packs more features per LDS
+      // tile: fewer tiles re-reading its rows, more waves scanning
+      const bool pk8 = cls_lds != nullptr && s_count <= 255;
+      const int psh = pk8 ? 2 : 1;                // log2(classes per word)
+      const int fbits = pk8 ? 8 : 16;             // bits per count
+      const uint32_t fmask = pk8 ? 0xffu : 0xffffu;
       int Wn = W, fstr = fstride, Ftn = Ft;
       if (cls_lds) {
-        Wn = (ncls + 1) >> 1;
+        Wn = (ncls + (1 << psh) - 1) >> psh;
         fstr = fin_fstride(B, Wn);
         Ftn = min(min(F, kFinMaxF), (Ft * fstride) / fstr);
         if (Ftn >= 16 && Ftn < F) Ftn &= ~15;  // (16-B row loads at every tile start)
@@ -544,8 +549,8 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           for (int u = 0; u < kFinUnroll; ++u) {
             if (ent[u] == 0xffffffffu) continue;
             const int sl = cmap ? cmap[lab[u]] : lab[u];  // (compacted class slot)
-            const uint32_t inc = 1u << ((sl & 1) * 16);
-            const int off = sl >> 1;
+            const uint32_t inc = 1u << ((sl & ((1 << psh) - 1)) * fbits);
+            const int off = sl >> psh;
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
               if (v >= vec) break;
@@ -702,8 +707,8 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
               const int b = b0 + k;
-              const uint32_t v = (c >= 0 && b < nb) ? h[b * Wn + (j >> 1)] : 0u;
-              vv[g][k] = (j & 1) ? (v >> 16) : (v & 0xffffu);
+              const uint32_t v = (c >= 0 && b < nb) ? h[b * Wn + (j >> psh)] : 0u;
+              vv[g][k] = (v >> ((j & ((1 << psh) - 1)) * fbits)) & fmask;
             }
           }
 #pragma unroll
@@ -749,8 +754,8 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           for (int k = 0; k < 4; ++k) {
             const int b = b0 + k;
             const uint32_t v = b < nb ? h[b * Wn] : 0u;
-            vlo[k] = v & 0xffffu;
-            vhi[k] = v >> 16;
+            vlo[k] = v & fmask;
+            vhi[k] = (v >> fbits) & fmask;
           }
 #pragma unroll
           for (int half = 0; half < 2; ++half) {
@@ -879,8 +884,8 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           uint32_t s = 0;
           const uint32_t* h = hist + bf * fstr;
           for (int b = lane; b <= bb; b += kWave) {
-            const uint32_t v = h[b * Wn + (j >> 1)];
-            s += (j & 1) ? (v >> 16) : (v & 0xffffu);
+            const uint32_t v = h[b * Wn + (j >> psh)];
+            s += (v >> ((j & ((1 << psh) - 1)) * fbits)) & fmask;
           }
           s = wave_sum_u32(s);
           if (lane == 0) s_left[c] = (int32_t)s;
@@ -1661,7 +1666,11 @@ __device__ __forceinline__ void tiny_sorted_subtree(
         if (ct <= bb) LM |= 1ull << j;
       }
     } else {
-      double bg = -__builtin_inf(), bc = __builtin_inf();
+      // candidates compare by their tie-rounding grid index q = rint(cost / tu):
+      // the gain pterm - q tu orders exactly as -q (tu >> the fp64 error of the
+      // product and the difference), so (max gain, min cost) is (min q) -- the
+      // grid product and the subtraction are never computed per candidate
+      double bq = __builtin_inf();
       bf = 0x7fffffff;
       // this lane's row in the node: {in : 8, in and class 1 : 8}, fetched per
       // feature at sorted position k with one ds_bpermute from lane srt[f][k]
@@ -1671,15 +1680,13 @@ __device__ __forceinline__ void tiny_sorted_subtree(
       auto cost_of = [&](uint32_t v, int ml, int l1) -> double {
         const int mr = mm - ml, r1 = mc1 - l1;
         const bool ok = (v & 0x80u) && ml >= mslw && mr >= mslw;
-        const double c = tie_round(hval(ml, l1) + hval(mr, r1), tinv, tu);
-        return ok ? c : __builtin_inf();
+        const double q = __builtin_rint((hval(ml, l1) + hval(mr, r1)) * tinv);
+        return ok ? q : __builtin_inf();
       };
-      auto take = [&](int f, double cost, uint32_t v) {
-        const double g = pterm - cost;
-        const bool better = g > bg;  // features ascend: strict > keeps the lowest
-        bg = better ? g : bg;
+      auto take = [&](int f, double q, uint32_t v) {
+        const bool better = q < bq;  // features ascend: strict < keeps the lowest
+        bq = better ? q : bq;
         bf = better ? f : bf;
-        bc = better ? cost : bc;
         bb = better ? (v >> 8) : bb;
       };
       // two features per DPP scan: {in, class 1} counts of feature a in the low
@@ -1698,22 +1705,19 @@ __device__ __forceinline__ void tiny_sorted_subtree(
       }
 #pragma unroll
       for (int dd = kWave / 2; dd > 0; dd >>= 1) {
-        const double og = __shfl_xor(bg, dd, kWave);
+        const double oq = __shfl_xor(bq, dd, kWave);
         const int of = __shfl_xor(bf, dd, kWave);
-        const double oc = __shfl_xor(bc, dd, kWave);
         const uint32_t ob = (uint32_t)__shfl_xor((int)bb, dd, kWave);
-        const bool tk =
-            og > bg || (og == bg && (of < bf || (of == bf && (oc < bc || (oc == bc && ob < bb)))));
+        const bool tk = oq < bq || (oq == bq && (of < bf || (of == bf && ob < bb)));
         if (tk) {
-          bg = og;
+          bq = oq;
           bf = of;
-          bc = oc;
           bb = ob;
         }
       }
       bf = __builtin_amdgcn_readfirstlane(bf);
       bb = (uint32_t)__builtin_amdgcn_readfirstlane((int)bb);
-      if (!(bg > -__builtin_inf()) || bf < 0) continue;  // leaf: the creation record stands
+      if (!(bq < __builtin_inf()) || bf < 0) continue;  // leaf: the creation record stands
       // left rows: sorted positions of feature bf with code <= bb, scattered back to lanes
       {
         const uint32_t v = srt[bf * kWave + lane];
