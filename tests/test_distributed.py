@@ -478,3 +478,28 @@ def test_tree_digest_covers_thresholds():
     a = DecisionTreeClassifier(device="cpu").fit(X, y).tree_arrays_
     b = DecisionTreeClassifier(device="cpu").fit(X * 10, y).tree_arrays_
     assert tree_digest(a) != tree_digest(b)  # same structure, different thresholds
+
+
+def _counted_rows(rank, world):
+    import torch
+
+    from mpitree_amd.parallel.strategies import SubtreeComm
+
+    comm = SubtreeComm()
+    # rank r packed 3 + 4 r rows into a buffer of 8 rows (rank 1's 7 rows fit, a
+    # later rank would exceed rank 0's buffer: the exchange pads a copy)
+    k = 3 + 4 * rank
+    buf = torch.full((max(k, 8), 5), -1, dtype=torch.int32)
+    buf[:k] = torch.arange(k * 5, dtype=torch.int32).reshape(k, 5) + 1000 * rank
+    out = comm.all_gather_rows_counted(buf, torch.tensor([k], dtype=torch.int64))
+    return {"rows": out.numpy()}
+
+
+def test_all_gather_rows_counted_pads_and_concatenates():
+    """The one-wait row exchange (device-side counts) equals the concatenation of
+    every rank's first k rows, also when a peer has more rows than this buffer."""
+    outs = run_ranks(_counted_rows, 3)
+    want = np.concatenate([np.arange((3 + 4 * r) * 5).reshape(-1, 5) + 1000 * r
+                           for r in range(3)])
+    for o in outs:
+        np.testing.assert_array_equal(o["rows"], want)
