@@ -245,11 +245,11 @@ class DecisionTreeClassifier(_BaseTree, ClassifierMixin):
         """
         leaves = self.apply(X)
         if isinstance(leaves, torch.Tensor):
-            counts = torch.from_numpy(self._arrays.count).to(leaves.device)[leaves]
+            counts = torch.from_numpy(self._arrays.count).to(leaves.device)[leaves].long()
             if normalize:
                 return counts.double() / counts.sum(1, keepdim=True)
             return counts
-        counts = self._arrays.count[leaves]
+        counts = self._arrays.count[leaves].astype(np.int64, copy=False)
         if normalize:
             return counts / counts.sum(axis=1, keepdims=True)
         return counts

@@ -33,7 +33,7 @@ class TreeArrays:
     depth: np.ndarray  # int32 [N]
     n_samples: np.ndarray  # int64 [N]
     impurity: np.ndarray  # float64 [N]
-    count: Optional[np.ndarray] = None  # int64 [N, C] (classification)
+    count: Optional[np.ndarray] = None  # [N, C] class counts: int32 (GPU), int64 (host)
     value: Optional[np.ndarray] = None  # float64 [N] (regression leaf mean)
     meta: dict = field(default_factory=dict)
 
@@ -41,7 +41,7 @@ class TreeArrays:
     def from_packed(cls, buf: np.ndarray, N: int, C: int, regression: bool,
                     max_depth: int | None = None) -> "TreeArrays":
         """Views of the device assembly's packed columns (``ops/csrc/assemble.hip``
-        ``asm_cols``): n_samples i64 | threshold f64 | impurity f64 | counts i64
+        ``asm_cols``): n_samples i64 | threshold f64 | impurity f64 | counts i32
         [N, C] (or leaf value f64 + fixed-point sum i64) | feature, threshold_bin,
         left, right, depth i32. Every column is final: no host pass follows."""
         o = 0
@@ -60,7 +60,7 @@ class TreeArrays:
             value = take(np.float64, N)
             s_fixed = take(np.int64, N)
         else:
-            count = take(np.int64, N * C).reshape(N, C)
+            count = take(np.int32, N * C).reshape(N, C)
         feature = take(np.int32, N)
         threshold_bin = take(np.int32, N)
         left = take(np.int32, N)

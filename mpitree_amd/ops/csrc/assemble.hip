@@ -145,7 +145,8 @@ __global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __
 // host round trip. Every column of the finished tree is emitted in its final
 // dtype -- the host receives numpy views, nothing is derived after the copy:
 //   n_samples i64 [N] | threshold f64 [N] | impurity f64 [N]
-//   | counts i64 [N][C] (classification) or leaf value f64 [N] + fixed-point
+//   | counts i32 [N][C] (classification: rows < 2^31, half the bytes of the one
+//     D2H at many classes) or leaf value f64 [N] + fixed-point
 //     target sum i64 [N] (regression)
 //   | feature i32 [N] | threshold_bin i32 [N] | left i32 [N] | right i32 [N]
 // (thresholds: edges[feature][bin], or per position from thr_pos -- the exact
@@ -160,7 +161,7 @@ struct AsmCols {
   int64_t* nsamp;
   double* threshold;
   double* impurity;
-  int64_t* count;  // classification
+  int32_t* count;  // classification
   double* value;   // regression
   int64_t* sum;    // regression
   int32_t* feature;
@@ -171,7 +172,7 @@ struct AsmCols {
 };
 
 __host__ __device__ inline int64_t asm_bytes(int64_t N, int C, bool reg) {
-  return N * (24 + (reg ? 16 : 8 * (int64_t)C) + 20);
+  return N * (24 + (reg ? 16 : 4 * (int64_t)C) + 20);
 }
 
 __device__ inline AsmCols asm_cols(uint8_t* base, int64_t N, int C, bool reg) {
@@ -192,8 +193,8 @@ __device__ inline AsmCols asm_cols(uint8_t* base, int64_t N, int C, bool reg) {
     o.sum = reinterpret_cast<int64_t*>(p);
     p += N * 8;
   } else {
-    o.count = reinterpret_cast<int64_t*>(p);
-    p += N * 8 * (int64_t)C;
+    o.count = reinterpret_cast<int32_t*>(p);
+    p += N * 4 * (int64_t)C;
   }
   o.feature = reinterpret_cast<int32_t*>(p);
   o.bin = o.feature + N;
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
     double acc = 0.0;
     for (int c = 0; c < C; ++c) {
       const int64_t v = (int64_t)s[c];
-      o.count[(int64_t)j * C + c] = v;
+      o.count[(int64_t)j * C + c] = (int32_t)v;
       m += v;
       sq += v * v;
       acc = acc + T(v);

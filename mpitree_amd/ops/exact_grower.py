@@ -395,11 +395,20 @@ class ExactGrower:
         rk = torch.empty(Pp, dtype=torch.int32, device=dev)
         hip.asm_rank(s(), be.pos_rec.data_ptr(), Pp, tile.data_ptr(), total.data_ptr(),
                      rk.data_ptr(), mask=resolved.data_ptr())
-        k = int(total[0].item())
-        rows = torch.empty((max(k, 1), 3), dtype=torch.int64, device=dev)
-        hip.xe_resolved_pack(s(), be.pos_rec.data_ptr(), pos_thr.data_ptr(), Pp,
-                             rk.data_ptr(), rows.data_ptr())
-        allr = comm.all_gather_rows(rows[:k])
+        if hasattr(comm, "all_gather_rows_counted"):
+            # pack into a position-space-sized buffer: the counts travel on the
+            # device and the exchange makes one host wait
+            rows = hb._workspace(dev, "xe.resolved", Pp * 3 * 8)[: Pp * 3 * 8]
+            rows = rows.view(torch.int64).view(Pp, 3)
+            hip.xe_resolved_pack(s(), be.pos_rec.data_ptr(), pos_thr.data_ptr(), Pp,
+                                 rk.data_ptr(), rows.data_ptr())
+            allr = comm.all_gather_rows_counted(rows, total[0:1])
+        else:
+            k = int(total[0].item())
+            rows = torch.empty((max(k, 1), 3), dtype=torch.int64, device=dev)
+            hip.xe_resolved_pack(s(), be.pos_rec.data_ptr(), pos_thr.data_ptr(), Pp,
+                                 rk.data_ptr(), rows.data_ptr())
+            allr = comm.all_gather_rows(rows[:k])
         hip.xe_resolved_scatter(s(), allr.data_ptr(), int(allr.shape[0]),
                                 be.pos_rec.data_ptr(), pos_thr.data_ptr())
         self._keep_r = (allr, rows, resolved, tile, total, rk)
