@@ -59,6 +59,13 @@ struct XeArgs {
   uint64_t* pstat;     // [PMAX][F_loc] left counts (partition)
   int32_t* tick;       // [4] {scan ticket, partition ticket, watchdog, -}
   uint32_t tag;        // this level's status tag (30 bits, nonzero)
+  // two-class chunk totals counted by the partition (no xe_tot pass over the lists):
+  // sitem [SMAX][2] = first next-level item of each split node's frontier child (-1:
+  // leaf or finisher job), nctl = the next level's ctl, tot_ready = this level's
+  // totals were counted by the previous level's partition; null / 0: xe_tot
+  const int32_t* sitem;
+  const int32_t* nctl;
+  int tot_ready;
 };
 
 __host__ __device__ inline int xe_cc(int C) { return C > 0 ? C : 1; }
@@ -89,6 +96,7 @@ struct XePlanArgs {
   int32_t* host_ctl;   // host-mapped {next frontier size, jobs so far, tag}
   int32_t host_tag;
   int32_t* tick;       // XeArgs::tick: the planner rearms both tickets
+  int32_t* sitem;      // XeArgs::sitem, or null
 };
 
 

@@ -1030,6 +1030,10 @@ __global__ __launch_bounds__(kXePlanThreads) void xe_plan_kernel(XePlanArgs a) {
         S[1] = m;
         S[2] = feat;
         S[3] = nl;
+        if (a.sitem) {  // (the partition counts the frontier children's chunk totals)
+          a.sitem[o_ns * 2 + 0] = -1;
+          a.sitem[o_ns * 2 + 1] = -1;
+        }
         // partition items of this split node
         for (int q = 0; q < np; ++q) {
           int64_t* it = a.pitems + (int64_t)(o_np + q) * 4;
@@ -1079,6 +1083,7 @@ __global__ __launch_bounds__(kXePlanThreads) void xe_plan_kernel(XePlanArgs a) {
             a.nxt.depth[sl] = cd;
             for (int k = 0; k < Cs; ++k) a.nxt.stats[(int64_t)sl * Cs + k] = child_stat(k);
             a.nxt.ifirst[sl] = io;
+            if (a.sitem) a.sitem[o_ns * 2 + c] = io;
             const int64_t nck = (cm + kXeChunk - 1) / kXeChunk;
             for (int q = 0; q < nck; ++q) {
               int64_t* it = a.nxt.items + (int64_t)(io + q) * 4;
@@ -1261,6 +1266,52 @@ __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a,
       if (lane == 0) xe_publish(st, a.tag, kXeIncl, (uint32_t)(lb + T));
     }
     const int64_t nlj = a.split[j * 4 + 3];
+    if (!kReg && a.sitem) {
+      // the next level's two-class chunk totals: this unit's left rows land at
+      // [lb, lb + T) of the left child, its right rows at [(c0 - s0) - lb, ...) of
+      // the right child -- each a run of <= 1024 positions, so at most two
+      // 2048-entry chunks per side; count {class 0, class 1} per chunk
+      const int64_t pl0 = lb, pr0 = (c0 - s0) - lb;
+      const int64_t ql0 = pl0 / kXeChunk, qr0 = pr0 / kXeChunk;
+      uint32_t acc[2] = {0u, 0u};  // [side]: {chunk 0 class 0, chunk 0 class 1, chunk 1 c0, c1} bytes
+      uint32_t acc2[2] = {0u, 0u};
+      int lrun = 0, rrun = 0;
+#pragma unroll
+      for (int q = 0; q < kXePartPer; ++q) {
+        const int64_t i = (int64_t)q * kWave + lane;
+        const unsigned long long vm = __ballot(i < cn);
+        const unsigned long long rm = vm & ~bal[q];
+        const bool go = (bal[q] >> lane) & 1ull;
+        if (i < cn) {
+          const int lab = xe_lab(e[q]) & 1;
+          const int64_t pos = go ? pl0 + lrun + __popcll(bal[q] & lt)
+                                 : pr0 + rrun + __popcll(rm & lt);
+          const int k = (int)(pos / kXeChunk - (go ? ql0 : qr0));  // 0 or 1
+          const uint32_t one = 1u << (16 * lab);
+          if (k == 0) acc[go ? 0 : 1] += one;
+          else acc2[go ? 0 : 1] += one;
+        }
+        lrun += __popcll(bal[q]);
+        rrun += __popcll(rm);
+      }
+#pragma unroll
+      for (int sd = 0; sd < 2; ++sd) {
+        const uint32_t t0 = wave_sum_u32(acc[sd]), t1 = wave_sum_u32(acc2[sd]);
+        const int32_t it0 = a.sitem[j * 2 + sd];
+        if (lane == 0 && it0 >= 0) {
+          const int64_t qb = sd == 0 ? ql0 : qr0;
+          const int Cc = xe_cc(a.C);
+          for (int k = 0; k < 2; ++k) {
+            const uint32_t t = k == 0 ? t0 : t1;
+            if (t == 0u) continue;
+            unsigned long long* o = reinterpret_cast<unsigned long long*>(
+                a.tot + ((int64_t)(it0 + qb + k) * a.F_loc + f) * Cc);
+            atomicAdd(o, (unsigned long long)(t & 0xffffu));
+            if (Cc > 1) atomicAdd(o + 1, (unsigned long long)(t >> 16));
+          }
+        }
+      }
+    }
     if constexpr (kStage) {
       // the unit's left rows go to s0 + lb + [0, T), its right rows to rbase + [0, cn - T)
       const int64_t rbase = s0 + nlj + (c0 - s0) - lb;
@@ -1311,6 +1362,16 @@ __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a,
       }
     }
   }
+}
+
+// Zero the next level's chunk totals (the partition adds into them): grid-stride
+// over the device count of next-level items.
+__global__ __launch_bounds__(256) void xe_tot_zero_kernel(int64_t* __restrict__ tot,
+                                                          const int32_t* __restrict__ nctl,
+                                                          int64_t per_item) {
+  const int64_t total = (int64_t)nctl[1] * per_item;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256)
+    tot[i] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1591,9 +1652,10 @@ void xe_level_scan(hipStream_t s, const XeArgs& a, const XeLists& cur, int items
                    int slots_bound) {
   if (items_bound <= 0 || slots_bound <= 0) return;
   const int Cc = xe_cc(a.C);
-  // chunk totals, carries, then the scan
+  // chunk totals (unless the previous partition counted them), carries, then the scan
   const int gx = xe_gx(items_bound, a.F_loc);
-  hipLaunchKernelGGL(xe_tot_kernel, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
+  if (!a.tot_ready)
+    hipLaunchKernelGGL(xe_tot_kernel, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
   const int64_t nc = (int64_t)slots_bound * a.F_loc * Cc;
   hipLaunchKernelGGL(xe_carry_kernel, dim3((unsigned)((nc + kXeThreads - 1) / kXeThreads)),
                      dim3(kXeThreads), 0, s, a, cur);
@@ -1637,6 +1699,9 @@ void xe_flag(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_boun
 void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_bound,
                   int splits_bound) {
   if (pitems_bound <= 0 || splits_bound <= 0) return;
+  if (a.sitem && a.nctl)
+    hipLaunchKernelGGL(xe_tot_zero_kernel, dim3(1024), dim3(256), 0, s, a.tot, a.nctl,
+                       (int64_t)a.F_loc * xe_cc(a.C));
   int dev = 0, n_cu = 0;
   MT_HIP_CHECK(hipGetDevice(&dev));
   MT_HIP_CHECK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));

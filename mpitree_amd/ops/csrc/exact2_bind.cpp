@@ -28,6 +28,7 @@ struct XeCtx {
   int64_t* Yb[2]{};
   XePlanArgs p{};
   uint32_t seq = 1;  // fit sequence number: look-back status tags differ per (fit, level)
+  int32_t* sitem = nullptr;  // two-class chunk totals counted by the partition (or null)
 
   XeArgs args(int lvl) const {
     XeArgs x = a;
@@ -37,6 +38,9 @@ struct XeCtx {
     x.D = Eb[c ^ 1];
     x.Y = Yb[c];
     x.DY = Yb[c ^ 1];
+    x.sitem = sitem;
+    x.nctl = sitem ? L[c ^ 1].ctl : nullptr;
+    x.tot_ready = sitem != nullptr && lvl > 0;
     return x;
   }
 };
@@ -105,6 +109,11 @@ void bind_exact2(py::module_& m) {
         a.pstat = ptr<uint64_t>(u("pstat"));
         a.tick = ptr<int32_t>(u("tick"));
         a.tag = 1;
+        // (two classes: the partition counts the next level's chunk totals)
+        c.sitem = (a.C > 0 && a.C <= 2 && d.contains("sitem")) ? ptr<int32_t>(u("sitem")) : nullptr;
+        a.sitem = nullptr;
+        a.nctl = nullptr;
+        a.tot_ready = 0;
         XePlanArgs& p = c.p;
         p.rec = a.rec;
         p.split = a.split;
@@ -124,6 +133,7 @@ void bind_exact2(py::module_& m) {
         p.msl = g("msl");
         p.fr = g("fr");
         p.tick = a.tick;
+        p.sitem = c.sitem;
         return c;
       }))
       .def("begin", [](XeCtx& c, int64_t seq) { c.seq = (uint32_t)seq; })

@@ -263,6 +263,7 @@ class ExactGrower:
                 flag=torch.empty((n + 31) // 32, dtype=torch.int32, device=dev),
                 # look-back status words (tagged per fit and level: zeroed once)
                 pstat=torch.zeros((2 * IMAX, F_loc), **i64),  # (2 wave units per item)
+                sitem=torch.empty((KMAX, 2), **i32),  # (partition-counted chunk totals)
                 tick=torch.zeros(4, **i32),
                 jobs=torch.empty((JMAX, JW), **i64),
                 job_count=torch.zeros(1, **i32),
@@ -284,6 +285,8 @@ class ExactGrower:
             rec=ptr["rec"], split=ptr["split"],
             pitems=ptr["pitems"], pfirst=ptr["pfirst"], flag=ptr["flag"],
             pstat=ptr["pstat"], tick=ptr["tick"], pos_rec=be.pos_rec.data_ptr(),
+            **({"sitem": ptr["sitem"]} if os.environ.get("MPITREE_EXACT_PART_TOT", "1") != "0"
+               else {}),
             pos_st=be.pos_st.data_ptr(), pos_thr=pos_thr.data_ptr(), jobs=ptr["jobs"],
             job_count=ptr["job_count"], max_depth=md, mss=mss, fr=fr), lp[0], lp[1])
         ws["root"].copy_(torch.from_numpy(np.ascontiguousarray(root_stats, np.int64)))
