@@ -1177,12 +1177,6 @@ constexpr int kXeSub = kWave * kXePartPer;             // entries per wave unit 
 constexpr int kXeSubPerChunk = kXeChunk / kXeSub;      // 2
 constexpr int kXePartLdsWords = 36 * 1024;             // 144 KB of flag words in LDS
 constexpr int64_t kXePartLdsRows = (int64_t)kXePartLdsWords * 32;
-// classification: each wave stages half a unit (512 entries) in LDS in destination
-// order and stores it as two contiguous runs (left, right) -- whole cache lines
-// from one wave instead of two interleaved partial runs per store instruction
-constexpr int kXeStage = kXeSub / 2;
-constexpr int kXeStageWords = kXePartWaves * kXeStage;  // 32 KB per workgroup
-constexpr int kXeLdsTotalWords = 40 * 1024;             // 160 KB
 #ifndef MT_XE_PART_BATCH  // (4 / 8 / 32 / 64 measured slower: profiles/kernel_experiments.md)
 #define MT_XE_PART_BATCH 16
 #endif
@@ -1204,7 +1198,7 @@ __device__ __forceinline__ int xe_part_batch(int F_loc) {
   return kXePartBatch;
 }
 
-template <bool kLdsFlags, bool kReg, bool kStage>
+template <bool kLdsFlags, bool kReg>
 __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a, XeLists cur) {
   extern __shared__ uint32_t s_flag[];
   const int nw = kLdsFlags ? (int)((a.n + 31) >> 5) : 0;
@@ -1212,7 +1206,6 @@ __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a,
     for (int i = threadIdx.x; i < nw; i += blockDim.x) s_flag[i] = a.flag[i];
     __syncthreads();
   }
-  uint32_t* const stg = s_flag + ((nw + 3) & ~3) + (threadIdx.x >> 6) * kXeStage;
   const uint32_t* fl = kLdsFlags ? s_flag : a.flag;
   const int lane = lane_id();
   const unsigned long long lt = (1ull << lane) - 1ull;
@@ -1312,53 +1305,15 @@ __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a,
         }
       }
     }
-    if constexpr (kStage) {
-      // the unit's left rows go to s0 + lb + [0, T), its right rows to rbase + [0, cn - T)
-      const int64_t rbase = s0 + nlj + (c0 - s0) - lb;
-      int lrun = 0, rrun = 0;  // left / right rows of the unit stored so far
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int hn = (int)min<int64_t>(cn - (int64_t)h * kXeStage, kXeStage);
-        if (hn <= 0) break;  // (wave-uniform)
-        constexpr int kQ = kXePartPer / 2;
-        int tl = 0;
-#pragma unroll
-        for (int q = 0; q < kQ; ++q) tl += __popcll(bal[h * kQ + q]);
-        int lc = 0, rc = 0;
-#pragma unroll
-        for (int q = 0; q < kQ; ++q) {
-          const int qq = h * kQ + q;
-          const int64_t i = (int64_t)qq * kWave + lane;
-          const unsigned long long vm = __ballot(i < cn);
-          const unsigned long long rm = vm & ~bal[qq];
-          if (i < cn)
-            stg[((bal[qq] >> lane) & 1ull) ? lc + __popcll(bal[qq] & lt)
-                                           : tl + rc + __popcll(rm & lt)] = e[qq];
-          lc += __popcll(bal[qq]);
-          rc += __popcll(rm);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        for (int p = lane; p < hn; p += kWave) {
-          const int64_t dst = p < tl ? s0 + lb + lrun + p : rbase + rrun + (p - tl);
-          O[dst] = stg[p];
-        }
-        lrun += tl;
-        rrun += hn - tl;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();  // (the next half reuses the staging words)
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < kXePartPer; ++q) {
-        const int64_t i = (int64_t)q * kWave + lane;
-        const int64_t l = lb + __popcll(bal[q] & lt);
-        lb += __popcll(bal[q]);
-        if (i < cn) {
-          const int64_t dst = ((bal[q] >> lane) & 1ull) ? s0 + l : s0 + nlj + (c0 + i - s0) - l;
-          O[dst] = e[q];
-          if constexpr (kReg) a.DY[(int64_t)f * a.n + dst] = y[q];
-        }
+    for (int q = 0; q < kXePartPer; ++q) {
+      const int64_t i = (int64_t)q * kWave + lane;
+      const int64_t l = lb + __popcll(bal[q] & lt);
+      lb += __popcll(bal[q]);
+      if (i < cn) {
+        const int64_t dst = ((bal[q] >> lane) & 1ull) ? s0 + l : s0 + nlj + (c0 + i - s0) - l;
+        O[dst] = e[q];
+        if constexpr (kReg) a.DY[(int64_t)f * a.n + dst] = y[q];
       }
     }
   }
@@ -1713,37 +1668,23 @@ void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems
     const char* v = std::getenv("MPITREE_EXACT_PART_LDS");
     return v && v[0] == '0';
   }();
-  static const bool stage_off = [] {  // (MPITREE_EXACT_PART_STAGE=0: unstaged scatter, A/B)
-    const char* v = std::getenv("MPITREE_EXACT_PART_STAGE");
-    return v && v[0] == '0';
-  }();
-  const int64_t flag_words = ((a.n + 31) / 32 + 3) & ~(int64_t)3;
-  // classification stages its scatter when the staging words fit next to the flags
-  const bool stage_lds = a.C != 0 && !stage_off && flag_words + kXeStageWords <= kXeLdsTotalWords;
   if (a.n <= kXePartLdsRows && !lds_off) {
-    const size_t lds = (size_t)(stage_lds ? flag_words + kXeStageWords : (a.n + 31) / 32) * 4;
-#define MT_XP(REG, ST)                                                                        \
-  MT_HIP_CHECK(mt_set_max_lds((const void*)xe_part_kernel<true, REG, ST>, (int)lds));        \
-  hipLaunchKernelGGL((xe_part_kernel<true, REG, ST>), dim3(grid), dim3(kXePartWaves * kWave),  \
+    const size_t lds = (size_t)((a.n + 31) / 32) * 4;
+#define MT_XP(REG)                                                                          \
+  MT_HIP_CHECK(mt_set_max_lds((const void*)xe_part_kernel<true, REG>, (int)lds));          \
+  hipLaunchKernelGGL((xe_part_kernel<true, REG>), dim3(grid), dim3(kXePartWaves * kWave),   \
                      lds, s, a, cur);
     if (a.C == 0) {
-      MT_XP(true, false)
-    } else if (stage_lds) {
-      MT_XP(false, true)
+      MT_XP(true)
     } else {
-      MT_XP(false, false)
+      MT_XP(false)
     }
 #undef MT_XP
   } else if (a.C == 0) {
-    hipLaunchKernelGGL((xe_part_kernel<false, true, false>), dim3(grid * 2),
-                       dim3(kXePartWaves * kWave), 0, s, a, cur);
-  } else if (!stage_off) {
-    const size_t lds = (size_t)kXeStageWords * 4;
-    MT_HIP_CHECK(mt_set_max_lds((const void*)xe_part_kernel<false, false, true>, (int)lds));
-    hipLaunchKernelGGL((xe_part_kernel<false, false, true>), dim3(grid * 2),
-                       dim3(kXePartWaves * kWave), lds, s, a, cur);
+    hipLaunchKernelGGL((xe_part_kernel<false, true>), dim3(grid * 2), dim3(kXePartWaves * kWave),
+                       0, s, a, cur);
   } else {
-    hipLaunchKernelGGL((xe_part_kernel<false, false, false>), dim3(grid * 2),
+    hipLaunchKernelGGL((xe_part_kernel<false, false>), dim3(grid * 2),
                        dim3(kXePartWaves * kWave), 0, s, a, cur);
   }
   MT_HIP_CHECK(hipGetLastError());
