@@ -51,7 +51,7 @@ int finish_feature_tile(int F, int B, int C);
 int asm_tiles(int64_t P);
 void launch_grow_plan(hipStream_t, const PlanArgs&);
 size_t exact_setup_temp_bytes(int64_t, int);
-void exact_setup_sort(hipStream_t, const float*, int64_t, int, uint64_t*, uint64_t*, uint32_t*,
+void exact_setup_sort(hipStream_t, const float*, int64_t, int, uint32_t*, uint32_t*, uint32_t*,
                       uint32_t*, void*, size_t, int32_t*, int32_t*, int, int);
 void bind_exact2(pybind11::module_& m);
 void bind_grow(pybind11::module_& m);
@@ -308,7 +308,7 @@ PYBIND11_MODULE(_hip, m) {
                                uintptr_t k1, uintptr_t r0, uintptr_t r1, uintptr_t temp,
                                size_t temp_bytes, uintptr_t cnt, uintptr_t nuniq, int xs,
                                int f_lo) {
-    mt::exact_setup_sort(S(s), P<float>(X), n, F, P<uint64_t>(k0), P<uint64_t>(k1),
+    mt::exact_setup_sort(S(s), P<float>(X), n, F, P<uint32_t>(k0), P<uint32_t>(k1),
                          P<uint32_t>(r0), P<uint32_t>(r1), P<void>(temp), temp_bytes,
                          P<int32_t>(cnt), P<int32_t>(nuniq), xs, f_lo);
   }, py::arg("s"), py::arg("X"), py::arg("n"), py::arg("F"), py::arg("k0"), py::arg("k1"),

@@ -128,7 +128,7 @@ void xe_resolved_pack(hipStream_t s, const int32_t* pos_rec, const double* pos_t
                       const int32_t* rank, int64_t* rows);
 void xe_resolved_scatter(hipStream_t s, const int64_t* rows, int64_t k, int32_t* pos_rec,
                          double* pos_thr);
-void xe_emit(hipStream_t s, const uint64_t* keys, const uint32_t* rows, int64_t n, int F_loc,
+void xe_emit(hipStream_t s, const uint32_t* keys, const uint32_t* rows, int64_t n, int F_loc,
              int nc, int chunk, const int32_t* cbase, const int32_t* ylab, const int64_t* yfix,
              uint32_t* E, int64_t* Y, uint32_t* rank_at);
 

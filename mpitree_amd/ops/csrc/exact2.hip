@@ -1536,10 +1536,10 @@ __global__ __launch_bounds__(256) void xe_resolved_scatter_kernel(const int64_t*
 }
 
 // ---------------------------------------------------------------------------
-// Setup: sorted keys {feature : 32 | value bits : 32} with row ids (exact_setup.hip
+// Setup: each feature's sorted 32-bit value keys with row ids (exact_setup.hip
 // sort) -> entries, value ranks by sorted position, duplicate flags. cbase: per-(feature,
 // chunk) first rank (exact_setup's count / scan of value changes).
-__global__ __launch_bounds__(256) void xe_emit_kernel(const uint64_t* __restrict__ keys,
+__global__ __launch_bounds__(256) void xe_emit_kernel(const uint32_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ rows, int64_t n,
                                                       int nc, int chunk,
                                                       const int32_t* __restrict__ cbase,
@@ -1560,7 +1560,7 @@ __global__ __launch_bounds__(256) void xe_emit_kernel(const uint64_t* __restrict
   for (int64_t b = p0; b < p1; b += 256) {
     const int64_t p = b + threadIdx.x;
     const bool in = p < p1;
-    const uint64_t key = in ? keys[base + p] : 0ull;
+    const uint32_t key = in ? keys[base + p] : 0u;
     const bool nw = in && (p == 0 || keys[base + p - 1] != key);
     const bool dn = in && p + 1 < n && keys[base + p + 1] == key;
     const bool dup = in && (!nw || dn);
@@ -1744,7 +1744,7 @@ void xe_resolved_scatter(hipStream_t s, const int64_t* rows, int64_t k, int32_t*
   MT_HIP_CHECK(hipGetLastError());
 }
 
-void xe_emit(hipStream_t s, const uint64_t* keys, const uint32_t* rows, int64_t n, int F_loc,
+void xe_emit(hipStream_t s, const uint32_t* keys, const uint32_t* rows, int64_t n, int F_loc,
              int nc, int chunk, const int32_t* cbase, const int32_t* ylab, const int64_t* yfix,
              uint32_t* E, int64_t* Y, uint32_t* rank_at) {
   if (n <= 0 || F_loc <= 0) return;

@@ -202,7 +202,7 @@ void bind_exact2(py::module_& m) {
   m.def("xe_emit", [](uintptr_t s, uintptr_t keys, uintptr_t rows, int64_t n, int F_loc, int nc,
                       int chunk, uintptr_t cbase, uintptr_t ylab, uintptr_t yfix, uintptr_t E,
                       uintptr_t Y, uintptr_t rank_at) {
-    xe_emit(stream_of(s), ptr<uint64_t>(keys), ptr<uint32_t>(rows), n, F_loc, nc, chunk,
+    xe_emit(stream_of(s), ptr<uint32_t>(keys), ptr<uint32_t>(rows), n, F_loc, nc, chunk,
             ptr<int32_t>(cbase), ptr<int32_t>(ylab), ptr<int64_t>(yfix), ptr<uint32_t>(E),
             ptr<int64_t>(Y), ptr<uint32_t>(rank_at));
   });

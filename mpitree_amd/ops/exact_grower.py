@@ -6,8 +6,8 @@ subtrees to MPI sub-communicators (``:446-477``). The histogram engines are
 exact only while a feature has at most 256 values; beyond that a GPU fit runs
 this engine (``ops/csrc/exact2.hip``, classification and regression):
 
-* setup: every feature column of this rank's block sorted once (one stable
-  radix sort of {feature, value} keys, ``exact_setup.hip``) into 4-byte list
+* setup: every feature column of this rank's block sorted once (a batched
+  one-sweep radix sort of 32-bit value keys, ``exact_setup.hip``) into 4-byte list
   entries {row, duplicate flag, label} (+ the fixed-point targets for
   regression) and a per-row value-rank table;
 * a fixed chain of launches per level (chunk totals, carries, scan, select,
@@ -113,7 +113,7 @@ class ExactGrower:
         ylab = y32.data_ptr() if packed else 0
         yf = yfix.data_ptr() if reg else 0
         if Xd.dtype == torch.float32:
-            keys = [torch.empty((F_loc, n), dtype=torch.int64, device=dev) for _ in range(2)]
+            keys = [torch.empty((F_loc, n), dtype=torch.int32, device=dev) for _ in range(2)]
             rows = [torch.empty((F_loc, n), dtype=torch.int32, device=dev) for _ in range(2)]
             tb = int(hip.exact_setup_temp_bytes(n, F_loc))
             temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)

@@ -493,6 +493,49 @@ def test_gpu_exact_setup_native_equals_torch_path():
     assert g32.tree_arrays_.equal(h.tree_arrays_)
 
 
+@pytest.mark.parametrize("n", [1, 4095, 4097, 300_001])
+def test_gpu_exact_setup_sort_equals_stable_sort(n):
+    """The batched one-sweep radix sort (exact_setup.hip) against torch's stable
+    sort of each column (ties by row id, -0.0 == 0.0): sorted rows, per-chunk
+    value-change counts and unique counts; a column block of a wider X (f_lo, xs)."""
+    from mpitree_amd.ops import native
+
+    hip = native.hip()
+    rng = np.random.default_rng(n)
+    F, f_lo, xs = 9, 2, 12
+    Xh = rng.normal(size=(n, xs)).astype(np.float32)
+    Xh[:, 3] = np.round(Xh[:, 3], 1)  # many ties
+    Xh[:, 4] = 7.0  # one value
+    Xh[rng.random((n, xs)) < 0.03] = -0.0
+    Xh[rng.random((n, xs)) < 0.03] = 0.0
+    X = torch.from_numpy(Xh).cuda()
+    dev = X.device
+    keys = [torch.empty((F, n), dtype=torch.int32, device=dev) for _ in range(2)]
+    rows = [torch.empty((F, n), dtype=torch.int32, device=dev) for _ in range(2)]
+    tb = int(hip.exact_setup_temp_bytes(n, F))
+    temp = torch.empty(tb, dtype=torch.uint8, device=dev)
+    chunk = int(hip.exact_setup_chunk())
+    nc = -(-n // chunk)
+    cnt = torch.empty((F, nc), dtype=torch.int32, device=dev)
+    nuniq = torch.empty(F, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    hip.exact_setup_sort(s, X.data_ptr(), n, F, keys[0].data_ptr(), keys[1].data_ptr(),
+                         rows[0].data_ptr(), rows[1].data_ptr(), temp.data_ptr(), tb,
+                         cnt.data_ptr(), nuniq.data_ptr(), xs=xs, f_lo=f_lo)
+    torch.cuda.synchronize()
+    xt = (X[:, f_lo:f_lo + F] + 0.0).t().contiguous()
+    vals, order = torch.sort(xt, dim=1, stable=True)
+    assert torch.equal(rows[1].long(), order)
+    new = torch.ones_like(vals, dtype=torch.int32)
+    new[:, 1:] = (vals[:, 1:] != vals[:, :-1]).int()
+    assert torch.equal(nuniq.cpu(), new.sum(1).int().cpu())
+    pad = torch.zeros((F, nc * chunk), dtype=torch.int32, device=dev)
+    pad[:, :n] = new
+    per = pad.view(F, nc, chunk).sum(2)
+    excl = torch.cumsum(per, 1) - per
+    assert torch.equal(cnt.cpu(), excl.int().cpu())
+
+
 @pytest.mark.parametrize("C", [130, 300])
 def test_gpu_exact_many_classes_matches_host(C):
     """More than 128 classes on continuous features: labels leave the list
