@@ -320,10 +320,14 @@ def fit_tree(
                 # max_bins=None (exact): bin at 256 first -- one code byte, the
                 # histogram engines -- and take the presorted exact engine only
                 # when some feature turns out to have more than 256 values
+                from ..ops.exact_grower import MAX_ROWS
+
+                probe = max_bins is None and 0 < n < MAX_ROWS
                 prep = prepare(Xd, y, regression=regression,
                                max_bins=256 if max_bins is None else max_bins,
                                encode_labels=_encode_labels, encode_targets=_encode_targets,
-                               exponent=fixed_point_exponent, sync=_sync_prepare)
+                               exponent=fixed_point_exponent, sync=_sync_prepare,
+                               exact_probe=probe)
                 if prep.verify is not None:
                     # the bin kernel's flags are read after growth (see prepare): a
                     # sampled exact-mode feature that missed a value redoes the fit
@@ -351,6 +355,13 @@ def fit_tree(
                            "the GPU for this fit (>= 2^24 rows or >= 2^20 classes): using "
                            "256 quantile bins per feature")
             quantile_fallback = True
+            if probe:  # the probe left out the quantile edges and the codes: bin again
+                prep = prepare(Xd, y, regression=regression, max_bins=256,
+                               encode_labels=_encode_labels, encode_targets=_encode_targets,
+                               exponent=fixed_point_exponent, sync=True)
+                mapper, codes_rm, codes_fm, nb = (prep.mapper, prep.codes_rm, prep.codes_fm,
+                                                  prep.nbins)
+                yd, classes, y_exp, root = prep.y, prep.classes, prep.y_exp, prep.root
         lo, hi = comm.local_rows(n)
         if (lo, hi) != (0, n):  # data-parallel shard of a replicated input
             codes_rm = codes_rm[lo:hi].contiguous()

@@ -36,7 +36,7 @@ void launch_init_idx(hipStream_t, uint32_t*, const int32_t*, int, int64_t);
 void launch_predict(hipStream_t, const void*, bool, int64_t, int, const void*, const double*,
                     int32_t*);
 void launch_bin(hipStream_t, const void*, bool, int64_t, int, const void*, int, int,
-                const int32_t*, const uint8_t*, void*, int, void*, int, int32_t*);
+                const int32_t*, const uint8_t*, void*, int, void*, int, int32_t*, int);
 void launch_xlog2x(hipStream_t, double*, int64_t);
 void launch_label_count(hipStream_t, const int64_t*, int64_t, int64_t, int, uint32_t*, bool);
 void launch_label_encode(hipStream_t, const int64_t*, int64_t, int64_t, const int64_t*, int32_t*);
@@ -75,7 +75,7 @@ void launch_hist_reduce_tasks(hipStream_t, const int64_t*, int, const int64_t*, 
                               void*, int, int, int, const int32_t*, const int32_t*, bool);
 int edges_sample_rows(bool x64);
 void launch_edges(hipStream_t, const void*, bool, int64_t, int, int, int, void*, int32_t*,
-                  uint8_t*, double*);
+                  uint8_t*, double*, int);
 void launch_asm_rank(hipStream_t, const int32_t*, int64_t, int32_t*, int64_t*, int32_t*,
                      const uint8_t*);
 void launch_own_pack(hipStream_t, const int64_t*, int, uint8_t*, const int32_t*, const void*,
@@ -165,15 +165,16 @@ PYBIND11_MODULE(_hip, m) {
       "bin",
       [](uintptr_t s, uintptr_t X, bool x64, int64_t n, int F, uintptr_t edges, int Bmax,
          uintptr_t nbins, uintptr_t exact, uintptr_t codes_rm, int row_elems, uintptr_t codes_fm,
-         int cb, uintptr_t bad, int estride) {
+         int cb, uintptr_t bad, int estride, bool skip_inexact) {
         mt::launch_bin(S(s), P<void>(X), x64, n, F, P<void>(edges), Bmax,
                        estride > 0 ? estride : Bmax, P<int32_t>(nbins), P<uint8_t>(exact),
-                       P<void>(codes_rm), row_elems, P<void>(codes_fm), cb, P<int32_t>(bad));
+                       P<void>(codes_rm), row_elems, P<void>(codes_fm), cb, P<int32_t>(bad),
+                       skip_inexact ? 1 : 0);
       },
       py::arg("s"), py::arg("X"), py::arg("x64"), py::arg("n"), py::arg("F"), py::arg("edges"),
       py::arg("Bmax"), py::arg("nbins"), py::arg("exact"), py::arg("codes_rm"),
       py::arg("row_elems"), py::arg("codes_fm"), py::arg("cb"), py::arg("bad"),
-      py::arg("estride") = 0);
+      py::arg("estride") = 0, py::arg("skip_inexact") = false);
   m.def("finish_lds_bytes", &mt::finish_lds_bytes);
   m.def("finish_feature_tile", &mt::finish_feature_tile);
   m.def("finish", [](uintptr_t s, uintptr_t codes_rm, int64_t row_words, uintptr_t codes_fm,
@@ -337,13 +338,13 @@ PYBIND11_MODULE(_hip, m) {
   m.def(
       "edges",
       [](uintptr_t s, uintptr_t X, bool x64, int64_t n, int F, int rows, int limit,
-         uintptr_t edges, uintptr_t nbins, uintptr_t exact, uintptr_t pack) {
+         uintptr_t edges, uintptr_t nbins, uintptr_t exact, uintptr_t pack, bool probe) {
         mt::launch_edges(S(s), P<void>(X), x64, n, F, rows, limit, P<void>(edges),
-                         P<int32_t>(nbins), P<uint8_t>(exact), P<double>(pack));
+                         P<int32_t>(nbins), P<uint8_t>(exact), P<double>(pack), probe ? 1 : 0);
       },
       py::arg("s"), py::arg("X"), py::arg("x64"), py::arg("n"), py::arg("F"), py::arg("rows"),
       py::arg("limit"), py::arg("edges"), py::arg("nbins"), py::arg("exact"),
-      py::arg("pack") = 0);
+      py::arg("pack") = 0, py::arg("probe") = false);
   m.def("asm_rank", [](uintptr_t s, uintptr_t rec, int64_t npos, uintptr_t tile, uintptr_t total,
                        uintptr_t rank, uintptr_t mask) {
     mt::launch_asm_rank(S(s), P<int32_t>(rec), npos, P<int32_t>(tile), P<int64_t>(total),

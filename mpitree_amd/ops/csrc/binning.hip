@@ -58,7 +58,8 @@ __global__ __launch_bounds__(kEdgeThreads) void edges_kernel(const XT* __restric
                                                              int F, int s, int S, int limit,
                                                              XT* __restrict__ edges,
                                                              int32_t* __restrict__ nbins,
-                                                             uint8_t* __restrict__ exact) {
+                                                             uint8_t* __restrict__ exact,
+                                                             int probe) {
   using K = typename KeyOf<XT>::T;
   extern __shared__ __align__(16) uint8_t smem[];
   XT* key = reinterpret_cast<XT*>(smem);
@@ -116,6 +117,16 @@ __global__ __launch_bounds__(kEdgeThreads) void edges_kernel(const XT* __restric
   }
   __syncthreads();
   XT* out = edges + (int64_t)f * limit;
+  if (probe && s_over) {
+    // exact-threshold probe (core/fit.py, max_bins=None): more than `limit` values
+    // send the fit to the presorted-list engine, which needs no quantile edges
+    for (int i = tid; i < limit; i += kEdgeThreads) out[i] = (XT)__builtin_inf();
+    if (tid == 0) {
+      nbins[f] = limit;
+      exact[f] = 0;
+    }
+    return;
+  }
   if (!s_over) {
     // exact: sort the <= limit distinct values (compact them into key[] first)
     const int m = s_cnt;
@@ -223,6 +234,32 @@ __global__ __launch_bounds__(kEdgeThreads) void edges_kernel(const XT* __restric
   }
 }
 
+// skip_inexact (the exact-threshold probe): when any feature came back inexact the
+// fit runs the presorted-list engine and never reads the codes; a bin workgroup then
+// only checks its rows x features for non-finite values (flags bit 1).
+__device__ __forceinline__ bool bin_any_inexact(const uint8_t* __restrict__ exact, int F) {
+  __shared__ int s_any;
+  if (threadIdx.x == 0) s_any = 0;
+  __syncthreads();
+  for (int f = threadIdx.x; f < F; f += blockDim.x)
+    if (!exact[f]) s_any = 1;
+  __syncthreads();
+  return s_any != 0;
+}
+
+template <typename XT>
+__device__ __forceinline__ void bin_finite_only(const XT* __restrict__ X, int F, int64_t r0,
+                                                int64_t r1, int f0, int nf,
+                                                int32_t* __restrict__ flags) {
+  const int64_t total = (r1 - r0) * nf;
+  for (int64_t i = threadIdx.x; i < total; i += blockDim.x) {
+    const int64_t r = r0 + i / nf;
+    const int f = f0 + (int)(i % nf);
+    const XT v = X[r * F + f];
+    if (!(v - v == (XT)0)) atomicOr(&flags[f], 2);
+  }
+}
+
 constexpr int kBinRows = 256;
 constexpr int kBinFt = 16;                          // features per tile
 constexpr int kBinPer = kBinRows * kBinFt / 256;    // elements per thread
@@ -236,9 +273,15 @@ __global__ __launch_bounds__(256) void bin_kernel(const XT* __restrict__ X, int6
                                                   const uint8_t* __restrict__ exact,
                                                   CodeT* __restrict__ codes_rm, int row_elems,
                                                   CodeT* __restrict__ codes_fm,
-                                                  int32_t* __restrict__ flags) {
+                                                  int32_t* __restrict__ flags, int skip_inexact) {
   extern __shared__ __align__(16) uint8_t smem[];
   __shared__ int s_flag[kBinFt];
+  if (skip_inexact && bin_any_inexact(exact, F)) {
+    const int64_t a = blockIdx.x * (int64_t)kBinRows;
+    bin_finite_only<XT>(X, F, a, min<int64_t>(n, a + kBinRows), blockIdx.y * kBinFt,
+                        min(kBinFt, F - (int)blockIdx.y * kBinFt), flags);
+    return;
+  }
   __shared__ int32_t s_nb[kBinFt];
   __shared__ uint8_t s_ex[kBinFt];
   // [kBinFt][ES] when staged; the odd row stride ES spreads the 16 features'
@@ -336,8 +379,14 @@ __global__ __launch_bounds__(kBrThreads) void bin_rows_kernel(
     const float* __restrict__ X, int64_t n, int F, const float* __restrict__ edges, int Bmax,
     int estride, int steps0, const int32_t* __restrict__ nbins, const uint8_t* __restrict__ exact,
     uint8_t* __restrict__ codes_rm, int row_elems, uint8_t* __restrict__ codes_fm,
-    int32_t* __restrict__ flags, int64_t rows_per_block, int fm_vec) {
+    int32_t* __restrict__ flags, int64_t rows_per_block, int fm_vec, int skip_inexact) {
   extern __shared__ __align__(16) uint8_t smem[];
+  if (skip_inexact && bin_any_inexact(exact, F)) {
+    const int64_t a = blockIdx.x * rows_per_block;
+    bin_finite_only<float>(X, F, a, min<int64_t>(n, a + rows_per_block), blockIdx.y * kBrFt,
+                           min(kBrFt, F - (int)blockIdx.y * kBrFt), flags);
+    return;
+  }
   __shared__ int s_flag[kBrFt];
   __shared__ int s_aff[kBrFt];  // edges are e0, e0 + 1, ..., e0 + nb - 1 (integers)
   const int ES = Bmax | 1;
@@ -510,7 +559,8 @@ __global__ __launch_bounds__(256) void edges_pack_kernel(const XT* __restrict__ 
 }
 
 void launch_edges(hipStream_t stream, const void* X, bool x64, int64_t n, int F, int s, int limit,
-                  void* edges, int32_t* nbins, uint8_t* exact, double* pack) {
+                  void* edges, int32_t* nbins, uint8_t* exact, double* pack, int probe) {
+  if (probe && limit > kEdgeHash / 2) throw std::runtime_error("edges probe needs limit <= 1024");
   if (F <= 0) return;
   int S = 1;
   while (S < s) S <<= 1;
@@ -521,7 +571,7 @@ void launch_edges(hipStream_t stream, const void* X, bool x64, int64_t n, int F,
   MT_HIP_CHECK(mt_set_max_lds((const void*)edges_kernel<XT>,                              \
                                    (int)lds));     \
   hipLaunchKernelGGL(edges_kernel<XT>, dim3(F), dim3(kEdgeThreads), lds, stream, (const XT*)X, \
-                     n, F, s, S, limit, (XT*)edges, nbins, exact);                             \
+                     n, F, s, S, limit, (XT*)edges, nbins, exact, probe);                      \
   if (pack) {                                                                                  \
     const int64_t tot = (int64_t)F * limit + 2 * F;                                            \
     const int g = (int)std::min<int64_t>((tot + 255) / 256, 1024);                             \
@@ -539,7 +589,7 @@ void launch_edges(hipStream_t stream, const void* X, bool x64, int64_t n, int F,
 
 void launch_bin(hipStream_t stream, const void* X, bool x64, int64_t n, int F, const void* edges,
                 int Bmax, int estride, const int32_t* nbins, const uint8_t* exact, void* codes_rm,
-                int row_elems, void* codes_fm, int code_bytes, int32_t* flags) {
+                int row_elems, void* codes_fm, int code_bytes, int32_t* flags, int skip_inexact) {
   if (n <= 0) return;
   const int xb = x64 ? 8 : 4;
   const size_t edge_bytes = (size_t)kBinFt * (Bmax | 1) * xb;
@@ -563,7 +613,7 @@ void launch_bin(hipStream_t stream, const void* X, bool x64, int64_t n, int F, c
     hipLaunchKernelGGL(bin_rows_kernel, dim3(gx, (unsigned)tiles), dim3(kBrThreads), lds2, stream,
                        (const float*)X, n, F, (const float*)edges, Bmax, estride, steps0, nbins,
                        exact, (uint8_t*)codes_rm, row_elems, (uint8_t*)codes_fm, flags, rpb,
-                       fm_vec);
+                       fm_vec, skip_inexact);
     MT_HIP_CHECK(hipGetLastError());
     return;
   }
@@ -574,7 +624,7 @@ void launch_bin(hipStream_t stream, const void* X, bool x64, int64_t n, int F, c
                                      (int)lds));   \
     hipLaunchKernelGGL((bin_kernel<XT, CT, L>), grid, dim3(256), lds, stream, (const XT*)X, n, \
                        F, (const XT*)edges, Bmax, estride, steps0, nbins, exact, (CT*)codes_rm, \
-                       row_elems, (CT*)codes_fm, flags);                                       \
+                       row_elems, (CT*)codes_fm, flags, skip_inexact);                         \
   }
 #define MT_BIN2(XT, CT)      \
   if (lds_edges) {           \

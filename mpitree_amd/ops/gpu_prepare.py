@@ -169,7 +169,7 @@ class _Targets:
 
 
 def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
-            encode_targets, exponent, sync: bool = False) -> Prepared:
+            encode_targets, exponent, sync: bool = False, exact_probe: bool = False) -> Prepared:
     """Bin ``Xd`` (device, fp32/fp64) and encode ``y`` with two host syncs.
 
     ``encode_labels`` / ``encode_targets`` are the host encoders of
@@ -182,13 +182,17 @@ def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
     flags until the tree is assembled; ``Prepared.verify`` checks them then
     (non-finite input raises, an exact-mode sample that missed a value asks
     for a redo with ``sync=True``, which checks before growing).
+
+    ``exact_probe`` (exact-threshold requests): features past ``max_bins`` values
+    get no quantile edges and, when any feature has them, the bin pass writes no
+    codes (``DeviceBinning``); such a result is only for the presorted-list engine.
     """
     n = Xd.shape[0]
     dev = Xd.device
     stream = torch.cuda.current_stream(dev)
     lab = (_Targets(y, n, dev, encode_targets, exponent) if regression
            else _Labels(y, n, dev, encode_labels))
-    binning = DeviceBinning(Xd, max_bins)
+    binning = DeviceBinning(Xd, max_bins, probe=exact_probe)
     early = binning.early
     if early:  # <= 256 bins: the bin kernel reads the bin counts on the device
         tables = torch.cuda.Event()

@@ -126,8 +126,14 @@ class DeviceBinning:
     the stand-alone form.
     """
 
-    def __init__(self, X: torch.Tensor, max_bins=256, sample_rows: int | None = None):
+    def __init__(self, X: torch.Tensor, max_bins=256, sample_rows: int | None = None,
+                 probe: bool = False):
         hip = self.hip = native.hip()
+        # probe (exact-threshold requests): a feature whose sample exceeds the limit
+        # is only marked inexact (no quantile edges), and the early bin pass then
+        # only checks for non-finite values -- the fit goes to the presorted-list
+        # engine, which reads neither
+        self.probe = bool(probe)
         self.X = X
         n, F = self.n, self.F = X.shape
         dev = self.dev = X.device
@@ -141,7 +147,8 @@ class DeviceBinning:
         # fp64 [F*L edges | F counts | F exact flags]: the host's copy in one D2H
         self.pack = torch.empty(F * L + 2 * F, dtype=torch.float64, device=dev)
         hip.edges(_stream(), X.data_ptr(), self.x64, n, F, s, L, self.edges.data_ptr(),
-                  self.nb.data_ptr(), self.exact.data_ptr(), pack=self.pack.data_ptr())
+                  self.nb.data_ptr(), self.exact.data_ptr(), pack=self.pack.data_ptr(),
+                  probe=self.probe)
         self._host_pack = _pinned_copy(self.pack, "bin.pack")
         # the code buffers' shapes are known up front for <= 256 bins
         self._codes = self._alloc_codes(1) if L <= 256 else None
@@ -155,7 +162,7 @@ class DeviceBinning:
         flags = torch.zeros(self.F, dtype=torch.int32, device=self.dev)
         return cb, row_elems, codes_rm, codes_fm, flags
 
-    def _run_bin(self, edges_t, nb_t, exact_t, bmax):
+    def _run_bin(self, edges_t, nb_t, exact_t, bmax, skip_inexact=False):
         cb = 1 if bmax <= 256 else 2
         if self._codes is None or self._codes[0] != cb:
             self._codes = self._alloc_codes(cb)
@@ -163,7 +170,8 @@ class DeviceBinning:
         self._codes = None  # buffers belong to this pass
         self.hip.bin(_stream(), self.X.data_ptr(), self.x64, self.n, self.F, edges_t.data_ptr(),
                      bmax, nb_t.data_ptr(), exact_t.data_ptr(), codes_rm.data_ptr(), row_elems,
-                     codes_fm.data_ptr(), cb, flags.data_ptr(), estride=int(edges_t.stride(0)))
+                     codes_fm.data_ptr(), cb, flags.data_ptr(), estride=int(edges_t.stride(0)),
+                     skip_inexact=skip_inexact)
         return codes_rm, codes_fm, flags
 
     @property
@@ -177,7 +185,7 @@ class DeviceBinning:
         it reads the bin counts from the device, so the fit's first sync covers
         edges, codes and flags together."""
         self.codes_rm, self.codes_fm, flags = self._run_bin(self.edges, self.nb, self.exact,
-                                                            self.limit)
+                                                            self.limit, skip_inexact=self.probe)
         self._host_flags = _pinned_copy(flags, "bin.flags")
         self._flags_ready = torch.cuda.Event()
         self._flags_ready.record(torch.cuda.current_stream(self.dev))
@@ -198,7 +206,7 @@ class DeviceBinning:
         self.host_tables()
         if not getattr(self, "_launched", False):
             self.codes_rm, self.codes_fm, flags = self._run_bin(self.edges, self.nb, self.exact,
-                                                                self.bmax)
+                                                                self.bmax, skip_inexact=self.probe)
             self._host_flags = _pinned_copy(flags, "bin.flags")
             self._launched = True
 

@@ -653,6 +653,32 @@ def test_gpu_exact_engine_device_tensors_and_quantile_optin():
     assert q.fit_stats_["engine"].startswith("hip-") and q.fit_stats_["engine"] != "hip-exact"
 
 
+def test_gpu_exact_probe_fallback_and_nonfinite(monkeypatch):
+    """The exact-threshold probe skips quantile edges and codes when a feature has
+    more than 256 values; when the exact engine cannot take the fit (monkeypatched
+    here; >= 2^24 rows or >= 2^20 classes for real) the fit bins again and equals
+    the explicit 256-quantile-bin fit; a non-finite value still raises."""
+    from mpitree_amd.core import fit as fit_mod
+
+    rng = np.random.default_rng(11)
+    X = rng.normal(size=(20000, 6)).astype(np.float32)
+    X[:, 2] = rng.integers(0, 5, size=20000)
+    y = (X[:, 0] + X[:, 1] > 0).astype(np.int64) + (X[:, 2] > 2)
+    q = DecisionTreeClassifier(max_depth=8, max_bins=256, device="cuda").fit(X, y)
+    monkeypatch.setattr(fit_mod, "_exact_device_ok", lambda *a: False)
+    g = DecisionTreeClassifier(max_depth=8, device="cuda").fit(X, y)
+    assert g.fit_stats_["engine"] != "hip-exact"
+    assert g.tree_arrays_.equal(q.tree_arrays_)
+    monkeypatch.undo()
+    Xb = X.copy()
+    Xb[12345, 4] = np.nan
+    with pytest.raises(ValueError, match="NaN or infinity"):
+        DecisionTreeClassifier(device="cuda").fit(Xb, y)
+    Xb[12345, 4] = np.inf
+    with pytest.raises(ValueError, match="NaN or infinity"):
+        DecisionTreeClassifier(device="cuda").fit(Xb, y)
+
+
 @pytest.mark.parametrize("shape", [(2, 1, 2), (7, 3, 3), (150, 4, 3), (241, 1, 241), (600, 5, 40),
                                    (1024, 9, 2), (1000, 2, 300)])
 @pytest.mark.parametrize("crit", ["entropy", "gini"])
