@@ -52,7 +52,7 @@ int asm_tiles(int64_t P);
 void launch_grow_plan(hipStream_t, const PlanArgs&);
 size_t exact_setup_temp_bytes(int64_t, int);
 void exact_setup_sort(hipStream_t, const float*, int64_t, int, uint32_t*, uint32_t*, uint32_t*,
-                      uint32_t*, void*, size_t, int32_t*, int32_t*, int, int);
+                      uint32_t*, void*, size_t, int32_t*, int32_t*, int, int, const int32_t*);
 void bind_exact2(pybind11::module_& m);
 void bind_grow(pybind11::module_& m);
 int exact_setup_chunk();
@@ -308,13 +308,13 @@ PYBIND11_MODULE(_hip, m) {
   m.def("exact_setup_sort", [](uintptr_t s, uintptr_t X, int64_t n, int F, uintptr_t k0,
                                uintptr_t k1, uintptr_t r0, uintptr_t r1, uintptr_t temp,
                                size_t temp_bytes, uintptr_t cnt, uintptr_t nuniq, int xs,
-                               int f_lo) {
+                               int f_lo, uintptr_t ylab) {
     mt::exact_setup_sort(S(s), P<float>(X), n, F, P<uint32_t>(k0), P<uint32_t>(k1),
                          P<uint32_t>(r0), P<uint32_t>(r1), P<void>(temp), temp_bytes,
-                         P<int32_t>(cnt), P<int32_t>(nuniq), xs, f_lo);
+                         P<int32_t>(cnt), P<int32_t>(nuniq), xs, f_lo, P<const int32_t>(ylab));
   }, py::arg("s"), py::arg("X"), py::arg("n"), py::arg("F"), py::arg("k0"), py::arg("k1"),
      py::arg("r0"), py::arg("r1"), py::arg("temp"), py::arg("temp_bytes"), py::arg("cnt"),
-     py::arg("nuniq"), py::arg("xs") = 0, py::arg("f_lo") = 0);
+     py::arg("nuniq"), py::arg("xs") = 0, py::arg("f_lo") = 0, py::arg("ylab") = 0);
   m.def("fp_combine", [](uintptr_t s, uintptr_t g, int nranks, int KB, int R, uintptr_t dcount,
                          uintptr_t rec) {
     mt::launch_fp_combine(S(s), P<int64_t>(g), nranks, KB, R, P<int32_t>(dcount),

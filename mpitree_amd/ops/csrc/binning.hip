@@ -251,13 +251,13 @@ template <typename XT>
 __device__ __forceinline__ void bin_finite_only(const XT* __restrict__ X, int F, int64_t r0,
                                                 int64_t r1, int f0, int nf,
                                                 int32_t* __restrict__ flags) {
-  const int64_t total = (r1 - r0) * nf;
-  for (int64_t i = threadIdx.x; i < total; i += blockDim.x) {
-    const int64_t r = r0 + i / nf;
-    const int f = f0 + (int)(i % nf);
-    const XT v = X[r * F + f];
-    if (!(v - v == (XT)0)) atomicOr(&flags[f], 2);
-  }
+  // one wave per row at a time, lanes over the tile's features (contiguous reads)
+  const int lane = lane_id(), nwv = blockDim.x / kWave;
+  for (int64_t r = r0 + (threadIdx.x >> 6); r < r1; r += nwv)
+    for (int f = lane; f < nf; f += kWave) {
+      const XT v = X[r * F + f0 + f];
+      if (!(v - v == (XT)0)) atomicOr(&flags[f0 + f], 2);
+    }
 }
 
 constexpr int kBinRows = 256;

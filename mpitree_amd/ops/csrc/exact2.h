@@ -54,6 +54,7 @@ struct XeArgs {
   int64_t* pitems;     // [PMAX][4] {split j, segment start, chunk start, chunk count}
   int32_t* pfirst;     // [SMAX + 1]
   uint32_t* flag;      // [(n + 31) / 32] row-direction bits (1: left)
+  uint8_t* flagb;      // [(n + 31) / 32 * 32] row-direction bytes, packed into flag (or null)
   // single-pass scans (decoupled look-back): per (item, feature) status words
   // {tag : 30, state : 2 (1 aggregate, 2 inclusive prefix), value : 32}
   uint64_t* pstat;     // [PMAX][F_loc] left counts (partition)

@@ -1152,12 +1152,38 @@ __global__ __launch_bounds__(kXeThreads) void xe_flag_kernel(XeArgs a, XeLists c
       const int64_t p = c0 + i;
       const bool left = (p - s0) < nl;
       const uint32_t r = xe_row(Ef[p]);
-      if (left)
+      if (a.flagb) {  // plain byte stores; xe_flag_pack_kernel packs them
+        if (left || write_right) a.flagb[r] = left ? 1 : 0;
+      } else if (left) {
         atomicOr(a.flag + (r >> 5), 1u << (r & 31));
-      else if (write_right)
+      } else if (write_right) {
         atomicAnd(a.flag + (r >> 5), ~(1u << (r & 31)));
+      }
     }
   }
+}
+
+// flag[w] = the 32 row-direction bytes of rows 32w .. 32w + 31 as bits. (Device-wide
+// bit atomics are performed past the XCDs' non-coherent L2s: 1M of them took 41 us
+// per level; byte stores + this pass take a fraction of that.)
+__global__ __launch_bounds__(256) void xe_flag_pack_kernel(const uint8_t* __restrict__ flagb,
+                                                           uint32_t* __restrict__ flag,
+                                                           int64_t nw) {
+  const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= nw) return;
+  const uint4* src = reinterpret_cast<const uint4*>(flagb + w * 32);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint4 v = src[h];
+    const uint32_t q[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        bits |= (((q[k] >> (8 * b)) & 0xffu) != 0u ? 1u : 0u) << (h * 16 + k * 4 + b);
+  }
+  flag[w] = bits;
 }
 
 // xe_part: stable partition of every split segment of every feature list into
@@ -1203,7 +1229,26 @@ __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a,
   extern __shared__ uint32_t s_flag[];
   const int nw = kLdsFlags ? (int)((a.n + 31) >> 5) : 0;
   if constexpr (kLdsFlags) {
-    for (int i = threadIdx.x; i < nw; i += blockDim.x) s_flag[i] = a.flag[i];
+    // 16-byte loads, kU in flight per lane before the LDS stores: the copy is one
+    // round of L2 latency instead of one per 4 KB
+    constexpr int kU = 8;
+    const int nq = nw >> 2;
+    const uint4* src = reinterpret_cast<const uint4*>(a.flag);
+    uint4* dst = reinterpret_cast<uint4*>(s_flag);
+    for (int i0 = threadIdx.x; i0 < nq; i0 += (int)blockDim.x * kU) {
+      uint4 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int i = i0 + u * (int)blockDim.x;
+        if (i < nq) v[u] = src[i];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int i = i0 + u * (int)blockDim.x;
+        if (i < nq) dst[i] = v[u];
+      }
+    }
+    for (int i = (nq << 2) + threadIdx.x; i < nw; i += blockDim.x) s_flag[i] = a.flag[i];
     __syncthreads();
   }
   const uint32_t* fl = kLdsFlags ? s_flag : a.flag;
@@ -1213,7 +1258,20 @@ __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a,
   // tickets are claimed kXePartBatch at a time (one counter serialises its
   // atomics: ~10 ns each) and run in order, so the wave holding the smallest
   // unfinished ticket still never waits
-  const int batch = xe_part_batch(a.F_loc);
+  // a level with under 4 tickets per wave (the deep levels: a few long segments)
+  // claims smaller batches -- still divisors of F_loc -- so its tickets spread over
+  // the waves; a 16-ticket batch ran them one after another (~130 us for 8 items).
+  // (A batch that does not divide F_loc, e.g. 15 of 64, stalled the top levels 200x.)
+  const int64_t per_wave = total / ((int64_t)gridDim.x * kXePartWaves);
+  int batch = xe_part_batch(a.F_loc);
+  if (per_wave < 4) {
+    batch = 1;
+    for (int d = (int)std::max<int64_t>(per_wave, 1); d >= 1; --d)
+      if (a.F_loc % d == 0) {
+        batch = d;
+        break;
+      }
+  }
   for (int t = 0, tb = 0;; ++t) {
     if (t == tb) {
       int c = 0;
@@ -1504,7 +1562,7 @@ __global__ __launch_bounds__(256) void xe_rank_kernel(
   int64_t lo = 0, hi = n;  // first sorted position with value >= thr
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    if (xe_x(X, x64, F, rows[mid], R[0]) < thr) lo = mid + 1; else hi = mid;
+    if (xe_x(X, x64, F, xe_row(rows[mid]), R[0]) < thr) lo = mid + 1; else hi = mid;
   }
   R[1] = (int32_t)rank_at[(int64_t)f * n + lo];
   if (resolved) resolved[p] = 1;
@@ -1537,12 +1595,16 @@ __global__ __launch_bounds__(256) void xe_resolved_scatter_kernel(const int64_t*
 
 // ---------------------------------------------------------------------------
 // Setup: each feature's sorted 32-bit value keys with row ids (exact_setup.hip
-// sort) -> entries, value ranks by sorted position, duplicate flags. cbase: per-(feature,
-// chunk) first rank (exact_setup's count / scan of value changes).
+// sort; with packed labels the sort already carries them in bits 25..31 of the row
+// value) -> entries, value ranks by sorted position, duplicate flags. cbase: per-
+// (feature, chunk) first rank (exact_setup's count / scan of value changes).
+// One workgroup per (4096-entry chunk, feature): entry k * 256 + t of the chunk is
+// thread t's k-th; neighbours come from adjacent lanes, the ranks from 16 wave scans
+// and one workgroup barrier.
+constexpr int kXeEmitK = 16;  // entries per thread (chunk = 16 x 256)
 __global__ __launch_bounds__(256) void xe_emit_kernel(const uint32_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ rows, int64_t n,
-                                                      int nc, int chunk,
-                                                      const int32_t* __restrict__ cbase,
+                                                      int nc, const int32_t* __restrict__ cbase,
                                                       const int32_t* __restrict__ ylab,
                                                       const int64_t* __restrict__ yfix,
                                                       uint32_t* __restrict__ E,
@@ -1550,36 +1612,48 @@ __global__ __launch_bounds__(256) void xe_emit_kernel(const uint32_t* __restrict
                                                       uint32_t* __restrict__ rank_at) {
   const int f = blockIdx.y, c = blockIdx.x;
   const int64_t base = (int64_t)f * n;
-  const int64_t p0 = (int64_t)c * chunk;
-  const int64_t p1 = min<int64_t>(p0 + chunk, n);
-  __shared__ int32_t s_w[256 / kWave];
-  __shared__ int32_t s_carry;
-  const int lane = lane_id(), w = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_carry = cbase[(int64_t)f * nc + c];
-  __syncthreads();
-  for (int64_t b = p0; b < p1; b += 256) {
-    const int64_t p = b + threadIdx.x;
-    const bool in = p < p1;
+  const int64_t p0 = (int64_t)c * (kXeEmitK * 256);
+  __shared__ uint32_t s_w[kXeEmitK][256 / kWave];
+  const int tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  uint32_t incl[kXeEmitK];
+  uint32_t dupm = 0;  // bit k: entry k is a duplicate value
+#pragma unroll
+  for (int k = 0; k < kXeEmitK; ++k) {
+    const int64_t p = p0 + k * 256 + tid;
+    const bool in = p < n;
     const uint32_t key = in ? keys[base + p] : 0u;
-    const bool nw = in && (p == 0 || keys[base + p - 1] != key);
-    const bool dn = in && p + 1 < n && keys[base + p + 1] == key;
-    const bool dup = in && (!nw || dn);
-    const uint32_t incl = wave_incl_scan_dpp(nw ? 1u : 0u);
-    if (lane == kWave - 1) s_w[w] = (int32_t)incl;
-    __syncthreads();
-    int32_t off = s_carry;
-    for (int k = 0; k < w; ++k) off += s_w[k];
-    const int32_t rank = off + (int32_t)incl - 1;
-    if (in) {
-      const uint32_t row = rows[base + p];
-      const uint32_t lab = ylab ? (uint32_t)ylab[row] : 0u;
-      E[base + p] = row | ((uint32_t)dup << 24) | (lab << 25);
-      if (Y) Y[base + p] = yfix[row];
-      rank_at[base + p] = (uint32_t)rank;
+    uint32_t prev = __shfl_up(key, 1, kWave);
+    uint32_t next = __shfl_down(key, 1, kWave);
+    if (lane == 0 && in && p > 0) prev = keys[base + p - 1];
+    if (lane == kWave - 1 && p + 1 < n) next = keys[base + p + 1];
+    const bool nwv = in && (p == 0 || prev != key);
+    const bool dn = in && p + 1 < n && next == key;
+    if (in && (!nwv || dn)) dupm |= 1u << k;
+    incl[k] = wave_incl_scan_dpp(nwv ? 1u : 0u);
+    if (lane == kWave - 1) s_w[k][w] = incl[k];
+  }
+  __syncthreads();
+  int32_t run = cbase[(int64_t)f * nc + c];
+#pragma unroll
+  for (int k = 0; k < kXeEmitK; ++k) {
+    int32_t off = run;
+    int32_t tot = 0;
+#pragma unroll
+    for (int q = 0; q < 256 / kWave; ++q) {
+      const int32_t v = (int32_t)s_w[k][q];
+      off += q < w ? v : 0;
+      tot += v;
     }
-    __syncthreads();
-    if (threadIdx.x == 255) s_carry = off + (int32_t)incl;
-    __syncthreads();
+    run += tot;
+    const int64_t p = p0 + k * 256 + tid;
+    if (p < n) {
+      const uint32_t rv = rows[base + p];
+      const uint32_t row = rv & 0xFFFFFFu;
+      const uint32_t lab = ylab ? (uint32_t)ylab[row] << 25 : 0u;
+      E[base + p] = rv | (((dupm >> k) & 1u) << 24) | lab;
+      if (Y) Y[base + p] = yfix[row];
+      rank_at[base + p] = (uint32_t)(off + (int32_t)incl[k] - 1);
+    }
   }
 }
 
@@ -1649,6 +1723,12 @@ void xe_flag(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_boun
   hipLaunchKernelGGL(xe_flag_kernel, dim3(std::min(pitems_bound, 4096)), dim3(kXeThreads), 0, s, a,
                      cur, write_right);
   MT_HIP_CHECK(hipGetLastError());
+  if (a.flagb) {
+    const int64_t nw = (a.n + 31) / 32;
+    hipLaunchKernelGGL(xe_flag_pack_kernel, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s,
+                       a.flagb, a.flag, nw);
+    MT_HIP_CHECK(hipGetLastError());
+  }
 }
 
 void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_bound,
@@ -1748,7 +1828,8 @@ void xe_emit(hipStream_t s, const uint32_t* keys, const uint32_t* rows, int64_t 
              int nc, int chunk, const int32_t* cbase, const int32_t* ylab, const int64_t* yfix,
              uint32_t* E, int64_t* Y, uint32_t* rank_at) {
   if (n <= 0 || F_loc <= 0) return;
-  hipLaunchKernelGGL(xe_emit_kernel, dim3(nc, F_loc), dim3(256), 0, s, keys, rows, n, nc, chunk,
+  if (chunk != kXeEmitK * 256) throw std::runtime_error("xe_emit: chunk must be 4096");
+  hipLaunchKernelGGL(xe_emit_kernel, dim3(nc, F_loc), dim3(256), 0, s, keys, rows, n, nc,
                      cbase, ylab, yfix, E, Y, rank_at);
   MT_HIP_CHECK(hipGetLastError());
 }

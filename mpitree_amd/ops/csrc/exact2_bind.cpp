@@ -106,6 +106,7 @@ void bind_exact2(py::module_& m) {
         a.pitems = ptr<int64_t>(u("pitems"));
         a.pfirst = ptr<int32_t>(u("pfirst"));
         a.flag = ptr<uint32_t>(u("flag"));
+        a.flagb = d.contains("flagb") ? ptr<uint8_t>(u("flagb")) : nullptr;
         a.pstat = ptr<uint64_t>(u("pstat"));
         a.tick = ptr<int32_t>(u("tick"));
         a.tag = 1;

@@ -118,11 +118,12 @@ __global__ __launch_bounds__(kWave * kRsScanGroups) void xs_tile_scan_kernel(
 // One stable counting pass on digit (key >> shift) & 255: tile t (kNT * 16 keys) of
 // feature f puts its keys with digit d at the feature's digit base + pref[f][t][d]
 // onwards. Dynamic LDS: the tile's keys and rows in digit order (kNT * 128 bytes).
-template <int kNT, bool kFirst>
+template <int kNT, bool kFirst, bool kLab>
 __global__ __launch_bounds__(kNT) void xs_scatter_kernel(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ rin,
     uint32_t* __restrict__ kout, uint32_t* __restrict__ rout, int64_t n, int T, int shift,
-    const uint32_t* __restrict__ pref, const uint32_t* __restrict__ totals) {
+    const uint32_t* __restrict__ pref, const uint32_t* __restrict__ totals,
+    const int32_t* __restrict__ ylab) {
   constexpr int kW = kNT / kWave, kTile = kNT * kRsItems;
   extern __shared__ uint32_t s_dyn[];
   uint32_t* const s_key = s_dyn;
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(kNT) void xs_scatter_kernel(
     const int i = w * (kWave * kRsItems) + k * kWave + lane;
     const bool in = i < cnt;
     key[k] = in ? kin[base + p0 + i] : 0u;
-    if constexpr (kFirst) {
+    if constexpr (kFirst) {  // row ids (packed labels join them at the store)
       row[k] = (uint32_t)(p0 + i);
     } else {
       row[k] = in ? rin[base + p0 + i] : 0u;
@@ -214,7 +215,9 @@ __global__ __launch_bounds__(kNT) void xs_scatter_kernel(
     const uint32_t kk = s_key[i];
     const int64_t dst = base + (int64_t)(s_goff[(kk >> shift) & 255u] + i);
     kout[dst] = kk;
-    rout[dst] = s_row[i];
+    uint32_t rv = s_row[i];
+    if constexpr (kLab) rv |= (uint32_t)ylab[rv] << 25;  // (rows of this tile: a local read)
+    rout[dst] = rv;
   }
 }
 
@@ -280,14 +283,15 @@ size_t exact_setup_temp_bytes(int64_t n, int F) {
 template <int kNT>
 static void xs_sort_passes(hipStream_t stream, int64_t n, int F, int64_t T, uint32_t* keys0,
                            uint32_t* keys1, uint32_t* rows0, uint32_t* rows1, uint32_t* counts,
-                           uint32_t* totals) {
+                           uint32_t* totals, const int32_t* ylab) {
   // keys 1 -> 0 -> 1 -> 0 -> 1; rows (generated) -> 0 -> 1 -> 0 -> 1
   uint32_t* kb[2] = {keys0, keys1};
   uint32_t* rb[2] = {rows0, rows1};
   const unsigned grid = (unsigned)(F * T);
   const int lds = kNT * kRsItems * 2 * 4;
-  MT_HIP_CHECK(mt_set_max_lds((const void*)xs_scatter_kernel<kNT, true>, lds));
-  MT_HIP_CHECK(mt_set_max_lds((const void*)xs_scatter_kernel<kNT, false>, lds));
+  MT_HIP_CHECK(mt_set_max_lds((const void*)xs_scatter_kernel<kNT, true, false>, lds));
+  MT_HIP_CHECK(mt_set_max_lds((const void*)xs_scatter_kernel<kNT, true, true>, lds));
+  MT_HIP_CHECK(mt_set_max_lds((const void*)xs_scatter_kernel<kNT, false, false>, lds));
   for (int q = 0; q < kRsPasses; ++q) {
     const int src = (q & 1) ? 0 : 1, dst = src ^ 1;
     hipLaunchKernelGGL(xs_tile_count_kernel<kNT>, dim3(grid), dim3(kNT), 0, stream, kb[src], n,
@@ -296,12 +300,18 @@ static void xs_sort_passes(hipStream_t stream, int64_t n, int F, int64_t T, uint
     hipLaunchKernelGGL(xs_tile_scan_kernel, dim3(F, 256 / kWave), dim3(kWave * kRsScanGroups), 0,
                        stream, counts, (int)T, totals);
     MT_HIP_CHECK(hipGetLastError());
-    if (q == 0) {
-      hipLaunchKernelGGL((xs_scatter_kernel<kNT, true>), dim3(grid), dim3(kNT), lds, stream,
-                         kb[src], nullptr, kb[dst], rb[dst], n, (int)T, 8 * q, counts, totals);
+    if (q == 0 && ylab) {
+      hipLaunchKernelGGL((xs_scatter_kernel<kNT, true, true>), dim3(grid), dim3(kNT), lds, stream,
+                         kb[src], nullptr, kb[dst], rb[dst], n, (int)T, 8 * q, counts, totals,
+                         ylab);
+    } else if (q == 0) {
+      hipLaunchKernelGGL((xs_scatter_kernel<kNT, true, false>), dim3(grid), dim3(kNT), lds,
+                         stream, kb[src], nullptr, kb[dst], rb[dst], n, (int)T, 8 * q, counts,
+                         totals, nullptr);
     } else {
-      hipLaunchKernelGGL((xs_scatter_kernel<kNT, false>), dim3(grid), dim3(kNT), lds, stream,
-                         kb[src], rb[src], kb[dst], rb[dst], n, (int)T, 8 * q, counts, totals);
+      hipLaunchKernelGGL((xs_scatter_kernel<kNT, false, false>), dim3(grid), dim3(kNT), lds, stream,
+                         kb[src], rb[src], kb[dst], rb[dst], n, (int)T, 8 * q, counts, totals,
+                         nullptr);
     }
     MT_HIP_CHECK(hipGetLastError());
   }
@@ -309,10 +319,12 @@ static void xs_sort_passes(hipStream_t stream, int64_t n, int F, int64_t T, uint
 
 // Phase 1 (before the host learns the largest unique count): keys, sort, counts.
 // keys/rows: two u32 buffers each of n * F (ping-pong; the result is in [1]);
-// cnt: int32 [F][nc]; nuniq: int32 [F].
+// cnt: int32 [F][nc]; nuniq: int32 [F]; ylab (or null): labels < 128 carried in bits
+// 25..31 of the sorted row values.
 void exact_setup_sort(hipStream_t stream, const float* X, int64_t n, int F, uint32_t* keys0,
                       uint32_t* keys1, uint32_t* rows0, uint32_t* rows1, void* temp,
-                      size_t temp_bytes, int32_t* cnt, int32_t* nuniq, int xs, int f_lo) {
+                      size_t temp_bytes, int32_t* cnt, int32_t* nuniq, int xs, int f_lo,
+                      const int32_t* ylab) {
   if (xs <= 0) xs = F;
   if (n <= 0 || F <= 0) return;
   if (n >= (int64_t)1 << 24) throw std::runtime_error("exact setup: rows < 2^24");
@@ -326,11 +338,11 @@ void exact_setup_sort(hipStream_t stream, const float* X, int64_t n, int F, uint
   hipLaunchKernelGGL(xs_keys_kernel, tg, dim3(kXsThreads), 0, stream, X, n, F, xs, f_lo, keys1);
   MT_HIP_CHECK(hipGetLastError());
   if (xs_nt() == 256) {
-    xs_sort_passes<256>(stream, n, F, T, keys0, keys1, rows0, rows1, counts, totals);
+    xs_sort_passes<256>(stream, n, F, T, keys0, keys1, rows0, rows1, counts, totals, ylab);
   } else if (xs_nt() == 1024) {
-    xs_sort_passes<1024>(stream, n, F, T, keys0, keys1, rows0, rows1, counts, totals);
+    xs_sort_passes<1024>(stream, n, F, T, keys0, keys1, rows0, rows1, counts, totals, ylab);
   } else {
-    xs_sort_passes<512>(stream, n, F, T, keys0, keys1, rows0, rows1, counts, totals);
+    xs_sort_passes<512>(stream, n, F, T, keys0, keys1, rows0, rows1, counts, totals, ylab);
   }
   const int nc = (int)((n + kXsChunk - 1) / kXsChunk);
   hipLaunchKernelGGL(xs_count_kernel, dim3(nc, F), dim3(kXsThreads), 0, stream, keys1, n, nc,

@@ -124,9 +124,10 @@ class ExactGrower:
             hip.exact_setup_sort(s, Xd.data_ptr(), n, F_loc, keys[0].data_ptr(),
                                  keys[1].data_ptr(), rows[0].data_ptr(), rows[1].data_ptr(),
                                  temp.data_ptr(), tb, cnt.data_ptr(), nuniq.data_ptr(),
-                                 xs=F, f_lo=f_lo)
+                                 xs=F, f_lo=f_lo, ylab=ylab)
+            # (the sort carried the packed labels: the emit gathers none)
             hip.xe_emit(s, keys[1].data_ptr(), rows[1].data_ptr(), n, F_loc, nc, chunk,
-                        cnt.data_ptr(), ylab, yf, E[0].data_ptr(),
+                        cnt.data_ptr(), 0, yf, E[0].data_ptr(),
                         Y[0].data_ptr() if reg else 0, rank_at.data_ptr())
             root_rows = rows[1]
             del keys, rows, temp, cnt, nuniq  # (stream-ordered frees)
@@ -261,6 +262,7 @@ class ExactGrower:
                 pitems=torch.empty((IMAX, 4), **i64),
                 pfirst=torch.empty(KMAX + 1, **i32),
                 flag=torch.empty((n + 31) // 32, dtype=torch.int32, device=dev),
+                flagb=torch.zeros((n + 31) // 32 * 32, dtype=torch.uint8, device=dev),
                 # look-back status words (tagged per fit and level: zeroed once)
                 pstat=torch.zeros((2 * IMAX, F_loc), **i64),  # (2 wave units per item)
                 sitem=torch.empty((KMAX, 2), **i32),  # (partition-counted chunk totals)
@@ -284,6 +286,8 @@ class ExactGrower:
             gthr=ptr["gthr"],
             rec=ptr["rec"], split=ptr["split"],
             pitems=ptr["pitems"], pfirst=ptr["pfirst"], flag=ptr["flag"],
+            **({"flagb": ptr["flagb"]} if os.environ.get("MPITREE_EXACT_FLAG_BYTES", "1") != "0"
+               else {}),
             pstat=ptr["pstat"], tick=ptr["tick"], pos_rec=be.pos_rec.data_ptr(),
             **({"sitem": ptr["sitem"]} if os.environ.get("MPITREE_EXACT_PART_TOT", "1") != "0"
                else {}),
@@ -321,6 +325,7 @@ class ExactGrower:
             _step(dev, "plan")
             if P > 1:  # the split feature's owner sets the left rows; summed over ranks
                 ws["flag"].zero_()
+                ws["flagb"].zero_()
                 ctx.flag(s(), lvl, ib, 0)
                 comm.all_reduce_device(ws["flag"])
                 comm_bytes.append(int(getattr(comm, "bytes_communicated", 0) - b0))
