@@ -116,7 +116,8 @@ void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems
 void xe_local_codes(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const int64_t* Y0,
                     const int64_t* Y1, const void* X, int x64, int F, int fg_lo, int64_t n,
                     int F_loc, int f_lo, const int64_t* jobs, int J, int JW, uint8_t* codes_fm,
-                    uint32_t* ent, int64_t* yv, const int32_t* ylab);
+                    uint8_t* codes_rm, int row_bytes, uint32_t* ent, int64_t* yv,
+                    const int32_t* ylab);
 void xe_codes_rm(hipStream_t s, const uint8_t* codes_fm, int64_t n, int F, int row_bytes,
                  const int64_t* jobs, int J, int JW, uint8_t* codes_rm);
 void xe_fix(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const void* X, int x64, int F,

@@ -1425,15 +1425,20 @@ __global__ void xe_init_kernel(XeLists L, int64_t n, int Cs, const int64_t* __re
 // features: codes_fm[f_lo + f][v]; the label-packed entries ent[v] (classes)
 // (classification) or the row ids ent[v] = v and targets yv[v] (regression).
 // jobs: int64 [J][W] = {start, rows, depth, position, list buffer, ...}
+template <typename XT>
 __global__ __launch_bounds__(kXeLocalMax) void xe_local_codes_kernel(
     const uint32_t* __restrict__ E0, const uint32_t* __restrict__ E1,
-    const int64_t* __restrict__ Y0, const int64_t* __restrict__ Y1, const void* __restrict__ X,
-    int x64, int F, int fg_lo, int64_t n, int F_loc, int f_lo,
+    const int64_t* __restrict__ Y0, const int64_t* __restrict__ Y1, const XT* __restrict__ X,
+    int F, int fg_lo, int64_t n, int F_loc, int f_lo,
     const int64_t* __restrict__ jobs, int JW, uint8_t* __restrict__ codes_fm,
+    uint8_t* __restrict__ codes_rm, int row_bytes,
     uint32_t* __restrict__ ent, int64_t* __restrict__ yv, const int32_t* __restrict__ ylab) {
+  // kFt features per pass: the codes of the pass in LDS (both output layouts are
+  // written from there); values are read from X only where two adjacent entries
+  // are both duplicated values (rare on continuous data)
+  constexpr int kFt = 32;
+  __shared__ uint8_t cb[kFt * kXeLocalMax];  // [kFt][kXeLocalMax] codes by virtual row
   __shared__ uint32_t s_row[kXeLocalMax];
-  __shared__ uint32_t s_w[kXeLocalMax / kWave];
-  __shared__ uint32_t s_e[kXeLocalMax + 1];
   const int64_t* J = jobs + (int64_t)blockIdx.x * JW;
   const int64_t s = J[0];
   const int m = (int)J[1];
@@ -1458,12 +1463,14 @@ __global__ __launch_bounds__(kXeLocalMax) void xe_local_codes_kernel(
       __syncthreads();
     }
   }
-  // virtual index of a row: binary search in s_row[0, m)
+  // virtual index of a row: binary search in s_row[0, m) -- a fixed 8 steps, so the
+  // searches of a wave's entries unroll and overlap
   auto vidx = [&](uint32_t row) -> int {
-    int lo = 0, hi = m;
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (s_row[mid] <= row) lo = mid; else hi = mid;
+    int lo = 0;
+#pragma unroll
+    for (int step = kXeLocalMax / 2; step > 0; step >>= 1) {
+      const int mid = lo + step;
+      if (mid < m && s_row[mid] <= row) lo = mid;
     }
     return lo;
   };
@@ -1477,33 +1484,92 @@ __global__ __launch_bounds__(kXeLocalMax) void xe_local_codes_kernel(
       ent[s + v] = (lab << 24) | (uint32_t)(s + v);  // (finisher jobs: <= 256 classes)
     }
   }
-  for (int f = 0; f < F_loc; ++f) {
-    const uint32_t e = t < m ? E[(int64_t)f * n + s + t] : 0xFFFFFFFFu;
-    s_e[t] = e;
-    __syncthreads();
-    // offset of the first entry of this value: inclusive max-scan of run starts
-    bool start = t == 0;
-    if (t > 0 && t < m) {
-      const uint32_t pe = s_e[t - 1];
-      start = !(xe_dup(e) && xe_dup(pe)) ||
-              xe_x(X, x64, F, xe_row(e), fg_lo + f) != xe_x(X, x64, F, xe_row(pe), fg_lo + f);
-    }
-    uint32_t b = (t < m && start) ? (uint32_t)t : 0u;
+  for (int f0 = 0; f0 < F_loc; f0 += kFt) {
+    const int nf = min(kFt, F_loc - f0);
+    // one wave per feature, 4 consecutive entries per lane: the offset of the first
+    // entry of each value is an inclusive max-scan of the run starts. The wave's
+    // kFw features load their entries and virtual rows first (independent chains).
+    constexpr int kFw = kFt / (kXeLocalMax / kWave);
+    constexpr int kPer = kXeLocalMax / kWave;  // entries per lane (4)
+    uint32_t e[kFw][kPer];
+    int vv[kFw][kPer];
 #pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-      const uint32_t o = __shfl_up(b, d, kWave);
-      if (lane >= d) b = max(b, o);
+    for (int r = 0; r < kFw; ++r) {
+      const int k = w + r * (kXeLocalMax / kWave);
+      const uint32_t* Ef = E + (int64_t)(f0 + k) * n + s;
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        const int i = lane * kPer + q;
+        e[r][q] = (k < nf && i < m) ? Ef[i] : 0xFFFFFFFFu;
+      }
     }
-    if (lane == kWave - 1) s_w[w] = b;
+#pragma unroll
+    for (int r = 0; r < kFw; ++r)
+#pragma unroll
+      for (int q = 0; q < kPer; ++q)
+        vv[r][q] = e[r][q] != 0xFFFFFFFFu ? vidx(xe_row(e[r][q])) : 0;
+#pragma unroll
+    for (int r = 0; r < kFw; ++r) {
+      const int k = w + r * (kXeLocalMax / kWave);
+      if (k >= nf) break;  // (wave-uniform)
+      const XT* xk = X + fg_lo + f0 + k;
+      const uint32_t pe = __shfl_up(e[r][kPer - 1], 1, kWave);
+      uint32_t b = 0;
+      uint32_t bq[kPer];
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        const int i = lane * kPer + q;
+        const uint32_t ep = q == 0 ? pe : e[r][q - 1];
+        const bool start =
+            i == 0 || (i < m && (!(xe_dup(e[r][q]) && xe_dup(ep)) ||
+                                 xk[(int64_t)xe_row(e[r][q]) * F] != xk[(int64_t)xe_row(ep) * F]));
+        if (i < m && start) b = (uint32_t)i;
+        bq[q] = b;  // (max so far: starts ascend within the lane)
+      }
+      // exclusive max over the lower lanes
+      uint32_t x = b;
+#pragma unroll
+      for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t o = __shfl_up(x, d, kWave);
+        if (lane >= d) x = max(x, o);
+      }
+      uint32_t ex = __shfl_up(x, 1, kWave);
+      if (lane == 0) ex = 0;
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        const int i = lane * kPer + q;
+        if (i < m) cb[k * kXeLocalMax + vv[r][q]] = (uint8_t)max(ex, bq[q]);
+      }
+    }
     __syncthreads();
-    for (int k = 0; k < w; ++k) b = max(b, s_w[k]);
-    if (t < m) codes_fm[(int64_t)(f_lo + f) * n + s + vidx(xe_row(e))] = (uint8_t)b;
+    for (int i = t; i < nf * m; i += kXeLocalMax) {
+      const int k = i / m, v = i - k * m;
+      codes_fm[(int64_t)(f_lo + f0 + k) * n + s + v] = cb[k * kXeLocalMax + v];
+    }
+    if (codes_rm) {  // one-rank fits: the row-major codes too (4 features a word)
+      const int wpr = (nf + 3) >> 2;
+      for (int i = t; i < m * wpr; i += kXeLocalMax) {
+        const int v = i / wpr, q = i - v * wpr;
+        uint32_t word = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if (4 * q + b < nf) word |= (uint32_t)cb[(4 * q + b) * kXeLocalMax + v] << (8 * b);
+        *reinterpret_cast<uint32_t*>(codes_rm + (s + v) * row_bytes + f0 + 4 * q) = word;
+      }
+      if (f0 + kFt >= F_loc)  // zero padding bytes past the last feature
+        for (int i = t; i < m * (row_bytes - F_loc); i += kXeLocalMax) {
+          const int pw = row_bytes - F_loc;
+          const int v = i / pw, c = i - v * pw;
+          codes_rm[(s + v) * row_bytes + F_loc + c] = 0;
+        }
+    }
     __syncthreads();
   }
 }
 
 // Row-major copy of the finisher codes: codes_rm[v][f] for every virtual row of
-// every job (the finisher reads both layouts).
+// every job (the finisher reads both layouts; feature-parallel fits, after the
+// codes all-gather -- one-rank fits write it from xe_local_codes_kernel).
 __global__ __launch_bounds__(256) void xe_codes_rm_kernel(const uint8_t* __restrict__ codes_fm,
                                                           int64_t n, int F, int row_bytes,
                                                           const int64_t* __restrict__ jobs,
@@ -1773,10 +1839,20 @@ void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems
 void xe_local_codes(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const int64_t* Y0,
                     const int64_t* Y1, const void* X, int x64, int F, int fg_lo, int64_t n,
                     int F_loc, int f_lo, const int64_t* jobs, int J, int JW, uint8_t* codes_fm,
-                    uint32_t* ent, int64_t* yv, const int32_t* ylab) {
+                    uint8_t* codes_rm, int row_bytes, uint32_t* ent, int64_t* yv,
+                    const int32_t* ylab) {
   if (J <= 0) return;
-  hipLaunchKernelGGL(xe_local_codes_kernel, dim3(J), dim3(kXeLocalMax), 0, s, E0, E1, Y0, Y1, X,
-                     x64, F, fg_lo, n, F_loc, f_lo, jobs, JW, codes_fm, ent, yv, ylab);
+  if (codes_rm && (f_lo != 0 || (row_bytes & 3) || row_bytes < F_loc))
+    throw std::runtime_error("xe_local_codes: row-major codes need f_lo = 0, 4-byte rows");
+  if (x64) {
+    hipLaunchKernelGGL(xe_local_codes_kernel<double>, dim3(J), dim3(kXeLocalMax), 0, s, E0, E1,
+                       Y0, Y1, (const double*)X, F, fg_lo, n, F_loc, f_lo, jobs, JW, codes_fm,
+                       codes_rm, row_bytes, ent, yv, ylab);
+  } else {
+    hipLaunchKernelGGL(xe_local_codes_kernel<float>, dim3(J), dim3(kXeLocalMax), 0, s, E0, E1,
+                       Y0, Y1, (const float*)X, F, fg_lo, n, F_loc, f_lo, jobs, JW, codes_fm,
+                       codes_rm, row_bytes, ent, yv, ylab);
+  }
   MT_HIP_CHECK(hipGetLastError());
 }
 

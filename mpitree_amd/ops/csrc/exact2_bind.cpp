@@ -164,15 +164,18 @@ void bind_exact2(py::module_& m) {
   m.def("xe_local_codes", [](uintptr_t s, uintptr_t E0, uintptr_t E1, uintptr_t Y0, uintptr_t Y1,
                              uintptr_t X, int x64, int F, int fg_lo, int64_t n, int F_loc,
                              int f_lo, uintptr_t jobs, int J, int JW, uintptr_t codes_fm,
-                             uintptr_t ent, uintptr_t yv, uintptr_t ylab) {
+                             uintptr_t ent, uintptr_t yv, uintptr_t ylab, uintptr_t codes_rm,
+                             int row_bytes) {
     xe_local_codes(stream_of(s), ptr<uint32_t>(E0), ptr<uint32_t>(E1), ptr<int64_t>(Y0),
                    ptr<int64_t>(Y1), ptr<void>(X), x64, F, fg_lo, n, F_loc, f_lo,
-                   ptr<int64_t>(jobs), J, JW, ptr<uint8_t>(codes_fm), ptr<uint32_t>(ent),
+                   ptr<int64_t>(jobs), J, JW, ptr<uint8_t>(codes_fm), ptr<uint8_t>(codes_rm),
+                   row_bytes, ptr<uint32_t>(ent),
                    ptr<int64_t>(yv), ptr<int32_t>(ylab));
   }, py::arg("s"), py::arg("E0"), py::arg("E1"), py::arg("Y0"), py::arg("Y1"), py::arg("X"),
      py::arg("x64"), py::arg("F"), py::arg("fg_lo"), py::arg("n"), py::arg("F_loc"),
      py::arg("f_lo"), py::arg("jobs"), py::arg("J"), py::arg("JW"), py::arg("codes_fm"),
-     py::arg("ent"), py::arg("yv"), py::arg("ylab") = 0);
+     py::arg("ent"), py::arg("yv"), py::arg("ylab") = 0, py::arg("codes_rm") = 0,
+     py::arg("row_bytes") = 0);
   m.def("xe_codes_rm", [](uintptr_t s, uintptr_t codes_fm, int64_t n, int F, int row_bytes,
                           uintptr_t jobs, int J, int JW, uintptr_t codes_rm) {
     xe_codes_rm(stream_of(s), ptr<uint8_t>(codes_fm), n, F, row_bytes, ptr<int64_t>(jobs), J, JW,

@@ -454,14 +454,15 @@ class ExactGrower:
                            Xd.data_ptr(), x64, F, f_lo, n, F_loc, 0, jobs.data_ptr(), J, JW,
                            fm_out.data_ptr(), loc["ent"].data_ptr(),
                            loc["yv"].data_ptr() if reg else 0,
-                           0 if reg or _packed_labels(self.C) else self._y32.data_ptr())
+                           0 if reg or _packed_labels(self.C) else self._y32.data_ptr(),
+                           codes_rm=0 if P > 1 else loc["rm"].data_ptr(), row_bytes=rb)
         if P > 1:  # every rank's feature block of the codes -> all features on every rank
             g = loc["gather"]
             comm.all_gather_device(g.view(-1), loc["blk"].view(-1))
             for r, (lo, hi) in enumerate(blocks):
                 loc["fm"][lo:hi].copy_(g[r, : hi - lo])
-        hip.xe_codes_rm(s(), loc["fm"].data_ptr(), n, F, rb, jobs.data_ptr(), J, JW,
-                        loc["rm"].data_ptr())
+            hip.xe_codes_rm(s(), loc["fm"].data_ptr(), n, F, rb, jobs.data_ptr(), J, JW,
+                            loc["rm"].data_ptr())
         # the finisher reads the binned engine's fields: point them at the local codes
         be.codes_rm, be.codes_fm = loc["rm"], loc["fm"]
         be.row_elems, be.cb, be.B, be.nbins = rb, 1, 256, loc["nbins"]
