@@ -347,10 +347,13 @@ def fit_tree(
                 if checkpoint is not None:  # the same tree, just no mid-fit state
                     logger.warning("the exact-threshold GPU engine keeps no level "
                                    "checkpoint: fitting without one")
+                # (the bin pass's flags -- non-finite input -- are read after the fit,
+                # so the host enqueues the setup without waiting for them)
+                res = _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t0,
+                                        t_start, F, regression)
                 if prep.verify is not None and not prep.verify():
                     return fit_tree(X, y, **redo)
-                return _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t0,
-                                         t_start, F, regression)
+                return res
             logger.warning("exact thresholds on > 256-value features are not available on "
                            "the GPU for this fit (>= 2^24 rows or >= 2^20 classes): using "
                            "256 quantile bins per feature")

@@ -251,12 +251,22 @@ template <typename XT>
 __device__ __forceinline__ void bin_finite_only(const XT* __restrict__ X, int F, int64_t r0,
                                                 int64_t r1, int f0, int nf,
                                                 int32_t* __restrict__ flags) {
-  // one wave per row at a time, lanes over the tile's features (contiguous reads)
+  // one wave per row, lanes over the tile's features (contiguous reads), kU rows'
+  // loads in flight per lane before any check
+  constexpr int kU = 8;
   const int lane = lane_id(), nwv = blockDim.x / kWave;
-  for (int64_t r = r0 + (threadIdx.x >> 6); r < r1; r += nwv)
+  for (int64_t rb = r0 + (threadIdx.x >> 6); rb < r1; rb += (int64_t)nwv * kU)
     for (int f = lane; f < nf; f += kWave) {
-      const XT v = X[r * F + f0 + f];
-      if (!(v - v == (XT)0)) atomicOr(&flags[f0 + f], 2);
+      XT v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t r = rb + (int64_t)u * nwv;
+        v[u] = r < r1 ? X[r * F + f0 + f] : (XT)0;
+      }
+      bool bad = false;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) bad |= !(v[u] - v[u] == (XT)0);
+      if (bad) atomicOr(&flags[f0 + f], 2);
     }
 }
 
