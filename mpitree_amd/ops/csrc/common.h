@@ -39,6 +39,29 @@ constexpr int kWave = 64;  // CDNA wavefront width
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 
+// Work claims of a wave: `batch` consecutive items per atomic on one counter (each
+// atomic on a shared counter serialises, ~10 ns), and no claim after a batch that
+// reached the end. Returns the next item; >= K: done.
+struct WaveClaim {
+  int k = 0, end = 0;
+};
+__device__ __forceinline__ int wave_claim_next(WaveClaim& c, int32_t* counter, int K, int batch) {
+  if (c.k >= c.end) {
+    if (c.end >= K && c.end > 0) return K;
+    int v = 0;
+    if ((threadIdx.x & (kWave - 1)) == 0) v = atomicAdd(counter, batch);
+    v = __builtin_amdgcn_readfirstlane(v);
+    c.k = v;
+    c.end = v + batch;
+  }
+  return c.k++;
+}
+// Items per claim: up to 4 while every wave still gets >= 4 claims.
+__device__ __forceinline__ int wave_claim_batch(int K) {
+  const int waves = (int)(gridDim.x * (blockDim.x / kWave));
+  return max(1, min(4, K / max(1, 4 * waves)));
+}
+
 // Inclusive wave64 prefix sum (Hillis-Steele over __shfl_up).
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
   const int lane = lane_id();

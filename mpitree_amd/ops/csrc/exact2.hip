@@ -1274,6 +1274,9 @@ __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a,
   }
   for (int t = 0, tb = 0;; ++t) {
     if (t == tb) {
+      // a wave whose last batch reached the end claims nothing more (a relaxed
+      // load of the counter before each claim measured slower: 14.9 -> 16.6 ms)
+      if (tb >= total && tb > 0) break;
       int c = 0;
       if (lane == 0) c = atomicAdd(a.tick + 1, batch);
       t = __builtin_amdgcn_readfirstlane(c);

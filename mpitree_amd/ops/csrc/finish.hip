@@ -1113,10 +1113,10 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
   const int nw = (int)min<int64_t>(row_words, kTinyMaxF / 4);
   uint32_t* my_codes = &s_codes[wave][lane * kTinyStride];
   const uint8_t* my_bytes = reinterpret_cast<const uint8_t*>(my_codes);
+  WaveClaim claim;
+  const int claim_batch = wave_claim_batch(K);
   for (;;) {
-    int k = 0;
-    if (lane == 0) k = atomicAdd(tiny_counter, 1);
-    k = __builtin_amdgcn_readfirstlane(k);
+    const int k = wave_claim_next(claim, tiny_counter, K, claim_batch);
     if (k >= K) break;
     const int64_t* rec = tiny + (int64_t)k * 8;
     const int64_t start = rec[0];
@@ -1801,10 +1801,10 @@ __global__ __launch_bounds__(kW * kWave) void finish_tiny_sorted_kernel(
   for (int a = threadIdx.x; a <= kTinyRows; a += blockDim.x) s_hrow[a] = 8u * (uint32_t)tiny_h_idx(a, 0);
   __syncthreads();
   const int K = *tiny_count;
+  WaveClaim claim;
+  const int claim_batch = wave_claim_batch(K);
   for (;;) {
-    int k = 0;
-    if (lane == 0) k = atomicAdd(tiny_counter, 1);
-    k = __builtin_amdgcn_readfirstlane(k);
+    const int k = wave_claim_next(claim, tiny_counter, K, claim_batch);
     if (k >= K) break;
     const int64_t* rec = tiny + (int64_t)k * 8;
     tiny_sorted_subtree<CodeT>(codes_rm, row_words, rec[3] ? buf1 : buf0, y, rl, rec[0], (int)rec[1],

@@ -503,10 +503,10 @@ __global__ __launch_bounds__(256) void finish_tiny_reg_kernel(
   const int K = *tiny_count;
   const int nwords = (F + 3) >> 2;
   const int mslw = (int)(msl < 65 ? msl : 65);
+  WaveClaim claim;
+  const int claim_batch = wave_claim_batch(K);
   for (;;) {
-    int k = 0;
-    if (lane == 0) k = atomicAdd(tiny_counter, 1);
-    k = __builtin_amdgcn_readfirstlane(k);
+    const int k = wave_claim_next(claim, tiny_counter, K, claim_batch);
     if (k >= K) break;
     const int64_t* rec = tiny + (int64_t)k * 8;
     const int64_t start = rec[0];
