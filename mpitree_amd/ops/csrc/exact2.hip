@@ -1218,9 +1218,10 @@ __device__ __forceinline__ int xe_part_batch(int F_loc) {
   if (F_loc <= kXePartBatch) return F_loc;
   for (int d = kXePartBatch; d >= 4; --d)
     if (F_loc % d == 0) return d;
-  // no divisor: a claim of kXePartBatch < F_loc tickets still never holds a
-  // ticket and the one it depends on (F_loc earlier); it only straddles two
-  // sub-chunks, which costs nothing like 16x the counter atomics
+  // no divisor: tickets run over F_loc rounded up to a multiple of the batch (the
+  // padding tickets are skipped) -- a batch that straddles sub-chunks shifts each
+  // ticket's dependency to another position of an earlier batch, which chains the
+  // waves (a 15-ticket batch over 64 lists ran 200x slower)
   return kXePartBatch;
 }
 
@@ -1254,7 +1255,14 @@ __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a,
   const uint32_t* fl = kLdsFlags ? s_flag : a.flag;
   const int lane = lane_id();
   const unsigned long long lt = (1ull << lane) - 1ull;
-  const int64_t total = (int64_t)cur.ctl[3] * kXeSubPerChunk * a.F_loc;
+  // tickets per sub-chunk: F_loc rounded up to a multiple of the batch
+  const int B0 = xe_part_batch(a.F_loc);
+#ifndef MT_XE_PART_NOPAD  // (A/B build: the unpadded ticket order)
+  const int Fp = (a.F_loc + B0 - 1) / B0 * B0;
+#else
+  const int Fp = a.F_loc;
+#endif
+  const int64_t total = (int64_t)cur.ctl[3] * kXeSubPerChunk * Fp;
   // tickets are claimed kXePartBatch at a time (one counter serialises its
   // atomics: ~10 ns each) and run in order, so the wave holding the smallest
   // unfinished ticket still never waits
@@ -1263,11 +1271,11 @@ __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a,
   // the waves; a 16-ticket batch ran them one after another (~130 us for 8 items).
   // (A batch that does not divide F_loc, e.g. 15 of 64, stalled the top levels 200x.)
   const int64_t per_wave = total / ((int64_t)gridDim.x * kXePartWaves);
-  int batch = xe_part_batch(a.F_loc);
+  int batch = B0;
   if (per_wave < 4) {
     batch = 1;
     for (int d = (int)std::max<int64_t>(per_wave, 1); d >= 1; --d)
-      if (a.F_loc % d == 0) {
+      if (Fp % d == 0) {
         batch = d;
         break;
       }
@@ -1283,8 +1291,9 @@ __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a,
       tb = t + batch;
     }
     if (t >= total) break;
-    const int f = t % a.F_loc;
-    const int u = t / a.F_loc;  // sub-chunk index over the level's partition items
+    const int f = t % Fp;
+    const int u = t / Fp;  // sub-chunk index over the level's partition items
+    if (f >= a.F_loc) continue;  // (padding ticket)
     const int it = u / kXeSubPerChunk, k = u % kXeSubPerChunk;
     const int64_t j = a.pitems[(int64_t)it * 4 + 0], s0 = a.pitems[(int64_t)it * 4 + 1];
     const int64_t c0 = a.pitems[(int64_t)it * 4 + 2] + (int64_t)k * kXeSub;
