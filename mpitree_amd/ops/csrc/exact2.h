@@ -125,7 +125,7 @@ void xe_fix(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const void* X
             double* pos_thr);
 void xe_rank(hipStream_t s, int32_t* pos_rec, const double* pos_thr, int64_t P,
              const uint32_t* root_rows, const uint32_t* rank_at, const void* X, int x64, int F,
-             int64_t n, int f_lo, int F_loc, uint8_t* resolved);
+             int64_t n, int f_lo, int F_loc, uint8_t* resolved, const uint32_t* keys);
 void xe_resolved_pack(hipStream_t s, const int32_t* pos_rec, const double* pos_thr, int64_t P,
                       const int32_t* rank, int64_t* rows);
 void xe_resolved_scatter(hipStream_t s, const int64_t* rows, int64_t k, int32_t* pos_rec,

@@ -1628,7 +1628,7 @@ __global__ __launch_bounds__(256) void xe_rank_kernel(
     int32_t* __restrict__ pos_rec, const double* __restrict__ pos_thr, int64_t P,
     const uint32_t* __restrict__ root_rows, const uint32_t* __restrict__ rank_at,
     const void* __restrict__ X, int x64, int F, int64_t n, int f_lo, int F_loc,
-    uint8_t* __restrict__ resolved) {
+    uint8_t* __restrict__ resolved, const uint32_t* __restrict__ keys) {
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (p >= P) return;
   int32_t* R = pos_rec + p * 6;
@@ -1638,9 +1638,19 @@ __global__ __launch_bounds__(256) void xe_rank_kernel(
   const double thr = pos_thr[p];
   const uint32_t* rows = root_rows + (int64_t)f * n;
   int64_t lo = 0, hi = n;  // first sorted position with value >= thr
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (xe_x(X, x64, F, xe_row(rows[mid]), R[0]) < thr) lo = mid + 1; else hi = mid;
+  if (keys) {  // fp32 input: the setup's sorted order-preserving keys, one read a step
+    const uint32_t* kf = keys + (int64_t)f * n;
+    const uint32_t b = __float_as_uint((float)thr + 0.0f);
+    const uint32_t tk = (b >> 31) ? ~b : (b | 0x80000000u);
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (kf[mid] < tk) lo = mid + 1; else hi = mid;
+    }
+  } else {
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (xe_x(X, x64, F, xe_row(rows[mid]), R[0]) < thr) lo = mid + 1; else hi = mid;
+    }
   }
   R[1] = (int32_t)rank_at[(int64_t)f * n + lo];
   if (resolved) resolved[p] = 1;
@@ -1887,11 +1897,11 @@ void xe_fix(hipStream_t s, const uint32_t* E0, const uint32_t* E1, const void* X
 
 void xe_rank(hipStream_t s, int32_t* pos_rec, const double* pos_thr, int64_t P,
              const uint32_t* root_rows, const uint32_t* rank_at, const void* X, int x64, int F,
-             int64_t n, int f_lo, int F_loc, uint8_t* resolved) {
+             int64_t n, int f_lo, int F_loc, uint8_t* resolved, const uint32_t* keys) {
   const int64_t b = (P + 255) / 256;
   if (b == 0) return;
   hipLaunchKernelGGL(xe_rank_kernel, dim3((unsigned)b), dim3(256), 0, s, pos_rec, pos_thr, P,
-                     root_rows, rank_at, X, x64, F, n, f_lo, F_loc, resolved);
+                     root_rows, rank_at, X, x64, F, n, f_lo, F_loc, resolved, keys);
   MT_HIP_CHECK(hipGetLastError());
 }
 

@@ -189,10 +189,13 @@ void bind_exact2(py::module_& m) {
   });
   m.def("xe_rank", [](uintptr_t s, uintptr_t pos_rec, uintptr_t pos_thr, int64_t P,
                       uintptr_t root_rows, uintptr_t rank_at, uintptr_t X, int x64, int F,
-                      int64_t n, int f_lo, int F_loc, uintptr_t resolved) {
+                      int64_t n, int f_lo, int F_loc, uintptr_t resolved, uintptr_t keys) {
     xe_rank(stream_of(s), ptr<int32_t>(pos_rec), ptr<double>(pos_thr), P, ptr<uint32_t>(root_rows),
-            ptr<uint32_t>(rank_at), ptr<void>(X), x64, F, n, f_lo, F_loc, ptr<uint8_t>(resolved));
-  });
+            ptr<uint32_t>(rank_at), ptr<void>(X), x64, F, n, f_lo, F_loc, ptr<uint8_t>(resolved),
+            ptr<uint32_t>(keys));
+  }, py::arg("s"), py::arg("pos_rec"), py::arg("pos_thr"), py::arg("P"), py::arg("root_rows"),
+     py::arg("rank_at"), py::arg("X"), py::arg("x64"), py::arg("F"), py::arg("n"),
+     py::arg("f_lo"), py::arg("F_loc"), py::arg("resolved"), py::arg("keys") = 0);
   m.def("xe_resolved_pack", [](uintptr_t s, uintptr_t pos_rec, uintptr_t pos_thr, int64_t P,
                                uintptr_t rank, uintptr_t rows) {
     xe_resolved_pack(stream_of(s), ptr<int32_t>(pos_rec), ptr<double>(pos_thr), P,

@@ -130,6 +130,7 @@ class ExactGrower:
                         cnt.data_ptr(), 0, yf, E[0].data_ptr(),
                         Y[0].data_ptr() if reg else 0, rank_at.data_ptr())
             root_rows = rows[1]
+            sorted_keys = keys[1]  # (kept for the threshold-rank searches after growth)
             del keys, rows, temp, cnt, nuniq  # (stream-ordered frees)
         else:  # fp64: per-feature stable sorts (ties by row id, -0.0 == 0.0)
             xt = Xd[:, f_lo:f_lo + F_loc].t().contiguous()
@@ -148,10 +149,11 @@ class ExactGrower:
             E[0].copy_(ent)
             rank_at.copy_(rank)
             root_rows = o32
+            sorted_keys = None
             if reg:
                 Y[0].copy_(yfix[order])
             del vals, order, new, nxt_same, dup, rank, ent
-        return E, Y, (root_rows, rank_at)
+        return E, Y, (root_rows, rank_at, sorted_keys)
 
     # --------------------------------------------------------------- fit
     def fit(self, Xd: torch.Tensor, y_codes: torch.Tensor, root, C: int, crit: Criterion,
@@ -389,12 +391,13 @@ class ExactGrower:
         s = hb._stream
         dev = Xd.device
         Pp = int(be.pos_rec.shape[0])
-        root_rows, rank_at = ranks
+        root_rows, rank_at, sorted_keys = ranks
         x64 = int(Xd.dtype == torch.float64)
         resolved = torch.zeros(Pp, dtype=torch.uint8, device=dev) if P > 1 else None
         hip.xe_rank(s(), be.pos_rec.data_ptr(), pos_thr.data_ptr(), Pp, root_rows.data_ptr(),
                     rank_at.data_ptr(), Xd.data_ptr(), x64, F, n, f_lo, F_loc,
-                    0 if resolved is None else resolved.data_ptr())
+                    0 if resolved is None else resolved.data_ptr(),
+                    keys=0 if sorted_keys is None else sorted_keys.data_ptr())
         if P == 1:
             return
         tiles = int(hip.asm_tiles(Pp))
