@@ -746,13 +746,18 @@ __global__ __launch_bounds__(kXeThreads) void xe_gthr_kernel(XeArgs a, XeLists L
 // xe_select: per slot, the best split over this rank's features.
 // rec [K][R] = {gain bits, feature (global, -1 none), position, n_left, m,
 //               threshold value rank, threshold row, left[Cc]}
-__global__ __launch_bounds__(kXeThreads) void xe_select_kernel(XeArgs a, XeLists L) {
-  __shared__ double s_gain[kXeWaves];
-  __shared__ int s_feat[kXeWaves];
-  __shared__ int64_t s_pos[kXeWaves];
+// kXeSelThreads: 1024 while a level has few slots (a level-0 slot's 64 features x ~500
+// chunk records per wave-feature loop were a 52 us chain of dependent loads with 4
+// waves), 256 past that (many slots of few records)
+template <int kXeSelThreads>
+__global__ __launch_bounds__(kXeSelThreads) void xe_select_kernel(XeArgs a, XeLists L) {
+  constexpr int kXeSelWaves = kXeSelThreads / kWave;
+  __shared__ double s_gain[kXeSelWaves];
+  __shared__ int s_feat[kXeSelWaves];
+  __shared__ int64_t s_pos[kXeSelWaves];
   __shared__ double s_pterm;
   __shared__ uint32_t s_c[kXeMaxC];
-  __shared__ int64_t s_sum[kXeWaves];
+  __shared__ int64_t s_sum[kXeSelWaves];
   const int64_t slot = blockIdx.x;
   if (slot >= L.ctl[0]) return;
   const int tid = threadIdx.x, lane = lane_id(), wave = tid >> 6;
@@ -774,7 +779,7 @@ __global__ __launch_bounds__(kXeThreads) void xe_select_kernel(XeArgs a, XeLists
       s_pterm = a.crit == kEntropy ? xlog2x((uint64_t)m) - acc : gini_term(m, sq);
     }
   }
-  for (int c = tid; c < a.C && c < kXeMaxC; c += kXeThreads) s_c[c] = 0;
+  for (int c = tid; c < a.C && c < kXeMaxC; c += kXeSelThreads) s_c[c] = 0;
   __syncthreads();
   const double pterm = s_pterm;
   const double tu = a.C ? tie_unit(xe_tl(m, a.xtab, a.xtab_n), m) : 0.0;
@@ -784,7 +789,7 @@ __global__ __launch_bounds__(kXeThreads) void xe_select_kernel(XeArgs a, XeLists
   int64_t bp = -1;
   // one wave per feature, lanes over the slot's chunks: (key, position) minimum
   // (a level-0 slot holds n / 2048 chunks per feature)
-  for (int f = wave; f < a.F_loc; f += kXeWaves) {
+  for (int f = wave; f < a.F_loc; f += kXeSelWaves) {
     uint64_t bk = ~0ull, bpos = ~0ull;
     for (int it = i0 + lane; it < i1; it += kWave) {
       const uint64_t* c = a.cbest + ((int64_t)it * a.F_loc + f) * 2;
@@ -833,7 +838,7 @@ __global__ __launch_bounds__(kXeThreads) void xe_select_kernel(XeArgs a, XeLists
   g = s_gain[0];
   bf = s_feat[0];
   bp = s_pos[0];
-  for (int w = 1; w < kXeWaves; ++w)
+  for (int w = 1; w < kXeSelWaves; ++w)
     if (s_gain[w] > g || (s_gain[w] == g && s_feat[w] < bf)) {
       g = s_gain[w];
       bf = s_feat[w];
@@ -849,7 +854,7 @@ __global__ __launch_bounds__(kXeThreads) void xe_select_kernel(XeArgs a, XeLists
       out[5] = -1;
       out[6] = -1;
     }
-    for (int c = tid; c < Cc; c += kXeThreads) out[7 + c] = 0;
+    for (int c = tid; c < Cc; c += kXeSelThreads) out[7 + c] = 0;
     return;
   }
   // left statistics: the carry of the chunk holding bp + the chunk's entries up to it
@@ -861,40 +866,40 @@ __global__ __launch_bounds__(kXeThreads) void xe_select_kernel(XeArgs a, XeLists
   if (a.C == 0) {
     const int64_t* Yp = a.Y + (int64_t)fl * a.n;
     int64_t s = 0;
-    for (int64_t p = cfirst + tid; p <= start + bp; p += kXeThreads) s += Yp[p];
+    for (int64_t p = cfirst + tid; p <= start + bp; p += kXeSelThreads) s += Yp[p];
     s = wave_sum_i64(s);
     if (lane == 0) s_sum[wave] = s;
     __syncthreads();
     if (tid == 0) {
       int64_t t = car[0];
-      for (int w = 0; w < kXeWaves; ++w) t += s_sum[w];
+      for (int w = 0; w < kXeSelWaves; ++w) t += s_sum[w];
       out[7] = t;
     }
   } else if (a.C <= 2) {  // class-1 entries counted, class 0 the rest
     uint32_t ones = 0;
-    for (int64_t p = cfirst + tid; p <= start + bp; p += kXeThreads)
+    for (int64_t p = cfirst + tid; p <= start + bp; p += kXeSelThreads)
       ones += xe_lab(Ef[p]) == 1 ? 1u : 0u;
     ones = wave_sum_u32(ones);
     if (lane == 0) s_sum[wave] = ones;
     __syncthreads();
     if (tid == 0) {
       int64_t t = 0;
-      for (int w = 0; w < kXeWaves; ++w) t += s_sum[w];
+      for (int w = 0; w < kXeSelWaves; ++w) t += s_sum[w];
       const int64_t nrows = bp - (cfirst - start) + 1;
       out[7] = car[0] + (nrows - t);
       if (a.C == 2) out[8] = car[1] + t;
     }
   } else if (a.C > kXeMaxC) {  // many classes: the chunk carry, then count into the record
-    for (int c = tid; c < a.C; c += kXeThreads) out[7 + c] = car[c];
+    for (int c = tid; c < a.C; c += kXeSelThreads) out[7 + c] = car[c];
     __threadfence_block();
     __syncthreads();
-    for (int64_t p = cfirst + tid; p <= start + bp; p += kXeThreads)
+    for (int64_t p = cfirst + tid; p <= start + bp; p += kXeSelThreads)
       atomicAdd(reinterpret_cast<unsigned long long*>(out + 7 + xe_label(a, Ef[p])), 1ull);
   } else {
-    for (int64_t p = cfirst + tid; p <= start + bp; p += kXeThreads)
+    for (int64_t p = cfirst + tid; p <= start + bp; p += kXeSelThreads)
       atomicAdd(&s_c[xe_label(a, Ef[p])], 1u);
     __syncthreads();
-    for (int c = tid; c < a.C; c += kXeThreads) out[7 + c] = car[c] + (int64_t)s_c[c];
+    for (int c = tid; c < a.C; c += kXeSelThreads) out[7 + c] = car[c] + (int64_t)s_c[c];
   }
   if (tid == 0) {
     const uint32_t row = xe_row(Ef[start + bp]);
@@ -1797,7 +1802,11 @@ void xe_level_scan(hipStream_t s, const XeArgs& a, const XeLists& cur, int items
   }
   else
     hipLaunchKernelGGL(xe_scan_kernel<2>, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
-  hipLaunchKernelGGL(xe_select_kernel, dim3(slots_bound), dim3(kXeThreads), 0, s, a, cur);
+  if (slots_bound <= 512)
+    hipLaunchKernelGGL(xe_select_kernel<1024>, dim3(slots_bound), dim3(1024), 0, s, a, cur);
+  else
+    hipLaunchKernelGGL(xe_select_kernel<kXeThreads>, dim3(slots_bound), dim3(kXeThreads), 0, s, a,
+                       cur);
   MT_HIP_CHECK(hipGetLastError());
 }
 
