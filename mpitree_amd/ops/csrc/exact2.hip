@@ -277,6 +277,46 @@ __global__ __launch_bounds__(kXeThreads) void xe_carry_kernel(XeArgs a, XeLists 
   }
 }
 
+// The same with one wave per (slot, feature, class): 64 totals per round trip and a
+// wave prefix sum (integer sums: any order is exact). For levels with few slots, each
+// holding hundreds of chunks (level 0: ~500 chunks, 50 us serially per thread).
+__global__ __launch_bounds__(kXeThreads) void xe_carry_wave_kernel(XeArgs a, XeLists L) {
+  const int K = L.ctl[0];
+  const int Cc = xe_cc(a.C);
+  const int lane = lane_id();
+  const int64_t g = ((int64_t)blockIdx.x * kXeThreads + threadIdx.x) >> 6;  // wave
+  if (g >= (int64_t)K * a.F_loc * Cc) return;
+  const int k = (int)(g % Cc);
+  const int f = (int)((g / Cc) % a.F_loc);
+  const int64_t slot = g / ((int64_t)Cc * a.F_loc);
+  const int i0 = L.ifirst[slot], i1 = L.ifirst[slot + 1];
+  if (lane == 0 && k == 0 && a.nmin) a.nmin[slot * a.F_loc + f] = 0xffffffffu;
+  int64_t acc = 0;
+  for (int it0 = i0; it0 < i1; it0 += kWave) {
+    const int it = it0 + lane;
+    const int64_t v = it < i1 ? a.tot[((int64_t)it * a.F_loc + f) * Cc + k] : 0;
+    const int64_t incl = wave_incl_scan_i64(v);
+    if (it < i1) a.carry[((int64_t)it * a.F_loc + f) * Cc + k] = acc + incl - v;
+    acc += __shfl(incl, kWave - 1, kWave);
+  }
+  if (a.C == 0 && f == 0 && k == 0) {
+    int64_t mn = LLONG_MAX, mx = LLONG_MIN;
+    for (int it = i0 + lane; it < i1; it += kWave) {
+      mn = a.cmm[it * 2 + 0] < mn ? a.cmm[it * 2 + 0] : mn;
+      mx = a.cmm[it * 2 + 1] > mx ? a.cmm[it * 2 + 1] : mx;
+    }
+    for (int d = kWave / 2; d > 0; d >>= 1) {
+      const int64_t o1 = __shfl_xor(mn, d, kWave), o2 = __shfl_xor(mx, d, kWave);
+      mn = o1 < mn ? o1 : mn;
+      mx = o2 > mx ? o2 : mx;
+    }
+    if (lane == 0) {
+      L.minmax[slot * 2 + 0] = mn;
+      L.minmax[slot * 2 + 1] = mx;
+    }
+  }
+}
+
 // Feature value of a row (the input matrix, fp32 or fp64, row-major [n][F]).
 __device__ __forceinline__ double xe_x(const void* X, int x64, int F, uint32_t row, int fg) {
   const int64_t o = (int64_t)row * F + fg;
@@ -1779,8 +1819,13 @@ void xe_level_scan(hipStream_t s, const XeArgs& a, const XeLists& cur, int items
   if (!a.tot_ready)
     hipLaunchKernelGGL(xe_tot_kernel, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
   const int64_t nc = (int64_t)slots_bound * a.F_loc * Cc;
-  hipLaunchKernelGGL(xe_carry_kernel, dim3((unsigned)((nc + kXeThreads - 1) / kXeThreads)),
-                     dim3(kXeThreads), 0, s, a, cur);
+  if (slots_bound <= 64)  // few slots of many chunks: a wave each
+    hipLaunchKernelGGL(xe_carry_wave_kernel,
+                       dim3((unsigned)((nc * kWave + kXeThreads - 1) / kXeThreads)),
+                       dim3(kXeThreads), 0, s, a, cur);
+  else
+    hipLaunchKernelGGL(xe_carry_kernel, dim3((unsigned)((nc + kXeThreads - 1) / kXeThreads)),
+                       dim3(kXeThreads), 0, s, a, cur);
   if (a.C == 0)
     hipLaunchKernelGGL(xe_scan_kernel<0>, dim3(gx, a.F_loc), dim3(kXeThreads), 0, s, a, cur);
   else if (a.C <= 2) {  // one wave per (item, feature): no workgroup barriers
