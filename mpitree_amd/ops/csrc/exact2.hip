@@ -955,10 +955,44 @@ __global__ __launch_bounds__(kXeSelThreads) void xe_select_kernel(XeArgs a, XeLi
 
 // ---------------------------------------------------------------------------
 // Planner (one workgroup): see XePlanArgs in exact2.h.
+// Chunk-item runs of more than kXePlanDefer items (a big node's partition items or a big
+// child's next-level items) are written by the whole workgroup after the node pass
+// instead of by the node's thread (level 0: ~1000 items by one thread, 79 us).
+constexpr int kXePlanDefer = 16;
+constexpr int kXePlanBig = 64;
+struct XePlanRun {
+  int64_t* base;  // the run's first item
+  int64_t s0, m;  // segment start and length
+  int tag, cnt;   // item tag (split or slot index), items
+};
 struct XePlanShared {
   int w[kXePlanWaves];
   int carry[4];
+  int nbig;
+  XePlanRun big[kXePlanBig];
 };
+
+// Items q of a segment [s0, s0 + m): {tag, s0, s0 + q chunk, min(chunk, m - q chunk)}.
+__device__ __forceinline__ void xe_plan_item(int64_t* it, int tag, int64_t s0, int64_t m, int q) {
+  it[0] = tag;
+  it[1] = s0;
+  it[2] = s0 + (int64_t)q * kXeChunk;
+  const int64_t rem = m - (int64_t)q * kXeChunk;
+  it[3] = rem < kXeChunk ? rem : kXeChunk;
+}
+
+// A run of cnt items: deferred to the workgroup when long and a record is free.
+__device__ __forceinline__ void xe_plan_run(XePlanShared& sh, int64_t* base, int tag, int64_t s0,
+                                            int64_t m, int cnt) {
+  if (cnt > kXePlanDefer) {
+    const int b = atomicAdd(&sh.nbig, 1);
+    if (b < kXePlanBig) {
+      sh.big[b] = XePlanRun{base, s0, m, tag, cnt};
+      return;
+    }
+  }
+  for (int q = 0; q < cnt; ++q) xe_plan_item(base + (int64_t)q * 4, tag, s0, m, q);
+}
 
 __device__ __forceinline__ int xe_scan_excl(int v, int* s_w, int& total) {
   const int lane = lane_id(), w = threadIdx.x >> 6;
@@ -989,6 +1023,7 @@ __global__ __launch_bounds__(kXePlanThreads) void xe_plan_kernel(XePlanArgs a) {
     sh.carry[1] = 0;  // split nodes
     sh.carry[2] = 0;  // next chunk items
     sh.carry[3] = 0;  // partition items
+    sh.nbig = 0;
   }
   __syncthreads();
   for (int b0 = 0; b0 < K; b0 += kXePlanThreads) {
@@ -1080,14 +1115,7 @@ __global__ __launch_bounds__(kXePlanThreads) void xe_plan_kernel(XePlanArgs a) {
           a.sitem[o_ns * 2 + 1] = -1;
         }
         // partition items of this split node
-        for (int q = 0; q < np; ++q) {
-          int64_t* it = a.pitems + (int64_t)(o_np + q) * 4;
-          it[0] = o_ns;
-          it[1] = start;
-          it[2] = start + (int64_t)q * kXeChunk;
-          const int64_t rem = m - (int64_t)q * kXeChunk;
-          it[3] = rem < kXeChunk ? rem : kXeChunk;
-        }
+        xe_plan_run(sh, a.pitems + (int64_t)o_np * 4, o_ns, start, m, np);
         a.pfirst[o_ns] = o_np;
         const int cd = depth + 1;
         int sl = o_nn, io = o_ni;
@@ -1130,18 +1158,20 @@ __global__ __launch_bounds__(kXePlanThreads) void xe_plan_kernel(XePlanArgs a) {
             a.nxt.ifirst[sl] = io;
             if (a.sitem) a.sitem[o_ns * 2 + c] = io;
             const int64_t nck = (cm + kXeChunk - 1) / kXeChunk;
-            for (int q = 0; q < nck; ++q) {
-              int64_t* it = a.nxt.items + (int64_t)(io + q) * 4;
-              it[0] = sl;
-              it[1] = cst;
-              it[2] = cst + (int64_t)q * kXeChunk;
-              const int64_t rem = cm - (int64_t)q * kXeChunk;
-              it[3] = rem < kXeChunk ? rem : kXeChunk;
-            }
+            xe_plan_run(sh, a.nxt.items + (int64_t)io * 4, sl, cst, cm, (int)nck);
             io += (int)nck;
             ++sl;
           }
         }
+      }
+    }
+    __syncthreads();
+    {  // the deferred long item runs, by the whole workgroup
+      const int nb = min(sh.nbig, kXePlanBig);
+      for (int b = 0; b < nb; ++b) {
+        const XePlanRun e = sh.big[b];
+        for (int q = tid; q < e.cnt; q += kXePlanThreads)
+          xe_plan_item(e.base + (int64_t)q * 4, e.tag, e.s0, e.m, q);
       }
     }
     __syncthreads();
@@ -1150,6 +1180,7 @@ __global__ __launch_bounds__(kXePlanThreads) void xe_plan_kernel(XePlanArgs a) {
       sh.carry[1] += t_ns;
       sh.carry[2] += t_ni;
       sh.carry[3] += t_np;
+      sh.nbig = 0;
     }
     __syncthreads();
   }
