@@ -211,13 +211,31 @@ __global__ __launch_bounds__(kNT) void xs_scatter_kernel(
     }
   }
   __syncthreads();
-  for (int i = tid; i < cnt; i += kNT) {
-    const uint32_t kk = s_key[i];
-    const int64_t dst = base + (int64_t)(s_goff[(kk >> shift) & 255u] + i);
-    kout[dst] = kk;
-    uint32_t rv = s_row[i];
-    if constexpr (kLab) rv |= (uint32_t)ylab[rv] << 25;  // (rows of this tile: a local read)
-    rout[dst] = rv;
+  // 4 entries per lane per step: their label reads (pass 0 with packed labels: rows
+  // of this tile, a local window) are in flight together
+  constexpr int kS = 4;
+  for (int i0 = tid; i0 < cnt; i0 += kNT * kS) {
+    uint32_t kk[kS], rv[kS];
+#pragma unroll
+    for (int u = 0; u < kS; ++u) {
+      const int i = i0 + u * kNT;
+      kk[u] = i < cnt ? s_key[i] : 0u;
+      rv[u] = i < cnt ? s_row[i] : 0u;
+    }
+    if constexpr (kLab) {
+#pragma unroll
+      for (int u = 0; u < kS; ++u)
+        if (i0 + u * kNT < cnt) rv[u] |= (uint32_t)ylab[rv[u]] << 25;
+    }
+#pragma unroll
+    for (int u = 0; u < kS; ++u) {
+      const int i = i0 + u * kNT;
+      if (i < cnt) {
+        const int64_t dst = base + (int64_t)(s_goff[(kk[u] >> shift) & 255u] + i);
+        kout[dst] = kk[u];
+        rout[dst] = rv[u];
+      }
+    }
   }
 }
 
