@@ -192,14 +192,17 @@ def _finalize(ta: TreeArrays, mapper: BinMapper, regression: bool, y_exp: int) -
     return ta
 
 
-def _exact_device_ok(n, F, C, regression) -> bool:
+def _exact_device_ok(n, F, C, regression, P=1, free_bytes=None) -> bool:
     """The device-driven exact engine (``ops/exact_grower.py``) takes any
     feature count and any class count below 2^20 on fewer than 2^24 rows (its
     <= 256-row finisher jobs run where the local-code finishers fit: at most 256
-    classes; otherwise its level loop grows to the leaves)."""
-    from ..ops.exact_grower import exact_supported
+    classes; otherwise its level loop grows to the leaves) -- when its workspace
+    fits the device (no finisher: buffers grow as n F C)."""
+    from ..ops.exact_grower import exact_fits_memory, exact_supported
 
-    return exact_supported(n, C, regression)
+    if not exact_supported(n, C, regression):
+        return False
+    return exact_fits_memory(n, F, C, regression, P, free_bytes)
 
 
 def _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t_bin, t_start, F, regression):
@@ -343,19 +346,28 @@ def fit_tree(
         from ..ops.exact_grower import needs_exact
 
         if max_bins is None and g_mapper is None and needs_exact(mapper):
-            if _exact_device_ok(n, F, C, regression):
+            P_fp = comm.world_size if comm.world_size > 1 and F >= comm.world_size else 1
+            if _exact_device_ok(n, F, C, regression, P_fp):
                 if checkpoint is not None:  # the same tree, just no mid-fit state
                     logger.warning("the exact-threshold GPU engine keeps no level "
                                    "checkpoint: fitting without one")
                 # (the bin pass's flags -- non-finite input -- are read after the fit,
                 # so the host enqueues the setup without waiting for them)
-                res = _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t0,
-                                        t_start, F, regression)
+                try:
+                    res = _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t0,
+                                            t_start, F, regression)
+                except Exception:
+                    # non-finite input (the bin pass's flags) explains any failure of
+                    # the engine on it: that ValueError takes precedence
+                    if prep.verify is not None and not prep.verify():
+                        return fit_tree(X, y, **redo)
+                    raise
                 if prep.verify is not None and not prep.verify():
                     return fit_tree(X, y, **redo)
                 return res
             logger.warning("exact thresholds on > 256-value features are not available on "
-                           "the GPU for this fit (>= 2^24 rows or >= 2^20 classes): using "
+                           "the GPU for this fit (>= 2^24 rows, >= 2^20 classes, or a list "
+                           "engine workspace beyond half the free device memory): using "
                            "256 quantile bins per feature")
             quantile_fallback = True
             if probe:  # the probe left out the quantile edges and the codes: bin again

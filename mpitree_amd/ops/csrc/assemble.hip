@@ -292,11 +292,13 @@ __global__ __launch_bounds__(256) void own_mark_kernel(const int64_t* __restrict
 template <typename StatT>
 __global__ __launch_bounds__(kAsmThreads) void own_pack_kernel(
     const int32_t* __restrict__ rec, const StatT* __restrict__ st, int64_t P, int C,
-    const int32_t* __restrict__ rank, StatT* __restrict__ rows) {
+    const int32_t* __restrict__ rank, StatT* __restrict__ rows, int64_t row_cap) {
+  // row_cap: rows the buffer holds; the count past it (asm_rank's total) makes
+  // the host raise on every rank, so rows beyond it are never written
   const int64_t p = (int64_t)blockIdx.x * kAsmThreads + threadIdx.x;
   if (p >= P) return;
   const int j = rank[p];
-  if (j < 0) return;
+  if (j < 0 || j >= row_cap) return;
   StatT* o = rows + (int64_t)j * (7 + C);
   o[0] = (StatT)p;
   for (int k = 0; k < 6; ++k) o[1 + k] = (StatT)rec[p * 6 + k];
@@ -318,7 +320,8 @@ __global__ __launch_bounds__(256) void own_scatter_kernel(const StatT* __restric
 
 void launch_own_pack(hipStream_t stream, const int64_t* ranges, int cap, uint8_t* mask,
                      const int32_t* rec, const void* st, bool st64, int64_t P, int C,
-                     int32_t* tile, int64_t* total, int32_t* rank, void* rows) {
+                     int32_t* tile, int64_t* total, int32_t* rank, void* rows,
+                     int64_t row_cap) {
   if (cap > 0)
     hipLaunchKernelGGL(own_mark_kernel, dim3(cap), dim3(256), 0, stream, ranges, mask);
   launch_asm_rank(stream, rec, P, tile, total, rank, mask);
@@ -326,10 +329,10 @@ void launch_own_pack(hipStream_t stream, const int64_t* ranges, int cap, uint8_t
   if (blocks == 0) return;
   if (st64)
     hipLaunchKernelGGL(own_pack_kernel<int64_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
-                       stream, rec, (const int64_t*)st, P, C, rank, (int64_t*)rows);
+                       stream, rec, (const int64_t*)st, P, C, rank, (int64_t*)rows, row_cap);
   else
     hipLaunchKernelGGL(own_pack_kernel<int32_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
-                       stream, rec, (const int32_t*)st, P, C, rank, (int32_t*)rows);
+                       stream, rec, (const int32_t*)st, P, C, rank, (int32_t*)rows, row_cap);
   MT_HIP_CHECK(hipGetLastError());
 }
 

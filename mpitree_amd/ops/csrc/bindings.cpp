@@ -79,7 +79,7 @@ void launch_edges(hipStream_t, const void*, bool, int64_t, int, int, int, void*,
 void launch_asm_rank(hipStream_t, const int32_t*, int64_t, int32_t*, int64_t*, int32_t*,
                      const uint8_t*);
 void launch_own_pack(hipStream_t, const int64_t*, int, uint8_t*, const int32_t*, const void*,
-                     bool, int64_t, int, int32_t*, int64_t*, int32_t*, void*);
+                     bool, int64_t, int, int32_t*, int64_t*, int32_t*, void*, int64_t);
 void launch_own_scatter(hipStream_t, const void*, int64_t, int, int32_t*, void*, bool);
 int64_t asm_node_bytes(int C, bool reg);
 int small_fit_max_rows();
@@ -353,11 +353,13 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("rank"), py::arg("mask") = 0);
   m.def("own_pack", [](uintptr_t s, uintptr_t ranges, int cap, uintptr_t mask, uintptr_t rec,
                        uintptr_t st, bool st64, int64_t npos, int C, uintptr_t tile,
-                       uintptr_t total, uintptr_t rank, uintptr_t rows) {
+                       uintptr_t total, uintptr_t rank, uintptr_t rows, int64_t row_cap) {
     mt::launch_own_pack(S(s), P<int64_t>(ranges), cap, P<uint8_t>(mask), P<int32_t>(rec),
                         P<void>(st), st64, npos, C, P<int32_t>(tile), P<int64_t>(total),
-                        P<int32_t>(rank), P<void>(rows));
-  });
+                        P<int32_t>(rank), P<void>(rows), row_cap);
+  }, py::arg("s"), py::arg("ranges"), py::arg("cap"), py::arg("mask"), py::arg("rec"),
+     py::arg("st"), py::arg("st64"), py::arg("npos"), py::arg("C"), py::arg("tile"),
+     py::arg("total"), py::arg("rank"), py::arg("rows"), py::arg("row_cap") = INT64_MAX);
   m.def("own_scatter", [](uintptr_t s, uintptr_t rows, int64_t k, int C, uintptr_t rec,
                           uintptr_t st, bool st64) {
     mt::launch_own_scatter(S(s), P<void>(rows), k, C, P<int32_t>(rec), P<void>(st), st64);

@@ -171,7 +171,7 @@ def exchange_ranges(be, comm, ranges: torch.Tensor, bound: int):
     base = buf.data_ptr()
     hip.own_pack(s, ranges.data_ptr(), int(ranges.shape[0]), base + o_mask, be.pos_rec.data_ptr(),
                  be.pos_st.data_ptr(), reg, Pp, C, base + o_tile, base + o_total, base + o_rank,
-                 base + o_rows)
+                 base + o_rows, row_cap=bound)
     k_dev = buf[o_total : o_total + 8].view(torch.int64)
     if hasattr(comm, "all_gather_rows_counted"):
         allr = comm.all_gather_rows_counted(

@@ -68,6 +68,61 @@ def exact_supported(n: int, C: int, regression: bool) -> bool:
     return regression or 1 <= C <= int(native.hip().xe_max_classes())
 
 
+def exact_finisher_rows(F: int, C: int, regression: bool) -> int:
+    """Rows of the largest segment the engine hands to a finisher job (0: its
+    levels grow to the leaves -- the local-code finishers take <= 256 classes and
+    the regression finisher <= 256 features)."""
+    from . import native
+
+    hip = native.hip()
+    fr = int(hip.xe_local_max())
+    if regression and F > 256:
+        fr = 0
+    if not regression and (C > 256 or int(hip.finish_feature_tile(F, 256, C)) <= 0):
+        fr = 0
+    return fr
+
+
+def exact_workspace_bytes(n: int, F_loc: int, C: int, regression: bool, fr: int,
+                          chunk: int, rec_width: int) -> int:
+    """Device bytes of one fit's list engine on a rank holding ``F_loc`` features:
+    the sorted lists (+ fixed-point targets), the setup sort's temporaries, the
+    per-item / per-node level buffers (sized by ``KMAX = n / (fr + 1)``: with no
+    finisher every level can hold ~n / 2 nodes, and the (items x features x
+    classes) chunk totals and carries grow as n F C) and the position space."""
+    KMAX = n // (fr + 1) + 2
+    IMAX = KMAX + n // max(chunk, 1) + 2
+    Cc = 1 if regression else max(int(C), 1)
+    Cs = 2 if regression else max(int(C), 1)
+    b = 0
+    b += 2 * F_loc * n * 4 + F_loc * n * 4             # E[2], rank_at
+    b += 4 * F_loc * n * 4                              # setup keys[2], rows[2]
+    if regression:
+        b += 2 * F_loc * n * 8                          # Y[2]
+    b += 2 * IMAX * F_loc * Cc * 8                      # tot, carry
+    b += IMAX * F_loc * (16 + 4) + 2 * IMAX * F_loc * 8  # cbest, cmin, pstat
+    b += KMAX * (F_loc * 4 + rec_width * 8 + 64 + 2 * Cs * 8)  # nmin, rec, lists
+    b += (2 * n) * (6 * 4 + Cs * 8 + 8)                 # position space + thresholds
+    return int(b)
+
+
+def exact_fits_memory(n: int, F: int, C: int, regression: bool, P: int = 1,
+                      free_bytes: int | None = None) -> bool:
+    """Whether the list engine's workspace fits in half of the free device memory
+    (else the fit takes 256 quantile bins: ADVICE r4 -- at 1M x 64 with 300
+    classes the no-finisher chunk totals alone would need ~150 GB each)."""
+    from . import native
+
+    hip = native.hip()
+    F_loc = -(-F // max(P, 1))
+    fr = exact_finisher_rows(F, C, regression)
+    need = exact_workspace_bytes(n, F_loc, C, regression, fr, int(hip.xe_chunk()),
+                                 int(hip.xe_rec_width(0 if regression else int(C))))
+    if free_bytes is None:
+        free_bytes = int(torch.cuda.mem_get_info()[0])
+    return need <= free_bytes // 2
+
+
 def needs_exact(mapper) -> bool:
     """A binned fit cannot be exact: some feature kept quantile edges."""
     ex = np.asarray(getattr(mapper, "exact", []), dtype=bool)
@@ -220,11 +275,7 @@ class ExactGrower:
             self.stats.update(levels=0, finisher_subtrees=0)
             return be.assemble_positions(None, int(crit), y_exp, thr_pos=pos_thr)
 
-        fr = int(hip.xe_local_max())
-        if reg and F > 256:
-            fr = 0  # (the regression finisher keeps <= 256 features): levels to the leaves
-        if not reg and (C > 256 or int(hip.finish_feature_tile(F, 256, C)) <= 0):
-            fr = 0  # (the local-code finishers take <= 256 classes): levels to the leaves
+        fr = exact_finisher_rows(F, Cx, reg)  # (0: levels to the leaves)
         env = os.environ.get("MPITREE_EXACT_FINISHER_ROWS")  # (tests: 0 = no finisher)
         if env is not None:
             fr = max(0, min(fr, int(env)))

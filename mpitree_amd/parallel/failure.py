@@ -75,6 +75,7 @@ class FitGuard:
     """Context of one collective fit on ``comm`` (see the module docstring)."""
 
     POLL_S = 0.2
+    STORE_ERRORS = 5  # consecutive failed store polls read as a torn-down group
 
     def __init__(self, comm):
         self.comm = comm
@@ -107,10 +108,17 @@ class FitGuard:
     # --------------------------------------------------------- watchdog
     def _watch(self):
         seen = None
+        errors = 0
         while not self._done.wait(self.POLL_S):
             n = self._nfail()
             if n == 0:
+                errors = 0
                 continue
+            if n < 0:  # a store error: transient (retry), or the group is gone
+                errors += 1
+                if errors < self.STORE_ERRORS:
+                    continue
+            errors = 0
             ABORT.set()  # host loops raise at their next check
             if seen is None:
                 seen = time.monotonic()
@@ -134,10 +142,15 @@ class FitGuard:
             self._thread.start()
         return self
 
-    def __exit__(self, *exc):
+    def stop(self) -> None:
+        """End the watchdog (idempotent)."""
         self._done.set()
         if self._thread is not None:
             self._thread.join(timeout=5)
+            self._thread = None
+
+    def __exit__(self, *exc):
+        self.stop()
         ABORT.clear()
         return False
 
@@ -168,6 +181,10 @@ class FitGuard:
             time.sleep(0.01)
             n = self._nfail()
         if n == self.P:
+            # every rank failed and agreed: nobody is inside a collective, and the
+            # status all-gather that follows must not be aborted by the watchdog
+            self.stop()
+            ABORT.clear()
             return None
         msg = self._first_failure()
         try:

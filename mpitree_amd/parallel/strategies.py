@@ -215,14 +215,20 @@ class DistComm(LocalComm):
         import torch
 
         P = self.world_size
-        kd = k_dev.reshape(1).to(torch.int64)
-        sizes_d = torch.empty(P, dtype=torch.int64, device=kd.device)
-        self.all_gather_device(sizes_d, kd)
-        sizes = sizes_d.cpu().numpy()  # the one host wait
+        k_cap = torch.empty(2, dtype=torch.int64, device=k_dev.device)
+        k_cap[0:1].copy_(k_dev.reshape(1))
+        k_cap[1] = int(buf.shape[0])
+        sizes_d = torch.empty(2 * P, dtype=torch.int64, device=k_dev.device)
+        self.all_gather_device(sizes_d, k_cap)
+        kc = sizes_d.cpu().numpy().reshape(P, 2)  # the one host wait
+        sizes = kc[:, 0]
         kmax = int(max(1, sizes.max()))
         k, cap, w = int(sizes[self.rank]), int(buf.shape[0]), int(buf.shape[1])
-        if k > cap:
-            raise RuntimeError(f"row exchange: {k} rows exceed the buffer ({cap})")
+        over = np.nonzero(kc[:, 0] > kc[:, 1])[0]
+        if over.size:  # every rank sees every count and capacity: all raise here
+            r = int(over[0])
+            raise RuntimeError(f"row exchange: rank {r} packed {int(kc[r, 0])} rows into a "
+                               f"buffer of {int(kc[r, 1])}")
         if kmax <= cap:
             src = buf[:kmax].contiguous()
         else:  # a peer has more rows than this buffer holds: pad a copy

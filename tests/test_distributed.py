@@ -503,3 +503,26 @@ def test_all_gather_rows_counted_pads_and_concatenates():
                            for r in range(3)])
     for o in outs:
         np.testing.assert_array_equal(o["rows"], want)
+
+
+def _counted_rows_overflow(rank, world):
+    import torch
+
+    from mpitree_amd.parallel.strategies import SubtreeComm
+
+    comm = SubtreeComm()
+    # rank 1 reports 9 packed rows for a 4-row buffer: every rank must raise at
+    # the count exchange (no rank goes on into the row all-gather)
+    k = 9 if rank == 1 else 2
+    buf = torch.zeros((4, 3), dtype=torch.int32)
+    try:
+        comm.all_gather_rows_counted(buf, torch.tensor([k], dtype=torch.int64))
+    except RuntimeError as e:
+        return {"err": str(e)}
+    return {"err": None}
+
+
+def test_all_gather_rows_counted_overflow_raises_on_every_rank():
+    outs = run_ranks(_counted_rows_overflow, 3)
+    for o in outs:
+        assert "rank 1 packed 9 rows" in str(o["err"])

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build a variant of the HIP extension with one source recompiled under extra
 # -D flags (the other objects come from the last in-tree build). Output:
-# variants/<name>.so, which tools/gpu_ab_so.sh swaps in for an A/B run.
+# variants/<name>.so, which `tools/gpu.sh ab:so=<name>` swaps in for an A/B run.
 # Usage: bash tools/build_variant.sh <name> <source.hip> -DFLAG=V ...
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
