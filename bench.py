@@ -34,6 +34,12 @@ row-sharded histograms reduced per feature block to their owner ranks (BASELINE
 config 4: ``--n 10000000 --features 128 --strategy data``). The JSON line reports the
 level loop that actually ran (``config.level_loop``) and the bytes moved.
 
+Every quantized-data run also times the same estimator on the continuous
+companion data set (same shape and label model, N(0, 1) features: the
+reference's every-unique-value threshold semantics on the presorted-list exact
+engine) and reports it as ``continuous_ms_per_step`` next to the headline
+(``--no-continuous`` skips it; ``--continuous`` makes it the headline).
+
 ``MPITREE_BENCH_BACKEND=gloo`` rehearses the multi-rank path with ranks
 sharing the visible GPUs (collectives over gloo instead of RCCL).
 """
@@ -107,6 +113,8 @@ def main(argv=None):
     ap.add_argument("--regression", action="store_true")
     ap.add_argument("--continuous", action="store_true",
                     help="N(0,1) features: exact thresholds over every unique value")
+    ap.add_argument("--no-continuous", action="store_true",
+                    help="skip the continuous companion timing (continuous_ms_per_step)")
     ap.add_argument("--max-bins", type=int, default=0,
                     help="> 0: quantile bins (e.g. 1024 with --continuous: 16-bit codes)")
     ap.add_argument("--profile-levels", action="store_true")
@@ -170,12 +178,36 @@ def main(argv=None):
         est.fit(X, y)
     barrier()
     dt = (time.perf_counter() - t0) / a.steps
-    if dist is not None:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+
+    def reduce_max(v):
+        if dist is None:
+            return v
+        t = torch.tensor([v], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        return float(t.item())
+
+    dt = reduce_max(dt)
     stats = est.fit_stats_
     ta = est.tree_arrays_
+    cont = None
+    if not a.continuous and not a.no_continuous and a.max_bins <= 0:
+        # the same estimator and shape on continuous features (exact presorted-list
+        # engine, the reference's threshold semantics), timed the same way
+        gen = make_regression if a.regression else make_classification
+        kw = {} if a.regression else {"n_classes": a.classes}
+        Xc, yc = gen(a.n, a.features, levels=None, seed=1, device=dev, **kw)
+        ksteps = max(1, min(a.steps, 10))
+        est.fit(Xc, yc)  # warmup (setup buffers, level-loop workspace)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(ksteps):
+            est.fit(Xc, yc)
+        barrier()
+        cont = {"ms_per_step": round(reduce_max((time.perf_counter() - t0) / ksteps) * 1e3, 3),
+                "steps": ksteps, "tree_nodes": est.fit_stats_.get("node_count"),
+                "engine": est.fit_stats_.get("engine"),
+                "thresholds": est.fit_stats_.get("thresholds")}
+        del Xc, yc
     # the fit returned finished columns (numpy arrays over host memory, no
     # lazily derived attributes): check it, outside the timed region
     cols = ("feature", "threshold", "threshold_bin", "left", "right", "depth", "n_samples",
@@ -206,6 +238,7 @@ def main(argv=None):
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(dt * 1e3, 3),
+            "continuous_ms_per_step": None if cont is None else cont["ms_per_step"],
             "fit_seconds": round(dt, 6),
             "higher_is_better": True,
             "scaling": "strong",
@@ -242,6 +275,7 @@ def main(argv=None):
                 "comm_bytes_per_level": stats.get("comm_bytes_per_level"),
                 "peak_device_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 3),
             },
+            "continuous": cont,
             "reference_note": "reference is infeasible at this size (BASELINE.md: >=775 CPU-h "
                               "for the root node alone); vs_baseline is null",
         }

@@ -771,6 +771,8 @@ class DeviceGrower:
             else:  # (ownership: one job -- every rank grows it, nothing to exchange)
                 self._run_jobs(d_jobs.view(1, -1), n, split=not own)
         if comm is not None and P > 1:
+            check_abort()
+            fault_point(comm, "exchange")  # (after the switch: peers wait in the exchange)
             t1 = time.perf_counter()
             b0 = comm.bytes_communicated
             if getattr(self, "_owned", None) is not None:

@@ -536,6 +536,8 @@ class ExactGrower:
         if Jm:
             be.launch_finisher(fj, Jm, n, self.p, be.pos_rec, be.pos_st)
         if P > 1:  # finished job ranges -> every rank
+            check_abort()
+            fault_point(comm, "exchange")
             rg = torch.stack([fj[:, 3], fj[:, 3] + 2 * fj[:, 1] - 1], 1).contiguous()
             if rg.shape[0] == 0:
                 rg = torch.zeros((1, 2), dtype=torch.int64, device=dev)

@@ -526,3 +526,54 @@ def test_all_gather_rows_counted_overflow_raises_on_every_rank():
     outs = run_ranks(_counted_rows_overflow, 3)
     for o in outs:
         assert "rank 1 packed 9 rows" in str(o["err"])
+
+
+def _fault_mid_loop_gpu(rank, world, strategy, where, continuous):
+    import os
+    import time
+
+    import torch
+
+    from mpitree_amd import ParallelDecisionTreeClassifier
+    from mpitree_amd.parallel.failure import CollectiveFitAborted
+    from mpitree_amd.utils.datasets import make_classification
+    from mpitree_amd.utils.observability import InjectedFault
+
+    dev = torch.device("cuda", 0)
+    X, y = make_classification(200_000, 16, levels=None if continuous else 256, seed=7,
+                               device=dev)
+    os.environ.update(MPITREE_FAULT_RANK="1", MPITREE_FAULT_AT=where, MPITREE_FAIL_WAIT="2")
+    kind, t0 = "ok", time.monotonic()
+    mode = ""
+    try:
+        est = ParallelDecisionTreeClassifier(strategy=strategy, device="cuda")
+        est.fit(X, y)
+        mode = est.fit_stats_.get("mode", "")
+    except InjectedFault:
+        kind = "injected"
+    except CollectiveFitAborted as e:
+        kind = "peer" if "rank 1" in str(e) and "InjectedFault" in str(e) else f"other:{e}"
+    except Exception as e:  # noqa: BLE001
+        kind = f"other:{type(e).__name__}:{e}"
+    torch.cuda.synchronize()
+    return {"kind": np.array([kind]), "s": np.array([time.monotonic() - t0]),
+            "mode": np.array([mode])}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strategy,where,continuous", [
+    ("auto", "level:2", False),     # replicated levels (before the ownership switch)
+    ("auto", "exchange", False),    # after the switch: the peer waits in the node exchange
+    ("feature", "level:2", False),  # the peer waits in that level's record all-gather
+    ("auto", "level:2", True),      # exact engine, feature-parallel levels
+    ("auto", "exchange", True),     # exact engine: the peer waits in the finisher exchange
+])
+def test_gpu_fault_inside_fit_raises_everywhere(strategy, where, continuous):
+    """Two gloo ranks sharing one MI355X, rank 1 raising inside the device level
+    loop, after the ownership switch, or inside the exact engine: every rank
+    raises (the injected error, or CollectiveFitAborted naming rank 1) within
+    30 s instead of blocking in a collective (parallel/failure.py)."""
+    outs = run_ranks(_fault_mid_loop_gpu, 2, strategy, where, continuous, start_method="spawn")
+    kinds = [str(o["kind"][0]) for o in outs]
+    assert kinds == ["peer", "injected"], kinds
+    assert max(float(o["s"][0]) for o in outs) < 30
