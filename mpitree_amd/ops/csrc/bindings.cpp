@@ -241,6 +241,7 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("task_bound"), py::arg("slab"), py::arg("hist"), py::arg("F_h"), py::arg("B"),
      py::arg("C"), py::arg("dred"), py::arg("dtasks"), py::arg("zero") = true);
   m.def("job_sort_max", &mt::job_sort_max);
+  m.def("fin_tiny_batch", []() { return mt::kFinTinyBatch; });
   m.def("job_sort", [](uintptr_t s, uintptr_t jobs, int J, int W, uintptr_t out,
                        uintptr_t counters) {
     mt::launch_job_sort(S(s), P<int64_t>(jobs), J, W, P<int64_t>(out), P<int32_t>(counters));

@@ -58,6 +58,12 @@ constexpr int kFinTab = 1024;    // LDS x*log2(x) entries
 #ifndef MT_FIN_PAIR
 #define MT_FIN_PAIR 1
 #endif
+#ifndef MT_FIN_PF  // the hand-off check's loads issued before the partition (1) or in place
+#define MT_FIN_PF 0
+#endif
+#ifndef MT_FIN_PRED  // fp32 first pass: look up the terms of non-candidate bins too (0) or
+#define MT_FIN_PRED 0   // only those of candidate bins (exec-masked LDS reads: fewer conflicts)
+#endif
 #ifndef MT_FIN_VMASK  // fp32 first pass: terms {T(ml), T(l0), T(l1), T(mr), T(r0), T(r1)}
 #define MT_FIN_VMASK 0  // computed on the VALU (bit set) instead of looked up in LDS
 #endif
@@ -152,7 +158,20 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
   __shared__ int s_bf, s_bb;
   __shared__ int s_lc, s_rc;
   __shared__ int s_cand_total;
-  if (threadIdx.x == 0) s_cand_total = 0;
+  __shared__ int s_tnext, s_tend;  // this workgroup's reserved tiny records (thread 0)
+  if (threadIdx.x == 0) {
+    s_cand_total = 0;
+    s_tnext = s_tend = 0;
+  }
+  // a tiny-subtree record (thread 0 only): one device atomic per kFinTinyBatch
+  auto tiny_slot = [&]() -> int64_t {
+    if (s_tnext == s_tend) {
+      const int t = atomicAdd(tiny_count, kFinTinyBatch);
+      s_tnext = t;
+      s_tend = t + kFinTinyBatch;
+    }
+    return (int64_t)(s_tnext++);
+  };
 
   const int tid = threadIdx.x;
   // C > 2 (generic path): the node's present class ids + their count at [C],
@@ -272,8 +291,17 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         // bins to one broadcast entry measured slower (the selects cost more VALU
         // than the bank conflicts they remove)
         const uint32_t xs[6] = {ml, l0, l1, mr, t0 - l0, t1 - l1};
+        if (MT_FIN_PRED) {
 #pragma unroll
-        for (int e = 0; e < 6; ++e) tv[q][k][e] = ((kFinVMask >> e) & 1) ? tfv(xs[e]) : lk(xs[e]);
+          for (int e = 0; e < 6; ++e) tv[q][k][e] = 0.0f;
+          if (ok[q][k]) {
+#pragma unroll
+            for (int e = 0; e < 6; ++e) tv[q][k][e] = lk(xs[e]);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 6; ++e) tv[q][k][e] = ((kFinVMask >> e) & 1) ? tfv(xs[e]) : lk(xs[e]);
+        }
       }
     }
 #pragma unroll
@@ -403,7 +431,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
       R[4] = (int32_t)jb[2];
       R[5] = (int32_t)jb[1];
       if (jb[1] <= tiny_rows) {  // the whole job is tiny: one wave finishes it
-        const int64_t t = atomicAdd(tiny_count, 1);
+        const int64_t t = tiny_slot();
         int64_t* tr = tiny + t * 8;
         tr[0] = jb[0];
         tr[1] = jb[1];
@@ -520,30 +548,34 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         const int my_w = w_lo + sub * vec;
         const bool active = sub * vec < words;
         for (int base_r = tid >> lane_shift; base_r < m; base_r += rpp * kFinUnroll) {
+          // unconditional loads (an absent row re-reads the segment's first entry /
+          // row 0): every gather of the unrolled rows is in flight before the
+          // first use -- guarded loads compiled to one wait per row
           uint32_t ent[kFinUnroll];
+          bool okr[kFinUnroll];
 #pragma unroll
           for (int u = 0; u < kFinUnroll; ++u) {
             const int r = base_r + u * rpp;
-            ent[u] = (active && r < m) ? src[start + r] : 0xffffffffu;
+            okr[u] = active && r < m;
+            ent[u] = src[start + (okr[u] ? r : 0)];
           }
           uint32_t wv[kFinUnroll][4];
           int lab[kFinUnroll];
 #pragma unroll
           for (int u = 0; u < kFinUnroll; ++u) {
-            const bool ok = ent[u] != 0xffffffffu;
-            const uint32_t row = rl.shift ? (ent[u] & rl.mask) : ent[u];
-            lab[u] = ok ? (rl.shift ? (int)(ent[u] >> rl.shift) : y[row]) : 0;
+            const uint32_t row = okr[u] ? (rl.shift ? (ent[u] & rl.mask) : ent[u]) : 0u;
+            lab[u] = rl.shift ? (int)(ent[u] >> rl.shift) : y[row];
             if (vec == 4) {
-              const uint4 v = ok ? *reinterpret_cast<const uint4*>(codes_rm + (int64_t)row * row_words + my_w)
-                                 : make_uint4(0, 0, 0, 0);
+              const uint4 v = *reinterpret_cast<const uint4*>(codes_rm + (int64_t)row * row_words + my_w);
               wv[u][0] = v.x;
               wv[u][1] = v.y;
               wv[u][2] = v.z;
               wv[u][3] = v.w;
             } else {
-              wv[u][0] = ok ? codes_rm[(int64_t)row * row_words + my_w] : 0u;
+              wv[u][0] = codes_rm[(int64_t)row * row_words + my_w];
               wv[u][1] = wv[u][2] = wv[u][3] = 0u;
             }
+            if (!okr[u]) ent[u] = 0xffffffffu;
           }
 #pragma unroll
           for (int u = 0; u < kFinUnroll; ++u) {
@@ -836,6 +868,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
       __syncthreads();
       mark(1);
       int bf = -1, bb = -1;
+      int pf_head = 0, pf_pushed = 0;  // (thread 0: hand-off check, loaded early)
       bool decided = false;
       if constexpr (kC2) {
         int tot = 0, cw = -1;
@@ -890,6 +923,13 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           s = wave_sum_u32(s);
           if (lane == 0) s_left[c] = (int32_t)s;
         }
+        // the hand-off check's two device-scope loads (thread 0, children below),
+        // issued before the partition so their latency overlaps it
+        if (MT_FIN_PF && kC2 && tid == 0) {
+          pf_head = __hip_atomic_load(job_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          pf_pushed = (int)(__hip_atomic_load(q_word, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) >> 32);
+        }
         // ---- partition rows src -> dst (unstable; left from the front, right from the back)
         const CodeT* col = codes_fm + (int64_t)bf * n_rows;
         const unsigned long long lt = (1ull << lane) - 1ull;
@@ -897,15 +937,12 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           uint32_t ent[kFinUnroll];
           uint32_t cv[kFinUnroll];
 #pragma unroll
-          for (int u = 0; u < kFinUnroll; ++u) {
+          for (int u = 0; u < kFinUnroll; ++u) {  // (unconditional: see the histogram)
             const int r = r0 + u * kFinThreads + tid;
-            ent[u] = r < m ? src[start + r] : 0u;
+            ent[u] = src[start + (r < m ? r : 0)];
           }
 #pragma unroll
-          for (int u = 0; u < kFinUnroll; ++u) {
-            const int r = r0 + u * kFinThreads + tid;
-            cv[u] = r < m ? (uint32_t)col[ent[u] & rl.mask] : 0u;
-          }
+          for (int u = 0; u < kFinUnroll; ++u) cv[u] = (uint32_t)col[ent[u] & rl.mask];
 #pragma unroll
           for (int u = 0; u < kFinUnroll; ++u) {
             const int r = r0 + u * kFinThreads + tid;
@@ -972,10 +1009,14 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
           if (is_left ? tlf : trf) continue;
           const int cm_rows = is_left ? nl : nr;
           if (kC2 && pass == 0 && cm_rows > MT_FIN_HANDOFF * tiny_rows) {
-            const int head = __hip_atomic_load(job_counter, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-            const int pushed = (int)(__hip_atomic_load(q_word, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT) >> 32);
+            // (values from before the partition: a stale one only changes whether
+            // this child is handed off, never the tree)
+            const int head = MT_FIN_PF ? pf_head
+                                       : __hip_atomic_load(job_counter, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+            const int pushed = MT_FIN_PF ? pf_pushed
+                                         : (int)(__hip_atomic_load(q_word, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT) >> 32);
             if (head > J + pushed && pushed < task_cap) {
               const int k = (int)(__hip_atomic_fetch_add(q_word, 1ull << 32, __ATOMIC_RELAXED,
                                                          __HIP_MEMORY_SCOPE_AGENT) >> 32);
@@ -1000,7 +1041,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
             }
           }
           if (cm_rows <= tiny_rows) {  // hand the tiny subtree to a wavefront
-            const int64_t t = atomicAdd(tiny_count, 1);
+            const int64_t t = tiny_slot();
             int64_t* tr = tiny + t * 8;
             tr[0] = is_left ? start : start + nl;
             tr[1] = cm_rows;
@@ -1032,6 +1073,8 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         __hip_atomic_store(q_finished, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  if (tid == 0)  // reserved records left unused: empty (m = 0), skipped by the tiny kernels
+    for (int k = s_tnext; k < s_tend; ++k) tiny[(int64_t)k * 8 + 1] = 0;
   if (prof && tid == 0) {
     int64_t* P = prof + (int64_t)blockIdx.x * 10;
     P[0] = s_pr[0];
@@ -1121,6 +1164,7 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
     const int64_t* rec = tiny + (int64_t)k * 8;
     const int64_t start = rec[0];
     const int m = (int)rec[1];
+    if (m < 2) continue;  // (an unused reserved record)
     const int depth0 = (int)rec[2];
     const uint32_t* src = rec[3] ? buf1 : buf0;
     const int64_t root_slot = rec[4];
@@ -1807,6 +1851,7 @@ __global__ __launch_bounds__(kW * kWave) void finish_tiny_sorted_kernel(
     const int k = wave_claim_next(claim, tiny_counter, K, claim_batch);
     if (k >= K) break;
     const int64_t* rec = tiny + (int64_t)k * 8;
+    if (rec[1] < 2) continue;  // (an unused reserved record)
     tiny_sorted_subtree<CodeT>(codes_rm, row_words, rec[3] ? buf1 : buf0, y, rl, rec[0], (int)rec[1],
                         (int)rec[2], rec[4], F, C, crit, max_depth, mss, msl, s_h, s_hrow, srt, flag,
                         s_mask[wave], s_dep[wave], s_slot[wave], TinyOut{node_i32, node_cnt});

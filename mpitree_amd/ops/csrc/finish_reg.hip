@@ -72,8 +72,19 @@ __global__ __launch_bounds__(kRegThreads, 2) void finish_reg_kernel(
   __shared__ double w_gain[kRegWaves];
   __shared__ int w_feat[kRegWaves], w_bin[kRegWaves];
   __shared__ int s_lc, s_rc;
+  __shared__ int s_tnext, s_tend;  // this workgroup's reserved tiny records (thread 0)
 
   const int tid = threadIdx.x;
+  if (tid == 0) s_tnext = s_tend = 0;
+  // a tiny-subtree record (thread 0 only): one device atomic per kFinTinyBatch
+  auto tiny_slot = [&]() -> int64_t {
+    if (s_tnext == s_tend) {
+      const int t = atomicAdd(tiny_count, kFinTinyBatch);
+      s_tnext = t;
+      s_tend = t + kFinTinyBatch;
+    }
+    return (int64_t)(s_tnext++);
+  };
   const int wave = tid >> 6;
   const int lane = lane_id();
   const int n_tiles = (F + kRegFT - 1) / kRegFT;
@@ -135,7 +146,7 @@ __global__ __launch_bounds__(kRegThreads, 2) void finish_reg_kernel(
       node_st[(int64_t)r * 2 + 1] = jb[6];
       s_sp = 0;
       if (jb[1] <= tiny_rows) {  // the whole job goes to a wavefront
-        const int t = atomicAdd(tiny_count, 1);
+        const int t = (int)tiny_slot();
         int64_t* tr = tiny + (int64_t)t * 8;
         tr[0] = jb[0];
         tr[1] = jb[1];
@@ -395,7 +406,7 @@ __global__ __launch_bounds__(kRegThreads, 2) void finish_reg_kernel(
             }
           }
           if (cm <= tiny_rows) {
-            const int t = atomicAdd(tiny_count, 1);
+            const int t = (int)tiny_slot();
             int64_t* tr = tiny + (int64_t)t * 8;
             tr[0] = cstart;
             tr[1] = cm;
@@ -422,6 +433,8 @@ __global__ __launch_bounds__(kRegThreads, 2) void finish_reg_kernel(
         __hip_atomic_store(q_finished, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  if (tid == 0)  // reserved records left unused: empty (m = 0), skipped by the tiny kernel
+    for (int k = s_tnext; k < s_tend; ++k) tiny[(int64_t)k * 8 + 1] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -511,6 +524,7 @@ __global__ __launch_bounds__(256) void finish_tiny_reg_kernel(
     const int64_t* rec = tiny + (int64_t)k * 8;
     const int64_t start = rec[0];
     const int m = (int)rec[1];
+    if (m < 2) continue;  // (an unused reserved record)
     const int depth0 = (int)rec[2];
     const uint32_t* src = rec[3] ? buf1 : buf0;
     const int64_t root_slot = rec[4];

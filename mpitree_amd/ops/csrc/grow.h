@@ -15,6 +15,11 @@ constexpr int kFinCounterWords = 128;
 // {completed, handed off} queue word, the finished epoch and the watchdog, each
 // on its own 128-B line (the regression finisher keeps its tiny words at 1, 2)
 constexpr int kFinCtrTinyCount = 32;
+// tiny-subtree records a block-finisher workgroup reserves per global atomic (a
+// returning device-scope atomic costs ~1-3 us under load, on thread 0's serial
+// path between two barriers); unused reserved records are left with m = 0 and
+// the tiny kernels skip them. The tiny list holds J + rows / 2 + grid * this.
+constexpr int kFinTinyBatch = 16;
 constexpr int kFinCtrQueue = 64;
 constexpr int kFinCtrFinished = 96;
 constexpr int kFinCtrWatch = 100;

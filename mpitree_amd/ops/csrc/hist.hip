@@ -98,20 +98,22 @@ __global__ __launch_bounds__(kHistThreads) void hist_cls_lds_kernel(
     }
     uint32_t w[kUnroll][VEC];
     int lab[kUnroll];
+    // every row gather of the unrolled rows in flight before the first use: the
+    // loads are unconditional (an absent row reads row 0) -- a guarded load made
+    // the compiler wait for each row's gather in turn
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const bool ok = ent[u] != 0xffffffffu;
-      const uint32_t row = rl.shift ? (ent[u] & rl.mask) : ent[u];
-      lab[u] = ok ? (rl.shift ? (int)(ent[u] >> rl.shift) : y[row]) : 0;
+      const uint32_t row = ok ? (rl.shift ? (ent[u] & rl.mask) : ent[u]) : 0u;
+      lab[u] = rl.shift ? (int)(ent[u] >> rl.shift) : y[row];
       if constexpr (VEC == 4) {
-        uint4 v = ok ? *reinterpret_cast<const uint4*>(codes + (int64_t)row * row_words + my_w)
-                     : make_uint4(0, 0, 0, 0);
+        const uint4 v = *reinterpret_cast<const uint4*>(codes + (int64_t)row * row_words + my_w);
         w[u][0] = v.x;
         w[u][1] = v.y;
         w[u][2] = v.z;
         w[u][3] = v.w;
       } else {
-        w[u][0] = ok ? codes[(int64_t)row * row_words + my_w] : 0u;
+        w[u][0] = codes[(int64_t)row * row_words + my_w];
       }
     }
 #pragma unroll
@@ -301,10 +303,21 @@ __global__ __launch_bounds__(256) void hist_reduce_cls_kernel(
   const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (e >= Ep) return;
   uint32_t a0 = 0, a1 = 0;
-  for (int64_t j = k0; j < k1; ++j) {
-    const uint32_t v = slab[(first + j) * Ep + e];
-    a0 += v & 0xffffu;
-    a1 += v >> 16;
+  // every slab load of the group in flight before the first add (a rolled loop
+  // waited for each load in turn: one L2 / MALL round trip per slab)
+  constexpr int kGMax = 16;
+  for (int64_t jb = k0; jb < k1; jb += kGMax) {
+    uint32_t v[kGMax];
+#pragma unroll
+    for (int u = 0; u < kGMax; ++u) {
+      const int64_t j = jb + u;
+      v[u] = j < k1 ? slab[(first + j) * Ep + e] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kGMax; ++u) {
+      a0 += v[u] & 0xffffu;
+      a1 += v[u] >> 16;
+    }
   }
   const int64_t fb = e / W;
   const int wc = (int)(e - fb * W);

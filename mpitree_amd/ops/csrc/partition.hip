@@ -56,9 +56,14 @@ __global__ __launch_bounds__(kPartThreads) void partition_kernel(
     valid[k] = e < cn;
     ent[k] = valid[k] ? idx[c0 + e] : 0u;
   }
+  // the split feature's codes of all the thread's rows in flight at once
+  // (unconditional gathers; a guarded one waited for each row in turn)
+  uint32_t cv[kPartRows];
+#pragma unroll
+  for (int k = 0; k < kPartRows; ++k) cv[k] = (uint32_t)col[ent[k] & mask];
 #pragma unroll
   for (int k = 0; k < kPartRows; ++k) {
-    go[k] = valid[k] && (uint32_t)col[ent[k] & mask] <= bin;
+    go[k] = valid[k] && cv[k] <= bin;
     my_l += (valid[k] && go[k]) ? 1u : 0u;
     my_r += (valid[k] && !go[k]) ? 1u : 0u;
   }

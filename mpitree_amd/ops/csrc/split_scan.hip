@@ -27,6 +27,20 @@ __device__ __forceinline__ double tlog(uint64_t x, const double* __restrict__ ta
   return x < (uint64_t)tn ? __ldg(tab + x) : xlog2x(x);
 }
 
+// N table values with every load in flight before the first use: unconditional
+// loads (clamped index), the evaluated form only for counts past the table. The
+// per-value form above compiled to a guarded load and a wait per lookup -- 24
+// dependent L2 round trips per bin group of a two-class scan.
+template <int N>
+__device__ __forceinline__ void tlog_batch(const uint32_t (&x)[N], double (&out)[N],
+                                           const double* __restrict__ tab, int tn) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = __ldg(tab + min(x[i], (uint32_t)(tn - 1)));
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    if (x[i] >= (uint32_t)tn) out[i] = xlog2x(x[i]);
+}
+
 // hist: uint32 [slots][F_h][B][C]; nodes: int64 [k] slot ids
 // out_cost: f64 [k][F_h]; out_bin: i32 [k][F_h]
 // Fused sibling derivation (device level loop): with ``der``, slots >= *nbuilt
@@ -70,10 +84,27 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
       const uint32_t* sp = hist + (d[2] * F_h + f) * E;
       uint32_t* out = hist + (slot * F_h + f) * E;
       uint32_t* loc = der_lds ? sm + 4 * 2 * C + wave * E : nullptr;
-      for (int64_t e = lane; e < E; e += kWave) {
-        const uint32_t v = pp[e] - sp[e];
-        if (der_lds) loc[e] = v;
-        out[e] = v;
+      // kDU loads of each operand in flight per lane (a rolled loop waited for
+      // every element pair in turn: 8 round trips for a 256-bin two-class feature)
+      constexpr int kDU = 8;
+      for (int64_t e0 = lane; e0 < E; e0 += (int64_t)kWave * kDU) {
+        uint32_t a[kDU], bq[kDU];
+#pragma unroll
+        for (int u = 0; u < kDU; ++u) {
+          const int64_t e = e0 + (int64_t)u * kWave;
+          const int64_t es = e < E ? e : 0;
+          a[u] = pp[es];
+          bq[u] = sp[es];
+        }
+#pragma unroll
+        for (int u = 0; u < kDU; ++u) {
+          const int64_t e = e0 + (int64_t)u * kWave;
+          if (e < E) {
+            const uint32_t v = a[u] - bq[u];
+            if (der_lds) loc[e] = v;
+            out[e] = v;
+          }
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -86,6 +117,112 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
     }
   }
   auto hv = [&](int64_t i) -> uint32_t { return gp ? gp[i] - gs[i] : h[i]; };
+
+  // ---- <= 2 classes, <= 256 bins (the common shape): one load of the lane's 4
+  // bins x 2 classes (unconditional, clamped), totals from the prefix scans, and
+  // every x*log2(x) lookup issued in two batches -- no separate totals pass, no
+  // per-lookup round trip
+  if (C <= 2 && nb <= kChunk && gp == nullptr) {
+    const int b0 = lane * kBinsPerLane;
+    uint32_t v[2][kBinsPerLane], p[2][kBinsPerLane], incl[2], tc[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int cc = c < C ? c : C - 1;
+#pragma unroll
+      for (int k = 0; k < kBinsPerLane; ++k) {
+        const int b = b0 + k;
+        const uint32_t raw = h[(int64_t)(b < nb ? b : nb - 1) * C + cc];
+        v[c][k] = (b < nb && c < C) ? raw : 0u;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      p[c][0] = v[c][0];
+#pragma unroll
+      for (int k = 1; k < kBinsPerLane; ++k) p[c][k] = p[c][k - 1] + v[c][k];
+      incl[c] = wave_incl_scan_dpp(p[c][kBinsPerLane - 1]);
+      tc[c] = (uint32_t)__builtin_amdgcn_readlane((int)incl[c], kWave - 1);
+    }
+    const uint32_t m2 = tc[0] + tc[1];
+    const double tu2 = tie_unit(tlog((uint64_t)m2, xtab, xtab_n), (int64_t)m2);
+    const double tinv2 = 1.0 / tu2;
+    uint32_t L[2][kBinsPerLane], ml[kBinsPerLane];
+#pragma unroll
+    for (int k = 0; k < kBinsPerLane; ++k) ml[k] = 0u;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int k = 0; k < kBinsPerLane; ++k) {
+        L[c][k] = incl[c] - p[c][kBinsPerLane - 1] + p[c][k];
+        ml[k] += L[c][k];
+      }
+    double cost[kBinsPerLane];
+    if (crit == kEntropy) {
+      // class 0 then class 1, left then right: the host's summation order
+      uint32_t xs[4 * kBinsPerLane];
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int k = 0; k < kBinsPerLane; ++k) {
+          xs[(2 * c) * kBinsPerLane + k] = L[c][k];
+          xs[(2 * c + 1) * kBinsPerLane + k] = tc[c] - L[c][k];
+        }
+      double tv[4 * kBinsPerLane];
+      tlog_batch(xs, tv, xtab, xtab_n);
+      uint32_t xm[2 * kBinsPerLane];
+#pragma unroll
+      for (int k = 0; k < kBinsPerLane; ++k) {
+        xm[k] = ml[k];
+        xm[kBinsPerLane + k] = m2 - ml[k];
+      }
+      double tm2[2 * kBinsPerLane];
+      tlog_batch(xm, tm2, xtab, xtab_n);
+#pragma unroll
+      for (int k = 0; k < kBinsPerLane; ++k) {
+        double sl = 0.0, sr = 0.0;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          if (tc[c] == 0u) continue;  // (absent class: the generic pass skips it too)
+          sl = sl + tv[(2 * c) * kBinsPerLane + k];
+          sr = sr + tv[(2 * c + 1) * kBinsPerLane + k];
+        }
+        cost[k] = (tm2[k] - sl) + (tm2[kBinsPerLane + k] - sr);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kBinsPerLane; ++k) {
+        int64_t ql = 0, qr = 0;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int64_t a = L[c][k], r = (int64_t)tc[c] - a;
+          ql += a * a;
+          qr += r * r;
+        }
+        cost[k] = gini_term(ml[k], ql) + gini_term((int64_t)m2 - ml[k], qr);
+      }
+    }
+    double bc = __builtin_inf();
+    int bb = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < kBinsPerLane; ++k) {
+      const int b = b0 + k;
+      const int64_t mlk = ml[k];
+      const int64_t mrk = (int64_t)m2 - mlk;
+      if (b < nb && (v[0][k] | v[1][k]) && mlk >= msl && mrk >= msl) {
+        const double cr = tie_round(cost[k], tinv2, tu2);
+        if (cr < bc) {
+          bc = cr;
+          bb = b;
+        }
+      }
+    }
+    wave_argmin_dpp(bc, bb);  // one pass: lanes own ascending bins
+    if (lane == 0) {
+      out_cost[node * F_h + f] = bc;
+      out_bin[node * F_h + f] = bc < __builtin_inf() ? bb : -1;
+    }
+    return;
+  }
 
   // pass 1: per-class totals, kScanCG classes at a time (independent reductions)
   uint32_t m = 0;
@@ -166,18 +303,27 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
         const int c = c0 + g;
         const uint32_t excl = incl[g] - p[g][kBinsPerLane - 1] + carry[c];
         const uint32_t tc = tot[c];
+        uint32_t xs[2 * kBinsPerLane];
 #pragma unroll
         for (int k = 0; k < kBinsPerLane; ++k) {
           const uint32_t L = excl + p[g][k];
           const uint32_t R = tc - L;
+          xs[2 * k] = L;
+          xs[2 * k + 1] = R;
           mL[k] += L;
           nonempty[k] |= v[g][k];
-          if (crit == kEntropy) {
-            sL[k] = sL[k] + tl(L);
-            sR[k] = sR[k] + tl(R);
-          } else {
+          if (crit != kEntropy) {
             qL[k] += (int64_t)L * L;
             qR[k] += (int64_t)R * R;
+          }
+        }
+        if (crit == kEntropy) {
+          double tv[2 * kBinsPerLane];
+          tlog_batch(xs, tv, xtab, xtab_n);
+#pragma unroll
+          for (int k = 0; k < kBinsPerLane; ++k) {
+            sL[k] = sL[k] + tv[2 * k];
+            sR[k] = sR[k] + tv[2 * k + 1];
           }
         }
         const uint32_t chunk_total = __shfl(incl[g], kWave - 1, kWave);
@@ -189,6 +335,16 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
       class_pass(std::integral_constant<int, 1>{});
     else
       class_pass(std::integral_constant<int, kScanCG>{});
+    double tm[2 * kBinsPerLane];
+    if (crit == kEntropy) {
+      uint32_t xm[2 * kBinsPerLane];
+#pragma unroll
+      for (int k = 0; k < kBinsPerLane; ++k) {
+        xm[2 * k] = mL[k];
+        xm[2 * k + 1] = m - mL[k];
+      }
+      tlog_batch(xm, tm, xtab, xtab_n);
+    }
 #pragma unroll
     for (int k = 0; k < kBinsPerLane; ++k) {
       const int b = b0 + k;
@@ -197,7 +353,7 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
       if (b < nb && nonempty[k] && ml >= msl && mr >= msl) {
         double cost;
         if (crit == kEntropy)
-          cost = (tl((uint64_t)ml) - sL[k]) + (tl((uint64_t)mr) - sR[k]);
+          cost = (tm[2 * k] - sL[k]) + (tm[2 * k + 1] - sR[k]);
         else
           cost = gini_term(ml, qL[k]) + gini_term(mr, qR[k]);
         cost = tie_round(cost, tinv, tu);
@@ -337,7 +493,16 @@ __global__ __launch_bounds__(256) void select_kernel(
     const uint32_t* h = (const uint32_t*)hist_v + (slot * F_h) * (int64_t)B * C;
     for (int c = wave; c < C; c += 4) {
       uint32_t s = 0;
-      for (int b = lane; b < B; b += kWave) s += h[(int64_t)b * C + c];
+      for (int b0 = lane; b0 < B; b0 += 4 * kWave) {  // 4 bins per lane in flight
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int b = b0 + u * kWave;
+          v[u] = h[(int64_t)(b < B ? b : 0) * C + c];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s += (b0 + u * kWave < B) ? v[u] : 0u;
+      }
       s = wave_sum_u32(s);
       if (lane == 0) cls[c] = s;
     }
@@ -430,7 +595,16 @@ __global__ __launch_bounds__(256) void select_kernel(
     int64_t* left = cls + C;
     for (int c = wave; c < C; c += 4) {
       uint32_t s = 0;
-      for (int b = lane; b <= bb; b += kWave) s += h[(int64_t)b * C + c];
+      for (int b0 = lane; b0 <= bb; b0 += 4 * kWave) {  // 4 bins per lane in flight
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int b = b0 + u * kWave;
+          v[u] = h[(int64_t)(b <= bb ? b : 0) * C + c];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s += (b0 + u * kWave <= bb) ? v[u] : 0u;
+      }
       s = wave_sum_u32(s);
       if (lane == 0) left[c] = s;
     }

@@ -27,6 +27,13 @@ MAX_ITEM_ROWS = 65535  # 16-bit packed LDS counters
 N_CU = 256  # MI355X compute units
 
 
+def _tiny_batch(hip) -> int:
+    """Tiny-subtree records a finisher workgroup reserves at a time (grow.h
+    kFinTinyBatch; 1 for an extension built before the batched reservation)."""
+    f = getattr(hip, "fin_tiny_batch", None)
+    return int(f()) if f is not None else 1
+
+
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 _cur_dev = getattr(torch._C, "_cuda_getDevice", None)
 
@@ -696,11 +703,12 @@ class HipBackend:
             self._launch_finisher_reg(d_jobs, J, job_rows, params, rec, cnt, counter, grid, slot)
             return
         tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
-        # every tiny subtree has >= 2 rows and they partition the job rows
-        tiny = torch.empty((int(job_rows // 2 + J + 1), 8), dtype=torch.int64,
-                           device=self.device)
         md = -1 if params.max_depth is None else int(params.max_depth)
         grid = int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU)) if grid is None else int(grid)
+        # every tiny subtree has >= 2 rows and they partition the job rows; each
+        # workgroup reserves records kFinTinyBatch at a time
+        tiny = torch.empty((int(job_rows // 2 + J + 1 + grid * _tiny_batch(self.hip)), 8),
+                           dtype=torch.int64, device=self.device)
         if C > 2:  # (the hand-off queue is on the two-class kernel only)
             grid = min(grid, J)
         # subtrees handed to idle workgroups (each > 2 tiny_rows rows, disjoint)
@@ -736,7 +744,6 @@ class HipBackend:
     def _launch_finisher_reg(self, d_jobs, J, job_rows, params, rec, st64, counter, grid_o=None,
                              slot=0):
         tiny_rows = int(os.environ.get("MPITREE_TINY_ROWS", 64))
-        tiny = torch.empty((int(job_rows // 2 + J + 1), 8), dtype=torch.int64, device=self.device)
         md = -1 if params.max_depth is None else int(params.max_depth)
         grid = os.environ.get("MPITREE_FIN_GRID") if grid_o is None else grid_o
         if grid is None:  # as many persistent workgroups as fit a CU (LDS tile, VGPRs)
@@ -751,6 +758,8 @@ class HipBackend:
             task_cap = 0
         elif steal == "-1":
             task_cap, grid = -1, min(grid, J)
+        cap = int(job_rows // 2 + J + 1 + grid * _tiny_batch(self.hip))
+        tiny = torch.empty((cap, 8), dtype=torch.int64, device=self.device)
         tasks = torch.empty((max(task_cap, 1), 7), dtype=torch.int64, device=self.device)
         flags, epoch = _task_flags(self.device, max(task_cap, 0) + grid, slot)
         self.hip.finish_reg(_stream(), self.codes_rm.data_ptr(), self.row_elems * self.cb // 4,
