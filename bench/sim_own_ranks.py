@@ -111,10 +111,10 @@ def main():
     for _ in range(2):
         fit()
     ref, ref_rows = reference_rows(fit, dev, a.regression)
-    for P in [int(v) for v in a.ranks.split(",")]:
+    for P in [int(v) for v in a.ranks.replace("+", ",").split(",")]:
         per_rank = []
         for r in range(P) if a.only_rank is None else [a.only_rank]:
-            times, st = [], {}
+            times, st, ph = [], {}, []
             for i in range(a.reps + 2):
                 comm = SimOwnComm(P, r, dev, ref_rows) if P > 1 else None
                 torch.cuda.synchronize()
@@ -124,17 +124,23 @@ def main():
                 if i >= 2:
                     times.append((time.perf_counter() - t0) * 1e3)
                 st = res.stats
+                if i >= 2:
+                    ph.append({k: v * 1e3 for k, v in res.timings.items()
+                               if isinstance(v, float)})
                 assert res.arrays.equal(ref.arrays), f"P={P} rank {r}: tree differs"
             per_rank.append(dict(ms=float(np.median(times)), rows=st.get("own_rows", a.n),
                                  units=st.get("own_units", 0), levels=st.get("levels"),
                                  mode=st.get("mode", "single-gpu"),
-                                 exchange_mb=st.get("comm_bytes_exchange", 0) / 1e6))
+                                 exchange_mb=st.get("comm_bytes_exchange", 0) / 1e6,
+                                 phases={k: round(float(np.median([d.get(k, 0.0) for d in ph])), 3)
+                                         for k in ph[0]}))
         ms = [p["ms"] for p in per_rank]
         out = dict(P=P, max_rank_ms=round(max(ms), 3), mean_rank_ms=round(float(np.mean(ms)), 3),
                    rank_ms=[round(v, 3) for v in ms], rows_owned=[p["rows"] for p in per_rank],
                    units=per_rank[0]["units"], levels=[p["levels"] for p in per_rank],
                    mode=per_rank[0]["mode"], exchange_mb=round(per_rank[0]["exchange_mb"], 2),
-                   nodes=ref.arrays.node_count, tree_equal=True)
+                   nodes=ref.arrays.node_count, tree_equal=True,
+                   phases_max_rank=per_rank[int(np.argmax(ms))]["phases"])
         print(json.dumps(out), flush=True)
 
 

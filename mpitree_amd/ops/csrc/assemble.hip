@@ -36,16 +36,48 @@ __device__ __forceinline__ bool asm_live(const int32_t* __restrict__ rec,
   return p < P && rec[p * 6 + 5] > 0 && (mask == nullptr || mask[p] != 0);
 }
 
+// {depth, n} of the thread's kAsmPer positions of a tile (and the mask bytes),
+// every load issued before the first use: unconditional, clamped to P - 1 (the
+// short-circuit form above compiled to one load and wait per position)
+__device__ __forceinline__ void asm_load_tile(const int32_t* __restrict__ rec,
+                                              const uint8_t* __restrict__ mask, int64_t base,
+                                              int64_t P, bool (&live)[kAsmPer],
+                                              int (&depth)[kAsmPer]) {
+  int2 dn[kAsmPer];
+  uint8_t mk[kAsmPer];
+#pragma unroll
+  for (int k = 0; k < kAsmPer; ++k) {
+    const int64_t p = base + (int64_t)k * kAsmThreads + threadIdx.x;
+    const int64_t pc = p < P ? p : P - 1;
+    dn[k] = *reinterpret_cast<const int2*>(rec + pc * 6 + 4);
+    mk[k] = 1;
+  }
+  if (mask != nullptr) {
+#pragma unroll
+    for (int k = 0; k < kAsmPer; ++k) {
+      const int64_t p = base + (int64_t)k * kAsmThreads + threadIdx.x;
+      mk[k] = mask[p < P ? p : P - 1];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kAsmPer; ++k) {
+    const int64_t p = base + (int64_t)k * kAsmThreads + threadIdx.x;
+    live[k] = p < P && dn[k].y > 0 && mk[k] != 0;
+    depth[k] = dn[k].x;
+  }
+}
+
 __global__ __launch_bounds__(kAsmThreads) void asm_count_kernel(const int32_t* __restrict__ rec,
                                                                 int64_t P,
                                                                 int32_t* __restrict__ tile_cnt,
                                                                 const uint8_t* __restrict__ mask) {
   const int64_t base = (int64_t)blockIdx.x * kAsmTile;
   int c = 0;
-  for (int k = 0; k < kAsmPer; ++k) {
-    const int64_t p = base + (int64_t)k * kAsmThreads + threadIdx.x;  // coalesced
-    c += asm_live(rec, mask, p, P) ? 1 : 0;
-  }
+  bool live[kAsmPer];
+  int depth[kAsmPer];
+  asm_load_tile(rec, mask, base, P, live, depth);  // (coalesced positions)
+#pragma unroll
+  for (int k = 0; k < kAsmPer; ++k) c += live[k] ? 1 : 0;
   c = (int)wave_sum_u32((uint32_t)c);
   __shared__ int w[kAsmThreads / kWave];
   if (lane_id() == 0) w[threadIdx.x >> 6] = c;
@@ -104,12 +136,14 @@ __global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __
   const int lane = lane_id(), wv = (int)(threadIdx.x >> 6);
   uint32_t flags = 0;
   int dmax = 0;
+  bool live[kAsmPer];
+  int depth[kAsmPer];
+  asm_load_tile(rec, mask, base, P, live, depth);
 #pragma unroll
   for (int k = 0; k < kAsmPer; ++k) {
-    const int64_t p = base + (int64_t)k * kAsmThreads + threadIdx.x;
-    const bool v = asm_live(rec, mask, p, P);
+    const bool v = live[k];
     flags |= (uint32_t)v << k;
-    if (v) dmax = max(dmax, rec[p * 6 + 4]);
+    if (v) dmax = max(dmax, depth[k]);
     const unsigned long long b = __ballot(v);
     if (lane == 0) s_mask[k][wv] = b;
   }

@@ -17,6 +17,7 @@ namespace py = pybind11;
 
 namespace mt {
 int hist_feature_tile(int F_h, int B, int C, bool reg, int lds_budget);
+int hist_class_tile(int F_h, int B, int C, bool reg, int lds_budget);
 int64_t hist_slab_words(int F_h, int B, int C, bool reg);
 void launch_hist(hipStream_t, const void*, int, int64_t, const uint32_t*, const void*, int,
                  const int64_t*, int, void*, void*, int, int, int, int, bool, int,
@@ -27,7 +28,9 @@ void launch_hist_derive(hipStream_t, const int64_t*, int, const void*, void*, in
                         const int32_t*);
 void launch_scan(hipStream_t, const void*, const int64_t*, int, const int32_t*, int, int, int,
                  int, int, int, double*, int32_t*, int64_t*, const double*, int,
-                 const int32_t*, const int64_t*, const void*, const int32_t*);
+                 const int32_t*, const int64_t*, const void*, const int32_t*, int32_t*,
+                 int32_t*);
+bool scan_fused_select_ok(int B, int C, int crit);
 void launch_partition(hipStream_t, const void*, int, int64_t, uint32_t*, uint32_t*, uint32_t,
                       const int64_t*, int, const int64_t*, int32_t*, const int32_t*, bool);
 void launch_seg_stats(hipStream_t, const uint32_t*, const void*, int, bool, const int64_t*, int,
@@ -48,6 +51,7 @@ void launch_finish(hipStream_t, const void*, int64_t, const void*, int, int64_t,
 int finish_lds_bytes(int F, int B, int C);
 void launch_hw_xlog2x(hipStream_t, float*, int);
 int finish_feature_tile(int F, int B, int C);
+int finish_job_rows_cap(int C);
 int asm_tiles(int64_t P);
 void launch_grow_plan(hipStream_t, const PlanArgs&);
 size_t exact_setup_temp_bytes(int64_t, int);
@@ -100,6 +104,7 @@ static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "mpitree_amd gfx950 HIP kernels";
   m.def("hist_feature_tile", &mt::hist_feature_tile);
+  m.def("hist_class_tile", &mt::hist_class_tile);
   m.def("hist_slab_words", &mt::hist_slab_words);
   m.def("hist", [](uintptr_t s, uintptr_t codes, int cb, int64_t rs, uintptr_t idx, uintptr_t y,
                    int lab_shift, uintptr_t items, int n_items, uintptr_t hist, uintptr_t slab,
@@ -134,7 +139,7 @@ PYBIND11_MODULE(_hip, m) {
     mt::launch_scan(S(s), P<void>(hist), P<int64_t>(nodes), k, P<int32_t>(nbins), F_h, f_lo, B, C,
                     crit, msl, P<double>(cost), P<int32_t>(bins), P<int64_t>(rec),
                     P<double>(xtab), xtab_n, P<int32_t>(dcount), P<int64_t>(der), P<void>(prev),
-                    P<int32_t>(nbuilt));
+                    P<int32_t>(nbuilt), nullptr, nullptr);
   }, "", py::arg("s"), py::arg("hist"), py::arg("nodes"), py::arg("k"), py::arg("nbins"),
      py::arg("F_h"), py::arg("f_lo"), py::arg("B"), py::arg("C"), py::arg("crit"), py::arg("msl"),
      py::arg("cost"), py::arg("bins"), py::arg("rec"), py::arg("xtab"), py::arg("xtab_n"),
@@ -177,6 +182,7 @@ PYBIND11_MODULE(_hip, m) {
       py::arg("estride") = 0, py::arg("skip_inexact") = false);
   m.def("finish_lds_bytes", &mt::finish_lds_bytes);
   m.def("finish_feature_tile", &mt::finish_feature_tile);
+  m.def("finish_job_rows_cap", &mt::finish_job_rows_cap);
   m.def("finish", [](uintptr_t s, uintptr_t codes_rm, int64_t row_words, uintptr_t codes_fm,
                      int cb, int64_t n_rows, uintptr_t idx, uintptr_t tmp, uintptr_t y,
                      int lab_shift, uintptr_t jobs, int J, uintptr_t counter, uintptr_t nbins,
@@ -242,6 +248,7 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("C"), py::arg("dred"), py::arg("dtasks"), py::arg("zero") = true);
   m.def("job_sort_max", &mt::job_sort_max);
   m.def("fin_tiny_batch", []() { return mt::kFinTinyBatch; });
+  m.def("scan_fused_select_ok", &mt::scan_fused_select_ok);
   m.def("job_sort", [](uintptr_t s, uintptr_t jobs, int J, int W, uintptr_t out,
                        uintptr_t counters) {
     mt::launch_job_sort(S(s), P<int64_t>(jobs), J, W, P<int64_t>(out), P<int32_t>(counters));

@@ -103,6 +103,7 @@ struct XePlanArgs {
 
 // launchers (exact2.hip)
 int xe_chunk();
+int xe_part_units();  // partition wave units (status words) per chunk item
 int xe_local_max();
 int xe_max_classes();
 int xe_packed_classes();

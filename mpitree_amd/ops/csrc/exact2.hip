@@ -614,20 +614,35 @@ __device__ __forceinline__ void xe_scan_wave_c2(const XeArgs& a, const XeLists& 
   // caller only runs chunks whose fp32 minimum is within it
   float wmin = __builtin_inff();  // kPass 1: the chunk's fp32 minimum
   constexpr int kRound = kWave * kXePer;  // 512
-  for (int r0 = 0; r0 < cn; r0 += kRound) {
-    uint32_t e[kXePer];
+  constexpr int kRounds = kXeChunk / kRound;  // an item holds at most kXeChunk entries
+  // pass 1 (every chunk, the hot pass): every round's entries and the entry after
+  // the item in flight at once -- unconditional loads clamped into the item (the
+  // rounds used to load, wait and compute one after another); the other passes
+  // keep one round in registers (pass 2 runs on few chunks, at its register budget)
+  // (holding every round for pass 1 measured slower: 102 -> 116 us a level at 126
+  // VGPRs, half the waves; MT_XE_HOLD_ROUNDS=1 builds it)
+#ifndef MT_XE_HOLD_ROUNDS
+#define MT_XE_HOLD_ROUNDS 0
+#endif
+  constexpr bool kAll = MT_XE_HOLD_ROUNDS && kPass == 1;
+  constexpr int kHeld = kAll ? kRounds : 1;
+  uint32_t ea[kHeld][kXePer];
+  auto load_round = [&](int r, uint32_t (&dst)[kXePer]) {
 #pragma unroll
     for (int k = 0; k < kXePer; ++k) {
-      const int i = r0 + k * kWave + lane;
-      e[k] = i < cn ? Ef[c0 + i] : 0xFFFFFFFFu;
+      const int i = r * kRound + k * kWave + lane;
+      dst[k] = Ef[c0 + (i < cn ? i : cn - 1)];
     }
-    // entries past the round: lane 63 of the last row reads its successor
-    const int iend = r0 + kRound;  // first index of the next round
-    uint32_t after = 0xFFFFFFFFu;
-    if (lane == kWave - 1) {
-      if (iend < cn) after = Ef[c0 + iend];
-      else if (p0 + cn < m) after = Ef[c0 + cn];
-    }
+  };
+  uint32_t tail = 0xFFFFFFFFu;
+  if constexpr (kAll) {
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) load_round(r, ea[r]);
+    tail = Ef[c0 + (p0 + cn < m ? cn : cn - 1)];  // the next item's first entry
+  }
+  // one round of the item: its entries e[] (past the item: all ones) and the
+  // entry after the round (the next round's first, or the next item's first)
+  auto round = [&](const int r0, uint32_t (&e)[kXePer], const uint32_t after) {
     unsigned long long bal[kXePer];
     int l1[kXePer];
     bool valid[kXePer];
@@ -678,7 +693,7 @@ __device__ __forceinline__ void xe_scan_wave_c2(const XeArgs& a, const XeLists& 
     }
     if constexpr (kPass == 1) {
       wmin = fminf(wmin, fm);
-      continue;
+      return;
     }
     const float thr = kPass == 2 ? gthr : fm + thr_pad;
 #pragma unroll
@@ -690,6 +705,40 @@ __device__ __forceinline__ void xe_scan_wave_c2(const XeArgs& a, const XeLists& 
         mine = key;
         mine_pos = pos;
       }
+    }
+    };
+  if constexpr (kAll) {
+#pragma unroll
+    for (int rr = 0; rr < kRounds; ++rr) {
+      const int r0 = rr * kRound;
+      if (r0 >= cn) break;
+      uint32_t e[kXePer];
+#pragma unroll
+      for (int k = 0; k < kXePer; ++k)
+        e[k] = r0 + k * kWave + lane < cn ? ea[rr][k] : 0xFFFFFFFFu;
+      uint32_t after = 0xFFFFFFFFu;
+      if (r0 + kRound < cn)
+        after = (uint32_t)__builtin_amdgcn_readlane((int)ea[rr + 1 < kRounds ? rr + 1 : rr][0], 0);
+      else if (p0 + cn < m)
+        after = tail;
+      round(r0, e, after);
+    }
+  } else {
+    for (int r0 = 0; r0 < cn; r0 += kRound) {
+      uint32_t e[kXePer];
+#pragma unroll
+      for (int k = 0; k < kXePer; ++k) {
+        const int i = r0 + k * kWave + lane;
+        e[k] = i < cn ? Ef[c0 + i] : 0xFFFFFFFFu;
+      }
+      // entries past the round: lane 63 of the last row reads its successor
+      const int iend = r0 + kRound;  // first index of the next round
+      uint32_t after = 0xFFFFFFFFu;
+      if (lane == kWave - 1) {
+        if (iend < cn) after = Ef[c0 + iend];
+        else if (p0 + cn < m) after = Ef[c0 + cn];
+      }
+      round(r0, e, after);
     }
   }
   if constexpr (kPass == 1) {
@@ -1276,7 +1325,7 @@ __global__ __launch_bounds__(256) void xe_flag_pack_kernel(const uint8_t* __rest
 constexpr int kXePartWaves = 16;                       // waves per workgroup
 constexpr int kXePartPer = 16;                         // entries per lane and unit
 constexpr int kXeSub = kWave * kXePartPer;             // entries per wave unit (1024)
-constexpr int kXeSubPerChunk = kXeChunk / kXeSub;      // 2
+constexpr int kXeSubPerChunk = kXeChunk / kXeSub;      // wave units per chunk item (2)
 constexpr int kXePartLdsWords = 36 * 1024;             // 144 KB of flag words in LDS
 constexpr int64_t kXePartLdsRows = (int64_t)kXePartLdsWords * 32;
 #ifndef MT_XE_PART_BATCH  // (4 / 8 / 32 / 64 measured slower: profiles/kernel_experiments.md)
@@ -1312,19 +1361,18 @@ __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a,
     const int nq = nw >> 2;
     const uint4* src = reinterpret_cast<const uint4*>(a.flag);
     uint4* dst = reinterpret_cast<uint4*>(s_flag);
-    for (int i0 = threadIdx.x; i0 < nq; i0 += (int)blockDim.x * kU) {
+    // full rounds without guards (guarded loads / stores were issued one at a
+    // time: a load, its wait, its LDS store), then the remainder
+    const int bd = (int)blockDim.x;
+    int i0 = threadIdx.x;
+    for (; i0 + (kU - 1) * bd < nq; i0 += bd * kU) {
       uint4 v[kU];
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int i = i0 + u * (int)blockDim.x;
-        if (i < nq) v[u] = src[i];
-      }
+      for (int u = 0; u < kU; ++u) v[u] = src[i0 + u * bd];
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int i = i0 + u * (int)blockDim.x;
-        if (i < nq) dst[i] = v[u];
-      }
+      for (int u = 0; u < kU; ++u) dst[i0 + u * bd] = v[u];
     }
+    for (int i = i0; i < nq; i += bd) dst[i] = src[i];
     for (int i = (nq << 2) + threadIdx.x; i < nw; i += blockDim.x) s_flag[i] = a.flag[i];
     __syncthreads();
   }
@@ -1823,6 +1871,7 @@ __global__ __launch_bounds__(256) void xe_emit_kernel(const uint32_t* __restrict
 
 // --------------------------------------------------------------- launchers
 int xe_chunk() { return kXeChunk; }
+int xe_part_units() { return kXeSubPerChunk; }
 int xe_local_max() { return kXeLocalMax; }
 int xe_max_classes() { return kXeMaxClasses; }
 int xe_packed_classes() { return kXeMaxC; }

@@ -64,6 +64,7 @@ XeLists lists_of(const py::dict& d) {
 
 void bind_exact2(py::module_& m) {
   m.def("xe_chunk", &xe_chunk);
+  m.def("xe_part_units", &xe_part_units);
   m.def("xe_local_max", &xe_local_max);
   m.def("xe_max_classes", &xe_max_classes);
   m.def("xe_packed_classes", &xe_packed_classes);

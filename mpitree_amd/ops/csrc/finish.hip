@@ -42,7 +42,12 @@ constexpr int kFinThreadsWide = 1024;  // one workgroup per CU (F = 128 histogra
 // job_counter word layout: kFinCtr* in grow.h (int32 [kFinCounterWords], zeroed
 // before each launch)
 constexpr int kFinStack = 40;    // >= log2(max job rows) + 2
-constexpr int kFinMaxC = 256;    // classes supported by the block finisher
+constexpr int kFinMaxC = 256;    // classes of the full-width histogram layout
+// past kFinMaxC classes the jobs hold at most kFinClassJobRows rows, so every
+// node has at most that many present classes and counts below 256: its
+// compacted histogram (four 8-bit counts a word) is sized like one of
+// kFinClassJobRows classes, whatever C is
+constexpr int kFinClassJobRows = 255;
 constexpr int kFinStackC = 16;   // C <= this: DFS-stack class counts in LDS, else global scratch
 constexpr int kFinMaxB = 4096;   // bins (16-bit codes past 256: multi-pass scans, feature tiles)
 constexpr int kTinyMaxC = 16;    // classes supported by the generic tiny kernel
@@ -92,6 +97,8 @@ __device__ __forceinline__ float tfv(uint32_t x) {
 // LDS banks for the atomics), rounded to 4 so each feature row is 16-B aligned.
 __host__ __device__ inline int fin_fstride(int B, int W) { return ((B * W + 1) + 3) & ~3; }
 __host__ __device__ inline int fstride_of(int B, int C) { return fin_fstride(B, (C + 1) >> 1); }
+// classes the LDS histogram tile is sized for
+__host__ __device__ inline int fin_tile_classes(int C) { return C > kFinMaxC ? kFinClassJobRows : C; }
 
 inline int getenv_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -177,7 +184,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
   // C > 2 (generic path): the node's present class ids + their count at [C],
   // then the class -> compacted slot map [C]
   int32_t* const cls_lds =
-      (!kC2 && C > 2) ? reinterpret_cast<int32_t*>(hist + Ft * fstride_of(B, C)) +
+      (!kC2 && C > 2) ? reinterpret_cast<int32_t*>(hist + Ft * fstride_of(B, fin_tile_classes(C))) +
                             (B > 256 ? (kFinThreadsWide / kWave) * C : 0)
                       : nullptr;
   int32_t* const cmap = cls_lds ? cls_lds + C + 1 : nullptr;
@@ -190,7 +197,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
   int32_t* const s_left = (!kC2 && gstk && cmap) ? cmap + 2 * C : s_left_l;
   const int wave = tid >> 6;
   const int lane = lane_id();
-  const int W = (C + 1) >> 1;
+  const int W = (fin_tile_classes(C) + 1) >> 1;
   const int fstride = fin_fstride(B, W);
   constexpr int cpw = 4 / sizeof(CodeT);
   const int tn = min(kFinTab, xtab_n);
@@ -1882,9 +1889,8 @@ static int tiny_sorted_waves(int F, int cb = 1) {
 // else tiles sized for two 512-thread workgroups per CU (<= 62 KB), or -- when
 // that leaves fewer than 4 features per tile (many classes) -- for one
 // 1024-thread workgroup per CU (<= 140 KB).
-int finish_feature_tile(int F, int B, int C) {
-  if (F <= 0 || C > kFinMaxC || B <= 0 || B > kFinMaxB) return 0;
-  const int per_f = fin_fstride(B, (C + 1) / 2) * 4;
+static int finish_feature_tile_of(int F, int B, int Ct) {
+  const int per_f = fin_fstride(B, (Ct + 1) / 2) * 4;
   if (F <= kFinMaxF && F * per_f <= 150 * 1024) return F;
   int ft = 62 * 1024 / per_f;
   if (ft < 4) ft = 140 * 1024 / per_f;
@@ -1894,14 +1900,27 @@ int finish_feature_tile(int F, int B, int C) {
   if (ft >= 16) ft &= ~15;  // 16-B row loads stay aligned at every tile start
   return std::min(ft, F);
 }
-int finish_lds_bytes(int F, int B, int C) {
+static int finish_lds_bytes_of(int F, int B, int C, int ft) {
   // + per-wave class carries of the multi-pass (B > 256) scan, + the node's
   // present-class list (C > 2)
-  return finish_feature_tile(F, B, C) * fin_fstride(B, (C + 1) / 2) * 4 +
+  return ft * fin_fstride(B, (fin_tile_classes(C) + 1) / 2) * 4 +
          (B > 256 ? (kFinThreadsWide / kWave) * C * 4 : 0) + (C > 2 ? (2 * C + 1) * 4 : 0) +
          (C > kFinStackC ? 2 * C * 4 : 0);
 }
+int finish_feature_tile(int F, int B, int C) {
+  if (F <= 0 || C <= 0 || B <= 0 || B > kFinMaxB) return 0;
+  if (C > kFinMaxC && B > 256) return 0;  // (many classes: one 256-bin pass only)
+  const int ft = finish_feature_tile_of(F, B, fin_tile_classes(C));
+  // the class arrays grow with C: past what one CU's LDS holds, no finisher
+  if (ft <= 0 || finish_lds_bytes_of(F, B, C, ft) > 150 * 1024) return 0;
+  return ft;
+}
+int finish_lds_bytes(int F, int B, int C) {
+  return finish_lds_bytes_of(F, B, C, finish_feature_tile(F, B, C));
+}
 int finish_max_classes() { return kFinMaxC; }
+// Largest finisher job (rows) for C classes (the x log2 x table bound otherwise).
+int finish_job_rows_cap(int C) { return C > kFinMaxC ? kFinClassJobRows : (1 << 16) - 1; }
 
 // Global scratch for the DFS stack's class counts and the node's / left class
 // counts (C > kFinStackC): [grid][kFinStack + 2][C], grow-only, one buffer per
@@ -1935,7 +1954,8 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   // job j's root position); rows a fit never writes keep n = 0 (host memset).
   if (J <= 0) return;
   const int Ft = finish_feature_tile(F, B, C);
-  if (Ft <= 0) throw std::runtime_error("finisher: unsupported shape (C > 256 or B > 256)");
+  if (Ft <= 0) throw std::runtime_error("finisher: unsupported shape (class arrays or bins "
+                                        "past the LDS budget)");
   // the two-class kernel (fp32 prefilter, hand-off queue) needs the single-pass
   // layout (Ft == F <= kFinMaxF: per-feature LDS arrays)
   const bool c2 = C <= 2 && Ft == F && F <= kFinMaxF && B <= 256;

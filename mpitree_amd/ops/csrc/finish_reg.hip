@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kRegThreads, 2) void finish_reg_kernel(
   const int n_tiles = (F + kRegFT - 1) / kRegFT;
   const int tile_words = kRegFT * B;  // per array
   const bool vec4 = (row_words % 4) == 0 && sizeof(CodeT) == 1;
-  for (int f = tid; f < F; f += kRegThreads) s_nb[f] = min(B, nbins[f]);
+  for (int f = tid; f < min(F, kRegMaxF); f += kRegThreads) s_nb[f] = min(B, nbins[f]);
   __syncthreads();
 
   // Hand-off queue (as in finish_cls_kernel): a workgroup that splits a node
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(kRegThreads, 2) void finish_reg_kernel(
         // ---- scan the tile: wave w takes features f0 + w, f0 + w + 4, ...
         for (int fl = wave; fl < nf; fl += kRegWaves) {
           const int f = f0 + fl;
-          const int nb = s_nb[f];
+          const int nb = f < kRegMaxF ? s_nb[f] : min(B, nbins[f]);  // (wide: from memory)
           const int b0 = lane * 4;
           uint32_t cn[4];
           long long cs[4];
@@ -860,8 +860,10 @@ void launch_finish_reg(hipStream_t stream, const void* codes_rm, int64_t row_wor
                        int tiny_rows, int64_t* tiny, int tiny_grid, int64_t* tasks,
                        int32_t* task_flag, int32_t epoch, int task_cap) {
   if (J <= 0) return;
-  if (F > kRegMaxF) throw std::runtime_error("regression finisher supports at most 256 features");
   if (code_bytes != 1) tiny_rows = 0;
+  // the tiny kernel keeps every feature's lane order in LDS: past what a CU holds
+  // (about 512 features) the block kernel grows the subtrees to the leaves
+  if ((size_t)kRegTinyWaves * reg_tiny_wave_bytes(F) > 160 * 1024) tiny_rows = 0;
   tiny_rows = std::min(tiny_rows, kRegTinyRows);
   const size_t lds = (size_t)finish_reg_lds_bytes(B);
 #define MT_FR(CT)                                                                           \

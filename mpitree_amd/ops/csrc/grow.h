@@ -95,6 +95,17 @@ struct PlanArgs {
   int32_t host_tag;    // written last: the host polls it to know the slot is complete
   int dp;              // rows sharded across ranks: local segments fixed up after partition
   OwnArgs own;         // subtree ownership (own.P < 2: off)
+  // fused selection (two-class levels with no collective between scan and plan):
+  // the planner builds each node's split record (``rec``) itself from the scan's
+  // per-feature results -- cost / bin [K][F], left counts at the best bin
+  // [K][F][2], node class totals and node term [K][4] = {t0, t1, term (f64)} --
+  // and no select kernel runs
+  const double* sel_cost = nullptr;
+  const int32_t* sel_bins = nullptr;
+  const int32_t* sel_left = nullptr;
+  const int32_t* sel_tot = nullptr;
+  int sel_F = 0;
+  int crit = 0;
 };
 
 }  // namespace mt

@@ -440,12 +440,65 @@ __device__ bool own_switch(const PlanArgs& a, OwnShared& os, PlanShared& sh, int
   return true;
 }
 
+// Fused selection: the split record of every frontier node from the scan's
+// per-feature results (what select_kernel computes from the histograms): node
+// term from the class totals (x log2 x evaluated, as the select kernel does),
+// best gain over the features in ascending order with a strict > (ties to the
+// lowest feature), the winning bin and its left counts. One thread per node.
+__device__ void plan_fused_select(const PlanArgs& a, int K) {
+  const int C = a.C;
+  const int R = 5 + 2 * C;
+  const int F = a.sel_F;
+  int64_t* rec = const_cast<int64_t*>(a.rec);
+  constexpr int kU = 32;  // cost loads in flight per thread
+  for (int i = threadIdx.x; i < K; i += kPlanThreads) {
+    int64_t tot[2];
+    tot[0] = a.sel_tot[(int64_t)i * 4 + 0];
+    tot[1] = C > 1 ? a.sel_tot[(int64_t)i * 4 + 1] : 0;
+    const int64_t mm = tot[0] + tot[1];
+    const double pterm = reinterpret_cast<const double*>(a.sel_tot)[(int64_t)i * 2 + 1];
+    double g = -__builtin_inf();
+    int bf = -1;
+    for (int f0 = 0; f0 < F; f0 += kU) {
+      double cv[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) cv[u] = a.sel_cost[(int64_t)i * F + min(f0 + u, F - 1)];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (f0 + u < F && cv[u] < __builtin_inf()) {
+          const double gf = pterm - cv[u];
+          if (gf > g) {
+            g = gf;
+            bf = f0 + u;
+          }
+        }
+      }
+    }
+    int64_t* out = rec + (int64_t)i * R;
+    const bool ok = g > -__builtin_inf();
+    out[0] = (int64_t)double_to_bits(g);
+    out[1] = ok ? bf : -1;
+    out[2] = ok ? a.sel_bins[(int64_t)i * F + bf] : -1;
+    int64_t nl = 0;
+    for (int c = 0; c < C; ++c) {
+      const int64_t l = ok ? a.sel_left[((int64_t)i * F + bf) * 2 + c] : 0;
+      out[5 + c] = l;
+      out[5 + C + c] = tot[c];
+      nl += l;
+    }
+    out[3] = nl;
+    out[4] = mm;
+  }
+  __syncthreads();  // (records read by other threads below, e.g. the ownership pass)
+}
+
 __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
   __shared__ PlanShared sh;
   const int tid = threadIdx.x;
   const int C = a.C;
   const int JW = plan_job_width(a);
   const int K = a.cur.ctl[0];
+  if (a.sel_left) plan_fused_select(a, K);
   // ---- pass 0 (subtree ownership, before the switch): maybe switch this level
   __shared__ OwnShared own_sh;
   bool own_sw = false;
@@ -476,9 +529,12 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     }
     return d;
   };
-  // ---- pass 1: totals (built / derived next-frontier children, split nodes)
+  // ---- pass 1: totals (built / derived next-frontier children, split nodes);
+  // a frontier of at most kPlanThreads nodes takes its total from pass 2's scan
+  // (one decision per node instead of two)
+  const bool one_chunk = K <= kPlanThreads;
   int nb_tot = 0;
-  for (int b0 = 0; b0 < K; b0 += kPlanThreads) {
+  for (int b0 = 0; b0 < K && !one_chunk; b0 += kPlanThreads) {
     const int i = b0 + tid;
     int nb = 0;
     if (i < K && active(i)) nb = decide(i).built >= 0 ? 1 : 0;
@@ -486,12 +542,12 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     plan_scan_excl(nb, sh.w, t);
     nb_tot += t;
   }
-  const int NB = nb_tot;
+  int NB = nb_tot;
   if (tid == 0) {
     sh.carry[0] = 0;  // built slots
     sh.carry[1] = 0;  // derived slots
     sh.carry[2] = 0;  // split nodes
-    a.nxt.ctl[10] = atomicAdd(a.job_count, 0);  // jobs before this level (dp fixup)
+    if (a.dp) a.nxt.ctl[10] = atomicAdd(a.job_count, 0);  // jobs before this level (dp fixup)
   }
   __syncthreads();
   // ---- pass 2: write decided nodes, jobs, split list, next frontier, derive list
@@ -510,6 +566,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     int tbd, ts;
     const int obd = plan_scan_excl(nb | (nd << 16), sh.w, tbd);
     const int tb = tbd & 0xffff, td = tbd >> 16;
+    if (one_chunk) NB = tb;  // (block-uniform: the scan's total)
     const int ob = (obd & 0xffff) + sh.carry[0];
     const int od = (obd >> 16) + sh.carry[1];
     const int os = plan_scan_excl(ns, sh.w, ts) + sh.carry[2];

@@ -34,7 +34,8 @@ void launch_hist_derive(hipStream_t, const int64_t*, int, const void*, void*, in
                         const int32_t*);
 void launch_scan(hipStream_t, const void*, const int64_t*, int, const int32_t*, int, int, int,
                  int, int, int, double*, int32_t*, int64_t*, const double*, int,
-                 const int32_t*, const int64_t*, const void*, const int32_t*);
+                 const int32_t*, const int64_t*, const void*, const int32_t*, int32_t*,
+                 int32_t*);
 void launch_grow_plan(hipStream_t, const PlanArgs&);
 void launch_partition(hipStream_t, const void*, int, int64_t, uint32_t*, uint32_t*, uint32_t,
                       const int64_t*, int, const int64_t*, int32_t*, const int32_t*, bool);
@@ -82,6 +83,10 @@ struct GrowCtx {
   const int32_t* nbins = nullptr;
   const double* xtab = nullptr;
   int32_t* host_ctl = nullptr;  // 64 host-mapped slots of 16 int32
+  // fused selection (two classes, <= 256 bins): [KMAX][F_h][2] left counts and
+  // [KMAX][2] class totals from the scan; null: the select kernel runs
+  int32_t* sel_left = nullptr;
+  int32_t* sel_tot = nullptr;
   int xtab_n = 0;
   int cb = 1, lab_shift = 0, F_h = 0, f_lo = 0, B = 0, C = 0, reg = 0, crit = 0;
   int md = -1, n_cu = 256, lds_budget = 0;
@@ -120,7 +125,7 @@ struct GrowCtx {
     if (lvl > 0 && reg) launch_hist_derive(s, cur.der, (int)kb, Hp, H, E, true, ctl + 4);
     launch_scan(s, H, ident, (int)kb, nbins, F_h, f_lo, B, C, crit, (int)msl, cost, bins, rec,
                 xtab, xtab_n, ctl, fuse ? cur.der : nullptr, fuse ? Hp : nullptr,
-                fuse ? ctl + 1 : nullptr);
+                fuse ? ctl + 1 : nullptr, sel_left, sel_tot);
     PlanArgs a{cur,       nxt,        rec,        split,
                pitems,    cursors,    ctl + 5,    pos_rec,
                reg ? nullptr : (int32_t*)pos_st,  reg ? (int64_t*)pos_st : nullptr,
@@ -128,6 +133,14 @@ struct GrowCtx {
                C,         md,         n_cu,       mss,
                msl,       fr,         host_ctl + (lvl % 64) * 16,
                tag0 + (lvl % 4096) + 1, 0, own};
+    if (sel_left) {
+      a.sel_cost = cost;
+      a.sel_bins = bins;
+      a.sel_left = sel_left;
+      a.sel_tot = sel_tot;
+      a.sel_F = F_h;
+      a.crit = crit;
+    }
     launch_grow_plan(s, a);
     const int pb = (int)std::min<int64_t>(PMAX, n_loc / 1024 + kb + 1);
     launch_partition(s, codes_fm, cb, n_codes, src, dst, row_mask, pitems, pb, split, cursors,
@@ -197,6 +210,10 @@ void bind_grow(py::module_& m) {
         c.PMAX = g("PMAX");
         c.MMAX = g("MMAX");
         c.tag0 = (int32_t)g("tag0");
+        if (d.contains("sel_left")) {
+          c.sel_left = ptr<int32_t>(g("sel_left"));
+          c.sel_tot = ptr<int32_t>(g("sel_tot"));
+        }
         if (own.size()) {
           auto o = [&](const char* k) { return own[k].cast<int64_t>(); };
           c.own = OwnArgs{(int)o("P"), (int)o("rank"), (int)o("min_units"), (int)o("cap"),

@@ -45,7 +45,11 @@ __global__ __launch_bounds__(kHistThreads) void hist_cls_lds_kernel(
     const int32_t* __restrict__ y, RowLab rl, const int64_t* __restrict__ items,
     uint32_t* __restrict__ hist, uint32_t* __restrict__ slab, int F_h, int f_lo, int B, int C,
     int ft, int lane_shift, const int32_t* __restrict__ dcount, const int64_t* __restrict__ zred,
-    const int32_t* __restrict__ zcount, int64_t zE) {
+    const int32_t* __restrict__ zcount, int64_t zE, int ct) {
+  // ct: classes per LDS tile (C: no class tiling). With many classes a single
+  // feature's [B][C] counts exceed the LDS budget: grid.y then covers feature
+  // tiles x class tiles of ct classes (ct even), each workgroup counting the rows
+  // whose label falls in its class range (the codes are read once per tile)
   // zred (optional, device-planned levels): zero the multi-item slots {slot, -, -}
   // [*zcount] that the following slab reduction adds into -- one launch less per
   // level. This kernel writes single-item slots and slabs only, never a zred slot.
@@ -67,9 +71,13 @@ __global__ __launch_bounds__(kHistThreads) void hist_cls_lds_kernel(
   if (dcount && (int)blockIdx.x >= *dcount) return;
   extern __shared__ uint32_t lds[];
   constexpr int cpw = 4 / sizeof(CodeT);  // codes per 32-bit word
-  const int W = (C + 1) >> 1;
+  const int n_ct = (C + ct - 1) / ct;
+  const int c_tile = (int)blockIdx.y % n_ct;
+  const int c_lo = c_tile * ct, c_hi = min(C, c_lo + ct);
+  const int W = (c_hi - c_lo + 1) >> 1;  // words of this tile's classes
+  const int Wall = (C + 1) >> 1;         // words of every class (slab layout)
   const int fstride = B * W + 1;
-  const int t0 = blockIdx.y * ft;
+  const int t0 = (int)(blockIdx.y / n_ct) * ft;
   const int t1 = min(F_h, t0 + ft);
   const int nf = t1 - t0;
   const int g0 = f_lo + t0, g1 = f_lo + t1;
@@ -118,9 +126,10 @@ __global__ __launch_bounds__(kHistThreads) void hist_cls_lds_kernel(
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      if (ent[u] == 0xffffffffu) continue;
-      const uint32_t inc = 1u << ((lab[u] & 1) * 16);
-      const int off = lab[u] >> 1;
+      if (ent[u] == 0xffffffffu || lab[u] < c_lo || lab[u] >= c_hi) continue;
+      const int lt = lab[u] - c_lo;  // (c_lo even: the class keeps its half-word)
+      const uint32_t inc = 1u << ((lt & 1) * 16);
+      const int off = lt >> 1;
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
 #pragma unroll
@@ -138,11 +147,14 @@ __global__ __launch_bounds__(kHistThreads) void hist_cls_lds_kernel(
   __syncthreads();
 
   const int per_f = B * W;
-  if (dest >= 0) {  // packed image -> slab (tile's features are contiguous)
-    uint32_t* out = slab + dest * (int64_t)F_h * per_f + (int64_t)t0 * per_f;
+  if (dest >= 0) {  // packed image -> slab [F_h][B][Wall] (this tile's words of it)
+    uint32_t* out = slab + dest * (int64_t)F_h * B * Wall + (int64_t)t0 * B * Wall;
     for (int e = threadIdx.x; e < nf * per_f; e += blockDim.x) {
       const int f = e / per_f;
-      out[e] = lds[f * fstride + (e - f * per_f)];
+      const int rem = e - f * per_f;
+      const int b = rem / W;
+      const int w = rem - b * W;
+      out[((int64_t)f * B + b) * Wall + (c_lo >> 1) + w] = lds[f * fstride + rem];
     }
     return;
   }
@@ -153,9 +165,10 @@ __global__ __launch_bounds__(kHistThreads) void hist_cls_lds_kernel(
     const int b = rem / W;
     const int wc = rem - b * W;
     const uint32_t v = lds[f * fstride + rem];
-    const int64_t o = ((int64_t)(t0 + f) * B + b) * C + 2 * wc;
+    const int c = c_lo + 2 * wc;
+    const int64_t o = ((int64_t)(t0 + f) * B + b) * C + c;
     out[o] = v & 0xffffu;
-    if (2 * wc + 1 < C) out[o + 1] = v >> 16;
+    if (c + 1 < c_hi) out[o + 1] = v >> 16;
   }
 }
 
@@ -416,6 +429,17 @@ int hist_feature_tile(int F_h, int B, int C, bool reg, int lds_budget) {
   return ft;
 }
 
+// Classes per LDS tile of the classification histogram kernel: C when a
+// feature's whole [B][C] histogram fits the budget (hist_feature_tile > 0), else
+// the largest even count that fits one feature (0: not even two classes fit).
+int hist_class_tile(int F_h, int B, int C, bool reg, int lds_budget) {
+  if (reg) return hist_feature_tile(F_h, B, C, reg, lds_budget) > 0 ? 2 : 0;
+  if (hist_feature_tile(F_h, B, C, reg, lds_budget) > 0) return C;
+  const int words = lds_budget / 4 - 1;  // per feature: B * ct / 2 + 1 words
+  int ct = 2 * (words / std::max(B, 1));
+  return ct >= 2 ? std::min(ct, C) : 0;
+}
+
 // Words of the packed classification slab per work item ([F_h][B][W]).
 int64_t hist_slab_words(int F_h, int B, int C, bool reg) {
   return reg ? (int64_t)F_h * B * 2 : (int64_t)F_h * B * ((C + 1) / 2);
@@ -432,7 +456,9 @@ void launch_hist(hipStream_t stream, const void* codes, int code_bytes, int64_t 
   if (n_items <= 0) return;
   const int ft = hist_feature_tile(F_h, B, C, reg, lds_budget);
   const int64_t Eu = (int64_t)F_h * B * C;
-  const bool fuse_zero = zred && zred_bound > 0 && !reg && ft != 0 && (Eu & 3) == 0;
+  const bool fuse_zero = zred && zred_bound > 0 && !reg &&
+                         (ft != 0 || hist_class_tile(F_h, B, C, reg, lds_budget) > 0) &&
+                         (Eu & 3) == 0;
   if (zred && zred_bound > 0 && !fuse_zero) {
     hipLaunchKernelGGL(zero_slots_kernel,
                        dim3((unsigned)std::min<int64_t>((Eu / 4 + 255) / 256, 64), zred_bound),
@@ -440,6 +466,35 @@ void launch_hist(hipStream_t stream, const void* codes, int code_bytes, int64_t 
     MT_HIP_CHECK(hipGetLastError());
   }
   RowLab rl{lab_shift ? ((1u << lab_shift) - 1u) : 0xffffffffu, lab_shift};
+  // many classes: class-tiled LDS histograms (one feature per tile)
+  const int ct = reg ? 0 : hist_class_tile(F_h, B, C, reg, lds_budget);
+  if (ft == 0 && ct > 0 && ct < C) {
+    const int n_ct = (C + ct - 1) / ct;
+    const int64_t row_words = row_stride_bytes / 4;
+    const int cpw = 4 / code_bytes;
+    int words = 1;
+    for (int f = 0; f < F_h; ++f) {
+      const int a = f_lo + f, b = a + 1;
+      words = std::max(words, (b + cpw - 1) / cpw - a / cpw);
+    }
+    const int shift = std::min(ceil_pow2_shift(words), 6);
+    const size_t lds = (size_t)(B * ((ct + 1) / 2) + 1) * 4;
+    dim3 grid(n_items, F_h * n_ct);
+#define MT_CLS_CT(CT)                                                                         \
+  MT_HIP_CHECK(mt_set_max_lds((const void*)hist_cls_lds_kernel<CT, 1>, (int)lds));           \
+  hipLaunchKernelGGL((hist_cls_lds_kernel<CT, 1>), grid, dim3(kHistThreads), lds, stream,     \
+                     (const uint32_t*)codes, row_words, idx, (const int32_t*)y, rl, items,    \
+                     (uint32_t*)hist, (uint32_t*)slab, F_h, f_lo, B, C, 1, shift, dcount,    \
+                     fuse_zero ? zred : nullptr, zcount, Eu, ct);
+    if (code_bytes == 1) {
+      MT_CLS_CT(uint8_t)
+    } else {
+      MT_CLS_CT(uint16_t)
+    }
+#undef MT_CLS_CT
+    MT_HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (ft == 0) {
     dim3 grid(n_items);
     const int64_t row_elems = row_stride_bytes / code_bytes;
@@ -506,7 +561,7 @@ void launch_hist(hipStream_t stream, const void* codes, int code_bytes, int64_t 
   hipLaunchKernelGGL((hist_cls_lds_kernel<CT, V>), grid, dim3(kHistThreads), lds, stream,     \
                      (const uint32_t*)codes, row_words, idx, (const int32_t*)y, rl, items,    \
                      (uint32_t*)hist, (uint32_t*)slab, F_h, f_lo, B, C, ft, shift, dcount,   \
-                     fuse_zero ? zred : nullptr, zcount, Eu);
+                     fuse_zero ? zred : nullptr, zcount, Eu, C);
   if (code_bytes == 1) {
     if (vec4) {
       MT_CLS(uint8_t, 4)

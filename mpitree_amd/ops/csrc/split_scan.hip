@@ -54,7 +54,12 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
     double* __restrict__ out_cost, int32_t* __restrict__ out_bin,
     const double* __restrict__ xtab, int xtab_n, const int32_t* __restrict__ dcount,
     const int64_t* __restrict__ der, const uint32_t* __restrict__ prev,
-    const int32_t* __restrict__ nbuilt, int der_lds) {
+    const int32_t* __restrict__ nbuilt, int der_lds, int32_t* __restrict__ sel_left,
+    int32_t* __restrict__ sel_tot) {
+  // sel_left / sel_tot (fused selection, two-class fast path): the left class
+  // counts at this feature's best bin [node][F_h][2] and, from feature 0's wave,
+  // the node's class totals and node term [node][4] = {t0, t1, term (f64)}, for
+  // the planner to build the split record
   // der_lds: the derived histogram (B*C words per wave) fits in LDS; else the
   // scan reads parent - sibling from global memory on the fly (many classes)
   if (dcount && (int)blockIdx.x >= *dcount) return;  // device-side node count
@@ -217,9 +222,41 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
       }
     }
     wave_argmin_dpp(bc, bb);  // one pass: lanes own ascending bins
+    const bool found = bc < __builtin_inf();
     if (lane == 0) {
       out_cost[node * F_h + f] = bc;
-      out_bin[node * F_h + f] = bc < __builtin_inf() ? bb : -1;
+      out_bin[node * F_h + f] = found ? bb : -1;
+    }
+    if (sel_left) {
+      // the winning bin's left counts live in lane bb / 4, register bb % 4
+      const int src = found ? (bb >> 2) : 0, kk = found ? (bb & 3) : 0;
+      uint32_t lsel[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        uint32_t x = L[c][0];
+#pragma unroll
+        for (int k = 1; k < kBinsPerLane; ++k) x = kk == k ? L[c][k] : x;
+        lsel[c] = (uint32_t)__builtin_amdgcn_readlane((int)x, src);
+      }
+      if (lane == 0) {
+        sel_left[(node * F_h + f) * 2 + 0] = found ? (int32_t)lsel[0] : 0;
+        sel_left[(node * F_h + f) * 2 + 1] = found ? (int32_t)lsel[1] : 0;
+        if (f == 0) {
+          sel_tot[node * 4 + 0] = (int32_t)tc[0];
+          sel_tot[node * 4 + 1] = (int32_t)tc[1];
+          // the node term as select_kernel computes it (classes in order; the
+          // table holds x log2 x bit for bit)
+          double acc = 0.0;
+          int64_t sq = 0;
+          for (int c = 0; c < C; ++c) {
+            acc = acc + tlog((uint64_t)tc[c], xtab, xtab_n);
+            sq += (int64_t)tc[c] * tc[c];
+          }
+          const double pt = crit == kEntropy ? tlog((uint64_t)m2, xtab, xtab_n) - acc
+                                             : gini_term((int64_t)m2, sq);
+          reinterpret_cast<double*>(sel_tot)[node * 2 + 1] = pt;
+        }
+      }
     }
     return;
   }
@@ -624,12 +661,19 @@ __global__ __launch_bounds__(256) void select_kernel(
 // flagship: the scan went from ~19 to ~82 us per level -- every workgroup's
 // agent-scope release writes back its XCD's L2 -- against the ~6 us launch
 // it saves.
+bool scan_fused_select_ok(int B, int C, int crit) {
+  return C <= 2 && B <= kChunk && crit != kSquaredError;
+}
+
 void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int k,
                  const int32_t* nbins, int F_h, int f_lo, int B, int C, int crit, int msl,
                  double* cost, int32_t* bins, int64_t* rec, const double* xtab, int xtab_n,
                  const int32_t* dcount, const int64_t* der, const void* prev,
-                 const int32_t* nbuilt) {
+                 const int32_t* nbuilt, int32_t* sel_left, int32_t* sel_tot) {
+  // sel_left (fused selection): the planner builds the records, no select launch
   if (k <= 0) return;
+  if (sel_left && !scan_fused_select_ok(B, C, crit))
+    throw std::runtime_error("scan: fused selection needs <= 2 classes and <= 256 bins");
   dim3 grid(k, (F_h + 3) / 4);
   if (crit == kSquaredError) {
     hipLaunchKernelGGL(scan_reg_kernel, grid, dim3(256), 0, stream, (const int64_t*)hist, nodes,
@@ -643,9 +687,10 @@ void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int
     MT_HIP_CHECK(mt_set_max_lds((const void*)scan_cls_kernel, (int)lds));
     hipLaunchKernelGGL(scan_cls_kernel, grid, dim3(256), lds, stream, (uint32_t*)hist,
                        nodes, nbins, F_h, f_lo, B, C, crit, msl, cost, bins, xtab, xtab_n,
-                       dcount, der, (const uint32_t*)prev, nbuilt, der_lds);
+                       dcount, der, (const uint32_t*)prev, nbuilt, der_lds, sel_left, sel_tot);
   }
   MT_HIP_CHECK(hipGetLastError());
+  if (sel_left) return;
   const size_t sel_lds = crit == kSquaredError ? 16 : (size_t)2 * C * sizeof(int64_t);
   MT_HIP_CHECK(mt_set_max_lds((const void*)select_kernel, (int)sel_lds));
   hipLaunchKernelGGL(select_kernel, dim3(k), dim3(256), sel_lds, stream, hist, nodes, cost, bins,

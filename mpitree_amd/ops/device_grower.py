@@ -139,8 +139,31 @@ def device_loop_supported(be, params, comm) -> bool:
             return False
     if params.finisher_rows <= 0 or not be.finisher_supported():
         return False
-    # the planner drives the LDS histogram path only
-    return be.hip.hist_feature_tile(be.F, be.B, be.C, bool(be.reg), hb.LDS_BUDGET) > 0
+    # the planner drives the LDS histogram path only (feature or class tiles)
+    if not be.lds_hist():
+        return False
+    # two levels of [KMAX][F][B][C] histograms plus the item slabs must fit (many
+    # classes: ~19.7 MB per node at 64 x 256 x 300)
+    return level_loop_bytes(be.n, be.F, be.B, be.C, bool(be.reg), int(params.finisher_rows),
+                            be.hip) <= free_device_bytes(be.device) // 2
+
+
+def level_loop_bytes(n, F, B, C, reg, fr, hip) -> int:
+    """Device bytes of the level loop's histogram buffers (both level parities)
+    and item slabs for ``n`` rows with finisher jobs of at most ``fr`` rows."""
+    KMAX = n // (fr + 1) + 2
+    IMAX = KMAX + n // 1024 + 2 * hb.N_CU + 16
+    esz = 8 if reg else 4
+    hist = 2 * KMAX * F * B * (2 if reg else C) * esz
+    slab = IMAX * int(hip.hist_slab_words(F, B, C, reg)) * esz
+    return int(hist + slab)
+
+
+def free_device_bytes(dev) -> int:
+    try:
+        return int(torch.cuda.mem_get_info(dev)[0])
+    except Exception:  # pragma: no cover - (no CUDA context: tests on CPU)
+        return 1 << 62
 
 
 def exchange_ranges(be, comm, ranges: torch.Tensor, bound: int):
@@ -501,6 +524,11 @@ class DeviceGrower:
             MMAX = KMAX + n_loc // 4096 + 16
             E = F_h * B * C
             hdt = torch.int64 if reg else torch.int32
+            # two classes, <= 256 bins, no collective between scan and plan: the
+            # planner builds the split records from the scan's per-feature results
+            # (no select launch)
+            fsel = (not (reg or dp or fp) and bool(hip.scan_fused_select_ok(B, C, int(be.crit)))
+                    and os.environ.get("MPITREE_FUSED_SELECT", "1") != "0")
 
             def make():
                 i64 = dict(dtype=torch.int64, device=dev)
@@ -532,9 +560,15 @@ class DeviceGrower:
                     own_ranges=torch.zeros((OWN_CAP if own else 1, 2), **i64),
                     own_node=torch.empty(KMAX if own else 1, dtype=torch.int32, device=dev),
                     own_job=torch.empty(JMAX if own else 1, dtype=torch.int32, device=dev),
+                    # fused selection: per-feature left counts and node totals (scan)
+                    sel_left=torch.empty((KMAX, F_h, 2) if fsel else 1, dtype=torch.int32,
+                                         device=dev),
+                    sel_tot=torch.empty((KMAX, 4) if fsel else 1, dtype=torch.int32,
+                                        device=dev),
                 )
 
-            ws = self._workspace((str(dev), n, n_loc, F, f_lo, F_h, B, C, reg, fr, dp, own), make)
+            ws = self._workspace((str(dev), n, n_loc, F, f_lo, F_h, B, C, reg, fr, dp, own, fsel),
+                                 make)
             sets, hists, slab, rec = ws["sets"], ws["hists"], ws["slab"], ws["rec"]
             cost, bins, ident, split = ws["cost"], ws["bins"], ws["ident"], ws["split"]
             pitems, cursors, jobs, job_count = (ws["pitems"], ws["cursors"], ws["jobs"],
@@ -604,7 +638,9 @@ class DeviceGrower:
                     n_loc=n_loc, F_h=F_h, f_lo=f_lo, B=B, C=C, reg=int(reg), crit=int(be.crit),
                     E=E, max_depth=md, mss=mss, msl=msl, fr=fr, n_cu=plan_cu,
                     lds_budget=hb.LDS_BUDGET, KMAX=KMAX, IMAX=IMAX, TMAX=TMAX, RMAX=RMAX,
-                    PMAX=PMAX, MMAX=MMAX, tag0=tag0), ptrs[0], ptrs[1], own_args)
+                    PMAX=PMAX, MMAX=MMAX, tag0=tag0,
+                    **(dict(sel_left=ws["sel_left"].data_ptr(), sel_tot=ws["sel_tot"].data_ptr())
+                       if fsel else {})), ptrs[0], ptrs[1], own_args)
 
             def plan(cur, nxt, lvl, fixup=False):
                 hip.grow_plan(s(), cur, nxt, rec.data_ptr(), split.data_ptr(), pitems.data_ptr(),

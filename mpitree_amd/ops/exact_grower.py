@@ -100,7 +100,7 @@ def exact_workspace_bytes(n: int, F_loc: int, C: int, regression: bool, fr: int,
     if regression:
         b += 2 * F_loc * n * 8                          # Y[2]
     b += 2 * IMAX * F_loc * Cc * 8                      # tot, carry
-    b += IMAX * F_loc * (16 + 4) + 2 * IMAX * F_loc * 8  # cbest, cmin, pstat
+    b += IMAX * F_loc * (16 + 4) + 4 * IMAX * F_loc * 8  # cbest, cmin, pstat
     b += KMAX * (F_loc * 4 + rec_width * 8 + 64 + 2 * Cs * 8)  # nmin, rec, lists
     b += (2 * n) * (6 * 4 + Cs * 8 + 8)                 # position space + thresholds
     return int(b)
@@ -317,7 +317,8 @@ class ExactGrower:
                 flag=torch.empty((n + 31) // 32, dtype=torch.int32, device=dev),
                 flagb=torch.zeros((n + 31) // 32 * 32, dtype=torch.uint8, device=dev),
                 # look-back status words (tagged per fit and level: zeroed once)
-                pstat=torch.zeros((2 * IMAX, F_loc), **i64),  # (2 wave units per item)
+                # (one status word per partition wave unit: xe_part_units per item)
+                pstat=torch.zeros((int(hip.xe_part_units()) * IMAX, F_loc), **i64),
                 sitem=torch.empty((KMAX, 2), **i32),  # (partition-counted chunk totals)
                 tick=torch.zeros(4, **i32),
                 jobs=torch.empty((JMAX, JW), **i64),

@@ -453,10 +453,15 @@ class HipBackend:
         self._F_h = F_h
         dt = torch.int64 if self.reg else torch.int32
         shape = (max(slots, 1), F_h, self.B, 2 if self.reg else self.C)
-        ft = self.hip.hist_feature_tile(F_h, self.B, self.C, self.reg, LDS_BUDGET)
-        if ft == 0:
+        if not self.lds_hist(F_h):  # global-atomic histograms add into zeroed slots
             return torch.zeros(shape, dtype=dt, device=self.device)
         return torch.empty(shape, dtype=dt, device=self.device)
+
+    def lds_hist(self, F_h: int | None = None) -> bool:
+        """Histograms built in LDS (feature tiles, or class tiles of one feature
+        past the budget) rather than by global atomics."""
+        F_h = self.F if F_h is None else F_h
+        return self.hip.hist_class_tile(F_h, self.B, self.C, self.reg, LDS_BUDGET) > 0
 
     # ------------------------------------------------------------ histograms
     def build_hist(self, hist, slots, starts, counts, f_lo=0, f_hi=None):
@@ -468,17 +473,17 @@ class HipBackend:
         starts = np.asarray(starts, dtype=np.int64)
         counts = np.asarray(counts, dtype=np.int64)
         total = int(counts.sum())
-        ft = self.hip.hist_feature_tile(F_h, self.B, self.C, self.reg, LDS_BUDGET)
+        lds = self.lds_hist(F_h)
         # ~2 workgroups per CU over the whole level, at most 65535 rows per item
         chunk = int(min(MAX_ITEM_ROWS, max(1024, -(-total // (2 * N_CU)))))
-        if ft == 0:
+        if not lds:
             chunk = MAX_ITEM_ROWS  # global-atomic fallback: every item adds into hist
         k = np.maximum(1, -(-counts // chunk))
         node_of = np.repeat(np.arange(len(slots)), k)
         first = np.cumsum(k) - k
         i_in = np.arange(node_of.size) - first[node_of]
         c0 = i_in * chunk
-        multi = (k > 1) & (ft > 0)
+        multi = (k > 1) & lds
         slab_base = np.cumsum(np.where(multi, k, 0)) - np.where(multi, k, 0)
         dest = np.where(multi[node_of], slab_base[node_of] + i_in, -1)
         items = np.stack([slots[node_of], starts[node_of] + c0,
@@ -566,15 +571,19 @@ class HipBackend:
 
     # -------------------------------------------------------------- finisher
     def finisher_supported(self) -> bool:
-        if self.reg:
-            return self.B <= 256 and self.F <= 256
+        if self.reg:  # (features past 256: more LDS tiles per node, no tiny kernel)
+            return self.B <= 256
         # C <= 256, any F, B <= 4096 (16-bit codes past 256 bins: multi-pass
         # scans): the block finisher tiles features (and classes' words) through
         # LDS when one node's histogram does not fit in one pass
         return self.hip.finish_feature_tile(self.F, self.B, self.C) > 0
 
-    # finisher jobs index the x*log2(x) table with row counts: keep them below it
-    max_finisher_rows = XTAB_N - 1
+    @property
+    def max_finisher_rows(self) -> int:
+        """Finisher jobs index the x*log2(x) table with row counts (keep them
+        below it); past 256 classes a job holds at most 255 rows, so a node's
+        present classes and counts fit the finisher's 8-bit compacted histograms."""
+        return int(min(XTAB_N - 1, self.hip.finish_job_rows_cap(int(self.C))))
 
     # ------------------------------------------------ pre-order position space
     def begin_positions(self, P: int):

@@ -411,6 +411,25 @@ def test_gpu_regression_device_loop_matches_host(monkeypatch, seed, max_depth):
     assert r1.arrays.equal(r3.arrays)
 
 
+@pytest.mark.parametrize("F", [300, 600])
+def test_gpu_regression_wide_features_device_loop(F):
+    """Regression past 256 features runs the device level loop and the block
+    finisher (features past its per-feature LDS arrays read their bin counts from
+    memory; past ~512 features no tiny kernel): the host-built tree bit for bit."""
+    from mpitree_amd.core.fit import fit_tree
+
+    rng = np.random.default_rng(F)
+    n = 6000
+    X = rng.integers(0, 24, size=(n, F)).astype(np.float32)
+    y = np.round(X[:, 0] * 0.5 + X[:, F - 1] * 1.5 + rng.integers(0, 5, size=n), 1)
+    kw = dict(regression=True, criterion=2, max_depth=None, min_samples_split=2)
+    g = fit_tree(X, y, device="cuda", **kw)
+    assert g.engine == "hip-device-loop" and g.stats.get("finisher_subtrees", 0) > 0
+    h = fit_tree(X, y, device="cpu", **kw)
+    assert g.arrays.equal(h.arrays)
+    assert np.array_equal(g.arrays.value, h.arrays.value)
+
+
 @pytest.mark.parametrize("F", [100, 128])
 def test_gpu_many_features_tiny_paths_match_host(F):
     """F > 64: the tiny kernels' lane-per-feature small-node path walks several
@@ -752,22 +771,25 @@ def test_gpu_finisher_handoff_queue_single_job(monkeypatch, regression):
     assert g2.arrays.equal(h.arrays, check_impurity=not regression)
 
 
-@pytest.mark.parametrize("C,F,n", [(64, 16, 40000), (200, 8, 30000), (2, 300, 20000),
-                                   (5, 300, 8000)])
-def test_gpu_finisher_many_classes_and_features(C, F, n):
+@pytest.mark.parametrize("C,F,n,levels", [(64, 16, 40000, 48), (200, 8, 30000, 48),
+                                          (2, 300, 20000, 48), (5, 300, 8000, 48),
+                                          (200, 6, 30000, 256), (300, 5, 12000, 256)])
+def test_gpu_finisher_many_classes_and_features(C, F, n, levels):
     # the block finisher tiles features through LDS when one node's histogram does
     # not fit (many classes: 16-bit class pairs per bin; many features), keeps the
     # DFS stack's class counts in global scratch past 16 classes, and the sorted
-    # tiny kernel runs with fewer waves per workgroup for wide rows
-    rng = np.random.default_rng(C * 1000 + F)
-    X, y = random_problem(rng, n, F, C, levels=48)
+    # tiny kernel runs with fewer waves per workgroup for wide rows. Level
+    # histograms past the LDS budget (256 bins x 200 classes) are class-tiled;
+    # past 256 classes the finisher jobs hold <= 255 rows -- every shape runs the
+    # device level loop
+    rng = np.random.default_rng(C * 1000 + F + levels)
+    X, y = random_problem(rng, n, F, C, levels=levels)
     cpu = DecisionTreeClassifier(device="cpu").fit(X, y)
     gpu = DecisionTreeClassifier(device="cuda").fit(torch.from_numpy(X).cuda(),
                                                     torch.from_numpy(y).cuda())
     st = gpu.fit_stats_
     assert st.get("finisher_subtrees", 0) > 0, st
-    if C <= 64:  # (C = 200: the level histograms exceed LDS -> host-driven levels)
-        assert st["engine"] == "hip-device-loop", st["engine"]
+    assert st["engine"] == "hip-device-loop", st["engine"]
     assert gpu.tree_arrays_.equal(cpu.tree_arrays_), (gpu.tree_arrays_.node_count,
                                                       cpu.tree_arrays_.node_count)
 

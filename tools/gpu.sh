@@ -12,8 +12,9 @@
 #   dist                 distributed GPU tests (gloo ranks, one card)  -> gputests_dist.log
 #   bench[:ARGS]         bench.py --steps 20 --warmup 3 ARGS           -> bench.log (appended)
 #   ab:CFG1;CFG2;...     bench under each setting, alternated twice     -> ab.log
-#                        (CFG: "ENV=1 ENV2=x", or "so=NAME" to swap in variants/NAME.so from
-#                        tools/build_variant.sh; BENCH_ARGS passes extra bench.py arguments)
+#                        (CFG: "ENV=1 ENV2=x"; "so=NAME" swaps in variants/NAME.so from
+#                        tools/build_variant.sh; "dir=PATH" runs PATH/bench.py, a whole
+#                        tree from tools/snapshot_tree.sh; BENCH_ARGS: extra bench.py args)
 #   configs[:NAMES]      bench/baseline_configs.py NAMES --reps 5       -> baseline_configs.jsonl
 #   prof:NAME[:ARGS]     rocprofv3 kernel trace + stats of bench.py ARGS
 #                        -> prof_NAME.{top,summary,timeline}.txt, kernel_stats.csv
@@ -78,9 +79,11 @@ for step in "$@"; do
         for cfg in "base=1" "${cfgs[@]}"; do
           echo "== $cfg" >> gpurun_out/ab.log
           envs=$cfg
+          script=bench.py
           if [[ $cfg == so=* ]]; then cp "variants/${cfg#so=}.so" "$SO"; envs="base=1"; fi
+          if [[ $cfg == dir=* ]]; then script="${cfg#dir=}/bench.py"; envs="base=1"; fi
           # shellcheck disable=SC2086
-          env $envs timeout -k 10 150 python -u bench.py --steps 20 --warmup 3 $BENCH_ARGS \
+          env $envs timeout -k 10 150 python -u "$script" --steps 20 --warmup 3 $BENCH_ARGS \
             2>>gpurun_out/ab.err | python -c "import json,sys; d=json.loads(sys.stdin.read()); \
 print(d['ms_per_step'], d['config']['tree_nodes'])" >> gpurun_out/ab.log
           cp gpurun_out/.base.so "$SO"
