@@ -43,24 +43,103 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mpitree_amd.core.levelwise import LocalComm  # noqa: E402
 
 
+class SimSlot:
+    """The shared tree buffer stand-in: mapped pinned host memory holding the
+    reference tree's packed columns (the other ranks' nodes) before each fit."""
+
+    def __init__(self, ref_bytes: np.ndarray):
+        import ctypes
+
+        from mpitree_amd.ops import native
+        from mpitree_amd.parallel.shared_tree import HEADER
+
+        hip = native.hip()
+        size = HEADER + ref_bytes.size
+        self.host = int(hip.host_alloc(size, coherent=False))
+        self.nd = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(self.host))
+        self.dev = int(hip.host_device_ptr(self.host))
+        self.nbytes = size
+        self.ref = ref_bytes
+        self.header = HEADER
+
+    def prefill(self):
+        self.nd[self.header :] = self.ref
+
+
+class SimPool:
+    """Shared-host assembly stand-in: one slot, no peers to wait for."""
+
+    def __init__(self, slot: SimSlot):
+        self.slot = slot
+
+    def free_mask(self) -> int:
+        return 1
+
+    def choose(self, masks, need: int):
+        assert need <= self.slot.ref.size, "tree larger than the reference"
+        return self.slot
+
+    def take_next(self):
+        return self.slot
+
+    def plan_next(self, masks, current, need: int) -> None:
+        return None
+
+    def barrier(self, slot) -> None:
+        return None
+
+
 class SimOwnComm(LocalComm):
-    """Rank ``rank`` of a P-rank subtree-ownership group, without other ranks:
-    the node exchange returns this rank's rows plus every node of a reference fit."""
+    """Rank ``rank`` of a P-rank subtree-ownership group, without other ranks.
+    Shared-host assembly (the default on one node): the segment-count all-gather
+    returns every segment's node count from the reference fit's position space
+    and the shared buffer already holds the reference tree, so the rank writes
+    only its own nodes. ``--no-shared`` (``MPITREE_SHM_TREE=0``): the node
+    exchange returns this rank's rows plus every node of the reference fit."""
 
     kind = "subtree"
     simulated = True
 
-    def __init__(self, P: int, rank: int, device, ref_rows: torch.Tensor):
+    def __init__(self, P: int, rank: int, device, ref_rows: torch.Tensor, ref_pos=None,
+                 ref_depth=0, pool=None):
         self.world_size = P
         self.rank = rank
         self.device = device
         self.bytes_communicated = 0
         self.ref_rows = ref_rows
+        self.ref_pos, self.ref_depth = ref_pos, int(ref_depth)
+        self._shm_pool = pool if pool is not None else False
+        self._head = torch.tensor([int(ref_depth), 1], dtype=torch.int64, device=device)
 
     def all_gather_rows(self, t):
         # bytes of a real exchange: every rank's rows, padded to the largest share
         self.bytes_communicated += self.ref_rows.numel() * self.ref_rows.element_size()
         return torch.cat([t, self.ref_rows.to(t.dtype)], 0)
+
+    def all_gather_seg_counts(self, out, inp, segs, S):
+        # every rank's row: its segments' node counts (from the reference positions)
+        # (a few small kernels: what the real all-gather costs is estimated apart)
+        P, W = self.world_size, inp.numel()
+        g = out.view(P, W)
+        cnt = torch.searchsorted(self.ref_pos, segs[:S, :2].contiguous()).diff(dim=1)[:, 0]
+        mine = segs[:S, 2][None, :] == torch.arange(P, device=segs.device)[:, None]
+        g[:, 2 : 2 + S] = mine * cnt[None, :]
+        g[:, :2] = self._head
+        self.bytes_communicated += P * W * 8
+
+
+def packed_bytes(ta) -> np.ndarray:
+    """A finished tree's columns in the device assembly's packed layout
+    (``TreeArrays.from_packed``)."""
+    cols = [ta.n_samples.astype(np.int64), ta.threshold.astype(np.float64),
+            ta.impurity.astype(np.float64)]
+    if ta.value is not None:
+        cols += [ta.value.astype(np.float64), ta.meta["sum_fixed"].astype(np.int64)]
+    else:
+        cols += [ta.count.astype(np.int32)]
+    cols += [c.astype(np.int32) for c in (ta.feature, ta.threshold_bin, ta.left, ta.right,
+                                          ta.depth)]
+    return np.concatenate([np.ascontiguousarray(c).view(np.uint8).reshape(-1) for c in cols])
 
 
 def reference_rows(fit, dev, regression=False):
@@ -92,6 +171,8 @@ def main():
     ap.add_argument("--only-rank", type=int, default=None,
                     help="simulate this rank only (profiling one rank's kernel sequence)")
     ap.add_argument("--regression", action="store_true")
+    ap.add_argument("--no-shared", action="store_true",
+                    help="node exchange + full-tree copy instead of the shared-host assembly")
     a = ap.parse_args()
     if a.units_per_rank is not None:
         os.environ["MPITREE_OWN_UNITS_PER_RANK"] = str(a.units_per_rank)
@@ -111,12 +192,19 @@ def main():
     for _ in range(2):
         fit()
     ref, ref_rows = reference_rows(fit, dev, a.regression)
+    ref_pos = ref_rows[:, 0].long().contiguous()  # live positions, ascending
+    pool = None
+    if not a.no_shared:
+        pool = SimPool(SimSlot(packed_bytes(ref.arrays)))
     for P in [int(v) for v in a.ranks.replace("+", ",").split(",")]:
         per_rank = []
         for r in range(P) if a.only_rank is None else [a.only_rank]:
             times, st, ph = [], {}, []
             for i in range(a.reps + 2):
-                comm = SimOwnComm(P, r, dev, ref_rows) if P > 1 else None
+                comm = (SimOwnComm(P, r, dev, ref_rows, ref_pos, ref.arrays.max_depth, pool)
+                        if P > 1 else None)
+                if pool is not None:
+                    pool.slot.prefill()
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 res = fit(comm)

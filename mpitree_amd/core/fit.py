@@ -132,11 +132,18 @@ def _encode_labels(y, n):
     return classes, enc.astype(np.int32)
 
 
+def _ceil_log2(x: float) -> int:
+    """ceil(log2(x)) for x > 0, exact (frexp: x = m 2^k, m in [0.5, 1)); the
+    device encoder (misc.hip target_encode_kernel) computes it the same way."""
+    m, k = math.frexp(x)
+    return k - 1 if m == 0.5 else k
+
+
 def fixed_point_exponent(absmax: float, n: int) -> int:
     """Exponent e with sum(|round(y * 2**e)|) < 2**62 for n rows."""
     if absmax <= 0 or not math.isfinite(absmax):
         return 0
-    e = 62 - math.ceil(math.log2(max(n, 1) + 1)) - math.ceil(math.log2(absmax * (1 + 2**-40)))
+    e = 62 - _ceil_log2(float(max(n, 1)) + 1.0) - _ceil_log2(absmax * (1 + 2**-40))
     return int(max(min(e, 1000), -1000))
 
 

@@ -20,6 +20,8 @@
 //
 // so the host receives the finished, pre-ordered tree in one pinned copy.
 #include "common.h"
+
+#include <stdexcept>
 #include "criterion.h"
 
 namespace mt {
@@ -117,8 +119,9 @@ __global__ __launch_bounds__(kAsmThreads) void asm_offsets_kernel(int32_t* __res
   }
 }
 
-// Final node id of every written position (positions no node occupies get -1),
-// and the tree's depth (max over written positions) into total[1]. Position
+// Final node id of every written position (a position no node occupies gets
+// ~(written positions before it), negative: the shared-host assembly ranks
+// other ranks' segment roots with it), and the tree's depth (max over written positions) into total[1]. Position
 // p = tile + k * kAsmThreads + thread (coalesced, the count kernel's order);
 // the in-tile rank comes from per-(k, wave) ballot masks kept in LDS, and
 // each workgroup adds one atomic for the depth.
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __
     if (p < P) {
       int r = off + __popcll(s_mask[k][wv] & below);
       for (int w = 0; w < wv; ++w) r += __popcll(s_mask[k][w]);
-      rank[p] = ((flags >> k) & 1u) ? r : -1;
+      rank[p] = ((flags >> k) & 1u) ? r : ~r;  // (unwritten: ~ its exclusive rank)
     }
     off += s_ktot[k];
   }
@@ -238,26 +241,137 @@ __device__ inline AsmCols asm_cols(uint8_t* base, int64_t N, int C, bool reg) {
   return o;
 }
 
+// ---------------------------------------------------------------------------
+// Node-local shared-host assembly (several ranks of one node, subtree ownership;
+// parallel/shared_tree.py). Rank r's position space holds the replicated prefix
+// (the levels before the ownership switch) and its own segments; other ranks'
+// segments are empty. With every segment's node count (one small all-gather) a
+// rank knows the final id of each of its nodes: its local rank plus the nodes of
+// other ranks' segments that start before it. Each rank then writes its own nodes
+// (rank 0 also the prefix) straight into the node's shared host buffer (a
+// registered /dev/shm mapping, zero-copy over PCIe), so no rank receives the
+// other ranks' nodes over xGMI and each moves 1 / P of the tree over PCIe.
+//
+// tab: int64 [n][4] {lo, hi, owner, foreign nodes in segments up to and including
+// this one}, ascending lo (shm_seg_prefix_kernel).
+struct ShmPlace {
+  bool own;
+  int64_t e, lo, hi;
+};
+
+// entry index of the last segment with lo <= x (strict: lo < x), -1 if none
+__device__ inline int shm_find(const int64_t* __restrict__ tab, int n, int64_t x, bool strict) {
+  int lo = 0, hi = n;  // first entry with lo > x (strict: >= x)
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    const int64_t v = tab[(int64_t)mid * 4];
+    if (strict ? v < x : v <= x)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo - 1;
+}
+
+__device__ inline int64_t shm_foreign_before(const int64_t* __restrict__ tab, int n, int64_t x) {
+  const int k = shm_find(tab, n, x, true);
+  return k >= 0 ? tab[(int64_t)k * 4 + 3] : 0;
+}
+
+// {lo_k, hi_k, owner_k, foreign before lo_k (exclusive), foreign through k, lo_{k+1}}
+// of the last segment k with lo <= p0 (k = -1: {-1, -1, -1, 0, 0, lo_0})
+__device__ inline void shm_block_ctx(const int64_t* __restrict__ tab, int n, int64_t p0,
+                                     int64_t* ctx) {
+  const int k = shm_find(tab, n, p0, false);
+  if (k >= 0) {
+    ctx[0] = tab[(int64_t)k * 4 + 0];
+    ctx[1] = tab[(int64_t)k * 4 + 1];
+    ctx[2] = tab[(int64_t)k * 4 + 2];
+    ctx[3] = k > 0 ? tab[(int64_t)(k - 1) * 4 + 3] : 0;
+    ctx[4] = tab[(int64_t)k * 4 + 3];
+  } else {
+    ctx[0] = ctx[1] = ctx[2] = -1;
+    ctx[3] = ctx[4] = 0;
+  }
+  ctx[5] = k + 1 < n ? tab[(int64_t)(k + 1) * 4] : INT64_MAX;
+}
+
+// where a live position p lies: inside a segment (its own, since it is written
+// here) or in the replicated prefix; e = foreign nodes ranked before p
+__device__ inline ShmPlace shm_place(const int64_t* __restrict__ tab, int n,
+                                     const int64_t* ctx, int64_t p) {
+  ShmPlace r;
+  int64_t lo, hi, eb, ei;
+  if (p >= ctx[0] && p < ctx[5]) {  // (the workgroup's segment context: no search)
+    lo = ctx[0];
+    hi = ctx[1];
+    eb = ctx[3];
+    ei = ctx[4];
+  } else {
+    const int k = shm_find(tab, n, p, false);
+    lo = k >= 0 ? tab[(int64_t)k * 4 + 0] : -1;
+    hi = k >= 0 ? tab[(int64_t)k * 4 + 1] : -1;
+    eb = k > 0 ? tab[(int64_t)(k - 1) * 4 + 3] : 0;
+    ei = k >= 0 ? tab[(int64_t)k * 4 + 3] : 0;
+  }
+  r.own = lo >= 0 && p < hi;
+  r.lo = lo;
+  r.hi = hi;
+  // segments with lo < p: through k, except k itself when p is its first position
+  r.e = (lo >= 0 && lo < p) ? ei : eb;
+  return r;
+}
+
 // StatT: int32 class counts (classification) or int64 {count, fixed-point sum}.
 template <typename StatT>
 __global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
     const int32_t* __restrict__ rec, const StatT* __restrict__ st, int64_t P, int C,
     const int32_t* __restrict__ rank, const double* __restrict__ edges, int EB,
     const int64_t* __restrict__ total, uint8_t* __restrict__ base, bool reg, int crit, int y_exp,
-    const double* __restrict__ xtab, int xtab_n, const double* __restrict__ thr_pos) {
+    const double* __restrict__ xtab, int xtab_n, const double* __restrict__ thr_pos,
+    const int64_t* __restrict__ tab, int n_tab, int me, bool emit_prefix, int64_t cap_nodes) {
   const int64_t p = (int64_t)blockIdx.x * kAsmThreads + threadIdx.x;
+  // shared-host assembly: the table segment around this workgroup's first position
+  __shared__ int64_t s_ctx[6];
+  if (tab != nullptr) {
+    if (threadIdx.x == 0) shm_block_ctx(tab, n_tab, (int64_t)blockIdx.x * kAsmThreads, s_ctx);
+    __syncthreads();
+  }
   if (p >= P) return;
-  const int j = rank[p];
-  if (j < 0) return;
-  const AsmCols o = asm_cols(base, *total, C, reg);
+  const int j0 = rank[p];
+  if (j0 < 0) return;
+  const int64_t N = *total;
+  if (cap_nodes > 0 && N > cap_nodes) return;  // (the host buffer is too small: re-emitted)
+  int64_t j = j0;
+  int64_t e_own = 0;  // foreign nodes ranked before p
+  bool in_seg = false;
+  int64_t seg_lo = 0, seg_hi = 0;
+  if (tab != nullptr) {
+    ShmPlace pl = shm_place(tab, n_tab, s_ctx, p);
+    if (!pl.own && !emit_prefix) return;  // replicated prefix nodes: one rank writes them
+    e_own = pl.e;
+    in_seg = pl.own;
+    seg_lo = pl.lo;
+    seg_hi = pl.hi;
+    j += e_own;
+  }
+  const AsmCols o = asm_cols(base, N, C, reg);
   const int32_t* R = rec + p * 6;
   const int f = R[0];
   const int b = R[1];
+  // a child's final id: its local exclusive rank plus the foreign nodes before it
+  auto child = [&](int64_t q) -> int32_t {
+    const int rq = rank[q];
+    const int64_t loc = rq >= 0 ? rq : ~rq;
+    if (tab == nullptr) return (int32_t)loc;
+    const int64_t e = (in_seg && q >= seg_lo && q < seg_hi) ? e_own : shm_foreign_before(tab, n_tab, q);
+    return (int32_t)(loc + e);
+  };
   if (f >= 0) {
     o.feature[j] = f;
     o.bin[j] = b;
-    o.left[j] = rank[R[2]];
-    o.right[j] = rank[R[3]];
+    o.left[j] = child(R[2]);
+    o.right[j] = child(R[3]);
     o.threshold[j] = thr_pos ? thr_pos[p] : edges[(int64_t)f * EB + b];
   } else {
     o.feature[j] = -1;
@@ -383,6 +497,131 @@ void launch_own_scatter(hipStream_t stream, const void* rows, int64_t k, int C, 
   MT_HIP_CHECK(hipGetLastError());
 }
 
+// gvec (int64, this rank's all-gather row): [0] local tree depth, [1] left to the
+// host (its free shared-buffer slots), [2 + s] nodes of segment s when this rank
+// owns it (0 otherwise). A segment's count is the difference of the exclusive
+// ranks at its ends (asm_rank_kernel: every position carries one).
+__global__ __launch_bounds__(256) void shm_seg_count_kernel(const int64_t* __restrict__ segs, int S,
+                                                            int me, const int32_t* __restrict__ rank,
+                                                            int64_t P, const int64_t* __restrict__ total,
+                                                            int64_t* __restrict__ gvec) {
+  const int s = blockIdx.x * 256 + threadIdx.x;
+  if (s == 0) gvec[0] = total[1];
+  if (s >= S) return;
+  const int64_t lo = segs[(int64_t)s * 3 + 0], hi = segs[(int64_t)s * 3 + 1];
+  const int64_t owner = segs[(int64_t)s * 3 + 2];
+  auto excl = [&](int64_t x) -> int64_t {
+    if (x >= P) return total[0];
+    const int r = rank[x];
+    return r >= 0 ? r : ~r;
+  };
+  gvec[2 + s] = (owner == me && lo < hi) ? excl(hi) - excl(lo) : 0;
+}
+
+constexpr int kShmMaxSegs = 4096;  // 2 per ownership unit (grow.hip kOwnMax = 2048)
+
+// One workgroup: every segment's count (summed over the gathered rows: one owner
+// each), the segments sorted by lo (bitonic, LDS), the running count of other
+// ranks' nodes -> tab [S][4]; unused entries get lo = INT64_MAX (sorted last).
+// total becomes the whole tree's {nodes, depth}.
+__global__ __launch_bounds__(1024) void shm_seg_prefix_kernel(const int64_t* __restrict__ gall,
+                                                              int nranks, int W,
+                                                              const int64_t* __restrict__ segs,
+                                                              int S, int me, int64_t* __restrict__ total,
+                                                              int64_t* __restrict__ tab) {
+  __shared__ uint64_t key[kShmMaxSegs];
+  __shared__ int32_t idx[kShmMaxSegs];
+  __shared__ int64_t wsum[1024 / kWave];
+  __shared__ int64_t carry;
+  const int tid = threadIdx.x;
+  int N2 = 1;
+  while (N2 < S) N2 <<= 1;
+  for (int i = tid; i < N2; i += 1024) {
+    uint64_t k = ~0ull;
+    if (i < S) {
+      const int64_t lo = segs[(int64_t)i * 3 + 0], hi = segs[(int64_t)i * 3 + 1];
+      if (lo < hi) k = (uint64_t)lo;
+    }
+    key[i] = k;
+    idx[i] = i;
+  }
+  __syncthreads();
+  for (int size = 2; size <= N2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < N2; i += 1024) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const uint64_t ka = key[i], kb = key[j];
+          const bool up = (i & size) == 0;
+          if ((ka > kb) == up) {
+            key[i] = kb;
+            key[j] = ka;
+            const int32_t t = idx[i];
+            idx[i] = idx[j];
+            idx[j] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (int b0 = 0; b0 < S; b0 += 1024) {
+    const int k = b0 + tid;
+    int64_t v = 0, lo = INT64_MAX, hi = INT64_MAX, owner = -1;
+    if (k < S && key[k] != ~0ull) {
+      const int s = idx[k];
+      lo = segs[(int64_t)s * 3 + 0];
+      hi = segs[(int64_t)s * 3 + 1];
+      owner = segs[(int64_t)s * 3 + 2];
+      int64_t c = 0;
+      for (int r = 0; r < nranks; ++r) c += gall[(int64_t)r * W + 2 + s];
+      v = owner != me ? c : 0;
+    }
+    // inclusive block scan of v
+    int64_t x = v;
+    for (int d = 1; d < kWave; d <<= 1) {
+      const int64_t y = __shfl_up(x, d, kWave);
+      if (lane_id() >= d) x += y;
+    }
+    if (lane_id() == kWave - 1) wsum[tid / kWave] = x;
+    __syncthreads();
+    int64_t off = carry;
+    for (int w = 0; w < tid / kWave; ++w) off += wsum[w];
+    if (k < S) {
+      tab[(int64_t)k * 4 + 0] = lo;
+      tab[(int64_t)k * 4 + 1] = hi;
+      tab[(int64_t)k * 4 + 2] = owner;
+      tab[(int64_t)k * 4 + 3] = off + x;
+    }
+    __syncthreads();
+    if (tid == 1023) carry = off + x;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    int64_t d = 0;
+    for (int r = 0; r < nranks; ++r) d = max(d, gall[(int64_t)r * W]);
+    total[0] += carry;
+    total[1] = d;
+  }
+}
+
+void launch_shm_seg_count(hipStream_t stream, const int64_t* segs, int S, int me,
+                          const int32_t* rank, int64_t P, const int64_t* total, int64_t* gvec) {
+  hipLaunchKernelGGL(shm_seg_count_kernel, dim3((unsigned)((S + 255) / 256 + (S == 0))), dim3(256),
+                     0, stream, segs, S, me, rank, P, total, gvec);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+void launch_shm_seg_prefix(hipStream_t stream, const int64_t* gall, int nranks, int W,
+                           const int64_t* segs, int S, int me, int64_t* total, int64_t* tab) {
+  if (S > kShmMaxSegs) throw std::runtime_error("shared-host assembly: too many segments");
+  hipLaunchKernelGGL(shm_seg_prefix_kernel, dim3(1), dim3(1024), 0, stream, gall, nranks, W, segs,
+                     S, me, total, tab);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
 int asm_tiles(int64_t P) { return (int)((P + kAsmTile - 1) / kAsmTile); }
 
 int64_t asm_node_bytes(int C, bool reg) { return asm_bytes(1, C, reg); }
@@ -390,17 +629,18 @@ int64_t asm_node_bytes(int C, bool reg) { return asm_bytes(1, C, reg); }
 void launch_asm_emit(hipStream_t stream, const int32_t* rec, const void* st, bool st64,
                      int64_t P, int C, const int32_t* rank, const double* edges, int EB,
                      const int64_t* total, uint8_t* base, bool reg, int crit, int y_exp,
-                     const double* xtab, int xtab_n, const double* thr_pos) {
+                     const double* xtab, int xtab_n, const double* thr_pos, const int64_t* tab,
+                     int n_tab, int me, bool emit_prefix, int64_t cap_nodes) {
   const int64_t blocks = (P + kAsmThreads - 1) / kAsmThreads;
   if (blocks == 0) return;
   if (st64)
     hipLaunchKernelGGL(asm_emit_kernel<int64_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
                        stream, rec, (const int64_t*)st, P, C, rank, edges, EB, total, base, reg,
-                       crit, y_exp, xtab, xtab_n, thr_pos);
+                       crit, y_exp, xtab, xtab_n, thr_pos, tab, n_tab, me, emit_prefix, cap_nodes);
   else
     hipLaunchKernelGGL(asm_emit_kernel<int32_t>, dim3((unsigned)blocks), dim3(kAsmThreads), 0,
                        stream, rec, (const int32_t*)st, P, C, rank, edges, EB, total, base, reg,
-                       crit, y_exp, xtab, xtab_n, thr_pos);
+                       crit, y_exp, xtab, xtab_n, thr_pos, tab, n_tab, me, emit_prefix, cap_nodes);
   MT_HIP_CHECK(hipGetLastError());
 }
 

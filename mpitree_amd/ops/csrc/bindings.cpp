@@ -92,7 +92,12 @@ void launch_small_fit(hipStream_t, const void*, int, int64_t, int, int, const in
                       int64_t);
 void launch_asm_emit(hipStream_t, const int32_t*, const void*, bool, int64_t, int,
                      const int32_t*, const double*, int, const int64_t*, uint8_t*, bool, int, int,
-                     const double*, int, const double*);
+                     const double*, int, const double*, const int64_t*, int, int, bool, int64_t);
+void launch_targets(hipStream_t, const void*, bool, int64_t, int64_t*, int64_t*);
+void launch_shm_seg_count(hipStream_t, const int64_t*, int, int, const int32_t*, int64_t,
+                          const int64_t*, int64_t*);
+void launch_shm_seg_prefix(hipStream_t, const int64_t*, int, int, const int64_t*, int, int,
+                           int64_t*, int64_t*);
 }  // namespace mt
 
 template <typename T>
@@ -275,14 +280,15 @@ PYBIND11_MODULE(_hip, m) {
                            uintptr_t jobs, uintptr_t job_count, int C, int max_depth, int n_cu,
                            int64_t mss, int64_t msl, int64_t fr, uintptr_t host_ctl, int host_tag,
                            int dp, py::dict own) {
-    mt::OwnArgs o{0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, 0};
+    mt::OwnArgs o{0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr};
     if (own.size()) {
       auto g = [&](const char* k) { return own[k].cast<int64_t>(); };
       o = mt::OwnArgs{(int)g("P"), (int)g("rank"), (int)g("min_units"), (int)g("cap"),
                       P<int32_t>((uintptr_t)g("state")), P<int64_t>((uintptr_t)g("ranges")),
                       P<int32_t>((uintptr_t)g("node_owner")),
                       P<int32_t>((uintptr_t)g("job_owner")),
-                      own.contains("jobs_at_switch") ? (int)g("jobs_at_switch") : 0};
+                      own.contains("jobs_at_switch") ? (int)g("jobs_at_switch") : 0,
+                      own.contains("segs") ? P<int64_t>((uintptr_t)g("segs")) : nullptr};
     }
     return mt::PlanArgs{lists(cur),          lists(nxt),         P<int64_t>(rec),
                         P<int64_t>(split),   P<int64_t>(pitems), P<int32_t>(cursors),
@@ -330,12 +336,17 @@ PYBIND11_MODULE(_hip, m) {
   });
   // Host-mapped, fine-grained (coherent) memory the kernels can store into
   // directly: the level loop's termination counters travel without a copy.
-  m.def("host_alloc", [](size_t nbytes) {
+  // (coherent = false: coarse-grained, written through the L2 with full PCIe
+  // write bursts -- what a kernel streaming a finished tree to the host wants;
+  // tools/probes/zc_probe.hip)
+  m.def("host_alloc", [](size_t nbytes, bool coherent) {
     void* p = nullptr;
-    MT_HIP_CHECK(hipHostMalloc(&p, nbytes, hipHostMallocMapped | hipHostMallocCoherent));
+    MT_HIP_CHECK(hipHostMalloc(&p, nbytes,
+                               coherent ? (hipHostMallocMapped | hipHostMallocCoherent)
+                                        : (hipHostMallocMapped | hipHostMallocNonCoherent)));
     std::memset(p, 0, nbytes);
     return reinterpret_cast<uintptr_t>(p);
-  });
+  }, py::arg("nbytes"), py::arg("coherent") = true);
   m.def("host_device_ptr", [](uintptr_t p) {
     void* d = nullptr;
     MT_HIP_CHECK(hipHostGetDevicePointer(&d, reinterpret_cast<void*>(p), 0));
@@ -376,14 +387,43 @@ PYBIND11_MODULE(_hip, m) {
   m.def("asm_emit", [](uintptr_t s, uintptr_t rec, uintptr_t st, bool st64, int64_t npos, int C,
                        uintptr_t rank, uintptr_t edges, int EB, uintptr_t total, uintptr_t base,
                        bool reg, int crit, int y_exp, uintptr_t xtab, int xtab_n,
-                       uintptr_t thr_pos) {
+                       uintptr_t thr_pos, uintptr_t tab, int n_tab, int me, bool emit_prefix,
+                       int64_t cap_nodes) {
     mt::launch_asm_emit(S(s), P<int32_t>(rec), P<void>(st), st64, npos, C, P<int32_t>(rank),
                         P<double>(edges), EB, P<int64_t>(total), P<uint8_t>(base), reg, crit,
-                        y_exp, P<double>(xtab), xtab_n, P<double>(thr_pos));
+                        y_exp, P<double>(xtab), xtab_n, P<double>(thr_pos), P<int64_t>(tab),
+                        n_tab, me, emit_prefix, cap_nodes);
   }, py::arg("s"), py::arg("rec"), py::arg("st"), py::arg("st64"), py::arg("npos"), py::arg("C"),
      py::arg("rank"), py::arg("edges"), py::arg("EB"), py::arg("total"), py::arg("base"),
      py::arg("reg"), py::arg("crit"), py::arg("y_exp"), py::arg("xtab"), py::arg("xtab_n"),
-     py::arg("thr_pos") = 0);
+     py::arg("thr_pos") = 0, py::arg("tab") = 0, py::arg("n_tab") = 0, py::arg("me") = 0,
+     py::arg("emit_prefix") = true, py::arg("cap_nodes") = 0);
+  m.def("targets", [](uintptr_t s, uintptr_t y, bool y64, int64_t n, uintptr_t st, uintptr_t out) {
+    mt::launch_targets(S(s), P<void>(y), y64, n, P<int64_t>(st), P<int64_t>(out));
+  });
+  // node-local shared-host assembly (parallel/shared_tree.py)
+  m.def("shm_seg_count", [](uintptr_t s, uintptr_t segs, int S_, int me, uintptr_t rank,
+                            int64_t npos, uintptr_t total, uintptr_t gvec) {
+    mt::launch_shm_seg_count(S(s), P<int64_t>(segs), S_, me, P<int32_t>(rank), npos,
+                             P<int64_t>(total), P<int64_t>(gvec));
+  });
+  m.def("shm_seg_prefix", [](uintptr_t s, uintptr_t gall, int nranks, int W, uintptr_t segs,
+                             int S_, int me, uintptr_t total, uintptr_t tab) {
+    mt::launch_shm_seg_prefix(S(s), P<int64_t>(gall), nranks, W, P<int64_t>(segs), S_, me,
+                              P<int64_t>(total), P<int64_t>(tab));
+  });
+  // pin (and map for device access) host memory the process did not allocate
+  // through HIP, e.g. a /dev/shm mapping several ranks share
+  m.def("host_register", [](uintptr_t p, size_t nbytes) {
+    MT_HIP_CHECK(hipHostRegister(reinterpret_cast<void*>(p), nbytes,
+                                 hipHostRegisterMapped | hipHostRegisterPortable));
+    void* d = nullptr;
+    MT_HIP_CHECK(hipHostGetDevicePointer(&d, reinterpret_cast<void*>(p), 0));
+    return reinterpret_cast<uintptr_t>(d);
+  });
+  m.def("host_unregister", [](uintptr_t p) {
+    MT_HIP_CHECK(hipHostUnregister(reinterpret_cast<void*>(p)));
+  });
   m.def("label_count", [](uintptr_t s, uintptr_t y, int64_t n, int64_t lo, int R,
                           uintptr_t counts, bool checked) {
     mt::launch_label_count(S(s), P<int64_t>(y), n, lo, R, P<uint32_t>(counts), checked);

@@ -72,6 +72,11 @@ struct OwnArgs {
   // level loop becomes a finisher job instead (when it has at most this many
   // rows): the rank's own work is its finisher jobs, no own levels
   int jobs_at_switch = 0;
+  // (optional) [2 * cap][3] every unit's position segments {lo, hi, owner}, in unit
+  // order: a node unit's left and right child subtrees, a job unit's subtree and an
+  // empty {0, 0, -1}; the node-local shared-host assembly ranks its own nodes with
+  // them (assemble.hip shm_*)
+  int64_t* segs = nullptr;
 };
 
 struct PlanArgs {

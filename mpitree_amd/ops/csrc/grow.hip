@@ -404,6 +404,23 @@ __device__ bool own_switch(const PlanArgs& a, OwnShared& os, PlanShared& sh, int
       a.own.ranges[(int64_t)k * 2 + 0] = lo;
       a.own.ranges[(int64_t)k * 2 + 1] = hi;
     }
+    if (a.own.segs) {  // every unit's child segments, with its owner (same on every rank)
+      int64_t* sg = a.own.segs + (int64_t)u * 6;
+      const int64_t owner = (id & kOwnJob) ? a.own.job_owner[id & ~kOwnJob] : a.own.node_owner[id];
+      int64_t mid = hi, lo2 = 0, hi2 = 0, own2 = -1;
+      if (!(id & kOwnJob)) {  // left child subtree [pos + 1, pos + 2 nl), right the rest
+        mid = a.cur.pos[id] + 2 * plan_decide(a, id).nl;
+        lo2 = mid;
+        hi2 = hi;
+        own2 = owner;
+      }
+      sg[0] = lo;
+      sg[1] = mid;
+      sg[2] = owner;
+      sg[3] = lo2;
+      sg[4] = hi2;
+      sg[5] = own2;
+    }
   }
   __syncthreads();
   const int NR = os.nr;

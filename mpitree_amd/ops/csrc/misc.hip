@@ -3,6 +3,7 @@
 #include "criterion.h"
 
 #include <algorithm>
+#include <climits>
 
 namespace mt {
 
@@ -105,6 +106,102 @@ void launch_label_encode(hipStream_t stream, const int64_t* y, int64_t n, int64_
   if (n <= 0) return;
   hipLaunchKernelGGL(label_encode_kernel, dim3(label_grid(n)), dim3(256), 0, stream, y, n, lo,
                      lut, out);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
+// ---- device-resident regression targets (ops/gpu_prepare.py) --------------
+// Fixed-point int64 targets yi = rint(ldexp(y, e)) with the exponent chosen from
+// max |y| (core/fit.py fixed_point_exponent), their root statistics {sum, min,
+// max} and the finite check, in two launches and no host round trip: the host
+// reads {finite, e, sum, min, max} together with the binning's first wait.
+// st: int64 [8] = {max |y| bits, non-finite count, e, sum, min, max, -, -}.
+
+// ceil(log2(x)) for x > 0, exact (frexp: x = m 2^k, m in [0.5, 1))
+__device__ inline int ceil_log2_exact(double x) {
+  int k;
+  const double m = frexp(x, &k);
+  return m == 0.5 ? k - 1 : k;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void target_stats_kernel(const T* __restrict__ y, int64_t n,
+                                                           int64_t* __restrict__ st) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st[4] = INT64_MAX;
+    st[5] = INT64_MIN;
+  }
+  double amax = 0.0;
+  unsigned bad = 0;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double v = (double)y[i];
+    if (!isfinite(v)) {
+      ++bad;
+    } else {
+      amax = fmax(amax, fabs(v));
+    }
+  }
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    amax = fmax(amax, __shfl_xor(amax, d, kWave));
+    bad += __shfl_xor(bad, d, kWave);
+  }
+  if (lane_id() == 0) {
+    // non-negative doubles order as their bit patterns
+    atomicMax(reinterpret_cast<unsigned long long*>(st), (unsigned long long)__double_as_longlong(amax));
+    if (bad) atomicAdd(reinterpret_cast<unsigned long long*>(st) + 1, (unsigned long long)bad);
+  }
+}
+
+__device__ inline int fixed_point_exponent_dev(double absmax, int64_t n) {
+  if (!(absmax > 0.0) || !isfinite(absmax)) return 0;
+  const int e = 62 - ceil_log2_exact((double)(n > 1 ? n : 1) + 1.0) -
+                ceil_log2_exact(absmax * (1.0 + 0x1p-40));
+  return e > 1000 ? 1000 : (e < -1000 ? -1000 : e);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void target_encode_kernel(const T* __restrict__ y, int64_t n,
+                                                            int64_t* __restrict__ st,
+                                                            int64_t* __restrict__ out) {
+  const int e = fixed_point_exponent_dev(__longlong_as_double(st[0]), n);
+  if (blockIdx.x == 0 && threadIdx.x == 0) st[2] = e;
+  long long sum = 0, mn = LLONG_MAX, mx = LLONG_MIN;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double v = (double)y[i];
+    const long long q = isfinite(v) ? (long long)rint(ldexp(v, e)) : 0;
+    out[i] = q;
+    sum += q;
+    mn = q < mn ? q : mn;
+    mx = q > mx ? q : mx;
+  }
+  for (int d = kWave / 2; d > 0; d >>= 1) {
+    sum += __shfl_xor(sum, d, kWave);
+    const long long a = __shfl_xor(mn, d, kWave), b = __shfl_xor(mx, d, kWave);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if (lane_id() == 0) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(st) + 3, (unsigned long long)sum);
+    atomicMin(reinterpret_cast<long long*>(st) + 4, mn);
+    atomicMax(reinterpret_cast<long long*>(st) + 5, mx);
+  }
+}
+
+void launch_targets(hipStream_t stream, const void* y, bool y64, int64_t n, int64_t* st,
+                    int64_t* out) {
+  MT_HIP_CHECK(hipMemsetAsync(st, 0, 8 * sizeof(int64_t), stream));
+  if (n <= 0) return;
+  const unsigned g = std::min(label_grid(n), 1024u);
+  if (y64) {
+    hipLaunchKernelGGL(target_stats_kernel<double>, dim3(g), dim3(256), 0, stream,
+                       (const double*)y, n, st);
+    hipLaunchKernelGGL(target_encode_kernel<double>, dim3(g), dim3(256), 0, stream,
+                       (const double*)y, n, st, out);
+  } else {
+    hipLaunchKernelGGL(target_stats_kernel<float>, dim3(g), dim3(256), 0, stream,
+                       (const float*)y, n, st);
+    hipLaunchKernelGGL(target_encode_kernel<float>, dim3(g), dim3(256), 0, stream,
+                       (const float*)y, n, st, out);
+  }
   MT_HIP_CHECK(hipGetLastError());
 }
 

@@ -65,6 +65,7 @@ from ..models.tree_arrays import TreeArrays
 from ..utils.observability import profiling
 from . import hip_backend as hb
 from ..parallel.failure import ABORT, check_abort, fault_point
+from ..parallel import shared_tree
 from ..parallel.strategies import feature_blocks
 
 __all__ = ["DeviceGrower", "device_loop_supported"]
@@ -512,6 +513,7 @@ class DeviceGrower:
         J = 0
         t0 = time.perf_counter()
         comm_bytes = []
+        shared = None
         if not root_term and jobs_host is None:
             KMAX = n // (fr + 1) + 2
             IMAX = KMAX + n_loc // 1024 + 2 * hb.N_CU + 16
@@ -560,6 +562,8 @@ class DeviceGrower:
                     own_ranges=torch.zeros((OWN_CAP if own else 1, 2), **i64),
                     own_node=torch.empty(KMAX if own else 1, dtype=torch.int32, device=dev),
                     own_job=torch.empty(JMAX if own else 1, dtype=torch.int32, device=dev),
+                    # every unit's child segments {lo, hi, owner} (shared-host assembly)
+                    own_segs=torch.zeros((2 * OWN_CAP if own else 1, 3), **i64),
                     # fused selection: per-feature left counts and node totals (scan)
                     sel_left=torch.empty((KMAX, F_h, 2) if fsel else 1, dtype=torch.int32,
                                          device=dev),
@@ -617,7 +621,8 @@ class DeviceGrower:
                                 ranges=ws["own_ranges"].data_ptr(),
                                 node_owner=ws["own_node"].data_ptr(),
                                 job_owner=ws["own_job"].data_ptr(),
-                                jobs_at_switch=own_jobs_at_switch(be))
+                                jobs_at_switch=own_jobs_at_switch(be),
+                                segs=ws["own_segs"].data_ptr())
 
             plan_cu = hb.N_CU * HIST_ITEMS_PER_CU // 2  # (the planner makes 2 items per "CU")
             # single-rank and subtree-ownership levels (no collective between the
@@ -812,7 +817,15 @@ class DeviceGrower:
             t1 = time.perf_counter()
             b0 = comm.bytes_communicated
             if getattr(self, "_owned", None) is not None:
-                self._exchange_owned(self._owned)
+                # ranks of one node: each writes its own nodes into a shared host
+                # buffer (no node exchange); otherwise one all-gather of the nodes
+                pool = shared_tree.pool_for(comm, hip)
+                if pool is not None:
+                    shared = dict(comm=comm, pool=pool, segs=self._owned["own_segs"],
+                                  S=2 * int(self.stats["own_units"]))
+                    self.stats["assembly"] = "shared-host"
+                else:
+                    self._exchange_owned(self._owned)
             elif not (own and getattr(self, "_pre_live", None) is None):
                 self._exchange_nodes()
             self._owned = None
@@ -832,7 +845,8 @@ class DeviceGrower:
         table = None
         if d_edges is None:
             table = edges if isinstance(edges, np.ndarray) else edges.padded_edges()
-        ta = be.assemble_positions(table, int(p.criterion), y_exp, d_edges=d_edges)
+        ta = be.assemble_positions(table, int(p.criterion), y_exp, d_edges=d_edges,
+                                   shared=shared)
         self.timings["assemble"] = time.perf_counter() - t0
         if self.ckpt is not None:
             self.stats["checkpoint_levels_saved"] = self.ckpt.saved_levels

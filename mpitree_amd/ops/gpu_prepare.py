@@ -128,13 +128,27 @@ class _Labels:
 
 
 class _Targets:
-    """Regression targets as fixed-point int64 (exponent chosen from max |y|)."""
+    """Regression targets as fixed-point int64 (exponent chosen from max |y|).
+
+    fp32 / fp64 device targets: two kernels (``misc.hip`` target_stats /
+    target_encode) find max |y|, pick the exponent on the device, encode and
+    reduce the root {sum, min, max}, all enqueued ahead of the binning -- the
+    host reads the result with the binning's first wait (no second sync)."""
 
     def __init__(self, y, n, dev, encode_fallback, exponent):
         self.y, self.n, self.dev = y, n, dev
         self.fallback, self.exponent = encode_fallback, exponent
         self.dev_path = torch.is_tensor(y) and y.is_cuda and y.dim() == 1 and y.shape[0] == n
+        self.fused = False
         if self.dev_path and n > 0:
+            if y.dtype in (torch.float32, torch.float64) and y.is_contiguous():
+                self.fused = True
+                st = torch.empty(8, dtype=torch.int64, device=dev)
+                self.yi = torch.empty(n, dtype=torch.int64, device=dev)
+                native.hip().targets(_stream(), y.data_ptr(), y.dtype == torch.float64, n,
+                                     st.data_ptr(), self.yi.data_ptr())
+                self._st = _pinned_copy(st, "prep.reg.fused")
+                return
             self.yd = y.double()
             st = torch.stack([self.yd.abs().max(), torch.isfinite(self.yd).all().double()])
             self._st = _pinned_copy(st, "prep.reg.st")
@@ -142,8 +156,15 @@ class _Targets:
             self.dev_path = False
 
     def after_first_sync(self) -> bool:
-        """True: the fixed-point targets need another sync (always, on the device path)."""
+        """True: the fixed-point targets need another sync (the unfused device path)."""
         if not self.dev_path:
+            return False
+        if self.fused:
+            st = np.array(self._st, dtype=np.int64)
+            if st[1]:
+                raise ValueError("Input y contains NaN or infinity.")
+            self.e = int(st[2])
+            self._root = st[3:6].copy()
             return False
         if not self._st[1]:
             raise ValueError("Input y contains NaN or infinity.")

@@ -358,38 +358,43 @@ def _pinned_copy(t: torch.Tensor, key: str) -> np.ndarray:
     return view.numpy()
 
 
-_OUT_POOL: list = []  # (pinned tensor, its numpy view) pairs the assembled trees view
+_ZC_POOL: list = []  # [ndarray, device pointer, host pointer] of mapped host buffers
 
 
-def _pinned_out(nbytes: int):
-    """A pinned host buffer of at least ``nbytes`` for a fit's tree columns, as
-    ``(tensor, ndarray)`` over the same memory.
+def _zc_out(nbytes: int):
+    """A pinned, device-mapped host buffer of at least ``nbytes`` for a fit's tree
+    columns, as ``(ndarray, device pointer)``: the assembly's emit kernel stores
+    into it directly (zero-copy over PCIe: ~55 GB/s on MI355X against ~30-46 GB/s
+    for a device write plus a D2H DMA, ``tools/probes/zc_probe.hip``).
 
-    Pinning is the expensive part of a host allocation (~0.5 ms for a 12 MB
-    tree, more than its D2H copy), so buffers are pooled. The returned
-    :class:`TreeArrays` columns are numpy views of the pooled ndarray (numpy
-    points every view's ``base`` at it), so a buffer whose ndarray has no
-    references besides this pool's is free to reuse: a tree a caller still
-    holds is never overwritten."""
+    Pinning is the expensive part of a host allocation, so buffers are
+    pooled: the returned :class:`TreeArrays` columns are
+    numpy views of the pooled ndarray, so a buffer whose ndarray has no
+    references besides this pool's is free to reuse."""
+    import ctypes
 
-    def free(i) -> bool:  # references: the pool's tuple and getrefcount's argument
-        return sys.getrefcount(_OUT_POOL[i][1]) <= 2
+    def free(i) -> bool:  # references: the pool's entry and getrefcount's argument
+        return sys.getrefcount(_ZC_POOL[i][0]) <= 2
 
     best = None
-    for i in range(len(_OUT_POOL)):
-        if _OUT_POOL[i][0].numel() >= nbytes and free(i):
-            if best is None or _OUT_POOL[i][0].numel() < _OUT_POOL[best][0].numel():
+    for i in range(len(_ZC_POOL)):
+        if _ZC_POOL[i][0].size >= nbytes and free(i):
+            if best is None or _ZC_POOL[i][0].size < _ZC_POOL[best][0].size:
                 best = i
     if best is not None:
-        return _OUT_POOL[best]
-    buf = torch.empty(max(int(nbytes * 1.25), 1 << 16), dtype=torch.uint8, pin_memory=True)
-    ent = (buf, buf.numpy())
-    if len(_OUT_POOL) >= 8:  # keep a few: drop the oldest free buffer
-        drop = [i for i in range(len(_OUT_POOL)) if free(i)]
+        return _ZC_POOL[best][0], _ZC_POOL[best][1]
+    hip = native.hip()
+    if len(_ZC_POOL) >= 8:  # keep a few: drop the oldest free buffer
+        drop = [i for i in range(len(_ZC_POOL)) if free(i)]
         if drop:
-            _OUT_POOL.pop(drop[0])
-    _OUT_POOL.append(ent)
-    return ent
+            hptr = _ZC_POOL.pop(drop[0])[2]
+            hip.host_free(hptr)
+    size = max(int(nbytes * 1.25), 1 << 16)
+    hptr = int(hip.host_alloc(size, coherent=False))
+    nd = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(hptr))
+    ent = [nd, int(hip.host_device_ptr(hptr)), hptr]
+    _ZC_POOL.append(ent)
+    return ent[0], ent[1]
 
 
 def xlog2x_table_f32(device) -> torch.Tensor:
@@ -612,14 +617,17 @@ class HipBackend:
         self.pos_st.index_copy_(0, d_pos, d_st.reshape(-1, self.C).to(self.pos_st.dtype))
 
     def assemble_positions(self, edges, crit: int, y_exp: int = 0, d_edges=None,
-                           thr_pos=None) -> TreeArrays:
+                           thr_pos=None, shared=None) -> TreeArrays:
         """Compact the position space into the finished, pre-ordered
-        :class:`TreeArrays` (numpy views of one pinned host buffer; every column
+        :class:`TreeArrays` (numpy views of one mapped host buffer; every column
         is computed on the device, nothing is derived on the host afterwards).
         ``d_edges``: the device fp64 threshold table ``[F, W]`` (any row stride);
         otherwise ``edges`` (host ``[F, W]``) is uploaded. Rank -> emit run back
-        to back (the emit kernel lays the columns out from the device node
-        count), then the host waits for the node count and the single D2H."""
+        to back; the emit kernel stores the columns straight into pinned host
+        memory (zero-copy over PCIe: no device staging buffer, no separate D2H),
+        laid out from the device node count, then the host waits once.
+        ``shared``: the node-local shared-host assembly of a subtree-ownership fit
+        (``parallel/shared_tree.py``): dict(comm, pool, segs, S)."""
         P, C = self.P, self.C
         hip = self.hip
         s = _stream()
@@ -630,41 +638,79 @@ class HipBackend:
         al = lambda x: (x + 255) // 256 * 256  # noqa: E731
         o_total = al(max(tiles, 1) * 4)
         o_rank = o_total + 256
-        o_out = o_rank + al(P * 4)
-        ws = _workspace(self.device, "asm", o_out + P * bpn)
+        ws = _workspace(self.device, "asm", o_rank + al(P * 4))
         base = ws.data_ptr()
         total = ws[o_total : o_total + 16].view(torch.int64)  # {nodes, depth}
         hip.asm_rank(s, self.pos_rec.data_ptr(), P, base, base + o_total, base + o_rank)
-        hip.asm_emit(s, self.pos_rec.data_ptr(), self.pos_st.data_ptr(), self.reg, P, C,
-                     base + o_rank, 0 if d_edges is None else d_edges.data_ptr(),
-                     0 if d_edges is None else int(d_edges.stride(0)),
-                     base + o_total, base + o_out, bool(self.reg), int(crit), int(y_exp),
-                     self.xtab.data_ptr(), XTAB_N,
-                     thr_pos=0 if thr_pos is None else thr_pos.data_ptr())
-        h_total = _pinned_copy(total, "asm.total")
-        # the columns are laid out from the device node count, so a copy sized for
-        # the previous fit's count on this position space (a refit of the same
-        # data: the same count) is a prefix-complete guess, enqueued before the
-        # wait -- one host wait instead of two; a larger tree copies the rest
-        # after the count arrives
+
+        def emit(out_dev: int, cap_nodes: int, **kw):
+            hip.asm_emit(s, self.pos_rec.data_ptr(), self.pos_st.data_ptr(), self.reg, P, C,
+                         base + o_rank, 0 if d_edges is None else d_edges.data_ptr(),
+                         0 if d_edges is None else int(d_edges.stride(0)),
+                         base + o_total, out_dev, bool(self.reg), int(crit), int(y_exp),
+                         self.xtab.data_ptr(), XTAB_N,
+                         thr_pos=0 if thr_pos is None else thr_pos.data_ptr(),
+                         cap_nodes=cap_nodes, **kw)
+
+        if shared is not None:
+            return self._assemble_shared(shared, emit, total, base + o_rank, bpn)
+        # the emit lays the columns out from the device node count, so a buffer
+        # sized for the previous fit's count on this position space (a refit of
+        # the same data: the same count) is written in the same pass; a larger
+        # tree (the kernel writes nothing past the buffer) is emitted again
         key = (str(self.device), P, C, bool(self.reg))
-        guess = _ASM_HINT.get(key, 0)
-        host, have = None, 0
-        if guess:
-            have = guess * bpn
-            host, host_np = _pinned_out(have)
-            host[:have].copy_(ws[o_out : o_out + have], non_blocking=True)
+        nd, dptr = _zc_out(max(_ASM_HINT.get(key, 0), 1) * bpn)
+        emit(dptr, nd.size // bpn)
+        h_total = _pinned_copy(total, "asm.total")
         torch.cuda.current_stream(self.device).synchronize()
         self._check_finisher_watch()
         N, max_depth = int(h_total[0]), int(h_total[1])
         _ASM_HINT[key] = N
         nbytes = N * bpn
-        if nbytes > have:
-            host, host_np = _pinned_out(nbytes)
-            host[:nbytes].copy_(ws[o_out : o_out + nbytes], non_blocking=True)
+        if nbytes > nd.size:
+            nd, dptr = _zc_out(nbytes)
+            emit(dptr, nd.size // bpn)
             torch.cuda.current_stream(self.device).synchronize()
         self.pos_rec = self.pos_st = None
-        return TreeArrays.from_packed(host_np[:nbytes], N, C, bool(self.reg),
+        return TreeArrays.from_packed(nd[:nbytes], N, C, bool(self.reg), max_depth=max_depth)
+
+    def _assemble_shared(self, sh, emit, total, rank_ptr: int, bpn: int) -> TreeArrays:
+        """Each rank of one node writes its own nodes (rank 0 also the replicated
+        prefix) into one shared host buffer (``parallel/shared_tree.py``)."""
+        from ..parallel.shared_tree import HEADER
+
+        comm, pool, segs, S = sh["comm"], sh["pool"], sh["segs"], int(sh["S"])
+        hip = self.hip
+        s = _stream()
+        Pn, me = int(comm.world_size), int(comm.rank)
+        W = 2 + int(segs.shape[0])
+        g = _workspace(self.device, "shm.seg", (W * (Pn + 1) + 4 * int(segs.shape[0])) * 8)
+        g = g[: (W * (Pn + 1) + 4 * int(segs.shape[0])) * 8].view(torch.int64)
+        gvec, gall, tab = g[:W], g[W : W * (Pn + 1)], g[W * (Pn + 1) :]
+        hip.shm_seg_count(s, segs.data_ptr(), S, me, rank_ptr, self.P, total.data_ptr(),
+                          gvec.data_ptr())
+        gvec[1].fill_(pool.free_mask())
+        comm.all_gather_seg_counts(gall, gvec, segs, S)
+        hip.shm_seg_prefix(s, gall.data_ptr(), Pn, W, segs.data_ptr(), S, me, total.data_ptr(),
+                           tab.data_ptr())
+        kw = dict(tab=tab.data_ptr(), n_tab=S, me=me, emit_prefix=me == 0)
+        slot = pool.take_next()  # (agreed last fit: emit before the host wait)
+        if slot is not None:
+            emit(slot.dev + HEADER, (slot.nbytes - HEADER) // bpn, **kw)
+        h = _pinned_copy(torch.cat([total, gall.view(Pn, W)[:, 1]]), "shm.total")
+        torch.cuda.current_stream(self.device).synchronize()
+        self._check_finisher_watch()
+        N, max_depth = int(h[0]), int(h[1])
+        nbytes = N * bpn
+        masks = [int(v) for v in h[2 : 2 + Pn]]
+        if slot is None or nbytes > slot.nbytes - HEADER:  # (every rank sees the same N)
+            slot = pool.choose(masks, nbytes)
+            emit(slot.dev + HEADER, 0, **kw)
+            torch.cuda.current_stream(self.device).synchronize()
+        pool.barrier(slot)
+        pool.plan_next(masks, slot, nbytes)
+        self.pos_rec = self.pos_st = None
+        return TreeArrays.from_packed(slot.nd[HEADER : HEADER + nbytes], N, self.C, bool(self.reg),
                                       max_depth=max_depth)
 
     def small_fit_supported(self, comm=None) -> bool:

@@ -256,6 +256,11 @@ class DistComm(LocalComm):
             dist.all_gather_into_tensor(out, inp, group=self.group)
         self.bytes_communicated += inp.numel() * inp.element_size() * self.world_size
 
+    def all_gather_seg_counts(self, out: torch.Tensor, inp: torch.Tensor, segs, S: int) -> None:
+        """The shared-host assembly's per-segment node counts (``segs``/``S``: the
+        segment table, used by simulated communicators only)."""
+        self.all_gather_device(out, inp)
+
     def all_reduce_device(self, t: torch.Tensor, op=dist.ReduceOp.SUM) -> None:
         if self._staged(t):
             h = t.cpu()

@@ -136,13 +136,15 @@ def _fit_rank_gpu_large(rank, world, regression, strategy="auto"):
     for it in range(2):  # repeated fits: the job split must not depend on append order
         est = cls(strategy=strategy, device="cuda").fit(X, y)
         ta = est.tree_arrays_
-        for k in FIELDS:
+        for k in FIELDS + ("threshold", "impurity"):
             outs[f"{k}{it}"] = getattr(ta, k)
+        outs[f"stat{it}"] = ta.value if regression else ta.count
         outs[f"engine{it}"] = np.array([est.fit_stats_["engine"]])
         outs[f"mode{it}"] = np.array([est.fit_stats_.get("mode", "")])
         outs[f"bytes{it}"] = np.array(est.fit_stats_.get("comm_bytes_per_level", [0]) or [0])
         outs[f"xbytes{it}"] = np.array([est.fit_stats_.get("comm_bytes_exchange", 0)])
         outs[f"own_rows{it}"] = np.array([est.fit_stats_.get("own_rows", -1)])
+        outs[f"asm{it}"] = np.array([est.fit_stats_.get("assembly", "")])
     return outs
 
 
@@ -177,10 +179,14 @@ def test_gpu_ranks_equal_single_gpu_at_scale(regression, strategy, world):
             if want == "subtree-owned":  # no per-level collective, one node exchange
                 assert o[f"bytes{it}"].sum() == 0 and o[f"xbytes{it}"][0] > 0
                 assert o[f"own_rows{it}"][0] > 0  # every rank owns units
+                # ranks of one node: each wrote its own nodes into the shared tree
+                # (the first fit's tree is still held: the repeat takes another slot)
+                assert str(o[f"asm{it}"][0]) == "shared-host"
             else:
                 assert o[f"bytes{it}"].sum() > 0  # per-level collectives ran
-            for k in FIELDS:
+            for k in FIELDS + ("threshold", "impurity"):
                 np.testing.assert_array_equal(o[f"{k}{it}"], getattr(ref, k), err_msg=k)
+            np.testing.assert_array_equal(o[f"stat{it}"], ref.value if regression else ref.count)
 
 
 def _fit_rank_gpu_exact(rank, world, regression):
