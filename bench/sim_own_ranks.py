@@ -101,7 +101,7 @@ class SimOwnComm(LocalComm):
     simulated = True
 
     def __init__(self, P: int, rank: int, device, ref_rows: torch.Tensor, ref_pos=None,
-                 ref_depth=0, pool=None):
+                 ref_depth=0, pool=None, ref_recs=None):
         self.world_size = P
         self.rank = rank
         self.device = device
@@ -110,6 +110,19 @@ class SimOwnComm(LocalComm):
         self.ref_pos, self.ref_depth = ref_pos, int(ref_depth)
         self._shm_pool = pool if pool is not None else False
         self._head = torch.tensor([int(ref_depth), 1], dtype=torch.int64, device=device)
+        self.ref_recs, self._lvl = ref_recs, 0
+
+    def all_gather_device(self, out, inp):
+        # feature-parallel prefix levels: every other rank's best split of each
+        # node stands in as the reference fit's (global best) record, which the
+        # combine picks over this rank's block-best (ties: the lower feature)
+        P = self.world_size
+        ref = self.ref_recs[self._lvl].reshape(-1)
+        self._lvl += 1
+        o = out.view(P, -1)
+        o.copy_(ref[None, :].expand(P, -1))
+        o[self.rank].copy_(inp.view(-1))
+        self.bytes_communicated += inp.numel() * inp.element_size() * P
 
     def all_gather_rows(self, t):
         # bytes of a real exchange: every rank's rows, padded to the largest share
@@ -191,7 +204,11 @@ def main():
 
     for _ in range(2):
         fit()
+    from mpitree_amd.ops import device_grower as dg
+
+    dg.REC_DUMP = []  # the reference fit's per-level split records (prefix stand-in)
     ref, ref_rows = reference_rows(fit, dev, a.regression)
+    ref_recs, dg.REC_DUMP = dg.REC_DUMP, None
     ref_pos = ref_rows[:, 0].long().contiguous()  # live positions, ascending
     pool = None
     if not a.no_shared:
@@ -201,8 +218,8 @@ def main():
         for r in range(P) if a.only_rank is None else [a.only_rank]:
             times, st, ph = [], {}, []
             for i in range(a.reps + 2):
-                comm = (SimOwnComm(P, r, dev, ref_rows, ref_pos, ref.arrays.max_depth, pool)
-                        if P > 1 else None)
+                comm = (SimOwnComm(P, r, dev, ref_rows, ref_pos, ref.arrays.max_depth, pool,
+                                   ref_recs) if P > 1 else None)
                 if pool is not None:
                     pool.slot.prefill()
                 torch.cuda.synchronize()
@@ -217,6 +234,7 @@ def main():
                                if isinstance(v, float)})
                 assert res.arrays.equal(ref.arrays), f"P={P} rank {r}: tree differs"
             per_rank.append(dict(ms=float(np.median(times)), rows=st.get("own_rows", a.n),
+                                 fp_levels=st.get("fp_prefix_levels", 0),
                                  units=st.get("own_units", 0), levels=st.get("levels"),
                                  mode=st.get("mode", "single-gpu"),
                                  exchange_mb=st.get("comm_bytes_exchange", 0) / 1e6,
@@ -227,6 +245,7 @@ def main():
                    rank_ms=[round(v, 3) for v in ms], rows_owned=[p["rows"] for p in per_rank],
                    units=per_rank[0]["units"], levels=[p["levels"] for p in per_rank],
                    mode=per_rank[0]["mode"], exchange_mb=round(per_rank[0]["exchange_mb"], 2),
+                   fp_prefix_levels=[p["fp_levels"] for p in per_rank],
                    nodes=ref.arrays.node_count, tree_equal=True,
                    phases_max_rank=per_rank[int(np.argmax(ms))]["phases"])
         print(json.dumps(out), flush=True)

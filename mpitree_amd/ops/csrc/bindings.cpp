@@ -280,7 +280,7 @@ PYBIND11_MODULE(_hip, m) {
                            uintptr_t jobs, uintptr_t job_count, int C, int max_depth, int n_cu,
                            int64_t mss, int64_t msl, int64_t fr, uintptr_t host_ctl, int host_tag,
                            int dp, py::dict own) {
-    mt::OwnArgs o{0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr};
+    mt::OwnArgs o{0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, 0, nullptr, 0};
     if (own.size()) {
       auto g = [&](const char* k) { return own[k].cast<int64_t>(); };
       o = mt::OwnArgs{(int)g("P"), (int)g("rank"), (int)g("min_units"), (int)g("cap"),
@@ -288,7 +288,8 @@ PYBIND11_MODULE(_hip, m) {
                       P<int32_t>((uintptr_t)g("node_owner")),
                       P<int32_t>((uintptr_t)g("job_owner")),
                       own.contains("jobs_at_switch") ? (int)g("jobs_at_switch") : 0,
-                      own.contains("segs") ? P<int64_t>((uintptr_t)g("segs")) : nullptr};
+                      own.contains("segs") ? P<int64_t>((uintptr_t)g("segs")) : nullptr,
+                      own.contains("build_all") ? (int)g("build_all") : 0};
     }
     return mt::PlanArgs{lists(cur),          lists(nxt),         P<int64_t>(rec),
                         P<int64_t>(split),   P<int64_t>(pitems), P<int32_t>(cursors),

@@ -77,6 +77,10 @@ struct OwnArgs {
   // empty {0, 0, -1}; the node-local shared-host assembly ranks its own nodes with
   // them (assemble.hip shm_*)
   int64_t* segs = nullptr;
+  // 1: the levels before the switch were feature-parallel (each rank holds only
+  // its feature block of the histograms), so at the switch every next-frontier
+  // child is built from rows (no larger sibling is derived from a parent)
+  int build_all = 0;
 };
 
 struct PlanArgs {

@@ -526,6 +526,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
   auto active = [&](int i) {
     return !own_sw || a.own.node_owner[i] < 0 || a.own.node_owner[i] == a.own.rank;
   };
+  const bool build_all = own_sw && a.own.build_all;
   // decisions of this level; at the switch (jobs_at_switch) the children that
   // would keep growing become finisher jobs: the rank's own work is its jobs
   auto decide = [&](int i) {
@@ -554,7 +555,10 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
   for (int b0 = 0; b0 < K && !one_chunk; b0 += kPlanThreads) {
     const int i = b0 + tid;
     int nb = 0;
-    if (i < K && active(i)) nb = decide(i).built >= 0 ? 1 : 0;
+    if (i < K && active(i)) {
+      const Decision d = decide(i);
+      nb = d.built < 0 ? 0 : (build_all && d.fate[0] == 2 && d.fate[1] == 2) ? 2 : 1;
+    }
     int t;
     plan_scan_excl(nb, sh.w, t);
     nb_tot += t;
@@ -576,8 +580,10 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     d.fate[0] = d.fate[1] = 0;
     if (i < K) d = decide(i);
     const bool act = i < K && active(i);
-    const int nb = act && d.built >= 0 ? 1 : 0;
-    const int nd = act && (d.fate[0] == 2 && d.fate[1] == 2) ? 1 : 0;
+    // (switch after feature-parallel levels: both children of a pair are built)
+    const bool both = build_all && d.fate[0] == 2 && d.fate[1] == 2;
+    const int nb = act && d.built >= 0 ? (both ? 2 : 1) : 0;
+    const int nd = act && (d.fate[0] == 2 && d.fate[1] == 2) && !both ? 1 : 0;
     const int ns = act && d.split ? 1 : 0;
     // built / derived offsets share one scan (each field <= kPlanThreads < 2^16)
     int tbd, ts;
@@ -630,6 +636,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
         if (d.built >= 0) {
           slot[d.built] = ob;
           if (nd) slot[1 - d.built] = NB + od;
+          if (both) slot[1 - d.built] = ob + 1;
         }
         for (int c = 0; c < 2; ++c) {
           const int64_t cm = c == 0 ? d.nl : d.nr;
@@ -679,7 +686,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
               for (int k = 0; k < C; ++k)
                 a.nxt.stats[(int64_t)sl * C + k] = (int32_t)plan_child_stat(a, i, r, d.nl, c, k);
             }
-            if (c != d.built) {  // derived: parent slot i of this level, sibling built slot
+            if (c != d.built && !both) {  // derived: parent slot i, sibling built slot
               int64_t* D = a.nxt.der + (int64_t)(sl - NB) * 3;
               D[0] = sl;
               D[1] = i;

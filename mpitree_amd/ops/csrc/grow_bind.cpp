@@ -220,7 +220,8 @@ void bind_grow(py::module_& m) {
                           ptr<int32_t>(o("state")), ptr<int64_t>(o("ranges")),
                           ptr<int32_t>(o("node_owner")), ptr<int32_t>(o("job_owner")),
                           own.contains("jobs_at_switch") ? (int)o("jobs_at_switch") : 0,
-                          own.contains("segs") ? ptr<int64_t>(o("segs")) : nullptr};
+                          own.contains("segs") ? ptr<int64_t>(o("segs")) : nullptr,
+                          own.contains("build_all") ? (int)o("build_all") : 0};
         }
         return c;
       }), py::arg("args"), py::arg("l0"), py::arg("l1"), py::arg("own") = py::dict())

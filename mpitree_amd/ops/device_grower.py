@@ -70,6 +70,8 @@ from ..parallel.strategies import feature_blocks
 
 __all__ = ["DeviceGrower", "device_loop_supported"]
 
+REC_DUMP = None  # list: the single-rank level loop appends each level's split records
+
 _WORKSPACES: dict = {}  # (device, n, F, B, C, reg, fr) -> level-loop buffers
 _HOST_CTL: dict = {}  # device index -> (device pointer, numpy view [64, 16] int32)
 _FIT_SEQ = [0]  # per-process fit counter: tags host slots so stale values never match
@@ -479,6 +481,13 @@ class DeviceGrower:
         fp, dp, own, f_lo, f_hi = self._mode(F)
         F_h = f_hi - f_lo
         P = getattr(comm, "world_size", 1)
+        # subtree ownership: the replicated levels before the switch run
+        # feature-parallel -- each rank histograms and scans its feature block
+        # only, one all-gather of the split records per level (fp_combine), and
+        # the switch level builds every child of the first owned level from rows
+        fpx = (own and F >= P and self.ckpt is None
+               and os.environ.get("MPITREE_OWN_FP_PREFIX", "1") != "0")
+        x_lo, x_hi = feature_blocks(F, P)[int(comm.rank)] if fpx else (0, F)
         # data-parallel with >= P features: built histograms reduced per feature
         # block to the block's owner (reduce-scatter by feature), scans per block
         dprs = dp and F_h < F
@@ -541,7 +550,7 @@ class DeviceGrower:
                     slab=torch.empty((IMAX, hip.hist_slab_words(F_h, B, C, reg)), dtype=hdt,
                                      device=dev),
                     rec=torch.empty((KMAX, R), **i64),
-                    grec=torch.empty((P * KMAX * R) if (fp or dprs) else 1, **i64),
+                    grec=torch.empty((P * KMAX * R) if (fp or dprs or fpx) else 1, **i64),
                     # the other ranks' feature blocks of this rank's built histograms
                     rs=[torch.empty((KMAX, hi - lo, B, C), dtype=hdt, device=dev)
                         if r != int(comm.rank) else None
@@ -571,8 +580,8 @@ class DeviceGrower:
                                         device=dev),
                 )
 
-            ws = self._workspace((str(dev), n, n_loc, F, f_lo, F_h, B, C, reg, fr, dp, own, fsel),
-                                 make)
+            ws = self._workspace((str(dev), n, n_loc, F, f_lo, F_h, B, C, reg, fr, dp, own, fsel,
+                                  fpx), make)
             sets, hists, slab, rec = ws["sets"], ws["hists"], ws["slab"], ws["rec"]
             cost, bins, ident, split = ws["cost"], ws["bins"], ws["ident"], ws["split"]
             pitems, cursors, jobs, job_count = (ws["pitems"], ws["cursors"], ws["jobs"],
@@ -622,7 +631,7 @@ class DeviceGrower:
                                 node_owner=ws["own_node"].data_ptr(),
                                 job_owner=ws["own_job"].data_ptr(),
                                 jobs_at_switch=own_jobs_at_switch(be),
-                                segs=ws["own_segs"].data_ptr())
+                                segs=ws["own_segs"].data_ptr(), build_all=int(fpx))
 
             plan_cu = hb.N_CU * HIST_ITEMS_PER_CU // 2  # (the planner makes 2 items per "CU")
             # single-rank and subtree-ownership levels (no collective between the
@@ -656,12 +665,15 @@ class DeviceGrower:
                               fr, 0 if fixup else hctl_dev + (lvl % 64) * 64,
                               tag0 + (lvl % 4096) + 1, dp=int(dp), fixup=fixup, own=own_args)
 
+            fpx_on = fpx  # (until the switch: feature-parallel levels)
+            # a level can switch only once it has min_units units (<= 2^level)
+            x_first = max(0, int(np.ceil(np.log2(max(1, own_min_units(P)))))) if fpx else 0
             while True:
                 if P > 1:  # failure containment: a failed peer / injected fault
                     check_abort()
                     fault_point(comm, f"level:{lvl}")
                 b0 = getattr(comm, "bytes_communicated", 0)
-                if ctx is not None:
+                if ctx is not None and not fpx_on:
                     ctx.level(s(), lvl)
                     if ck is not None and (lvl - first_lvl + 1) % ck_every == 0:
                         self._ckpt_save(lvl, ws, sets, hists, rank, P)
@@ -673,6 +685,8 @@ class DeviceGrower:
                             break
                     if lvl > 4096:
                         raise RuntimeError("device level loop did not terminate")
+                    if REC_DUMP is not None:  # (tools: per-level split records)
+                        REC_DUMP.append(rec[: int(min(2 ** min(lvl - 1, 40), KMAX))].clone())
                     continue
                 if prof:
                     marks.append([])
@@ -680,6 +694,10 @@ class DeviceGrower:
                 cur, nxt = ptrs[lvl % 2], ptrs[(lvl + 1) % 2]
                 nxt_t = sets[(lvl + 1) % 2]
                 H, Hp = hists[lvl % 2], hists[(lvl + 1) % 2]
+                l_lo, l_F = (x_lo, x_hi - x_lo) if fpx_on else (f_lo, F_h)
+                if fpx_on:  # this rank's feature block, node-major
+                    H = H.view(-1)[: KMAX * l_F * B * C].view(KMAX, l_F, B, C)
+                    Hp = Hp.view(-1)[: KMAX * l_F * B * C].view(KMAX, l_F, B, C)
                 kb = int(min(2 ** min(lvl, 40), KMAX))
                 ib = int(min(IMAX, kb + n_loc // 1024 + 2 * hb.N_CU + 1))
                 ctl = cur["ctl"]
@@ -722,7 +740,7 @@ class DeviceGrower:
                         if w is not None:
                             w.wait()
                 else:
-                    build(H, f_lo, F_h)
+                    build(H, l_lo, l_F)
                     if dp:  # sum the built slots' histograms over the row shards
                         comm.all_reduce_device(H[:nbb])
                 mark()
@@ -730,14 +748,14 @@ class DeviceGrower:
                 # (parent - built sibling, written back for select / next level)
                 fuse = lvl > 0 and not reg
                 if lvl > 0 and reg:
-                    hip.hist_derive(s(), cur["der"], kb, Hp.data_ptr(), H.data_ptr(), E, reg,
-                                    dcount=ctl + 4 * 4)
-                hip.scan(s(), H.data_ptr(), ident.data_ptr(), kb, be.nbins.data_ptr(), F_h, f_lo,
+                    hip.hist_derive(s(), cur["der"], kb, Hp.data_ptr(), H.data_ptr(),
+                                    l_F * B * C, reg, dcount=ctl + 4 * 4)
+                hip.scan(s(), H.data_ptr(), ident.data_ptr(), kb, be.nbins.data_ptr(), l_F, l_lo,
                          B, C, int(be.crit), msl, cost.data_ptr(), bins.data_ptr(),
                          rec.data_ptr(), be.xtab.data_ptr(), hb.XTAB_N, dcount=ctl,
                          der=cur["der"] if fuse else 0, prev=Hp.data_ptr() if fuse else 0,
                          nbuilt=ctl + 4 * 1 if fuse else 0)
-                if fp or dprs:  # every rank's best split of each node -> the global best
+                if fp or dprs or fpx_on:  # every rank's best split of each node -> the global best
                     g = ws["grec"][: P * kb * R]
                     comm.all_gather_device(g, rec[:kb].reshape(-1))
                     hip.fp_combine(s(), g.data_ptr(), P, kb, R, ctl, rec.data_ptr())
@@ -768,6 +786,18 @@ class DeviceGrower:
                 # lagged completion check: the planner stored the next level's
                 # frontier size + job count into host slot lvl % 64
                 lvl += 1
+                if fpx_on and lvl - 1 >= x_first:
+                    # the next level's kernels depend on whether this one switched:
+                    # wait for its planner (levels that cannot switch keep the lag)
+                    L = lvl - 1
+                    _wait_slot(hctl, L % 64, tag0 + (L % 4096) + 1)
+                    self.stats["fp_prefix_levels"] = L + 1
+                    if int(hctl[L % 64, 0]) == 0:
+                        done_at = L
+                        break
+                    if int(hctl[L % 64, 3]):  # switched: own levels (all features) follow
+                        fpx_on = False
+                    continue
                 if lvl - 2 >= first_lvl:
                     _wait_slot(hctl, (lvl - 2) % 64, tag0 + ((lvl - 2) % 4096) + 1)
                     if int(hctl[(lvl - 2) % 64, 0]) == 0:

@@ -145,6 +145,7 @@ def _fit_rank_gpu_large(rank, world, regression, strategy="auto"):
         outs[f"xbytes{it}"] = np.array([est.fit_stats_.get("comm_bytes_exchange", 0)])
         outs[f"own_rows{it}"] = np.array([est.fit_stats_.get("own_rows", -1)])
         outs[f"asm{it}"] = np.array([est.fit_stats_.get("assembly", "")])
+        outs[f"fpx{it}"] = np.array([est.fit_stats_.get("fp_prefix_levels", 0)])
     return outs
 
 
@@ -176,8 +177,13 @@ def test_gpu_ranks_equal_single_gpu_at_scale(regression, strategy, world):
         for it in range(2):
             assert str(o[f"engine{it}"][0]) == "hip-device-loop"
             assert str(o[f"mode{it}"][0]) == want
-            if want == "subtree-owned":  # no per-level collective, one node exchange
-                assert o[f"bytes{it}"].sum() == 0 and o[f"xbytes{it}"][0] > 0
+            if want == "subtree-owned":
+                # feature-parallel levels until the switch (one record all-gather
+                # each), then none; one segment-count exchange at the end
+                nfp = int(o[f"fpx{it}"][0])
+                b = o[f"bytes{it}"]
+                assert nfp > 0 and b.size == nfp and (b > 0).all(), (nfp, b)
+                assert o[f"xbytes{it}"][0] > 0
                 assert o[f"own_rows{it}"][0] > 0  # every rank owns units
                 # ranks of one node: each wrote its own nodes into the shared tree
                 # (the first fit's tree is still held: the repeat takes another slot)

@@ -1,0 +1,84 @@
+"""The node-local shared-host tree pool (parallel/shared_tree.py): every rank
+makes the same slot choice from the gathered free masks, a slot a rank still
+views is never reused, and ranks of one machine see each other's writes after
+the flag barrier. Host memory stands in for the HIP registration (no GPU)."""
+import multiprocessing as mp
+
+import numpy as np
+import pytest
+
+from mpitree_amd.parallel import shared_tree as st
+
+
+class _FakeHip:
+    def host_register(self, p, n):
+        return p  # (the device pointer of a mapped host range)
+
+    def host_unregister(self, p):
+        pass
+
+
+class _Comm:
+    def __init__(self, rank, P):
+        self.rank, self.world_size = rank, P
+
+
+def _pool(rank=0, P=2, uid=None):
+    return st.ShmTreePool(_Comm(rank, P), _FakeHip(), uid if uid is not None else 0x5EED + rank)
+
+
+def test_choose_reuses_only_slots_free_everywhere():
+    pool = _pool()
+    a = pool.choose([0, 0], 1000)  # nothing exists: a new slot
+    assert a.nbytes - st.HEADER >= 1000 and pool.free_mask() == 1
+    view = a.nd[st.HEADER : st.HEADER + 64]  # a tree this rank still holds
+    assert pool.free_mask() == 0
+    b = pool.choose([pool.free_mask(), 1], 1000)  # busy here: another slot
+    assert b is not a
+    del view
+    assert pool.free_mask() == 3
+    # the peer still holds slot 0: slot 1 is the only one free everywhere
+    assert pool.choose([3, 2], 1000) is b
+    # too small everywhere: a new, larger slot
+    c = pool.choose([3, 3], 10 << 20)
+    assert c is not a and c is not b and c.nbytes - st.HEADER >= 10 << 20
+    for sl in list(pool.slots.values()):
+        sl.close()
+
+
+def test_next_slot_is_agreed_ahead_and_excludes_the_current():
+    pool = _pool()
+    cur = pool.choose([0, 0], 4096)
+    pool.plan_next([pool.free_mask(), pool.free_mask()], cur, 4096)
+    nxt = pool.take_next()
+    assert nxt is not None and nxt is not cur and pool.take_next() is None
+    for sl in list(pool.slots.values()):
+        sl.close()
+
+
+def _rank_main(rank, uid, q):
+    pool = st.ShmTreePool(_Comm(rank, 2), _FakeHip(), uid)
+    slot = pool.choose([0, 0], 1 << 16)  # same name on both ranks
+    data = slot.nd[st.HEADER : st.HEADER + (1 << 16)].view(np.int64)
+    half = data.size // 2
+    data[rank * half : (rank + 1) * half] = rank + 1  # this rank's nodes
+    pool.barrier(slot)
+    q.put((rank, int(data[:half].sum()), int(data[half:].sum()), half))
+    del data
+    slot.close()
+
+
+@pytest.mark.timeout(60)
+def test_two_ranks_share_one_buffer_through_the_barrier():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    uid = int.from_bytes(np.random.default_rng().bytes(5), "little")
+    ps = [ctx.Process(target=_rank_main, args=(r, uid, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = sorted(q.get(timeout=50) for _ in range(2))
+    for p in ps:
+        p.join(20)
+        assert p.exitcode == 0
+    for rank, s0, s1, half in got:
+        assert s0 == half and s1 == 2 * half  # both ranks' halves, seen by each
