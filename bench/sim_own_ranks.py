@@ -184,9 +184,13 @@ def main():
     ap.add_argument("--only-rank", type=int, default=None,
                     help="simulate this rank only (profiling one rank's kernel sequence)")
     ap.add_argument("--regression", action="store_true")
+    ap.add_argument("--fp-prefix", default=None, choices=["0", "1"],
+                    help="force the feature-parallel prefix levels off / on")
     ap.add_argument("--no-shared", action="store_true",
                     help="node exchange + full-tree copy instead of the shared-host assembly")
     a = ap.parse_args()
+    if a.fp_prefix is not None:
+        os.environ["MPITREE_OWN_FP_PREFIX"] = a.fp_prefix
     if a.units_per_rank is not None:
         os.environ["MPITREE_OWN_UNITS_PER_RANK"] = str(a.units_per_rank)
     from mpitree_amd.core.fit import fit_tree

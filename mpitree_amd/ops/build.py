@@ -31,7 +31,7 @@ ARCH = os.environ.get("MPITREE_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["hist.hip", "split_scan.hip", "partition.hip", "predict.hip", "misc.hip",
                "finish.hip", "finish_reg.hip", "assemble.hip", "binning.hip", "grow.hip",
-               "exact2.hip", "exact_setup.hip", "small_fit.hip", "bindings.cpp",
+               "exact2.hip", "exact_setup.hip", "small_fit.hip", "dp_route.hip", "bindings.cpp",
                "exact2_bind.cpp", "grow_bind.cpp"]
 CPU_SOURCES = ["cpu_builder.cpp"]
 HEADERS = ["common.h", "criterion.h", "cpu_builder_core.h", "grow.h", "tiny_sort.h", "exact2.h"]

@@ -93,6 +93,13 @@ void launch_small_fit(hipStream_t, const void*, int, int64_t, int, int, const in
 void launch_asm_emit(hipStream_t, const int32_t*, const void*, bool, int64_t, int,
                      const int32_t*, const double*, int, const int64_t*, uint8_t*, bool, int, int,
                      const double*, int, const double*, const int64_t*, int, int, bool, int64_t);
+void launch_dp_plan(hipStream_t, const int64_t*, int, int, int, const int64_t*, int, int,
+                    int64_t*, int64_t*, int64_t*, int64_t*);
+void launch_dp_gather(hipStream_t, const int64_t*, int, int, int, const uint32_t*,
+                      const uint32_t*, uint32_t, const uint8_t*, int64_t, const void*, bool,
+                      const int64_t*, uint8_t*, void*);
+void launch_dp_place(hipStream_t, const int64_t*, int64_t, const uint8_t*, const void*, bool,
+                     int64_t, uint8_t*, void*);
 void launch_targets(hipStream_t, const void*, bool, int64_t, int64_t*, int64_t*);
 void launch_shm_seg_count(hipStream_t, const int64_t*, int, int, const int32_t*, int64_t,
                           const int64_t*, int64_t*);
@@ -354,6 +361,12 @@ PYBIND11_MODULE(_hip, m) {
     return reinterpret_cast<uintptr_t>(d);
   });
   m.def("host_free", [](uintptr_t p) { MT_HIP_CHECK(hipHostFree(reinterpret_cast<void*>(p))); });
+  // stream-ordered device -> pinned host copy (DMA)
+  m.def("copy_d2h", [](uintptr_t s, uintptr_t dst, uintptr_t src, size_t nbytes) {
+    if (nbytes)
+      MT_HIP_CHECK(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src),
+                                  nbytes, hipMemcpyDeviceToHost, S(s)));
+  });
   m.def("edges_sample_rows", &mt::edges_sample_rows);
   m.def(
       "edges",
@@ -401,6 +414,26 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("emit_prefix") = true, py::arg("cap_nodes") = 0);
   m.def("targets", [](uintptr_t s, uintptr_t y, bool y64, int64_t n, uintptr_t st, uintptr_t out) {
     mt::launch_targets(S(s), P<void>(y), y64, n, P<int64_t>(st), P<int64_t>(out));
+  });
+  // data-parallel subtree finishing (ops/device_grower.py _dp_finish)
+  m.def("dp_plan", [](uintptr_t s, uintptr_t jobs, int J, int W, int C, uintptr_t allc, int P_,
+                      int me, uintptr_t soff, uintptr_t hdr, uintptr_t jobs2, uintptr_t seg) {
+    mt::launch_dp_plan(S(s), P<int64_t>(jobs), J, W, C, P<int64_t>(allc), P_, me,
+                       P<int64_t>(soff), P<int64_t>(hdr), P<int64_t>(jobs2), P<int64_t>(seg));
+  });
+  m.def("dp_gather", [](uintptr_t s, uintptr_t jobs, int J, int W, int C, uintptr_t idx,
+                        uintptr_t tmp, uint32_t row_mask, uintptr_t codes_rm, int64_t row_bytes,
+                        uintptr_t y, bool y64, uintptr_t soff, uintptr_t out_codes,
+                        uintptr_t out_y) {
+    mt::launch_dp_gather(S(s), P<int64_t>(jobs), J, W, C, P<uint32_t>(idx), P<uint32_t>(tmp),
+                         row_mask, P<uint8_t>(codes_rm), row_bytes, P<void>(y), y64,
+                         P<int64_t>(soff), P<uint8_t>(out_codes), P<void>(out_y));
+  });
+  m.def("dp_place", [](uintptr_t s, uintptr_t seg, int64_t nseg, uintptr_t in_codes,
+                       uintptr_t in_y, bool y64, int64_t row_bytes, uintptr_t out_codes,
+                       uintptr_t out_y) {
+    mt::launch_dp_place(S(s), P<int64_t>(seg), nseg, P<uint8_t>(in_codes), P<void>(in_y), y64,
+                        row_bytes, P<uint8_t>(out_codes), P<void>(out_y));
   });
   // node-local shared-host assembly (parallel/shared_tree.py)
   m.def("shm_seg_count", [](uintptr_t s, uintptr_t segs, int S_, int me, uintptr_t rank,

@@ -509,13 +509,34 @@ __device__ void plan_fused_select(const PlanArgs& a, int K) {
   __syncthreads();  // (records read by other threads below, e.g. the ownership pass)
 }
 
+// MT_PLAN_PROF (variant builds, bench/plan_prof.py): per-phase wall-clock ticks
+// (100 MHz) summed over launches, read back with mt_plan_prof_read
+#ifdef MT_PLAN_PROF
+__device__ unsigned long long g_plan_prof[32];
+#define PLAN_MARK(k)                                                   \
+  do {                                                                 \
+    if (threadIdx.x == 0) {                                            \
+      const unsigned long long t_ = wall_clock64();                    \
+      atomicAdd(&g_plan_prof[k], t_ - plan_t_prev_);                   \
+      plan_t_prev_ = t_;                                               \
+    }                                                                  \
+  } while (0)
+#else
+#define PLAN_MARK(k)
+#endif
+
 __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
   __shared__ PlanShared sh;
   const int tid = threadIdx.x;
+#ifdef MT_PLAN_PROF
+  unsigned long long plan_t_prev_ = wall_clock64();
+  if (tid == 0) atomicAdd(&g_plan_prof[31], 1ull);
+#endif
   const int C = a.C;
   const int JW = plan_job_width(a);
   const int K = a.cur.ctl[0];
   if (a.sel_left) plan_fused_select(a, K);
+  PLAN_MARK(0);
   // ---- pass 0 (subtree ownership, before the switch): maybe switch this level
   __shared__ OwnShared own_sh;
   bool own_sw = false;
@@ -547,6 +568,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     }
     return d;
   };
+  PLAN_MARK(1);
   // ---- pass 1: totals (built / derived next-frontier children, split nodes);
   // a frontier of at most kPlanThreads nodes takes its total from pass 2's scan
   // (one decision per node instead of two)
@@ -571,6 +593,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     if (a.dp) a.nxt.ctl[10] = atomicAdd(a.job_count, 0);  // jobs before this level (dp fixup)
   }
   __syncthreads();
+  PLAN_MARK(2);
   // ---- pass 2: write decided nodes, jobs, split list, next frontier, derive list
   for (int b0 = 0; b0 < K; b0 += kPlanThreads) {
     const int i = b0 + tid;
@@ -709,8 +732,10 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
   const int K2 = NB + ND;
   __threadfence_block();  // nxt.start / cnt written above are read by other threads below
   __syncthreads();
+  PLAN_MARK(3);
   // ---- pass 3: histogram items of the next level's built slots (dp: after the partition)
   if (!a.dp) plan_hist_items(a, sh, NB);
+  PLAN_MARK(4);
   // ---- pass 4: partition items of this level's split nodes (kPartChunk rows each)
   __syncthreads();
   if (tid == 0) sh.carry[3] = 0;
@@ -741,6 +766,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
     __syncthreads();
   }
   const int n_pitems = sh.carry[3];
+  PLAN_MARK(5);
   // ---- pass 5 (regression): min/max work items over every next-frontier slot
   if (a.reg && !a.dp) plan_minmax_items(a, sh, K2);
   if (tid == 0) {
@@ -771,7 +797,17 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
       __hip_atomic_store(a.host_ctl + 2, a.host_tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
+  PLAN_MARK(6);
 }
+
+#ifdef MT_PLAN_PROF
+extern "C" void mt_plan_prof_read(unsigned long long* out) {
+  MT_HIP_CHECK(hipDeviceSynchronize());
+  MT_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_plan_prof), sizeof(g_plan_prof)));
+  const unsigned long long z[32] = {};
+  MT_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_plan_prof), z, sizeof(z)));
+}
+#endif
 
 // Data-parallel levels: after this rank's partition, every next-frontier slot
 // and every job appended this level learns its local row segment from its

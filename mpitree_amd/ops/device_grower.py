@@ -92,6 +92,22 @@ POLL_TIMEOUT_S = float(os.environ.get("MPITREE_POLL_TIMEOUT", "120"))
 HIST_ITEMS_PER_CU = max(1, min(2, int(os.environ.get("MPITREE_HIST_ITEMS", "2"))))
 
 
+def fp_prefix_pays(n: int, F: int, P: int, reg: bool) -> bool:
+    """Whether the replicated levels before the ownership switch run
+    feature-parallel (``MPITREE_OWN_FP_PREFIX`` = 1 / 0 forces it). A rank then
+    histograms 1 / P of the features -- saving (1 - 1/P) of a level's histogram
+    build, ~0.6 ps (classification) / ~3 ps (regression: int64 slabs) per
+    row x feature at the top levels (profiles/r5/) -- but each level adds a
+    record all-gather, a select and a combine (~40 us with RCCL latency). The
+    1M x 64 classification tree breaks even at P = 8; its regression tree and
+    10M-row fits gain."""
+    env = os.environ.get("MPITREE_OWN_FP_PREFIX")
+    if env is not None:
+        return env != "0"
+    per = 3.1e-12 if reg else 0.625e-12  # (s per row x feature of one level)
+    return (1.0 - 1.0 / max(P, 1)) * n * F * per > 40e-6
+
+
 def own_jobs_at_switch(be) -> int:
     """``MPITREE_OWN_JOBS=1``: at the ownership switch the owned children that would
     keep growing become finisher jobs (up to the finisher's row limit), so a rank
@@ -317,74 +333,66 @@ class DeviceGrower:
 
     def _dp_finish(self, d_jobs, W: int):
         """Data-parallel subtree finishing: each job's rows are spread over the
-        ranks; every rank sends its share of job j to owner(j) (one all_to_all of
-        row-major codes + targets), the owner lays its jobs' rows out
-        contiguously and runs the finisher on them (into the shared position
-        space). Jobs: int64 [J][W] = {local start, rows, depth, pos, buffer,
-        stats[C], local rows, src}."""
+        ranks; every rank sends its share of job j to owner(j) (serpentine over
+        the largest-first order; one all_to_all of row-major codes + targets),
+        the owner lays its jobs' rows out contiguously and runs the finisher on
+        them (into the shared position space). The routing -- owners, send
+        offsets, per-rank counts, the owned jobs' layout -- runs on the device
+        (``dp_route.hip``); the one host wait reads the all_to_all split sizes.
+        Jobs: int64 [J][W] = {local start, rows, depth, pos, buffer, stats[C],
+        local rows, src}."""
         be, comm, p = self.be, self.comm, self.p
+        hip = be.hip
         dev = be.device
+        s = hb._stream
         P, r = comm.world_size, comm.rank
         C = be.C
         J = int(d_jobs.shape[0])
-        owner = self._owners(J, P, dev)
-        lstart, lcnt = d_jobs[:, 0], d_jobs[:, 5 + C]
+        d_jobs = d_jobs.contiguous()
+        i64 = dict(dtype=torch.int64, device=dev)
         # every rank's local rows per job: [P, J]
-        allc = torch.empty(P * J, dtype=torch.int64, device=dev)
-        comm.all_gather_device(allc, lcnt.contiguous())
-        allc = allc.view(P, J)
-        # this rank's rows, grouped by destination (job order within a destination)
-        order = torch.argsort(owner, stable=True)
-        cnt_o = lcnt[order]
-        seg_id = torch.repeat_interleave(torch.arange(J, device=dev), cnt_o)
-        seg_first = torch.cumsum(cnt_o, 0) - cnt_o
-        pos_in = torch.arange(seg_id.numel(), device=dev) - seg_first[seg_id]
-        jsel = order[seg_id]
-        ent_i = be.idx[lstart[jsel] + pos_in]
-        ent_t = be.tmp[lstart[jsel] + pos_in]
-        ent = torch.where(d_jobs[jsel, 4] == 0, ent_i, ent_t)
-        rows = (ent.long() & be.row_mask)
-        send_counts = torch.zeros(P, dtype=torch.int64, device=dev).index_add_(0, owner, lcnt)
-        recv_counts = allc[:, owner == r].sum(1)  # from each source rank
-        sc = send_counts.cpu().tolist()  # one host sync per fit (the all_to_all needs the splits)
-        rc = recv_counts.cpu().tolist()
-        R_tot = int(sum(rc))
-        codes_s = be.codes_rm.index_select(0, rows)
-        y_s = be.y.index_select(0, rows)
-        codes_r = torch.empty((R_tot,) + tuple(be.codes_rm.shape[1:]), dtype=be.codes_rm.dtype,
-                              device=dev)
-        y_r = torch.empty(R_tot, dtype=be.y.dtype, device=dev)
-        comm.all_to_all_device(codes_r, codes_s, rc, sc)
-        comm.all_to_all_device(y_r, y_s, rc, sc)
-        self.stats["dp_rows_exchanged"] = int(sum(sc))
-        mine = torch.nonzero(owner == r).squeeze(1)  # owned jobs, in job order
-        Jm = int(mine.numel())
+        allc = torch.empty(P * J, **i64)
+        comm.all_gather_device(allc, d_jobs[:, 5 + C].contiguous())
+        soff = torch.empty(J, **i64)
+        hdr = torch.empty(4 + 2 * P, **i64)
+        jobs2 = torch.empty((J // P + 2, 5 + C), **i64)  # (owned: ceil(J / P))
+        seg = torch.empty((P * (J // P + 2), 3), **i64)
+        hip.dp_plan(s(), d_jobs.data_ptr(), J, W, C, allc.data_ptr(), P, r, soff.data_ptr(),
+                    hdr.data_ptr(), jobs2.data_ptr(), seg.data_ptr())
+        rb = int(be.row_elems * be.cb)
+        n_send = int(be.n)  # (every local row belongs to at most one job)
+        codes_s = hb._workspace(dev, "dp.send", n_send * rb)
+        ysz = be.y.element_size()
+        y_s = hb._workspace(dev, "dp.send_y", n_send * ysz).view(be.y.dtype)
+        y64 = be.y.dtype == torch.int64
+        hip.dp_gather(s(), d_jobs.data_ptr(), J, W, C, be.idx.data_ptr(), be.tmp.data_ptr(),
+                      int(be.row_mask), be.codes_rm.data_ptr(), rb, be.y.data_ptr(), y64,
+                      soff.data_ptr(), codes_s.data_ptr(), y_s.data_ptr())
+        h = hb._pinned_copy(hdr, "dp.hdr")
+        torch.cuda.current_stream(dev).synchronize()  # (the split sizes, for the host)
+        Jm, R_tot = int(h[0]), int(h[1])
+        sc = [int(v) for v in h[4 : 4 + P]]
+        rc = [int(v) for v in h[4 + P : 4 + 2 * P]]
+        n_out = sum(sc)
+        codes_r = torch.empty(max(R_tot, 1) * rb, dtype=torch.uint8, device=dev)
+        y_r = torch.empty(max(R_tot, 1), dtype=be.y.dtype, device=dev)
+        comm.all_to_all_device(codes_r[: R_tot * rb], codes_s[: n_out * rb],
+                               [v * rb for v in rc], [v * rb for v in sc])
+        comm.all_to_all_device(y_r[:R_tot], y_s[:n_out], rc, sc)
+        self.stats["dp_rows_exchanged"] = n_out
         if Jm == 0:
             return
-        cm = allc[:, mine]                       # [P, Jm] rows of each owned job per source
-        gcount = cm.sum(0)                       # == d_jobs[mine, 1]
-        new_start = torch.cumsum(gcount, 0) - gcount
-        # segment (s, j): source block offset + prefix within the block -> new position
-        blk = torch.cumsum(recv_counts, 0) - recv_counts
-        within = torch.cumsum(cm, 1) - cm        # offset of job j inside source s's block
-        dst_off = new_start[None, :] + (torch.cumsum(cm, 0) - cm)
-        src_off = blk[:, None] + within
-        flat = cm.reshape(-1)
-        sid = torch.repeat_interleave(torch.arange(flat.numel(), device=dev), flat)
-        first = torch.cumsum(flat, 0) - flat
-        k = torch.arange(sid.numel(), device=dev) - first[sid]
-        perm = torch.empty(R_tot, dtype=torch.int64, device=dev)
-        perm[dst_off.reshape(-1)[sid] + k] = src_off.reshape(-1)[sid] + k
-        codes_rm = codes_r.index_select(0, perm)
-        y_loc = y_r.index_select(0, perm).contiguous()
-        codes_fm = codes_rm[:, : be.F].t().contiguous()
-        be2 = hb.HipBackend(dev)
-        be2.setup(codes_rm, codes_fm, y_loc, be.nbins, n_bins=be.B, n_classes=C,
-                  criterion=be.crit)
-        jobs2 = torch.cat([new_start[:, None], d_jobs[mine, 1:5], d_jobs[mine, 5:5 + C]], 1)
-        jobs2[:, 4] = 0  # rows in be2.idx
-        be2.launch_finisher(jobs2.contiguous(), Jm, R_tot, p, be.pos_rec, be.pos_st)
-        self._dp_keep = (be2, codes_r, y_r, jobs2)
+        codes2 = torch.empty((R_tot, be.row_elems), dtype=be.codes_rm.dtype, device=dev)
+        y2 = torch.empty(R_tot, dtype=be.y.dtype, device=dev)
+        hip.dp_place(s(), seg.data_ptr(), P * Jm, codes_r.data_ptr(), y_r.data_ptr(), y64, rb,
+                     codes2.data_ptr(), y2.data_ptr())
+        codes_fm = codes2[:, : be.F].t().contiguous()
+        be2 = getattr(self, "_dp_be", None)
+        if be2 is None or be2.device != dev:
+            be2 = self._dp_be = hb.HipBackend(dev)
+        be2.setup(codes2, codes_fm, y2, be.nbins, n_bins=be.B, n_classes=C, criterion=be.crit)
+        be2.launch_finisher(jobs2[:Jm], Jm, R_tot, p, be.pos_rec, be.pos_st)
+        self._dp_keep = (codes_r, y_r, codes2, y2, codes_fm, jobs2, seg)
 
     def _exchange_nodes(self):
         """Every rank ends with every finished node: compact the positions this
@@ -485,8 +493,7 @@ class DeviceGrower:
         # feature-parallel -- each rank histograms and scans its feature block
         # only, one all-gather of the split records per level (fp_combine), and
         # the switch level builds every child of the first owned level from rows
-        fpx = (own and F >= P and self.ckpt is None
-               and os.environ.get("MPITREE_OWN_FP_PREFIX", "1") != "0")
+        fpx = own and F >= P and self.ckpt is None and fp_prefix_pays(int(n), F, P, reg)
         x_lo, x_hi = feature_blocks(F, P)[int(comm.rank)] if fpx else (0, F)
         # data-parallel with >= P features: built histograms reduced per feature
         # block to the block's owner (reduce-scatter by feature), scans per block

@@ -359,6 +359,10 @@ def _pinned_copy(t: torch.Tensor, key: str) -> np.ndarray:
 
 
 _ZC_POOL: list = []  # [ndarray, device pointer, host pointer] of mapped host buffers
+_ZC_COHERENT = os.environ.get("MPITREE_ZC_COHERENT", "0") == "1"
+# single-process assembly: emit straight into host memory (1) or into device memory
+# plus one DMA (0); the shared-host assembly of several ranks always stores directly
+_ZC_EMIT = os.environ.get("MPITREE_ZC_EMIT", "0") == "1"
 
 
 def _zc_out(nbytes: int):
@@ -390,7 +394,7 @@ def _zc_out(nbytes: int):
             hptr = _ZC_POOL.pop(drop[0])[2]
             hip.host_free(hptr)
     size = max(int(nbytes * 1.25), 1 << 16)
-    hptr = int(hip.host_alloc(size, coherent=False))
+    hptr = int(hip.host_alloc(size, coherent=_ZC_COHERENT))
     nd = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(hptr))
     ent = [nd, int(hip.host_device_ptr(hptr)), hptr]
     _ZC_POOL.append(ent)
@@ -659,17 +663,29 @@ class HipBackend:
         # the same data: the same count) is written in the same pass; a larger
         # tree (the kernel writes nothing past the buffer) is emitted again
         key = (str(self.device), P, C, bool(self.reg))
-        nd, dptr = _zc_out(max(_ASM_HINT.get(key, 0), 1) * bpn)
-        emit(dptr, nd.size // bpn)
+        guess = min(max(_ASM_HINT.get(key, 0), 1), P) * bpn
+        nd, dptr = _zc_out(guess)
+        if _ZC_EMIT:  # the emit kernel stores into the host buffer (PCIe writes)
+            emit(dptr, nd.size // bpn)
+        else:  # the emit writes device memory, one DMA copies the guessed bytes
+            dbuf = _workspace(self.device, "asm.out", P * bpn)
+            emit(dbuf.data_ptr(), 0)
+            hip.copy_d2h(s, int(nd.ctypes.data), dbuf.data_ptr(), guess)
         h_total = _pinned_copy(total, "asm.total")
         torch.cuda.current_stream(self.device).synchronize()
         self._check_finisher_watch()
         N, max_depth = int(h_total[0]), int(h_total[1])
         _ASM_HINT[key] = N
         nbytes = N * bpn
-        if nbytes > nd.size:
+        if _ZC_EMIT and nbytes > nd.size:
             nd, dptr = _zc_out(nbytes)
             emit(dptr, nd.size // bpn)
+            torch.cuda.current_stream(self.device).synchronize()
+        elif not _ZC_EMIT and nbytes > guess:  # (a larger tree than the guess)
+            if nbytes > nd.size:
+                nd, dptr = _zc_out(nbytes)
+                guess = 0
+            hip.copy_d2h(s, int(nd.ctypes.data) + guess, dbuf.data_ptr() + guess, nbytes - guess)
             torch.cuda.current_stream(self.device).synchronize()
         self.pos_rec = self.pos_st = None
         return TreeArrays.from_packed(nd[:nbytes], N, C, bool(self.reg), max_depth=max_depth)

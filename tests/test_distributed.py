@@ -1,6 +1,8 @@
 """Distributed strategies on CPU ranks (gloo): every rank returns the same
 tree, and it is identical to the single-process tree."""
 
+import os
+
 import numpy as np
 import pytest
 
@@ -126,6 +128,9 @@ def _fit_rank_gpu_large(rank, world, regression, strategy="auto"):
     from mpitree_amd.utils.datasets import make_classification, make_regression
 
     dev = torch.device("cuda", 0)
+    # "subtree": the replicated prefix levels forced feature-parallel (the
+    # heuristic keeps these small shapes replicated, as "auto" shows)
+    os.environ["MPITREE_OWN_FP_PREFIX"] = "1" if strategy == "subtree" else "0"
     if regression:
         X, y = make_regression(200_000, 16, levels=64, seed=5, device=dev)
         cls = ParallelDecisionTreeRegressor
@@ -178,11 +183,15 @@ def test_gpu_ranks_equal_single_gpu_at_scale(regression, strategy, world):
             assert str(o[f"engine{it}"][0]) == "hip-device-loop"
             assert str(o[f"mode{it}"][0]) == want
             if want == "subtree-owned":
-                # feature-parallel levels until the switch (one record all-gather
-                # each), then none; one segment-count exchange at the end
+                # "subtree": feature-parallel levels until the switch (one record
+                # all-gather each), then none; "auto": no per-level collective.
+                # One segment-count exchange at the end.
                 nfp = int(o[f"fpx{it}"][0])
                 b = o[f"bytes{it}"]
-                assert nfp > 0 and b.size == nfp and (b > 0).all(), (nfp, b)
+                if strategy == "subtree":
+                    assert nfp > 0 and b.size == nfp and (b > 0).all(), (nfp, b)
+                else:
+                    assert nfp == 0 and b.sum() == 0, (nfp, b)
                 assert o[f"xbytes{it}"][0] > 0
                 assert o[f"own_rows{it}"][0] > 0  # every rank owns units
                 # ranks of one node: each wrote its own nodes into the shared tree
