@@ -71,6 +71,10 @@ from ..parallel.strategies import feature_blocks
 __all__ = ["DeviceGrower", "device_loop_supported"]
 
 REC_DUMP = None  # list: the single-rank level loop appends each level's split records
+# dict (per-rank simulations, bench/sim_dp_ranks.py): the single-rank level loop
+# adds "hists" (each level's slot histograms) and "jobs" / "idx" / "tmp" / "row_mask"
+# (the sorted finisher jobs and the row buffers they index)
+DUMP = None
 
 _WORKSPACES: dict = {}  # (device, n, F, B, C, reg, fr) -> level-loop buffers
 _HOST_CTL: dict = {}  # device index -> (device pointer, numpy view [64, 16] int32)
@@ -350,6 +354,9 @@ class DeviceGrower:
         J = int(d_jobs.shape[0])
         d_jobs = d_jobs.contiguous()
         i64 = dict(dtype=torch.int64, device=dev)
+        note = getattr(comm, "note_phase", None)  # (tracing / simulated communicators)
+        if note is not None:
+            note("dp_finish")
         # every rank's local rows per job: [P, J]
         allc = torch.empty(P * J, **i64)
         comm.all_gather_device(allc, d_jobs[:, 5 + C].contiguous())
@@ -682,6 +689,11 @@ class DeviceGrower:
                 b0 = getattr(comm, "bytes_communicated", 0)
                 if ctx is not None and not fpx_on:
                     ctx.level(s(), lvl)
+                    if REC_DUMP is not None:  # (tools: per-level split records)
+                        REC_DUMP.append(rec[: int(min(2 ** min(lvl, 40), KMAX))].clone())
+                    if DUMP is not None:
+                        kbd = int(min(2 ** min(lvl, 40), KMAX))
+                        DUMP.setdefault("hists", []).append(hists[lvl % 2][:kbd].clone())
                     if ck is not None and (lvl - first_lvl + 1) % ck_every == 0:
                         self._ckpt_save(lvl, ws, sets, hists, rank, P)
                     lvl += 1
@@ -692,8 +704,6 @@ class DeviceGrower:
                             break
                     if lvl > 4096:
                         raise RuntimeError("device level loop did not terminate")
-                    if REC_DUMP is not None:  # (tools: per-level split records)
-                        REC_DUMP.append(rec[: int(min(2 ** min(lvl - 1, 40), KMAX))].clone())
                     continue
                 if prof:
                     marks.append([])
@@ -835,6 +845,9 @@ class DeviceGrower:
                     order = torch.argsort(jobs[:J, 1] * (1 << 32) - jobs[:J, 3],
                                           descending=True)
                     d_jobs = jobs[:J].index_select(0, order)
+                if DUMP is not None:
+                    DUMP.update(jobs=d_jobs.clone(), idx=be.idx.clone(), tmp=be.tmp.clone(),
+                                row_mask=int(be.row_mask))
                 if dp:
                     self._dp_finish(d_jobs, W)
                 else:

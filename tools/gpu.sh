@@ -23,6 +23,7 @@
 #   pmc[:ARGS]           two PMC passes over bench/pmc_fit.py ARGS      -> pmc_report.md
 #   sim:ARGS             bench/sim_own_ranks.py ARGS                    -> sim_own.jsonl
 #   simx:ARGS            bench/sim_exact_ranks.py ARGS                  -> sim_exact.jsonl
+#   simdp:ARGS           bench/sim_dp_ranks.py ARGS (data parallel)     -> sim_dp.jsonl
 #   py:SCRIPT[:ARGS]     python -u SCRIPT ARGS (150 s)                  -> py_<script>.log
 #
 # ARGS use ',' for spaces: "bench:--continuous,--steps,10" runs
@@ -131,6 +132,10 @@ print(d['ms_per_step'], d['config']['tree_nodes'])" >> gpurun_out/ab.log
       # shellcheck disable=SC2046
       timeout -k 10 400 python -u bench/sim_exact_ranks.py $(args_of "$rest") \
         >> gpurun_out/sim_exact.jsonl 2>> gpurun_out/sim_exact.err ;;
+    simdp)
+      # shellcheck disable=SC2046
+      timeout -k 10 600 python -u bench/sim_dp_ranks.py $(args_of "$rest") \
+        >> gpurun_out/sim_dp.jsonl 2>> gpurun_out/sim_dp.err ;;
     py)
       script=${rest%%:*}
       sargs=""
