@@ -18,6 +18,9 @@ One JSON line per config (wall-clock per fit, samples/s, tree size):
   1m_q1024    1M x 64 continuous features, 1024 quantile bins (16-bit codes), 1 GPU
   1m_c64      1M x 64 classification with 64 classes, 1 GPU (feature-tiled finisher)
   200k_f512   200k x 512 classification, 1 GPU (feature-tiled finisher)
+  1m_c300     1M x 64 classification with 300 classes (class-tiled level histograms,
+              255-row finisher jobs), 1 GPU
+  200k_f512_reg  200k x 512 regression (regression finisher past 256 features), 1 GPU
   10m         10M x 128 synthetic classification, 1 GPU (the 8-GPU
               data-parallel run is bench.py under torchrun)
 
@@ -146,7 +149,7 @@ def main(argv=None):
     ap.add_argument("names", nargs="*",
                     default=["iris", "sweep", "sweep_gpu", "100k", "1m", "1m_exact",
                              "100k_exact", "1m_reg", "1m_exact_reg", "1m_q1024", "1m_c64",
-                             "200k_f512", "10m"])
+                             "200k_f512", "1m_c300", "200k_f512_reg", "10m"])
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args(argv)
     for name in a.names:
@@ -188,6 +191,12 @@ def main(argv=None):
         elif name == "200k_f512":
             rows = [{"config": "200k x 512 classification, full depth, 1 GPU",
                      **_gpu_fit(200_000, 512, a.reps)}]
+        elif name == "1m_c300":
+            rows = [{"config": "1M x 64 classification, 300 classes, full depth, 1 GPU",
+                     **_gpu_fit(1_000_000, 64, max(2, a.reps // 2), classes=300)}]
+        elif name == "200k_f512_reg":
+            rows = [{"config": "200k x 512 regression (squared_error), full depth, 1 GPU",
+                     **_gpu_fit(200_000, 512, a.reps, regression=True)}]
         elif name == "10m":
             rows = [{"config": "10M x 128 classification, full depth, 1 GPU",
                      **_gpu_fit(10_000_000, 128, max(2, a.reps // 2))}]

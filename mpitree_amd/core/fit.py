@@ -405,6 +405,14 @@ def fit_tree(
         # (regression: the hand-off queue gains 0.35 ms at any of n/512 .. n/128)
         default_fr = int(env) if env else (max(2048, n // 512) if regression
                                            else max(2048, min(n // 128, 32768)))
+        if not env and F > 128:
+            # a finisher node scans F x B bins whatever its rows: past 128 features
+            # smaller jobs (more level-loop levels, which scan many nodes at once) win
+            # (200k x 512: classification 20.5 -> 11.8 ms at 512 rows; regression,
+            # whose features past 256 read their bins from memory, 313 -> 76 ms at 128;
+            # profiles/baseline_configs.md)
+            default_fr = min(default_fr, 128 if (regression and F > 256)
+                             else max(256, (1 << 18) // F))
         if not env and C > 2:
             # (more classes: no hand-off queue, and a node's histogram scan grows
             # with B * C -- smaller jobs keep every finisher workgroup busy)

@@ -29,7 +29,7 @@ void launch_hist_derive(hipStream_t, const int64_t*, int, const void*, void*, in
 void launch_scan(hipStream_t, const void*, const int64_t*, int, const int32_t*, int, int, int,
                  int, int, int, double*, int32_t*, int64_t*, const double*, int,
                  const int32_t*, const int64_t*, const void*, const int32_t*, int32_t*,
-                 int32_t*);
+                 int32_t*, const int32_t*);
 bool scan_fused_select_ok(int B, int C, int crit);
 void launch_partition(hipStream_t, const void*, int, int64_t, uint32_t*, uint32_t*, uint32_t,
                       const int64_t*, int, const int64_t*, int32_t*, const int32_t*, bool);
@@ -147,15 +147,16 @@ PYBIND11_MODULE(_hip, m) {
   m.def("scan", [](uintptr_t s, uintptr_t hist, uintptr_t nodes, int k, uintptr_t nbins, int F_h,
                    int f_lo, int B, int C, int crit, int msl, uintptr_t cost, uintptr_t bins,
                    uintptr_t rec, uintptr_t xtab, int xtab_n, uintptr_t dcount, uintptr_t der,
-                   uintptr_t prev, uintptr_t nbuilt) {
+                   uintptr_t prev, uintptr_t nbuilt, uintptr_t node_tot) {
     mt::launch_scan(S(s), P<void>(hist), P<int64_t>(nodes), k, P<int32_t>(nbins), F_h, f_lo, B, C,
                     crit, msl, P<double>(cost), P<int32_t>(bins), P<int64_t>(rec),
                     P<double>(xtab), xtab_n, P<int32_t>(dcount), P<int64_t>(der), P<void>(prev),
-                    P<int32_t>(nbuilt), nullptr, nullptr);
+                    P<int32_t>(nbuilt), nullptr, nullptr, P<int32_t>(node_tot));
   }, "", py::arg("s"), py::arg("hist"), py::arg("nodes"), py::arg("k"), py::arg("nbins"),
      py::arg("F_h"), py::arg("f_lo"), py::arg("B"), py::arg("C"), py::arg("crit"), py::arg("msl"),
      py::arg("cost"), py::arg("bins"), py::arg("rec"), py::arg("xtab"), py::arg("xtab_n"),
-     py::arg("dcount") = 0, py::arg("der") = 0, py::arg("prev") = 0, py::arg("nbuilt") = 0);
+     py::arg("dcount") = 0, py::arg("der") = 0, py::arg("prev") = 0, py::arg("nbuilt") = 0,
+     py::arg("node_tot") = 0);
   m.def("partition", [](uintptr_t s, uintptr_t codes_fm, int cb, int64_t n_rows, uintptr_t idx,
                         uintptr_t tmp, uint32_t mask, uintptr_t items, int n_items,
                         uintptr_t split, uintptr_t cursors, uintptr_t dcount, bool copy_back) {
@@ -311,10 +312,11 @@ PYBIND11_MODULE(_hip, m) {
                                  uintptr_t pos_st64, int reg, int out_buf, uintptr_t jobs,
                                  uintptr_t job_count, int C, int max_depth, int n_cu, int64_t mss,
                                  int64_t msl, int64_t fr, uintptr_t host_ctl, int host_tag,
-                                 int dp, bool fixup, py::dict own) {
-    const mt::PlanArgs a = plan_args(cur, nxt, rec, split, pitems, cursors, pctl, pos_rec, pos_st,
-                                     pos_st64, reg, out_buf, jobs, job_count, C, max_depth, n_cu,
-                                     mss, msl, fr, host_ctl, host_tag, dp, own);
+                                 int dp, bool fixup, py::dict own, int derive_free) {
+    mt::PlanArgs a = plan_args(cur, nxt, rec, split, pitems, cursors, pctl, pos_rec, pos_st,
+                               pos_st64, reg, out_buf, jobs, job_count, C, max_depth, n_cu,
+                               mss, msl, fr, host_ctl, host_tag, dp, own);
+    a.derive_free = derive_free;
     if (fixup)
       mt::launch_grow_dp_fixup(S(s), a);
     else
@@ -324,7 +326,7 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("pos_st"), py::arg("pos_st64"), py::arg("reg"), py::arg("out_buf"), py::arg("jobs"),
      py::arg("job_count"), py::arg("C"), py::arg("max_depth"), py::arg("n_cu"), py::arg("mss"),
      py::arg("msl"), py::arg("fr"), py::arg("host_ctl"), py::arg("host_tag"), py::arg("dp") = 0,
-     py::arg("fixup") = false, py::arg("own") = py::dict());
+     py::arg("fixup") = false, py::arg("own") = py::dict(), py::arg("derive_free") = 0);
   m.def("exact_setup_temp_bytes", &mt::exact_setup_temp_bytes);
   m.def("exact_setup_chunk", &mt::exact_setup_chunk);
   m.def("exact_setup_sort", [](uintptr_t s, uintptr_t X, int64_t n, int F, uintptr_t k0,

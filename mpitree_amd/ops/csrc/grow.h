@@ -115,6 +115,9 @@ struct PlanArgs {
   const int32_t* sel_tot = nullptr;
   int sel_F = 0;
   int crit = 0;
+  // 1: every next-frontier child is built from rows, none derived (one histogram
+  // buffer for both level parities: many-class fits whose two would not fit)
+  int derive_free = 0;
 };
 
 }  // namespace mt

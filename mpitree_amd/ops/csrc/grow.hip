@@ -547,7 +547,7 @@ __global__ __launch_bounds__(kPlanThreads) void grow_plan_kernel(PlanArgs a) {
   auto active = [&](int i) {
     return !own_sw || a.own.node_owner[i] < 0 || a.own.node_owner[i] == a.own.rank;
   };
-  const bool build_all = own_sw && a.own.build_all;
+  const bool build_all = a.derive_free || (own_sw && a.own.build_all);
   // decisions of this level; at the switch (jobs_at_switch) the children that
   // would keep growing become finisher jobs: the rank's own work is its jobs
   auto decide = [&](int i) {

@@ -35,7 +35,7 @@ void launch_hist_derive(hipStream_t, const int64_t*, int, const void*, void*, in
 void launch_scan(hipStream_t, const void*, const int64_t*, int, const int32_t*, int, int, int,
                  int, int, int, double*, int32_t*, int64_t*, const double*, int,
                  const int32_t*, const int64_t*, const void*, const int32_t*, int32_t*,
-                 int32_t*);
+                 int32_t*, const int32_t*);
 void launch_grow_plan(hipStream_t, const PlanArgs&);
 void launch_partition(hipStream_t, const void*, int, int64_t, uint32_t*, uint32_t*, uint32_t,
                       const int64_t*, int, const int64_t*, int32_t*, const int32_t*, bool);
@@ -95,6 +95,7 @@ struct GrowCtx {
   int64_t KMAX = 0, IMAX = 0, TMAX = 0, RMAX = 0, PMAX = 0, MMAX = 0;
   int64_t mss = 2, msl = 1, fr = 0;
   int32_t tag0 = 0;
+  int derive_free = 0;
   OwnArgs own{0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, 0};
 
   void level(hipStream_t s, int lvl) {
@@ -125,7 +126,7 @@ struct GrowCtx {
     if (lvl > 0 && reg) launch_hist_derive(s, cur.der, (int)kb, Hp, H, E, true, ctl + 4);
     launch_scan(s, H, ident, (int)kb, nbins, F_h, f_lo, B, C, crit, (int)msl, cost, bins, rec,
                 xtab, xtab_n, ctl, fuse ? cur.der : nullptr, fuse ? Hp : nullptr,
-                fuse ? ctl + 1 : nullptr, sel_left, sel_tot);
+                fuse ? ctl + 1 : nullptr, sel_left, sel_tot, reg ? nullptr : cur.stats);
     PlanArgs a{cur,       nxt,        rec,        split,
                pitems,    cursors,    ctl + 5,    pos_rec,
                reg ? nullptr : (int32_t*)pos_st,  reg ? (int64_t*)pos_st : nullptr,
@@ -133,6 +134,7 @@ struct GrowCtx {
                C,         md,         n_cu,       mss,
                msl,       fr,         host_ctl + (lvl % 64) * 16,
                tag0 + (lvl % 4096) + 1, 0, own};
+    a.derive_free = derive_free;
     if (sel_left) {
       a.sel_cost = cost;
       a.sel_bins = bins;
@@ -210,6 +212,7 @@ void bind_grow(py::module_& m) {
         c.PMAX = g("PMAX");
         c.MMAX = g("MMAX");
         c.tag0 = (int32_t)g("tag0");
+        c.derive_free = d.contains("derive_free") ? (int)g("derive_free") : 0;
         if (d.contains("sel_left")) {
           c.sel_left = ptr<int32_t>(g("sel_left"));
           c.sel_tot = ptr<int32_t>(g("sel_tot"));

@@ -144,7 +144,19 @@ __global__ __launch_bounds__(256) void target_stats_kernel(const T* __restrict__
     amax = fmax(amax, __shfl_xor(amax, d, kWave));
     bad += __shfl_xor(bad, d, kWave);
   }
+  // one atomic per workgroup (same-address atomics serialise in the L2)
+  __shared__ double s_a[4];
+  __shared__ unsigned s_b[4];
   if (lane_id() == 0) {
+    s_a[threadIdx.x >> 6] = amax;
+    s_b[threadIdx.x >> 6] = bad;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) {
+      amax = fmax(amax, s_a[w]);
+      bad += s_b[w];
+    }
     // non-negative doubles order as their bit patterns
     atomicMax(reinterpret_cast<unsigned long long*>(st), (unsigned long long)__double_as_longlong(amax));
     if (bad) atomicAdd(reinterpret_cast<unsigned long long*>(st) + 1, (unsigned long long)bad);
@@ -179,7 +191,19 @@ __global__ __launch_bounds__(256) void target_encode_kernel(const T* __restrict_
     mn = a < mn ? a : mn;
     mx = b > mx ? b : mx;
   }
+  __shared__ long long s_s[4], s_mn[4], s_mx[4];
   if (lane_id() == 0) {
+    s_s[threadIdx.x >> 6] = sum;
+    s_mn[threadIdx.x >> 6] = mn;
+    s_mx[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) {
+      sum += s_s[w];
+      mn = s_mn[w] < mn ? s_mn[w] : mn;
+      mx = s_mx[w] > mx ? s_mx[w] : mx;
+    }
     atomicAdd(reinterpret_cast<unsigned long long*>(st) + 3, (unsigned long long)sum);
     atomicMin(reinterpret_cast<long long*>(st) + 4, mn);
     atomicMax(reinterpret_cast<long long*>(st) + 5, mx);
@@ -190,7 +214,7 @@ void launch_targets(hipStream_t stream, const void* y, bool y64, int64_t n, int6
                     int64_t* out) {
   MT_HIP_CHECK(hipMemsetAsync(st, 0, 8 * sizeof(int64_t), stream));
   if (n <= 0) return;
-  const unsigned g = std::min(label_grid(n), 1024u);
+  const unsigned g = std::min(label_grid(n), 512u);
   if (y64) {
     hipLaunchKernelGGL(target_stats_kernel<double>, dim3(g), dim3(256), 0, stream,
                        (const double*)y, n, st);

@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
     const double* __restrict__ xtab, int xtab_n, const int32_t* __restrict__ dcount,
     const int64_t* __restrict__ der, const uint32_t* __restrict__ prev,
     const int32_t* __restrict__ nbuilt, int der_lds, int32_t* __restrict__ sel_left,
-    int32_t* __restrict__ sel_tot) {
+    int32_t* __restrict__ sel_tot, const int32_t* __restrict__ node_tot) {
   // sel_left / sel_tot (fused selection, two-class fast path): the left class
   // counts at this feature's best bin [node][F_h][2] and, from feature 0's wave,
   // the node's class totals and node term [node][4] = {t0, t1, term (f64)}, for
@@ -261,9 +261,22 @@ __global__ __launch_bounds__(256) void scan_cls_kernel(
     return;
   }
 
-  // pass 1: per-class totals, kScanCG classes at a time (independent reductions)
+  // pass 1: per-class totals -- the node's class counts when the caller has them
+  // (the device level loop: int32 [node][C]; every feature's bins sum to them),
+  // else kScanCG classes at a time over the bins (independent reductions)
   uint32_t m = 0;
-  for (int c0 = 0; c0 < C; c0 += kScanCG) {
+  if (node_tot != nullptr) {
+    const int32_t* nt = node_tot + node * C;
+    uint32_t part = 0;
+    for (int c = lane; c < C; c += kWave) {
+      const uint32_t t = (uint32_t)nt[c];
+      tot[c] = t;
+      carry[c] = 0;
+      part += t;
+    }
+    m = wave_sum_u32(part);
+  }
+  for (int c0 = 0; c0 < C && node_tot == nullptr; c0 += kScanCG) {
     uint32_t s[kScanCG];
 #pragma unroll
     for (int g = 0; g < kScanCG; ++g) s[g] = 0;
@@ -669,7 +682,8 @@ void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int
                  const int32_t* nbins, int F_h, int f_lo, int B, int C, int crit, int msl,
                  double* cost, int32_t* bins, int64_t* rec, const double* xtab, int xtab_n,
                  const int32_t* dcount, const int64_t* der, const void* prev,
-                 const int32_t* nbuilt, int32_t* sel_left, int32_t* sel_tot) {
+                 const int32_t* nbuilt, int32_t* sel_left, int32_t* sel_tot,
+                 const int32_t* node_tot) {
   // sel_left (fused selection): the planner builds the records, no select launch
   if (k <= 0) return;
   if (sel_left && !scan_fused_select_ok(B, C, crit))
@@ -687,7 +701,8 @@ void launch_scan(hipStream_t stream, const void* hist, const int64_t* nodes, int
     MT_HIP_CHECK(mt_set_max_lds((const void*)scan_cls_kernel, (int)lds));
     hipLaunchKernelGGL(scan_cls_kernel, grid, dim3(256), lds, stream, (uint32_t*)hist,
                        nodes, nbins, F_h, f_lo, B, C, crit, msl, cost, bins, xtab, xtab_n,
-                       dcount, der, (const uint32_t*)prev, nbuilt, der_lds, sel_left, sel_tot);
+                       dcount, der, (const uint32_t*)prev, nbuilt, der_lds, sel_left, sel_tot,
+                       node_tot);
   }
   MT_HIP_CHECK(hipGetLastError());
   if (sel_left) return;

@@ -165,21 +165,48 @@ def device_loop_supported(be, params, comm) -> bool:
     # the planner drives the LDS histogram path only (feature or class tiles)
     if not be.lds_hist():
         return False
-    # two levels of [KMAX][F][B][C] histograms plus the item slabs must fit (many
-    # classes: ~19.7 MB per node at 64 x 256 x 300)
-    return level_loop_bytes(be.n, be.F, be.B, be.C, bool(be.reg), int(params.finisher_rows),
-                            be.hip) <= free_device_bytes(be.device) // 2
+    # the level's [KMAX][F][B][C] histograms (two level parities, or one when
+    # derive-free) plus the item slabs must fit (many classes: ~19.7 MB per node
+    # at 64 x 256 x 300)
+    n, F, B, C, reg = be.n, be.F, be.B, be.C, bool(be.reg)
+    fr = int(params.finisher_rows)
+    par = 1 if derive_free_levels(n, F, B, C, reg, fr, be.hip, be.device) else 2
+    return level_loop_bytes(n, F, B, C, reg, fr, be.hip, par) <= free_device_bytes(be.device) // 2
 
 
-def level_loop_bytes(n, F, B, C, reg, fr, hip) -> int:
-    """Device bytes of the level loop's histogram buffers (both level parities)
-    and item slabs for ``n`` rows with finisher jobs of at most ``fr`` rows."""
+def slab_rows(n_loc: int) -> int:
+    """Item slabs a level can need: only nodes split over several items use
+    them, and such items hold >= 1024 rows each plus one partial item per node
+    (plan_hist_items: <= 2 n / 1024)."""
+    return 2 * (n_loc // 1024) + 16
+
+
+def level_loop_bytes(n, F, B, C, reg, fr, hip, parities: int = 2) -> int:
+    """Device bytes of the level loop's histogram buffers (``parities`` level
+    parities) and item slabs for ``n`` rows with finisher jobs of at most ``fr``
+    rows."""
     KMAX = n // (fr + 1) + 2
     IMAX = KMAX + n // 1024 + 2 * hb.N_CU + 16
     esz = 8 if reg else 4
-    hist = 2 * KMAX * F * B * (2 if reg else C) * esz
-    slab = IMAX * int(hip.hist_slab_words(F, B, C, reg)) * esz
+    hist = parities * KMAX * F * B * (2 if reg else C) * esz
+    slab = min(IMAX, slab_rows(n)) * int(hip.hist_slab_words(F, B, C, reg)) * esz
     return int(hist + slab)
+
+
+def derive_free_levels(n, F, B, C, reg, fr, hip, device) -> bool:
+    """Whether the level loop keeps ONE histogram buffer and builds every child
+    from rows (no parent - sibling derivation, which needs the parent level's
+    histograms): when two parities would take more than 40 % of the device
+    (1M x 64 with 300 classes: 154 GB of histograms for 255-row finisher jobs).
+    ``MPITREE_DERIVE_FREE`` = 1 / 0 forces it."""
+    env = os.environ.get("MPITREE_DERIVE_FREE")
+    if env is not None:
+        return env != "0"
+    try:
+        total = int(torch.cuda.get_device_properties(device).total_memory)
+    except Exception:  # pragma: no cover - (no device: tests on CPU)
+        return False
+    return level_loop_bytes(n, F, B, C, reg, fr, hip, 2) > 0.4 * total
 
 
 def free_device_bytes(dev) -> int:
@@ -554,14 +581,18 @@ class DeviceGrower:
             # (no select launch)
             fsel = (not (reg or dp or fp) and bool(hip.scan_fused_select_ok(B, C, int(be.crit)))
                     and os.environ.get("MPITREE_FUSED_SELECT", "1") != "0")
+            dfree = derive_free_levels(n_loc, F_h, B, C, reg, fr, hip, dev)
+            if dfree:
+                self.stats["derive_free"] = True
 
             def make():
                 i64 = dict(dtype=torch.int64, device=dev)
                 return dict(
                     sets=[self._lists(KMAX, IMAX, TMAX, MMAX, C, reg, dev) for _ in range(2)],
                     hists=[torch.empty((KMAX, F_h, B, C), dtype=hdt, device=dev)
-                           for _ in range(2)],
-                    slab=torch.empty((IMAX, hip.hist_slab_words(F_h, B, C, reg)), dtype=hdt,
+                           for _ in range(1 if dfree else 2)] * (2 if dfree else 1),
+                    slab=torch.empty((min(IMAX, slab_rows(n_loc)),
+                                      hip.hist_slab_words(F_h, B, C, reg)), dtype=hdt,
                                      device=dev),
                     rec=torch.empty((KMAX, R), **i64),
                     grec=torch.empty((P * KMAX * R) if (fp or dprs or fpx) else 1, **i64),
@@ -595,7 +626,7 @@ class DeviceGrower:
                 )
 
             ws = self._workspace((str(dev), n, n_loc, F, f_lo, F_h, B, C, reg, fr, dp, own, fsel,
-                                  fpx), make)
+                                  fpx, dfree), make)
             sets, hists, slab, rec = ws["sets"], ws["hists"], ws["slab"], ws["rec"]
             cost, bins, ident, split = ws["cost"], ws["bins"], ws["ident"], ws["split"]
             pitems, cursors, jobs, job_count = (ws["pitems"], ws["cursors"], ws["jobs"],
@@ -666,7 +697,7 @@ class DeviceGrower:
                     n_loc=n_loc, F_h=F_h, f_lo=f_lo, B=B, C=C, reg=int(reg), crit=int(be.crit),
                     E=E, max_depth=md, mss=mss, msl=msl, fr=fr, n_cu=plan_cu,
                     lds_budget=hb.LDS_BUDGET, KMAX=KMAX, IMAX=IMAX, TMAX=TMAX, RMAX=RMAX,
-                    PMAX=PMAX, MMAX=MMAX, tag0=tag0,
+                    PMAX=PMAX, MMAX=MMAX, tag0=tag0, derive_free=int(dfree),
                     **(dict(sel_left=ws["sel_left"].data_ptr(), sel_tot=ws["sel_tot"].data_ptr())
                        if fsel else {})), ptrs[0], ptrs[1], own_args)
 
@@ -677,7 +708,8 @@ class DeviceGrower:
                               be.pos_st.data_ptr() if reg else 0, int(reg), (lvl + 1) % 2,
                               jobs.data_ptr(), job_count.data_ptr(), C, md, plan_cu, mss, msl,
                               fr, 0 if fixup else hctl_dev + (lvl % 64) * 64,
-                              tag0 + (lvl % 4096) + 1, dp=int(dp), fixup=fixup, own=own_args)
+                              tag0 + (lvl % 4096) + 1, dp=int(dp), fixup=fixup, own=own_args,
+                              derive_free=int(dfree))
 
             fpx_on = fpx  # (until the switch: feature-parallel levels)
             # a level can switch only once it has min_units units (<= 2^level)
@@ -771,7 +803,8 @@ class DeviceGrower:
                          B, C, int(be.crit), msl, cost.data_ptr(), bins.data_ptr(),
                          rec.data_ptr(), be.xtab.data_ptr(), hb.XTAB_N, dcount=ctl,
                          der=cur["der"] if fuse else 0, prev=Hp.data_ptr() if fuse else 0,
-                         nbuilt=ctl + 4 * 1 if fuse else 0)
+                         nbuilt=ctl + 4 * 1 if fuse else 0,
+                         node_tot=0 if reg else cur["stats"])
                 if fp or dprs or fpx_on:  # every rank's best split of each node -> the global best
                     g = ws["grec"][: P * kb * R]
                     comm.all_gather_device(g, rec[:kb].reshape(-1))

@@ -411,6 +411,26 @@ def test_gpu_regression_device_loop_matches_host(monkeypatch, seed, max_depth):
     assert r1.arrays.equal(r3.arrays)
 
 
+@pytest.mark.parametrize("regression,C", [(False, 2), (False, 7), (True, 0)])
+def test_gpu_derive_free_levels_match_host(monkeypatch, regression, C):
+    """Derive-free levels (one histogram buffer; every child built from rows --
+    what many-class fits too large for two level parities take): the same tree as
+    the host builder."""
+    from mpitree_amd.core.fit import fit_tree
+
+    monkeypatch.setenv("MPITREE_DERIVE_FREE", "1")
+    rng = np.random.default_rng(41 + C)
+    X, y = random_problem(rng, 30000, 9, max(C, 2), 40, regression=regression)
+    kw = dict(regression=regression, criterion=2 if regression else 0, max_depth=None,
+              min_samples_split=2, finisher_rows=500)
+    g = fit_tree(X, y, device="cuda", **kw)
+    assert g.engine == "hip-device-loop" and g.stats.get("derive_free")
+    h = fit_tree(X, y, device="cpu", **kw)
+    assert g.arrays.equal(h.arrays)
+    if regression:
+        assert np.array_equal(g.arrays.value, h.arrays.value)
+
+
 @pytest.mark.parametrize("F", [300, 600])
 def test_gpu_regression_wide_features_device_loop(F):
     """Regression past 256 features runs the device level loop and the block
