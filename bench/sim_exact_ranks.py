@@ -87,6 +87,11 @@ class Recorder:
         def fix(s, *a):
             from mpitree_amd.ops import hip_backend as hb
 
+            if rec.fm is None:  # (one GPU: the local-codes kernel wrote codes_rm itself)
+                loc = next(iter(rec.eg._WS["loc"].values()))
+                rec.fm = loc["fm"].clone()
+                J = int(a[10])  # xe_fix(s, E0, E1, X, x64, F, n, f_lo, F_loc, jobs, J, ...)
+                rec.jobs = rec._ws()["jobs"][:J].clone()
             dev = rec.fm.device
             rows = hb._workspace(dev, "pos_rec", 0)
             rec.prefix = rows.clone()  # position records before the threshold fix
@@ -135,6 +140,8 @@ class SimFeatureComm(LocalComm):
 
     def all_reduce_device(self, t, op=None):
         self.bytes_communicated += t.numel() * t.element_size()
+        if t.numel() == 1:  # the watchdog word (MAX over ranks): this rank's stands
+            return
         t.copy_(self.ref["flag"][self.flag_lvl])
         self.flag_lvl += 1
 
@@ -210,7 +217,7 @@ def main():
                         min_samples_split=2, max_bins=None, device="cuda", comm=comm)
 
     fit()
-    P_list = [int(v) for v in a.ranks.split(",")]
+    P_list = [int(v) for v in a.ranks.replace("+", ",").split(",")]
     ref, data = build_reference(fit, dev, P_list, 2)
     assert ref.engine == "hip-exact", ref.engine
     for P in P_list:
