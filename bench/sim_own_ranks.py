@@ -144,12 +144,11 @@ class SimOwnComm(LocalComm):
 def packed_bytes(ta) -> np.ndarray:
     """A finished tree's columns in the device assembly's packed layout
     (``TreeArrays.from_packed``)."""
-    cols = [ta.n_samples.astype(np.int64), ta.threshold.astype(np.float64),
-            ta.impurity.astype(np.float64)]
+    cols = [ta.n_samples.astype(np.int64), ta.threshold.astype(np.float64)]
     if ta.value is not None:
-        cols += [ta.value.astype(np.float64), ta.meta["sum_fixed"].astype(np.int64)]
+        cols += [ta.value.astype(np.float64)]
     else:
-        cols += [ta.count.astype(np.int32)]
+        cols += [ta.impurity.astype(np.float64), ta.count.astype(np.int32)]
     cols += [c.astype(np.int32) for c in (ta.feature, ta.threshold_bin, ta.left, ta.right,
                                           ta.depth)]
     return np.concatenate([np.ascontiguousarray(c).view(np.uint8).reshape(-1) for c in cols])

@@ -41,9 +41,10 @@ class TreeArrays:
     def from_packed(cls, buf: np.ndarray, N: int, C: int, regression: bool,
                     max_depth: int | None = None) -> "TreeArrays":
         """Views of the device assembly's packed columns (``ops/csrc/assemble.hip``
-        ``asm_cols``): n_samples i64 | threshold f64 | impurity f64 | counts i32
-        [N, C] (or leaf value f64 + fixed-point sum i64) | feature, threshold_bin,
-        left, right, depth i32. Every column is final: no host pass follows."""
+        ``asm_cols``): n_samples i64 | threshold f64 | impurity f64 + counts i32
+        [N, C] (or the leaf value f64: a regression tree's impurity is NaN at every
+        node, a read-only broadcast view here) | feature, threshold_bin, left,
+        right, depth i32. Every column is final: no host pass follows."""
         o = 0
 
         def take(dtype, count):
@@ -54,12 +55,12 @@ class TreeArrays:
 
         n_samples = take(np.int64, N)
         threshold = take(np.float64, N)
-        impurity = take(np.float64, N)
-        count = value = s_fixed = None
-        if regression:
+        count = value = None
+        if regression:  # (impurity: NaN at every node of a regression tree)
+            impurity = np.broadcast_to(np.float64(np.nan), (N,))
             value = take(np.float64, N)
-            s_fixed = take(np.int64, N)
         else:
+            impurity = take(np.float64, N)
             count = take(np.int32, N * C).reshape(N, C)
         feature = take(np.int32, N)
         threshold_bin = take(np.int32, N)
@@ -69,8 +70,6 @@ class TreeArrays:
         ta = cls(feature=feature, threshold=threshold, threshold_bin=threshold_bin, left=left,
                  right=right, depth=depth, n_samples=n_samples, impurity=impurity, count=count,
                  value=value)
-        if regression:
-            ta.meta["sum_fixed"] = s_fixed
         ta.meta["final"] = True  # thresholds, impurities and values need no host pass
         if max_depth is not None:
             ta.meta["max_depth"] = int(max_depth)

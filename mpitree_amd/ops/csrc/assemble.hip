@@ -181,10 +181,10 @@ __global__ __launch_bounds__(kAsmThreads) void asm_rank_kernel(const int32_t* __
 // from the device (asm_offsets_kernel's total), so the emit launch needs no
 // host round trip. Every column of the finished tree is emitted in its final
 // dtype -- the host receives numpy views, nothing is derived after the copy:
-//   n_samples i64 [N] | threshold f64 [N] | impurity f64 [N]
-//   | counts i32 [N][C] (classification: rows < 2^31, half the bytes of the one
-//     D2H at many classes) or leaf value f64 [N] + fixed-point
-//     target sum i64 [N] (regression)
+//   n_samples i64 [N] | threshold f64 [N]
+//   | impurity f64 [N] + counts i32 [N][C] (classification: rows < 2^31, half the
+//     bytes of the one D2H at many classes) or leaf value f64 [N] (regression:
+//     impurity is NaN for every node, the host makes it a broadcast view)
 //   | feature i32 [N] | threshold_bin i32 [N] | left i32 [N] | right i32 [N]
 // (thresholds: edges[feature][bin], or per position from thr_pos -- the exact
 // engine's split values)
@@ -209,7 +209,7 @@ struct AsmCols {
 };
 
 __host__ __device__ inline int64_t asm_bytes(int64_t N, int C, bool reg) {
-  return N * (24 + (reg ? 16 : 4 * (int64_t)C) + 20);
+  return N * (reg ? 8 + 8 + 8 + 20 : 24 + 4 * (int64_t)C + 20);
 }
 
 __device__ inline AsmCols asm_cols(uint8_t* base, int64_t N, int C, bool reg) {
@@ -219,17 +219,17 @@ __device__ inline AsmCols asm_cols(uint8_t* base, int64_t N, int C, bool reg) {
   p += N * 8;
   o.threshold = reinterpret_cast<double*>(p);
   p += N * 8;
-  o.impurity = reinterpret_cast<double*>(p);
-  p += N * 8;
+  o.impurity = nullptr;
   o.count = nullptr;
   o.value = nullptr;
   o.sum = nullptr;
-  if (reg) {
+  if (reg) {  // (no impurity column: NaN for every regression node, made on the host
+              //  as a broadcast view; no fixed-point sum: the value is final)
     o.value = reinterpret_cast<double*>(p);
     p += N * 8;
-    o.sum = reinterpret_cast<int64_t*>(p);
-    p += N * 8;
   } else {
+    o.impurity = reinterpret_cast<double*>(p);
+    p += N * 8;
     o.count = reinterpret_cast<int32_t*>(p);
     p += N * 4 * (int64_t)C;
   }
@@ -388,9 +388,7 @@ __global__ __launch_bounds__(kAsmThreads) void asm_emit_kernel(
   if (reg) {
     const int64_t m = (int64_t)s[0], sf = (int64_t)s[1];
     o.nsamp[j] = m;
-    o.sum[j] = sf;
     o.value[j] = ldexp((double)sf / (double)(m > 1 ? m : 1), -y_exp);
-    o.impurity[j] = __builtin_nan("");
   } else {
     int64_t m = 0, sq = 0;
     double acc = 0.0;
