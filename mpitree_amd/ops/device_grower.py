@@ -93,7 +93,13 @@ def own_min_units(P: int) -> int:
 POLL_TIMEOUT_S = float(os.environ.get("MPITREE_POLL_TIMEOUT", "120"))
 # histogram work items per CU and level (1 or 2): fewer, larger items write fewer
 # LDS slabs for the reduction to read back
-HIST_ITEMS_PER_CU = max(1, min(2, int(os.environ.get("MPITREE_HIST_ITEMS", "2"))))
+def hist_items_per_cu(reg: bool) -> int:
+    """Histogram work items per CU and level: 2 for classification, 1 for
+    regression, whose int64 {count, sum} slabs double the reduction's reads
+    (1M x 64 regression 9.35 -> 9.07 ms, profiles/r5/ab_hist_items_reg.log);
+    ``MPITREE_HIST_ITEMS`` forces it."""
+    env = os.environ.get("MPITREE_HIST_ITEMS")
+    return max(1, min(2, int(env))) if env else (1 if reg else 2)
 
 
 def fp_prefix_pays(n: int, F: int, P: int, reg: bool) -> bool:
@@ -649,7 +655,7 @@ class DeviceGrower:
             else:
                 # level 0: the root, built from rows (one init launch; root stats H2D)
                 chunk = int(min(hb.MAX_ITEM_ROWS,
-                                max(1024, -(-n_loc // (HIST_ITEMS_PER_CU * hb.N_CU)))))
+                                max(1024, -(-n_loc // (hist_items_per_cu(reg) * hb.N_CU)))))
                 ws["root_host"].numpy()[: root_full.size] = root_full
                 ws["root"].copy_(ws["root_host"], non_blocking=True)
                 hip.grow_init(s(), ptrs[0], n_loc, n, chunk, C, int(reg), ws["root"].data_ptr(),
@@ -678,7 +684,8 @@ class DeviceGrower:
                                 jobs_at_switch=own_jobs_at_switch(be),
                                 segs=ws["own_segs"].data_ptr(), build_all=int(fpx))
 
-            plan_cu = hb.N_CU * HIST_ITEMS_PER_CU // 2  # (the planner makes 2 items per "CU")
+            # (the planner makes 2 items per "CU")
+            plan_cu = hb.N_CU * hist_items_per_cu(reg) // 2
             # single-rank and subtree-ownership levels (no collective between the
             # kernels, no per-phase profile events): one C++ call enqueues a level
             ctx = None
