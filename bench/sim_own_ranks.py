@@ -41,6 +41,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from mpitree_amd.core.levelwise import LocalComm  # noqa: E402
+from mpitree_amd.parallel.shared_tree import GATHER_HDR  # noqa: E402
 
 
 class SimSlot:
@@ -75,14 +76,14 @@ class SimPool:
     def free_mask(self) -> int:
         return 1
 
-    def choose(self, masks, need: int):
+    def choose(self, masks, need: int, shm_free=None):
         assert need <= self.slot.ref.size, "tree larger than the reference"
         return self.slot
 
     def take_next(self):
         return self.slot
 
-    def plan_next(self, masks, current, need: int) -> None:
+    def plan_next(self, masks, current, need: int, shm_free=None) -> None:
         return None
 
     def barrier(self, slot) -> None:
@@ -109,7 +110,8 @@ class SimOwnComm(LocalComm):
         self.ref_rows = ref_rows
         self.ref_pos, self.ref_depth = ref_pos, int(ref_depth)
         self._shm_pool = pool if pool is not None else False
-        self._head = torch.tensor([int(ref_depth), 1], dtype=torch.int64, device=device)
+        self._head = torch.tensor([int(ref_depth), 1, 1 << 62], dtype=torch.int64,
+                                  device=device)
         self.ref_recs, self._lvl = ref_recs, 0
 
     def all_gather_device(self, out, inp):
@@ -136,8 +138,9 @@ class SimOwnComm(LocalComm):
         g = out.view(P, W)
         cnt = torch.searchsorted(self.ref_pos, segs[:S, :2].contiguous()).diff(dim=1)[:, 0]
         mine = segs[:S, 2][None, :] == torch.arange(P, device=segs.device)[:, None]
-        g[:, 2 : 2 + S] = mine * cnt[None, :]
-        g[:, :2] = self._head
+        H = GATHER_HDR
+        g[:, H : H + S] = mine * cnt[None, :]
+        g[:, :H] = self._head
         self.bytes_communicated += P * W * 8
 
 

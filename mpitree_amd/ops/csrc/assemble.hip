@@ -495,10 +495,13 @@ void launch_own_scatter(hipStream_t stream, const void* rows, int64_t k, int C, 
   MT_HIP_CHECK(hipGetLastError());
 }
 
-// gvec (int64, this rank's all-gather row): [0] local tree depth, [1] left to the
-// host (its free shared-buffer slots), [2 + s] nodes of segment s when this rank
-// owns it (0 otherwise). A segment's count is the difference of the exclusive
-// ranks at its ends (asm_rank_kernel: every position carries one).
+// gvec (int64, this rank's all-gather row): [0] local tree depth, [1] and [2] left
+// to the host (its free shared-buffer slots, the free bytes of its /dev/shm),
+// [kShmHdr + s] nodes of segment s when this rank owns it (0 otherwise). A
+// segment's count is the difference of the exclusive ranks at its ends
+// (asm_rank_kernel: every position carries one).
+constexpr int kShmHdr = 3;  // header words of a gathered row (shared_tree.GATHER_HDR)
+
 __global__ __launch_bounds__(256) void shm_seg_count_kernel(const int64_t* __restrict__ segs, int S,
                                                             int me, const int32_t* __restrict__ rank,
                                                             int64_t P, const int64_t* __restrict__ total,
@@ -513,7 +516,7 @@ __global__ __launch_bounds__(256) void shm_seg_count_kernel(const int64_t* __res
     const int r = rank[x];
     return r >= 0 ? r : ~r;
   };
-  gvec[2 + s] = (owner == me && lo < hi) ? excl(hi) - excl(lo) : 0;
+  gvec[kShmHdr + s] = (owner == me && lo < hi) ? excl(hi) - excl(lo) : 0;
 }
 
 constexpr int kShmMaxSegs = 4096;  // 2 per ownership unit (grow.hip kOwnMax = 2048)
@@ -574,7 +577,7 @@ __global__ __launch_bounds__(1024) void shm_seg_prefix_kernel(const int64_t* __r
       hi = segs[(int64_t)s * 3 + 1];
       owner = segs[(int64_t)s * 3 + 2];
       int64_t c = 0;
-      for (int r = 0; r < nranks; ++r) c += gall[(int64_t)r * W + 2 + s];
+      for (int r = 0; r < nranks; ++r) c += gall[(int64_t)r * W + kShmHdr + s];
       v = owner != me ? c : 0;
     }
     // inclusive block scan of v

@@ -906,7 +906,8 @@ class DeviceGrower:
             fault_point(comm, "exchange")  # (after the switch: peers wait in the exchange)
             t1 = time.perf_counter()
             b0 = comm.bytes_communicated
-            if getattr(self, "_owned", None) is not None:
+            owned = getattr(self, "_owned", None)
+            if owned is not None:
                 # ranks of one node: each writes its own nodes into a shared host
                 # buffer (no node exchange); otherwise one all-gather of the nodes
                 pool = shared_tree.pool_for(comm, hip)
@@ -937,6 +938,10 @@ class DeviceGrower:
             table = edges if isinstance(edges, np.ndarray) else edges.padded_edges()
         ta = be.assemble_positions(table, int(p.criterion), y_exp, d_edges=d_edges,
                                    shared=shared)
+        if ta is None:  # (/dev/shm too small for the tree, on every rank alike)
+            self.stats["assembly"] = "exchange (/dev/shm short)"
+            self._exchange_owned(owned)
+            ta = be.assemble_positions(table, int(p.criterion), y_exp, d_edges=d_edges)
         self.timings["assemble"] = time.perf_counter() - t0
         if self.ckpt is not None:
             self.stats["checkpoint_levels_saved"] = self.ckpt.saved_levels

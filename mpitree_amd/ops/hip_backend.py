@@ -690,22 +690,25 @@ class HipBackend:
         self.pos_rec = self.pos_st = None
         return TreeArrays.from_packed(nd[:nbytes], N, C, bool(self.reg), max_depth=max_depth)
 
-    def _assemble_shared(self, sh, emit, total, rank_ptr: int, bpn: int) -> TreeArrays:
+    def _assemble_shared(self, sh, emit, total, rank_ptr: int, bpn: int):
         """Each rank of one node writes its own nodes (rank 0 also the replicated
-        prefix) into one shared host buffer (``parallel/shared_tree.py``)."""
-        from ..parallel.shared_tree import HEADER
+        prefix) into one shared host buffer (``parallel/shared_tree.py``). None
+        (on every rank alike) when the node's /dev/shm cannot hold a new buffer
+        for the tree: the caller falls back to the node exchange."""
+        from ..parallel.shared_tree import GATHER_HDR, HEADER, shm_free_bytes
 
         comm, pool, segs, S = sh["comm"], sh["pool"], sh["segs"], int(sh["S"])
         hip = self.hip
         s = _stream()
         Pn, me = int(comm.world_size), int(comm.rank)
-        W = 2 + int(segs.shape[0])
-        g = _workspace(self.device, "shm.seg", (W * (Pn + 1) + 4 * int(segs.shape[0])) * 8)
-        g = g[: (W * (Pn + 1) + 4 * int(segs.shape[0])) * 8].view(torch.int64)
+        W = GATHER_HDR + int(segs.shape[0])
+        nw = W * (Pn + 1) + 4 * int(segs.shape[0])
+        g = _workspace(self.device, "shm.seg", nw * 8)[: nw * 8].view(torch.int64)
         gvec, gall, tab = g[:W], g[W : W * (Pn + 1)], g[W * (Pn + 1) :]
         hip.shm_seg_count(s, segs.data_ptr(), S, me, rank_ptr, self.P, total.data_ptr(),
                           gvec.data_ptr())
         gvec[1].fill_(pool.free_mask())
+        gvec[2].fill_(shm_free_bytes())
         comm.all_gather_seg_counts(gall, gvec, segs, S)
         hip.shm_seg_prefix(s, gall.data_ptr(), Pn, W, segs.data_ptr(), S, me, total.data_ptr(),
                            tab.data_ptr())
@@ -713,18 +716,22 @@ class HipBackend:
         slot = pool.take_next()  # (agreed last fit: emit before the host wait)
         if slot is not None:
             emit(slot.dev + HEADER, (slot.nbytes - HEADER) // bpn, **kw)
-        h = _pinned_copy(torch.cat([total, gall.view(Pn, W)[:, 1]]), "shm.total")
+        gv = gall.view(Pn, W)
+        h = _pinned_copy(torch.cat([total, gv[:, 1], gv[:, 2]]), "shm.total")
         torch.cuda.current_stream(self.device).synchronize()
         self._check_finisher_watch()
         N, max_depth = int(h[0]), int(h[1])
         nbytes = N * bpn
         masks = [int(v) for v in h[2 : 2 + Pn]]
+        free = [int(v) for v in h[2 + Pn : 2 + 2 * Pn]]
         if slot is None or nbytes > slot.nbytes - HEADER:  # (every rank sees the same N)
-            slot = pool.choose(masks, nbytes)
+            slot = pool.choose(masks, nbytes, shm_free=free)
+            if slot is None:
+                return None
             emit(slot.dev + HEADER, 0, **kw)
             torch.cuda.current_stream(self.device).synchronize()
         pool.barrier(slot)
-        pool.plan_next(masks, slot, nbytes)
+        pool.plan_next(masks, slot, nbytes, shm_free=free)
         self.pos_rec = self.pos_st = None
         return TreeArrays.from_packed(slot.nd[HEADER : HEADER + nbytes], N, self.C, bool(self.reg),
                                       max_depth=max_depth)

@@ -42,10 +42,16 @@ import numpy as np
 
 from .failure import ABORT, check_abort
 
-__all__ = ["ShmTreePool", "pool_for", "HEADER"]
+__all__ = ["ShmTreePool", "pool_for", "HEADER", "GATHER_HDR", "shm_free_bytes"]
 
 HEADER = 4096  # per-rank flag words (64 B apart), then the packed tree columns
+GATHER_HDR = 3  # gathered row: {depth, free-slot mask, /dev/shm free bytes}, counts
 MAX_SLOTS = 8
+SHM_MARGIN = 64 << 20  # /dev/shm left free when a new slot is created
+
+
+def _margin() -> int:
+    return int(float(os.environ.get("MPITREE_SHM_MARGIN_MB", SHM_MARGIN >> 20)) * (1 << 20))
 POLL_TIMEOUT_S = float(os.environ.get("MPITREE_POLL_TIMEOUT", "120"))
 
 
@@ -59,6 +65,16 @@ def _host_key() -> int:
         pass
     h = hashlib.sha1((socket.gethostname() + "|" + boot).encode()).digest()
     return int.from_bytes(h[:7], "little")
+
+
+def shm_free_bytes() -> int:
+    """Bytes a new /dev/shm mapping can still take (a container's /dev/shm is
+    often a 64 MB tmpfs; touching a page past it is a SIGBUS, not an error)."""
+    try:
+        st = os.statvfs("/dev/shm")
+    except OSError:
+        return 0
+    return int(st.f_bavail) * int(st.f_frsize)
 
 
 class _Slot:
@@ -129,10 +145,14 @@ class ShmTreePool:
                 m |= 1 << i
         return m
 
-    def choose(self, masks, need: int, exclude: _Slot | None = None) -> _Slot:
+    def choose(self, masks, need: int, exclude: _Slot | None = None,
+               shm_free=None) -> _Slot | None:
         """The slot every rank uses for ``need`` bytes of tree: the smallest slot
         free on every rank that holds it, else a new one (a free too-small slot is
-        replaced). ``masks``: every rank's :meth:`free_mask` (from the all-gather)."""
+        replaced). ``masks``: every rank's :meth:`free_mask` (from the all-gather);
+        ``shm_free``: every rank's :func:`shm_free_bytes` from the same gather --
+        None (on every rank alike) when a new slot would not fit beside
+        ``SHM_MARGIN`` in the smallest of them."""
         both = ~0
         for m in masks:
             both &= int(m)
@@ -146,6 +166,9 @@ class ShmTreePool:
                     best = i
         if best is not None:
             return self.slots[best]
+        size = HEADER + max(1 << 20, int(need * 1.25) + 4095) // 4096 * 4096
+        if shm_free is not None and size + _margin() > min(int(v) for v in shm_free):
+            return None
         idx = next((i for i in range(MAX_SLOTS) if i not in self.slots), None)
         if idx is None:  # replace the largest slot free everywhere (none: grow the pool)
             cand = [i for i in self.slots if (both >> i) & 1]
@@ -155,7 +178,6 @@ class ShmTreePool:
                 idx = max(cand, key=lambda i: self.slots[i].nbytes)
                 self.slots.pop(idx).close()
         self.gen += 1
-        size = HEADER + max(1 << 20, int(need * 1.25) + 4095) // 4096 * 4096
         name = f"/mpitree-{self.uid:x}-{idx}-{self.gen}"
         if idx >= 62:
             raise RuntimeError("shared-host assembly: more than 62 trees of this "
@@ -172,10 +194,11 @@ class ShmTreePool:
         sl, self.next = getattr(self, "next", None), None
         return sl
 
-    def plan_next(self, masks, current: _Slot, need: int) -> None:
+    def plan_next(self, masks, current: _Slot, need: int, shm_free=None) -> None:
         """Agree on the next fit's slot now (the same masks on every rank), sized
-        for a tree like this one (a larger one is re-emitted after the wait)."""
-        self.next = self.choose(masks, need, exclude=current)
+        for a tree like this one (a larger one is re-emitted after the wait; None:
+        /dev/shm is short, the next fit chooses after its wait)."""
+        self.next = self.choose(masks, need, exclude=current, shm_free=shm_free)
 
     def barrier(self, slot: _Slot) -> None:
         """Every rank has written its nodes into ``slot`` (flag words in its header;

@@ -131,6 +131,8 @@ def _fit_rank_gpu_large(rank, world, regression, strategy="auto"):
     # "subtree": the replicated prefix levels forced feature-parallel (the
     # heuristic keeps these small shapes replicated, as "auto" shows)
     os.environ["MPITREE_OWN_FP_PREFIX"] = "1" if strategy == "subtree" else "0"
+    if strategy == "subtree":  # /dev/shm "full" on every rank: the node exchange
+        os.environ["MPITREE_SHM_MARGIN_MB"] = str(1 << 40)
     if regression:
         X, y = make_regression(200_000, 16, levels=64, seed=5, device=dev)
         cls = ParallelDecisionTreeRegressor
@@ -195,8 +197,10 @@ def test_gpu_ranks_equal_single_gpu_at_scale(regression, strategy, world):
                 assert o[f"xbytes{it}"][0] > 0
                 assert o[f"own_rows{it}"][0] > 0  # every rank owns units
                 # ranks of one node: each wrote its own nodes into the shared tree
-                # (the first fit's tree is still held: the repeat takes another slot)
-                assert str(o[f"asm{it}"][0]) == "shared-host"
+                # (the first fit's tree is still held: the repeat takes another
+                # slot); "subtree" runs with /dev/shm too short for any slot
+                assert str(o[f"asm{it}"][0]) == ("exchange (/dev/shm short)"
+                                                 if strategy == "subtree" else "shared-host")
             else:
                 assert o[f"bytes{it}"].sum() > 0  # per-level collectives ran
             for k in FIELDS + ("threshold", "impurity"):

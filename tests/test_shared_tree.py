@@ -56,6 +56,21 @@ def test_next_slot_is_agreed_ahead_and_excludes_the_current():
         sl.close()
 
 
+def test_short_dev_shm_refuses_a_new_slot_but_reuses_one():
+    pool = _pool()
+    a = pool.choose([0, 0], 1 << 20)
+    small = [st.SHM_MARGIN, 10 * st.SHM_MARGIN]  # one rank's /dev/shm is nearly full
+    # a new slot would not fit beside the margin on that rank: every rank falls back
+    assert pool.choose([0, 0], 1 << 20, shm_free=small) is None
+    # an existing free slot costs no /dev/shm: it is still chosen
+    assert pool.choose([1, 1], 1 << 20, shm_free=small) is a
+    pool.plan_next([1, 1], a, 1 << 20, shm_free=small)
+    assert pool.take_next() is None
+    assert st.shm_free_bytes() >= 0
+    for sl in list(pool.slots.values()):
+        sl.close()
+
+
 def _rank_main(rank, uid, q):
     pool = st.ShmTreePool(_Comm(rank, 2), _FakeHip(), uid)
     slot = pool.choose([0, 0], 1 << 16)  # same name on both ranks
