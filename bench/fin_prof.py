@@ -36,6 +36,10 @@ print(f"blocks={len(P)} jobs={len(keep['counts'])} job rows: max={keep['counts']
       f"mean={keep['counts'].mean():.0f}")
 print(f"wall us: max={wall.max():.0f} mean={wall.mean():.0f} p50={np.median(wall):.0f} "
       f"start max={start.max():.1f}")
+end = (P[:, 1] - P[:, 0].min()) / 100.0
+q = np.percentile(end, [10, 50, 90, 99])
+print(f"block end us: p10={q[0]:.0f} p50={q[1]:.0f} p90={q[2]:.0f} p99={q[3]:.0f} "
+      f"max={end.max():.0f}; idle share of the span {(end.max() - end).mean() / end.max():.1%}")
 print(f"nodes/block: max={P[:, 2].max()} mean={P[:, 2].mean():.1f} total={P[:, 2].sum()}; "
       f"rows/block: max={P[:, 3].max()} mean={P[:, 3].mean():.0f} total={P[:, 3].sum()}")
 cyc = P[:, 4:9].sum(0)

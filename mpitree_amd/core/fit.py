@@ -212,10 +212,12 @@ def _exact_device_ok(n, F, C, regression, P=1, free_bytes=None) -> bool:
     return exact_fits_memory(n, F, C, regression, P, free_bytes)
 
 
-def _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t_bin, t_start, F, regression):
+def _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t_bin, t_start, F, regression,
+                      checkpoint=None):
     """Every unique value a threshold on continuous features, classification or
     regression: the device-driven presorted-list engine; feature-parallel over
-    the ranks of a multi-GPU fit (``ops/exact_grower.py``)."""
+    the ranks of a multi-GPU fit (``ops/exact_grower.py``). ``checkpoint``:
+    level resume of the list engine (the signature covers the raw features)."""
     from ..ops.exact_grower import ExactGrower
 
     timings["bin"] = time.perf_counter() - t_bin
@@ -232,7 +234,12 @@ def _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t_bin, t_start, 
     # ranks every rank grows the same tree on all features (replicated, as the
     # reference's ranks do above their split level)
     fp = comm.world_size > 1 and F >= comm.world_size
-    g = ExactGrower(params, comm if fp else None)
+    if checkpoint is not None and comm.world_size > 1 and not fp:
+        logger.warning("replicated exact fits (fewer features than ranks) keep no level "
+                       "checkpoint: fitting without one")
+        checkpoint = None
+    ckpt = _level_checkpoint(checkpoint, Xd, yd, params, C)
+    g = ExactGrower(params, comm if fp else None, checkpoint=ckpt)
     with roctx_range("mpitree.grow"):
         ta = g.fit(Xd, yd, root, C, crit, prep.y_exp, timings=timings)
     stats = dict(g.stats)
@@ -355,14 +362,11 @@ def fit_tree(
         if max_bins is None and g_mapper is None and needs_exact(mapper):
             P_fp = comm.world_size if comm.world_size > 1 and F >= comm.world_size else 1
             if _exact_device_ok(n, F, C, regression, P_fp):
-                if checkpoint is not None:  # the same tree, just no mid-fit state
-                    logger.warning("the exact-threshold GPU engine keeps no level "
-                                   "checkpoint: fitting without one")
                 # (the bin pass's flags -- non-finite input -- are read after the fit,
                 # so the host enqueues the setup without waiting for them)
                 try:
                     res = _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t0,
-                                            t_start, F, regression)
+                                            t_start, F, regression, checkpoint)
                 except Exception:
                     # non-finite input (the bin pass's flags) explains any failure of
                     # the engine on it: that ValueError takes precedence

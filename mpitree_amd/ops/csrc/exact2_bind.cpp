@@ -29,6 +29,7 @@ struct XeCtx {
   XePlanArgs p{};
   uint32_t seq = 1;  // fit sequence number: look-back status tags differ per (fit, level)
   int32_t* sitem = nullptr;  // two-class chunk totals counted by the partition (or null)
+  int first = 0;  // first level this process runs (a resumed fit: > 0)
 
   XeArgs args(int lvl) const {
     XeArgs x = a;
@@ -40,7 +41,9 @@ struct XeCtx {
     x.DY = Yb[c ^ 1];
     x.sitem = sitem;
     x.nctl = sitem ? L[c ^ 1].ctl : nullptr;
-    x.tot_ready = sitem != nullptr && lvl > 0;
+    // (the level a resumed fit starts at recounts its chunk totals: the saved
+    // state holds no partition-counted ones)
+    x.tot_ready = sitem != nullptr && lvl > first;
     return x;
   }
 };
@@ -139,6 +142,7 @@ void bind_exact2(py::module_& m) {
         return c;
       }))
       .def("begin", [](XeCtx& c, int64_t seq) { c.seq = (uint32_t)seq; })
+      .def("resume_at", [](XeCtx& c, int lvl) { c.first = lvl; })
       .def("init", [](XeCtx& c, uintptr_t s, uintptr_t root) {
         xe_init(stream_of(s), c.L[0], c.a.n, c.a.C > 0 ? c.a.C : 2, ptr<int64_t>(root),
                 c.p.job_count);

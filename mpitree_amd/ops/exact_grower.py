@@ -144,11 +144,58 @@ def _owners(J: int, P: int, device) -> torch.Tensor:
 class ExactGrower:
     """One exact-threshold fit on the current GPU (optionally feature-parallel)."""
 
-    def __init__(self, params, comm=None):
+    def __init__(self, params, comm=None, checkpoint=None):
         self.p = params
         self.comm = comm
+        self.ckpt = checkpoint  # utils/level_checkpoint.LevelCheckpoint (or None)
         self.timings: dict = {}
         self.stats: dict = {}
+
+    # -------------------------------------------------------- checkpoint
+    def _ckpt_save(self, lvl, ws, E, Y, be, pos_thr, rank, P):
+        """After level ``lvl``'s partition: one sync, then the loop's device
+        state -- both list buffers (this rank's features), the next frontier,
+        the position space and the finisher jobs (nothing once the next
+        frontier is empty: the loop is about to end)."""
+        torch.cuda.synchronize(be.device)
+        nxt = ws["L"][(lvl + 1) % 2]
+        if int(nxt["ctl"][0]) == 0:
+            return
+        jc = int(ws["job_count"][0])
+        arrs = {"set_" + k: v.cpu().numpy() for k, v in nxt.items()}
+        for i in range(2):
+            arrs[f"E{i}"] = E[i].cpu().numpy()
+            if Y[i] is not None:
+                arrs[f"Y{i}"] = Y[i].cpu().numpy()
+        arrs["pos_rec"] = be.pos_rec.cpu().numpy()
+        arrs["pos_st"] = be.pos_st.cpu().numpy()
+        arrs["pos_thr"] = pos_thr.cpu().numpy()
+        arrs["jobs"] = ws["jobs"][: max(jc, 1)].cpu().numpy()
+        arrs["job_count"] = np.array([jc], np.int64)
+        self.ckpt.save_device(lvl, arrs, rank, P)
+
+    def _ckpt_restore(self, st, ws, E, Y, be, pos_thr) -> int:
+        """Load a saved level's state; returns that level."""
+        lvl = int(st["level"][0])
+        dev = be.device
+
+        def put(dst, a):
+            dst.copy_(torch.from_numpy(np.ascontiguousarray(a)).to(dev))
+
+        for k, v in ws["L"][(lvl + 1) % 2].items():
+            put(v, st["set_" + k])
+        for i in range(2):
+            put(E[i], st[f"E{i}"])
+            if Y[i] is not None:
+                put(Y[i], st[f"Y{i}"])
+        put(be.pos_rec, st["pos_rec"])
+        put(be.pos_st, st["pos_st"])
+        put(pos_thr, st["pos_thr"])
+        jc = int(st["job_count"][0])
+        if jc:
+            put(ws["jobs"][:jc], st["jobs"][:jc])
+        ws["job_count"].fill_(jc)
+        return lvl
 
     # ------------------------------------------------------------- setup
     def _setup(self, Xd, F, f_lo, F_loc, y32, yfix, reg):
@@ -349,7 +396,19 @@ class ExactGrower:
             job_count=ptr["job_count"], max_depth=md, mss=mss, fr=fr), lp[0], lp[1])
         ws["root"].copy_(torch.from_numpy(np.ascontiguousarray(root_stats, np.int64)))
         ws["tick"].zero_()  # work tickets + the look-back watchdog
-        ctx.init(s(), ws["root"].data_ptr())
+        ck = self.ckpt
+        state = None
+        if ck is not None:
+            state = ck.load_device(rank, P, (lambda a: comm._all_gather(a)) if P > 1 else None)
+        first_lvl = 0  # levels before it ran in an earlier process (resume)
+        if state is not None:
+            first_lvl = self._ckpt_restore(state, ws, E, Y, be, pos_thr) + 1
+            ctx.resume_at(first_lvl)
+            self.stats["resumed_from_level"] = first_lvl - 1
+            del state
+        else:
+            ctx.init(s(), ws["root"].data_ptr())
+        ck_every = max(1, int(os.environ.get("MPITREE_CKPT_EVERY", "1")))
         self._keep = (ctx, E, Y, ranks)
 
         # ---- level loop: enqueue only; a lagged host-mapped slot tells the end
@@ -358,7 +417,7 @@ class ExactGrower:
         ctx.begin(_FIT_SEQ[0] + 1)
         tag0 = _FIT_SEQ[0] << 12
         t1 = time.perf_counter()
-        lvl, done_at = 0, None
+        lvl, done_at = first_lvl, None
         comm_bytes = []
         while True:
             if P > 1:  # failure containment: a failed peer / injected fault
@@ -388,6 +447,8 @@ class ExactGrower:
             _step(dev, "flag")
             ctx.partition(s(), lvl, ib, kb)
             _step(dev, "partition")
+            if ck is not None and (lvl - first_lvl + 1) % ck_every == 0:
+                self._ckpt_save(lvl, ws, E, Y, be, pos_thr, rank, P)
             if _DEBUG_SYNC:  # (MPITREE_EXACT_SYNC=1: sync + report every level)
                 torch.cuda.synchronize(dev)
                 ni = int(L[lvl % 2]["ctl"][1])
@@ -397,7 +458,7 @@ class ExactGrower:
                       f"items {ni}, partition status tags {(st >> np.uint64(34)).tolist()} "
                       f"states {((st >> np.uint64(32)) & np.uint64(3)).tolist()}", flush=True)
             lvl += 1
-            if lvl >= 2:
+            if lvl - 2 >= first_lvl:
                 _wait_slot(hctl, (lvl - 2) % 64, tag0 + ((lvl - 2) % 4096) + 1)
                 if int(hctl[(lvl - 2) % 64, 0]) == 0:
                     done_at = lvl - 2
@@ -431,6 +492,9 @@ class ExactGrower:
         if timings is not None:
             timings["assemble"] = time.perf_counter() - t3
         self._keep = None
+        if ck is not None:
+            self.stats["checkpoint_levels_saved"] = ck.saved_levels
+            ck.clear()
         return ta
 
     # --------------------------------------------------------- finisher

@@ -31,6 +31,13 @@ k-th level. Multi-GPU fits save one file per rank in two generations (levels
 alternate between them); on resume the ranks all-gather which levels they
 hold and restart from the newest level every rank has, so a crash between
 two ranks' writes never mixes levels.
+
+The exact-threshold list engine (``ops/exact_grower.py``, continuous features)
+resumes the same way: after a level's partition it saves both presorted list
+buffers of the rank's features (and the regression targets riding with them),
+the next frontier, the position space with the resolved thresholds and the
+finisher jobs; the resumed level recounts its chunk totals. Its signature
+digests the raw feature values.
 """
 
 from __future__ import annotations

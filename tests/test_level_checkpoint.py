@@ -89,13 +89,42 @@ def test_gpu_resume_equals_device_loop(tmp_path, regression):
     np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy())
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("regression,stop", [(False, 3), (False, 11), (True, 5)])
+def test_gpu_exact_resume_equals_uninterrupted(tmp_path, regression, stop):
+    """The exact (continuous-threshold) list engine resumes too: interrupted after
+    a level -- before and after the first finisher jobs -- and resumed, it
+    restores both list buffers, the frontier, the position space and the jobs,
+    and builds the uninterrupted tree."""
+    from mpitree_amd.utils.datasets import make_classification, make_regression
+
+    if regression:
+        X, y = make_regression(60_000, 10, levels=None, seed=4, device="cuda")
+        make = lambda: DecisionTreeRegressor(device="cuda")  # noqa: E731
+    else:
+        X, y = make_classification(80_000, 10, levels=None, seed=4, device="cuda")
+        make = lambda: DecisionTreeClassifier(device="cuda")  # noqa: E731
+    ref = make().fit(X, y)
+    assert ref.fit_stats_["engine"] == "hip-exact"
+    res = _interrupted_then_resumed(make, X, y, tmp_path / "x.npz", stop)
+    assert res.fit_stats_["engine"] == "hip-exact"
+    assert res.fit_stats_["checkpoint_levels_saved"] >= 1
+    assert res._arrays.equal(ref._arrays, check_impurity=False)
+    np.testing.assert_array_equal(res.tree_arrays_.threshold, ref.tree_arrays_.threshold)
+
+
 def _ckpt_rank(rank, world, path, strategy, stop):
     import torch
 
     from mpitree_amd import ParallelDecisionTreeClassifier
     from mpitree_amd.utils.datasets import make_classification
 
-    X, y = make_classification(200_000, 16, seed=9, device=torch.device("cuda", 0))
+    dev = torch.device("cuda", 0)
+    if strategy == "exact":  # continuous features: the feature-parallel list engine
+        X, y = make_classification(80_000, 10, levels=None, seed=9, device=dev)
+        strategy = "auto"
+    else:
+        X, y = make_classification(200_000, 16, seed=9, device=dev)
     make = lambda: ParallelDecisionTreeClassifier(strategy=strategy, device="cuda")  # noqa: E731
     ck = LevelCheckpoint(path)
     ck.fail_after_level = stop
@@ -113,11 +142,11 @@ def _ckpt_rank(rank, world, path, strategy, stop):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("strategy", ["data", "feature"])
+@pytest.mark.parametrize("strategy", ["data", "feature", "exact"])
 def test_gpu_ranks_resume(tmp_path, strategy):
-    """Two ranks (gloo, sharing one GPU): per-rank device-loop checkpoints, the
-    ranks agree on the level to resume from, and the resumed trees equal the
-    single-GPU tree."""
+    """Two ranks (gloo, sharing one GPU): per-rank device-loop (or exact list
+    engine) checkpoints, the ranks agree on the level to resume from, and the
+    resumed trees equal the single-GPU tree."""
     import torch
 
     from mpitree_amd.utils.datasets import make_classification
@@ -125,11 +154,15 @@ def test_gpu_ranks_resume(tmp_path, strategy):
 
     path = str(tmp_path / "d.npz")
     outs = run_ranks(_ckpt_rank, 2, path, strategy, 2, start_method="spawn")
-    X, y = make_classification(200_000, 16, seed=9, device=torch.device("cuda", 0))
+    dev = torch.device("cuda", 0)
+    if strategy == "exact":
+        X, y = make_classification(80_000, 10, levels=None, seed=9, device=dev)
+    else:
+        X, y = make_classification(200_000, 16, seed=9, device=dev)
     ref = DecisionTreeClassifier(device="cuda").fit(X, y).tree_arrays_
     for o in outs:
         assert int(o["raised"][0]) == 1 and int(o["resumed"][0]) == 2
-        assert str(o["engine"][0]) == "hip-device-loop"
+        assert str(o["engine"][0]) == ("hip-exact" if strategy == "exact" else "hip-device-loop")
         assert int(o["left"][0]) == 0  # every rank's files removed after the fit
         np.testing.assert_array_equal(o["feature"], ref.feature)
         np.testing.assert_array_equal(o["threshold"], ref.threshold)
