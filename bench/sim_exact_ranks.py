@@ -90,7 +90,7 @@ class Recorder:
             if rec.fm is None:  # (one GPU: the local-codes kernel wrote codes_rm itself)
                 loc = next(iter(rec.eg._WS["loc"].values()))
                 rec.fm = loc["fm"].clone()
-                J = int(a[10])  # xe_fix(s, E0, E1, X, x64, F, n, f_lo, F_loc, jobs, J, ...)
+                J = int(a[9])  # xe_fix(s, E0, E1, X, x64, F, n, f_lo, F_loc, jobs, J, JW, ...)
                 rec.jobs = rec._ws()["jobs"][:J].clone()
             dev = rec.fm.device
             rows = hb._workspace(dev, "pos_rec", 0)
@@ -197,12 +197,34 @@ def build_reference(fit, dev, P_list, C):
     return res, dict(rec=R.rec, flag=R.flag, fm=R.fm, resolved=resolved, others=others)
 
 
+def _diff(a, b) -> dict:
+    """Which columns of two trees differ, and where first (diagnostics)."""
+    out = {"nodes": [int(a.node_count), int(b.node_count)]}
+    for k in ("feature", "threshold_bin", "left", "right", "depth", "n_samples", "threshold",
+              "count", "value", "impurity"):
+        x, y = getattr(a, k), getattr(b, k)
+        if x is None or y is None:
+            continue
+        if x.shape != y.shape:
+            out[k] = f"shape {x.shape} vs {y.shape}"
+            continue
+        ne = ~((x == y) | (np.isnan(x) & np.isnan(y)) if x.dtype.kind == "f" else (x == y))
+        if ne.ndim > 1:
+            ne = ne.any(axis=tuple(range(1, ne.ndim)))
+        if ne.any():
+            i = int(np.argmax(ne))
+            out[k] = dict(n=int(ne.sum()), first=i, got=str(x[i]), want=str(y[i]),
+                          depth=int(b.depth[i]), n_samples=int(b.n_samples[i]))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--features", type=int, default=64)
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--only-rank", type=int, default=None)
     a = ap.parse_args()
     from mpitree_amd.core.fit import fit_tree
 
@@ -222,7 +244,7 @@ def main():
     assert ref.engine == "hip-exact", ref.engine
     for P in P_list:
         per_rank = []
-        for r in range(P):
+        for r in range(P) if a.only_rank is None or P == 1 else [a.only_rank]:
             if P > 1:
                 data_r = dict(data, others=data["others"])
                 data_r["others"] = {r: data["others"][(P, r)]}
@@ -238,7 +260,10 @@ def main():
                     ph.append({k: v * 1e3 for k, v in res.timings.items()
                                if k in ("exact_setup", "levels", "finisher", "assemble")})
                 st = res.stats
-                assert res.arrays.equal(ref.arrays), f"P={P} rank {r}: tree differs"
+                if not res.arrays.equal(ref.arrays):
+                    print(json.dumps(dict(P=P, rank=r, diff=_diff(res.arrays, ref.arrays))),
+                          flush=True)
+                    raise AssertionError(f"P={P} rank {r}: tree differs")
             per_rank.append(dict(ms=float(np.median(times)),
                                  phases={k: round(float(np.median([q[k] for q in ph])), 2)
                                          for k in ph[0]},

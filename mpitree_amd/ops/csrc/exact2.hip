@@ -766,22 +766,29 @@ __device__ __forceinline__ void xe_scan_wave_c2(const XeArgs& a, const XeLists& 
   }
 }
 
+// Pass-2 pairs per wave step: one chunk item's features (at most a wave)
+__host__ __device__ inline int xe_p2_pairs(int F_loc) { return F_loc < kWave ? F_loc : kWave; }
+
 // One wave per (chunk item, feature) pair, grid-stride over the level's pairs.
 template <int kPass>
 __global__ __launch_bounds__(kXeThreads) void xe_scan_c2_kernel(XeArgs a, XeLists L) {
   const int64_t total = (int64_t)L.ctl[1] * a.F_loc;
   const int64_t waves = (int64_t)gridDim.x * kXeWaves;
   if constexpr (kPass == 2) {
-    // 64 pairs per wave step: each lane checks one chunk's fp32 minimum against
-    // its node's threshold (lane-parallel empty records for the rest), then the
-    // wave scans the few candidate chunks one by one
+    // xe_p2_pairs(F_loc) pairs per wave step: each lane checks one chunk's fp32
+    // minimum against its node's threshold (lane-parallel empty records for the
+    // rest), then the wave scans the few candidate chunks one by one. Fewer than
+    // 64 pairs when a chunk item has fewer features (feature-parallel ranks):
+    // 64 pairs would span several consecutive chunks of one node -- the chunks
+    // around its best threshold, candidates together -- and serialise them.
     const int lane = lane_id();
-    for (int64_t b = ((int64_t)blockIdx.x * kXeWaves + (threadIdx.x >> 6)) * kWave; b < total;
-         b += waves * kWave) {
+    const int pw = xe_p2_pairs(a.F_loc);
+    for (int64_t b = ((int64_t)blockIdx.x * kXeWaves + (threadIdx.x >> 6)) * pw; b < total;
+         b += waves * pw) {
       const int64_t w = b + lane;
       bool cand = false;
       float th = 0.0f;
-      if (w < total) {
+      if (lane < pw && w < total) {
         const int64_t it = w / a.F_loc;
         th = a.gthr[L.items[it * 4 + 0]];
         cand = xe_fval(a.cmin[w]) <= th;  // (an empty chunk's key decodes to NaN)
@@ -1350,32 +1357,133 @@ __device__ __forceinline__ int xe_part_batch(int F_loc) {
   return kXePartBatch;
 }
 
-template <bool kLdsFlags, bool kReg>
-__global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a, XeLists cur) {
+// The n-bit row-direction flags -> this workgroup's LDS (every thread returns
+// after the barrier)
+__device__ __forceinline__ void xe_flags_to_lds(const XeArgs& a, uint32_t* s_flag) {
+  const int nw = (int)((a.n + 31) >> 5);
+  // 16-byte loads, kU in flight per lane before the LDS stores: the copy is one
+  // round of L2 latency instead of one per 4 KB
+  constexpr int kU = 8;
+  const int nq = nw >> 2;
+  const uint4* src = reinterpret_cast<const uint4*>(a.flag);
+  uint4* dst = reinterpret_cast<uint4*>(s_flag);
+  // full rounds without guards (guarded loads / stores were issued one at a
+  // time: a load, its wait, its LDS store), then the remainder
+  const int bd = (int)blockDim.x;
+  int i0 = threadIdx.x;
+  for (; i0 + (kU - 1) * bd < nq; i0 += bd * kU) {
+    uint4 v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) v[u] = src[i0 + u * bd];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) dst[i0 + u * bd] = v[u];
+  }
+  for (int i = i0; i < nq; i += bd) dst[i] = src[i];
+  for (int i = (nq << 2) + threadIdx.x; i < nw; i += blockDim.x) s_flag[i] = a.flag[i];
+  __syncthreads();
+}
+
+// Counted partition, pass 1 (the default; MPITREE_EXACT_PART_COUNTED=0 keeps the
+// single-pass look-back partition): every wave unit's left rows -> pstat[u][f].
+// The single-pass kernel claimed its units through one ticket counter (a device
+// atomic per 1-16 units, serialised on one address) and waited in look-back
+// chains as long at 8 lists as at 64 (n / 1024 units per list at the root): a
+// feature-parallel rank with 8 lists spent 114 us a level on 8M entries
+// (profiles/r5/exact_p8_rank_kernels.txt). Counting first reads the entries
+// twice but leaves no wait and no shared counter anywhere.
+template <bool kLdsFlags>
+__global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_count_kernel(XeArgs a, XeLists cur) {
   extern __shared__ uint32_t s_flag[];
-  const int nw = kLdsFlags ? (int)((a.n + 31) >> 5) : 0;
-  if constexpr (kLdsFlags) {
-    // 16-byte loads, kU in flight per lane before the LDS stores: the copy is one
-    // round of L2 latency instead of one per 4 KB
-    constexpr int kU = 8;
-    const int nq = nw >> 2;
-    const uint4* src = reinterpret_cast<const uint4*>(a.flag);
-    uint4* dst = reinterpret_cast<uint4*>(s_flag);
-    // full rounds without guards (guarded loads / stores were issued one at a
-    // time: a load, its wait, its LDS store), then the remainder
-    const int bd = (int)blockDim.x;
-    int i0 = threadIdx.x;
-    for (; i0 + (kU - 1) * bd < nq; i0 += bd * kU) {
-      uint4 v[kU];
+  if constexpr (kLdsFlags) xe_flags_to_lds(a, s_flag);
+  const uint32_t* fl = kLdsFlags ? s_flag : a.flag;
+  const int lane = lane_id();
+  const int64_t total = (int64_t)cur.ctl[3] * kXeSubPerChunk * a.F_loc;
+  for (int64_t w = (int64_t)blockIdx.x * kXePartWaves + (threadIdx.x >> 6); w < total;
+       w += (int64_t)gridDim.x * kXePartWaves) {
+    const int f = (int)(w % a.F_loc);
+    const int64_t u = w / a.F_loc;
+    const int64_t it = u / kXeSubPerChunk, k = u % kXeSubPerChunk;
+    const int64_t c0 = a.pitems[it * 4 + 2] + k * kXeSub;
+    const int64_t cn = a.pitems[it * 4 + 3] - k * kXeSub;  // may be <= 0
+    const uint32_t* Ef = a.E + (int64_t)f * a.n;
+    uint32_t e[kXePartPer];
 #pragma unroll
-      for (int u = 0; u < kU; ++u) v[u] = src[i0 + u * bd];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) dst[i0 + u * bd] = v[u];
+    for (int q = 0; q < kXePartPer; ++q) {
+      const int64_t i = (int64_t)q * kWave + lane;
+      e[q] = i < cn ? Ef[c0 + i] : 0xFFFFFFFFu;
     }
-    for (int i = i0; i < nq; i += bd) dst[i] = src[i];
-    for (int i = (nq << 2) + threadIdx.x; i < nw; i += blockDim.x) s_flag[i] = a.flag[i];
+    uint32_t T = 0;
+#pragma unroll
+    for (int q = 0; q < kXePartPer; ++q) {
+      const int64_t i = (int64_t)q * kWave + lane;
+      const uint32_t r = xe_row(e[q]);
+      T += (uint32_t)__popcll(__ballot(i < cn && ((fl[r >> 5] >> (r & 31)) & 1u)));
+    }
+    if (lane == 0) a.pstat[w] = T;
+  }
+}
+
+// Counted partition, pass 2: per list, the exclusive prefix of the units' left
+// rows within each split segment (a unit whose chunk starts its segment resets
+// the sum), in place. One 1024-thread workgroup per list, 1024 units a round.
+__global__ __launch_bounds__(1024) void xe_part_prefix_kernel(XeArgs a, XeLists cur) {
+  __shared__ uint64_t s_tail[1024 / kWave];
+  __shared__ int s_head[1024 / kWave];
+  __shared__ uint64_t s_carry;
+  const int f = blockIdx.x;
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  const int64_t U = (int64_t)cur.ctl[3] * kXeSubPerChunk;
+  if (tid == 0) s_carry = 0;
+  __syncthreads();
+  for (int64_t b0 = 0; b0 < U; b0 += 1024) {
+    const int64_t u = b0 + tid;
+    uint64_t v = 0;
+    int h = 0;
+    if (u < U) {
+      const int64_t it = u / kXeSubPerChunk, k = u % kXeSubPerChunk;
+      h = k == 0 && a.pitems[it * 4 + 2] == a.pitems[it * 4 + 1];  // (chunk start == segment start)
+      v = a.pstat[u * a.F_loc + f];
+    }
+    // segmented inclusive scan in the wave: (h1, v1) . (h2, v2) = (h1 | h2, h2 ? v2 : v1 + v2)
+    uint64_t x = v;
+    int hx = h;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const uint64_t y = __shfl_up(x, d, kWave);
+      const int hy = __shfl_up(hx, d, kWave);
+      if (lane >= d) {
+        if (!hx) x += y;
+        hx |= hy;
+      }
+    }
+    if (lane == kWave - 1) {
+      s_tail[wv] = x;
+      s_head[wv] = hx;
+    }
+    __syncthreads();
+    // the prefix entering this lane's run: earlier waves (back to the nearest head)
+    // and the carry of the earlier rounds
+    if (!hx) {
+      uint64_t add = 0;
+      int w = wv - 1;
+      for (; w >= 0; --w) {
+        add += s_tail[w];
+        if (s_head[w]) break;
+      }
+      if (w < 0) add += s_carry;
+      x += add;
+    }
+    if (u < U) a.pstat[u * a.F_loc + f] = x - v;  // exclusive
+    __syncthreads();
+    if (tid == 1023) s_carry = x;  // (the round's last unit: inclusive, carried on)
     __syncthreads();
   }
+}
+
+template <bool kLdsFlags, bool kReg, bool kPre>
+__global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a, XeLists cur) {
+  extern __shared__ uint32_t s_flag[];
+  if constexpr (kLdsFlags) xe_flags_to_lds(a, s_flag);
   const uint32_t* fl = kLdsFlags ? s_flag : a.flag;
   const int lane = lane_id();
   const unsigned long long lt = (1ull << lane) - 1ull;
@@ -1404,15 +1512,25 @@ __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a,
         break;
       }
   }
-  for (int t = 0, tb = 0;; ++t) {
+  // counted partition: no unit waits on another, so a static grid-stride slice
+  // replaces the ticket counter (one device atomic per claim, serialised on one
+  // address: ~90 us a level at 8 lists with 1- and 2-ticket batches)
+  const int gw = (int)blockIdx.x * kXePartWaves + (int)(threadIdx.x >> 6);
+  const int nwv = (int)gridDim.x * kXePartWaves;
+  for (int t = 0, tb = 0, nclaim = 0;; ++t) {
     if (t == tb) {
-      // a wave whose last batch reached the end claims nothing more (a relaxed
-      // load of the counter before each claim measured slower: 14.9 -> 16.6 ms)
-      if (tb >= total && tb > 0) break;
-      int c = 0;
-      if (lane == 0) c = atomicAdd(a.tick + 1, batch);
-      t = __builtin_amdgcn_readfirstlane(c);
-      tb = t + batch;
+      if constexpr (kPre) {
+        t = gw + nclaim++ * nwv;
+        tb = t + 1;
+      } else {
+        // a wave whose last batch reached the end claims nothing more (a relaxed
+        // load of the counter before each claim measured slower: 14.9 -> 16.6 ms)
+        if (tb >= total && tb > 0) break;
+        int c = 0;
+        if (lane == 0) c = atomicAdd(a.tick + 1, batch);
+        t = __builtin_amdgcn_readfirstlane(c);
+        tb = t + batch;
+      }
     }
     if (t >= total) break;
     const int f = t % Fp;
@@ -1446,11 +1564,15 @@ __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_kernel(XeArgs a,
     // exclusive prefix of left rows over the segment's earlier sub-chunks
     const int qs = (int)((c0 - s0) / kXeSub);
     uint64_t* st = a.pstat + (int64_t)u * a.F_loc + f;
-    if (lane == 0) xe_publish(st, a.tag, qs == 0 ? kXeIncl : kXeAgg, T);
     int64_t lb = 0;
-    if (qs > 0) {
-      lb = xe_lookback(st, a.F_loc, qs, a.tag, a.tick + 2);
-      if (lane == 0) xe_publish(st, a.tag, kXeIncl, (uint32_t)(lb + T));
+    if constexpr (kPre) {  // (counted partition: the prefix is already there)
+      lb = (int64_t)st[0];
+    } else {
+      if (lane == 0) xe_publish(st, a.tag, qs == 0 ? kXeIncl : kXeAgg, T);
+      if (qs > 0) {
+        lb = xe_lookback(st, a.F_loc, qs, a.tag, a.tick + 2);
+        if (lane == 0) xe_publish(st, a.tag, kXeIncl, (uint32_t)(lb + T));
+      }
     }
     const int64_t nlj = a.split[j * 4 + 3];
     if (!kReg && a.sitem) {
@@ -1916,10 +2038,10 @@ void xe_level_scan(hipStream_t s, const XeArgs& a, const XeLists& cur, int items
       hipLaunchKernelGGL(xe_gthr_kernel, dim3((unsigned)((slots_bound + kXeWaves - 1) / kXeWaves)),
                          dim3(kXeThreads), 0, s, a, cur);
       // pass 2: 64 chunk checks per wave step, entries read only near the minimum
+      const int64_t pw = (int64_t)xe_p2_pairs(a.F_loc) * kXeWaves;  // pairs per workgroup step
       hipLaunchKernelGGL(xe_scan_c2_kernel<2>,
                          dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(
-                             ((int64_t)items_bound * a.F_loc + kXeThreads - 1) / kXeThreads,
-                             MT_XE_P2_GRID))),
+                             ((int64_t)items_bound * a.F_loc + pw - 1) / pw, MT_XE_P2_GRID))),
                          dim3(kXeThreads), 0, s, a, cur);
     } else {
       hipLaunchKernelGGL(xe_scan_c2_kernel<0>, g, dim3(kXeThreads), 0, s, a, cur);
@@ -1970,25 +2092,49 @@ void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems
     const char* v = std::getenv("MPITREE_EXACT_PART_LDS");
     return v && v[0] == '0';
   }();
-  if (a.n <= kXePartLdsRows && !lds_off) {
-    const size_t lds = (size_t)((a.n + 31) / 32) * 4;
-#define MT_XP(REG)                                                                          \
-  MT_HIP_CHECK(mt_set_max_lds((const void*)xe_part_kernel<true, REG>, (int)lds));          \
-  hipLaunchKernelGGL((xe_part_kernel<true, REG>), dim3(grid), dim3(kXePartWaves * kWave),   \
-                     lds, s, a, cur);
-    if (a.C == 0) {
-      MT_XP(true)
+  // counted partition (count, per-segment prefix, scatter: no look-back waits,
+  // no ticket counter) -- faster at every list count measured: 8 lists 114 ->
+  // ~15 us a level, the 64-list continuous fit 14.27 -> 13.46 ms
+  // (profiles/r5/ab_exact_counted.log); MPITREE_EXACT_PART_COUNTED=0: the
+  // single-pass look-back partition (read per launch: tests switch it)
+  const char* cv = std::getenv("MPITREE_EXACT_PART_COUNTED");
+  const bool counted = !(cv && cv[0] == '0');
+  const bool in_lds = a.n <= kXePartLdsRows && !lds_off;
+  const size_t lds = in_lds ? (size_t)((a.n + 31) / 32) * 4 : 0;
+  const int g = in_lds ? grid : grid * 2;
+  if (counted) {
+    if (in_lds) {
+      MT_HIP_CHECK(mt_set_max_lds((const void*)xe_part_count_kernel<true>, (int)lds));
+      hipLaunchKernelGGL(xe_part_count_kernel<true>, dim3(g), dim3(kXePartWaves * kWave), lds, s,
+                         a, cur);
     } else {
-      MT_XP(false)
+      hipLaunchKernelGGL(xe_part_count_kernel<false>, dim3(g), dim3(kXePartWaves * kWave), 0, s,
+                         a, cur);
     }
-#undef MT_XP
-  } else if (a.C == 0) {
-    hipLaunchKernelGGL((xe_part_kernel<false, true>), dim3(grid * 2), dim3(kXePartWaves * kWave),
-                       0, s, a, cur);
-  } else {
-    hipLaunchKernelGGL((xe_part_kernel<false, false>), dim3(grid * 2),
-                       dim3(kXePartWaves * kWave), 0, s, a, cur);
+    hipLaunchKernelGGL(xe_part_prefix_kernel, dim3(a.F_loc), dim3(1024), 0, s, a, cur);
   }
+#define MT_XP(LDS, REG, PRE)                                                                    \
+  do {                                                                                          \
+    if (LDS) MT_HIP_CHECK(mt_set_max_lds((const void*)xe_part_kernel<LDS, REG, PRE>, (int)lds)); \
+    hipLaunchKernelGGL((xe_part_kernel<LDS, REG, PRE>), dim3(g), dim3(kXePartWaves * kWave),    \
+                       lds, s, a, cur);                                                         \
+  } while (0)
+#define MT_XP2(LDS, REG) \
+  do {                   \
+    if (counted)         \
+      MT_XP(LDS, REG, true); \
+    else                 \
+      MT_XP(LDS, REG, false); \
+  } while (0)
+  if (in_lds) {
+    if (a.C == 0) MT_XP2(true, true);
+    else MT_XP2(true, false);
+  } else {
+    if (a.C == 0) MT_XP2(false, true);
+    else MT_XP2(false, false);
+  }
+#undef MT_XP2
+#undef MT_XP
   MT_HIP_CHECK(hipGetLastError());
 }
 

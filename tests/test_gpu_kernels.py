@@ -659,6 +659,31 @@ def test_gpu_exact_finisher_handoff_same_tree(monkeypatch):
     np.testing.assert_array_equal(a.tree_arrays_.threshold, b.tree_arrays_.threshold)
 
 
+@pytest.mark.parametrize("n,F,regression", [(40000, 12, False), (30000, 40, False),
+                                             (30000, 10, True), (1_300_000, 3, False)])
+def test_gpu_exact_counted_partition_same_tree(monkeypatch, n, F, regression):
+    """The counted partition (count, per-segment prefix, scatter; the default for
+    <= 16 lists a rank) and the single-pass look-back partition build the same
+    tree -- with the flags in LDS and, past 1.18M rows, read from global memory."""
+    from mpitree_amd import DecisionTreeRegressor
+
+    rng = np.random.default_rng(n + F)
+    X = rng.normal(size=(n, F)).astype(np.float32)
+    X[:, 1] = np.round(X[:, 1], 2)  # ties
+    s = X[:, 0] + X[:, 1] * X[:, 2] + rng.normal(scale=0.5, size=n)
+    y = s.astype(np.float64) if regression else (s > 0).astype(np.int64)
+    cls = DecisionTreeRegressor if regression else DecisionTreeClassifier
+    Xd, yd = torch.from_numpy(X).cuda(), torch.from_numpy(y).cuda()
+    out = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MPITREE_EXACT_PART_COUNTED", mode)
+        est = cls(device="cuda", max_depth=14 if n > 10**6 else None).fit(Xd, yd)
+        assert est.fit_stats_["engine"] == "hip-exact"
+        out.append(est.tree_arrays_)
+    assert out[0].equal(out[1], check_impurity=not regression)
+    np.testing.assert_array_equal(out[0].threshold, out[1].threshold)
+
+
 @pytest.mark.parametrize("shape", [(50000, 6, None, 1), (8000, 3, 5, 2)])
 def test_gpu_exact_regression_matches_host(shape):
     """Regression on continuous features: exact thresholds on the GPU (the

@@ -17,7 +17,7 @@
 #                        tree from tools/snapshot_tree.sh; BENCH_ARGS: extra bench.py args)
 #   configs[:NAMES]      bench/baseline_configs.py NAMES --reps 5       -> baseline_configs.jsonl
 #   prof:NAME[:ARGS]     rocprofv3 kernel trace + stats of bench.py ARGS
-#                        -> prof_NAME.{top,summary,timeline}.txt, kernel_stats.csv
+#                        -> prof_NAME.{top,summary,timeline,lastfit}.txt, kernel_stats.csv
 #   profpy:NAME:SCRIPT[:ARGS]  the same for python3 SCRIPT ARGS (e.g. bench/sim_own_ranks.py)
 #   fin                  block-finisher phase profile (bench/fin_prof.py) -> fin_prof.log
 #   pmc[:ARGS]           two PMC passes over bench/pmc_fit.py ARGS      -> pmc_report.md
@@ -46,6 +46,7 @@ prof() {  # name, seconds, command...
     python tools/rocpd_top.py "$db" 40 > "gpurun_out/prof_$name.top.txt"
     python tools/rocpd_summary.py "$db" > "gpurun_out/prof_$name.summary.md"
     python tools/rocpd_timeline.py "$db" --n 400 > "gpurun_out/prof_$name.timeline.txt" || true
+    python tools/rocpd_timeline.py "$db" --agg > "gpurun_out/prof_$name.lastfit.txt" || true
   fi
   find "gpurun_out/prof_$name" -name '*kernel_stats.csv' -exec cp {} "gpurun_out/prof_$name.kernel_stats.csv" \;
   rm -rf "gpurun_out/prof_$name"  # the databases exceed what gpurun copies back

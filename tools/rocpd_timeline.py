@@ -13,6 +13,8 @@ def main():
     ap.add_argument("db")
     ap.add_argument("--first-kernel", default="edges_kernel")
     ap.add_argument("--n", type=int, default=80)
+    ap.add_argument("--agg", action="store_true",
+                    help="per-kernel totals of the last fit instead of the timeline")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end from kernels order by start").fetchall()
@@ -21,6 +23,18 @@ def main():
         raise SystemExit("marker kernel not found")
     fit = rows[idx[-1]:]
     t0 = fit[0][1]
+    if a.agg:
+        tot = {}
+        for name, st, en in fit:
+            short = name.split("(")[0].replace("void ", "")[:60]
+            cnt, d = tot.get(short, (0, 0.0))
+            tot[short] = (cnt + 1, d + (en - st) / 1e3)
+        span = (max(r[2] for r in fit) - t0) / 1e3
+        print(f"last fit: span {span:.1f} us, kernel time {sum(d for _, d in tot.values()):.1f} us")
+        print(f"{'kernel':62s} {'calls':>5s} {'total us':>9s} {'avg us':>7s}")
+        for k, (cnt, d) in sorted(tot.items(), key=lambda x: -x[1][1]):
+            print(f"{k:62s} {cnt:5d} {d:9.1f} {d / cnt:7.1f}")
+        return
     prev = t0
     gaps = 0.0
     for k, (name, st, en) in enumerate(fit):
