@@ -190,7 +190,14 @@ def main():
                     help="force the feature-parallel prefix levels off / on")
     ap.add_argument("--no-shared", action="store_true",
                     help="node exchange + full-tree copy instead of the shared-host assembly")
+    ap.add_argument("--cprofile", default=None,
+                    help="write a cProfile of the timed fits' host code to this file")
     a = ap.parse_args()
+    prof = None
+    if a.cprofile:
+        import cProfile
+
+        prof = cProfile.Profile()
     if a.fp_prefix is not None:
         os.environ["MPITREE_OWN_FP_PREFIX"] = a.fp_prefix
     if a.units_per_rank is not None:
@@ -229,9 +236,13 @@ def main():
                 if pool is not None:
                     pool.slot.prefill()
                 torch.cuda.synchronize()
+                if prof is not None and i >= 2:
+                    prof.enable()
                 t0 = time.perf_counter()
                 res = fit(comm)
                 torch.cuda.synchronize()
+                if prof is not None:
+                    prof.disable()
                 if i >= 2:
                     times.append((time.perf_counter() - t0) * 1e3)
                 st = res.stats
@@ -255,6 +266,15 @@ def main():
                    nodes=ref.arrays.node_count, tree_equal=True,
                    phases_max_rank=per_rank[int(np.argmax(ms))]["phases"])
         print(json.dumps(out), flush=True)
+    if prof is not None:
+        import io
+        import pstats
+
+        with open(a.cprofile, "w") as f:
+            for key in ("tottime", "cumulative"):
+                sio = io.StringIO()
+                pstats.Stats(prof, stream=sio).sort_stats(key).print_stats(45)
+                f.write(f"==== by {key}\n{sio.getvalue()}\n")
 
 
 if __name__ == "__main__":
