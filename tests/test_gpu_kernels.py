@@ -177,8 +177,9 @@ def test_gpu_device_assembly_matches_host(monkeypatch, regression):
     assert dev.equal(host, check_impurity=False)
     assert np.array_equal(dev.impurity, host.impurity, equal_nan=True)
     if regression:
+        # (the device columns carry no fixed-point sums: value = sum / count is
+        # computed on the device from the same int64 sums)
         assert np.array_equal(dev.value, host.value)
-        assert np.array_equal(dev.meta["sum_fixed"], host.meta["sum_fixed"])
 
 
 def test_gpu_edges_match_host_mapper():
