@@ -395,8 +395,11 @@ class _ParallelMixin:
                 if torn is not None:
                     raise torn
             # one all-gather of {failed, tree digest}: failure propagation + consistency
+            # (a tree assembled in one node-shared buffer is the same memory on
+            # every rank: nothing to compare)
             check = os.environ.get("MPITREE_CHECK_CONSISTENCY", "1") != "0"
-            digest = tree_digest(self._arrays) if (error is None and check) else 0
+            shared = (getattr(self, "fit_stats_", None) or {}).get("assembly") == "shared-host"
+            digest = tree_digest(self._arrays) if (error is None and check and not shared) else 0
             try:
                 st = comm._all_gather(np.array([1 if error is not None else 0, digest],
                                                np.int64))

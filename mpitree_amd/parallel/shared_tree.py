@@ -129,7 +129,7 @@ class ShmTreePool:
     """The shared tree buffers of one communicator (same decisions on every rank)."""
 
     def __init__(self, comm, hip, uid: int):
-        self.comm, self.hip, self.uid = comm, hip, int(uid)
+        self.hip, self.uid = hip, int(uid)
         self.rank, self.P = int(comm.rank), int(comm.world_size)
         self.slots: dict[int, _Slot] = {}
         self.gen = 0
@@ -225,21 +225,60 @@ class ShmTreePool:
             slot.unlink()  # every rank has it mapped: the name is no longer needed
 
 
+_POOLS: dict = {}  # process group -> (pool or False, weakref of the group)
+
+
+def _group_key(comm):
+    """The process group a communicator runs on (estimators build a new
+    communicator per fit; the pool -- its registered buffers and the agreed
+    next slot -- belongs to the group, so consecutive fits reuse it)."""
+    group = getattr(comm, "group", None)
+    try:
+        import torch.distributed as dist
+
+        if group is None and dist.is_initialized():
+            group = dist.distributed_c10d._get_default_group()
+    except Exception:  # pragma: no cover - (no torch.distributed)
+        pass
+    return (id(group), int(comm.world_size), int(comm.rank)), group
+
+
+def _alive(entry, group) -> bool:
+    """The cached pool belongs to this very group object (not a destroyed group
+    whose id a new one reuses)."""
+    ref = entry[1]
+    return ref is None or ref() is group
+
+
+def _ref(group):
+    import weakref
+
+    try:
+        return weakref.ref(group)
+    except TypeError:  # (no weak references: the id alone)
+        return None
+
+
 def pool_for(comm, hip):
-    """The communicator's pool, or None when its ranks span hosts (or
-    ``MPITREE_SHM_TREE=0``). Collective on first use (one small all-gather)."""
+    """The pool of the communicator's process group, or None when its ranks span
+    hosts (or ``MPITREE_SHM_TREE=0``). Collective on the group's first use (one
+    small all-gather); later fits -- each with a new communicator -- reuse it."""
     pool = getattr(comm, "_shm_pool", None)
-    if pool is not None:
+    if pool is not None:  # (a communicator that carries its own, e.g. simulations)
         return pool or None
     if getattr(comm, "world_size", 1) <= 1 or not hasattr(comm, "_all_gather"):
         return None
     if os.environ.get("MPITREE_SHM_TREE", "1") == "0":
-        comm._shm_pool = False
         return None
+    key, group = _group_key(comm)
+    entry = _POOLS.get(key)
+    if entry is not None and _alive(entry, group):
+        return entry[0] or None
     uid = int.from_bytes(os.urandom(6), "little")
     g = comm._all_gather(np.array([_host_key(), uid], dtype=np.int64)).reshape(-1, 2)
     if not (g[:, 0] == g[0, 0]).all() or not os.path.isdir("/dev/shm"):
-        comm._shm_pool = False
-        return None
-    comm._shm_pool = ShmTreePool(comm, hip, int(g[0, 1]))
-    return comm._shm_pool
+        pool = False
+    else:
+        pool = ShmTreePool(comm, hip, int(g[0, 1]))
+    _POOLS[key] = (pool, _ref(group) if group is not None else None)
+    return pool or None
