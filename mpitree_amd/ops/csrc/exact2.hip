@@ -1394,6 +1394,13 @@ __device__ __forceinline__ void xe_flags_to_lds(const XeArgs& a, uint32_t* s_fla
 template <bool kLdsFlags>
 __global__ __launch_bounds__(kXePartWaves * kWave) void xe_part_count_kernel(XeArgs a, XeLists cur) {
   extern __shared__ uint32_t s_flag[];
+  if (a.sitem && a.nctl) {  // (xe_tot_zero_kernel's work: the next level's chunk totals,
+    // which the scatter adds into -- this level's scan has read them already)
+    const int64_t tz = (int64_t)a.nctl[1] * a.F_loc * xe_cc(a.C);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tz;
+         i += (int64_t)gridDim.x * blockDim.x)
+      a.tot[i] = 0;
+  }
   if constexpr (kLdsFlags) xe_flags_to_lds(a, s_flag);
   const uint32_t* fl = kLdsFlags ? s_flag : a.flag;
   const int lane = lane_id();
@@ -2078,7 +2085,9 @@ void xe_flag(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_boun
 void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems_bound,
                   int splits_bound) {
   if (pitems_bound <= 0 || splits_bound <= 0) return;
-  if (a.sitem && a.nctl)
+  const char* cv = std::getenv("MPITREE_EXACT_PART_COUNTED");
+  const bool counted = !(cv && cv[0] == '0');
+  if (a.sitem && a.nctl && !counted)  // (the counted partition's count kernel zeroes them)
     hipLaunchKernelGGL(xe_tot_zero_kernel, dim3(1024), dim3(256), 0, s, a.tot, a.nctl,
                        (int64_t)a.F_loc * xe_cc(a.C));
   int dev = 0, n_cu = 0;
@@ -2097,8 +2106,6 @@ void xe_partition(hipStream_t s, const XeArgs& a, const XeLists& cur, int pitems
   // ~15 us a level, the 64-list continuous fit 14.27 -> 13.46 ms
   // (profiles/r5/ab_exact_counted.log); MPITREE_EXACT_PART_COUNTED=0: the
   // single-pass look-back partition (read per launch: tests switch it)
-  const char* cv = std::getenv("MPITREE_EXACT_PART_COUNTED");
-  const bool counted = !(cv && cv[0] == '0');
   const bool in_lds = a.n <= kXePartLdsRows && !lds_off;
   const size_t lds = in_lds ? (size_t)((a.n + 31) / 32) * 4 : 0;
   const int g = in_lds ? grid : grid * 2;

@@ -177,7 +177,10 @@ def device_loop_supported(be, params, comm) -> bool:
     n, F, B, C, reg = be.n, be.F, be.B, be.C, bool(be.reg)
     fr = int(params.finisher_rows)
     par = 1 if derive_free_levels(n, F, B, C, reg, fr, be.hip, be.device) else 2
-    return level_loop_bytes(n, F, B, C, reg, fr, be.hip, par) <= free_device_bytes(be.device) // 2
+    need = level_loop_bytes(n, F, B, C, reg, fr, be.hip, par)
+    if need <= total_device_bytes(be.device) // 64:  # (no free-memory query: ~10 us a fit)
+        return True
+    return need <= free_device_bytes(be.device) // 2
 
 
 def slab_rows(n_loc: int) -> int:
@@ -199,6 +202,22 @@ def level_loop_bytes(n, F, B, C, reg, fr, hip, parities: int = 2) -> int:
     return int(hist + slab)
 
 
+_TOTAL_BYTES: dict = {}
+
+
+def total_device_bytes(device) -> int:
+    """The device's memory size (cached: a property query per fit costs host time)."""
+    key = str(device)
+    v = _TOTAL_BYTES.get(key)
+    if v is None:
+        try:
+            v = int(torch.cuda.get_device_properties(device).total_memory)
+        except Exception:  # pragma: no cover - (no device: tests on CPU)
+            v = 0
+        _TOTAL_BYTES[key] = v
+    return v
+
+
 def derive_free_levels(n, F, B, C, reg, fr, hip, device) -> bool:
     """Whether the level loop keeps ONE histogram buffer and builds every child
     from rows (no parent - sibling derivation, which needs the parent level's
@@ -208,9 +227,8 @@ def derive_free_levels(n, F, B, C, reg, fr, hip, device) -> bool:
     env = os.environ.get("MPITREE_DERIVE_FREE")
     if env is not None:
         return env != "0"
-    try:
-        total = int(torch.cuda.get_device_properties(device).total_memory)
-    except Exception:  # pragma: no cover - (no device: tests on CPU)
+    total = total_device_bytes(device)
+    if total <= 0:
         return False
     return level_loop_bytes(n, F, B, C, reg, fr, hip, 2) > 0.4 * total
 

@@ -374,6 +374,7 @@ class ExactGrower:
             )
         L = ws["L"]
         ptr = {k: (v.data_ptr() if isinstance(v, torch.Tensor) else 0) for k, v in ws.items()}
+        flag_bytes = os.environ.get("MPITREE_EXACT_FLAG_BYTES", "1") != "0"
         lp = [{k: v.data_ptr() for k, v in x.items()} for x in L]
         ctx = hip.XeCtx(dict(
             E0=E[0].data_ptr(), E1=E[1].data_ptr(),
@@ -387,8 +388,7 @@ class ExactGrower:
             gthr=ptr["gthr"],
             rec=ptr["rec"], split=ptr["split"],
             pitems=ptr["pitems"], pfirst=ptr["pfirst"], flag=ptr["flag"],
-            **({"flagb": ptr["flagb"]} if os.environ.get("MPITREE_EXACT_FLAG_BYTES", "1") != "0"
-               else {}),
+            **({"flagb": ptr["flagb"]} if flag_bytes else {}),
             pstat=ptr["pstat"], tick=ptr["tick"], pos_rec=be.pos_rec.data_ptr(),
             **({"sitem": ptr["sitem"]} if os.environ.get("MPITREE_EXACT_PART_TOT", "1") != "0"
                else {}),
@@ -437,8 +437,10 @@ class ExactGrower:
             ctx.plan(s(), lvl, hctl_dev + (lvl % 64) * 64, tag0 + (lvl % 4096) + 1)
             _step(dev, "plan")
             if P > 1:  # the split feature's owner sets the left rows; summed over ranks
-                ws["flag"].zero_()
-                ws["flagb"].zero_()
+                if flag_bytes:  # (the byte pack then writes every flag word)
+                    ws["flagb"].zero_()
+                else:
+                    ws["flag"].zero_()
                 ctx.flag(s(), lvl, ib, 0)
                 comm.all_reduce_device(ws["flag"])
                 comm_bytes.append(int(getattr(comm, "bytes_communicated", 0) - b0))
