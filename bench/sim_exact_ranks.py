@@ -138,6 +138,31 @@ class SimFeatureComm(LocalComm):
                     g[q, : hi - lo].copy_(self.ref["fm"][lo:hi])
         o[r].copy_(inp.reshape(-1))
 
+    def all_to_all_device(self, out, inp, out_splits, in_splits):
+        """The finisher codes: every other feature block's codes at this rank's
+        job positions (the reference fit's codes), this rank's own chunk as sent."""
+        from mpitree_amd.ops.exact_grower import _owners, own_positions
+        from mpitree_amd.parallel.strategies import feature_blocks
+
+        P, r = self.world_size, self.rank
+        self.bytes_communicated += int(sum(in_splits))
+        cache = self.ref.setdefault("mine", {})
+        if (P, r) not in cache:  # (the stand-in's own bookkeeping: once per rank)
+            fj = self.ref["fj"]
+            pos, sizes = own_positions(fj, _owners(int(fj.shape[0]), P, fj.device), P)
+            cache[(P, r)] = pos[int(sum(sizes[:r])) : int(sum(sizes[: r + 1]))].clone()
+        mine = cache[(P, r)]
+        off = 0
+        for q, (lo, hi) in enumerate(feature_blocks(self.F, P)):
+            k = int(out_splits[q])
+            if q == r:
+                s0 = int(sum(in_splits[:r]))
+                out[off : off + k].copy_(inp[s0 : s0 + k])
+            elif k:
+                torch.index_select(self.ref["fm"][lo:hi], 1, mine,
+                                   out=out[off : off + k].view(hi - lo, -1))
+            off += k
+
     def all_reduce_device(self, t, op=None):
         self.bytes_communicated += t.numel() * t.element_size()
         if t.numel() == 1:  # the watchdog word (MAX over ranks): this rank's stands
@@ -194,7 +219,7 @@ def build_reference(fit, dev, P_list, C):
             inside = torch.cumsum(mark, 0)[:Pp] > 0
             live = torch.nonzero(inside & (pre[:, 5] > 0)).squeeze(1)
             others[(P, r)] = torch.cat([live.to(torch.int32)[:, None], pre[live], pst[live]], 1)
-    return res, dict(rec=R.rec, flag=R.flag, fm=R.fm, resolved=resolved, others=others)
+    return res, dict(rec=R.rec, flag=R.flag, fm=R.fm, resolved=resolved, others=others, fj=fj)
 
 
 def _diff(a, b) -> dict:

@@ -135,6 +135,29 @@ def _packed_labels(C: int) -> bool:
     return C <= int(native.hip().xe_packed_classes())
 
 
+def own_sizes(fj: torch.Tensor, own: torch.Tensor, P: int) -> torch.Tensor:
+    """Rows of each rank's jobs (device [P])."""
+    return torch.zeros(P, dtype=torch.int64, device=fj.device).index_add_(0, own, fj[:, 1])
+
+
+def own_positions(fj: torch.Tensor, own: torch.Tensor, P: int, sizes=None):
+    """Job segment positions grouped by owner rank (ascending rank, jobs in
+    finisher order within a rank) and each rank's row total (host list: a host
+    wait unless ``sizes`` already holds them)."""
+    dev = fj.device
+    if sizes is None:
+        sizes = own_sizes(fj, own, P).cpu()
+    sizes = [int(v) for v in sizes.tolist()]
+    order = torch.argsort(own, stable=True)
+    js = fj.index_select(0, order)
+    cnt = js[:, 1]
+    excl = torch.cumsum(cnt, 0) - cnt
+    total = int(sum(sizes))
+    rep_start = torch.repeat_interleave(js[:, 0] - excl, cnt, output_size=total)
+    pos = rep_start + torch.arange(total, device=dev)
+    return pos, sizes
+
+
 def _owners(J: int, P: int, device) -> torch.Tensor:
     k = torch.arange(J, device=device)
     lap, off = k // P, k % P
@@ -542,6 +565,41 @@ class ExactGrower:
                                 be.pos_rec.data_ptr(), pos_thr.data_ptr())
         self._keep_r = (allr, rows, resolved, tile, total, rk)
 
+    def _exchange_codes(self, loc, fj, own, blocks, rank, P, F, h_sizes=None):
+        """Feature-parallel finisher codes: rank r holds its feature block's codes
+        (``loc["blk"]``) at every job position; after one all_to_all every rank
+        holds all features' codes (``loc["fm"]``) at its own jobs' positions.
+        ``fj``: the jobs in finisher order, ``own``: their owners. Blocks travel
+        feature-major ([features, positions]: the gathers read runs of positions,
+        the jobs' segments)."""
+        comm = self.comm
+        dev = fj.device
+        pos, sizes = own_positions(fj, own, P, h_sizes)
+        lo_me, hi_me = blocks[rank]
+        Fb_me = hi_me - lo_me
+        src = loc["blk"][:Fb_me]
+        in_splits = [int(k) * Fb_me for k in sizes]
+        send = torch.empty(max(1, sum(in_splits)), dtype=torch.uint8, device=dev)
+        o, p0 = 0, 0
+        for k in sizes:
+            if k:
+                torch.index_select(src, 1, pos[p0 : p0 + k],
+                                   out=send[o : o + k * Fb_me].view(Fb_me, k))
+            o += k * Fb_me
+            p0 += k
+        mine = pos[int(sum(sizes[:rank])) : int(sum(sizes[: rank + 1]))]
+        n_me = int(sizes[rank])
+        out_splits = [n_me * (hi - lo) for lo, hi in blocks]
+        recv = torch.empty(max(1, sum(out_splits)), dtype=torch.uint8, device=dev)
+        comm.all_to_all_device(recv[: sum(out_splits)], send[: sum(in_splits)], out_splits,
+                               in_splits)
+        off = 0
+        for (lo, hi), k in zip(blocks, out_splits):
+            if k:
+                loc["fm"][lo:hi].index_copy_(1, mine, recv[off : off + k].view(hi - lo, n_me))
+            off += k
+        self._keep_c = (send, recv)
+
     def _finish(self, ws, be, E, Y, Xd, J, JW, F, f_lo, F_loc, blocks, n, reg, pos_thr, P,
                 rank):
         """Grow the <= 256-row job segments on subtree-local codes; turn the
@@ -565,11 +623,19 @@ class ExactGrower:
                 tmp=torch.empty(n, dtype=torch.int32, device=dev),
                 yv=torch.empty(n, dtype=torch.int64, device=dev) if reg else None,
                 nbins=torch.full((F,), 256, dtype=torch.int32, device=dev),
-                gather=(torch.empty((P, Fb, n), dtype=torch.uint8, device=dev) if P > 1
-                        else None),
             )
         fm_out = loc["blk"] if P > 1 else loc["fm"]
         x64 = int(Xd.dtype == torch.float64)
+        fj = jobs.clone()
+        fj[:, 4] = 0  # rows live in the virtual row buffer (idx)
+        order = torch.argsort(fj[:, 1] * (1 << 32) - fj[:, 3], descending=True)
+        fj = fj.index_select(0, order)
+        h_sizes = own = None
+        if P > 1:  # (the owners' row totals travel to the host while the codes build)
+            own = _owners(J, P, dev)
+            h_sizes = hb._pinned_copy(own_sizes(fj, own, P), "exact.own_sizes")
+            ev = torch.cuda.Event()
+            ev.record()
         hip.xe_local_codes(s(), E[0].data_ptr(), E[1].data_ptr(),
                            Y[0].data_ptr() if reg else 0, Y[1].data_ptr() if reg else 0,
                            Xd.data_ptr(), x64, F, f_lo, n, F_loc, 0, jobs.data_ptr(), J, JW,
@@ -577,13 +643,16 @@ class ExactGrower:
                            loc["yv"].data_ptr() if reg else 0,
                            0 if reg or _packed_labels(self.C) else self._y32.data_ptr(),
                            codes_rm=0 if P > 1 else loc["rm"].data_ptr(), row_bytes=rb)
-        if P > 1:  # every rank's feature block of the codes -> all features on every rank
-            g = loc["gather"]
-            comm.all_gather_device(g.view(-1), loc["blk"].view(-1))
-            for r, (lo, hi) in enumerate(blocks):
-                loc["fm"][lo:hi].copy_(g[r, : hi - lo])
-            hip.xe_codes_rm(s(), loc["fm"].data_ptr(), n, F, rb, jobs.data_ptr(), J, JW,
-                            loc["rm"].data_ptr())
+        if P > 1:
+            # every rank grows its own jobs and needs every feature's codes at their
+            # positions only: one all_to_all of the feature blocks' codes at the
+            # destination's job positions (1 / P of an all-gather of all codes)
+            ev.synchronize()
+            self._exchange_codes(loc, fj, own, blocks, rank, P, F, h_sizes)
+            fj = fj[own == rank].contiguous()
+            if fj.shape[0]:
+                hip.xe_codes_rm(s(), loc["fm"].data_ptr(), n, F, rb, fj.data_ptr(),
+                                int(fj.shape[0]), JW, loc["rm"].data_ptr())
         # the finisher reads the binned engine's fields: point them at the local codes
         be.codes_rm, be.codes_fm = loc["rm"], loc["fm"]
         be.row_elems, be.cb, be.B, be.nbins = rb, 1, 256, loc["nbins"]
@@ -592,13 +661,6 @@ class ExactGrower:
             be.lab_shift, be.row_mask, be.y = 0, 0xFFFFFFFF, loc["yv"]
         else:
             be.lab_shift, be.row_mask, be.y = 24, (1 << 24) - 1, loc["ent"]
-        fj = jobs.clone()
-        fj[:, 4] = 0  # rows live in the virtual row buffer (idx)
-        order = torch.argsort(fj[:, 1] * (1 << 32) - fj[:, 3], descending=True)
-        fj = fj.index_select(0, order)
-        if P > 1:
-            own = _owners(J, P, dev) == rank
-            fj = fj[own].contiguous()
         Jm = int(fj.shape[0])
         if Jm:
             be.launch_finisher(fj, Jm, n, self.p, be.pos_rec, be.pos_st)

@@ -97,3 +97,45 @@ def test_two_ranks_share_one_buffer_through_the_barrier():
         assert p.exitcode == 0
     for rank, s0, s1, half in got:
         assert s0 == half and s1 == 2 * half  # both ranks' halves, seen by each
+
+
+def test_pool_belongs_to_the_group_not_the_communicator():
+    """Estimators build a communicator per fit: the pool (and its registered
+    buffers) is found again through the process group, the host-key all-gather
+    runs once."""
+    calls = []
+
+    class _G:  # a process group stand-in (weak-referenceable)
+        pass
+
+    class _C(_Comm):
+        def _all_gather(self, a):
+            calls.append(1)
+            return np.stack([a, a])
+
+    g = _G()
+    a, b = _C(0, 2), _C(0, 2)
+    a.group = b.group = g
+    p1 = st.pool_for(a, _FakeHip())
+    p2 = st.pool_for(b, _FakeHip())
+    assert p1 is not None and p1 is p2 and len(calls) == 1
+    c = _C(0, 2)
+    c.group = _G()  # another group: another pool
+    assert st.pool_for(c, _FakeHip()) is not p1 and len(calls) == 2
+
+
+def test_exact_own_positions_group_jobs_by_owner():
+    import torch
+
+    from mpitree_amd.ops.exact_grower import _owners, own_positions
+
+    # jobs {start, count, ...} in finisher order; owners dealt serpentine
+    fj = torch.tensor([[0, 5, 0, 0, 0], [10, 3, 0, 0, 0], [20, 4, 0, 0, 0],
+                       [30, 2, 0, 0, 0], [40, 1, 0, 0, 0]], dtype=torch.int64)
+    own = _owners(5, 2, fj.device)
+    pos, sizes = own_positions(fj, own, 2)
+    want = {0: [], 1: []}
+    for j in range(5):
+        want[int(own[j])] += list(range(int(fj[j, 0]), int(fj[j, 0] + fj[j, 1])))
+    assert sizes == [len(want[0]), len(want[1])]
+    assert pos.tolist() == want[0] + want[1]
