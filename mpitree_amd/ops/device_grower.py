@@ -665,7 +665,8 @@ class DeviceGrower:
                 state = ck.load_device(rank, P, (lambda a: comm._all_gather(a)) if P > 1
                                        else None)
             first_lvl = 0  # levels before it ran in an earlier process (resume)
-            ws["own_state"].zero_()  # (subtree ownership: not switched yet)
+            if own:  # (subtree ownership: not switched yet)
+                ws["own_state"].zero_()
             if state is not None:
                 first_lvl = self._ckpt_restore(state, ws, sets, hists) + 1
                 self.stats["resumed_from_level"] = first_lvl - 1
