@@ -955,12 +955,16 @@ class DeviceGrower:
         table = None
         if d_edges is None:
             table = edges if isinstance(edges, np.ndarray) else edges.padded_edges()
+        b_asm = getattr(comm, "bytes_communicated", 0)
         ta = be.assemble_positions(table, int(p.criterion), y_exp, d_edges=d_edges,
                                    shared=shared)
         if ta is None:  # (/dev/shm too small for the tree, on every rank alike)
             self.stats["assembly"] = "exchange (/dev/shm short)"
             self._exchange_owned(owned)
             ta = be.assemble_positions(table, int(p.criterion), y_exp, d_edges=d_edges)
+        if shared is not None:  # (the shared assembly's segment-count all-gather)
+            self.stats["comm_bytes_exchange"] = int(self.stats.get("comm_bytes_exchange", 0)
+                                                    + comm.bytes_communicated - b_asm)
         self.timings["assemble"] = time.perf_counter() - t0
         if self.ckpt is not None:
             self.stats["checkpoint_levels_saved"] = self.ckpt.saved_levels
