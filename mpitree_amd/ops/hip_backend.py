@@ -105,6 +105,14 @@ def _workspace(device, name: str, nbytes: int) -> torch.Tensor:
     return buf
 
 
+def _i64_scratch(device, name: str, rows: int, cols: int) -> torch.Tensor:
+    """An int64 [rows, cols] view of a reused scratch buffer (uninitialised; the
+    finisher's record lists: allocating them per launch cost host time right
+    where the GPU waits for the finisher's launch)."""
+    nb = int(rows) * int(cols) * 8
+    return _workspace(device, name, nb)[:nb].view(torch.int64).view(int(rows), int(cols))
+
+
 _uploaders: dict = {}
 
 
@@ -785,8 +793,8 @@ class HipBackend:
         grid = int(os.environ.get("MPITREE_FIN_GRID", 2 * N_CU)) if grid is None else int(grid)
         # every tiny subtree has >= 2 rows and they partition the job rows; each
         # workgroup reserves records kFinTinyBatch at a time
-        tiny = torch.empty((int(job_rows // 2 + J + 1 + grid * _tiny_batch(self.hip)), 8),
-                           dtype=torch.int64, device=self.device)
+        tiny = _i64_scratch(self.device, "fin.tiny",
+                            int(job_rows // 2 + J + 1 + grid * _tiny_batch(self.hip)), 8)
         if C > 2:  # (the hand-off queue is on the two-class kernel only)
             grid = min(grid, J)
         # subtrees handed to idle workgroups (each > 2 tiny_rows rows, disjoint)
@@ -796,7 +804,7 @@ class HipBackend:
             task_cap = 0  # no hand-offs: spare workgroups only wait for the end
         elif steal == "-1":
             task_cap = -1  # no queue at all (claims past the jobs exit at once)
-        tasks = torch.empty((max(task_cap, 1), 5 + C), dtype=torch.int64, device=self.device)
+        tasks = _i64_scratch(self.device, "fin.tasks", max(task_cap, 1), 5 + C)
         flags, epoch = _task_flags(self.device, max(task_cap, 0) + grid, slot)
         prof = None
         if os.environ.get("MPITREE_FIN_PROF"):
@@ -837,8 +845,8 @@ class HipBackend:
         elif steal == "-1":
             task_cap, grid = -1, min(grid, J)
         cap = int(job_rows // 2 + J + 1 + grid * _tiny_batch(self.hip))
-        tiny = torch.empty((cap, 8), dtype=torch.int64, device=self.device)
-        tasks = torch.empty((max(task_cap, 1), 7), dtype=torch.int64, device=self.device)
+        tiny = _i64_scratch(self.device, "fin.tiny", cap, 8)
+        tasks = _i64_scratch(self.device, "fin.tasks", max(task_cap, 1), 7)
         flags, epoch = _task_flags(self.device, max(task_cap, 0) + grid, slot)
         self.hip.finish_reg(_stream(), self.codes_rm.data_ptr(), self.row_elems * self.cb // 4,
                             self.codes_fm.data_ptr(), self.cb, self.n, self.idx.data_ptr(),
