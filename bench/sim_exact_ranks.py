@@ -4,16 +4,18 @@ The exact engine (``ops/exact_grower.py``, reference semantics: every unique
 value a candidate, ``/root/reference/mpitree/tree/decision_tree.py:73-90``) is
 feature-parallel over P ranks: rank r sorts, scans and partitions only its F/P
 presorted lists; per level it all-gathers the per-node best records
-(``fp_combine``) and all-reduces the n-bit row-direction flags; the finisher's
-local codes are all-gathered once, the finisher jobs are dealt serpentine and the
-finished position ranges plus the resolved thresholds are exchanged at the end.
+(``fp_combine``) and all-reduces the n-bit row-direction flags; the finisher jobs
+are dealt serpentine, one all_to_all brings every rank all features' local codes
+at its own jobs' positions, and the finished position ranges plus the resolved
+thresholds are exchanged at the end.
 
 Rank r's kernels depend on the other ranks only through those collectives, so
 rank r can run alone against a stand-in communicator that returns what the
 other ranks would have contributed -- recorded from a single-GPU reference fit
 of the same data (the P-rank tree is bit-identical to the 1-GPU tree, which
 the gloo GPU tests pin): the level's global best records, the level's direction
-flags, the finisher's local codes of the other feature blocks, the finished
+flags, the other feature blocks' finisher codes at the rank's job positions (the
+all_to_all), the finished
 records of the other ranks' job ranges (as they stand before the threshold
 fix), and every resolved threshold. The script checks every simulated rank's
 tree against the reference. Reported per P (median over reps):
@@ -122,20 +124,12 @@ class SimFeatureComm(LocalComm):
         self.flag_lvl = 0
         self.exchanges = 0
 
-    def all_gather_device(self, out, inp):
+    def all_gather_device(self, out, inp):  # the level's best records
         P, r = self.world_size, self.rank
         self.bytes_communicated += inp.numel() * inp.element_size() * P
         o = out.view(P, -1)
-        if inp.dtype == torch.int64:  # the level's best records
-            o.copy_(self.ref["rec"][self.lvl].reshape(1, -1).expand(P, -1))
-            self.lvl += 1
-        else:  # the finisher's local codes, [P, Fb, n]
-            from mpitree_amd.parallel.strategies import feature_blocks
-
-            g = out.view(P, -1, self.n)
-            for q, (lo, hi) in enumerate(feature_blocks(self.F, P)):
-                if q != r:
-                    g[q, : hi - lo].copy_(self.ref["fm"][lo:hi])
+        o.copy_(self.ref["rec"][self.lvl].reshape(1, -1).expand(P, -1))
+        self.lvl += 1
         o[r].copy_(inp.reshape(-1))
 
     def all_to_all_device(self, out, inp, out_splits, in_splits):

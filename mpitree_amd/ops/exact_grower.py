@@ -24,11 +24,15 @@ only its contiguous feature block -- setup, scans and partitions all shrink
 with 1/P -- and per level one ``all_gather`` of the per-node split records
 (``fp_combine_kernel``: max gain, ties to the lowest feature) plus one
 ``all_reduce`` of the n-bit row-direction flags (the split feature's owner
-sets them) keep the ranks in lock step. The finisher codes of every block are
-all-gathered once, the jobs are split across ranks (serpentine over the
-largest-first order) and one exchange of the finished position ranges plus
-one of the thresholds each rank resolved leave every rank with the same tree,
-equal to the single-GPU tree bit for bit.
+sets them) keep the ranks in lock step. The jobs are split across ranks
+(serpentine over the largest-first order), one ``all_to_all`` brings every rank
+all features' finisher codes at its own jobs' positions, and one exchange of the
+finished position ranges plus one of the thresholds each rank resolved leave
+every rank with the same tree, equal to the single-GPU tree bit for bit.
+Partition per level: count, per-segment prefix, grid-stride scatter (no
+look-back chain; ``xe_part_count_kernel`` / ``xe_part_prefix_kernel``).
+``fit(checkpoint=...)``: level resume (both list buffers, frontier, position
+space, finisher jobs).
 """
 
 from __future__ import annotations
