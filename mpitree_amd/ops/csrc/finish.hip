@@ -1948,7 +1948,7 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                    const float* xtabf, int xtab_n,
                    int32_t* node_i32, int32_t* node_cnt, int64_t* tasks, int32_t* task_flag,
                    int32_t epoch, int task_cap, int grid, int tiny_rows, int64_t* tiny,
-                   int tiny_grid, int64_t* prof) {
+                   int tiny_grid, int64_t* prof, int tiny_waves) {
   // counter: int32 [8] = {job cursor, tiny count, tiny cursor, -...}, zeroed by the
   // host. node_i32 / node_cnt are indexed by pre-order position (jobs[j][3] is
   // job j's root position); rows a fit never writes keep n = 0 (host memset).
@@ -2024,7 +2024,11 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   if (tiny_rows > 0) {
     if (tiny_sorted) {
       const int cb = code_bytes;
-      int w = getenv_int("MPITREE_TINY_WAVES", tiny_sorted_waves(F, cb));
+      // waves per workgroup: the most that fit a CU (many subtrees: occupancy), or
+      // the caller's request (few subtrees -- a subtree-owning rank -- spread over
+      // more CUs); MPITREE_TINY_WAVES overrides both
+      int w = getenv_int("MPITREE_TINY_WAVES",
+                         tiny_waves > 0 ? tiny_waves : tiny_sorted_waves(F, cb));
       for (int cand : {16, 8, 4, 2, 1}) {  // the largest allowed width <= the request
         if (cand <= w && tiny_sorted_lds(F, cand, cb) <= 160 * 1024) {
           w = cand;

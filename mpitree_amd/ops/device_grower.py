@@ -384,7 +384,7 @@ class DeviceGrower:
         J = int(d_jobs.shape[0])
         if J:
             be.launch_finisher(d_jobs.contiguous(), J, n, self.p, be.pos_rec, be.pos_st,
-                               counter)
+                               counter, share=int(getattr(comm, "world_size", 1) or 1))
 
     def _dp_finish(self, d_jobs, W: int):
         """Data-parallel subtree finishing: each job's rows are spread over the
@@ -449,7 +449,7 @@ class DeviceGrower:
         if be2 is None or be2.device != dev:
             be2 = self._dp_be = hb.HipBackend(dev)
         be2.setup(codes2, codes_fm, y2, be.nbins, n_bins=be.B, n_classes=C, criterion=be.crit)
-        be2.launch_finisher(jobs2[:Jm], Jm, R_tot, p, be.pos_rec, be.pos_st)
+        be2.launch_finisher(jobs2[:Jm], Jm, R_tot, p, be.pos_rec, be.pos_st, share=P)
         self._dp_keep = (codes_r, y_r, codes2, y2, codes_fm, jobs2, seg)
 
     def _exchange_nodes(self):

@@ -667,7 +667,7 @@ class ExactGrower:
             be.lab_shift, be.row_mask, be.y = 24, (1 << 24) - 1, loc["ent"]
         Jm = int(fj.shape[0])
         if Jm:
-            be.launch_finisher(fj, Jm, n, self.p, be.pos_rec, be.pos_st)
+            be.launch_finisher(fj, Jm, n, self.p, be.pos_rec, be.pos_st, share=P)
         if P > 1:  # finished job ranges -> every rank
             check_abort()
             fault_point(comm, "exchange")

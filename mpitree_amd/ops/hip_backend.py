@@ -776,10 +776,15 @@ class HipBackend:
                     "; the tree is incomplete")
 
     def launch_finisher(self, d_jobs, J: int, job_rows: int, params, rec, cnt, counter=None,
-                        grid=None, slot: int = 0):
+                        grid=None, slot: int = 0, share: int = 1):
         """Launch the block + wave finisher kernels on ``J`` device jobs
         (int64 [J][5 + C] = {start, count, depth, root position, buffer, counts},
-        largest first for load balance) writing into position space rec/cnt."""
+        largest first for load balance) writing into position space rec/cnt.
+        ``share`` > 1: this launch grows about 1 / share of the tree's subtrees (a
+        rank of a multi-GPU fit): the tiny-subtree kernel then runs 8-wave
+        workgroups, twice as many as the occupancy-first 16 for 64 features -- its
+        few subtrees spread over more CUs (P = 8 ownership rank 2.01-2.36 ->
+        1.96-1.97 ms; one GPU keeps 16: 3.41 vs 3.58 ms with 8)."""
         if J <= 0:
             return
         C = self.C
@@ -818,7 +823,8 @@ class HipBackend:
                         self.xtabf.data_ptr(), XTAB_N,
                         rec.data_ptr(), cnt.data_ptr(), tasks.data_ptr(), flags.data_ptr(),
                         epoch, task_cap, grid, tiny_rows, tiny.data_ptr(), 4 * N_CU,
-                        0 if prof is None else prof.data_ptr())
+                        0 if prof is None else prof.data_ptr(),
+                        tiny_waves=8 if share > 1 else 0)
         self._fin_keep = (counter, tasks, tiny, d_jobs)
         # the hand-off queue's watchdog word (+ completed tasks), read
         # with the assembly's node-count sync: a finisher that gave up waiting
