@@ -65,8 +65,9 @@ CONFIG_10M = "10M\u00d7128 synthetic, data-parallel histogram all-reduce, 288 GB
 # what actually ran, by the level loop's reported mode (config.name)
 MODE_TEXT = {
     "single-gpu": "one MI355X, no collectives",
-    "subtree-owned": "subtree ownership: replicated levels until >= 4 units per rank, LPT "
-                     "assignment, one RCCL all-gather of finished subtrees",
+    "subtree-owned": "subtree ownership: replicated levels until >= 2-4 units per rank, LPT "
+                     "assignment, each rank writes its subtrees into one node-shared host "
+                     "tree (one RCCL all-gather of segment counts)",
     "replicated": "replicated levels (too few units to switch), one RCCL all-gather of "
                   "finisher subtrees",
     "feature": "feature-parallel split search, one RCCL all-gather of split records per level",
@@ -227,7 +228,20 @@ def main(argv=None):
     else:
         baseline_cfg = CONFIG
     shape = f"{a.n:,}\u00d7{a.features} synthetic" + (" regression" if a.regression else "")
-    cfg_name = f"{shape}, {MODE_TEXT.get(mode, mode)}, {world}\u00d7MI355X"
+    # what the process group saw: backend, ranks and their GPUs (all-gathered), so
+    # a multi-GPU record proves N RCCL ranks on N distinct GPUs
+    from mpitree_amd.parallel.process_group import rank_topology
+
+    topo = rank_topology()
+    mode_text = MODE_TEXT.get(mode, mode)
+    if world > 1 and topo["dist_backend"] != "nccl":
+        # rehearsal: collectives over gloo, ranks sharing the visible GPUs
+        mode_text = mode_text.replace("RCCL", topo["dist_backend"])
+        hw = (f"{world} {topo['dist_backend']} ranks sharing {topo['distinct_gpus']} "
+              f"MI355X (rehearsal, not a multi-GPU run)")
+    else:
+        hw = f"{world}\u00d7MI355X"
+    cfg_name = f"{shape}, {mode_text}, {hw}"
     if rank == 0:
         value = a.n / dt
         out = {
@@ -251,6 +265,11 @@ def main(argv=None):
                        if a.continuous else "256-level quantized features")
                     + ", labels from a random linear + interaction score with Gaussian noise)",
             "materialized": materialized,
+            "dist_backend": topo["dist_backend"],
+            "world_size_seen": topo["world_size_seen"],
+            "distinct_gpus": topo["distinct_gpus"],
+            "rank_devices": [{"rank": r["rank"], "host": r["host"], "device": r["device"],
+                              "pci": r["pci"]} for r in topo["ranks"]],
             "config": {
                 "name": cfg_name,
                 "baseline_config": baseline_cfg,

@@ -199,7 +199,7 @@ def _finalize(ta: TreeArrays, mapper: BinMapper, regression: bool, y_exp: int) -
     return ta
 
 
-def _exact_device_ok(n, F, C, regression, P=1, free_bytes=None) -> bool:
+def _exact_device_ok(n, F, C, regression, P=1, free_bytes=None, comm=None) -> bool:
     """The device-driven exact engine (``ops/exact_grower.py``) takes any
     feature count and any class count below 2^20 on fewer than 2^24 rows (its
     <= 256-row finisher jobs run where the local-code finishers fit: at most 256
@@ -209,7 +209,7 @@ def _exact_device_ok(n, F, C, regression, P=1, free_bytes=None) -> bool:
 
     if not exact_supported(n, C, regression):
         return False
-    return exact_fits_memory(n, F, C, regression, P, free_bytes)
+    return exact_fits_memory(n, F, C, regression, P, free_bytes, comm=comm)
 
 
 def _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t_bin, t_start, F, regression,
@@ -361,7 +361,7 @@ def fit_tree(
 
         if max_bins is None and g_mapper is None and needs_exact(mapper):
             P_fp = comm.world_size if comm.world_size > 1 and F >= comm.world_size else 1
-            if _exact_device_ok(n, F, C, regression, P_fp):
+            if _exact_device_ok(n, F, C, regression, P_fp, comm=comm):
                 # (the bin pass's flags -- non-finite input -- are read after the fit,
                 # so the host enqueues the setup without waiting for them)
                 try:

@@ -180,7 +180,7 @@ def device_loop_supported(be, params, comm) -> bool:
     need = level_loop_bytes(n, F, B, C, reg, fr, be.hip, par)
     if need <= total_device_bytes(be.device) // 64:  # (no free-memory query: ~10 us a fit)
         return True
-    return need <= free_device_bytes(be.device) // 2
+    return need <= agreed_free_bytes(comm, be.device) // 2
 
 
 def slab_rows(n_loc: int) -> int:
@@ -238,6 +238,21 @@ def free_device_bytes(dev) -> int:
         return int(torch.cuda.mem_get_info(dev)[0])
     except Exception:  # pragma: no cover - (no CUDA context: tests on CPU)
         return 1 << 62
+
+
+def agreed_free_bytes(comm, dev) -> int:
+    """Free device bytes an engine decision may use: this rank's own reading
+    on a single-rank fit, the minimum over the ranks otherwise (ranks sharing a
+    card, or a fit near a threshold, read different values -- one rank taking
+    another engine than its peers would mismatch every collective after it).
+    ``MPITREE_FREE_BYTES`` overrides this rank's reading (tests)."""
+    env = os.environ.get("MPITREE_FREE_BYTES")
+    local = int(env) if env else free_device_bytes(dev)
+    if getattr(comm, "world_size", 1) <= 1 or not hasattr(comm, "_all_reduce"):
+        return local
+    import torch.distributed as tdist
+
+    return int(comm._all_reduce(np.array([local], np.int64), op=tdist.ReduceOp.MIN)[0])
 
 
 def exchange_ranges(be, comm, ranges: torch.Tensor, bound: int):
@@ -421,7 +436,8 @@ class DeviceGrower:
         n_send = int(be.n)  # (every local row belongs to at most one job)
         codes_s = hb._workspace(dev, "dp.send", n_send * rb)
         ysz = be.y.element_size()
-        y_s = hb._workspace(dev, "dp.send_y", n_send * ysz).view(be.y.dtype)
+        # (slice first: a grown workspace need not be a multiple of the element size)
+        y_s = hb._workspace(dev, "dp.send_y", n_send * ysz)[: n_send * ysz].view(be.y.dtype)
         y64 = be.y.dtype == torch.int64
         hip.dp_gather(s(), d_jobs.data_ptr(), J, W, C, be.idx.data_ptr(), be.tmp.data_ptr(),
                       int(be.row_mask), be.codes_rm.data_ptr(), rb, be.y.data_ptr(), y64,
@@ -662,6 +678,8 @@ class DeviceGrower:
             ck, rank = self.ckpt, int(getattr(comm, "rank", 0))
             state = None
             if ck is not None:
+                ck.layout = (f"device fr={fr} K={KMAX} I={IMAX} J={JMAX} T={TMAX} M={MMAX} "
+                             f"F={F_h}@{f_lo} W={W} dfree={int(dfree)}")
                 state = ck.load_device(rank, P, (lambda a: comm._all_gather(a)) if P > 1
                                        else None)
             first_lvl = 0  # levels before it ran in an earlier process (resume)

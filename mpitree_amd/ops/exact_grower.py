@@ -111,11 +111,15 @@ def exact_workspace_bytes(n: int, F_loc: int, C: int, regression: bool, fr: int,
 
 
 def exact_fits_memory(n: int, F: int, C: int, regression: bool, P: int = 1,
-                      free_bytes: int | None = None) -> bool:
+                      free_bytes: int | None = None, comm=None) -> bool:
     """Whether the list engine's workspace fits in half of the free device memory
     (else the fit takes 256 quantile bins: ADVICE r4 -- at 1M x 64 with 300
-    classes the no-finisher chunk totals alone would need ~150 GB each)."""
+    classes the no-finisher chunk totals alone would need ~150 GB each). A
+    workspace within 1/64 of the device needs no free-memory query; otherwise a
+    multi-rank fit (``comm``) decides from the minimum over the ranks, so every
+    rank takes the same engine."""
     from . import native
+    from .device_grower import agreed_free_bytes, total_device_bytes
 
     hip = native.hip()
     F_loc = -(-F // max(P, 1))
@@ -123,7 +127,9 @@ def exact_fits_memory(n: int, F: int, C: int, regression: bool, P: int = 1,
     need = exact_workspace_bytes(n, F_loc, C, regression, fr, int(hip.xe_chunk()),
                                  int(hip.xe_rec_width(0 if regression else int(C))))
     if free_bytes is None:
-        free_bytes = int(torch.cuda.mem_get_info()[0])
+        if need <= total_device_bytes(torch.device("cuda", torch.cuda.current_device())) // 64:
+            return True
+        free_bytes = agreed_free_bytes(comm, None)
     return need <= free_bytes // 2
 
 
@@ -426,6 +432,8 @@ class ExactGrower:
         ck = self.ckpt
         state = None
         if ck is not None:
+            # (a state saved with other finisher rows / chunk / buffer sizes is ignored)
+            ck.layout = f"exact fr={fr} chunk={chunk} K={KMAX} I={IMAX} J={JMAX} R={R} F={F_loc}"
             state = ck.load_device(rank, P, (lambda a: comm._all_gather(a)) if P > 1 else None)
         first_lvl = 0  # levels before it ran in an earlier process (resume)
         if state is not None:

@@ -101,6 +101,7 @@ def _workspace(device, name: str, nbytes: int) -> torch.Tensor:
     buf = _workspaces.get(key)
     if buf is None or buf.numel() < nbytes:
         cap = max(int(nbytes), int(1.25 * buf.numel()) if buf is not None else 0, 256)
+        cap = (cap + 255) // 256 * 256  # (any typed view of a full buffer stays aligned)
         buf = _workspaces[key] = torch.empty(cap, dtype=torch.uint8, device=device)
     return buf
 

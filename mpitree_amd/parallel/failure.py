@@ -103,11 +103,21 @@ class _Watcher:
             finally:
                 self.idle.set()
 
-    def arm(self, guard) -> None:
-        self.idle.wait(timeout=10)  # (the previous guard's loop has returned)
+    def arm(self, guard) -> bool:
+        """Hand ``guard`` to the thread; False when the previous guard's loop is
+        still busy after 10 s (a slow store call or a communicator abort): the
+        caller then starts a fresh watcher rather than fit without one."""
+        if not self.idle.wait(timeout=10):  # (the previous guard's loop has returned)
+            return False
         with self.lock:
             self.guard = guard
             self.armed.set()
+        return True
+
+    def is_current(self, guard) -> bool:
+        """Whether ``guard`` is still the armed guard (under the lock)."""
+        with self.lock:
+            return self.guard is guard
 
     def disarm(self, guard) -> None:
         """After ``guard._done`` is set: no further action on its behalf."""
@@ -124,6 +134,18 @@ def _watcher() -> _Watcher:
     w = _WATCHER[0]
     if w is None or w.pid != os.getpid():  # (first use, or a forked child)
         w = _WATCHER[0] = _Watcher()
+    return w
+
+
+def _arm_watcher(guard) -> _Watcher:
+    """Arm the process's watcher for ``guard``; a watcher whose previous loop is
+    stuck is abandoned (it can no longer act: its guard is not current) and a
+    fresh thread takes the fit."""
+    w = _watcher()
+    if not w.arm(guard):
+        logger.warning("fit watchdog busy with a previous fit: starting a fresh one")
+        w = _WATCHER[0] = _Watcher()
+        w.arm(guard)
     return w
 
 
@@ -175,6 +197,8 @@ class FitGuard:
                 if errors < self.STORE_ERRORS:
                     continue
             errors = 0
+            if not self._live():  # (a previous fit's loop: never abort the next fit)
+                return
             ABORT.set()  # host loops raise at their next check
             if seen is None:
                 seen = time.monotonic()
@@ -190,11 +214,15 @@ class FitGuard:
                     pass
                 return
 
+    def _live(self) -> bool:
+        """This guard's fit is running and its watcher still serves it."""
+        w = self._thread
+        return not self._done.is_set() and w is not None and w.is_current(self)
+
     def __enter__(self):
         ABORT.clear()
         if self.store is not None and self.P > 1:
-            self._thread = _watcher()
-            self._thread.arm(self)
+            self._thread = _arm_watcher(self)
         return self
 
     def stop(self) -> None:

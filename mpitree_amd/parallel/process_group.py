@@ -25,6 +25,7 @@ __all__ = [
     "world_size",
     "local_rank",
     "comm_device",
+    "rank_topology",
 ]
 
 DEFAULT_TIMEOUT = datetime.timedelta(seconds=int(os.environ.get("MPITREE_DIST_TIMEOUT", "600")))
@@ -77,3 +78,41 @@ def comm_device() -> torch.device:
     if dist.is_initialized() and dist.get_backend() == "nccl":
         return torch.device("cuda", torch.cuda.current_device())
     return torch.device("cpu")
+
+
+def _device_identity() -> dict:
+    """This process's current GPU as the runtime sees it (None fields on CPU)."""
+    out = {"device": None, "pci": None, "uuid": None, "name": None}
+    if not torch.cuda.is_available():
+        return out
+    d = torch.cuda.current_device()
+    pr = torch.cuda.get_device_properties(d)
+    out["device"] = int(d)
+    out["pci"] = "%04x:%02x:%02x" % (int(getattr(pr, "pci_domain_id", 0)),
+                                     int(getattr(pr, "pci_bus_id", 0)),
+                                     int(getattr(pr, "pci_device_id", 0)))
+    out["uuid"] = str(getattr(pr, "uuid", ""))
+    out["name"] = str(getattr(pr, "gcnArchName", pr.name))
+    return out
+
+
+def rank_topology() -> dict:
+    """What the process group actually saw, for records that must prove it
+    (bench.py): the backend, the world size and every rank's host, current
+    device index and PCI address, all-gathered (a collective: every rank calls
+    it). ``distinct_gpus`` counts different (host, PCI address) pairs -- N ranks
+    of an RCCL run on N distinct GPUs show N; ranks sharing a card (gloo
+    rehearsals) show fewer."""
+    import socket
+
+    me = dict(_device_identity(), rank=world_rank(), host=socket.gethostname())
+    if not (dist.is_available() and dist.is_initialized()):
+        ranks = [me]
+        backend = "none"
+    else:
+        ranks = [None] * dist.get_world_size()
+        dist.all_gather_object(ranks, me)
+        backend = str(dist.get_backend())
+    ids = {(r["host"], r["pci"]) for r in ranks if r["pci"] is not None}
+    return {"dist_backend": backend, "world_size_seen": len(ranks),
+            "distinct_gpus": len(ids), "ranks": ranks}

@@ -87,6 +87,9 @@ class LevelCheckpoint:
         self.fail_after_level = None  # tests: raise after saving this level
         self.saved_levels = 0
         self.resumed_from = None
+        # the saving engine's buffer layout (device loops: finisher rows and buffer
+        # dimensions); a saved state of another layout is ignored, never restored
+        self.layout = ""
 
     # ---------------------------------------------------------------- save
     def save(self, level: int, tab, fr: dict, deferred: dict, rows: np.ndarray) -> None:
@@ -159,6 +162,7 @@ class LevelCheckpoint:
         out["sig"] = np.frombuffer(self.signature.encode(), np.uint8)
         out["level"] = np.array([level], np.int64)
         out["device_loop"] = np.array([1], np.int64)
+        out["layout"] = np.frombuffer(self.layout.encode(), np.uint8)
         tmp = dst + ".tmp.npz"
         np.savez(tmp, **out)
         os.replace(tmp, dst)
@@ -175,7 +179,9 @@ class LevelCheckpoint:
             if not os.path.exists(f):
                 continue
             with np.load(f, allow_pickle=False) as z:
-                if "device_loop" in z.files and bytes(z["sig"]).decode() == self.signature:
+                lay = bytes(z["layout"]).decode() if "layout" in z.files else ""
+                if ("device_loop" in z.files and bytes(z["sig"]).decode() == self.signature
+                        and lay == self.layout):
                     have[int(z["level"][0])] = f
         if world > 1:
             mine = np.full(2, -1, np.int64)

@@ -262,26 +262,44 @@ def test_gpu_exact_feature_parallel_equals_single_gpu(regression, world):
         np.testing.assert_array_equal(o[key], getattr(ref.tree_arrays_, key))
 
 
-def _fit_rank_rccl(rank, world, strategy, regression):
+def _fit_rank_rccl(rank, world, strategy, regression, continuous=False):
     import torch
     import torch.distributed as dist
 
-    from mpitree_amd import ParallelDecisionTreeClassifier, ParallelDecisionTreeRegressor
-    from mpitree_amd.utils.datasets import make_classification, make_regression
+    from mpitree_amd.parallel.process_group import rank_topology
 
     assert dist.get_backend() == "nccl"
     dev = torch.device("cuda", rank)
-    if regression:
-        X, y = make_regression(200_000, 16, levels=64, seed=5, device=dev)
-        cls = ParallelDecisionTreeRegressor
-    else:
-        X, y = make_classification(300_000, 16, seed=5, device=dev)
-        cls = ParallelDecisionTreeClassifier
-    est = cls(strategy=strategy, device="cuda").fit(X, y)
+    # "subtree": the replicated prefix levels forced feature-parallel (the record
+    # all-gather + combine of every prefix level runs over RCCL)
+    os.environ["MPITREE_OWN_FP_PREFIX"] = "1" if strategy == "subtree" else "0"
+    X, y, cls = _rccl_data(regression, continuous, dev)
+    est = cls(strategy=strategy, device="cuda")
+    for _ in range(2):  # (the second fit reuses workspaces, pools and the watchdog)
+        est.fit(X, y)
     ta = est.tree_arrays_
-    out = {k: getattr(ta, k) for k in FIELDS}
-    out["mode"] = np.array([est.fit_stats_.get("mode", "")])
-    return out
+    outs = {k: getattr(ta, k) for k in FIELDS + ("threshold",)}
+    outs["stat"] = ta.value if regression else ta.count
+    outs["mode"] = np.array([est.fit_stats_.get("mode", "")])
+    outs["engine"] = np.array([est.fit_stats_.get("engine", "")])
+    topo = rank_topology()
+    outs["world_seen"] = np.array([topo["world_size_seen"]])
+    outs["gpus"] = np.array([topo["distinct_gpus"]])
+    outs["device"] = np.array([torch.cuda.current_device()])
+    return outs
+
+
+def _rccl_data(regression, continuous, dev):
+    from mpitree_amd import ParallelDecisionTreeClassifier, ParallelDecisionTreeRegressor
+    from mpitree_amd.utils.datasets import make_classification, make_regression
+
+    if regression:
+        X, y = make_regression(200_000, 16, levels=None if continuous else 64, seed=5,
+                               device=dev)
+        return X, y, ParallelDecisionTreeRegressor
+    X, y = make_classification(100_000 if continuous else 300_000, 16,
+                               levels=None if continuous else 256, seed=5, device=dev)
+    return X, y, ParallelDecisionTreeClassifier
 
 
 def _gpus() -> int:
@@ -293,31 +311,65 @@ def _gpus() -> int:
         return 0
 
 
+_RCCL_WORLDS = sorted({2, max(2, min(8, _gpus()))})
+_RCCL_CASES = [
+    # (strategy, regression, continuous, expected mode)
+    ("auto", False, False, "subtree-owned"),
+    ("subtree", False, False, "subtree-owned"),
+    ("feature", False, False, "feature"),
+    ("data", False, False, "data"),
+    ("auto", True, False, "subtree-owned"),
+    ("data", True, False, "data"),
+    ("auto", False, True, "feature"),  # exact engine, feature-parallel lists
+    ("auto", True, True, "feature"),
+]
+
+
 @pytest.mark.gpu
 @pytest.mark.skipif(_gpus() < 2, reason="RCCL needs one GPU per rank (>= 2 visible)")
-@pytest.mark.parametrize("strategy,regression", [("auto", False), ("data", False),
-                                                 ("auto", True), ("data", True)])
-def test_rccl_ranks_equal_single_gpu(strategy, regression):
+@pytest.mark.parametrize("world", _RCCL_WORLDS)
+@pytest.mark.parametrize("strategy,regression,continuous,want", _RCCL_CASES)
+def test_rccl_ranks_equal_single_gpu(world, strategy, regression, continuous, want):
     """Real RCCL (nccl backend, device_id init, on-stream collectives over xGMI):
-    2 ranks on 2 GPUs build the single-GPU tree bit for bit."""
+    2 and min(8, visible) ranks on as many GPUs build the single-GPU tree bit for
+    bit -- subtree ownership (with and without the feature-parallel prefix),
+    feature-parallel, data-parallel (async reduce-to-owner, device all_to_all),
+    and the exact engine's feature-parallel lists (codes all_to_all, flag
+    all-reduce). Every rank reports the world the group saw and a distinct GPU."""
     import torch
 
     from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
-    from mpitree_amd.utils.datasets import make_classification, make_regression
 
-    outs = run_ranks(_fit_rank_rccl, 2, strategy, regression, start_method="spawn",
-                     backend="nccl")
+    if world > _gpus():
+        pytest.skip(f"{world} ranks need {world} GPUs")
+    outs = run_ranks(_fit_rank_rccl, world, strategy, regression, continuous,
+                     start_method="spawn", backend="nccl")
     dev = torch.device("cuda", 0)
-    if regression:
-        X, y = make_regression(200_000, 16, levels=64, seed=5, device=dev)
-        ref = DecisionTreeRegressor(device="cuda").fit(X, y).tree_arrays_
-    else:
-        X, y = make_classification(300_000, 16, seed=5, device=dev)
-        ref = DecisionTreeClassifier(device="cuda").fit(X, y).tree_arrays_
+    X, y, _ = _rccl_data(regression, continuous, dev)
+    cls = DecisionTreeRegressor if regression else DecisionTreeClassifier
+    ref = cls(device="cuda").fit(X, y).tree_arrays_
+    assert sorted(int(o["device"][0]) for o in outs) == list(range(world))
     for o in outs:
-        assert str(o["mode"][0]) == ("data" if strategy == "data" else "subtree-owned")
-        for k in FIELDS:
+        assert int(o["world_seen"][0]) == world and int(o["gpus"][0]) == world
+        assert str(o["mode"][0]) == want, (str(o["mode"][0]), str(o["engine"][0]))
+        for k in FIELDS + ("threshold",):
             np.testing.assert_array_equal(o[k], getattr(ref, k), err_msg=k)
+        np.testing.assert_array_equal(o["stat"], ref.value if regression else ref.count)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(_gpus() < 2, reason="RCCL needs one GPU per rank (>= 2 visible)")
+@pytest.mark.parametrize("where", ["level:2", "exchange"])
+def test_rccl_fault_raises_everywhere(where):
+    """nccl fault injection: rank 1 raises inside the level loop or after the
+    ownership switch; every rank raises within 30 s (the failing rank's
+    communicator abort, or the peer's watchdog aborting its own RCCL
+    communicator -- parallel/failure.py) instead of hanging in a collective."""
+    outs = run_ranks(_fault_mid_loop_gpu, 2, "auto", where, False, start_method="spawn",
+                     backend="nccl")
+    kinds = [str(o["kind"][0]) for o in outs]
+    assert kinds[1] == "injected" and kinds[0] != "ok", kinds
+    assert max(float(o["s"][0]) for o in outs) < 30
 
 
 def _fault_rank(rank, world, fault_rank):
@@ -564,7 +616,7 @@ def _fault_mid_loop_gpu(rank, world, strategy, where, continuous):
     from mpitree_amd.utils.datasets import make_classification
     from mpitree_amd.utils.observability import InjectedFault
 
-    dev = torch.device("cuda", 0)
+    dev = torch.device("cuda", torch.cuda.current_device())  # (nccl: one GPU per rank)
     X, y = make_classification(200_000, 16, levels=None if continuous else 256, seed=7,
                                device=dev)
     os.environ.update(MPITREE_FAULT_RANK="1", MPITREE_FAULT_AT=where, MPITREE_FAIL_WAIT="2")
@@ -602,3 +654,31 @@ def test_gpu_fault_inside_fit_raises_everywhere(strategy, where, continuous):
     kinds = [str(o["kind"][0]) for o in outs]
     assert kinds == ["peer", "injected"], kinds
     assert max(float(o["s"][0]) for o in outs) < 30
+
+
+def _topology_rank(rank, world, agreed):
+    from mpitree_amd.ops.device_grower import agreed_free_bytes
+    from mpitree_amd.parallel.process_group import rank_topology
+    from mpitree_amd.parallel.strategies import FeatureParallelComm
+
+    topo = rank_topology()
+    out = {"backend": np.array([topo["dist_backend"]]),
+           "world": np.array([topo["world_size_seen"]]),
+           "ranks": np.array([r["rank"] for r in topo["ranks"]]),
+           "gpus": np.array([topo["distinct_gpus"]])}
+    if agreed:
+        # ranks reading different free memory decide from the minimum
+        os.environ["MPITREE_FREE_BYTES"] = str((rank + 1) * 1000)
+        out["free"] = np.array([agreed_free_bytes(FeatureParallelComm(), None)])
+    return out
+
+
+def test_rank_topology_and_agreed_free_bytes():
+    """The bench JSON's process-group fields (backend, world size the group saw,
+    every rank's device) over gloo, and the engine choice's free-memory reading
+    agreed as the minimum over the ranks."""
+    outs = run_ranks(_topology_rank, 3, True)
+    for o in outs:
+        assert str(o["backend"][0]) == "gloo" and int(o["world"][0]) == 3
+        assert list(o["ranks"]) == [0, 1, 2]
+        assert int(o["free"][0]) == 1000

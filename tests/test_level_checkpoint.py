@@ -223,3 +223,20 @@ def test_device_checkpoint_every_other_level_keeps_two_generations(tmp_path):
             levels.add(int(z["level"][0]))
     assert levels == {3, 5}
     ck.clear()
+
+
+def test_device_checkpoint_of_other_layout_is_ignored(tmp_path):
+    """A device-loop state saved with other finisher rows / buffer sizes (ADVICE
+    r5: MPITREE_EXACT_FINISHER_ROWS or chunk size changed between the runs) is
+    ignored instead of failing to copy into differently sized buffers."""
+    path = str(tmp_path / "l.npz")
+    ck = LevelCheckpoint(path, "sig")
+    ck.layout = "exact fr=256 K=10"
+    ck.save_device(4, {"x": np.array([4])})
+    same = LevelCheckpoint(path, "sig")
+    same.layout = "exact fr=256 K=10"
+    assert int(same.load_device()["level"][0]) == 4
+    other = LevelCheckpoint(path, "sig")
+    other.layout = "exact fr=0 K=99"
+    assert other.load_device() is None
+    ck.clear()

@@ -54,3 +54,39 @@ def test_peer_failure_sets_abort_while_armed():
     with _guard(store):
         time.sleep(0.05)
         assert not fl.ABORT.is_set()
+
+
+def test_stale_loop_never_aborts_the_next_fit():
+    """A previous fit's loop that sees its own failure counter after that fit
+    ended must not set ABORT for the fit running now."""
+    store = _Store()
+    old = _guard(store)
+    with old:
+        pass
+    store.add(old.pfx + "/nfail", 1)  # the old fit's counter moves late
+    with _guard(store):
+        old._done.clear()  # (as if the old loop were still polling)
+        t = threading.Thread(target=old._watch, daemon=True)
+        t.start()
+        time.sleep(0.1)
+        assert not fl.ABORT.is_set()
+        old._done.set()
+        t.join(2)
+
+
+def test_busy_watcher_is_replaced():
+    """A watcher whose previous loop is stuck is abandoned: the next fit gets a
+    fresh thread instead of running unwatched."""
+    w = fl._watcher()
+    w.idle.clear()  # (stuck in a previous guard's loop)
+    orig = w.idle.wait
+    w.idle.wait = lambda timeout=None: False
+    try:
+        store = _Store()
+        g = _guard(store)
+        with g:
+            assert fl._WATCHER[0] is not w
+            assert fl._WATCHER[0].is_current(g)
+    finally:
+        w.idle.wait = orig
+        w.idle.set()
