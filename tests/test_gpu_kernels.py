@@ -745,7 +745,7 @@ def test_gpu_exact_probe_fallback_and_nonfinite(monkeypatch):
     X[:, 2] = rng.integers(0, 5, size=20000)
     y = (X[:, 0] + X[:, 1] > 0).astype(np.int64) + (X[:, 2] > 2)
     q = DecisionTreeClassifier(max_depth=8, max_bins=256, device="cuda").fit(X, y)
-    monkeypatch.setattr(fit_mod, "_exact_device_ok", lambda *a: False)
+    monkeypatch.setattr(fit_mod, "_exact_device_ok", lambda *a, **k: False)
     g = DecisionTreeClassifier(max_depth=8, device="cuda").fit(X, y)
     assert g.fit_stats_["engine"] != "hip-exact"
     assert g.tree_arrays_.equal(q.tree_arrays_)
