@@ -105,16 +105,20 @@ def hist_items_per_cu(reg: bool) -> int:
 def fp_prefix_pays(n: int, F: int, P: int, reg: bool) -> bool:
     """Whether the replicated levels before the ownership switch run
     feature-parallel (``MPITREE_OWN_FP_PREFIX`` = 1 / 0 forces it). A rank then
-    histograms 1 / P of the features -- saving (1 - 1/P) of a level's histogram
-    build, ~0.6 ps (classification) / ~3 ps (regression: int64 slabs) per
-    row x feature at the top levels (profiles/r5/) -- but each level adds a
-    record all-gather, a select and a combine (~40 us with RCCL latency). The
-    1M x 64 classification tree breaks even at P = 8; its regression tree and
-    10M-row fits gain."""
+    histograms 1 / P of the features -- saving (1 - 1/P) of a level's per-row x
+    feature histogram cost -- but each level adds a record all-gather, a select
+    and a combine (~40 us with RCCL latency, an estimate: no multi-GPU box has
+    measured it). The per-row x feature costs are measured, not assumed:
+    ``bench/calib_hist.py`` fits the level-0 histogram (items + slab reduction)
+    as ``a + b rows x features`` over 250k..4M rows x 16..128 features --
+    classification b = 0.56 ps (a = 20 us), regression (int64 {count, sum} slabs)
+    b = 1.38 ps (a = 74 us), ``profiles/r6/calib_hist.jsonl``. The 1M x 64
+    classification tree breaks even at P = 8 and stays replicated; its regression
+    tree and 10M-row fits gain."""
     env = os.environ.get("MPITREE_OWN_FP_PREFIX")
     if env is not None:
         return env != "0"
-    per = 3.1e-12 if reg else 0.625e-12  # (s per row x feature of one level)
+    per = 1.38e-12 if reg else 0.56e-12  # (s per row x feature of one level, measured)
     return (1.0 - 1.0 / max(P, 1)) * n * F * per > 40e-6
 
 
