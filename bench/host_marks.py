@@ -69,7 +69,13 @@ def main():
     for obj, name in [(gp, "prepare"), (hb.HipBackend, "setup"), (hb.HipBackend, "begin_positions"),
                       (dg, "device_loop_supported"), (dg.DeviceGrower, "fit"),
                       (dg.DeviceGrower, "_workspace"), (hb.HipBackend, "assemble_positions"),
-                      (hb.HipBackend, "launch_finisher")]:
+                      (hb.HipBackend, "launch_finisher"),
+                      (gp._Labels, "__init__"), (gp._Labels, "after_first_sync"),
+                      (gp._Labels, "finish"), (hb.DeviceBinning, "__init__"),
+                      (hb.DeviceBinning, "launch_bin_early"), (hb.DeviceBinning, "launch_bin"),
+                      (hb.DeviceBinning, "finish"), (torch.cuda.Event, "synchronize"),
+                      (torch.cuda.Event, "record"), (fitmod, "_validate_X"),
+                      (fitmod, "resolve_device"), (fitmod, "_level_checkpoint")]:
         _wrap(obj, name, f"{getattr(obj, '__name__', '')}.{name}")
     orig_ctx = None
     from mpitree_amd.ops import native

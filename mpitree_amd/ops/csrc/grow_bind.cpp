@@ -228,6 +228,9 @@ void bind_grow(py::module_& m) {
         }
         return c;
       }), py::arg("args"), py::arg("l0"), py::arg("l1"), py::arg("own") = py::dict())
+      // a context reused by the next fit of the same workspace: only the host
+      // slot tag changes (the caller checks every other field is unchanged)
+      .def("set_tag0", [](GrowCtx& c, int64_t tag0) { c.tag0 = (int32_t)tag0; })
       .def("level", [](GrowCtx& c, uintptr_t s, int lvl) {
         c.level(reinterpret_cast<hipStream_t>(s), lvl);
       });

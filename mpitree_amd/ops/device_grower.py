@@ -731,6 +731,20 @@ class DeviceGrower:
             # kernels, no per-phase profile events): one C++ call enqueues a level
             ctx = None
             if not (dp or fp or prof) and os.environ.get("MPITREE_LEVEL_CTX", "1") != "0":
+                # the workspace's context is reused when nothing but the host slot
+                # tag differs from the last fit (building its ~60 fields costs ~30 us
+                # of host time while the GPU waits for the first level)
+                ctx_key = (bufs, be.codes_rm.data_ptr(), be.codes_fm.data_ptr(),
+                           be.y.data_ptr(), be.pos_rec.data_ptr(), be.pos_st.data_ptr(),
+                           be.nbins.data_ptr(), be.xtab.data_ptr(), hctl_dev, cb, rs,
+                           be.lab_shift, be.row_mask, be.n, int(be.crit), md, mss, msl,
+                           plan_cu, hb.LDS_BUDGET, tuple(sorted(own_args.items())))
+                cached = ws.get("ctx")
+                if cached is not None and cached[0] == ctx_key:
+                    ctx = cached[1]
+                    ctx.set_tag0(tag0)
+            if ctx is None and not (dp or fp or prof) and os.environ.get(
+                    "MPITREE_LEVEL_CTX", "1") != "0":
                 ctx = hip.GrowCtx(dict(
                     hist0=hists[0].data_ptr(), hist1=hists[1].data_ptr(), idx=bufs[0],
                     tmp=bufs[1], codes_rm=be.codes_rm.data_ptr(),
@@ -748,6 +762,7 @@ class DeviceGrower:
                     PMAX=PMAX, MMAX=MMAX, tag0=tag0, derive_free=int(dfree),
                     **(dict(sel_left=ws["sel_left"].data_ptr(), sel_tot=ws["sel_tot"].data_ptr())
                        if fsel else {})), ptrs[0], ptrs[1], own_args)
+                ws["ctx"] = (ctx_key, ctx)
 
             def plan(cur, nxt, lvl, fixup=False):
                 hip.grow_plan(s(), cur, nxt, rec.data_ptr(), split.data_ptr(), pitems.data_ptr(),

@@ -30,7 +30,7 @@ import numpy as np
 import torch
 
 from . import native
-from .hip_backend import DeviceBinning, _pinned_copy, _stream, _uploader
+from .hip_backend import DeviceBinning, _event, _pinned_copy, _stream, _uploader
 
 __all__ = ["Prepared", "prepare"]
 
@@ -211,12 +211,16 @@ def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
     n = Xd.shape[0]
     dev = Xd.device
     stream = torch.cuda.current_stream(dev)
+    # the edges kernel first: the label / target kernels and their host-side
+    # setup (~40 us of host time) then overlap it instead of delaying it. (A side
+    # stream for the label pass, so the bin kernel could follow the edges at
+    # once, measured 0.35 ms slower per flagship fit.)
+    binning = DeviceBinning(Xd, max_bins, probe=exact_probe)
     lab = (_Targets(y, n, dev, encode_targets, exponent) if regression
            else _Labels(y, n, dev, encode_labels))
-    binning = DeviceBinning(Xd, max_bins, probe=exact_probe)
     early = binning.early
     if early:  # <= 256 bins: the bin kernel reads the bin counts on the device
-        tables = torch.cuda.Event()
+        tables = _event(dev, "prep.tables")
         tables.record(stream)  # edge table + label count copies are enqueued before it
         binning.launch_bin_early()
         if sync:

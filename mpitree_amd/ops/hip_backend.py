@@ -203,7 +203,7 @@ class DeviceBinning:
         self.codes_rm, self.codes_fm, flags = self._run_bin(self.edges, self.nb, self.exact,
                                                             self.limit, skip_inexact=self.probe)
         self._host_flags = _pinned_copy(flags, "bin.flags")
-        self._flags_ready = torch.cuda.Event()
+        self._flags_ready = _event(self.dev, "bin.flags")
         self._flags_ready.record(torch.cuda.current_stream(self.dev))
         self._launched = True
 
@@ -350,6 +350,19 @@ def _task_flags(device, n: int, slot: int = 0):
         ent = _TASK_FLAGS[key] = [torch.zeros(max(n, 4096), dtype=torch.int32, device=device), 0]
     ent[1] = ent[1] % 0x7FFFFFFE + 1
     return ent[0], ent[1]
+
+
+_events: dict = {}
+
+
+def _event(device, key: str) -> torch.cuda.Event:
+    """A reusable event per (device, purpose): fits record and wait on it in
+    order, and creating one costs host time on the path to the first level."""
+    k = (str(device), key)
+    ev = _events.get(k)
+    if ev is None:
+        ev = _events[k] = torch.cuda.Event()
+    return ev
 
 
 def _pinned_copy(t: torch.Tensor, key: str) -> np.ndarray:
