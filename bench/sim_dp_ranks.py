@@ -13,15 +13,20 @@ Rank r's kernel sequence depends on the other ranks only through those
 collectives, so it runs alone here with a stand-in communicator that answers
 them from a single-GPU reference fit of the same data:
 
-* the block reduce returns the reference's (global) built histograms of the
-  rank's feature block for that level;
+* the level's reduce-scatter (or, for unequal feature blocks, the block reduce)
+  returns the reference's (global) built histograms of the rank's feature block
+  for that level;
 * the record all-gather returns the reference's per-node best records (the
   combine picks the global best, ties to the lower feature, as with real peers);
 * the job-row count all-gather returns every rank's rows of each job (from the
   reference's job segments), the all_to_all the other ranks' rows of the rank's
   jobs (ascending row order within a source, as each peer's stable partitions
   keep them);
-* the finished-node exchange returns the reference's nodes.
+* the finished nodes: with the node-shared host tree (the default on one node)
+  the segment-count all-gather returns every job's node count from the
+  reference positions and the shared buffer already holds the reference tree,
+  so the rank writes only its own jobs' nodes (``sim_own_ranks.SimPool``);
+  ``--no-shared`` keeps the node all-gather, answered with the reference's nodes.
 
 The simulated rank must rebuild the reference tree bit for bit (checked). Per P
 it reports the max / mean over ranks of the median fit time and the bytes the
@@ -45,6 +50,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from mpitree_amd.core.levelwise import LocalComm  # noqa: E402
+from mpitree_amd.parallel.shared_tree import GATHER_HDR  # noqa: E402
 
 
 class SimDPComm(LocalComm):
@@ -59,12 +65,16 @@ class SimDPComm(LocalComm):
         self.bytes_communicated = 0
         self.bytes = dict(reduce=0, records=0, counts=0, rows=0, nodes=0)
         self._red = 0  # block reduces so far (P per level)
+        self._rs = 0  # reduce-scatters so far (one per level)
         self._gat = 0  # record all-gathers so far (one per level)
-        self._shm_pool = False
+        self._shm_pool = False  # (main sets the shared-tree stand-in)
         self._finishing = False  # set once the level loop is over (job row counts)
 
     def note_phase(self, name):
         self._finishing = name == "dp_finish"
+
+    def _all_reduce(self, a, op=None):  # (the bin flags: every shard agrees here)
+        return a
 
     def local_rows(self, n):
         P, r = self.world_size, self.rank
@@ -84,6 +94,18 @@ class SimDPComm(LocalComm):
             k = min(nb, H.shape[0])
             t[:k].copy_(H[:k, lo:hi])
         return None
+
+    def reduce_scatter_device(self, out, inp):
+        # one per level: this rank's block of the reference's global built histograms
+        lvl = self._rs
+        self._rs += 1
+        self.bytes["reduce"] += inp.numel() * inp.element_size()
+        if lvl < len(self.ref["hists"]):  # (else: a lagged empty level)
+            lo, hi = self.ref["blocks"][self.rank]
+            H = self.ref["hists"][lvl]
+            o = out.view(-1, hi - lo, H.shape[2], H.shape[3])
+            k = min(o.shape[0], H.shape[0])
+            o[:k].copy_(H[:k, lo:hi])
 
     def all_gather_device(self, out, inp):
         P = self.world_size
@@ -116,6 +138,16 @@ class SimDPComm(LocalComm):
     def all_gather_rows(self, t):
         self.bytes["nodes"] += self.ref["rows"].numel() * self.ref["rows"].element_size()
         return torch.cat([t, self.ref["rows"].to(t.dtype)], 0)
+
+    def all_gather_seg_counts(self, out, inp, segs, S):
+        # every rank's row: its jobs' node counts (from the reference positions)
+        P, W = self.world_size, inp.numel()
+        g = out.view(P, W)
+        cnt = torch.searchsorted(self.ref["pos"], segs[:S, :2].contiguous()).diff(dim=1)[:, 0]
+        mine = segs[:S, 2][None, :] == torch.arange(P, device=segs.device)[:, None]
+        g[:, GATHER_HDR : GATHER_HDR + S] = mine * cnt[None, :]
+        g[:, :GATHER_HDR] = self.ref["head"]
+        self.bytes["nodes"] += P * W * 8
 
 
 def reference(fit, dev, X, y, P, F):
@@ -179,7 +211,11 @@ def main():
     ap.add_argument("--ranks", default="2+4+8")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--only-rank", type=int, default=None)
+    ap.add_argument("--no-shared", action="store_true",
+                    help="node all-gather instead of the node-shared host tree")
     a = ap.parse_args()
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from sim_own_ranks import SimPool, SimSlot, packed_bytes
     from mpitree_amd.core.fit import fit_tree
     from mpitree_amd.ops import gpu_prepare
     from mpitree_amd.utils.datasets import make_classification
@@ -212,6 +248,10 @@ def main():
     for P in [int(v) for v in a.ranks.replace("+", ",").split(",")]:
         ref = reference(fit, dev, X, y, P, a.features)
         ref["root"] = np.bincount(y.cpu().numpy(), minlength=2).astype(np.int64)
+        ref["pos"] = ref["rows"][:, 0].long().contiguous()  # live positions, ascending
+        ref["head"] = torch.tensor([int(ref["fit"].arrays.max_depth), 1, 1 << 62],
+                                   dtype=torch.int64, device=dev)
+        pool = None if a.no_shared else SimPool(SimSlot(packed_bytes(ref["fit"].arrays)))
         per_rank = []
         for r in range(P) if a.only_rank is None else [a.only_rank]:
             ref["recv_codes"] = {r: None}
@@ -220,6 +260,9 @@ def main():
             times, comm = [], None
             for i in range(a.reps + 1):
                 comm = SimDPComm(P, r, dev, ref)
+                if pool is not None:
+                    comm._shm_pool = pool
+                    pool.slot.prefill()
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 res = fit(comm)

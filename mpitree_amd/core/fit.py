@@ -328,6 +328,17 @@ def fit_tree(
             Xd = Xd.double()
         Xd = Xd.contiguous()
         t0 = time.perf_counter()
+        # a data-parallel rank of a replicated input bins only its own row shard
+        # (the edges still come from every row, so all ranks derive one table; the
+        # bin flags -- a missed exact value, non-finite input -- are combined over
+        # the ranks before anyone grows)
+        bin_rows, bin_agree = None, None
+        lo, hi = comm.local_rows(n)
+        if (lo, hi) != (0, n) and g_mapper is None:
+            import torch.distributed as tdist
+
+            bin_rows = (lo, hi)
+            bin_agree = lambda fl: comm._all_reduce(fl, op=tdist.ReduceOp.MAX)  # noqa: E731
         with roctx_range("mpitree.bin"):
             if g_mapper is not None:  # globally agreed edges / encodings (row shards)
                 from ..ops.gpu_prepare import prepare_with_mapper
@@ -344,7 +355,7 @@ def fit_tree(
                                max_bins=256 if max_bins is None else max_bins,
                                encode_labels=_encode_labels, encode_targets=_encode_targets,
                                exponent=fixed_point_exponent, sync=_sync_prepare,
-                               exact_probe=probe)
+                               exact_probe=probe, rows=bin_rows, agree=bin_agree)
                 if prep.verify is not None:
                     # the bin kernel's flags are read after growth (see prepare): a
                     # sampled exact-mode feature that missed a value redoes the fit
@@ -384,14 +395,15 @@ def fit_tree(
             if probe:  # the probe left out the quantile edges and the codes: bin again
                 prep = prepare(Xd, y, regression=regression, max_bins=256,
                                encode_labels=_encode_labels, encode_targets=_encode_targets,
-                               exponent=fixed_point_exponent, sync=True)
+                               exponent=fixed_point_exponent, sync=True, rows=bin_rows,
+                               agree=bin_agree)
                 mapper, codes_rm, codes_fm, nb = (prep.mapper, prep.codes_rm, prep.codes_fm,
                                                   prep.nbins)
                 yd, classes, y_exp, root = prep.y, prep.classes, prep.y_exp, prep.root
-        lo, hi = comm.local_rows(n)
         if (lo, hi) != (0, n):  # data-parallel shard of a replicated input
-            codes_rm = codes_rm[lo:hi].contiguous()
-            codes_fm = codes_fm[:, lo:hi].contiguous()
+            if bin_rows is None:  # (binned every row: keep this rank's)
+                codes_rm = codes_rm[lo:hi].contiguous()
+                codes_fm = codes_fm[:, lo:hi].contiguous()
             yd = yd[lo:hi]
             root = None
         yd = yd.contiguous()

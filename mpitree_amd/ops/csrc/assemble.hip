@@ -520,6 +520,7 @@ __global__ __launch_bounds__(256) void shm_seg_count_kernel(const int64_t* __res
 }
 
 constexpr int kShmMaxSegs = 4096;  // 2 per ownership unit (grow.hip kOwnMax = 2048)
+int shm_max_segs() { return kShmMaxSegs; }
 
 // One workgroup: every segment's count (summed over the gathered rows: one owner
 // each), the segments sorted by lo (bitonic, LDS), the running count of other

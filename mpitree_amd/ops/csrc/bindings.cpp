@@ -97,12 +97,13 @@ void launch_dp_plan(hipStream_t, const int64_t*, int, int, int, const int64_t*, 
                     int64_t*, int64_t*, int64_t*, int64_t*);
 void launch_dp_gather(hipStream_t, const int64_t*, int, int, int, const uint32_t*,
                       const uint32_t*, uint32_t, const uint8_t*, int64_t, const void*, bool,
-                      const int64_t*, uint8_t*, void*);
+                      const int64_t*, uint8_t*, void*, int64_t);
 void launch_dp_place(hipStream_t, const int64_t*, int64_t, const uint8_t*, const void*, bool,
-                     int64_t, uint8_t*, void*);
+                     int64_t, int64_t, int, int, uint8_t*, void*, void*);
 void launch_targets(hipStream_t, const void*, bool, int64_t, int64_t*, int64_t*);
 void launch_shm_seg_count(hipStream_t, const int64_t*, int, int, const int32_t*, int64_t,
                           const int64_t*, int64_t*);
+int shm_max_segs();
 void launch_shm_seg_prefix(hipStream_t, const int64_t*, int, int, const int64_t*, int, int,
                            int64_t*, int64_t*);
 }  // namespace mt
@@ -426,16 +427,19 @@ PYBIND11_MODULE(_hip, m) {
   m.def("dp_gather", [](uintptr_t s, uintptr_t jobs, int J, int W, int C, uintptr_t idx,
                         uintptr_t tmp, uint32_t row_mask, uintptr_t codes_rm, int64_t row_bytes,
                         uintptr_t y, bool y64, uintptr_t soff, uintptr_t out_codes,
-                        uintptr_t out_y) {
+                        uintptr_t out_y, int64_t max_rows) {
+    // max_rows: a bound on every job's local rows (the grid's row-tile extent)
     mt::launch_dp_gather(S(s), P<int64_t>(jobs), J, W, C, P<uint32_t>(idx), P<uint32_t>(tmp),
                          row_mask, P<uint8_t>(codes_rm), row_bytes, P<void>(y), y64,
-                         P<int64_t>(soff), P<uint8_t>(out_codes), P<void>(out_y));
+                         P<int64_t>(soff), P<uint8_t>(out_codes), P<void>(out_y), max_rows);
   });
+  // received rows -> job-contiguous row-major and feature-major codes + targets
   m.def("dp_place", [](uintptr_t s, uintptr_t seg, int64_t nseg, uintptr_t in_codes,
-                       uintptr_t in_y, bool y64, int64_t row_bytes, uintptr_t out_codes,
-                       uintptr_t out_y) {
+                       uintptr_t in_y, bool y64, int64_t row_bytes, int64_t rows, int F, int cb,
+                       uintptr_t out_rm, uintptr_t out_fm, uintptr_t out_y) {
     mt::launch_dp_place(S(s), P<int64_t>(seg), nseg, P<uint8_t>(in_codes), P<void>(in_y), y64,
-                        row_bytes, P<uint8_t>(out_codes), P<void>(out_y));
+                        row_bytes, rows, F, cb, P<uint8_t>(out_rm), P<void>(out_fm),
+                        P<void>(out_y));
   });
   // node-local shared-host assembly (parallel/shared_tree.py)
   m.def("shm_seg_count", [](uintptr_t s, uintptr_t segs, int S_, int me, uintptr_t rank,
@@ -443,6 +447,7 @@ PYBIND11_MODULE(_hip, m) {
     mt::launch_shm_seg_count(S(s), P<int64_t>(segs), S_, me, P<int32_t>(rank), npos,
                              P<int64_t>(total), P<int64_t>(gvec));
   });
+  m.def("shm_max_segs", &mt::shm_max_segs);  // segments one shared assembly can sort
   m.def("shm_seg_prefix", [](uintptr_t s, uintptr_t gall, int nranks, int W, uintptr_t segs,
                              int S_, int me, uintptr_t total, uintptr_t tab) {
     mt::launch_shm_seg_prefix(S(s), P<int64_t>(gall), nranks, W, P<int64_t>(segs), S_, me,

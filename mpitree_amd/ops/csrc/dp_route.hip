@@ -15,7 +15,7 @@
 //                      received rows;
 //   dp_gather_kernel   this rank's rows of every job -> the send buffer (row-
 //                      major codes + targets), grouped by destination rank;
-//   dp_place_kernel    received segments -> job-contiguous rows.
+//   dp_place_kernel    received rows -> job-contiguous rows (row- and feature-major).
 //
 // One host wait remains: all_to_all needs the split sizes on the host.
 #include "common.h"
@@ -176,50 +176,102 @@ __global__ __launch_bounds__(kDpThreads) void dp_plan_kernel(
   }
 }
 
-// One workgroup per job: this rank's rows of job j (entries of idx or tmp from
-// the job's local start; the low bits hold the row) -> send rows soff[j] + i.
-// Rows (padded to 4-byte words) are copied a word per thread, plus the target.
+// This rank's rows of job j (entries of idx or tmp from the job's local start;
+// the low bits hold the row) -> send rows soff[j] + i. Workgroup (x, j) copies
+// rows [64 y, 64 y + 64) of job x (the grid's y extent bounds every job's local
+// rows; surplus workgroups exit), 32 threads per 128-byte row slice: coalesced
+// loads and stores, and every CU busy (one workgroup per job left most idle).
 template <typename YT>
 __global__ __launch_bounds__(256) void dp_gather_kernel(
     const int64_t* __restrict__ jobs, int W, int C, const uint32_t* __restrict__ idx,
     const uint32_t* __restrict__ tmp, uint32_t row_mask, const uint8_t* __restrict__ codes_rm,
     int64_t row_bytes, const YT* __restrict__ y, const int64_t* __restrict__ soff,
     uint8_t* __restrict__ out_codes, YT* __restrict__ out_y) {
+  __shared__ uint32_t s_row[64];
   const int j = blockIdx.x;
   const int64_t* J = jobs + (int64_t)j * W;
   const int64_t start = J[0], cnt = J[5 + C];
+  const int64_t i0 = (int64_t)blockIdx.y * 64;
+  if (i0 >= cnt) return;  // (block-uniform)
   const uint32_t* src = J[4] == 0 ? idx : tmp;
   const int64_t o = soff[j];
-  const int chunks = (int)(row_bytes / 4);
-  const int64_t total = cnt * chunks;
-  for (int64_t t = threadIdx.x; t < total; t += 256) {
-    const int64_t i = t / chunks;
-    const int c = (int)(t - i * chunks);
-    const uint32_t row = src[start + i] & row_mask;
-    const uint32_t v = reinterpret_cast<const uint32_t*>(codes_rm + (int64_t)row * row_bytes)[c];
-    reinterpret_cast<uint32_t*>(out_codes + (o + i) * row_bytes)[c] = v;
-    if (c == 0) out_y[o + i] = y[row];
+  const int tid = threadIdx.x;
+  const int nr = cnt - i0 < 64 ? (int)(cnt - i0) : 64;
+  if (tid < nr) {
+    const uint32_t row = src[start + i0 + tid] & row_mask;
+    s_row[tid] = row;
+    out_y[o + i0 + tid] = y[row];
+  }
+  __syncthreads();
+  const int words = (int)(row_bytes / 4);
+  for (int e = tid; e < nr * 32; e += 256) {
+    const int r = e >> 5, w0 = e & 31;
+    const uint32_t* in = reinterpret_cast<const uint32_t*>(codes_rm + (int64_t)s_row[r] * row_bytes);
+    uint32_t* out = reinterpret_cast<uint32_t*>(out_codes + (o + i0 + r) * row_bytes);
+    for (int w = w0; w < words; w += 32) out[w] = in[w];
   }
 }
 
-// One workgroup per (owned job, source) segment: received rows -> new rows.
-template <typename YT>
-__global__ __launch_bounds__(256) void dp_place_kernel(const int64_t* __restrict__ seg,
-                                                       const uint8_t* __restrict__ in_codes,
-                                                       const YT* __restrict__ in_y,
-                                                       int64_t row_bytes,
-                                                       uint8_t* __restrict__ out_codes,
+// Received rows -> the owner's job-contiguous rows, in both code layouts the
+// finisher reads (row-major and feature-major) plus the targets. One workgroup
+// per 64 destination rows: each row's source (received) row comes from a binary
+// search over the segments -- {received offset, new offset, rows}, k-major, so
+// their new offsets ascend and tile [0, R) -- the tile's rows are staged through
+// LDS 32 words at a time (one 128-byte row slice per 32 threads: coalesced loads
+// and row-major stores), and each feature's 64 codes go out as one coalesced run
+// per wave (lanes = consecutive rows), which replaces a strided device transpose.
+template <typename CT, typename YT>
+__global__ __launch_bounds__(256) void dp_place_kernel(const int64_t* __restrict__ seg, int64_t nseg,
+                                                       int64_t R, const uint8_t* __restrict__ in_codes,
+                                                       const YT* __restrict__ in_y, int row_bytes,
+                                                       int F, uint8_t* __restrict__ out_rm,
+                                                       CT* __restrict__ out_fm,
                                                        YT* __restrict__ out_y) {
-  const int64_t* sg = seg + (int64_t)blockIdx.x * 3;
-  const int64_t a = sg[0], b = sg[1], cnt = sg[2];
-  const int chunks = (int)(row_bytes / 4);
-  const int64_t total = cnt * chunks;
-  for (int64_t t = threadIdx.x; t < total; t += 256) {
-    const int64_t i = t / chunks;
-    const int c = (int)(t - i * chunks);
-    reinterpret_cast<uint32_t*>(out_codes + (b + i) * row_bytes)[c] =
-        reinterpret_cast<const uint32_t*>(in_codes + (a + i) * row_bytes)[c];
-    if (c == 0) out_y[b + i] = in_y[a + i];
+  __shared__ int64_t s_src[64];
+  __shared__ uint32_t s_tile[64 * 33];  // 64 rows x 32 words (+1: conflict-free column reads)
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * 64;
+  if (tid < 64) {
+    const int64_t d = r0 + tid;
+    int64_t src = -1;
+    if (d < R) {
+      int64_t lo = 0, hi = nseg - 1;  // last segment with new offset <= d
+      while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (seg[mid * 3 + 1] <= d) lo = mid; else hi = mid - 1;
+      }
+      src = seg[lo * 3 + 0] + (d - seg[lo * 3 + 1]);
+      out_y[d] = in_y[src];
+    }
+    s_src[tid] = src;
+  }
+  __syncthreads();
+  const int words = row_bytes / 4;
+  constexpr int kEpw = 4 / (int)sizeof(CT);  // codes per word
+  const int i = tid & 63;                    // feature-major phase: this lane's row
+  for (int w0 = 0; w0 < words; w0 += 32) {
+    const int nw = words - w0 < 32 ? words - w0 : 32;
+    for (int e = tid; e < 64 * 32; e += 256) {
+      const int r = e >> 5, w = e & 31;
+      const int64_t sr = s_src[r];
+      uint32_t v = 0u;
+      if (w < nw && sr >= 0) {
+        v = reinterpret_cast<const uint32_t*>(in_codes + sr * row_bytes)[w0 + w];
+        reinterpret_cast<uint32_t*>(out_rm + (r0 + r) * row_bytes)[w0 + w] = v;
+      }
+      s_tile[r * 33 + w] = v;
+    }
+    __syncthreads();
+    const int e0 = w0 * kEpw;
+    const int ne = nw * kEpw;
+    if (r0 + i < R) {
+      for (int fe = tid >> 6; fe < ne && e0 + fe < F; fe += 4) {
+        const uint32_t word = s_tile[i * 33 + fe / kEpw];
+        out_fm[(int64_t)(e0 + fe) * R + r0 + i] =
+            (CT)(word >> (8 * (int)sizeof(CT) * (fe % kEpw)));
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -235,30 +287,36 @@ void launch_dp_plan(hipStream_t stream, const int64_t* jobs, int J, int W, int C
 void launch_dp_gather(hipStream_t stream, const int64_t* jobs, int J, int W, int C,
                       const uint32_t* idx, const uint32_t* tmp, uint32_t row_mask,
                       const uint8_t* codes_rm, int64_t row_bytes, const void* y, bool y64,
-                      const int64_t* soff, uint8_t* out_codes, void* out_y) {
-  if (J <= 0) return;
+                      const int64_t* soff, uint8_t* out_codes, void* out_y, int64_t max_rows) {
+  if (J <= 0 || max_rows <= 0) return;
   if (row_bytes % 4) throw std::runtime_error("data-parallel routing: row bytes % 4 != 0");
+  if (max_rows > 65535 * 64) throw std::runtime_error("data-parallel routing: job too large");
+  const dim3 g((unsigned)J, (unsigned)((max_rows + 63) / 64));
   if (y64)
-    hipLaunchKernelGGL(dp_gather_kernel<int64_t>, dim3(J), dim3(256), 0, stream, jobs, W, C, idx,
+    hipLaunchKernelGGL(dp_gather_kernel<int64_t>, g, dim3(256), 0, stream, jobs, W, C, idx,
                        tmp, row_mask, codes_rm, row_bytes, (const int64_t*)y, soff, out_codes,
                        (int64_t*)out_y);
   else
-    hipLaunchKernelGGL(dp_gather_kernel<int32_t>, dim3(J), dim3(256), 0, stream, jobs, W, C, idx,
+    hipLaunchKernelGGL(dp_gather_kernel<int32_t>, g, dim3(256), 0, stream, jobs, W, C, idx,
                        tmp, row_mask, codes_rm, row_bytes, (const int32_t*)y, soff, out_codes,
                        (int32_t*)out_y);
   MT_HIP_CHECK(hipGetLastError());
 }
 
 void launch_dp_place(hipStream_t stream, const int64_t* seg, int64_t nseg, const uint8_t* in_codes,
-                     const void* in_y, bool y64, int64_t row_bytes, uint8_t* out_codes,
-                     void* out_y) {
-  if (nseg <= 0) return;
-  if (y64)
-    hipLaunchKernelGGL(dp_place_kernel<int64_t>, dim3((unsigned)nseg), dim3(256), 0, stream, seg,
-                       in_codes, (const int64_t*)in_y, row_bytes, out_codes, (int64_t*)out_y);
-  else
-    hipLaunchKernelGGL(dp_place_kernel<int32_t>, dim3((unsigned)nseg), dim3(256), 0, stream, seg,
-                       in_codes, (const int32_t*)in_y, row_bytes, out_codes, (int32_t*)out_y);
+                     const void* in_y, bool y64, int64_t row_bytes, int64_t R, int F, int cb,
+                     uint8_t* out_rm, void* out_fm, void* out_y) {
+  if (nseg <= 0 || R <= 0) return;
+  if (row_bytes % 4) throw std::runtime_error("data-parallel placement: row bytes % 4 != 0");
+  const dim3 g((unsigned)((R + 63) / 64));
+#define MT_DP_PLACE(CT, YT)                                                                  \
+  hipLaunchKernelGGL((dp_place_kernel<CT, YT>), g, dim3(256), 0, stream, seg, nseg, R, in_codes, \
+                     (const YT*)in_y, (int)row_bytes, F, out_rm, (CT*)out_fm, (YT*)out_y)
+  if (cb == 1 && y64) MT_DP_PLACE(uint8_t, int64_t);
+  else if (cb == 1) MT_DP_PLACE(uint8_t, int32_t);
+  else if (y64) MT_DP_PLACE(uint16_t, int64_t);
+  else MT_DP_PLACE(uint16_t, int32_t);
+#undef MT_DP_PLACE
   MT_HIP_CHECK(hipGetLastError());
 }
 

@@ -28,13 +28,13 @@ the stream between the level kernels, never a host round trip):
   only; one ``all_gather_into_tensor`` of the per-node split records per level
   feeds ``fp_combine_kernel`` (max gain, ties to the lowest feature), after
   which the planner and partition run identically on every rank;
-* data-parallel (``strategy="data"``): rows sharded. Each level's built
-  (smaller-child) histograms are built one destination feature block at a
-  time, and each block is summed into its owner rank with a ``reduce``
-  enqueued (async) right behind its block's kernels, so block r's reduce runs
-  on the process group's stream while block r + 1 builds -- a reduce-scatter
-  by feature that overlaps the build (integer counts: exact, order
-  independent). Every rank then scans only its own block (deriving larger
+* data-parallel (``strategy="data"``): rows sharded (a replicated input is
+  binned per rank for its own shard only). Each level's built (smaller-child)
+  histograms are built one destination feature block at a time into one
+  block-major buffer and summed with ONE ``reduce_scatter`` (integer counts:
+  exact, order independent), so rank r receives the global histograms of its
+  feature block. (Unequal blocks: each block is summed into its owner with a
+  ``reduce`` enqueued right behind its block's kernels.) Every rank then scans only its own block (deriving larger
   siblings from its block of the parent) and the split records take the
   feature-parallel all-gather + ``fp_combine_kernel``. Local row segments are
   fixed up after the partition (``grow_dp_fixup_kernel``); regression purity
@@ -42,8 +42,11 @@ the stream between the level kernels, never a host round trip):
   all-reduce of the whole built histograms instead.)
 * subtree jobs (nodes of at most ``finisher_rows`` rows) are split across
   ranks (serpentine over the largest-first job order); data-parallel ranks
-  first send each job's rows to its owner (one ``all_to_all``); one
-  all-gather of the finished nodes leaves every rank with the full tree.
+  first send each job's rows to its owner (one ``all_to_all``; the owner lays
+  them out in both code layouts in one pass, ``dp_route.hip dp_place``); the
+  owners write their jobs' nodes into the node-shared host tree (one small
+  all-gather of segment counts), or one all-gather of the finished nodes when
+  the ranks span hosts.
 
 Every mode produces the single-GPU tree bit for bit (tests/test_gpu_kernels.py,
 tests/test_distributed.py).
@@ -405,6 +408,15 @@ class DeviceGrower:
             be.launch_finisher(d_jobs.contiguous(), J, n, self.p, be.pos_rec, be.pos_st,
                                counter, share=int(getattr(comm, "world_size", 1) or 1))
 
+    def _job_segs(self, d_jobs) -> torch.Tensor:
+        """The finisher jobs' position ranges and owners, int64 [J][3] = {lo, hi,
+        owner} (a job of r rows owns 2r - 1 positions from its root; owners
+        serpentine over the largest-first order, as ``_dp_finish`` sends them)."""
+        J = int(d_jobs.shape[0])
+        lo = d_jobs[:, 3]
+        own = self._owners(J, self.comm.world_size, d_jobs.device).to(torch.int64)
+        return torch.stack([lo, lo + 2 * d_jobs[:, 1] - 1, own], 1).contiguous()
+
     def _dp_finish(self, d_jobs, W: int):
         """Data-parallel subtree finishing: each job's rows are spread over the
         ranks; every rank sends its share of job j to owner(j) (serpentine over
@@ -445,7 +457,8 @@ class DeviceGrower:
         y64 = be.y.dtype == torch.int64
         hip.dp_gather(s(), d_jobs.data_ptr(), J, W, C, be.idx.data_ptr(), be.tmp.data_ptr(),
                       int(be.row_mask), be.codes_rm.data_ptr(), rb, be.y.data_ptr(), y64,
-                      soff.data_ptr(), codes_s.data_ptr(), y_s.data_ptr())
+                      soff.data_ptr(), codes_s.data_ptr(), y_s.data_ptr(),
+                      int(min(max(p.finisher_rows, 1), be.n)))
         h = hb._pinned_copy(hdr, "dp.hdr")
         torch.cuda.current_stream(dev).synchronize()  # (the split sizes, for the host)
         Jm, R_tot = int(h[0]), int(h[1])
@@ -461,10 +474,12 @@ class DeviceGrower:
         if Jm == 0:
             return
         codes2 = torch.empty((R_tot, be.row_elems), dtype=be.codes_rm.dtype, device=dev)
+        codes_fm = torch.empty((be.F, R_tot), dtype=be.codes_rm.dtype, device=dev)
         y2 = torch.empty(R_tot, dtype=be.y.dtype, device=dev)
+        # both code layouts the finisher reads, in one pass over the received rows
         hip.dp_place(s(), seg.data_ptr(), P * Jm, codes_r.data_ptr(), y_r.data_ptr(), y64, rb,
-                     codes2.data_ptr(), y2.data_ptr())
-        codes_fm = codes2[:, : be.F].t().contiguous()
+                     R_tot, be.F, int(be.cb), codes2.data_ptr(), codes_fm.data_ptr(),
+                     y2.data_ptr())
         be2 = getattr(self, "_dp_be", None)
         if be2 is None or be2.device != dev:
             be2 = self._dp_be = hb.HipBackend(dev)
@@ -577,6 +592,12 @@ class DeviceGrower:
         # block to the block's owner (reduce-scatter by feature), scans per block
         dprs = dp and F_h < F
         blocks = feature_blocks(F, P) if dprs else None
+        # equal blocks: every rank's built histograms laid out block-major in one
+        # buffer and summed with ONE reduce-scatter per level (P reduces to the
+        # blocks' owners paid P collective latencies)
+        rs_one = (dprs and len({hi - lo for lo, hi in blocks}) == 1
+                  and hasattr(comm, "reduce_scatter_device")
+                  and os.environ.get("MPITREE_DP_REDUCE_SCATTER", "1") != "0")
         s = hb._stream
         t0 = time.perf_counter()
         n_loc = int(n)
@@ -643,7 +664,9 @@ class DeviceGrower:
                     # the other ranks' feature blocks of this rank's built histograms
                     rs=[torch.empty((KMAX, hi - lo, B, C), dtype=hdt, device=dev)
                         if r != int(comm.rank) else None
-                        for r, (lo, hi) in enumerate(blocks)] if dprs else None,
+                        for r, (lo, hi) in enumerate(blocks)] if dprs and not rs_one else None,
+                    rsb=torch.empty(P * KMAX * F_h * B * C, dtype=hdt, device=dev)
+                    if rs_one else None,
                     cost=torch.empty((KMAX, F_h), dtype=torch.float64, device=dev),
                     bins=torch.empty((KMAX, F_h), dtype=torch.int32, device=dev),
                     ident=torch.arange(KMAX, **i64),
@@ -670,7 +693,7 @@ class DeviceGrower:
                 )
 
             ws = self._workspace((str(dev), n, n_loc, F, f_lo, F_h, B, C, reg, fr, dp, own, fsel,
-                                  fpx, dfree), make)
+                                  fpx, dfree, rs_one), make)
             sets, hists, slab, rec = ws["sets"], ws["hists"], ws["slab"], ws["rec"]
             cost, bins, ident, split = ws["cost"], ws["bins"], ws["ident"], ws["split"]
             pitems, cursors, jobs, job_count = (ws["pitems"], ws["cursors"], ws["jobs"],
@@ -840,7 +863,15 @@ class DeviceGrower:
                                               Ht.data_ptr(), nf, B, C, ctl + 4 * 3, ctl + 4 * 7,
                                               zero=False)
 
-                if dprs:
+                if rs_one:
+                    # every block's built slots, block-major, then one reduce-scatter:
+                    # this rank's block of the global histograms lands in H
+                    chunk = nbb * F_h * B * C
+                    flat = ws["rsb"]
+                    for r, (lo, hi) in enumerate(blocks):
+                        build(flat[r * chunk : (r + 1) * chunk].view(nbb, F_h, B, C), lo, hi - lo)
+                    comm.reduce_scatter_device(H.view(-1)[:chunk], flat[: P * chunk])
+                elif dprs:
                     # block r of the built slots -> rank r, enqueued behind block r's
                     # kernels: the reduce of block r overlaps the build of block r + 1
                     works = []
@@ -946,6 +977,7 @@ class DeviceGrower:
                                 row_mask=int(be.row_mask))
                 if dp:
                     self._dp_finish(d_jobs, W)
+                    self._dp_segs = self._job_segs(d_jobs)
                 else:
                     self._run_jobs(d_jobs, n, counter, split=not switched)
         elif jobs_host is not None:
@@ -955,6 +987,7 @@ class DeviceGrower:
                 self._pre_live = be.pos_rec[:, 5] > 0
             if dp:
                 self._dp_finish(d_jobs.view(1, -1), W)
+                self._dp_segs = self._job_segs(d_jobs.view(1, -1))
             else:  # (ownership: one job -- every rank grows it, nothing to exchange)
                 self._run_jobs(d_jobs.view(1, -1), n, split=not own)
         if comm is not None and P > 1:
@@ -963,10 +996,21 @@ class DeviceGrower:
             t1 = time.perf_counter()
             b0 = comm.bytes_communicated
             owned = getattr(self, "_owned", None)
-            if owned is not None:
+            dp_segs, self._dp_segs = getattr(self, "_dp_segs", None), None
+            pool = None
+            if owned is not None or (dp_segs is not None and
+                                     dp_segs.shape[0] <= int(hip.shm_max_segs())):
+                pool = shared_tree.pool_for(comm, hip)
+            if dp_segs is not None and pool is not None:
+                # data-parallel: every finisher job has one owner, whose finisher
+                # wrote its positions; the owners write their jobs' nodes (rank 0
+                # also the level nodes, on every rank alike) into the node-shared
+                # host tree, as subtree ownership does (no node all-gather)
+                shared = dict(comm=comm, pool=pool, segs=dp_segs, S=int(dp_segs.shape[0]))
+                self.stats["assembly"] = "shared-host"
+            elif owned is not None:
                 # ranks of one node: each writes its own nodes into a shared host
                 # buffer (no node exchange); otherwise one all-gather of the nodes
-                pool = shared_tree.pool_for(comm, hip)
                 if pool is not None:
                     shared = dict(comm=comm, pool=pool, segs=self._owned["own_segs"],
                                   S=2 * int(self.stats["own_units"]))
@@ -983,7 +1027,8 @@ class DeviceGrower:
                                   else "subtree-owned" if own else "replicated")
             self.stats["feature_block"] = [f_lo, f_hi]
             if dp:
-                self.stats["dp_reduce"] = "reduce-to-owner" if dprs else "all-reduce"
+                self.stats["dp_reduce"] = ("reduce-scatter" if rs_one else
+                                           "reduce-to-owner" if dprs else "all-reduce")
         self.timings["levels"] = time.perf_counter() - t0
         self.stats["levels"] = levels
         self.stats["finisher_subtrees"] = J
@@ -997,7 +1042,10 @@ class DeviceGrower:
                                    shared=shared)
         if ta is None:  # (/dev/shm too small for the tree, on every rank alike)
             self.stats["assembly"] = "exchange (/dev/shm short)"
-            self._exchange_owned(owned)
+            if owned is not None:
+                self._exchange_owned(owned)
+            else:
+                self._exchange_nodes()
             ta = be.assemble_positions(table, int(p.criterion), y_exp, d_edges=d_edges)
         if shared is not None:  # (the shared assembly's segment-count all-gather)
             self.stats["comm_bytes_exchange"] = int(self.stats.get("comm_bytes_exchange", 0)

@@ -190,7 +190,8 @@ class _Targets:
 
 
 def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
-            encode_targets, exponent, sync: bool = False, exact_probe: bool = False) -> Prepared:
+            encode_targets, exponent, sync: bool = False, exact_probe: bool = False,
+            rows=None, agree=None) -> Prepared:
     """Bin ``Xd`` (device, fp32/fp64) and encode ``y`` with two host syncs.
 
     ``encode_labels`` / ``encode_targets`` are the host encoders of
@@ -207,6 +208,11 @@ def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
     ``exact_probe`` (exact-threshold requests): features past ``max_bins`` values
     get no quantile edges and, when any feature has them, the bin pass writes no
     codes (``DeviceBinning``); such a result is only for the presorted-list engine.
+
+    ``rows`` = (lo, hi): codes for that row range only (a data-parallel rank's
+    shard of a replicated input; edges, labels and targets still cover every
+    row, so every rank derives the same tables). ``agree``: combines the bin
+    flags over the ranks (checked before growth, as with ``sync``).
     """
     n = Xd.shape[0]
     dev = Xd.device
@@ -215,7 +221,9 @@ def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
     # setup (~40 us of host time) then overlap it instead of delaying it. (A side
     # stream for the label pass, so the bin kernel could follow the edges at
     # once, measured 0.35 ms slower per flagship fit.)
-    binning = DeviceBinning(Xd, max_bins, probe=exact_probe)
+    if agree is not None:
+        sync = True  # the ranks' flags are combined before any rank grows
+    binning = DeviceBinning(Xd, max_bins, probe=exact_probe, rows=rows, agree=agree)
     lab = (_Targets(y, n, dev, encode_targets, exponent) if regression
            else _Labels(y, n, dev, encode_labels))
     early = binning.early

@@ -143,8 +143,14 @@ class DeviceBinning:
     """
 
     def __init__(self, X: torch.Tensor, max_bins=256, sample_rows: int | None = None,
-                 probe: bool = False):
+                 probe: bool = False, rows=None, agree=None):
         hip = self.hip = native.hip()
+        # rows = (lo, hi): the edges come from every row of X (a replicated input:
+        # every rank derives the same table), the codes only for rows [lo, hi) --
+        # a data-parallel rank bins its own shard. agree(flags) -> the flags of
+        # every rank combined (max), so all ranks take the same refit / error path.
+        self.lo, self.hi = (0, int(X.shape[0])) if rows is None else (int(rows[0]), int(rows[1]))
+        self.agree = agree
         # probe (exact-threshold requests): a feature whose sample exceeds the limit
         # is only marked inexact (no quantile edges), and the early bin pass then
         # only checks for non-finite values -- the fit goes to the presorted-list
@@ -170,7 +176,7 @@ class DeviceBinning:
         self._codes = self._alloc_codes(1) if L <= 256 else None
 
     def _alloc_codes(self, cb):
-        n, F = self.n, self.F
+        n, F = self.hi - self.lo, self.F
         ctype = torch.uint8 if cb == 1 else torch.int16
         row_elems = ((F * cb + 3) // 4) * 4 // cb
         codes_rm = torch.empty((n, row_elems), dtype=ctype, device=self.dev)
@@ -184,7 +190,9 @@ class DeviceBinning:
             self._codes = self._alloc_codes(cb)
         cb, row_elems, codes_rm, codes_fm, flags = self._codes
         self._codes = None  # buffers belong to this pass
-        self.hip.bin(_stream(), self.X.data_ptr(), self.x64, self.n, self.F, edges_t.data_ptr(),
+        # (a row range of the contiguous row-major input is contiguous too)
+        x_ptr = self.X.data_ptr() + self.lo * self.F * self.X.element_size()
+        self.hip.bin(_stream(), x_ptr, self.x64, self.hi - self.lo, self.F, edges_t.data_ptr(),
                      bmax, nb_t.data_ptr(), exact_t.data_ptr(), codes_rm.data_ptr(), row_elems,
                      codes_fm.data_ptr(), cb, flags.data_ptr(), estride=int(edges_t.stride(0)),
                      skip_inexact=skip_inexact)
@@ -232,6 +240,8 @@ class DeviceBinning:
         missed = False
         if check:
             fl = np.array(self._host_flags)
+            if self.agree is not None:
+                fl = np.asarray(self.agree(fl.astype(np.int64)), dtype=np.int64)
             if (fl & 2).any():
                 raise ValueError("Input X contains NaN or infinity.")
             missed = bool((fl & 1).any())
@@ -247,6 +257,8 @@ class DeviceBinning:
         (the codes were clamped to the sampled edges: the fit must be redone)."""
         self._flags_ready.synchronize()
         fl = np.array(self._host_flags)
+        if self.agree is not None:
+            fl = np.asarray(self.agree(fl.astype(np.int64)), dtype=np.int64)
         if (fl & 2).any():
             raise ValueError("Input X contains NaN or infinity.")
         return not bool((fl & 1).any())

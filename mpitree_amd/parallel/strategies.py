@@ -288,6 +288,18 @@ class DistComm(LocalComm):
         return dist.reduce(t, dst=gdst, op=dist.ReduceOp.SUM, group=self.group,
                            async_op=async_op)
 
+    def reduce_scatter_device(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        """``out`` = chunk ``rank`` of the sum over the ranks of ``inp`` (flat, P
+        equal contiguous chunks): one collective where P reduces to the chunks'
+        owners would each pay RCCL's latency."""
+        self.bytes_communicated += inp.numel() * inp.element_size()
+        if self._staged(inp):  # (gloo group: a host all-reduce, then this rank's chunk)
+            h = inp.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+            out.copy_(h.view(self.world_size, -1)[self.rank].view(out.shape))
+            return
+        dist.reduce_scatter_tensor(out.view(-1), inp, op=dist.ReduceOp.SUM, group=self.group)
+
     def all_to_all_device(self, out: torch.Tensor, inp: torch.Tensor, out_splits: list,
                           in_splits: list) -> None:
         """Rows (dim 0) of ``inp`` go to ranks by ``in_splits``; ``out`` receives by
