@@ -64,6 +64,7 @@ class SimDPComm(LocalComm):
         self.ref = ref
         self.bytes_communicated = 0
         self.bytes = dict(reduce=0, records=0, counts=0, rows=0, nodes=0)
+        self.calls = 0  # collectives a real group would issue (latency term of the estimate)
         self._red = 0  # block reduces so far (P per level)
         self._rs = 0  # reduce-scatters so far (one per level)
         self._gat = 0  # record all-gathers so far (one per level)
@@ -88,6 +89,7 @@ class SimDPComm(LocalComm):
         self._red += 1
         nb = t.shape[0]
         self.bytes["reduce"] += t.numel() * t.element_size()
+        self.calls += 1
         if dst == self.rank and lvl < len(self.ref["hists"]):  # (else: a lagged empty level)
             lo, hi = self.ref["blocks"][dst]
             H = self.ref["hists"][lvl]
@@ -100,6 +102,7 @@ class SimDPComm(LocalComm):
         lvl = self._rs
         self._rs += 1
         self.bytes["reduce"] += inp.numel() * inp.element_size()
+        self.calls += 1
         if lvl < len(self.ref["hists"]):  # (else: a lagged empty level)
             lo, hi = self.ref["blocks"][self.rank]
             H = self.ref["hists"][lvl]
@@ -119,10 +122,12 @@ class SimDPComm(LocalComm):
             self._gat += 1
             o[self.rank].copy_(inp.view(-1))
             self.bytes["records"] += inp.numel() * inp.element_size() * P
+            self.calls += 1
             return
         # the finisher jobs' per-rank row counts [P, J]
         out.view(P, -1).copy_(self.ref["allc"])
         self.bytes["counts"] += inp.numel() * inp.element_size() * P
+        self.calls += 1
 
     def all_to_all_device(self, out, inp, out_splits, in_splits):
         r = self.rank
@@ -131,6 +136,7 @@ class SimDPComm(LocalComm):
                   else src[: out.numel()])
         if out.dtype == torch.uint8:
             self.bytes["rows"] += int(sum(in_splits))
+        self.calls += 1
 
     def all_reduce_device(self, t, op=None):  # (regression only: not simulated)
         raise NotImplementedError("sim_dp_ranks simulates classification fits")
@@ -148,6 +154,7 @@ class SimDPComm(LocalComm):
         g[:, GATHER_HDR : GATHER_HDR + S] = mine * cnt[None, :]
         g[:, :GATHER_HDR] = self.ref["head"]
         self.bytes["nodes"] += P * W * 8
+        self.calls += 1
 
 
 def reference(fit, dev, X, y, P, F):
@@ -271,6 +278,7 @@ def main():
                     times.append((time.perf_counter() - t0) * 1e3)
                 assert res.arrays.equal(ref["fit"].arrays), f"P={P} rank {r}: tree differs"
             per_rank.append(dict(ms=float(np.median(times)), bytes=dict(comm.bytes),
+                                 calls=comm.calls,
                                  levels=res.stats.get("levels"),
                                  rows_exchanged=res.stats.get("dp_rows_exchanged", 0)))
             ref["recv_codes"] = ref["recv_y"] = None
@@ -281,6 +289,11 @@ def main():
                    bytes_per_rank_mb={k: round(max(p["bytes"][k] for p in per_rank) / 1e6, 2)
                                       for k in per_rank[0]["bytes"]},
                    rows_exchanged=[p["rows_exchanged"] for p in per_rank],
+                   # scaling_projection.md's xGMI estimate: S (P - 1) / P / 250 GB/s
+                   # + 20 us per collective
+                   est_collective_ms=round(max(
+                       sum(p["bytes"].values()) * (P - 1) / P / 250e9 * 1e3
+                       + 0.020 * p["calls"] for p in per_rank), 3),
                    nodes=ref["fit"].arrays.node_count)
         print(json.dumps(out), flush=True)
         del ref

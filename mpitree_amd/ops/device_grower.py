@@ -598,6 +598,10 @@ class DeviceGrower:
         rs_one = (dprs and len({hi - lo for lo, hi in blocks}) == 1
                   and hasattr(comm, "reduce_scatter_device")
                   and os.environ.get("MPITREE_DP_REDUCE_SCATTER", "1") != "0")
+        # ... built in ONE pass over this rank's rows (all features, node-major) and
+        # permuted block-major on the device, instead of P passes of one block each
+        one_build = rs_one and os.environ.get("MPITREE_DP_ONE_BUILD", "1") != "0"
+        F_slab = F if one_build else F_h  # (item slabs of a full-width build)
         s = hb._stream
         t0 = time.perf_counter()
         n_loc = int(n)
@@ -657,7 +661,7 @@ class DeviceGrower:
                     hists=[torch.empty((KMAX, F_h, B, C), dtype=hdt, device=dev)
                            for _ in range(1 if dfree else 2)] * (2 if dfree else 1),
                     slab=torch.empty((min(IMAX, slab_rows(n_loc)),
-                                      hip.hist_slab_words(F_h, B, C, reg)), dtype=hdt,
+                                      hip.hist_slab_words(F_slab, B, C, reg)), dtype=hdt,
                                      device=dev),
                     rec=torch.empty((KMAX, R), **i64),
                     grec=torch.empty((P * KMAX * R) if (fp or dprs or fpx) else 1, **i64),
@@ -667,6 +671,8 @@ class DeviceGrower:
                         for r, (lo, hi) in enumerate(blocks)] if dprs and not rs_one else None,
                     rsb=torch.empty(P * KMAX * F_h * B * C, dtype=hdt, device=dev)
                     if rs_one else None,
+                    hall=torch.empty(KMAX * F * B * C, dtype=hdt, device=dev)
+                    if one_build else None,
                     cost=torch.empty((KMAX, F_h), dtype=torch.float64, device=dev),
                     bins=torch.empty((KMAX, F_h), dtype=torch.int32, device=dev),
                     ident=torch.arange(KMAX, **i64),
@@ -693,7 +699,7 @@ class DeviceGrower:
                 )
 
             ws = self._workspace((str(dev), n, n_loc, F, f_lo, F_h, B, C, reg, fr, dp, own, fsel,
-                                  fpx, dfree, rs_one), make)
+                                  fpx, dfree, rs_one, one_build), make)
             sets, hists, slab, rec = ws["sets"], ws["hists"], ws["slab"], ws["rec"]
             cost, bins, ident, split = ws["cost"], ws["bins"], ws["ident"], ws["split"]
             pitems, cursors, jobs, job_count = (ws["pitems"], ws["cursors"], ws["jobs"],
@@ -868,8 +874,15 @@ class DeviceGrower:
                     # this rank's block of the global histograms lands in H
                     chunk = nbb * F_h * B * C
                     flat = ws["rsb"]
-                    for r, (lo, hi) in enumerate(blocks):
-                        build(flat[r * chunk : (r + 1) * chunk].view(nbb, F_h, B, C), lo, hi - lo)
+                    if one_build:
+                        Hall = ws["hall"][: nbb * F * B * C].view(nbb, F, B, C)
+                        build(Hall, 0, F)
+                        flat[: P * chunk].view(P, nbb, F_h * B * C).copy_(
+                            Hall.view(nbb, P, F_h * B * C).transpose(0, 1))
+                    else:
+                        for r, (lo, hi) in enumerate(blocks):
+                            build(flat[r * chunk : (r + 1) * chunk].view(nbb, F_h, B, C), lo,
+                                  hi - lo)
                     comm.reduce_scatter_device(H.view(-1)[:chunk], flat[: P * chunk])
                 elif dprs:
                     # block r of the built slots -> rank r, enqueued behind block r's
