@@ -351,20 +351,33 @@ def fit_tree(
                 from ..ops.exact_grower import MAX_ROWS
 
                 probe = max_bins is None and 0 < n < MAX_ROWS
+                # split: wait for the labels only, set up the label-dependent device
+                # buffers while the edges / bin kernels run, then read the edge table
+                split = bin_rows is None and os.environ.get("MPITREE_PREP_SPLIT", "1") != "0"
                 prep = prepare(Xd, y, regression=regression,
                                max_bins=256 if max_bins is None else max_bins,
                                encode_labels=_encode_labels, encode_targets=_encode_targets,
                                exponent=fixed_point_exponent, sync=_sync_prepare,
-                               exact_probe=probe, rows=bin_rows, agree=bin_agree)
-                if prep.verify is not None:
-                    # the bin kernel's flags are read after growth (see prepare): a
-                    # sampled exact-mode feature that missed a value redoes the fit
-                    # with the flags checked first
-                    redo = dict(regression=regression, criterion=criterion,
-                                max_depth=max_depth, min_samples_split=min_samples_split,
-                                min_samples_leaf=min_samples_leaf, max_bins=max_bins,
-                                device=device, comm=comm, finisher_rows=finisher_rows,
-                                engine=engine, checkpoint=checkpoint, _sync_prepare=True)
+                               exact_probe=probe, rows=bin_rows, agree=bin_agree, split=split)
+                # the bin kernel's flags are read after growth (see prepare): a
+                # sampled exact-mode feature that missed a value redoes the fit with
+                # the flags checked first
+                redo = dict(regression=regression, criterion=criterion,
+                            max_depth=max_depth, min_samples_split=min_samples_split,
+                            min_samples_leaf=min_samples_leaf, max_bins=max_bins,
+                            device=device, comm=comm, finisher_rows=finisher_rows,
+                            engine=engine, checkpoint=checkpoint, _sync_prepare=True)
+        be_early = None
+        if prep.resolve is not None:
+            # the labels are known and the edges / bin kernels still run: the
+            # histogram engine's label-dependent setup (row permutation, tables)
+            # happens now, ahead of the edge table (unused if the fit goes exact)
+            if (lo, hi) == (0, n):
+                be_early = HipBackend()
+                be_early.setup(prep.codes_rm, prep.codes_fm, prep.y.contiguous(), prep.nbins,
+                               n_bins=256, n_classes=0 if regression else len(prep.classes),
+                               criterion=crit)
+            prep.resolve()
         mapper, codes_rm, codes_fm, nb = prep.mapper, prep.codes_rm, prep.codes_fm, prep.nbins
         yd, classes, y_exp, root = prep.y, prep.classes, prep.y_exp, prep.root
         C = 0 if regression else len(classes)
@@ -400,6 +413,7 @@ def fit_tree(
                 mapper, codes_rm, codes_fm, nb = (prep.mapper, prep.codes_rm, prep.codes_fm,
                                                   prep.nbins)
                 yd, classes, y_exp, root = prep.y, prep.classes, prep.y_exp, prep.root
+                be_early = None
         if (lo, hi) != (0, n):  # data-parallel shard of a replicated input
             if bin_rows is None:  # (binned every row: keep this rank's)
                 codes_rm = codes_rm[lo:hi].contiguous()
@@ -410,9 +424,13 @@ def fit_tree(
         timings["bin"] = time.perf_counter() - t0
         if debug_enabled():
             check_device_inputs(codes_rm, codes_fm, nb, yd, C, regression)
-        be = HipBackend()
-        be.setup(codes_rm, codes_fm, yd, nb, n_bins=mapper.max_n_bins, n_classes=C,
-                 criterion=crit)
+        if be_early is not None:  # (set up before the edge table: only B was open)
+            be = be_early
+            be.B = int(mapper.max_n_bins)
+        else:
+            be = HipBackend()
+            be.setup(codes_rm, codes_fm, yd, nb, n_bins=mapper.max_n_bins, n_classes=C,
+                     criterion=crit)
         be.timing = profiling()  # synchronised per-phase timers (host-driven loop)
         env = os.environ.get("MPITREE_FINISHER_ROWS")
         # subtree jobs of up to n / 128 rows: idle finisher workgroups split big

@@ -34,6 +34,12 @@ from sklearn.utils.validation import check_is_fitted
 from ..core.criterion import parse_criterion
 from ..core.fit import fit_tree
 from .tree_arrays import TreeArrays
+from ..utils.level_checkpoint import CheckpointInterrupt
+
+# errors a rank raises from its own state, never from a collective a failed peer
+# broke: a rank keeps them even when a peer's failure reached it first (ranks
+# that fail alike -- invalid input, a checkpoint stop -- each report their own)
+_OWN_ERRORS = (ValueError, TypeError, CheckpointInterrupt)
 
 __all__ = [
     "DecisionTreeClassifier",
@@ -388,7 +394,8 @@ class _ParallelMixin:
                 self._fit_impl(X, y, comm=comm, **kw)
             except Exception as e:  # reported to every rank below
                 error = e
-                if isinstance(e, CollectiveFitAborted) or ABORT.is_set():
+                own = isinstance(e, _OWN_ERRORS)  # raised by this rank's own logic
+                if isinstance(e, CollectiveFitAborted) or (ABORT.is_set() and not own):
                     # (a peer failed first: its error, not this rank's broken collective)
                     error = CollectiveFitAborted(f"collective fit aborted ({guard.describe()})")
                 torn = guard.fail(error)

@@ -30,12 +30,13 @@ the stream between the level kernels, never a host round trip):
   which the planner and partition run identically on every rank;
 * data-parallel (``strategy="data"``): rows sharded (a replicated input is
   binned per rank for its own shard only). Each level's built (smaller-child)
-  histograms are built one destination feature block at a time into one
-  block-major buffer and summed with ONE ``reduce_scatter`` (integer counts:
-  exact, order independent), so rank r receives the global histograms of its
-  feature block. (Unequal blocks: each block is summed into its owner with a
-  ``reduce`` enqueued right behind its block's kernels.) Every rank then scans only its own block (deriving larger
-  siblings from its block of the parent) and the split records take the
+  histograms are built in one pass over the rank's rows, permuted block-major
+  and summed with ONE ``reduce_scatter`` (integer counts: exact, order
+  independent), so rank r receives the global histograms of its feature block.
+  (Unequal blocks: each block is built and summed into its owner with a
+  ``reduce`` enqueued right behind its kernels.) Every rank then scans only
+  its own block (deriving larger siblings from its block of the parent) and
+  the split records take the
   feature-parallel all-gather + ``fp_combine_kernel``. Local row segments are
   fixed up after the partition (``grow_dp_fixup_kernel``); regression purity
   takes one min/max all-reduce per level. (Fewer features than ranks: one

@@ -52,6 +52,9 @@ class Prepared:
     # deferred bin verification (None: already checked): call once the stream has
     # passed the bin kernel; False means the fit must be redone with sync=True
     verify: object = None
+    # prepare(split=True): the labels are ready, the edge table is not -- call
+    # once before reading mapper / d_edges64 / verify (waits for the edges kernel)
+    resolve: object = None
 
 
 def _np_dtype(dt: torch.dtype):
@@ -191,7 +194,7 @@ class _Targets:
 
 def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
             encode_targets, exponent, sync: bool = False, exact_probe: bool = False,
-            rows=None, agree=None) -> Prepared:
+            rows=None, agree=None, split: bool = False) -> Prepared:
     """Bin ``Xd`` (device, fp32/fp64) and encode ``y`` with two host syncs.
 
     ``encode_labels`` / ``encode_targets`` are the host encoders of
@@ -213,10 +216,19 @@ def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
     shard of a replicated input; edges, labels and targets still cover every
     row, so every rank derives the same tables). ``agree``: combines the bin
     flags over the ranks (checked before growth, as with ``sync``).
+
+    ``split`` (<= 256 bins, no ``sync``): the label / target pass runs first and
+    the host waits for it alone; the returned ``Prepared`` has no mapper yet and
+    ``resolve()`` waits for the edge table later -- so the caller's label-dependent
+    setup (buffers, the row permutation) overlaps the edges and bin kernels
+    instead of following them.
     """
     n = Xd.shape[0]
     dev = Xd.device
     stream = torch.cuda.current_stream(dev)
+    if split and agree is None and not sync and (max_bins or 0) <= 256:
+        return _prepare_split(Xd, y, regression, max_bins, encode_labels, encode_targets,
+                              exponent, exact_probe, rows, stream)
     # the edges kernel first: the label / target kernels and their host-side
     # setup (~40 us of host time) then overlap it instead of delaying it. (A side
     # stream for the label pass, so the bin kernel could follow the edges at
@@ -253,6 +265,45 @@ def prepare(Xd: torch.Tensor, y, *, regression: bool, max_bins, encode_labels,
     return Prepared(mapper=mapper, codes_rm=codes_rm, codes_fm=codes_fm, nbins=nb, y=yenc,
                     classes=classes, y_exp=y_exp, root=root, d_edges64=binning.d_edges64,
                     verify=binning.verify if deferred else None)
+
+
+def _prepare_split(Xd, y, regression, max_bins, encode_labels, encode_targets, exponent,
+                   exact_probe, rows, stream) -> Prepared:
+    """``prepare(split=True)``: labels -> edges -> bin on the stream, one host
+    wait for the labels; the edge table is read in ``Prepared.resolve``."""
+    n = Xd.shape[0]
+    dev = Xd.device
+    lab = (_Targets(y, n, dev, encode_targets, exponent) if regression
+           else _Labels(y, n, dev, encode_labels))
+    lab_ev = _event(dev, "prep.labels")
+    lab_ev.record(stream)
+    binning = DeviceBinning(Xd, max_bins, probe=exact_probe, rows=rows)
+    tables = _event(dev, "prep.tables")
+    tables.record(stream)
+    binning.launch_bin_early()
+    lab_ev.synchronize()  # the one early wait: label counts / target scale
+    if lab.after_first_sync():  # (labels outside the guess: another device round)
+        stream.synchronize()
+    if regression:
+        yenc, y_exp, root = lab.finish()
+        classes = None
+    else:
+        classes, yenc, root = lab.finish()
+        y_exp = 0
+    prep = Prepared(mapper=None, codes_rm=binning.codes_rm, codes_fm=binning.codes_fm,
+                    nbins=binning.nb, y=yenc, classes=classes, y_exp=y_exp, root=root,
+                    d_edges64=None)
+
+    def resolve():
+        tables.synchronize()  # (the edges kernel ran while the caller set up)
+        binning.launch_bin()  # host tables (the bin kernel is enqueued already)
+        prep.mapper = binning.finish(check=False)[0]
+        prep.d_edges64 = binning.d_edges64
+        prep.verify = binning.verify
+        prep.resolve = None
+
+    prep.resolve = resolve
+    return prep
 
 
 def prepare_with_mapper(Xd: torch.Tensor, y_enc, mapper, classes, y_exp: int) -> Prepared:
