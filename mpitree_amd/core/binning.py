@@ -90,6 +90,11 @@ class TableBinMapper(BinMapper):
         self.exact = exact
         self.max_bins = max_bins
 
+    def own_table(self) -> None:
+        """Copy the table if it is a view of another buffer (a reused pinned one)."""
+        if self._table.base is not None:
+            self._table = self._table.copy()
+
     @property
     def edges(self) -> list:
         if self._edges is None:

@@ -250,6 +250,9 @@ def _fit_exact_device(Xd, prep, C, crit, params, comm, timings, t_bin, t_start, 
             stats["mode"] = "replicated-exact"
     timings["total"] = time.perf_counter() - t_start
     mapper = BinMapper(edges=[], exact=np.ones(F, bool), max_bins=None)
+    from ..ops.hip_backend import run_deferred
+
+    run_deferred()
     return FitResult(arrays=ta, classes=prep.classes, n_features=F, mapper=mapper,
                      y_scale_exp=prep.y_exp, engine="hip-exact", timings=timings, stats=stats)
 
@@ -546,5 +549,9 @@ def fit_tree(
         logger.info("fit: engine=%s n=%d F=%d nodes=%d depth=%d %.3f ms", eng, n, F,
                     ta.node_count, ta.max_depth, timings["total"] * 1e3)
         logger.debug("fit timings (ms): %s", {k: round(v * 1e3, 3) for k, v in timings.items()})
+    if dev == "cuda":
+        from ..ops.hip_backend import run_deferred
+
+        run_deferred()  # (host work the level loop did not take: mapper tables)
     return FitResult(arrays=ta, classes=classes, n_features=F, mapper=mapper, y_scale_exp=y_exp,
                      engine=eng, timings=timings, stats=stats)

@@ -41,7 +41,8 @@ void launch_predict(hipStream_t, const void*, bool, int64_t, int, const void*, c
 void launch_bin(hipStream_t, const void*, bool, int64_t, int, const void*, int, int,
                 const int32_t*, const uint8_t*, void*, int, void*, int, int32_t*, int);
 void launch_xlog2x(hipStream_t, double*, int64_t);
-void launch_label_count(hipStream_t, const int64_t*, int64_t, int64_t, int, uint32_t*, bool);
+void launch_label_count(hipStream_t, const int64_t*, int64_t, int64_t, int, uint32_t*, bool,
+                        int32_t*);
 void launch_label_encode(hipStream_t, const int64_t*, int64_t, int64_t, const int64_t*, int32_t*);
 void launch_finish(hipStream_t, const void*, int64_t, const void*, int, int64_t, uint32_t*,
                    uint32_t*, const int32_t*, int, const int64_t*, int, int32_t*, const int32_t*,
@@ -465,11 +466,13 @@ PYBIND11_MODULE(_hip, m) {
   m.def("host_unregister", [](uintptr_t p) {
     MT_HIP_CHECK(hipHostUnregister(reinterpret_cast<void*>(p)));
   });
+  // enc (optional): also the labels' int32 codes y - lo (valid when they lie in range)
   m.def("label_count", [](uintptr_t s, uintptr_t y, int64_t n, int64_t lo, int R,
-                          uintptr_t counts, bool checked) {
-    mt::launch_label_count(S(s), P<int64_t>(y), n, lo, R, P<uint32_t>(counts), checked);
+                          uintptr_t counts, bool checked, uintptr_t enc) {
+    mt::launch_label_count(S(s), P<int64_t>(y), n, lo, R, P<uint32_t>(counts), checked,
+                           P<int32_t>(enc));
   }, py::arg("s"), py::arg("y"), py::arg("n"), py::arg("lo"), py::arg("R"), py::arg("counts"),
-     py::arg("checked") = false);
+     py::arg("checked") = false, py::arg("enc") = 0);
   m.def("label_encode", [](uintptr_t s, uintptr_t y, int64_t n, int64_t lo, uintptr_t lut,
                            uintptr_t out) {
     mt::launch_label_encode(S(s), P<int64_t>(y), n, lo, P<int64_t>(lut), P<int32_t>(out));

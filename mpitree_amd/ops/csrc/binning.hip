@@ -53,13 +53,40 @@ constexpr int kEdgeHash = 2048;  // hash slots (exact mode needs <= limit <= 102
 // One workgroup per feature. smem: sample [S] XT, hash [kEdgeHash] keys.
 // S = power of two >= s (padding +inf sorts last). Output: edges [F][limit]
 // (+inf padded), nbins [F], exact [F].
+// The edge sample, transposed: smp[f][i] = X[i n / s][f] for the s sampled rows.
+// One workgroup per 64 rows x 64 features through an LDS tile: each sampled row is
+// one contiguous read of its features (the per-feature workgroups of edges_kernel
+// otherwise gather every value alone, from a different row -- 64 workgroups on a
+// 256-CU chip, latency-bound at ~60 us for 1M x 64), and each feature's run of
+// 64 values is one contiguous write.
+template <typename XT>
+__global__ __launch_bounds__(256) void edges_sample_kernel(const XT* __restrict__ X, int64_t n,
+                                                           int F, int s,
+                                                           XT* __restrict__ smp) {
+  __shared__ XT tile[64][65];
+  const int i0 = blockIdx.x * 64, f0 = blockIdx.y * 64;
+  const int tid = threadIdx.x, c = tid & 63;
+  for (int r = tid >> 6; r < 64; r += 4) {
+    const int i = i0 + r, f = f0 + c;
+    XT v = (XT)0;
+    if (i < s && f < F) v = X[((int64_t)i * n / s) * F + f];  // (edges_kernel's sample rows)
+    tile[r][c] = v;
+  }
+  __syncthreads();
+  for (int q = tid >> 6; q < 64; q += 4) {
+    const int f = f0 + q, i = i0 + c;
+    if (f < F && i < s) smp[(int64_t)f * s + i] = tile[c][q];
+  }
+}
+
 template <typename XT>
 __global__ __launch_bounds__(kEdgeThreads) void edges_kernel(const XT* __restrict__ X, int64_t n,
                                                              int F, int s, int S, int limit,
                                                              XT* __restrict__ edges,
                                                              int32_t* __restrict__ nbins,
                                                              uint8_t* __restrict__ exact,
-                                                             int probe) {
+                                                             int probe,
+                                                             const XT* __restrict__ smp) {
   using K = typename KeyOf<XT>::T;
   extern __shared__ __align__(16) uint8_t smem[];
   XT* key = reinterpret_cast<XT*>(smem);
@@ -86,8 +113,12 @@ __global__ __launch_bounds__(kEdgeThreads) void edges_kernel(const XT* __restric
       const int i = i0 + u * kEdgeThreads;
       v[u] = __builtin_inf();
       if (i < s) {
-        const int64_t row = (int64_t)i * n / s;  // deterministic strided sample
-        v[u] = X[row * F + f];
+        if (smp != nullptr) {  // (the transposed sample: one contiguous run per feature)
+          v[u] = smp[(int64_t)f * s + i];
+        } else {
+          const int64_t row = (int64_t)i * n / s;  // deterministic strided sample
+          v[u] = X[row * F + f];
+        }
       }
     }
 #pragma unroll
@@ -577,11 +608,33 @@ void launch_edges(hipStream_t stream, const void* X, bool x64, int64_t n, int F,
   const int xb = x64 ? 8 : 4;
   const size_t lds = (size_t)S * xb + (size_t)kEdgeHash * xb;
   if (s > edges_sample_rows(x64)) throw std::runtime_error("edges sample exceeds LDS");
+  // the transposed sample (a device scratch per GPU, grown on demand; up to 256 MB --
+  // wider inputs keep the per-value gathers)
+  void* smp = nullptr;
+  const size_t smp_bytes = (size_t)s * F * xb;
+  if (smp_bytes <= ((size_t)256 << 20)) {
+    static void* bufs[64] = {};
+    static size_t caps[64] = {};
+    int dev = 0;
+    MT_HIP_CHECK(hipGetDevice(&dev));
+    if (dev < 64) {
+      if (caps[dev] < smp_bytes) {
+        if (bufs[dev]) MT_HIP_CHECK(hipFree(bufs[dev]));
+        MT_HIP_CHECK(hipMalloc(&bufs[dev], smp_bytes));
+        caps[dev] = smp_bytes;
+      }
+      smp = bufs[dev];
+    }
+  }
 #define MT_EDGES(XT)                                                                           \
   MT_HIP_CHECK(mt_set_max_lds((const void*)edges_kernel<XT>,                              \
                                    (int)lds));     \
+  if (smp)                                                                                     \
+    hipLaunchKernelGGL(edges_sample_kernel<XT>, dim3((unsigned)((s + 63) / 64),               \
+                       (unsigned)((F + 63) / 64)), dim3(256), 0, stream, (const XT*)X, n, F, s, \
+                       (XT*)smp);                                                              \
   hipLaunchKernelGGL(edges_kernel<XT>, dim3(F), dim3(kEdgeThreads), lds, stream, (const XT*)X, \
-                     n, F, s, S, limit, (XT*)edges, nbins, exact, probe);                      \
+                     n, F, s, S, limit, (XT*)edges, nbins, exact, probe, (const XT*)smp);      \
   if (pack) {                                                                                  \
     const int64_t tot = (int64_t)F * limit + 2 * F;                                            \
     const int g = (int)std::min<int64_t>((tot + 255) / 256, 1024);                             \

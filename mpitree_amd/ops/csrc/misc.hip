@@ -47,7 +47,8 @@ constexpr int kLabLds = 8192;
 __global__ __launch_bounds__(256) void label_count_kernel(const int64_t* __restrict__ y,
                                                           int64_t n, int64_t lo, int R,
                                                           uint32_t* __restrict__ counts,
-                                                          bool checked) {
+                                                          bool checked,
+                                                          int32_t* __restrict__ enc) {
   // checked: the range is a guess made before the labels' min/max reached the
   // host -- out-of-range labels are tallied in counts[R] instead of indexed
   __shared__ uint32_t h[kLabLds];
@@ -58,6 +59,7 @@ __global__ __launch_bounds__(256) void label_count_kernel(const int64_t* __restr
   uint32_t oob = 0;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int64_t d = y[i] - lo;
+    if (enc) enc[i] = (int32_t)d;  // (the int32 codes when the labels are 0..C-1)
     if (checked && (d < 0 || d >= R)) {
       ++oob;
       continue;
@@ -89,7 +91,7 @@ static unsigned label_grid(int64_t n) {
 }
 
 void launch_label_count(hipStream_t stream, const int64_t* y, int64_t n, int64_t lo, int R,
-                        uint32_t* counts, bool checked) {
+                        uint32_t* counts, bool checked, int32_t* enc) {
   // checked: counts has R + 1 entries, the last one counts labels outside the range
   MT_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(uint32_t) * (size_t)(R + (checked ? 1 : 0)),
                               stream));
@@ -97,7 +99,7 @@ void launch_label_count(hipStream_t stream, const int64_t* y, int64_t n, int64_t
   // LDS-privatised histograms: fewer, fuller blocks; global atomics otherwise
   const unsigned g = R <= kLabLds ? std::min(label_grid(n), 512u) : label_grid(n);
   hipLaunchKernelGGL(label_count_kernel, dim3(g), dim3(256), 0, stream, y, n, lo, R, counts,
-                     checked);
+                     checked, enc);
   MT_HIP_CHECK(hipGetLastError());
 }
 

@@ -814,6 +814,8 @@ class DeviceGrower:
                 b0 = getattr(comm, "bytes_communicated", 0)
                 if ctx is not None and not fpx_on:
                     ctx.level(s(), lvl)
+                    if hb._DEFERRED:  # (host work of the setup, now that the GPU is busy)
+                        hb.run_deferred()
                     if REC_DUMP is not None:  # (tools: per-level split records)
                         REC_DUMP.append(rec[: int(min(2 ** min(lvl, 40), KMAX))].clone())
                     if DUMP is not None:
@@ -919,6 +921,8 @@ class DeviceGrower:
                     hip.fp_combine(s(), g.data_ptr(), P, kb, R, ctl, rec.data_ptr())
                 mark()
                 plan(cur, nxt, lvl)
+                if hb._DEFERRED:
+                    hb.run_deferred()
                 mark()
                 pb = int(min(PMAX, n_loc // 1024 + kb + 1))
                 hip.partition(s(), be.codes_fm.data_ptr(), cb, be.n, src, dst, be.row_mask,

@@ -30,7 +30,8 @@ import numpy as np
 import torch
 
 from . import native
-from .hip_backend import DeviceBinning, _event, _pinned_copy, _stream, _uploader
+from .hip_backend import (DeviceBinning, _d2h, _event, _pinned_copy, _pinned_host, _stream,
+                          _uploader, _ws_tensor)
 
 __all__ = ["Prepared", "prepare"]
 
@@ -57,8 +58,14 @@ class Prepared:
     resolve: object = None
 
 
+_NP_DT: dict = {}
+
+
 def _np_dtype(dt: torch.dtype):
-    return torch.empty(0, dtype=dt).numpy().dtype
+    v = _NP_DT.get(dt)
+    if v is None:
+        v = _NP_DT[dt] = torch.empty(0, dtype=dt).numpy().dtype
+    return v
 
 
 class _Labels:
@@ -73,14 +80,17 @@ class _Labels:
         )
         self._counts = None
         if self.dev_path:
-            self.yl = (y if y.dtype == torch.int64 else y.long()).contiguous()
+            self.yl = y if (y.dtype == torch.int64 and y.is_contiguous()) else \
+                y.long().contiguous()
             # speculate that the labels lie in [0, _SPEC_R): the counts (and an
-            # out-of-range tally) then arrive with the fit's first sync
-            self.spec = torch.empty(_SPEC_R + 1, dtype=torch.int32, device=dev)
+            # out-of-range tally) then arrive with the fit's first sync; the same
+            # pass writes the int32 codes, valid when the labels are 0..C-1
+            self.spec = _ws_tensor(dev, "lab.spec", (_SPEC_R + 1,), torch.int32)
+            self.enc0 = _ws_tensor(dev, "lab.enc", (n,), torch.int32)
             native.hip().label_count(_stream(), self.yl.data_ptr(), n, 0, _SPEC_R,
-                                     self.spec.data_ptr(), checked=True)
-            self._spec = _pinned_copy(self.spec, "prep.lab.spec")
-            self.enc0 = self.yl.to(torch.int32)  # the codes when the labels are 0..C-1
+                                     self.spec.data_ptr(), True, self.enc0.data_ptr())
+            self._spec, hp = _pinned_host("prep.lab.spec", _SPEC_R + 1, np.int32)
+            _d2h(hp, self.spec)
 
     def after_first_sync(self) -> bool:
         """True when the labels need another device round (outside the guess)."""
@@ -113,21 +123,21 @@ class _Labels:
             root = np.bincount(enc, minlength=len(classes)).astype(np.int64)
             d = torch.from_numpy(np.ascontiguousarray(enc, np.int32)).to(self.dev)
             return classes, d, root
-        counts = np.array(self._counts, dtype=np.int64)
-        present = counts > 0
-        idx = np.nonzero(present)[0]
+        counts = self._counts
+        idx = np.flatnonzero(counts)
         classes = (idx + self.lo).astype(_np_dtype(self.y.dtype))
         last = int(idx[-1]) if idx.size else -1
         if self.lo == 0 and last + 1 == idx.size and self.enc0 is not None:
             enc = self.enc0
-        elif self.lo == 0 and present.all():
+        elif self.lo == 0 and idx.size == counts.size:
             enc = self.yl.to(torch.int32)
         else:
+            present = counts > 0
             (d_lut,) = _uploader(self.dev)(np.cumsum(present) - 1)
             enc = torch.empty(self.n, dtype=torch.int32, device=self.dev)
             native.hip().label_encode(_stream(), self.yl.data_ptr(), self.n, self.lo,
                                       d_lut.data_ptr(), enc.data_ptr())
-        return classes, enc, counts[present]
+        return classes, enc, counts[idx].astype(np.int64)
 
 
 class _Targets:
@@ -322,6 +332,7 @@ def prepare_with_mapper(Xd: torch.Tensor, y_enc, mapper, classes, y_exp: int) ->
     job = DeviceBinning.__new__(DeviceBinning)  # the bin pass alone (no edges kernel)
     job.hip, job.X, job.dev = hip, Xd, dev
     job.n, job.F = Xd.shape
+    job.lo, job.hi = 0, job.n  # (every row of this rank's shard)
     job.x64 = Xd.dtype == torch.float64
     job._codes = None
     codes_rm, codes_fm, flags = job._run_bin(edges_x, nb, exact, max(1, W))

@@ -34,6 +34,7 @@ def _tiny_batch(hip) -> int:
     return int(f()) if f is not None else 1
 
 
+_EDGE_ROWS: dict = {}  # x64 -> rows the edges kernel samples (asked once)
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 _cur_dev = getattr(torch._C, "_cuda_getDevice", None)
 
@@ -161,17 +162,21 @@ class DeviceBinning:
         dev = self.dev = X.device
         self.x64 = X.dtype == torch.float64
         self.limit = MAX_BINS_LIMIT if max_bins is None else int(max_bins)
-        s = min(n, int(sample_rows or hip.edges_sample_rows(self.x64)))
+        er = _EDGE_ROWS.get(self.x64)
+        if er is None:
+            er = _EDGE_ROWS[self.x64] = int(hip.edges_sample_rows(self.x64))
+        s = min(n, int(sample_rows or er))
         L = self.limit
-        self.edges = torch.empty((F, L), dtype=X.dtype, device=dev)
-        self.nb = torch.empty(F, dtype=torch.int32, device=dev)
-        self.exact = torch.empty(F, dtype=torch.uint8, device=dev)
+        # (setup buffers reused across fits of one shape: see _ws_tensor)
+        self.edges = _ws_tensor(dev, "bin.edges", (F, L), X.dtype)
+        self.nb = _ws_tensor(dev, "bin.nb", (F,), torch.int32)
+        self.exact = _ws_tensor(dev, "bin.exact", (F,), torch.uint8)
         # fp64 [F*L edges | F counts | F exact flags]: the host's copy in one D2H
-        self.pack = torch.empty(F * L + 2 * F, dtype=torch.float64, device=dev)
+        self.pack = _ws_tensor(dev, "bin.pack", (F * L + 2 * F,), torch.float64)
         hip.edges(_stream(), X.data_ptr(), self.x64, n, F, s, L, self.edges.data_ptr(),
-                  self.nb.data_ptr(), self.exact.data_ptr(), pack=self.pack.data_ptr(),
-                  probe=self.probe)
-        self._host_pack = _pinned_copy(self.pack, "bin.pack")
+                  self.nb.data_ptr(), self.exact.data_ptr(), self.pack.data_ptr(), self.probe)
+        self._host_pack, hp = _pinned_host("bin.pack", F * L + 2 * F, np.float64)
+        _d2h(hp, self.pack)
         # the code buffers' shapes are known up front for <= 256 bins
         self._codes = self._alloc_codes(1) if L <= 256 else None
 
@@ -179,9 +184,10 @@ class DeviceBinning:
         n, F = self.hi - self.lo, self.F
         ctype = torch.uint8 if cb == 1 else torch.int16
         row_elems = ((F * cb + 3) // 4) * 4 // cb
-        codes_rm = torch.empty((n, row_elems), dtype=ctype, device=self.dev)
-        codes_fm = torch.empty((F, n), dtype=ctype, device=self.dev)
-        flags = torch.zeros(self.F, dtype=torch.int32, device=self.dev)
+        codes_rm = _ws_tensor(self.dev, "bin.codes_rm", (n, row_elems), ctype)
+        codes_fm = _ws_tensor(self.dev, "bin.codes_fm", (F, n), ctype)
+        flags = _ws_tensor(self.dev, "bin.flags", (self.F,), torch.int32)
+        flags.zero_()
         return cb, row_elems, codes_rm, codes_fm, flags
 
     def _run_bin(self, edges_t, nb_t, exact_t, bmax, skip_inexact=False):
@@ -210,20 +216,24 @@ class DeviceBinning:
         edges, codes and flags together."""
         self.codes_rm, self.codes_fm, flags = self._run_bin(self.edges, self.nb, self.exact,
                                                             self.limit, skip_inexact=self.probe)
-        self._host_flags = _pinned_copy(flags, "bin.flags")
+        self._host_flags, hp = _pinned_host("bin.flags", self.F, np.int32)
+        _d2h(hp, flags)
         self._flags_ready = _event(self.dev, "bin.flags")
         self._flags_ready.record(torch.cuda.current_stream(self.dev))
         self._launched = True
 
     def host_tables(self):
-        """Host edge table and ``BinMapper`` (after a sync covering ``__init__``'s copy)."""
+        """Host edge table and ``BinMapper`` (after a sync covering ``__init__``'s copy).
+        The table stays a view of the pinned buffer until the level loop runs (its
+        private copy is deferred work: the next fit reuses the buffer)."""
         F, L = self.F, self.limit
         host = self._host_pack
-        self.host_edges = host[: F * L].reshape(F, L).copy()
+        self.host_edges = host[: F * L].reshape(F, L)
         self.host_nb = host[F * L : F * L + F].astype(np.int64)
         self.host_exact = host[F * L + F :].astype(bool)
         self.bmax = int(max(1, self.host_nb.max())) if F else 1
         self.mapper = TableBinMapper(self.host_edges, self.host_nb, self.host_exact.copy(), L)
+        defer(self.mapper.own_table)
 
     def launch_bin(self):
         """Enqueue the bin kernel (after a sync covering ``__init__``'s copy)."""
@@ -362,6 +372,55 @@ def _task_flags(device, n: int, slot: int = 0):
         ent = _TASK_FLAGS[key] = [torch.zeros(max(n, 4096), dtype=torch.int32, device=device), 0]
     ent[1] = ent[1] % 0x7FFFFFFE + 1
     return ent[0], ent[1]
+
+
+_ws_tensors: dict = {}
+
+
+def _ws_tensor(device, name: str, shape: tuple, dtype) -> torch.Tensor:
+    """A device tensor reused by consecutive fits of one shape (one dict lookup:
+    each fresh allocation costs host time on the path to the first level). The
+    fit's setup buffers only: nothing holds them once a fit returns."""
+    k = (str(device), name)
+    t = _ws_tensors.get(k)
+    if t is None or t.shape != shape or t.dtype != dtype:
+        t = _ws_tensors[k] = torch.empty(shape, dtype=dtype, device=device)
+    return t
+
+
+_pinned_np: dict = {}
+
+
+def _pinned_host(key: str, count: int, dtype) -> tuple:
+    """(numpy view, host address) of a reusable pinned buffer of ``count``
+    elements, for :func:`_d2h` (a raw async copy: no tensor views per fit)."""
+    ent = _pinned_np.get(key)
+    if ent is None or ent[0].size < count or ent[0].dtype != np.dtype(dtype):
+        t = torch.empty(max(int(count), 256), dtype=torch.from_numpy(np.zeros(0, dtype)).dtype,
+                        pin_memory=True)
+        arr = t.numpy()
+        ent = _pinned_np[key] = (arr, int(arr.ctypes.data), t)
+    return ent[0][:count], ent[1]
+
+
+def _d2h(host_ptr: int, t: torch.Tensor) -> None:
+    """Enqueue the copy of device tensor ``t`` (contiguous) to ``host_ptr``."""
+    native.hip().copy_d2h(_stream(), host_ptr, t.data_ptr(), t.numel() * t.element_size())
+
+
+_DEFERRED: list = []
+
+
+def defer(fn) -> None:
+    """Host work a fit needs done before it returns but not before its first
+    level: run by :func:`run_deferred` while the GPU grows the tree (the level
+    loop's host waits) instead of on the path to the first kernel."""
+    _DEFERRED.append(fn)
+
+
+def run_deferred() -> None:
+    while _DEFERRED:
+        _DEFERRED.pop(0)()
 
 
 _events: dict = {}
