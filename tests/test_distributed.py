@@ -506,6 +506,47 @@ def test_data_sharded_agrees_with_concatenated_fit(regression):
             np.testing.assert_array_equal(o["value"], ta.count)
 
 
+def _fit_sharded_gpu(rank, world, regression):
+    """The row-shard fit on GPU ranks (ranks sharing one card over gloo): the
+    agreed bin mapper is applied on the device (gpu_prepare.prepare_with_mapper)."""
+    from mpitree_amd import ParallelDecisionTreeClassifier, ParallelDecisionTreeRegressor
+    from mpitree_amd.utils.observability import tree_digest
+
+    Xs, ys = _sharded_data(5, regression)
+    cls = ParallelDecisionTreeRegressor if regression else ParallelDecisionTreeClassifier
+    est = cls(strategy="data", device="cuda").fit(Xs[rank], ys[rank], data_sharded=True)
+    ta = est.tree_arrays_
+    out = {k: getattr(ta, k) for k in FIELDS}
+    out["threshold"] = ta.threshold
+    out["value"] = ta.value if regression else ta.count
+    out["digest"] = np.array([tree_digest(ta)])
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("regression", [False, True])
+def test_gpu_data_sharded_agrees_with_concatenated_fit(regression):
+    """Row shards on GPU ranks build the single-process tree of the concatenated
+    data (agreed edges, classes and fixed-point scale; device binning of each
+    shard with the agreed table)."""
+    from mpitree_amd import DecisionTreeClassifier, DecisionTreeRegressor
+
+    outs = run_ranks(_fit_sharded_gpu, 2, regression, start_method="spawn")
+    Xs, ys = _sharded_data(5, regression)
+    X, y = np.concatenate(Xs), np.concatenate(ys)
+    cls = DecisionTreeRegressor if regression else DecisionTreeClassifier
+    ta = cls(device="cpu").fit(X, y).tree_arrays_
+    for o in outs:
+        assert o["digest"][0] == outs[0]["digest"][0]
+        for k in FIELDS:
+            np.testing.assert_array_equal(o[k], getattr(ta, k), err_msg=k)
+        np.testing.assert_array_equal(o["threshold"], ta.threshold)
+        if regression:
+            np.testing.assert_allclose(o["value"], ta.value, rtol=1e-12)
+        else:
+            np.testing.assert_array_equal(o["value"], ta.count)
+
+
 def _fit_sharded_continuous(rank, world, max_bins):
     from mpitree_amd import ParallelDecisionTreeClassifier
     from mpitree_amd.utils.observability import tree_digest
