@@ -153,13 +153,15 @@ def _fit_rank_gpu_large(rank, world, regression, strategy="auto"):
         outs[f"own_rows{it}"] = np.array([est.fit_stats_.get("own_rows", -1)])
         outs[f"asm{it}"] = np.array([est.fit_stats_.get("assembly", "")])
         outs[f"fpx{it}"] = np.array([est.fit_stats_.get("fp_prefix_levels", 0)])
+        outs[f"dpr{it}"] = np.array([est.fit_stats_.get("dp_reduce", "")])
+        outs[f"dprows{it}"] = np.array([est.fit_stats_.get("dp_rows_exchanged", -1)])
     return outs
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("regression", [False, True])
 @pytest.mark.parametrize("strategy,world", [("auto", 2), ("auto", 4), ("feature", 2),
-                                            ("data", 2), ("subtree", 3)])
+                                            ("data", 2), ("data", 4), ("subtree", 3)])
 def test_gpu_ranks_equal_single_gpu_at_scale(regression, strategy, world):
     """Thousands of finisher jobs (many with equal row counts) over 2-4 ranks:
     subtree ownership (auto / subtree: replicated levels until the LPT switch,
@@ -203,6 +205,12 @@ def test_gpu_ranks_equal_single_gpu_at_scale(regression, strategy, world):
                                                  if strategy == "subtree" else "shared-host")
             else:
                 assert o[f"bytes{it}"].sum() > 0  # per-level collectives ran
+            if want == "data":
+                # one reduce-scatter per level (equal feature blocks), the finisher
+                # rows routed to their owners, the owners' nodes in the shared tree
+                assert str(o[f"dpr{it}"][0]) == "reduce-scatter"
+                assert o[f"dprows{it}"][0] > 0
+                assert str(o[f"asm{it}"][0]) == "shared-host"
             for k in FIELDS + ("threshold", "impurity"):
                 np.testing.assert_array_equal(o[f"{k}{it}"], getattr(ref, k), err_msg=k)
             np.testing.assert_array_equal(o[f"stat{it}"], ref.value if regression else ref.count)
