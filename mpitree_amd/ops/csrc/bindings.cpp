@@ -48,7 +48,7 @@ void launch_finish(hipStream_t, const void*, int64_t, const void*, int, int64_t,
                    uint32_t*, const int32_t*, int, const int64_t*, int, int32_t*, const int32_t*,
                    int, int, int, int, int, int64_t, int64_t, const double*, const float*, int,
                    int32_t*, int32_t*, int64_t*, int32_t*, int32_t, int, int, int, int64_t*, int,
-                   int64_t*, int);
+                   int64_t*, int, int32_t*);
 int finish_lds_bytes(int F, int B, int C);
 void launch_hw_xlog2x(hipStream_t, float*, int);
 int finish_feature_tile(int F, int B, int C);
@@ -73,7 +73,7 @@ void launch_job_sort(hipStream_t, const int64_t*, int, int, int64_t*, int32_t*);
 void launch_finish_reg(hipStream_t, const void*, int64_t, const void*, int, int64_t, uint32_t*,
                        uint32_t*, const int64_t*, const int64_t*, int, int32_t*, const int32_t*,
                        int, int, int, int64_t, int64_t, int32_t*, int64_t*, int, int, int64_t*,
-                       int, int64_t*, int32_t*, int32_t, int);
+                       int, int64_t*, int32_t*, int32_t, int, int32_t*);
 void launch_seg_minmax(hipStream_t, const uint32_t*, const int64_t*, const int64_t*, int, int64_t*,
                        const int32_t*);
 void launch_hist_reduce_tasks(hipStream_t, const int64_t*, int, const int64_t*, int, const void*,
@@ -205,14 +205,15 @@ PYBIND11_MODULE(_hip, m) {
                      uintptr_t xtab, uintptr_t xtabf, int xtab_n, uintptr_t node_i32,
                      uintptr_t node_cnt, uintptr_t tasks, uintptr_t task_flag, int epoch,
                      int task_cap, int grid, int tiny_rows, uintptr_t tiny,
-                     int tiny_grid, uintptr_t prof, int tiny_waves) {
+                     int tiny_grid, uintptr_t prof, int tiny_waves, uintptr_t tiny_order) {
     mt::launch_finish(S(s), P<void>(codes_rm), row_words, P<void>(codes_fm), cb, n_rows,
                       P<uint32_t>(idx), P<uint32_t>(tmp), P<int32_t>(y), lab_shift,
                       P<int64_t>(jobs), J, P<int32_t>(counter), P<int32_t>(nbins), F, B, C, crit,
                       max_depth, mss, msl, P<double>(xtab), P<float>(xtabf), xtab_n, P<int32_t>(node_i32),
                       P<int32_t>(node_cnt), P<int64_t>(tasks), P<int32_t>(task_flag), epoch,
                       task_cap, grid, tiny_rows,
-                      P<int64_t>(tiny), tiny_grid, P<int64_t>(prof), tiny_waves);
+                      P<int64_t>(tiny), tiny_grid, P<int64_t>(prof), tiny_waves,
+                      P<int32_t>(tiny_order));
   }, py::arg("s"), py::arg("codes_rm"), py::arg("row_words"), py::arg("codes_fm"), py::arg("cb"),
      py::arg("n_rows"), py::arg("idx"), py::arg("tmp"), py::arg("y"), py::arg("lab_shift"),
      py::arg("jobs"), py::arg("J"), py::arg("counter"), py::arg("nbins"), py::arg("F"),
@@ -220,7 +221,8 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("msl"), py::arg("xtab"), py::arg("xtabf"), py::arg("xtab_n"), py::arg("node_i32"),
      py::arg("node_cnt"), py::arg("tasks"), py::arg("task_flag"), py::arg("epoch"),
      py::arg("task_cap"), py::arg("grid"), py::arg("tiny_rows"),
-     py::arg("tiny"), py::arg("tiny_grid"), py::arg("prof"), py::arg("tiny_waves") = 0);
+     py::arg("tiny"), py::arg("tiny_grid"), py::arg("prof"), py::arg("tiny_waves") = 0,
+     py::arg("tiny_order") = 0);
   m.def("asm_tiles", &mt::asm_tiles);
   m.def("small_fit_max_rows", &mt::small_fit_max_rows);
   m.def("small_fit", [](uintptr_t s, uintptr_t codes_fm, int cb, int64_t n_stride, int n, int F,
@@ -239,14 +241,20 @@ PYBIND11_MODULE(_hip, m) {
                          int max_depth, int64_t mss, int64_t msl, uintptr_t node_i32,
                          uintptr_t node_st, int grid, int tiny_rows, uintptr_t tiny,
                          int tiny_grid, uintptr_t tasks, uintptr_t task_flag, int epoch,
-                         int task_cap) {
+                         int task_cap, uintptr_t tiny_order) {
     mt::launch_finish_reg(S(s), P<void>(codes_rm), row_words, P<void>(codes_fm), cb, n_rows,
                           P<uint32_t>(buf0), P<uint32_t>(buf1), P<int64_t>(y), P<int64_t>(jobs),
                           J, P<int32_t>(counter), P<int32_t>(nbins), F, B, max_depth, mss, msl,
                           P<int32_t>(node_i32), P<int64_t>(node_st), grid, tiny_rows,
                           P<int64_t>(tiny), tiny_grid, P<int64_t>(tasks), P<int32_t>(task_flag),
-                          epoch, task_cap);
-  });
+                          epoch, task_cap, P<int32_t>(tiny_order));
+  }, py::arg("s"), py::arg("codes_rm"), py::arg("row_words"), py::arg("codes_fm"), py::arg("cb"),
+     py::arg("n_rows"), py::arg("buf0"), py::arg("buf1"), py::arg("y"), py::arg("jobs"),
+     py::arg("J"), py::arg("counter"), py::arg("nbins"), py::arg("F"), py::arg("B"),
+     py::arg("max_depth"), py::arg("mss"), py::arg("msl"), py::arg("node_i32"),
+     py::arg("node_st"), py::arg("grid"), py::arg("tiny_rows"), py::arg("tiny"),
+     py::arg("tiny_grid"), py::arg("tasks"), py::arg("task_flag"), py::arg("epoch"),
+     py::arg("task_cap"), py::arg("tiny_order") = 0);
   m.def("seg_minmax", [](uintptr_t s, uintptr_t idx, uintptr_t y, uintptr_t items, int n_items,
                          uintptr_t out, uintptr_t dcount) {
     mt::launch_seg_minmax(S(s), P<uint32_t>(idx), P<int64_t>(y), P<int64_t>(items), n_items,

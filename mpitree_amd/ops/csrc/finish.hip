@@ -1836,7 +1836,7 @@ __global__ __launch_bounds__(kW * kWave) void finish_tiny_sorted_kernel(
     const int64_t* __restrict__ tiny, const int32_t* __restrict__ tiny_count,
     int32_t* __restrict__ tiny_counter, int F, int C, int crit, int max_depth, int64_t mss,
     int64_t msl, const double* __restrict__ xtab, int32_t* __restrict__ node_i32,
-    int32_t* __restrict__ node_cnt) {
+    int32_t* __restrict__ node_cnt, const int32_t* __restrict__ order) {
   extern __shared__ __align__(16) uint32_t dyn[];
   __shared__ double s_h[kTinyH];
   __shared__ uint32_t s_hrow[kTinyRows + 1];
@@ -1857,7 +1857,8 @@ __global__ __launch_bounds__(kW * kWave) void finish_tiny_sorted_kernel(
   for (;;) {
     const int k = wave_claim_next(claim, tiny_counter, K, claim_batch);
     if (k >= K) break;
-    const int64_t* rec = tiny + (int64_t)k * 8;
+    // order (optional): the records by rows descending (launch_tiny_order)
+    const int64_t* rec = tiny + (int64_t)(order ? order[k] : k) * 8;
     if (rec[1] < 2) continue;  // (an unused reserved record)
     tiny_sorted_subtree<CodeT>(codes_rm, row_words, rec[3] ? buf1 : buf0, y, rl, rec[0], (int)rec[1],
                         (int)rec[2], rec[4], F, C, crit, max_depth, mss, msl, s_h, s_hrow, srt, flag,
@@ -1948,7 +1949,7 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
                    const float* xtabf, int xtab_n,
                    int32_t* node_i32, int32_t* node_cnt, int64_t* tasks, int32_t* task_flag,
                    int32_t epoch, int task_cap, int grid, int tiny_rows, int64_t* tiny,
-                   int tiny_grid, int64_t* prof, int tiny_waves) {
+                   int tiny_grid, int64_t* prof, int tiny_waves, int32_t* tiny_order) {
   // counter: int32 [8] = {job cursor, tiny count, tiny cursor, -...}, zeroed by the
   // host. node_i32 / node_cnt are indexed by pre-order position (jobs[j][3] is
   // job j's root position); rows a fit never writes keep n = 0 (host memset).
@@ -2037,6 +2038,12 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
       }
       // tiny_grid counts 4-wave workgroups: keep the total wave count
       const int g = std::max(1, tiny_grid * kTinyWaves / w);
+      // (tiny_order: [2 * 65] scratch, then the order; null keeps discovery order)
+      int32_t* order = nullptr;
+      if (tiny_order) {
+        order = tiny_order + 2 * 65;
+        launch_tiny_order(stream, tiny, counter + kFinCtrTinyCount, tiny_order, order, 128);
+      }
       const size_t lds = (size_t)w * tiny_wave_bytes(F, cb);
 #define MT_TS(W, CT)                                                                         \
   MT_HIP_CHECK(mt_set_max_lds((const void*)finish_tiny_sorted_kernel<W, CT>,            \
@@ -2044,7 +2051,7 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   hipLaunchKernelGGL((finish_tiny_sorted_kernel<W, CT>), dim3(g), dim3(W * kWave), lds,      \
                      stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,  \
                      counter + kFinCtrTinyCount, counter + kFinCtrTinyCount + 1, F, C, crit, \
-                     max_depth, mss, msl, xtab, node_i32, node_cnt);
+                     max_depth, mss, msl, xtab, node_i32, node_cnt, order);
 #define MT_TSW(CT)   \
   if (w == 16) {     \
     MT_TS(16, CT)    \

@@ -502,7 +502,8 @@ __global__ __launch_bounds__(256) void finish_tiny_reg_kernel(
     const uint32_t* __restrict__ buf1, const int64_t* __restrict__ y,
     const int64_t* __restrict__ tiny, const int32_t* __restrict__ tiny_count,
     int32_t* __restrict__ tiny_counter, int F, int max_depth, int64_t mss, int64_t msl,
-    int32_t* __restrict__ node_i32, int64_t* __restrict__ node_st) {
+    int32_t* __restrict__ node_i32, int64_t* __restrict__ node_st,
+    const int32_t* __restrict__ order) {
   extern __shared__ __align__(16) uint8_t dyn_reg[];
   __shared__ unsigned long long s_mask[kRegTinyWaves][kRegTinyStack];
   __shared__ int32_t s_dep[kRegTinyWaves][kRegTinyStack], s_slot[kRegTinyWaves][kRegTinyStack];
@@ -521,7 +522,8 @@ __global__ __launch_bounds__(256) void finish_tiny_reg_kernel(
   for (;;) {
     const int k = wave_claim_next(claim, tiny_counter, K, claim_batch);
     if (k >= K) break;
-    const int64_t* rec = tiny + (int64_t)k * 8;
+    // order (optional): the records by rows descending (launch_tiny_order)
+    const int64_t* rec = tiny + (int64_t)(order ? order[k] : k) * 8;
     const int64_t start = rec[0];
     const int m = (int)rec[1];
     if (m < 2) continue;  // (an unused reserved record)
@@ -858,7 +860,7 @@ void launch_finish_reg(hipStream_t stream, const void* codes_rm, int64_t row_wor
                        int32_t* counter, const int32_t* nbins, int F, int B, int max_depth,
                        int64_t mss, int64_t msl, int32_t* node_i32, int64_t* node_st, int grid,
                        int tiny_rows, int64_t* tiny, int tiny_grid, int64_t* tasks,
-                       int32_t* task_flag, int32_t epoch, int task_cap) {
+                       int32_t* task_flag, int32_t epoch, int task_cap, int32_t* tiny_order) {
   if (J <= 0) return;
   if (code_bytes != 1) tiny_rows = 0;
   // the tiny kernel keeps every feature's lane order in LDS: past what a CU holds
@@ -883,9 +885,15 @@ void launch_finish_reg(hipStream_t stream, const void* codes_rm, int64_t row_wor
   if (tiny_rows > 0) {
     const size_t tl = (size_t)kRegTinyWaves * reg_tiny_wave_bytes(F);
     MT_HIP_CHECK(mt_set_max_lds((const void*)finish_tiny_reg_kernel, (int)tl));
+    int32_t* order = nullptr;  // (tiny_order: [2 * 65] scratch, then the order)
+    if (tiny_order) {
+      order = tiny_order + 2 * 65;
+      launch_tiny_order(stream, tiny, counter + 1, tiny_order, order, 128);
+    }
     hipLaunchKernelGGL(finish_tiny_reg_kernel, dim3(tiny_grid), dim3(kRegTinyWaves * kWave), tl,
                        stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, tiny,
-                       counter + 1, counter + 2, F, max_depth, mss, msl, node_i32, node_st);
+                       counter + 1, counter + 2, F, max_depth, mss, msl, node_i32, node_st,
+                       order);
     MT_HIP_CHECK(hipGetLastError());
   }
 }

@@ -1,6 +1,8 @@
 // Level-loop work lists and planner arguments (grow.hip), shared with the
 // host bindings.
 #pragma once
+#include <hip/hip_runtime.h>
+
 #include <cstdint>
 
 namespace mt {
@@ -119,5 +121,9 @@ struct PlanArgs {
   // buffer for both level parities: many-class fits whose two would not fit)
   int derive_free = 0;
 };
+
+// tiny-subtree records by rows descending (misc.hip): order[] for the tiny kernels
+void launch_tiny_order(hipStream_t stream, const int64_t* tiny, const int32_t* count,
+                       int32_t* scratch, int32_t* order, int grid);
 
 }  // namespace mt

@@ -231,4 +231,72 @@ void launch_targets(hipStream_t stream, const void* y, bool y64, int64_t n, int6
   MT_HIP_CHECK(hipGetLastError());
 }
 
+
+// ---- tiny subtrees, largest first (finish.hip / finish_reg.hip) -----------
+// The tiny-subtree kernels' waves claim records in discovery order; a record's
+// chain of dependent node steps grows with its rows, so a late large subtree
+// leaves most waves idle at the end (a P = 8 rank has ~2 subtrees per wave).
+// order[] = the record indices by rows descending (a counting sort over rows
+// 0..64; unused reserved records, rows < 2, last): per-workgroup LDS counts,
+// one global reservation per bucket and workgroup, LDS cursors for the places.
+// scratch: int32 [2 * 65] bucket totals + cursors (zeroed by the launcher).
+constexpr int kTinyOrderB = 65;
+constexpr int kTinyOrderThreads = 256;
+
+__device__ __forceinline__ int tiny_order_bucket(const int64_t* __restrict__ tiny, int64_t k) {
+  const int64_t m = tiny[k * 8 + 1];
+  return 64 - (int)(m < 0 ? 0 : (m > 64 ? 64 : m));
+}
+
+__global__ __launch_bounds__(kTinyOrderThreads) void tiny_order_count_kernel(
+    const int64_t* __restrict__ tiny, const int32_t* __restrict__ count, int32_t* __restrict__ tot) {
+  __shared__ int32_t h[kTinyOrderB];
+  for (int i = threadIdx.x; i < kTinyOrderB; i += kTinyOrderThreads) h[i] = 0;
+  __syncthreads();
+  const int64_t K = *count;
+  const int64_t per = (K + gridDim.x - 1) / gridDim.x;
+  const int64_t k0 = (int64_t)blockIdx.x * per, k1 = k0 + per < K ? k0 + per : K;
+  for (int64_t k = k0 + threadIdx.x; k < k1; k += kTinyOrderThreads)
+    atomicAdd(&h[tiny_order_bucket(tiny, k)], 1);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kTinyOrderB; i += kTinyOrderThreads)
+    if (h[i]) atomicAdd(&tot[i], h[i]);
+}
+
+__global__ __launch_bounds__(kTinyOrderThreads) void tiny_order_place_kernel(
+    const int64_t* __restrict__ tiny, const int32_t* __restrict__ count,
+    const int32_t* __restrict__ tot, int32_t* __restrict__ cursor, int32_t* __restrict__ order) {
+  __shared__ int32_t h[kTinyOrderB], base[kTinyOrderB];
+  for (int i = threadIdx.x; i < kTinyOrderB; i += kTinyOrderThreads) h[i] = 0;
+  __syncthreads();
+  const int64_t K = *count;
+  const int64_t per = (K + gridDim.x - 1) / gridDim.x;
+  const int64_t k0 = (int64_t)blockIdx.x * per, k1 = k0 + per < K ? k0 + per : K;
+  for (int64_t k = k0 + threadIdx.x; k < k1; k += kTinyOrderThreads)
+    atomicAdd(&h[tiny_order_bucket(tiny, k)], 1);
+  __syncthreads();
+  if (threadIdx.x < kTinyOrderB) {  // (kTinyOrderB <= threads: one bucket a thread)
+    const int b = threadIdx.x;
+    int start = 0;
+    for (int i = 0; i < b; ++i) start += tot[i];
+    base[b] = start + (h[b] ? atomicAdd(&cursor[b], h[b]) : 0);
+    h[b] = 0;
+  }
+  __syncthreads();
+  for (int64_t k = k0 + threadIdx.x; k < k1; k += kTinyOrderThreads) {
+    const int b = tiny_order_bucket(tiny, k);
+    order[base[b] + atomicAdd(&h[b], 1)] = (int32_t)k;
+  }
+}
+
+void launch_tiny_order(hipStream_t stream, const int64_t* tiny, const int32_t* count,
+                       int32_t* scratch, int32_t* order, int grid) {
+  MT_HIP_CHECK(hipMemsetAsync(scratch, 0, sizeof(int32_t) * 2 * kTinyOrderB, stream));
+  hipLaunchKernelGGL(tiny_order_count_kernel, dim3(grid), dim3(kTinyOrderThreads), 0, stream,
+                     tiny, count, scratch);
+  hipLaunchKernelGGL(tiny_order_place_kernel, dim3(grid), dim3(kTinyOrderThreads), 0, stream,
+                     tiny, count, scratch, scratch + kTinyOrderB, order);
+  MT_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace mt

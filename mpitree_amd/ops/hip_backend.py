@@ -360,6 +360,22 @@ _REG_PER_CU: dict = {}  # (bins, code bytes) -> regression finisher workgroups p
 _FIN_WATCH: list = []  # pinned views of finisher watchdog words, checked at assembly
 
 
+def _tiny_order(device, cap: int, reg: bool) -> int:
+    """Scratch for the tiny-subtree kernels' largest-first order ([2 * 65] bucket
+    counts, then ``cap`` record indices), or 0: the records in discovery order.
+    Regression only by default (``MPITREE_TINY_LPT`` = 1 / 0 forces it): its
+    subtrees grow to single rows, so a subtree's chain grows with its rows and a
+    late large one idles the other waves -- 1M x 64 regression 8.90 -> 8.51 ms;
+    classification subtrees stop at pure nodes and the ordering's two launches
+    cost more than they balance (3.087 vs 3.098 ms; P = 8 rank 1.910 vs 1.915,
+    ``profiles/r6/ab_lpt_*.log``)."""
+    env = os.environ.get("MPITREE_TINY_LPT")
+    if (env == "0") if env is not None else not reg:
+        return 0
+    nb = (2 * 65 + int(cap)) * 4
+    return _workspace(device, "fin.tiny_order", nb).data_ptr()
+
+
 def _task_flags(device, n: int, slot: int = 0):
     """Epoch-tagged publish flags of the finisher's hand-off queue: a flag is
     set when it equals this launch's epoch, so the buffer is never cleared
@@ -909,7 +925,8 @@ class HipBackend:
                         rec.data_ptr(), cnt.data_ptr(), tasks.data_ptr(), flags.data_ptr(),
                         epoch, task_cap, grid, tiny_rows, tiny.data_ptr(), 4 * N_CU,
                         0 if prof is None else prof.data_ptr(),
-                        tiny_waves=8 if share > 1 else 0)
+                        tiny_waves=8 if share > 1 else 0,
+                        tiny_order=_tiny_order(self.device, tiny.shape[0], False))
         self._fin_keep = (counter, tasks, tiny, d_jobs)
         # the hand-off queue's watchdog word (+ completed tasks), read
         # with the assembly's node-count sync: a finisher that gave up waiting
@@ -945,7 +962,8 @@ class HipBackend:
                             counter.data_ptr(), self.nbins.data_ptr(), self.F, self.B, md,
                             int(params.min_samples_split), int(max(1, params.min_samples_leaf)),
                             rec.data_ptr(), st64.data_ptr(), grid, tiny_rows, tiny.data_ptr(),
-                            4 * N_CU, tasks.data_ptr(), flags.data_ptr(), epoch, task_cap)
+                            4 * N_CU, tasks.data_ptr(), flags.data_ptr(), epoch, task_cap,
+                            _tiny_order(self.device, tiny.shape[0], True))
         self._fin_keep = (counter, tasks, tiny, d_jobs)
         _FIN_WATCH.append(_pinned_copy(counter[100:101], f"fin.watch{len(_FIN_WATCH)}"))
 
