@@ -1141,7 +1141,7 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
     const int64_t* __restrict__ tiny, const int32_t* __restrict__ tiny_count,
     int32_t* __restrict__ tiny_counter, int F, int C, int crit, int max_depth, int64_t mss,
     int64_t msl, const double* __restrict__ xtab, int32_t* __restrict__ node_i32,
-    int32_t* __restrict__ node_cnt) {
+    int32_t* __restrict__ node_cnt, const int32_t* __restrict__ order) {
   constexpr int kMC = kMany ? kTinyRows : kTinyMaxC;  // class slots per wave
   __shared__ double s_tab[kTinyRows + 1];
   __shared__ uint32_t s_codes[kTinyWaves][kTinyRows * kTinyStride];
@@ -1168,7 +1168,8 @@ __global__ __launch_bounds__(256) void finish_tiny_kernel(
   for (;;) {
     const int k = wave_claim_next(claim, tiny_counter, K, claim_batch);
     if (k >= K) break;
-    const int64_t* rec = tiny + (int64_t)k * 8;
+    // order (optional): the records by rows descending (launch_tiny_order)
+    const int64_t* rec = tiny + (int64_t)(order ? order[k] : k) * 8;
     const int64_t start = rec[0];
     const int m = (int)rec[1];
     if (m < 2) continue;  // (an unused reserved record)
@@ -2023,6 +2024,12 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
 #undef MT_FIN_NT
   MT_HIP_CHECK(hipGetLastError());
   if (tiny_rows > 0) {
+    // (tiny_order: [2 * 65] scratch, then the order; null keeps discovery order)
+    int32_t* order = nullptr;
+    if (tiny_order) {
+      order = tiny_order + 2 * 65;
+      launch_tiny_order(stream, tiny, counter + kFinCtrTinyCount, tiny_order, order, 128);
+    }
     if (tiny_sorted) {
       const int cb = code_bytes;
       // waves per workgroup: the most that fit a CU (many subtrees: occupancy), or
@@ -2038,12 +2045,6 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
       }
       // tiny_grid counts 4-wave workgroups: keep the total wave count
       const int g = std::max(1, tiny_grid * kTinyWaves / w);
-      // (tiny_order: [2 * 65] scratch, then the order; null keeps discovery order)
-      int32_t* order = nullptr;
-      if (tiny_order) {
-        order = tiny_order + 2 * 65;
-        launch_tiny_order(stream, tiny, counter + kFinCtrTinyCount, tiny_order, order, 128);
-      }
       const size_t lds = (size_t)w * tiny_wave_bytes(F, cb);
 #define MT_TS(W, CT)                                                                         \
   MT_HIP_CHECK(mt_set_max_lds((const void*)finish_tiny_sorted_kernel<W, CT>,            \
@@ -2076,7 +2077,7 @@ void launch_finish(hipStream_t stream, const void* codes_rm, int64_t row_words,
   hipLaunchKernelGGL(finish_tiny_kernel<MANY>, dim3(tiny_grid), dim3(kTinyWaves * kWave), 0,  \
                      stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, rl, tiny,   \
                      counter + kFinCtrTinyCount, counter + kFinCtrTinyCount + 1, F, C, crit, \
-                     max_depth, mss, msl, xtab, node_i32, node_cnt);
+                     max_depth, mss, msl, xtab, node_i32, node_cnt, order);
       if (C > kTinyMaxC) {
         MT_TG(true)
       } else {

@@ -360,17 +360,17 @@ _REG_PER_CU: dict = {}  # (bins, code bytes) -> regression finisher workgroups p
 _FIN_WATCH: list = []  # pinned views of finisher watchdog words, checked at assembly
 
 
-def _tiny_order(device, cap: int, reg: bool) -> int:
+def _tiny_order(device, cap: int, on: bool) -> int:
     """Scratch for the tiny-subtree kernels' largest-first order ([2 * 65] bucket
     counts, then ``cap`` record indices), or 0: the records in discovery order.
-    Regression only by default (``MPITREE_TINY_LPT`` = 1 / 0 forces it): its
-    subtrees grow to single rows, so a subtree's chain grows with its rows and a
-    late large one idles the other waves -- 1M x 64 regression 8.90 -> 8.51 ms;
-    classification subtrees stop at pure nodes and the ordering's two launches
-    cost more than they balance (3.087 vs 3.098 ms; P = 8 rank 1.910 vs 1.915,
-    ``profiles/r6/ab_lpt_*.log``)."""
+    ``on``: regression and many classes by default (``MPITREE_TINY_LPT`` = 1 / 0
+    forces it): their subtrees keep splitting to (nearly) single rows, so a
+    subtree's chain grows with its rows and a late large one idles the other
+    waves -- 1M x 64 regression 8.90 -> 8.51 ms; two-class subtrees stop at pure
+    nodes and the ordering's two launches cost more than they balance (3.087 vs
+    3.098 ms; P = 8 rank 1.910 vs 1.915, ``profiles/r6/ab_lpt_*.log``)."""
     env = os.environ.get("MPITREE_TINY_LPT")
-    if (env == "0") if env is not None else not reg:
+    if (env == "0") if env is not None else not on:
         return 0
     nb = (2 * 65 + int(cap)) * 4
     return _workspace(device, "fin.tiny_order", nb).data_ptr()
@@ -926,7 +926,7 @@ class HipBackend:
                         epoch, task_cap, grid, tiny_rows, tiny.data_ptr(), 4 * N_CU,
                         0 if prof is None else prof.data_ptr(),
                         tiny_waves=8 if share > 1 else 0,
-                        tiny_order=_tiny_order(self.device, tiny.shape[0], False))
+                        tiny_order=_tiny_order(self.device, tiny.shape[0], C > 2))
         self._fin_keep = (counter, tasks, tiny, d_jobs)
         # the hand-off queue's watchdog word (+ completed tasks), read
         # with the assembly's node-count sync: a finisher that gave up waiting
