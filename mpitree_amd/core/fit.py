@@ -454,8 +454,11 @@ def fit_tree(
             # (more classes: no hand-off queue, and a node's histogram scan grows
             # with B * C -- smaller jobs keep every finisher workgroup busy)
             # (C = 64: 4096 -> 116.7 ms, 2048 -> 119.0, 1024 -> 134.5, 512 -> 168.0;
-            # profiles/r4/ab_c64_finisher_rows.log)
-            default_fr = min(default_fr, 4096 if C <= 64 else 2048)
+            # profiles/r4/ab_c64_finisher_rows.log; round 6, with the tiny subtrees
+            # largest first: 4096 -> 88.5 ms, 3000 -> 85.1, 2600 -> 87.5, 3400 -> 86.9,
+            # profiles/r6/ab_c64_finisher_rows.log -- measured at C = 64 only, so
+            # fewer classes keep 4096)
+            default_fr = min(default_fr, 4096 if C <= 16 else (3000 if C <= 64 else 2048))
         if finisher_rows is None or (comm.world_size > 1 and comm.kind == "data"):
             # data-parallel GPU ranks finish subtrees on their owners (rows sent
             # there first), so the finisher applies as on one GPU
