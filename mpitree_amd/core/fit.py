@@ -440,7 +440,9 @@ def fit_tree(
         # jobs between them (hand-off queue), so fewer replicated levels win
         # (profiles/kernel_experiments.md: 1M x 64 3.52 -> 3.33 ms at 2048 -> 8192)
         # (regression: the hand-off queue gains 0.35 ms at any of n/512 .. n/128)
-        default_fr = int(env) if env else (max(2048, n // 512) if regression
+        # (regression, round 6, tiny subtrees largest first: 1M x 64 2048 -> 3000 rows
+        # 8.59 -> 8.49 ms over three A/B runs, profiles/r6/ab_reg_finisher_rows.log)
+        default_fr = int(env) if env else (max(3000, n // 512) if regression
                                            else max(2048, min(n // 128, 32768)))
         if not env and F > 128:
             # a finisher node scans F x B bins whatever its rows: past 128 features
