@@ -461,6 +461,11 @@ def fit_tree(
             # profiles/r6/ab_c64_finisher_rows.log -- measured at C = 64 only, so
             # fewer classes keep 4096)
             default_fr = min(default_fr, 4096 if C <= 16 else (3000 if C <= 64 else 2048))
+        if not env and be.B > 256:
+            # the same scan per node over B bins (16-bit codes): jobs shrink by 256 / B
+            # (1M x 64, 1024 quantile bins: 7812 -> 2048 rows 33.8 -> 15.0 ms; 1024 rows
+            # 15.6, 4096 rows 22.0; profiles/r6/ab_q1024_finisher_rows*.log)
+            default_fr = max(1024, default_fr * 256 // int(be.B))
         if finisher_rows is None or (comm.world_size > 1 and comm.kind == "data"):
             # data-parallel GPU ranks finish subtrees on their owners (rows sent
             # there first), so the finisher applies as on one GPU
