@@ -442,8 +442,10 @@ def fit_tree(
         # (regression: the hand-off queue gains 0.35 ms at any of n/512 .. n/128)
         # (regression, round 6, tiny subtrees largest first: 1M x 64 2048 -> 3000 rows
         # 8.59 -> 8.49 ms over three A/B runs, profiles/r6/ab_reg_finisher_rows.log)
+        # (classification below 524k rows, round 6: 100k x 32 2048 -> 4096 rows 1.20 ->
+        # 1.11 ms at full depth, 1.13 -> 1.05 ms at depth 12; profiles/r6/ab_100k_*.log)
         default_fr = int(env) if env else (max(3000, n // 512) if regression
-                                           else max(2048, min(n // 128, 32768)))
+                                           else max(4096, min(n // 128, 32768)))
         if not env and F > 128:
             # a finisher node scans F x B bins whatever its rows: past 128 features
             # smaller jobs (more level-loop levels, which scan many nodes at once) win

@@ -2,7 +2,7 @@
 # in gpurun_out/ab_*.log (copied to profiles/r6/).
 set -e
 rm -f gpurun_out/ab.log
-BENCH_ARGS="--continuous --max-bins 1024 --steps 5 --warmup 2" bash tools/gpu.sh "ab:MPITREE_FINISHER_ROWS=1024;MPITREE_FINISHER_ROWS=2048;MPITREE_FINISHER_ROWS=3000"
-mv gpurun_out/ab.log gpurun_out/ab_q1024b.log
-BENCH_ARGS="--n 200000 --features 512 --no-continuous --steps 10 --warmup 2" bash tools/gpu.sh "ab:MPITREE_FINISHER_ROWS=256;MPITREE_FINISHER_ROWS=320;MPITREE_FINISHER_ROWS=384"
-mv gpurun_out/ab.log gpurun_out/ab_f512b.log
+BENCH_ARGS="--n 100000 --features 32 --max-depth 12 --no-continuous --steps 20 --warmup 3" bash tools/gpu.sh "ab:MPITREE_FINISHER_ROWS=4096;MPITREE_FINISHER_ROWS=8192;MPITREE_FINISHER_ROWS=16384"
+mv gpurun_out/ab.log gpurun_out/ab_100k_b.log
+BENCH_ARGS="--n 100000 --features 32 --no-continuous --steps 20 --warmup 3" bash tools/gpu.sh "ab:MPITREE_FINISHER_ROWS=4096;MPITREE_FINISHER_ROWS=8192"
+mv gpurun_out/ab.log gpurun_out/ab_100k_full.log
