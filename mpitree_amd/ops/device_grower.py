@@ -98,12 +98,15 @@ POLL_TIMEOUT_S = float(os.environ.get("MPITREE_POLL_TIMEOUT", "120"))
 # histogram work items per CU and level (1 or 2): fewer, larger items write fewer
 # LDS slabs for the reduction to read back
 def hist_items_per_cu(reg: bool) -> int:
-    """Histogram work items per CU and level: 2 for classification, 1 for
-    regression, whose int64 {count, sum} slabs double the reduction's reads
-    (1M x 64 regression 9.35 -> 9.07 ms, profiles/r5/ab_hist_items_reg.log);
-    ``MPITREE_HIST_ITEMS`` forces it."""
+    """Histogram work items per CU and level: 1 -- half the slabs for the
+    reduction to read back. Regression since round 5 (int64 {count, sum} slabs:
+    1M x 64 9.35 -> 9.07 ms, profiles/r5/ab_hist_items_reg.log), classification
+    since round 6 (C = 64 85.3 -> 83.3 ms, 10M x 128 41.86 -> 41.39 ms, 1024 bins
+    15.0 -> 14.7 ms, the flagship / 100k / 200k x 512 unchanged;
+    profiles/r6/ab_knobs_*.log, ab_hi_*.log); ``MPITREE_HIST_ITEMS`` = 2 restores
+    two."""
     env = os.environ.get("MPITREE_HIST_ITEMS")
-    return max(1, min(2, int(env))) if env else (1 if reg else 2)
+    return max(1, min(2, int(env))) if env else 1
 
 
 def fp_prefix_pays(n: int, F: int, P: int, reg: bool) -> bool:
