@@ -444,7 +444,12 @@ def fit_tree(
         # 8.59 -> 8.49 ms over three A/B runs, profiles/r6/ab_reg_finisher_rows.log)
         # (classification below 524k rows, round 6: 100k x 32 2048 -> 4096 rows 1.20 ->
         # 1.11 ms at full depth, 1.13 -> 1.05 ms at depth 12; profiles/r6/ab_100k_*.log)
-        default_fr = int(env) if env else (max(3000, n // 512) if regression
+        # (a rank of a multi-GPU regression fit keeps 2048: its finisher holds 1/P of
+        # the jobs, and fewer, larger ones balance worse -- simulated P = 8 rank 4.03
+        # ms at 2048 vs 4.12 at 3000, profiles/r6/sim_reg_p8_floor2048.jsonl,
+        # sim_own_after_tuning.jsonl)
+        reg_floor = 3000 if comm.world_size == 1 else 2048
+        default_fr = int(env) if env else (max(reg_floor, n // 512) if regression
                                            else max(4096, min(n // 128, 32768)))
         if not env and F > 128:
             # a finisher node scans F x B bins whatever its rows: past 128 features
