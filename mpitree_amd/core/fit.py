@@ -457,7 +457,13 @@ def fit_tree(
             # (200k x 512: classification 20.5 -> 11.8 ms at 512 rows; regression,
             # whose features past 256 read their bins from memory, 313 -> 76 ms at 128;
             # profiles/baseline_configs.md)
-            default_fr = min(default_fr, 128 if (regression and F > 256)
+            # (wide regression, round 6: the tiny-subtree kernel now runs narrower
+            # workgroups past ~300 features instead of handing those subtrees to the
+            # block kernel -- 200k x 512 75 -> 24.7 ms -- and then 512-row jobs win:
+            # 21.3 ms vs 22.6 at 256, 23.5 at 1024, 24.7 at 128;
+            # profiles/r6/ab_reg_wide_tiny*.log. Past ~1100 features no tiny kernel.)
+            wide_reg = 512 if F <= 1024 else 128
+            default_fr = min(default_fr, wide_reg if (regression and F > 256)
                              else max(256, (1 << 18) // F))
         if not env and C > 2:
             # (more classes: no hand-off queue, and a node's histogram scan grows

@@ -853,6 +853,11 @@ int finish_reg_blocks_per_cu(int B, int code_bytes) {
   return per_cu < 1 ? 1 : per_cu;
 }
 
+static int reg_env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
 // counter: int32 [4] = {job cursor, tiny count, tiny cursor, -}, zeroed by the host.
 void launch_finish_reg(hipStream_t stream, const void* codes_rm, int64_t row_words,
                        const void* codes_fm, int code_bytes, int64_t n_rows, uint32_t* buf0,
@@ -863,9 +868,16 @@ void launch_finish_reg(hipStream_t stream, const void* codes_rm, int64_t row_wor
                        int32_t* task_flag, int32_t epoch, int task_cap, int32_t* tiny_order) {
   if (J <= 0) return;
   if (code_bytes != 1) tiny_rows = 0;
-  // the tiny kernel keeps every feature's lane order in LDS: past what a CU holds
-  // (about 512 features) the block kernel grows the subtrees to the leaves
-  if ((size_t)kRegTinyWaves * reg_tiny_wave_bytes(F) > 160 * 1024) tiny_rows = 0;
+  // the tiny kernel keeps every feature's lane order in LDS: workgroups of fewer
+  // waves past 4 x that (2 waves up to ~590 features, 1 up to ~1180; the grid keeps
+  // the total wave count), and past one wave's worth the block kernel grows the
+  // subtrees to the leaves (MPITREE_REG_TINY_WAVES caps the width: A/B)
+  int tw = std::max(1, std::min(kRegTinyWaves, reg_env_int("MPITREE_REG_TINY_WAVES",
+                                                          kRegTinyWaves)));
+  while (tw > 1 && (size_t)tw * reg_tiny_wave_bytes(F) > 160 * 1024) tw >>= 1;
+  if ((size_t)tw * reg_tiny_wave_bytes(F) > 160 * 1024 ||
+      (tw < kRegTinyWaves && reg_env_int("MPITREE_REG_TINY_NARROW", 1) == 0))
+    tiny_rows = 0;
   tiny_rows = std::min(tiny_rows, kRegTinyRows);
   const size_t lds = (size_t)finish_reg_lds_bytes(B);
 #define MT_FR(CT)                                                                           \
@@ -883,14 +895,15 @@ void launch_finish_reg(hipStream_t stream, const void* codes_rm, int64_t row_wor
 #undef MT_FR
   MT_HIP_CHECK(hipGetLastError());
   if (tiny_rows > 0) {
-    const size_t tl = (size_t)kRegTinyWaves * reg_tiny_wave_bytes(F);
+    const size_t tl = (size_t)tw * reg_tiny_wave_bytes(F);
+    const int tg = std::max(1, tiny_grid * kRegTinyWaves / tw);
     MT_HIP_CHECK(mt_set_max_lds((const void*)finish_tiny_reg_kernel, (int)tl));
     int32_t* order = nullptr;  // (tiny_order: [2 * 65] scratch, then the order)
     if (tiny_order) {
       order = tiny_order + 2 * 65;
       launch_tiny_order(stream, tiny, counter + 1, tiny_order, order, 128);
     }
-    hipLaunchKernelGGL(finish_tiny_reg_kernel, dim3(tiny_grid), dim3(kRegTinyWaves * kWave), tl,
+    hipLaunchKernelGGL(finish_tiny_reg_kernel, dim3(tg), dim3(tw * kWave), tl,
                        stream, (const uint32_t*)codes_rm, row_words, buf0, buf1, y, tiny,
                        counter + 1, counter + 2, F, max_depth, mss, msl, node_i32, node_st,
                        order);

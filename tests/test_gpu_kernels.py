@@ -64,6 +64,21 @@ def test_gpu_classifier_matches_oracle(crit, seed):
     np.testing.assert_array_equal(clf.predict(Xd).cpu().numpy(), clf.predict(X))
 
 
+@pytest.mark.parametrize("F", [600, 1000])
+def test_gpu_wide_regression_tiny_kernel_matches_host(F):
+    # past ~300 features the regression tiny-subtree kernel runs 2-wave (past ~590:
+    # 1-wave) workgroups; the tree must equal the host builder's
+    rng = np.random.default_rng(F)
+    n = 3000
+    X = rng.integers(0, 200, size=(n, F)).astype(np.float32)
+    y = X[:, 0] * 0.5 + X[:, 1] - X[:, 7] + rng.normal(0, 5, n)
+    g = DecisionTreeRegressor(device="cuda").fit(torch.from_numpy(X).cuda(),
+                                                  torch.from_numpy(y).cuda())
+    h = DecisionTreeRegressor(device="cpu").fit(X, y)
+    assert g.fit_stats_["engine"].startswith("hip")
+    assert g.tree_arrays_.equal(h.tree_arrays_, check_impurity=False)
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_gpu_regressor_matches_oracle(seed):
     rng = np.random.default_rng(100 + seed)
