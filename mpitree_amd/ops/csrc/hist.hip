@@ -27,6 +27,10 @@
 //    to direct global atomics.
 #include "common.h"
 
+#ifndef MT_RED_ROWS_CAP  // device-planned slab reduction: capped row count (A/B: 0)
+#define MT_RED_ROWS_CAP 1
+#endif
+
 namespace mt {
 
 constexpr int kHistThreads = 512;
@@ -305,16 +309,19 @@ __global__ __launch_bounds__(256) void hist_reduce_cls_kernel(
     const int64_t* __restrict__ red, const uint32_t* __restrict__ slab,
     uint32_t* __restrict__ hist, int64_t Ep, int C, int W, int G,
     const int32_t* __restrict__ dcount) {
-  if (dcount && (int)blockIdx.y >= *dcount) return;
-  const int64_t slot = red[blockIdx.y * 3 + 0];
-  const int64_t first = red[blockIdx.y * 3 + 1];
-  const int64_t k = red[blockIdx.y * 3 + 2];
-  const int64_t k0 = (int64_t)blockIdx.z * G;
-  if (k0 >= k) return;
-  const int64_t k1 = min(k, k0 + G);
+  // rows past the grid's y extent: the device count can exceed the launch's rows
+  // (device-planned levels launch a capped row count and stride over the tasks)
+  const int ny = dcount ? *dcount : (int)gridDim.y;
   const int64_t Eu = (Ep / W) * C;
   const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (e >= Ep) return;
+  for (int ty = blockIdx.y; ty < ny; ty += gridDim.y) {
+  const int64_t slot = red[ty * 3 + 0];
+  const int64_t first = red[ty * 3 + 1];
+  const int64_t k = red[ty * 3 + 2];
+  const int64_t k0 = (int64_t)blockIdx.z * G;
+  if (k0 >= k) continue;
+  const int64_t k1 = min(k, k0 + G);
   uint32_t a0 = 0, a1 = 0;
   // every slab load of the group in flight before the first add (a rolled loop
   // waited for each load in turn: one L2 / MALL round trip per slab)
@@ -337,6 +344,7 @@ __global__ __launch_bounds__(256) void hist_reduce_cls_kernel(
   uint32_t* out = hist + slot * Eu + fb * C + 2 * wc;
   if (a0) atomicAdd(out, a0);
   if (a1 && 2 * wc + 1 < C) atomicAdd(out + 1, a1);
+  }
 }
 
 // regression slabs are already [F][B][2] int64
@@ -622,7 +630,13 @@ void launch_hist_reduce_tasks(hipStream_t stream, const int64_t* red, int red_bo
                        dim3(256), 0, stream, red, (uint32_t*)hist, Eu, dred);
     MT_HIP_CHECK(hipGetLastError());
   }
-  dim3 grid((unsigned)((Ep + 255) / 256), task_bound, 1);
+  // rows: the task bound, capped so the grid holds ~32k workgroups (many classes:
+  // ~10k column blocks a row, and a bound of hundreds of rows launched millions of
+  // workgroups that only checked the device count -- 2.6 ms a level at C = 300)
+  const int64_t xb = (Ep + 255) / 256;
+  const int rows = (int)std::max<int64_t>(
+      1, std::min<int64_t>(task_bound, MT_RED_ROWS_CAP ? (32768 + xb - 1) / xb : task_bound));
+  dim3 grid((unsigned)xb, rows, 1);
   hipLaunchKernelGGL(hist_reduce_cls_kernel, grid, dim3(256), 0, stream, tasks,
                      (const uint32_t*)slab, (uint32_t*)hist, Ep, C, W, 16, dtasks);
   MT_HIP_CHECK(hipGetLastError());
