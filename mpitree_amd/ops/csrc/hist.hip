@@ -27,6 +27,9 @@
 //    to direct global atomics.
 #include "common.h"
 
+#ifndef MT_HIST_ROWS_CAP  // class-tiled histograms: capped item row (A/B: 0)
+#define MT_HIST_ROWS_CAP 1
+#endif
 #ifndef MT_RED_ROWS_CAP  // device-planned slab reduction: capped row count (A/B: 0)
 #define MT_RED_ROWS_CAP 1
 #endif
@@ -71,8 +74,10 @@ __global__ __launch_bounds__(kHistThreads) void hist_cls_lds_kernel(
       }
     }
   }
-  // dcount (optional): device-side item count; the grid is an upper bound
-  if (dcount && (int)blockIdx.x >= *dcount) return;
+  // dcount (optional): device-side item count; the grid is an upper bound, or (the
+  // class-tiled launch) a capped row of workgroups that strides over the items
+  const int n_it = dcount ? *dcount : (int)gridDim.x;
+  if ((int)blockIdx.x >= n_it) return;
   extern __shared__ uint32_t lds[];
   constexpr int cpw = 4 / sizeof(CodeT);  // codes per 32-bit word
   const int n_ct = (C + ct - 1) / ct;
@@ -87,10 +92,11 @@ __global__ __launch_bounds__(kHistThreads) void hist_cls_lds_kernel(
   const int g0 = f_lo + t0, g1 = f_lo + t1;
   const int gw0 = (g0 / cpw) & ~(VEC - 1);  // first (VEC-aligned) code word
   const int nwords = (g1 + cpw - 1) / cpw - gw0;
-  const int64_t slot = items[blockIdx.x * 4 + 0];
-  const int64_t start = items[blockIdx.x * 4 + 1];
-  const int64_t count = items[blockIdx.x * 4 + 2];
-  const int64_t dest = items[blockIdx.x * 4 + 3];
+  for (int it = blockIdx.x; it < n_it; it += gridDim.x) {
+  const int64_t slot = items[it * 4 + 0];
+  const int64_t start = items[it * 4 + 1];
+  const int64_t count = items[it * 4 + 2];
+  const int64_t dest = items[it * 4 + 3];
 
   const int lds_words = nf * fstride;
   for (int e = threadIdx.x; e < lds_words; e += blockDim.x) lds[e] = 0u;
@@ -160,19 +166,21 @@ __global__ __launch_bounds__(kHistThreads) void hist_cls_lds_kernel(
       const int w = rem - b * W;
       out[((int64_t)f * B + b) * Wall + (c_lo >> 1) + w] = lds[f * fstride + rem];
     }
-    return;
+  } else {
+    uint32_t* out = hist + slot * (int64_t)F_h * B * C;
+    for (int e = threadIdx.x; e < nf * per_f; e += blockDim.x) {
+      const int f = e / per_f;
+      const int rem = e - f * per_f;
+      const int b = rem / W;
+      const int wc = rem - b * W;
+      const uint32_t v = lds[f * fstride + rem];
+      const int c = c_lo + 2 * wc;
+      const int64_t o = ((int64_t)(t0 + f) * B + b) * C + c;
+      out[o] = v & 0xffffu;
+      if (c + 1 < c_hi) out[o + 1] = v >> 16;
+    }
   }
-  uint32_t* out = hist + slot * (int64_t)F_h * B * C;
-  for (int e = threadIdx.x; e < nf * per_f; e += blockDim.x) {
-    const int f = e / per_f;
-    const int rem = e - f * per_f;
-    const int b = rem / W;
-    const int wc = rem - b * W;
-    const uint32_t v = lds[f * fstride + rem];
-    const int c = c_lo + 2 * wc;
-    const int64_t o = ((int64_t)(t0 + f) * B + b) * C + c;
-    out[o] = v & 0xffffu;
-    if (c + 1 < c_hi) out[o + 1] = v >> 16;
+  __syncthreads();  // (the next item zeroes the LDS image these loops read)
   }
 }
 
@@ -487,7 +495,12 @@ void launch_hist(hipStream_t stream, const void* codes, int code_bytes, int64_t 
     }
     const int shift = std::min(ceil_pow2_shift(words), 6);
     const size_t lds = (size_t)(B * ((ct + 1) / 2) + 1) * 4;
-    dim3 grid(n_items, F_h * n_ct);
+    // (a capped row of workgroups striding over the items: the item bound times
+    // F_h x class tiles launched ~1M workgroups a level at C = 300, most of them
+    // only reading the device count)
+    const int gx = MT_HIST_ROWS_CAP ? std::max(1, std::min(n_items, 32768 / (F_h * n_ct) + 1))
+                                    : n_items;
+    dim3 grid(gx, F_h * n_ct);
 #define MT_CLS_CT(CT)                                                                         \
   MT_HIP_CHECK(mt_set_max_lds((const void*)hist_cls_lds_kernel<CT, 1>, (int)lds));           \
   hipLaunchKernelGGL((hist_cls_lds_kernel<CT, 1>), grid, dim3(kHistThreads), lds, stream,     \
